@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MB/s staged end-to-end (download -> S3) + p50 job latency.
+
+BASELINE.json names the metric "MB/s staged end-to-end (download->S3) + p50 job latency at
+1/2/4/8 workers" and config 2 "100x100 MB HTTP URLs, N concurrent workers -> MinIO multipart".
+One rank = one worker process (the reference's scaling unit: one consumer per container,
+SURVEY §2.6). One "step" = every worker stages one 100 MB random-byte media blob:
+HTTP GET from the origin -> staging dir on disk -> media selection -> multipart PUT to the
+S3 endpoint -> done marker -> api.Convert published -> ack. Weak scaling: per-worker work is
+fixed as N grows.
+
+Launch: ``python bench.py`` (N=1) or ``python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N``. Rank 0 starts the native ``blobd`` peer (origin + S3 sink) and shares its
+port; ranks synchronise over gloo (the workload is host-side: there is no tensor compute).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import shutil
+import statistics
+import sys
+import tempfile
+import time
+
+os.environ.setdefault("LOG_LEVEL", "warn")
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "MB/s staged end-to-end (download->S3) + p50 job latency"
+
+
+def parse() -> argparse.Namespace:
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1, help="worker processes (one per GPU slot)")
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--size-mb", type=float, default=100.0, help="object size in MB (1e6 B)")
+    p.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
+    p.add_argument("--concurrency", type=int, default=2, help="jobs in flight per worker")
+    p.add_argument("--stage-dir", default="", help="download_path (default: a temp dir)")
+    p.add_argument("--compare-reference", action="store_true",
+                   help="also time reference-equivalent mode and report the ratio")
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, want: int):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+        if want != self.world and self.rank == 0:
+            print(f"[bench] --gpus {want} but WORLD_SIZE={self.world}; using {self.world} workers",
+                  file=sys.stderr)
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            self.dist.barrier()
+
+    def bcast(self, obj):
+        if self.world == 1:
+            return obj
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    def gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self) -> None:
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def cuda_sync() -> None:
+    # The driver's contract brackets the timed region with a device sync; the staging path does
+    # not use the device for HTTP jobs, so this is a no-op unless torch already initialised it.
+    try:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+async def run_phase(worker, blob_ep_url, rank: int, first: int, count: int, size: int,
+                    tag: str, media_type: str = "MOVIE"):
+    from downloader_amd.models import api
+    done = asyncio.Event()
+    results = []
+
+    def on_result(r):
+        results.append(r)
+        if len(results) >= count:
+            done.set()
+    worker.on_result = on_result
+    t0 = time.perf_counter()
+    for i in range(first, first + count):
+        url = blob_ep_url(f"r{rank}-j{i}.mkv", size, rank * 1_000_003 + i)
+        await worker.submit(api.make_download(f"bench-{tag}-r{rank}-j{i}", "http", url, media_type))
+    if count:
+        await done.wait()
+    dt = time.perf_counter() - t0
+    worker.on_result = None
+    return dt, results
+
+
+async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str):
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.service.worker import Worker
+    from downloader_amd.utils.config import load_config
+
+    size = int(args.size_mb * 1e6)
+    cfg = load_config(overrides={
+        "mode": mode,
+        "concurrency": args.concurrency,
+        "instance": {"download_path": stage_root},
+        "s3": {"endpoint": endpoint},
+        "broker": {"backend": "memory"},
+        "health": {"enabled": False},
+    })
+    worker = Worker(cfg, broker=MemoryBroker())
+    await worker.start(health=False)
+    host, port = endpoint.split(":")
+
+    def url(name, sz, seed):
+        return f"http://{host}:{port}/media/{name}?size={sz}&seed={seed}"
+
+    _, wres = await run_phase(worker, url, dist.rank, 0, args.warmup, size, mode)
+    bad = [r for r in wres if r.outcome != "staged"]
+    if bad:
+        raise RuntimeError(f"warmup job failed: {bad[0]}")
+    dist.barrier()
+    cuda_sync()
+    t0 = time.perf_counter()
+    dt, res = await run_phase(worker, url, dist.rank, args.warmup, args.steps, size, mode)
+    cuda_sync()
+    t1 = time.perf_counter()
+    bad = [r for r in res if r.outcome != "staged"]
+    await worker.stop()
+    return {"elapsed": t1 - t0, "latencies": [r.seconds for r in res],
+            "bytes": sum(r.bytes for r in res), "failed": len(bad),
+            "err": bad[0].error if bad else ""}
+
+
+def measure(args, dist: Dist, endpoint: str, mode: str):
+    stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
+    try:
+        out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root))
+    finally:
+        if not args.stage_dir:
+            shutil.rmtree(stage_root, ignore_errors=True)
+    dist.barrier()
+    allr = dist.gather(out)
+    elapsed = max(r["elapsed"] for r in allr)
+    total_bytes = sum(r["bytes"] for r in allr)
+    lats = [x for r in allr for x in r["latencies"]]
+    failed = sum(r["failed"] for r in allr)
+    if failed:
+        raise RuntimeError(f"{failed} timed jobs failed: {[r['err'] for r in allr if r['err']][:1]}")
+    return {"mbps": total_bytes / elapsed / 1e6, "elapsed": elapsed,
+            "p50": statistics.median(lats) if lats else 0.0,
+            "p90": sorted(lats)[int(0.9 * (len(lats) - 1))] if lats else 0.0,
+            "bytes": total_bytes}
+
+
+def main() -> int:
+    args = parse()
+    dist = Dist(args.gpus)
+    blob = None
+    endpoint = None
+    if dist.rank == 0:
+        from downloader_amd.bench.infra import Blobd
+        blob = Blobd(default_size=int(args.size_mb * 1e6)).start()
+        endpoint = blob.endpoint
+    endpoint = dist.bcast(endpoint)
+    try:
+        tuned = measure(args, dist, endpoint, args.mode)
+        ref = measure(args, dist, endpoint, "reference") if args.compare_reference else None
+    finally:
+        if blob is not None:
+            blob.stop()
+    if dist.rank == 0:
+        n = dist.world
+        line = {
+            "metric": METRIC,
+            "value": round(tuned["mbps"], 2),
+            "unit": "MB/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tuned["elapsed"] / max(1, args.steps) * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bytes",
+            "data": "synthetic random-byte media blobs served by the native blobd origin",
+            "p50_job_latency_s": round(tuned["p50"], 4),
+            "p90_job_latency_s": round(tuned["p90"], 4),
+            "mode": args.mode,
+            "concurrency_per_worker": args.concurrency if args.mode == "tuned" else 1,
+            "config": {
+                "model": "BASELINE.json config 2: HTTP media blob -> S3 multipart staging",
+                "global_batch": n,
+                "seq_len": int(args.size_mb * 1e6),
+                "parallelism": f"workers{n}",
+                "object_bytes": int(args.size_mb * 1e6),
+                "jobs_timed": n * args.steps,
+            },
+        }
+        if ref is not None:
+            line["reference_mode_MBps"] = round(ref["mbps"], 2)
+            line["reference_mode_p50_s"] = round(ref["p50"], 4)
+            line["vs_reference_mode"] = round(tuned["mbps"] / ref["mbps"], 3)
+        print(json.dumps(line), flush=True)
+    dist.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,70 @@
+"""Bench infrastructure: launches the native ``blobd`` peer (HTTP origin + S3 sink)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import tempfile
+import time
+import urllib.request
+from pathlib import Path
+from typing import Dict, Optional
+
+from ..ops import build
+
+PKG = Path(__file__).resolve().parents[1]
+
+
+class Blobd:
+    def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
+                 host: str = "127.0.0.1"):
+        self.keep_bytes = keep_bytes
+        self.default_size = default_size
+        self.host = host
+        self.proc: Optional[subprocess.Popen] = None
+        self.port = 0
+
+    def start(self, timeout: float = 30.0) -> "Blobd":
+        exe = build.build_blobd(verbose=False)
+        d = tempfile.mkdtemp(prefix="blobd-")
+        pf = os.path.join(d, "port")
+        self.proc = subprocess.Popen(
+            [str(exe), "--host", self.host, "--port", "0", "--port-file", pf,
+             "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)],
+            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        t0 = time.time()
+        while not os.path.exists(pf):
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"blobd exited: {self.proc.stderr.read().decode()}")
+            if time.time() - t0 > timeout:
+                self.stop()
+                raise RuntimeError("blobd did not start")
+            time.sleep(0.02)
+        self.port = int(open(pf).read().strip())
+        return self
+
+    @property
+    def endpoint(self) -> str:
+        return f"{self.host}:{self.port}"
+
+    def media_url(self, name: str, size: int, seed: int) -> str:
+        return f"http://{self.endpoint}/media/{name}?size={size}&seed={seed}"
+
+    def stats(self) -> Dict[str, int]:
+        with urllib.request.urlopen(f"http://{self.endpoint}/_stats", timeout=10) as r:
+            return json.loads(r.read())
+
+    def stop(self) -> None:
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+        self.proc = None
+
+    def __enter__(self) -> "Blobd":
+        return self.start()
+
+    def __exit__(self, *a) -> None:
+        self.stop()

@@ -1,0 +1,537 @@
+// blobd - native benchmark peer for the staging daemon.
+//
+// One multi-threaded HTTP/1.1 server that plays both external systems of the reference's
+// hot path: the HTTP origin (`request(url)`, lib/download.js:160) and the
+// S3/MinIO staging endpoint (`fPutObject`, lib/upload.js:45). Python servers would cap the
+// bench far below what one worker can move, so the peers are native too.
+//
+//   origin:  GET|HEAD /media/<name>?size=N&seed=S   deterministic random bytes, Range support
+//   s3:      HEAD|PUT /<bucket>, GET /<bucket>?list-type=2,
+//            PUT|GET|HEAD|DELETE /<bucket>/<key>, multipart (POST ?uploads, PUT ?partNumber,
+//            POST ?uploadId, DELETE ?uploadId)
+//   stats:   GET /_stats  (JSON: bytes received/served, objects, requests)
+//
+// Uploaded bodies are received into a per-connection buffer and folded into a 64-bit
+// checksum (so every byte crosses memory like a real store); objects <= --keep-bytes are
+// kept in memory (done markers, tests), larger ones keep only size + checksum.
+// SigV4 is NOT verified here (the Python FakeS3 does that in the test-suite).
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <cinttypes>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+struct Object {
+  std::string data;  // kept only when small
+  uint64_t size = 0;
+  uint64_t sum = 0;
+  std::string etag;
+};
+
+struct Upload {
+  std::string bucket, key;
+  std::map<int, Object> parts;
+};
+
+std::mutex g_mu;
+std::unordered_map<std::string, std::map<std::string, Object>> g_buckets;
+std::unordered_map<std::string, Upload> g_uploads;
+std::atomic<uint64_t> g_rx{0}, g_tx{0}, g_reqs{0}, g_objects{0}, g_upload_seq{1};
+std::vector<uint8_t> g_pool;  // random pool the origin serves from
+size_t g_keep_bytes = 1 << 20;
+uint64_t g_default_size = 100ull << 20;
+
+constexpr size_t kPool = 64ull << 20;
+
+uint64_t mix(uint64_t h, uint64_t v) {
+  h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  return h * 0xff51afd7ed558ccdull;
+}
+
+// Order-dependent 64-bit checksum of a byte stream fed in arbitrary chunk sizes:
+// processes whole 8-byte words; carries a partial word between calls.
+struct Summer {
+  uint64_t h = 0x12345678ull, carry = 0;
+  int nc = 0;
+  void feed(const uint8_t* p, size_t n) {
+    while (n && nc) {
+      carry |= (uint64_t)*p++ << (8 * nc);
+      --n;
+      if (++nc == 8) {
+        h = mix(h, carry);
+        carry = 0;
+        nc = 0;
+      }
+    }
+    size_t w = n / 8;
+    for (size_t i = 0; i < w; ++i) {
+      uint64_t v;
+      memcpy(&v, p + 8 * i, 8);
+      h = mix(h, v);
+    }
+    p += 8 * w;
+    n -= 8 * w;
+    while (n--) carry |= (uint64_t)*p++ << (8 * nc++);
+  }
+  uint64_t final() const { return nc ? mix(h, carry ^ ((uint64_t)nc << 56)) : h; }
+};
+
+std::string hex64(uint64_t a, uint64_t b) {
+  char buf[40];
+  snprintf(buf, sizeof buf, "%016" PRIx64 "%016" PRIx64, a, b);
+  return buf;
+}
+
+std::string url_decode(const std::string& s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size()) {
+      o.push_back((char)strtol(s.substr(i + 1, 2).c_str(), nullptr, 16));
+      i += 2;
+    } else {
+      o.push_back(s[i]);
+    }
+  }
+  return o;
+}
+
+std::string xml_escape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '&') o += "&amp;";
+    else if (c == '<') o += "&lt;";
+    else if (c == '>') o += "&gt;";
+    else o.push_back(c);
+  }
+  return o;
+}
+
+struct Request {
+  std::string method, path, query;
+  std::map<std::string, std::string> q;
+  std::map<std::string, std::string> h;
+  int64_t content_length = 0;
+  bool keep_alive = true;
+};
+
+class Conn {
+ public:
+  explicit Conn(int fd) : fd_(fd), buf_(1 << 20) {}
+  ~Conn() { ::close(fd_); }
+
+  void serve() {
+    for (;;) {
+      Request r;
+      if (!read_request(r)) return;
+      g_reqs++;
+      if (!dispatch(r)) return;
+      if (!r.keep_alive) return;
+    }
+  }
+
+ private:
+  bool fill() {
+    if (pos_ == end_) pos_ = end_ = 0;
+    if (end_ == buf_.size()) {
+      memmove(buf_.data(), buf_.data() + pos_, end_ - pos_);
+      end_ -= pos_;
+      pos_ = 0;
+    }
+    ssize_t r = ::recv(fd_, buf_.data() + end_, buf_.size() - end_, 0);
+    if (r <= 0) return false;
+    end_ += (size_t)r;
+    return true;
+  }
+
+  bool read_request(Request& r) {
+    std::string head;
+    for (;;) {
+      const char* b = (const char*)buf_.data() + pos_;
+      size_t n = end_ - pos_;
+      const char* e = (const char*)memmem(b, n, "\r\n\r\n", 4);
+      if (e) {
+        head.assign(b, (size_t)(e - b));
+        pos_ += (size_t)(e - b) + 4;
+        break;
+      }
+      if (n > 256 * 1024) return false;
+      if (!fill()) return false;
+    }
+    size_t le = head.find("\r\n");
+    std::string line = head.substr(0, le);
+    size_t s1 = line.find(' '), s2 = line.rfind(' ');
+    if (s1 == std::string::npos || s2 == s1) return false;
+    r.method = line.substr(0, s1);
+    std::string target = line.substr(s1 + 1, s2 - s1 - 1);
+    size_t qm = target.find('?');
+    r.path = url_decode(target.substr(0, qm));
+    if (qm != std::string::npos) {
+      r.query = target.substr(qm + 1);
+      size_t i = 0;
+      while (i <= r.query.size()) {
+        size_t amp = r.query.find('&', i);
+        if (amp == std::string::npos) amp = r.query.size();
+        std::string kv = r.query.substr(i, amp - i);
+        size_t eq = kv.find('=');
+        if (!kv.empty())
+          r.q[url_decode(kv.substr(0, eq))] = eq == std::string::npos ? "" : url_decode(kv.substr(eq + 1));
+        i = amp + 1;
+      }
+    }
+    size_t p = le == std::string::npos ? head.size() : le + 2;
+    while (p < head.size()) {
+      size_t e = head.find("\r\n", p);
+      if (e == std::string::npos) e = head.size();
+      std::string hl = head.substr(p, e - p);
+      size_t c = hl.find(':');
+      if (c != std::string::npos) {
+        std::string k = hl.substr(0, c);
+        for (auto& ch : k) ch = (char)tolower((unsigned char)ch);
+        size_t vs = hl.find_first_not_of(' ', c + 1);
+        r.h[k] = vs == std::string::npos ? "" : hl.substr(vs);
+      }
+      p = e + 2;
+    }
+    auto it = r.h.find("content-length");
+    if (it != r.h.end()) r.content_length = atoll(it->second.c_str());
+    it = r.h.find("connection");
+    if (it != r.h.end() && strcasestr(it->second.c_str(), "close")) r.keep_alive = false;
+    return true;
+  }
+
+  // Consume the request body, folding it into `s`; keep up to `keep` bytes in `out`.
+  bool read_body(int64_t n, Summer& s, std::string* out, size_t keep) {
+    while (n > 0) {
+      if (pos_ == end_ && !fill()) return false;
+      size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
+      s.feed(buf_.data() + pos_, k);
+      if (out && out->size() < keep) out->append((const char*)buf_.data() + pos_, std::min(k, keep - out->size()));
+      pos_ += k;
+      n -= (int64_t)k;
+      g_rx += k;
+    }
+    return true;
+  }
+
+  bool send_all(const void* p, size_t n) {
+    const char* c = (const char*)p;
+    while (n) {
+      ssize_t w = ::send(fd_, c, n, MSG_NOSIGNAL);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+      c += w;
+      n -= (size_t)w;
+    }
+    return true;
+  }
+
+  bool respond(int status, const char* reason, const std::string& body,
+               const std::string& extra = "", const char* ctype = "application/xml",
+               bool head_only = false) {
+    char hdr[512];
+    int n = snprintf(hdr, sizeof hdr,
+                     "HTTP/1.1 %d %s\r\nServer: blobd\r\nContent-Type: %s\r\nContent-Length: %zu\r\n",
+                     status, reason, ctype, body.size());
+    std::string out(hdr, (size_t)n);
+    out += extra;
+    out += "\r\n";
+    if (!head_only) out += body;
+    return send_all(out.data(), out.size());
+  }
+
+  bool s3_error(int status, const char* reason, const char* code, const std::string& res) {
+    return respond(status, reason,
+                   std::string("<?xml version=\"1.0\" encoding=\"UTF-8\"?><Error><Code>") + code +
+                       "</Code><Message>" + code + "</Message><Resource>" + xml_escape(res) +
+                       "</Resource></Error>");
+  }
+
+  bool origin(const Request& r) {
+    uint64_t size = g_default_size, seed = 0;
+    auto it = r.q.find("size");
+    if (it != r.q.end()) size = strtoull(it->second.c_str(), nullptr, 10);
+    it = r.q.find("seed");
+    if (it != r.q.end()) seed = strtoull(it->second.c_str(), nullptr, 10);
+    uint64_t start = 0, end = size ? size - 1 : 0;
+    bool ranged = false;
+    it = r.h.find("range");
+    if (it != r.h.end() && it->second.rfind("bytes=", 0) == 0) {
+      std::string spec = it->second.substr(6);
+      size_t dash = spec.find('-');
+      std::string a = spec.substr(0, dash), b = spec.substr(dash + 1);
+      if (a.empty()) {
+        uint64_t suf = strtoull(b.c_str(), nullptr, 10);
+        start = size > suf ? size - suf : 0;
+      } else {
+        start = strtoull(a.c_str(), nullptr, 10);
+        if (!b.empty()) end = std::min<uint64_t>(strtoull(b.c_str(), nullptr, 10), size - 1);
+      }
+      ranged = true;
+      if (start > end || start >= size)
+        return respond(416, "Range Not Satisfiable", "", "Content-Range: bytes */" + std::to_string(size) + "\r\n");
+    }
+    uint64_t len = size ? end - start + 1 : 0;
+    char hdr[512];
+    int n = snprintf(hdr, sizeof hdr,
+                     "HTTP/1.1 %d %s\r\nServer: blobd\r\nContent-Type: video/x-matroska\r\n"
+                     "Accept-Ranges: bytes\r\nContent-Length: %" PRIu64 "\r\n",
+                     ranged ? 206 : 200, ranged ? "Partial Content" : "OK", len);
+    std::string out(hdr, (size_t)n);
+    if (ranged)
+      out += "Content-Range: bytes " + std::to_string(start) + "-" + std::to_string(end) + "/" +
+             std::to_string(size) + "\r\n";
+    out += "\r\n";
+    if (!send_all(out.data(), out.size())) return false;
+    if (r.method == "HEAD") return true;
+    // Object byte at offset o = pool[(o + seed * 7919) % kPool]
+    uint64_t o = start, left = len;
+    while (left) {
+      uint64_t po = (o + seed * 7919ull) % kPool;
+      size_t k = (size_t)std::min<uint64_t>(left, std::min<uint64_t>(kPool - po, 4ull << 20));
+      if (!send_all(g_pool.data() + po, k)) return false;
+      g_tx += k;
+      o += k;
+      left -= k;
+    }
+    return true;
+  }
+
+  bool s3(const Request& r) {
+    std::string p = r.path.substr(1);
+    size_t sl = p.find('/');
+    std::string bucket = p.substr(0, sl), key = sl == std::string::npos ? "" : p.substr(sl + 1);
+    const std::string& m = r.method;
+    if (bucket.empty()) return s3_error(400, "Bad Request", "InvalidBucketName", r.path);
+    if (key.empty()) {
+      if (r.content_length > 0) {
+        Summer s;
+        if (!read_body(r.content_length, s, nullptr, 0)) return false;
+      }
+      std::lock_guard<std::mutex> lk(g_mu);
+      bool exists = g_buckets.count(bucket) > 0;
+      if (m == "HEAD") return respond(exists ? 200 : 404, exists ? "OK" : "Not Found", "", "", "application/xml", true);
+      if (m == "PUT") {
+        if (exists) return s3_error(409, "Conflict", "BucketAlreadyOwnedByYou", bucket);
+        g_buckets[bucket];
+        return respond(200, "OK", "");
+      }
+      if (!exists) return s3_error(404, "Not Found", "NoSuchBucket", bucket);
+      if (m == "GET") {
+        std::string prefix = r.q.count("prefix") ? r.q.at("prefix") : "";
+        std::string body = "<?xml version=\"1.0\" encoding=\"UTF-8\"?><ListBucketResult><Name>" + bucket +
+                           "</Name><IsTruncated>false</IsTruncated>";
+        for (auto& kv : g_buckets[bucket])
+          if (kv.first.compare(0, prefix.size(), prefix) == 0)
+            body += "<Contents><Key>" + xml_escape(kv.first) + "</Key><Size>" + std::to_string(kv.second.size) +
+                    "</Size><ETag>&quot;" + kv.second.etag + "&quot;</ETag></Contents>";
+        body += "</ListBucketResult>";
+        return respond(200, "OK", body);
+      }
+      return s3_error(405, "Method Not Allowed", "MethodNotAllowed", bucket);
+    }
+    // ---- object level
+    if (m == "PUT") {
+      Object o;
+      Summer s;
+      if (!read_body(r.content_length, s, &o.data, g_keep_bytes)) return false;
+      if ((uint64_t)r.content_length > g_keep_bytes) o.data.clear();
+      o.size = (uint64_t)r.content_length;
+      o.sum = s.final();
+      o.etag = hex64(o.sum, o.size);
+      auto up = r.q.find("uploadId");
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (up != r.q.end()) {
+        auto it = g_uploads.find(up->second);
+        if (it == g_uploads.end()) return s3_error(404, "Not Found", "NoSuchUpload", key);
+        int num = atoi(r.q.count("partNumber") ? r.q.at("partNumber").c_str() : "0");
+        std::string et = o.etag;
+        it->second.parts[num] = std::move(o);
+        return respond(200, "OK", "", "ETag: \"" + et + "\"\r\n");
+      }
+      if (!g_buckets.count(bucket)) return s3_error(404, "Not Found", "NoSuchBucket", bucket);
+      std::string et = o.etag;
+      g_buckets[bucket][key] = std::move(o);
+      g_objects++;
+      return respond(200, "OK", "", "ETag: \"" + et + "\"\r\n");
+    }
+    if (m == "POST") {
+      Summer s;
+      std::string body;
+      if (!read_body(r.content_length, s, &body, 1 << 20)) return false;
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (r.q.count("uploads")) {
+        std::string id = "up" + std::to_string(g_upload_seq++);
+        g_uploads[id] = Upload{bucket, key, {}};
+        return respond(200, "OK",
+                       "<?xml version=\"1.0\" encoding=\"UTF-8\"?><InitiateMultipartUploadResult><Bucket>" +
+                           bucket + "</Bucket><Key>" + xml_escape(key) + "</Key><UploadId>" + id +
+                           "</UploadId></InitiateMultipartUploadResult>");
+      }
+      auto up = r.q.find("uploadId");
+      if (up != r.q.end()) {
+        auto it = g_uploads.find(up->second);
+        if (it == g_uploads.end()) return s3_error(404, "Not Found", "NoSuchUpload", key);
+        Object o;
+        uint64_t h = 0x5bd1e995ull;
+        for (auto& kv : it->second.parts) {
+          o.size += kv.second.size;
+          h = mix(h, kv.second.sum);
+          if (o.size <= g_keep_bytes) o.data += kv.second.data;
+        }
+        if (o.size > g_keep_bytes) o.data.clear();
+        o.sum = h;
+        o.etag = hex64(h, o.size) + "-" + std::to_string(it->second.parts.size());
+        std::string et = o.etag;
+        g_buckets[bucket][key] = std::move(o);
+        g_uploads.erase(it);
+        g_objects++;
+        return respond(200, "OK",
+                       "<?xml version=\"1.0\" encoding=\"UTF-8\"?><CompleteMultipartUploadResult><Bucket>" +
+                           bucket + "</Bucket><Key>" + xml_escape(key) + "</Key><ETag>&quot;" + et +
+                           "&quot;</ETag></CompleteMultipartUploadResult>");
+      }
+      return s3_error(400, "Bad Request", "InvalidRequest", key);
+    }
+    if (r.content_length > 0) {
+      Summer s;
+      if (!read_body(r.content_length, s, nullptr, 0)) return false;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (m == "DELETE") {
+      auto up = r.q.find("uploadId");
+      if (up != r.q.end()) g_uploads.erase(up->second);
+      else if (g_buckets.count(bucket)) g_buckets[bucket].erase(key);
+      return respond(204, "No Content", "");
+    }
+    auto b = g_buckets.find(bucket);
+    if (b == g_buckets.end()) return s3_error(404, "Not Found", "NoSuchBucket", bucket);
+    auto o = b->second.find(key);
+    if (o == b->second.end()) {
+      if (m == "HEAD") return respond(404, "Not Found", "", "", "application/xml", true);
+      return s3_error(404, "Not Found", "NoSuchKey", key);
+    }
+    std::string extra = "ETag: \"" + o->second.etag + "\"\r\nX-Blobd-Sum: " + std::to_string(o->second.sum) + "\r\n";
+    if (m == "HEAD") {
+      char hdr[256];
+      int n = snprintf(hdr, sizeof hdr, "HTTP/1.1 200 OK\r\nContent-Length: %" PRIu64 "\r\n", o->second.size);
+      std::string out(hdr, (size_t)n);
+      out += extra + "\r\n";
+      return send_all(out.data(), out.size());
+    }
+    if (o->second.data.size() != o->second.size)
+      return s3_error(501, "Not Implemented", "NotStored", key);  // large bodies are not retained
+    return respond(200, "OK", o->second.data, extra, "application/octet-stream");
+  }
+
+  bool stats() {
+    char b[512];
+    size_t nup;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      nup = g_uploads.size();
+    }
+    snprintf(b, sizeof b,
+             "{\"bytes_received\":%" PRIu64 ",\"bytes_served\":%" PRIu64 ",\"requests\":%" PRIu64
+             ",\"objects\":%" PRIu64 ",\"open_uploads\":%zu}",
+             g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup);
+    return respond(200, "OK", b, "", "application/json");
+  }
+
+  bool dispatch(const Request& r) {
+    if (r.path == "/_stats") return stats();
+    if (r.path.rfind("/media/", 0) == 0 && (r.method == "GET" || r.method == "HEAD")) return origin(r);
+    return s3(r);
+  }
+
+  int fd_;
+  std::vector<uint8_t> buf_;
+  size_t pos_ = 0, end_ = 0;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  int port = 0;
+  std::string host = "127.0.0.1";
+  const char* port_file = nullptr;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&] { return i + 1 < argc ? argv[++i] : (char*)""; };
+    if (a == "--port") port = atoi(next());
+    else if (a == "--host") host = next();
+    else if (a == "--port-file") port_file = next();
+    else if (a == "--keep-bytes") g_keep_bytes = strtoull(next(), nullptr, 10);
+    else if (a == "--default-size") g_default_size = strtoull(next(), nullptr, 10);
+    else {
+      fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] [--default-size N]\n");
+      return 2;
+    }
+  }
+  signal(SIGPIPE, SIG_IGN);
+  g_pool.resize(kPool);
+  std::mt19937_64 rng(0xB10BDull);
+  for (size_t i = 0; i < kPool; i += 8) {
+    uint64_t v = rng();
+    memcpy(g_pool.data() + i, &v, 8);
+  }
+  int ls = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)port);
+  inet_pton(AF_INET, host.c_str(), &sa.sin_addr);
+  if (bind(ls, (sockaddr*)&sa, sizeof sa) < 0 || listen(ls, 1024) < 0) {
+    perror("bind/listen");
+    return 1;
+  }
+  socklen_t sl = sizeof sa;
+  getsockname(ls, (sockaddr*)&sa, &sl);
+  int bound = ntohs(sa.sin_port);
+  if (port_file) {
+    std::string tmp = std::string(port_file) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "w");
+    if (f) {
+      fprintf(f, "%d\n", bound);
+      fclose(f);
+      rename(tmp.c_str(), port_file);
+    }
+  }
+  printf("blobd listening on %s:%d\n", host.c_str(), bound);
+  fflush(stdout);
+  for (;;) {
+    int fd = accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
+    if (fd < 0) {
+      if (errno == EINTR || errno == ECONNABORTED) continue;
+      perror("accept");
+      continue;
+    }
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    int big = 4 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+    std::thread([fd] {
+      Conn c(fd);
+      c.serve();
+    }).detach();
+  }
+}

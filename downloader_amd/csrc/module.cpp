@@ -1,0 +1,242 @@
+// pybind11 bindings for the stager host-native module `_native`.
+// Every entry point that touches bytes releases the GIL so asyncio worker threads (and
+// several jobs in one worker process) run hashing and transfers truly in parallel.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "native.h"
+
+namespace py = pybind11;
+using namespace stager;
+
+namespace {
+
+struct BufView {
+  const uint8_t* p;
+  size_t n;
+  py::buffer_info info;  // keeps the exporter alive/locked
+};
+
+BufView view(const py::buffer& b) {
+  py::buffer_info info = b.request();
+  if (info.ndim > 1 && info.strides.back() != info.itemsize)
+    throw std::invalid_argument("buffer must be C-contiguous");
+  size_t n = (size_t)info.size * (size_t)info.itemsize;
+  return BufView{(const uint8_t*)info.ptr, n, std::move(info)};
+}
+
+py::dict head_to_dict(const ResponseHead& h) {
+  py::dict d;
+  d["status"] = h.status;
+  d["reason"] = h.reason;
+  py::list hs;
+  for (auto& kv : h.headers) hs.append(py::make_tuple(kv.first, kv.second));
+  d["headers"] = hs;
+  d["content_length"] = h.content_length;
+  d["chunked"] = h.chunked;
+  d["keep_alive"] = h.keep_alive;
+  return d;
+}
+
+ResponseHead dict_to_head(const py::dict& d) {
+  ResponseHead h;
+  h.status = d["status"].cast<int>();
+  h.content_length = d["content_length"].cast<int64_t>();
+  h.chunked = d["chunked"].cast<bool>();
+  h.keep_alive = d["keep_alive"].cast<bool>();
+  return h;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "stager host-native byte paths: hashing (OpenSSL EVP, threaded) and zero-copy HTTP";
+
+  m.def("digest_size", &digest_size);
+  m.def(
+      "digest",
+      [](const std::string& algo, const py::buffer& data) {
+        BufView v = view(data);
+        std::string out;
+        {
+          py::gil_scoped_release rel;
+          out = digest(algo, v.p, v.n);
+        }
+        return py::bytes(out);
+      },
+      py::arg("algo"), py::arg("data"));
+  m.def(
+      "hash_pieces",
+      [](const std::string& algo, const py::buffer& data, size_t piece_len, int threads) {
+        BufView v = view(data);
+        std::string out;
+        {
+          py::gil_scoped_release rel;
+          out = hash_pieces(algo, v.p, v.n, piece_len, threads);
+        }
+        return py::bytes(out);
+      },
+      py::arg("algo"), py::arg("data"), py::arg("piece_len"), py::arg("threads") = 0,
+      "Concatenated per-piece digests of a contiguous buffer.");
+  m.def(
+      "verify_pieces",
+      [](const std::vector<std::pair<std::string, int64_t>>& files, int64_t piece_len,
+         const py::bytes& hashes, const std::vector<int64_t>& which, int threads) {
+        std::string hs = hashes;
+        std::vector<uint8_t> ok;
+        {
+          py::gil_scoped_release rel;
+          ok = verify_pieces(files, piece_len, hs, which, threads);
+        }
+        return py::bytes((const char*)ok.data(), ok.size());
+      },
+      py::arg("files"), py::arg("piece_len"), py::arg("hashes"),
+      py::arg("which") = std::vector<int64_t>{}, py::arg("threads") = 0,
+      "SHA-1 verify torrent pieces stored across `files` [(path, length)]; returns one byte "
+      "(0/1) per checked piece.");
+  m.def(
+      "hash_storage_pieces",
+      [](const std::vector<std::pair<std::string, int64_t>>& files, int64_t piece_len,
+         const std::string& algo, int threads) {
+        std::string out;
+        {
+          py::gil_scoped_release rel;
+          out = hash_storage_pieces(files, piece_len, algo, threads);
+        }
+        return py::bytes(out);
+      },
+      py::arg("files"), py::arg("piece_len"), py::arg("algo") = "sha1", py::arg("threads") = 0);
+  m.def(
+      "hash_file_ranges",
+      [](const std::string& path, const std::vector<std::pair<int64_t, int64_t>>& ranges,
+         const std::string& algo, int threads) {
+        std::vector<std::string> out;
+        {
+          py::gil_scoped_release rel;
+          out = hash_file_ranges(path, ranges, algo, threads);
+        }
+        py::list l;
+        for (auto& s : out) l.append(py::bytes(s));
+        return l;
+      },
+      py::arg("path"), py::arg("ranges"), py::arg("algo"), py::arg("threads") = 0);
+
+  py::class_<Hasher>(m, "Hasher")
+      .def(py::init<const std::string&>())
+      .def("update",
+           [](Hasher& h, const py::buffer& data) {
+             BufView v = view(data);
+             if (v.n >= 65536) {
+               py::gil_scoped_release rel;
+               h.update(v.p, v.n);
+             } else {
+               h.update(v.p, v.n);
+             }
+           })
+      .def("update_fd",
+           [](Hasher& h, int fd, int64_t off, int64_t len) {
+             py::gil_scoped_release rel;
+             h.update_fd(fd, off, len);
+           })
+      .def("digest", [](const Hasher& h) { return py::bytes(h.digest()); })
+      .def("hexdigest",
+           [](const Hasher& h) {
+             std::string d = h.digest();
+             static const char* hx = "0123456789abcdef";
+             std::string s;
+             for (unsigned char c : d) {
+               s.push_back(hx[c >> 4]);
+               s.push_back(hx[c & 15]);
+             }
+             return s;
+           })
+      .def("copy", [](const Hasher& h) { return h.copy(); })
+      .def_property_readonly("name", &Hasher::algo);
+
+  py::class_<Progress>(m, "Progress")
+      .def(py::init<>())
+      .def_property_readonly("bytes", [](const Progress& p) { return p.bytes.load(); })
+      .def("cancel", [](Progress& p) { p.cancelled.store(true); })
+      .def_property_readonly("cancelled", [](const Progress& p) { return p.cancelled.load(); });
+
+  py::class_<HttpConn>(m, "HttpConn")
+      .def(py::init([](const std::string& host, int port, double cto, double iot) {
+             py::gil_scoped_release rel;
+             return new HttpConn(host, port, cto, iot);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("connect_timeout") = 10.0,
+           py::arg("io_timeout") = 300.0)
+      .def(
+          "request",
+          [](HttpConn& c, const py::bytes& head, const py::object& body, bool expect_body,
+             int64_t max_body) {
+            std::string hs = head;
+            std::string bs;
+            if (!body.is_none()) bs = body.cast<std::string>();
+            ResponseHead h;
+            std::string rb;
+            {
+              py::gil_scoped_release rel;
+              c.send_request(hs, (const uint8_t*)bs.data(), bs.size());
+              h = c.read_head();
+              if (expect_body) rb = c.read_body(h, max_body);
+            }
+            py::dict d = head_to_dict(h);
+            d["body"] = py::bytes(rb);
+            return d;
+          },
+          py::arg("head"), py::arg("body") = py::none(), py::arg("expect_body") = true,
+          py::arg("max_body") = (int64_t)64 << 20,
+          "Send a request with an in-memory body; return head + body.")
+      .def(
+          "request_fd",
+          [](HttpConn& c, const py::bytes& head, int fd, int64_t off, int64_t len,
+             Progress* prog, int64_t max_body) {
+            std::string hs = head;
+            ResponseHead h;
+            std::string rb;
+            {
+              py::gil_scoped_release rel;
+              c.send_request_fd(hs, fd, off, len, prog);
+              h = c.read_head();
+              rb = c.read_body(h, max_body);
+            }
+            py::dict d = head_to_dict(h);
+            d["body"] = py::bytes(rb);
+            return d;
+          },
+          py::arg("head"), py::arg("fd"), py::arg("offset"), py::arg("length"),
+          py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)64 << 20,
+          "Send a request whose body is a file range (sendfile); return head + body.")
+      .def(
+          "get_to_fd",
+          [](HttpConn& c, const py::bytes& head, int fd, int64_t off, int64_t max_bytes,
+             Progress* prog, int64_t max_err_body) {
+            std::string hs = head;
+            ResponseHead h;
+            int64_t n = 0;
+            std::string err;
+            {
+              py::gil_scoped_release rel;
+              c.send_request(hs, nullptr, 0);
+              h = c.read_head();
+              if (h.status >= 200 && h.status < 300)
+                n = c.read_body_to_fd(h, fd, off, max_bytes, prog);
+              else
+                err = c.read_body(h, max_err_body);
+            }
+            py::dict d = head_to_dict(h);
+            d["written"] = n;
+            d["body"] = py::bytes(err);
+            return d;
+          },
+          py::arg("head"), py::arg("fd"), py::arg("offset") = 0,
+          py::arg("max_bytes") = (int64_t)1 << 50, py::arg("progress") = nullptr,
+          py::arg("max_err_body") = (int64_t)1 << 20,
+          "Send a body-less request; a 2xx body is spliced into `fd` at `offset`.")
+      .def("close", &HttpConn::close)
+      .def_property_readonly("is_open", &HttpConn::is_open)
+      .def_property_readonly("reusable", &HttpConn::reusable)
+      .def_property_readonly("host", &HttpConn::host)
+      .def_property_readonly("port", &HttpConn::port);
+}

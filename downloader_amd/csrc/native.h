@@ -1,0 +1,125 @@
+// Shared declarations of the stager native module (_native).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+typedef struct evp_md_ctx_st EVP_MD_CTX;
+typedef struct evp_md_st EVP_MD;
+
+namespace stager {
+
+// ---- hashing.cpp -----------------------------------------------------------------------
+const EVP_MD* md_for(const std::string& algo);
+size_t digest_size(const std::string& algo);
+int resolve_threads(int threads, size_t work_items);
+
+class Hasher {
+ public:
+  explicit Hasher(const std::string& algo);
+  ~Hasher();
+  Hasher(const Hasher&) = delete;
+  Hasher& operator=(const Hasher&) = delete;
+  void update(const uint8_t* p, size_t n);
+  void update_fd(int fd, int64_t offset, int64_t length);
+  std::string digest() const;
+  std::unique_ptr<Hasher> copy() const;
+  const std::string& algo() const { return algo_; }
+
+ private:
+  std::string algo_;
+  EVP_MD_CTX* ctx_;
+};
+
+std::string digest(const std::string& algo, const uint8_t* p, size_t n);
+std::string hash_pieces(const std::string& algo, const uint8_t* p, size_t n, size_t piece_len,
+                        int threads);
+
+struct Storage {
+  struct Entry {
+    std::string path;
+    int64_t length;
+    int64_t offset;
+    int fd;
+  };
+  explicit Storage(const std::vector<std::pair<std::string, int64_t>>& files);
+  ~Storage();
+  void open_all(bool missing_ok);
+  void close_all();
+  bool read(int64_t off, int64_t len, uint8_t* buf) const;
+  std::vector<Entry> entries;
+  int64_t total = 0;
+};
+
+std::vector<uint8_t> verify_pieces(const std::vector<std::pair<std::string, int64_t>>& files,
+                                   int64_t piece_len, const std::string& hashes,
+                                   const std::vector<int64_t>& which, int threads);
+std::string hash_storage_pieces(const std::vector<std::pair<std::string, int64_t>>& files,
+                                int64_t piece_len, const std::string& algo, int threads);
+std::vector<std::string> hash_file_ranges(const std::string& path,
+                                          const std::vector<std::pair<int64_t, int64_t>>& ranges,
+                                          const std::string& algo, int threads);
+
+// ---- transfer.cpp ----------------------------------------------------------------------
+// Byte counter shared between a transfer running on a worker thread and the asyncio side
+// (progress telemetry, stall watchdog, cancellation).
+struct Progress {
+  std::atomic<int64_t> bytes{0};
+  std::atomic<bool> cancelled{false};
+};
+
+struct ResponseHead {
+  int status = 0;
+  std::string reason;
+  std::vector<std::pair<std::string, std::string>> headers;  // lower-cased names
+  int64_t content_length = -1;
+  bool chunked = false;
+  bool keep_alive = true;
+};
+
+class HttpConn {
+ public:
+  HttpConn(const std::string& host, int port, double connect_timeout_s, double io_timeout_s);
+  ~HttpConn();
+  HttpConn(const HttpConn&) = delete;
+  HttpConn& operator=(const HttpConn&) = delete;
+
+  // Send `head` (request line + headers + CRLFCRLF) and an optional in-memory body.
+  void send_request(const std::string& head, const uint8_t* body, size_t body_len);
+  // Send `head` and then `len` bytes of file `fd` from `off` with sendfile(2).
+  void send_request_fd(const std::string& head, int fd, int64_t off, int64_t len,
+                       Progress* prog);
+  ResponseHead read_head();
+  // Body into memory (bounded by max_bytes).
+  std::string read_body(const ResponseHead& h, int64_t max_bytes);
+  // Body into fd at `offset` (splice for Content-Length bodies, read/pwrite for chunked).
+  int64_t read_body_to_fd(const ResponseHead& h, int fd, int64_t offset, int64_t max_bytes,
+                          Progress* prog);
+  // Drain and discard a body (keeps the connection reusable).
+  void discard_body(const ResponseHead& h);
+  void close();
+  bool is_open() const { return fd_ >= 0; }
+  bool reusable() const { return fd_ >= 0 && reusable_; }
+  const std::string& host() const { return host_; }
+  int port() const { return port_; }
+
+ private:
+  size_t recv_some(uint8_t* p, size_t n);
+  void send_all(const uint8_t* p, size_t n);
+  std::string read_line();
+  int64_t take_buffered(uint8_t* p, int64_t n);
+  std::string host_;
+  int port_;
+  int fd_ = -1;
+  int pipe_[2] = {-1, -1};
+  size_t pipe_sz_ = 0;
+  bool reusable_ = true;
+  std::vector<uint8_t> rbuf_;
+  size_t rpos_ = 0, rend_ = 0;
+};
+
+}  // namespace stager

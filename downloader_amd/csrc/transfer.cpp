@@ -1,0 +1,432 @@
+// Native HTTP/1.1 transport for the staging hot loops (SURVEY.md §3 "hot loops"):
+//   (1) network -> disk: response bodies are spliced socket -> pipe -> file, so the payload
+//       never crosses into user space (the reference pipes `request` into a write stream,
+//       lib/download.js:159-160).
+//   (2) disk -> network: request bodies go file -> socket with sendfile(2) (the reference's
+//       minio-js fPutObject reads the file into JS buffers, lib/upload.js:45).
+// The Python side owns protocol logic (URLs, SigV4, retries); this layer owns bytes. Every
+// call blocks its calling thread and is invoked with the GIL released.
+#include "native.h"
+
+#include <arpa/inet.h>
+#include <cerrno>
+#include <cstring>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <stdexcept>
+#include <sys/sendfile.h>
+#include <sys/socket.h>
+#include <sys/types.h>
+#include <unistd.h>
+
+namespace stager {
+
+namespace {
+
+struct IoError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+std::string errstr(const char* what) { return std::string(what) + ": " + strerror(errno); }
+
+void set_timeouts(int fd, double s) {
+  if (s <= 0) return;
+  timeval tv;
+  tv.tv_sec = (time_t)s;
+  tv.tv_usec = (suseconds_t)((s - (double)tv.tv_sec) * 1e6);
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+}
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = (char)tolower((unsigned char)c);
+  return s;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t");
+  size_t b = s.find_last_not_of(" \t\r\n");
+  if (a == std::string::npos) return "";
+  return s.substr(a, b - a + 1);
+}
+
+}  // namespace
+
+HttpConn::HttpConn(const std::string& host, int port, double connect_timeout_s,
+                   double io_timeout_s)
+    : host_(host), port_(port), rbuf_(64 * 1024) {
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  std::string ps = std::to_string(port);
+  int rc = getaddrinfo(host.c_str(), ps.c_str(), &hints, &res);
+  if (rc != 0) throw IoError("getaddrinfo(" + host + "): " + gai_strerror(rc));
+  std::string last = "connect failed";
+  for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+    int fd = socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, ai->ai_protocol);
+    if (fd < 0) continue;
+    int r = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    if (r < 0 && errno == EINPROGRESS) {
+      pollfd p{fd, POLLOUT, 0};
+      int to = connect_timeout_s > 0 ? (int)(connect_timeout_s * 1000) : -1;
+      int pr = poll(&p, 1, to);
+      int soerr = 0;
+      socklen_t sl = sizeof(soerr);
+      if (pr == 1) getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl);
+      if (pr != 1 || soerr != 0) {
+        last = pr == 0 ? "connect timeout" : std::string("connect: ") + strerror(soerr ? soerr : errno);
+        ::close(fd);
+        continue;
+      }
+    } else if (r < 0) {
+      last = errstr("connect");
+      ::close(fd);
+      continue;
+    }
+    int fl = fcntl(fd, F_GETFL);
+    fcntl(fd, F_SETFL, fl & ~O_NONBLOCK);
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    int big = 4 << 20;
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &big, sizeof(big));
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &big, sizeof(big));
+    set_timeouts(fd, io_timeout_s);
+    fd_ = fd;
+    break;
+  }
+  freeaddrinfo(res);
+  if (fd_ < 0) throw IoError(last + " (" + host + ":" + ps + ")");
+}
+
+HttpConn::~HttpConn() { close(); }
+
+void HttpConn::close() {
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+  for (int i = 0; i < 2; ++i)
+    if (pipe_[i] >= 0) {
+      ::close(pipe_[i]);
+      pipe_[i] = -1;
+    }
+}
+
+void HttpConn::send_all(const uint8_t* p, size_t n) {
+  while (n) {
+    ssize_t w = ::send(fd_, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      reusable_ = false;
+      throw IoError(errstr("send"));
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+}
+
+size_t HttpConn::recv_some(uint8_t* p, size_t n) {
+  for (;;) {
+    ssize_t r = ::recv(fd_, p, n, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      reusable_ = false;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) throw IoError("recv timeout");
+      throw IoError(errstr("recv"));
+    }
+    return (size_t)r;
+  }
+}
+
+void HttpConn::send_request(const std::string& head, const uint8_t* body, size_t body_len) {
+  if (fd_ < 0) throw IoError("connection closed");
+  if (body_len && body_len <= 64 * 1024) {
+    std::string all = head;
+    all.append((const char*)body, body_len);
+    send_all((const uint8_t*)all.data(), all.size());
+    return;
+  }
+  send_all((const uint8_t*)head.data(), head.size());
+  if (body_len) send_all(body, body_len);
+}
+
+void HttpConn::send_request_fd(const std::string& head, int fd, int64_t off, int64_t len,
+                               Progress* prog) {
+  if (fd_ < 0) throw IoError("connection closed");
+  int cork = 1;
+  setsockopt(fd_, IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+  send_all((const uint8_t*)head.data(), head.size());
+  off_t o = (off_t)off;
+  int64_t left = len;
+  while (left > 0) {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      throw IoError("cancelled");
+    }
+    size_t chunk = (size_t)std::min<int64_t>(left, 8 << 20);
+    ssize_t w = ::sendfile(fd_, fd, &o, chunk);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      reusable_ = false;
+      throw IoError(errstr("sendfile"));
+    }
+    if (w == 0) {
+      reusable_ = false;
+      throw IoError("sendfile: source file shorter than declared length");
+    }
+    left -= w;
+    if (prog) prog->bytes.fetch_add(w, std::memory_order_relaxed);
+  }
+  cork = 0;
+  setsockopt(fd_, IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+}
+
+std::string HttpConn::read_line() {
+  std::string line;
+  for (;;) {
+    while (rpos_ < rend_) {
+      char c = (char)rbuf_[rpos_++];
+      line.push_back(c);
+      if (c == '\n') return line;
+      if (line.size() > 64 * 1024) throw IoError("header line too long");
+    }
+    rpos_ = rend_ = 0;
+    size_t r = recv_some(rbuf_.data(), rbuf_.size());
+    if (r == 0) {
+      reusable_ = false;
+      if (line.empty()) throw IoError("connection closed by peer");
+      return line;
+    }
+    rend_ = r;
+  }
+}
+
+ResponseHead HttpConn::read_head() {
+  ResponseHead h;
+  std::string status;
+  do {
+    status = read_line();
+  } while (status == "\r\n");  // tolerate stray CRLF
+  // HTTP/1.1 200 OK
+  if (status.compare(0, 5, "HTTP/") != 0) {
+    reusable_ = false;
+    throw IoError("malformed status line: " + trim(status));
+  }
+  size_t sp = status.find(' ');
+  h.status = atoi(status.c_str() + sp + 1);
+  size_t sp2 = status.find(' ', sp + 1);
+  h.reason = sp2 == std::string::npos ? "" : trim(status.substr(sp2 + 1));
+  bool http10 = status.compare(0, 8, "HTTP/1.0") == 0;
+  h.keep_alive = !http10;
+  for (;;) {
+    std::string line = read_line();
+    if (line == "\r\n" || line == "\n" || line.empty()) break;
+    size_t c = line.find(':');
+    if (c == std::string::npos) continue;
+    std::string k = lower(trim(line.substr(0, c)));
+    std::string v = trim(line.substr(c + 1));
+    if (k == "content-length") h.content_length = atoll(v.c_str());
+    if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) h.chunked = true;
+    if (k == "connection") {
+      std::string lv = lower(v);
+      if (lv.find("close") != std::string::npos) h.keep_alive = false;
+      if (lv.find("keep-alive") != std::string::npos) h.keep_alive = true;
+    }
+    h.headers.emplace_back(k, v);
+  }
+  if (!h.keep_alive) reusable_ = false;
+  if (h.content_length < 0 && !h.chunked && h.status != 204 && h.status != 304) {
+    // Body delimited by connection close.
+    reusable_ = false;
+  }
+  return h;
+}
+
+int64_t HttpConn::take_buffered(uint8_t* p, int64_t n) {
+  int64_t k = std::min<int64_t>(n, (int64_t)(rend_ - rpos_));
+  if (k > 0) {
+    memcpy(p, rbuf_.data() + rpos_, (size_t)k);
+    rpos_ += (size_t)k;
+  }
+  return k;
+}
+
+std::string HttpConn::read_body(const ResponseHead& h, int64_t max_bytes) {
+  std::string out;
+  auto append = [&](int64_t n, bool until_close) {
+    int64_t got = 0;
+    std::vector<uint8_t> tmp(64 * 1024);
+    while (until_close || got < n) {
+      int64_t want = until_close ? (int64_t)tmp.size() : std::min<int64_t>(n - got, (int64_t)tmp.size());
+      int64_t k = take_buffered(tmp.data(), want);
+      if (k == 0) {
+        size_t r = recv_some(tmp.data(), (size_t)want);
+        if (r == 0) {
+          if (until_close) break;
+          reusable_ = false;
+          throw IoError("connection closed mid-body");
+        }
+        k = (int64_t)r;
+      }
+      if ((int64_t)out.size() + k > max_bytes) {
+        reusable_ = false;
+        throw IoError("response body exceeds limit");
+      }
+      out.append((const char*)tmp.data(), (size_t)k);
+      got += k;
+    }
+  };
+  if (h.chunked) {
+    for (;;) {
+      std::string line = read_line();
+      int64_t n = strtoll(line.c_str(), nullptr, 16);
+      if (n == 0) {
+        while (true) {
+          std::string t = read_line();
+          if (t == "\r\n" || t.empty()) break;
+        }
+        break;
+      }
+      append(n, false);
+      read_line();
+    }
+  } else if (h.content_length >= 0) {
+    append(h.content_length, false);
+  } else if (h.status != 204 && h.status != 304) {
+    append(0, true);
+  }
+  return out;
+}
+
+int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
+                                  int64_t max_bytes, Progress* prog) {
+  int64_t written = 0;
+  auto check_cancel = [&] {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      throw IoError("cancelled");
+    }
+  };
+  auto pwrite_all = [&](const uint8_t* p, int64_t n) {
+    while (n > 0) {
+      ssize_t w = ::pwrite(fd, p, (size_t)n, offset + written);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        reusable_ = false;
+        throw IoError(errstr("pwrite"));
+      }
+      p += w;
+      n -= w;
+      written += w;
+      if (prog) prog->bytes.fetch_add(w, std::memory_order_relaxed);
+    }
+  };
+  // Copy exactly n bytes (or until EOF when n < 0) from the socket into fd.
+  auto copy_n = [&](int64_t n) {
+    if (written + std::max<int64_t>(n, 0) > max_bytes) {
+      reusable_ = false;
+      throw IoError("response body exceeds limit");
+    }
+    // 1) bytes already buffered after the header.
+    if (rpos_ < rend_) {
+      int64_t k = n < 0 ? (int64_t)(rend_ - rpos_) : std::min<int64_t>(n, (int64_t)(rend_ - rpos_));
+      pwrite_all(rbuf_.data() + rpos_, k);
+      rpos_ += (size_t)k;
+      if (n >= 0) n -= k;
+    }
+    if (n == 0) return;
+    // 2) zero-copy: socket -> pipe -> file.
+    if (pipe_[0] < 0) {
+      if (pipe2(pipe_, O_CLOEXEC) == 0) {
+        int want = 1 << 20;
+        int got = fcntl(pipe_[1], F_SETPIPE_SZ, want);
+        pipe_sz_ = got > 0 ? (size_t)got : 65536;
+      }
+    }
+    if (pipe_[0] >= 0) {
+      while (n != 0) {
+        check_cancel();
+        size_t want = n < 0 ? pipe_sz_ : (size_t)std::min<int64_t>(n, (int64_t)pipe_sz_);
+        ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+        if (in < 0) {
+          if (errno == EINTR) continue;
+          if (errno == EINVAL) break;  // fs does not support splice: fall back below
+          reusable_ = false;
+          if (errno == EAGAIN) throw IoError("recv timeout");
+          throw IoError(errstr("splice(sock)"));
+        }
+        if (in == 0) {
+          if (n < 0) return;
+          reusable_ = false;
+          throw IoError("connection closed mid-body");
+        }
+        ssize_t left = in;
+        while (left > 0) {
+          loff_t o = offset + written;
+          ssize_t out = ::splice(pipe_[0], nullptr, fd, &o, (size_t)left, SPLICE_F_MOVE);
+          if (out < 0) {
+            if (errno == EINTR) continue;
+            reusable_ = false;
+            throw IoError(errstr("splice(file)"));
+          }
+          left -= out;
+          written += out;
+          if (prog) prog->bytes.fetch_add(out, std::memory_order_relaxed);
+        }
+        if (n > 0) n -= in;
+        if (written > max_bytes) {
+          reusable_ = false;
+          throw IoError("response body exceeds limit");
+        }
+      }
+      if (n == 0) return;
+    }
+    // 3) fallback: recv + pwrite.
+    std::vector<uint8_t> tmp(1 << 20);
+    while (n != 0) {
+      check_cancel();
+      size_t want = n < 0 ? tmp.size() : (size_t)std::min<int64_t>(n, (int64_t)tmp.size());
+      size_t r = recv_some(tmp.data(), want);
+      if (r == 0) {
+        if (n < 0) return;
+        reusable_ = false;
+        throw IoError("connection closed mid-body");
+      }
+      pwrite_all(tmp.data(), (int64_t)r);
+      if (n > 0) n -= (int64_t)r;
+    }
+  };
+  if (h.chunked) {
+    for (;;) {
+      std::string line = read_line();
+      int64_t n = strtoll(line.c_str(), nullptr, 16);
+      if (n == 0) {
+        while (true) {
+          std::string t = read_line();
+          if (t == "\r\n" || t.empty()) break;
+        }
+        break;
+      }
+      copy_n(n);
+      read_line();
+    }
+  } else if (h.content_length >= 0) {
+    copy_n(h.content_length);
+  } else {
+    copy_n(-1);
+    reusable_ = false;
+  }
+  return written;
+}
+
+void HttpConn::discard_body(const ResponseHead& h) {
+  if (h.chunked || h.content_length > 0) {
+    read_body(h, (int64_t)1 << 40);
+  } else if (h.content_length < 0 && h.status != 204 && h.status != 304) {
+    reusable_ = false;
+  }
+}
+
+}  // namespace stager

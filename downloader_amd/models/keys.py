@@ -1,0 +1,64 @@
+"""S3 staging layout: object keys and the done marker.
+
+Reference contract:
+  * bucket ``triton-staging`` (lib/main.js:120, lib/upload.js:29-30)
+  * object key ``path.join(mediaId, 'original/', base64(basename(file)))`` (lib/upload.js:43-45)
+  * done marker ``path.join(mediaId, 'original/', 'done')`` with body ``"true"`` (lib/upload.js:55)
+
+``path.join`` is Node's POSIX join, which normalises the result: repeated slashes collapse,
+``.``/``..`` segments resolve and a trailing slash is kept. Standard base64 may contain ``/``
+(and ``//``), so the normalisation is observable in the key and is
+reproduced exactly here.
+"""
+from __future__ import annotations
+
+import base64
+import os
+
+STAGING_BUCKET = "triton-staging"
+DONE_BODY = b"true"
+
+
+def node_normalize(p: str) -> str:
+    """POSIX ``path.normalize`` with Node semantics."""
+    if p == "":
+        return "."
+    absolute = p.startswith("/")
+    trailing = p.endswith("/")
+    out: list[str] = []
+    for seg in p.split("/"):
+        if seg == "" or seg == ".":
+            continue
+        if seg == "..":
+            if out and out[-1] != "..":
+                out.pop()
+            elif not absolute:
+                out.append("..")
+            continue
+        out.append(seg)
+    s = "/".join(out)
+    if not s and not absolute:
+        s = "."
+    if s and trailing:
+        s += "/"
+    return ("/" + s) if absolute else s
+
+
+def node_join(*parts: str) -> str:
+    """POSIX ``path.join`` with Node semantics (empty segments dropped, then normalised)."""
+    joined = "/".join(p for p in parts if p)
+    return node_normalize(joined) if joined else "."
+
+
+def b64_name(basename: str) -> str:
+    """Standard-alphabet base64 of the UTF-8 basename (``Buffer.from(s).toString('base64')``)."""
+    return base64.b64encode(basename.encode("utf-8")).decode("ascii")
+
+
+def object_key(media_id: str, file_path: str) -> str:
+    """``<id>/original/<b64(basename)>`` exactly as lib/upload.js:43-44 builds it."""
+    return node_join(media_id, "original/", b64_name(os.path.basename(file_path)))
+
+
+def done_key(media_id: str) -> str:
+    return node_join(media_id, "original/", "done")

@@ -1,0 +1,327 @@
+"""HTTP/1.1 transports used by the S3 client and the HTTP fetcher.
+
+Two implementations behind one async interface:
+
+* ``NativeTransport`` - plain ``http://`` over the C++ ``HttpConn`` (keep-alive pool). Bodies
+  are spliced socket->file and sent file->socket with ``sendfile``; each request runs on a
+  dedicated thread pool with the GIL released, so many transfers proceed in parallel inside
+  one worker process.
+* ``AiohttpTransport`` - everything else (TLS for ``https://`` / ``bucket://`` sources).
+
+A request body is ``bytes`` or a ``FileRange``; a response body is returned in memory or
+written into a ``FileSink``.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
+from urllib.parse import urlsplit
+
+Headers = Sequence[Tuple[str, str]]
+
+
+class HttpError(Exception):
+    def __init__(self, msg: str, status: int = 0, body: bytes = b""):
+        super().__init__(msg)
+        self.status = status
+        self.body = body
+
+
+class TransportError(HttpError):
+    """Connection-level failure (reset, timeout, refused) - always retryable."""
+
+
+@dataclass
+class FileRange:
+    fd: int
+    offset: int
+    length: int
+
+
+@dataclass
+class FileSink:
+    fd: int
+    offset: int = 0
+    max_bytes: int = 1 << 50
+
+
+@dataclass
+class Response:
+    status: int
+    headers: List[Tuple[str, str]]
+    body: bytes = b""
+    written: int = 0
+    reason: str = ""
+
+    def header(self, name: str, default: Optional[str] = None) -> Optional[str]:
+        name = name.lower()
+        for k, v in self.headers:
+            if k == name:
+                return v
+        return default
+
+    @property
+    def ok(self) -> bool:
+        return 200 <= self.status < 300
+
+
+@dataclass
+class Progress:
+    """Byte counter updated while a transfer runs (native: updated from C++ threads)."""
+    native: object = None
+    _bytes: int = 0
+    cancelled: bool = False
+
+    @property
+    def bytes(self) -> int:
+        return self.native.bytes if self.native is not None else self._bytes
+
+    def add(self, n: int) -> None:
+        self._bytes += n
+
+    def cancel(self) -> None:
+        self.cancelled = True
+        if self.native is not None:
+            self.native.cancel()
+
+
+def split_host(url: str) -> Tuple[str, str, int, str]:
+    u = urlsplit(url)
+    scheme = u.scheme or "http"
+    port = u.port or (443 if scheme == "https" else 80)
+    path = u.path or "/"
+    if u.query:
+        path += "?" + u.query
+    return scheme, u.hostname or "", port, path
+
+
+def _build_head(method: str, host_hdr: str, path: str, headers: Headers,
+                body_len: Optional[int]) -> bytes:
+    lines = [f"{method} {path} HTTP/1.1", f"Host: {host_hdr}"]
+    have_len = False
+    for k, v in headers:
+        lk = k.lower()
+        if lk == "host":
+            continue
+        if lk == "content-length":
+            have_len = True
+        lines.append(f"{k}: {v}")
+    if body_len is not None and not have_len and (body_len > 0 or method in ("PUT", "POST")):
+        lines.append(f"Content-Length: {body_len}")
+    lines.append("User-Agent: downloader-amd/0.1")
+    return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
+
+
+class Transport:
+    async def request(self, method: str, url: str, headers: Headers = (),
+                      body: Union[None, bytes, FileRange] = None, sink: Optional[FileSink] = None,
+                      progress: Optional[Progress] = None, expect_body: bool = True) -> Response:
+        raise NotImplementedError
+
+    async def close(self) -> None:
+        pass
+
+
+class NativeTransport(Transport):
+    def __init__(self, max_workers: int = 32, connect_timeout: float = 10.0,
+                 io_timeout: float = 300.0, max_idle_per_host: int = 64):
+        from ..ops import native
+        self._n = native()
+        self._pool: Dict[Tuple[str, int], List[object]] = {}
+        self._lock = threading.Lock()
+        self._exec = ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="xfer")
+        self.connect_timeout = connect_timeout
+        self.io_timeout = io_timeout
+        self.max_idle = max_idle_per_host
+
+    def _acquire(self, host: str, port: int) -> Tuple[object, bool]:
+        with self._lock:
+            idle = self._pool.get((host, port))
+            if idle:
+                return idle.pop(), True
+        try:
+            return self._n.HttpConn(host, port, self.connect_timeout, self.io_timeout), False
+        except RuntimeError as e:
+            raise TransportError(str(e)) from e
+
+    def _release(self, conn) -> None:
+        if not conn.reusable:
+            conn.close()
+            return
+        with self._lock:
+            idle = self._pool.setdefault((conn.host, conn.port), [])
+            if len(idle) < self.max_idle:
+                idle.append(conn)
+                return
+        conn.close()
+
+    def _do(self, method: str, host: str, port: int, host_hdr: str, path: str,
+            headers: Headers, body, sink: Optional[FileSink], nprog,
+            expect_body: bool) -> Response:
+        blen = body.length if isinstance(body, FileRange) else (len(body) if body else 0)
+        head = _build_head(method, host_hdr, path, headers, blen if body is not None else
+                           (0 if method in ("PUT", "POST") else None))
+        for attempt in (0, 1):
+            conn, reused = self._acquire(host, port)
+            try:
+                if isinstance(body, FileRange):
+                    d = conn.request_fd(head, body.fd, body.offset, body.length, nprog)
+                elif sink is not None:
+                    d = conn.get_to_fd(head, sink.fd, sink.offset, sink.max_bytes, nprog)
+                else:
+                    d = conn.request(head, body, expect_body and method != "HEAD")
+            except RuntimeError as e:
+                conn.close()
+                # A pooled keep-alive socket may have been closed by the peer: retry once on
+                # a fresh connection (the whole request is re-sent; bodies are re-readable).
+                if reused and attempt == 0 and not (nprog is not None and nprog.cancelled):
+                    continue
+                raise TransportError(f"{method} {host}:{port}{path}: {e}") from e
+            self._release(conn)
+            return Response(d["status"], list(d["headers"]), d.get("body", b""),
+                            d.get("written", 0), d.get("reason", ""))
+        raise TransportError("unreachable")
+
+    async def request(self, method: str, url: str, headers: Headers = (),
+                      body: Union[None, bytes, FileRange] = None, sink: Optional[FileSink] = None,
+                      progress: Optional[Progress] = None, expect_body: bool = True) -> Response:
+        scheme, host, port, path = split_host(url)
+        if scheme != "http":
+            raise ValueError("NativeTransport handles plain http:// only")
+        host_hdr = host if port == 80 else f"{host}:{port}"
+        nprog = None
+        if progress is not None:
+            if progress.native is None:
+                progress.native = self._n.Progress()
+            nprog = progress.native
+        loop = asyncio.get_running_loop()
+        fut = loop.run_in_executor(self._exec, self._do, method, host, port, host_hdr, path,
+                                   headers, body, sink, nprog, expect_body)
+        try:
+            return await asyncio.shield(fut)
+        except asyncio.CancelledError:
+            if nprog is not None:
+                nprog.cancel()
+            raise
+
+    async def close(self) -> None:
+        with self._lock:
+            conns = [c for v in self._pool.values() for c in v]
+            self._pool.clear()
+        for c in conns:
+            c.close()
+        self._exec.shutdown(wait=False)
+
+
+class AiohttpTransport(Transport):
+    def __init__(self, connect_timeout: float = 10.0, io_timeout: float = 300.0,
+                 limit: int = 64, ssl_verify: bool = True):
+        self._session = None
+        self.connect_timeout = connect_timeout
+        self.io_timeout = io_timeout
+        self.limit = limit
+        self.ssl_verify = ssl_verify
+
+    async def _sess(self):
+        import aiohttp
+        if self._session is None or self._session.closed:
+            timeout = aiohttp.ClientTimeout(total=None, connect=self.connect_timeout,
+                                            sock_read=self.io_timeout)
+            conn = aiohttp.TCPConnector(limit=self.limit, ssl=None if self.ssl_verify else False)
+            self._session = aiohttp.ClientSession(timeout=timeout, connector=conn,
+                                                  auto_decompress=False)
+        return self._session
+
+    async def request(self, method: str, url: str, headers: Headers = (),
+                      body: Union[None, bytes, FileRange] = None, sink: Optional[FileSink] = None,
+                      progress: Optional[Progress] = None, expect_body: bool = True) -> Response:
+        import aiohttp
+        sess = await self._sess()
+        hdrs = [(k, v) for k, v in headers if k.lower() != "host"]
+        data = body
+        if isinstance(body, FileRange):
+            data = _file_iter(body, progress)
+            hdrs.append(("Content-Length", str(body.length)))
+        loop = asyncio.get_running_loop()
+        try:
+            async with sess.request(method, url, headers=hdrs, data=data,
+                                    allow_redirects=True, compress=None) as resp:
+                rh = [(k.lower(), v) for k, v in resp.headers.items()]
+                if sink is not None and 200 <= resp.status < 300:
+                    written = 0
+                    async for chunk in resp.content.iter_chunked(1 << 20):
+                        if progress is not None and progress.cancelled:
+                            raise TransportError("cancelled")
+                        if written + len(chunk) > sink.max_bytes:
+                            raise HttpError("response body exceeds limit", resp.status)
+                        await loop.run_in_executor(None, _pwrite_all, sink.fd, chunk,
+                                                   sink.offset + written)
+                        written += len(chunk)
+                        if progress is not None:
+                            progress.add(len(chunk))
+                    return Response(resp.status, rh, b"", written, resp.reason or "")
+                payload = b"" if method == "HEAD" or not expect_body else await resp.read()
+                return Response(resp.status, rh, payload, 0, resp.reason or "")
+        except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError,
+                asyncio.TimeoutError) as e:
+            raise TransportError(f"{method} {url}: {type(e).__name__}: {e}") from e
+
+    async def close(self) -> None:
+        if self._session is not None:
+            await self._session.close()
+
+
+def _pwrite_all(fd: int, data: bytes, off: int) -> None:
+    mv = memoryview(data)
+    while mv:
+        n = os.pwrite(fd, mv, off)
+        mv = mv[n:]
+        off += n
+
+
+async def _file_iter(fr: FileRange, progress: Optional[Progress]):
+    loop = asyncio.get_running_loop()
+    off, left = fr.offset, fr.length
+    while left > 0:
+        n = min(left, 1 << 20)
+        chunk = await loop.run_in_executor(None, os.pread, fr.fd, n, off)
+        if not chunk:
+            raise HttpError("file shorter than declared body length")
+        off += len(chunk)
+        left -= len(chunk)
+        if progress is not None:
+            progress.add(len(chunk))
+        yield chunk
+
+
+@dataclass
+class TransportSet:
+    """Picks the native transport for plain http and aiohttp for https."""
+    native: Optional[NativeTransport] = None
+    fallback: AiohttpTransport = field(default_factory=AiohttpTransport)
+
+    def for_url(self, url: str) -> Transport:
+        if self.native is not None and url.startswith("http://"):
+            return self.native
+        return self.fallback
+
+    async def request(self, method: str, url: str, **kw) -> Response:
+        return await self.for_url(url).request(method, url, **kw)
+
+    async def close(self) -> None:
+        if self.native is not None:
+            await self.native.close()
+        await self.fallback.close()
+
+
+def make_transports(native: bool = True, max_workers: int = 32, connect_timeout: float = 10.0,
+                    io_timeout: float = 300.0, ssl_verify: bool = True) -> TransportSet:
+    nt = NativeTransport(max_workers, connect_timeout, io_timeout) if native else None
+    return TransportSet(nt, AiohttpTransport(connect_timeout, io_timeout, ssl_verify=ssl_verify))
+
+
+Callback = Callable[[int], None]

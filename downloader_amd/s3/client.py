@@ -1,0 +1,407 @@
+"""Async S3 client (replaces minio-js as wrapped by ``triton-core/minio``).
+
+Operations the reference uses: ``getObject`` (done-marker probe,
+lib/main.js:120), ``bucketExists``/``makeBucket`` (lib/upload.js:29-31), ``fPutObject``
+(lib/upload.js:45), ``putObject`` with a string body (lib/upload.js:55), ``fGetObject`` and the
+``getObjects`` recursive listing (lib/download.js:217-225).
+
+Differences by design:
+  * multipart parts are uploaded concurrently (bounded by ``max_inflight_parts``) straight
+    from the page cache with ``sendfile``; the reference streams one part at a time.
+  * ``fget_object`` can split an object into parallel Range GETs.
+  * transient failures (connection errors, 5xx, SlowDown) are retried with backoff.
+  * an interrupted multipart upload can be resumed: parts whose ETag equals the local MD5
+    of the same range are skipped.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import random
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from urllib.parse import quote
+
+from ..net.http import (FileRange, FileSink, HttpError, Progress, Response, TransportError,
+                        TransportSet, make_transports)
+from . import sigv4
+
+NS = "{http://s3.amazonaws.com/doc/2006-03-01/}"
+MiB = 1 << 20
+MAX_PARTS = 10000
+MIN_PART = 5 * MiB
+
+
+class S3Error(Exception):
+    def __init__(self, code: str, message: str = "", status: int = 0, key: str = "",
+                 bucket: str = ""):
+        super().__init__(f"{code}: {message}" if message else code)
+        self.code = code
+        self.message = message
+        self.status = status
+        self.key = key
+        self.bucket = bucket
+
+    @property
+    def not_found(self) -> bool:
+        return self.code in ("NoSuchKey", "NoSuchBucket", "NotFound") or self.status == 404
+
+    @property
+    def retryable(self) -> bool:
+        return self.status >= 500 or self.code in ("SlowDown", "RequestTimeout",
+                                                   "InternalError", "ServiceUnavailable")
+
+
+@dataclass
+class ObjectInfo:
+    name: str
+    size: int
+    etag: str = ""
+    last_modified: str = ""
+
+
+def _strip(tag: str) -> str:
+    return tag.split("}", 1)[-1]
+
+
+def _find(el: ET.Element, name: str) -> Optional[ET.Element]:
+    for c in el:
+        if _strip(c.tag) == name:
+            return c
+    return None
+
+
+def _text(el: ET.Element, name: str, default: str = "") -> str:
+    c = _find(el, name)
+    return c.text or default if c is not None else default
+
+
+def parse_error(resp: Response, bucket: str = "", key: str = "") -> S3Error:
+    code, msg = "", ""
+    if resp.body:
+        try:
+            root = ET.fromstring(resp.body)
+            code = _text(root, "Code")
+            msg = _text(root, "Message")
+        except ET.ParseError:
+            msg = resp.body[:200].decode("utf-8", "replace")
+    if not code:
+        code = {404: "NotFound", 403: "AccessDenied", 503: "SlowDown", 500: "InternalError",
+                409: "Conflict", 400: "BadRequest"}.get(resp.status, f"HTTP{resp.status}")
+        if resp.status == 404 and key:
+            code = "NoSuchKey"
+    return S3Error(code, msg, resp.status, key, bucket)
+
+
+class S3Client:
+    def __init__(self, endpoint: str, access_key: str, secret_key: str, region: str = "us-east-1",
+                 secure: bool = False, transports: Optional[TransportSet] = None,
+                 part_size: int = 16 * MiB, multipart_threshold: int = 64 * MiB,
+                 max_inflight_parts: int = 8, unsigned_payload: bool = True, retries: int = 3,
+                 native: bool = True, connect_timeout: float = 10.0,
+                 request_timeout: float = 300.0):
+        if "://" in endpoint:
+            secure = endpoint.startswith("https://")
+            endpoint = endpoint.split("://", 1)[1]
+        self.endpoint = endpoint.rstrip("/")
+        self.base = ("https://" if secure else "http://") + self.endpoint
+        self.access_key = access_key
+        self.secret_key = secret_key
+        self.region = region
+        self._own_transports = transports is None
+        self.t = transports or make_transports(native=native, connect_timeout=connect_timeout,
+                                               io_timeout=request_timeout)
+        self.part_size = max(MIN_PART, part_size)
+        self.multipart_threshold = multipart_threshold
+        self.max_inflight_parts = max(1, max_inflight_parts)
+        self.unsigned_payload = unsigned_payload
+        self.retries = retries
+
+    @classmethod
+    def from_config(cls, s3cfg, transports: Optional[TransportSet] = None) -> "S3Client":
+        """``minio.newClient(config)`` equivalent (lib/main.js:41, lib/upload.js:20)."""
+        return cls(s3cfg.endpoint, s3cfg.access_key, s3cfg.secret_key, s3cfg.region,
+                   s3cfg.secure, transports, s3cfg.part_size, s3cfg.multipart_threshold,
+                   s3cfg.max_inflight_parts, s3cfg.unsigned_payload, s3cfg.retries,
+                   s3cfg.native_transport, s3cfg.connect_timeout_s, s3cfg.request_timeout_s)
+
+    async def close(self) -> None:
+        if self._own_transports:
+            await self.t.close()
+
+    # ------------------------------------------------------------------ request core
+    async def _payload_hash(self, body) -> str:
+        if body is None:
+            return sigv4.EMPTY_SHA256
+        if self.unsigned_payload:
+            return sigv4.UNSIGNED
+        from ..ops import native
+        if isinstance(body, FileRange):
+            h = native().Hasher("sha256")
+            await asyncio.get_running_loop().run_in_executor(
+                None, h.update_fd, body.fd, body.offset, body.length)
+            return h.hexdigest()
+        return native().digest("sha256", body).hex()
+
+    async def _request(self, method: str, bucket: str, key: str = "",
+                       query: Sequence[Tuple[str, str]] = (), body=None,
+                       headers: Optional[Dict[str, str]] = None, sink: Optional[FileSink] = None,
+                       progress: Optional[Progress] = None, ok: Sequence[int] = (),
+                       expect_body: bool = True) -> Response:
+        path = "/" + bucket + ("/" + key if key else "")
+        qs = sigv4.canonical_query(query)
+        url = self.base + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
+        phash = await self._payload_hash(body)
+        attempt = 0
+        while True:
+            hdrs = {"host": self.endpoint}
+            if headers:
+                hdrs.update({k.lower(): v for k, v in headers.items()})
+            sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
+                       self.region, phash)
+            try:
+                if sink is not None and attempt > 0:
+                    sink.max_bytes = sink.max_bytes  # body rewritten from the same offset
+                resp = await self.t.request(method, url, headers=list(hdrs.items()), body=body,
+                                            sink=sink, progress=progress,
+                                            expect_body=expect_body)
+            except TransportError as e:
+                err: Exception = e
+                retry = True
+            else:
+                if 200 <= resp.status < 300 or resp.status in ok:
+                    return resp
+                err = parse_error(resp, bucket, key)
+                retry = err.retryable
+            if not retry or attempt >= self.retries:
+                raise err
+            attempt += 1
+            await asyncio.sleep(min(5.0, 0.1 * (2 ** attempt)) * (0.5 + random.random()))
+
+    # ------------------------------------------------------------------ buckets
+    async def bucket_exists(self, bucket: str) -> bool:
+        r = await self._request("HEAD", bucket, ok=(404,), expect_body=False)
+        return r.status != 404
+
+    async def make_bucket(self, bucket: str) -> None:
+        body = b""
+        if self.region and self.region != "us-east-1":
+            body = (f'<CreateBucketConfiguration xmlns="{NS[1:-1]}"><LocationConstraint>'
+                    f"{self.region}</LocationConstraint></CreateBucketConfiguration>").encode()
+        try:
+            await self._request("PUT", bucket, body=body)
+        except S3Error as e:
+            if e.code not in ("BucketAlreadyOwnedByYou", "BucketAlreadyExists"):
+                raise
+
+    async def ensure_bucket(self, bucket: str) -> None:
+        if not await self.bucket_exists(bucket):
+            await self.make_bucket(bucket)
+
+    # ------------------------------------------------------------------ objects
+    async def get_object(self, bucket: str, key: str) -> bytes:
+        r = await self._request("GET", bucket, key)
+        return r.body
+
+    async def head_object(self, bucket: str, key: str) -> ObjectInfo:
+        r = await self._request("HEAD", bucket, key, ok=(404,), expect_body=False)
+        if r.status == 404:
+            raise S3Error("NoSuchKey", "", 404, key, bucket)
+        return ObjectInfo(key, int(r.header("content-length", "0") or 0),
+                          (r.header("etag") or "").strip('"'), r.header("last-modified") or "")
+
+    async def object_exists(self, bucket: str, key: str) -> bool:
+        try:
+            await self.head_object(bucket, key)
+            return True
+        except S3Error as e:
+            if e.not_found:
+                return False
+            raise
+
+    async def put_object(self, bucket: str, key: str, data, content_type: str = "") -> str:
+        if isinstance(data, str):
+            data = data.encode("utf-8")
+        hdrs = {"content-type": content_type} if content_type else None
+        r = await self._request("PUT", bucket, key, body=bytes(data), headers=hdrs)
+        return (r.header("etag") or "").strip('"')
+
+    async def delete_object(self, bucket: str, key: str) -> None:
+        await self._request("DELETE", bucket, key, ok=(404,))
+
+    async def fput_object(self, bucket: str, key: str, path: str,
+                          progress: Optional[Progress] = None, resume: bool = False,
+                          concurrency: Optional[int] = None) -> str:
+        size = os.path.getsize(path)
+        fd = os.open(path, os.O_RDONLY | getattr(os, "O_CLOEXEC", 0))
+        try:
+            if size <= self.multipart_threshold:
+                r = await self._request("PUT", bucket, key, body=FileRange(fd, 0, size),
+                                        progress=progress)
+                return (r.header("etag") or "").strip('"')
+            return await self._multipart(bucket, key, fd, size, path, progress, resume,
+                                         concurrency or self.max_inflight_parts)
+        finally:
+            os.close(fd)
+
+    def plan_parts(self, size: int) -> List[Tuple[int, int, int]]:
+        ps = self.part_size
+        while (size + ps - 1) // ps > MAX_PARTS:
+            ps *= 2
+        return [(i + 1, off, min(ps, size - off)) for i, off in enumerate(range(0, size, ps))]
+
+    async def _multipart(self, bucket: str, key: str, fd: int, size: int, path: str,
+                         progress: Optional[Progress], resume: bool, concurrency: int) -> str:
+        parts = self.plan_parts(size)
+        upload_id = None
+        done: Dict[int, str] = {}
+        if resume:
+            upload_id = await self.find_upload(bucket, key)
+            if upload_id:
+                done = await self._reusable_parts(bucket, key, upload_id, path, parts)
+        if not upload_id:
+            upload_id = await self.create_multipart_upload(bucket, key)
+        sem = asyncio.Semaphore(concurrency)
+        etags: Dict[int, str] = dict(done)
+
+        async def one(num: int, off: int, ln: int) -> None:
+            async with sem:
+                etags[num] = await self.upload_part(bucket, key, upload_id, num,
+                                                    FileRange(fd, off, ln), progress)
+
+        try:
+            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts if n not in done))
+            return await self.complete_multipart_upload(
+                bucket, key, upload_id, [(n, etags[n]) for n, _, _ in parts])
+        except BaseException:
+            if not resume:
+                try:
+                    await asyncio.shield(self.abort_multipart_upload(bucket, key, upload_id))
+                except Exception:
+                    pass
+            raise
+
+    async def _reusable_parts(self, bucket: str, key: str, upload_id: str, path: str,
+                              parts: List[Tuple[int, int, int]]) -> Dict[int, str]:
+        from ..ops import hashing
+        remote = {n: (e, s) for n, e, s in await self.list_parts(bucket, key, upload_id)}
+        cand = [(n, o, ln) for n, o, ln in parts if n in remote and remote[n][1] == ln]
+        if not cand:
+            return {}
+        loop = asyncio.get_running_loop()
+        md5s = await loop.run_in_executor(None, hashing.hash_file_ranges, path,
+                                          [(o, ln) for _, o, ln in cand], "md5")
+        return {n: remote[n][0] for (n, _, _), d in zip(cand, md5s) if d.hex() == remote[n][0]}
+
+    async def create_multipart_upload(self, bucket: str, key: str) -> str:
+        r = await self._request("POST", bucket, key, query=[("uploads", "")])
+        return _text(ET.fromstring(r.body), "UploadId")
+
+    async def upload_part(self, bucket: str, key: str, upload_id: str, num: int, body,
+                          progress: Optional[Progress] = None) -> str:
+        r = await self._request("PUT", bucket, key,
+                                query=[("partNumber", str(num)), ("uploadId", upload_id)],
+                                body=body, progress=progress)
+        return (r.header("etag") or "").strip('"')
+
+    async def complete_multipart_upload(self, bucket: str, key: str, upload_id: str,
+                                        parts: Sequence[Tuple[int, str]]) -> str:
+        xml = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>\"{e}\"</ETag></Part>"
+                      for n, e in parts)
+        body = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
+        r = await self._request("POST", bucket, key, query=[("uploadId", upload_id)], body=body)
+        root = ET.fromstring(r.body)
+        if _strip(root.tag) == "Error":
+            raise S3Error(_text(root, "Code"), _text(root, "Message"), 200, key, bucket)
+        return _text(root, "ETag").strip('"')
+
+    async def abort_multipart_upload(self, bucket: str, key: str, upload_id: str) -> None:
+        await self._request("DELETE", bucket, key, query=[("uploadId", upload_id)], ok=(404,))
+
+    async def list_parts(self, bucket: str, key: str, upload_id: str) -> List[Tuple[int, str, int]]:
+        out: List[Tuple[int, str, int]] = []
+        marker = ""
+        while True:
+            q = [("uploadId", upload_id)] + ([("part-number-marker", marker)] if marker else [])
+            r = await self._request("GET", bucket, key, query=q)
+            root = ET.fromstring(r.body)
+            for p in root:
+                if _strip(p.tag) == "Part":
+                    out.append((int(_text(p, "PartNumber")), _text(p, "ETag").strip('"'),
+                                int(_text(p, "Size", "0"))))
+            if _text(root, "IsTruncated") != "true":
+                return out
+            marker = _text(root, "NextPartNumberMarker")
+
+    async def find_upload(self, bucket: str, key: str) -> Optional[str]:
+        r = await self._request("GET", bucket, query=[("uploads", ""), ("prefix", key)])
+        root = ET.fromstring(r.body)
+        best = None
+        for u in root:
+            if _strip(u.tag) == "Upload" and _text(u, "Key") == key:
+                best = _text(u, "UploadId")
+        return best
+
+    async def fget_object(self, bucket: str, key: str, path: str, streams: int = 1,
+                          min_split: int = 32 * MiB, progress: Optional[Progress] = None) -> int:
+        """Download to ``path`` (via ``path + '.part'`` then rename, like minio-js)."""
+        tmp = path + ".part"
+        os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+        fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | getattr(os, "O_CLOEXEC", 0),
+                     0o644)
+        try:
+            size = -1
+            if streams > 1:
+                size = (await self.head_object(bucket, key)).size
+            if streams > 1 and size >= 2 * min_split:
+                os.ftruncate(fd, size)
+                n = min(streams, max(1, size // min_split))
+                step = (size + n - 1) // n
+                rngs = [(o, min(step, size - o)) for o in range(0, size, step)]
+
+                async def one(off: int, ln: int) -> None:
+                    await self._request("GET", bucket, key,
+                                        headers={"range": f"bytes={off}-{off + ln - 1}"},
+                                        sink=FileSink(fd, off, ln), progress=progress)
+                await asyncio.gather(*(one(o, ln) for o, ln in rngs))
+                written = size
+            else:
+                r = await self._request("GET", bucket, key, sink=FileSink(fd, 0),
+                                        progress=progress)
+                written = r.written
+        finally:
+            os.close(fd)
+        os.replace(tmp, path)
+        return written
+
+    async def list_objects(self, bucket: str, prefix: str = "", recursive: bool = True,
+                           max_keys: int = 1000) -> List[ObjectInfo]:
+        """ListObjectsV2 with pagination (``getObjects`` in triton-core/minio)."""
+        out: List[ObjectInfo] = []
+        token = ""
+        while True:
+            q = [("list-type", "2"), ("prefix", prefix), ("max-keys", str(max_keys))]
+            if not recursive:
+                q.append(("delimiter", "/"))
+            if token:
+                q.append(("continuation-token", token))
+            r = await self._request("GET", bucket, query=q)
+            root = ET.fromstring(r.body)
+            for c in root:
+                t = _strip(c.tag)
+                if t == "Contents":
+                    out.append(ObjectInfo(_text(c, "Key"), int(_text(c, "Size", "0")),
+                                          _text(c, "ETag").strip('"'), _text(c, "LastModified")))
+                elif t == "CommonPrefixes":
+                    out.append(ObjectInfo(_text(c, "Prefix"), 0))
+            if _text(root, "IsTruncated") != "true":
+                return out
+            token = _text(root, "NextContinuationToken")
+
+
+def object_url_path(bucket: str, key: str) -> str:
+    return "/" + quote(bucket) + "/" + quote(key, safe="/-_.~")
+
+
+ProgressCb = Callable[[int], None]

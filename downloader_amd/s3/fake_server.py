@@ -1,0 +1,370 @@
+"""In-process S3-compatible server for tests (MinIO stand-in; no MinIO binary in the image).
+
+Implements the subset the stager and the ``bucket://`` source use: bucket HEAD/PUT/DELETE,
+ListObjectsV2 (prefix, delimiter, continuation), object PUT/GET (Range)/HEAD/DELETE, multipart
+(initiate, upload part, complete, abort, list parts, list uploads). Requests are SigV4
+verified (``x-amz-content-sha256`` too unless UNSIGNED-PAYLOAD). ETags are MD5 / multipart
+``md5(concat(part md5s))-N`` like S3.
+
+Fault injection: ``faults.add(FaultRule(...))`` makes matching requests fail
+with a status/code, stall, or drop the connection mid-response.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import secrets
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+from urllib.parse import parse_qsl, unquote
+from xml.sax.saxutils import escape
+
+from aiohttp import web
+
+from . import sigv4
+
+XMLNS = "http://s3.amazonaws.com/doc/2006-03-01/"
+
+
+@dataclass
+class StoredObject:
+    data: bytes
+    etag: str
+    mtime: float = field(default_factory=time.time)
+    content_type: str = "application/octet-stream"
+
+
+@dataclass
+class Upload:
+    key: str
+    parts: Dict[int, Tuple[bytes, str]] = field(default_factory=dict)
+    initiated: float = field(default_factory=time.time)
+
+
+@dataclass
+class FaultRule:
+    method: str = "*"
+    path_contains: str = ""
+    query_contains: str = ""
+    times: int = 1
+    status: int = 503
+    code: str = "SlowDown"
+    delay_s: float = 0.0
+    drop_connection: bool = False
+
+    def matches(self, method: str, path: str, query: str) -> bool:
+        return ((self.method == "*" or self.method == method)
+                and self.path_contains in path and self.query_contains in query)
+
+
+class Faults:
+    def __init__(self) -> None:
+        self.rules: List[FaultRule] = []
+        self.fired: List[Tuple[str, str]] = []
+        self._lock = threading.Lock()
+
+    def add(self, rule: FaultRule) -> None:
+        with self._lock:
+            self.rules.append(rule)
+
+    def take(self, method: str, path: str, query: str) -> Optional[FaultRule]:
+        with self._lock:
+            for r in self.rules:
+                if r.times > 0 and r.matches(method, path, query):
+                    r.times -= 1
+                    self.fired.append((method, path))
+                    return r
+        return None
+
+
+def _xml(body: str) -> web.Response:
+    return web.Response(body=('<?xml version="1.0" encoding="UTF-8"?>' + body).encode(),
+                        content_type="application/xml")
+
+
+def _err(status: int, code: str, msg: str = "", resource: str = "") -> web.Response:
+    return web.Response(status=status, content_type="application/xml", body=(
+        f'<?xml version="1.0" encoding="UTF-8"?><Error><Code>{code}</Code>'
+        f"<Message>{escape(msg or code)}</Message><Resource>{escape(resource)}</Resource>"
+        f"<RequestId>{secrets.token_hex(8)}</RequestId></Error>").encode())
+
+
+class FakeS3:
+    def __init__(self, access_key: str = "minioadmin", secret_key: str = "minioadmin",
+                 verify_signatures: bool = True, host: str = "127.0.0.1", port: int = 0):
+        self.creds = {access_key: secret_key}
+        self.verify_signatures = verify_signatures
+        self.buckets: Dict[str, Dict[str, StoredObject]] = {}
+        self.uploads: Dict[str, Dict[str, Upload]] = {}
+        self.faults = Faults()
+        self.requests: List[Tuple[str, str]] = []
+        self.host = host
+        self.port = port
+        self._runner: Optional[web.AppRunner] = None
+        self._thread: Optional[threading.Thread] = None
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self.hooks: List[Callable[[str, str], None]] = []
+
+    # ---------------------------------------------------------------- lifecycle
+    @property
+    def endpoint(self) -> str:
+        return f"{self.host}:{self.port}"
+
+    async def start(self) -> str:
+        app = web.Application(client_max_size=1 << 40)
+        app.router.add_route("*", "/{tail:.*}", self._handle)
+        self._runner = web.AppRunner(app, access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+        return self.endpoint
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+    def start_in_thread(self) -> str:
+        ready = threading.Event()
+
+        def run() -> None:
+            self._loop = asyncio.new_event_loop()
+            asyncio.set_event_loop(self._loop)
+            self._loop.run_until_complete(self.start())
+            ready.set()
+            self._loop.run_forever()
+            self._loop.run_until_complete(self.stop())
+            self._loop.close()
+
+        self._thread = threading.Thread(target=run, daemon=True, name="fake-s3")
+        self._thread.start()
+        ready.wait(30)
+        return self.endpoint
+
+    def stop_thread(self) -> None:
+        if self._loop is not None:
+            self._loop.call_soon_threadsafe(self._loop.stop)
+        if self._thread is not None:
+            self._thread.join(10)
+
+    # ---------------------------------------------------------------- helpers for tests
+    def objects(self, bucket: str) -> Dict[str, StoredObject]:
+        return self.buckets.get(bucket, {})
+
+    def get(self, bucket: str, key: str) -> Optional[bytes]:
+        o = self.buckets.get(bucket, {}).get(key)
+        return None if o is None else o.data
+
+    def put(self, bucket: str, key: str, data: bytes) -> None:
+        self.buckets.setdefault(bucket, {})[key] = StoredObject(data, hashlib.md5(data).hexdigest())
+
+    # ---------------------------------------------------------------- dispatch
+    async def _handle(self, req: web.Request) -> web.StreamResponse:
+        raw_path, _, raw_query = req.raw_path.partition("?")
+        path = unquote(raw_path)
+        query = parse_qsl(raw_query, keep_blank_values=True)
+        self.requests.append((req.method, path))
+        for h in self.hooks:
+            h(req.method, path)
+        rule = self.faults.take(req.method, path, raw_query)
+        if rule is not None:
+            if rule.delay_s:
+                await asyncio.sleep(rule.delay_s)
+            if rule.drop_connection:
+                if req.transport is not None:
+                    req.transport.close()
+                raise web.HTTPInternalServerError()
+            if rule.status:
+                return _err(rule.status, rule.code, "injected fault", path)
+        body = await req.read() if req.can_read_body else b""
+        if self.verify_signatures:
+            hdrs = {k.lower(): v for k, v in req.headers.items()}
+            ok, reason = sigv4.verify(req.method, path, query, hdrs, self.creds)
+            if not ok:
+                return _err(403, reason, "signature check failed", path)
+            ph = hdrs.get("x-amz-content-sha256", "")
+            if ph != sigv4.UNSIGNED and ph != hashlib.sha256(body).hexdigest():
+                return _err(400, "XAmzContentSHA256Mismatch", "", path)
+        parts = path.lstrip("/").split("/", 1)
+        bucket = parts[0]
+        key = parts[1] if len(parts) > 1 else ""
+        q = dict(query)
+        if not bucket:
+            return self._list_buckets()
+        if not key:
+            return self._bucket_op(req.method, bucket, q)
+        return self._object_op(req, bucket, key, q, body)
+
+    def _list_buckets(self) -> web.Response:
+        b = "".join(f"<Bucket><Name>{escape(n)}</Name></Bucket>" for n in sorted(self.buckets))
+        return _xml(f'<ListAllMyBucketsResult xmlns="{XMLNS}"><Buckets>{b}</Buckets>'
+                    "</ListAllMyBucketsResult>")
+
+    def _bucket_op(self, method: str, bucket: str, q: Dict[str, str]) -> web.Response:
+        exists = bucket in self.buckets
+        if method == "HEAD":
+            return web.Response(status=200 if exists else 404)
+        if method == "PUT":
+            if exists:
+                return _err(409, "BucketAlreadyOwnedByYou", "", bucket)
+            self.buckets[bucket] = {}
+            self.uploads[bucket] = {}
+            return web.Response(status=200)
+        if not exists:
+            return _err(404, "NoSuchBucket", "", bucket)
+        if method == "DELETE":
+            if self.buckets[bucket]:
+                return _err(409, "BucketNotEmpty", "", bucket)
+            del self.buckets[bucket]
+            return web.Response(status=204)
+        if method == "GET" and "uploads" in q:
+            prefix = q.get("prefix", "")
+            ups = "".join(
+                f"<Upload><Key>{escape(u.key)}</Key><UploadId>{uid}</UploadId></Upload>"
+                for uid, u in self.uploads.get(bucket, {}).items() if u.key.startswith(prefix))
+            return _xml(f'<ListMultipartUploadsResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
+                        f"{ups}</ListMultipartUploadsResult>")
+        if method == "GET":
+            return self._list_v2(bucket, q)
+        return _err(405, "MethodNotAllowed", "", bucket)
+
+    def _list_v2(self, bucket: str, q: Dict[str, str]) -> web.Response:
+        prefix = q.get("prefix", "")
+        delim = q.get("delimiter", "")
+        max_keys = int(q.get("max-keys", "1000"))
+        start = q.get("continuation-token", "") or q.get("start-after", "")
+        keys = sorted(k for k in self.buckets[bucket] if k.startswith(prefix) and k > start)
+        contents, prefixes = [], []
+        seen = set()
+        last = ""
+        truncated = False
+        for k in keys:
+            if len(contents) + len(prefixes) >= max_keys:
+                truncated = True
+                break
+            if delim:
+                rest = k[len(prefix):]
+                if delim in rest:
+                    cp = prefix + rest.split(delim, 1)[0] + delim
+                    if cp not in seen:
+                        seen.add(cp)
+                        prefixes.append(cp)
+                    last = k
+                    continue
+            o = self.buckets[bucket][k]
+            contents.append(f"<Contents><Key>{escape(k)}</Key><Size>{len(o.data)}</Size>"
+                            f"<ETag>&quot;{o.etag}&quot;</ETag><LastModified>"
+                            f"{time.strftime('%Y-%m-%dT%H:%M:%S.000Z', time.gmtime(o.mtime))}"
+                            f"</LastModified><StorageClass>STANDARD</StorageClass></Contents>")
+            last = k
+        cps = "".join(f"<CommonPrefixes><Prefix>{escape(p)}</Prefix></CommonPrefixes>"
+                      for p in prefixes)
+        nxt = f"<NextContinuationToken>{escape(last)}</NextContinuationToken>" if truncated else ""
+        return _xml(f'<ListBucketResult xmlns="{XMLNS}"><Name>{bucket}</Name>'
+                    f"<Prefix>{escape(prefix)}</Prefix><KeyCount>{len(contents)}</KeyCount>"
+                    f"<MaxKeys>{max_keys}</MaxKeys><IsTruncated>{str(truncated).lower()}"
+                    f"</IsTruncated>{nxt}{''.join(contents)}{cps}</ListBucketResult>")
+
+    def _object_op(self, req: web.Request, bucket: str, key: str, q: Dict[str, str],
+                   body: bytes) -> web.Response:
+        if bucket not in self.buckets:
+            return _err(404, "NoSuchBucket", "", bucket)
+        objs = self.buckets[bucket]
+        ups = self.uploads.setdefault(bucket, {})
+        m = req.method
+        if m == "POST" and "uploads" in q:
+            uid = secrets.token_hex(16)
+            ups[uid] = Upload(key)
+            return _xml(f'<InitiateMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
+                        f"<Key>{escape(key)}</Key><UploadId>{uid}</UploadId>"
+                        "</InitiateMultipartUploadResult>")
+        if "uploadId" in q:
+            up = ups.get(q["uploadId"])
+            if up is None or up.key != key:
+                return _err(404, "NoSuchUpload", "", key)
+            if m == "PUT":
+                num = int(q.get("partNumber", "0"))
+                if not 1 <= num <= 10000:
+                    return _err(400, "InvalidArgument", "bad part number", key)
+                etag = hashlib.md5(body).hexdigest()
+                up.parts[num] = (body, etag)
+                return web.Response(status=200, headers={"ETag": f'"{etag}"'})
+            if m == "GET":
+                ps = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>&quot;{e}&quot;</ETag>"
+                             f"<Size>{len(d)}</Size></Part>"
+                             for n, (d, e) in sorted(up.parts.items()))
+                return _xml(f'<ListPartsResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
+                            f"<Key>{escape(key)}</Key><UploadId>{q['uploadId']}</UploadId>"
+                            f"<IsTruncated>false</IsTruncated>{ps}</ListPartsResult>")
+            if m == "DELETE":
+                del ups[q["uploadId"]]
+                return web.Response(status=204)
+            if m == "POST":
+                import xml.etree.ElementTree as ET
+                try:
+                    root = ET.fromstring(body)
+                except ET.ParseError:
+                    return _err(400, "MalformedXML", "", key)
+                want = []
+                for p in root:
+                    n = e = None
+                    for c in p:
+                        t = c.tag.split("}")[-1]
+                        if t == "PartNumber":
+                            n = int(c.text or 0)
+                        elif t == "ETag":
+                            e = (c.text or "").strip('"')
+                    want.append((n, e))
+                if [n for n, _ in want] != sorted(n for n, _ in want):
+                    return _err(400, "InvalidPartOrder", "", key)
+                datas, md5s = [], b""
+                for i, (n, e) in enumerate(want):
+                    got = up.parts.get(n)
+                    if got is None or got[1] != e:
+                        return _err(400, "InvalidPart", f"part {n}", key)
+                    if i < len(want) - 1 and len(got[0]) < 5 * 1024 * 1024:
+                        return _err(400, "EntityTooSmall", f"part {n}", key)
+                    datas.append(got[0])
+                    md5s += bytes.fromhex(got[1])
+                data = b"".join(datas)
+                etag = f"{hashlib.md5(md5s).hexdigest()}-{len(want)}"
+                objs[key] = StoredObject(data, etag)
+                del ups[q["uploadId"]]
+                return _xml(f'<CompleteMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}'
+                            f"</Bucket><Key>{escape(key)}</Key><ETag>&quot;{etag}&quot;</ETag>"
+                            "</CompleteMultipartUploadResult>")
+        if m == "PUT":
+            etag = hashlib.md5(body).hexdigest()
+            objs[key] = StoredObject(body, etag, content_type=req.headers.get(
+                "Content-Type", "application/octet-stream"))
+            return web.Response(status=200, headers={"ETag": f'"{etag}"'})
+        o = objs.get(key)
+        if m == "DELETE":
+            objs.pop(key, None)
+            return web.Response(status=204)
+        if o is None:
+            if m == "HEAD":
+                return web.Response(status=404)
+            return _err(404, "NoSuchKey", "The specified key does not exist.", key)
+        hdrs = {"ETag": f'"{o.etag}"', "Last-Modified": time.strftime(
+            "%a, %d %b %Y %H:%M:%S GMT", time.gmtime(o.mtime)), "Accept-Ranges": "bytes"}
+        if m == "HEAD":
+            hdrs["Content-Length"] = str(len(o.data))
+            return web.Response(status=200, headers=hdrs)
+        if m == "GET":
+            rng = req.headers.get("Range")
+            if rng and rng.startswith("bytes="):
+                a, _, b = rng[6:].partition("-")
+                start = int(a) if a else max(0, len(o.data) - int(b))
+                end = int(b) if (b and a) else len(o.data) - 1
+                end = min(end, len(o.data) - 1)
+                if start > end:
+                    return _err(416, "InvalidRange", "", key)
+                hdrs["Content-Range"] = f"bytes {start}-{end}/{len(o.data)}"
+                return web.Response(status=206, body=o.data[start:end + 1], headers=hdrs)
+            return web.Response(status=200, body=o.data, headers=hdrs,
+                                content_type=o.content_type)
+        return _err(405, "MethodNotAllowed", "", key)

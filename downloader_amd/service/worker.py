@@ -1,0 +1,286 @@
+"""Service kernel / job orchestrator (reference lib/main.js:40-205).
+
+Per delivery of ``v1.download`` (``processor``, lib/main.js:62-170):
+  1. decode ``api.Download`` (:63), emit status DOWNLOADING=2 (:68), register the job (:70-73)
+  2. idempotence guard: a staged ``<id>/original/done`` marker skips straight to 5 (:117-126)
+  3. run the stages in order, each seeing ``lastStage`` (:127-140)
+  4. failure policy (:141-151): ``ERRDLSTALL`` -> ack and drop; anything else -> status
+     ERRORED=6 and retry (reference: ``nack``)
+  5. publish ``api.Convert{createdAt, media}`` to ``v1.convert`` (:157-164), then ack (:168)
+
+Fixes: only NoSuchKey/404 means "not staged" (#5); a failed convert publish
+is nacked for redelivery instead of being left unacked (#8); the active-job registry really
+removes finished jobs (#2), so ``/health`` and shutdown behave.
+
+Retry policy (``broker.max_retries``, reference AMQP arg ``2`` INFERRED): a failed job is
+re-published with ``x-attempt`` + 1 after exponential backoff, then dead-lettered to
+``broker.dead_letter_queue`` when the budget is spent. ``mode: reference`` uses plain
+``nack(requeue)``.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+from ..broker.base import Broker, Delivery, make_broker
+from ..models import api, keys
+from ..net.http import TransportSet, make_transports
+from ..s3.client import S3Client, S3Error
+from ..stages import build_stages
+from ..stages.base import EventEmitter, Job, Services, Stage
+from ..utils.config import Config
+from ..utils.log import Logger, get_logger
+from ..utils.metrics import Metrics
+from ..utils.trace import Tracer, init_tracer
+from .telemetry import Telemetry
+
+
+@dataclass
+class ActiveJob:
+    job_id: str
+    creator_id: str
+    started: float = field(default_factory=time.time)
+    stage: str = ""
+
+
+@dataclass
+class JobResult:
+    job_id: str
+    outcome: str            # staged | skipped | stalled | retried | dead | failed | publish_failed
+    seconds: float
+    bytes: int = 0
+    error: str = ""
+
+
+class Worker:
+    def __init__(self, cfg: Config, broker: Optional[Broker] = None,
+                 s3: Optional[S3Client] = None, transports: Optional[TransportSet] = None,
+                 telemetry: Optional[Telemetry] = None, metrics: Optional[Metrics] = None,
+                 tracer: Optional[Tracer] = None, logger: Optional[Logger] = None):
+        self.cfg = cfg
+        self.log = logger or get_logger("main")
+        self.metrics = metrics or Metrics()
+        self.broker = broker or make_broker(cfg, self.metrics)
+        self.transports = transports or make_transports(
+            native=cfg.s3.native_transport or cfg.download.http_native,
+            max_workers=max(16, cfg.concurrency * (cfg.s3.max_inflight_parts + cfg.download.http_streams) * 2),
+            connect_timeout=cfg.s3.connect_timeout_s, io_timeout=cfg.s3.request_timeout_s)
+        self.s3 = s3 or S3Client.from_config(cfg.s3, self.transports)
+        self.telemetry = telemetry or Telemetry.from_config(cfg, self.broker, self.log)
+        self.tracer = tracer or init_tracer("downloader", cfg.trace.enabled, cfg.trace.path)
+        self.services = Services(cfg, self.telemetry, self.s3, self.transports, self.metrics,
+                                 self.tracer, self.log)
+        self.stages: List[Tuple[str, Stage]] = []
+        self.active: Dict[int, ActiveJob] = {}
+        self.results: List[JobResult] = []
+        self._consumer: Optional[str] = None
+        self._inflight: set = set()
+        self._stopping = False
+        self._health = None
+        self._seq = 0
+        self.on_result = None  # optional callback(JobResult)
+
+    # ------------------------------------------------------------------ lifecycle
+    async def init(self) -> None:
+        """Connect and build stages without consuming (used by tests and the bench)."""
+        await self.broker.connect()
+        await self.telemetry.connect()
+        for q in (self.cfg.broker.download_queue, self.cfg.broker.convert_queue,
+                  self.cfg.broker.dead_letter_queue):
+            await self.broker.declare(q)
+        if not self.stages:
+            self.stages = await build_stages(self.cfg.stages, self.cfg, self.services)
+
+    async def start(self, health: bool = True) -> None:
+        await self.init()
+        self._consumer = await self.broker.consume(self.cfg.broker.download_queue,
+                                                   self._on_delivery, self.cfg.broker.prefetch)
+        if health and self.cfg.health.enabled:
+            from .health import HealthServer
+            self._health = HealthServer(self, self.cfg.health)
+            await self._health.start()
+        if self.cfg.metrics.enabled and self.cfg.metrics.port:
+            self.metrics.expose(self.cfg.metrics.port)
+        self.log.info("successfully connected to queue and started server")
+
+    async def stop(self, drain_timeout: float = 30.0) -> int:
+        """Stop consuming, let in-flight jobs finish (bounded), close everything.
+        Returns the process exit code the reference's termHandler would use (lib/main.js:197-204):
+        0 when nothing was in flight, 1 otherwise."""
+        self._stopping = True
+        had_active = bool(self.active)
+        if self._consumer is not None:
+            try:
+                await self.broker.cancel(self._consumer)
+            except Exception:
+                pass
+            self._consumer = None
+        if self._inflight:
+            await asyncio.wait(list(self._inflight), timeout=drain_timeout)
+        if self._health is not None:
+            await self._health.stop()
+        for _, st in self.stages:
+            await st.close()
+        try:
+            await self.broker.close()
+        except Exception:
+            pass
+        await self.s3.close()
+        await self.transports.close()
+        return 1 if had_active and self.active else 0
+
+    # ------------------------------------------------------------------ message path
+    async def _on_delivery(self, d: Delivery) -> None:
+        t = asyncio.current_task()
+        self._inflight.add(t)
+        try:
+            await self.process(d)
+        finally:
+            self._inflight.discard(t)
+
+    async def process(self, d: Delivery) -> JobResult:
+        t0 = time.perf_counter()
+        try:
+            msg = api.decode(api.Download, d.body)
+        except Exception as e:
+            self.log.error("undecodable message dropped to dead-letter", err=str(e))
+            await self._dead_letter(d, f"decode: {e}")
+            return self._finish(JobResult("", "dead", time.perf_counter() - t0, error=str(e)))
+        media = msg.media
+        job_id, creator = media.id, media.creatorId
+        attempt = int(d.headers.get("x-attempt", 0) or 0)
+        child = self.log.child(jobId=job_id, fileId=creator)
+        self._seq += 1
+        slot = self._seq
+        self.active[slot] = ActiveJob(job_id, creator)
+        self.metrics.inflight.inc()
+        await self.telemetry.emit_status(job_id, api.STATUS_DOWNLOADING)
+        emitter = EventEmitter()
+        job = Job(msg=msg, media=media, logger=child, emitter=emitter, attempt=attempt,
+                  headers=dict(d.headers))
+        outcome, err = "staged", ""
+        try:
+            with self.tracer.span("job", traceparent=d.headers.get("traceparent"),
+                                  job_id=job_id, attempt=attempt) as span:
+                staged = await self._already_staged(job_id, child)
+                if not staged:
+                    child.info("starting main processor after successful stage init")
+                    try:
+                        await self._run_stages(job, slot)
+                    except Exception as e:
+                        code = getattr(e, "code", None)
+                        child.error("failed to invoke stage:", str(e))
+                        if code == "ERRDLSTALL":
+                            self.metrics.stalls.inc()
+                            if self.cfg.download.emit_errored_on_stall:
+                                await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
+                            await d.ack()
+                            return self._finish(JobResult(job_id, "stalled",
+                                                          time.perf_counter() - t0, error=str(e)))
+                        await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
+                        outcome = await self._retry(d, attempt, str(e))
+                        return self._finish(JobResult(job_id, outcome, time.perf_counter() - t0,
+                                                      error=str(e)))
+                    child.info("creating convert job")
+                else:
+                    outcome = "skipped"
+                    child.warn("skipping download due to files existing in triton-staging")
+                try:
+                    conv = api.make_convert(media)
+                    hdrs = {"traceparent": span.traceparent()}
+                    await self.broker.publish(self.cfg.broker.convert_queue, api.encode(conv), hdrs)
+                    self.metrics.messages.labels(self.cfg.broker.convert_queue, "publish").inc()
+                except Exception as e:
+                    child.error("failed to create job:", str(e))
+                    await d.nack(requeue=True)
+                    return self._finish(JobResult(job_id, "publish_failed",
+                                                  time.perf_counter() - t0, error=str(e)))
+                await d.ack()
+                return self._finish(JobResult(job_id, outcome, time.perf_counter() - t0,
+                                              job.stats.get("uploaded_bytes", 0)))
+        except Exception as e:  # infrastructure error outside the stage loop (e.g. S3 down)
+            err = str(e)
+            child.error("job failed outside stages", err=err)
+            await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
+            outcome = await self._retry(d, attempt, err)
+            return self._finish(JobResult(job_id, outcome, time.perf_counter() - t0, error=err))
+        finally:
+            self.active.pop(slot, None)
+            self.metrics.inflight.dec()
+
+    def _finish(self, r: JobResult) -> JobResult:
+        self.results.append(r)
+        self.metrics.jobs.labels(r.outcome).inc()
+        self.metrics.job_duration.labels(r.outcome).observe(r.seconds)
+        if self.on_result is not None:
+            self.on_result(r)
+        return r
+
+    async def _already_staged(self, job_id: str, log: Logger) -> bool:
+        log.info("checking s3 bucket to see if files already exist for id", job_id)
+        try:
+            await self.s3.get_object(self.cfg.s3.bucket, keys.done_key(job_id))
+            return True
+        except S3Error as e:
+            if e.not_found:
+                log.info("failed to find done file in staging")
+                return False
+            raise
+
+    async def _run_stages(self, job: Job, slot: int) -> None:
+        last: Any = {}
+        for name, fn in self.stages:
+            job.logger.info(f"invoking stage '{name}'")
+            self.active[slot].stage = name
+            job.last_stage = last
+            with self.tracer.span(f"stage.{name}"), self.metrics.time_stage(name):
+                last = await fn(job)
+            job.emitter.emit("progress", 0)
+
+    async def _retry(self, d: Delivery, attempt: int, err: str) -> str:
+        b = self.cfg.broker
+        if self.cfg.mode == "reference":
+            await d.nack(requeue=True)
+            return "failed"
+        if attempt >= b.max_retries:
+            await self._dead_letter(d, err)
+            return "dead"
+        delay = min(b.retry_backoff_max_s, b.retry_backoff_s * (2 ** attempt))
+        await asyncio.sleep(delay)
+        hdrs = dict(d.headers)
+        hdrs["x-attempt"] = attempt + 1
+        hdrs["x-last-error"] = err[:512]
+        try:
+            await self.broker.publish(b.download_queue, d.body, hdrs)
+        except Exception:
+            await d.nack(requeue=True)
+            return "failed"
+        self.metrics.retries.inc()
+        await d.ack()
+        return "retried"
+
+    async def _dead_letter(self, d: Delivery, err: str) -> None:
+        hdrs = dict(d.headers)
+        hdrs["x-last-error"] = err[:512]
+        try:
+            await self.broker.publish(self.cfg.broker.dead_letter_queue, d.body, hdrs)
+            await d.ack()
+        except Exception:
+            await d.nack(requeue=True)
+
+    # ------------------------------------------------------------------ direct API
+    async def submit(self, msg: Any, headers: Optional[Dict[str, Any]] = None) -> None:
+        await self.broker.publish(self.cfg.broker.download_queue, api.encode(msg), headers)
+
+    def health(self) -> Tuple[int, Dict[str, Any]]:
+        """``GET /health`` body/status (lib/main.js:176-192)."""
+        import os as _os
+        import socket
+        n = len(self.active)
+        if n == 0 and self.cfg.health.legacy_idle_500:
+            return 500, {"message": "Not Running Jobs"}
+        return 200, {"metadata": {"success": True, "host": socket.gethostname(),
+                                  "pid": _os.getpid()},
+                     "data": {"active": n}}

@@ -1,0 +1,136 @@
+"""Download stage (reference lib/download.js:230-276).
+
+Per job: resolve ``<download_path>/<media.id>`` (relative paths against the project root,
+lib/download.js:234-240; plus a per-attempt sub-directory, App. A #18), map the ``SourceType``
+enum name to a backend (lib/download.js:243,256), emit progress 0 (:255), run the backend,
+emit progress 50 (:272) and return ``{'path': dir}``.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import secrets
+from typing import Any, Awaitable, Callable, Dict
+
+from ..fetch import bucket as bucket_src
+from ..fetch import http as http_src
+from ..fetch import local as file_src
+from ..models import api
+from ..net.http import Progress
+from .base import DOWNLOADING, Job, ProtocolNotSupported, Services, Stage
+
+Backend = Callable[[str, Job, str], Awaitable[None]]
+
+
+class DownloadStage(Stage):
+    name = "download"
+
+    def __init__(self, cfg, services: Services):
+        self.cfg = cfg
+        self.sv = services
+        self.root = cfg.resolved_download_root()
+        self.methods: Dict[str, Backend] = {
+            "torrent": self.torrent,
+            "http": self.http,
+            "file": self.file,
+            "bucket": self.bucket,
+        }
+        self._torrent_client = None
+
+    def job_dir(self, job: Job) -> str:
+        d = os.path.join(str(self.root), job.id)
+        if self.cfg.instance.per_attempt_dirs:
+            job.attempt_id = job.attempt_id or secrets.token_hex(4)
+            d = os.path.join(d, job.attempt_id)
+        return d
+
+    def _count(self, proto: str, n: int) -> None:
+        if self.sv.metrics is not None and n:
+            self.sv.metrics.bytes_downloaded.labels(proto).inc(n)
+
+    async def run(self, job: Job) -> Any:
+        media = job.media
+        path = self.job_dir(job)
+        protocol = api.enum_to_string("SourceType", media.source)
+        try:
+            await asyncio.get_running_loop().run_in_executor(
+                None, lambda: os.makedirs(path, exist_ok=True))
+            job.logger.info("created downloadPath", path)
+        except OSError as e:
+            job.logger.error("Failed to create directory", str(e))
+        job.logger.info(f"Trying to download with protocol '{protocol}', the URL "
+                        f"'{self._redact(media.sourceURI, protocol)}'")
+        await self.sv.telemetry.emit_progress(job.id, DOWNLOADING, 0)
+        method = self.methods.get(protocol.lower())
+        if method is None:
+            raise ProtocolNotSupported()
+        try:
+            await method(media.sourceURI, job, path)
+        except Exception as e:
+            job.logger.error("Download error: ", str(e))
+            raise
+        job.logger.info("finished download")
+        await self.sv.telemetry.emit_progress(job.id, DOWNLOADING, 50)
+        return {"path": path}
+
+    @staticmethod
+    def _redact(uri: str, protocol: str) -> str:
+        if protocol.lower() == "bucket":
+            try:
+                return bucket_src.parse_bucket_uri(uri).redacted()
+            except ValueError:
+                return "bucket://<invalid>"
+        return uri
+
+    # ------------------------------------------------------------------ backends
+    async def http(self, url: str, job: Job, path: str) -> None:
+        job.logger.info("http", url)
+        if http_src.is_torrent_url(url):
+            job.logger.info("downloading a .torrent, chaining to torrent downloader")
+            await self.torrent(url, job, path)
+            return
+        out = os.path.join(path, http_src.output_name(url))
+        d = self.cfg.download
+        prog = Progress()
+        n = await http_src.download_to(self.sv.transports, url, out, d.http_streams,
+                                       d.http_min_split, prog, d.http_min_rate,
+                                       min(60.0, d.http_timeout_s), job.logger)
+        job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
+        self._count("http", n)
+
+    async def file(self, url: str, job: Job, path: str) -> None:
+        if not self.cfg.download.allow_file_urls:
+            raise file_src.FileUrlsNotAllowed()
+        src = file_src.file_uri_to_path(url)
+        out = file_src.target_path(url, path)
+        job.logger.debug("file", src, "->", out)
+        n = await asyncio.get_running_loop().run_in_executor(None, file_src.copy_file, src, out)
+        job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
+        self._count("file", n)
+
+    async def bucket(self, url: str, job: Job, path: str) -> None:
+        d = self.cfg.download
+        prog = Progress()
+        files = await bucket_src.fetch_bucket(url, path, secure=d.bucket_secure,
+                                              concurrency=d.bucket_concurrency,
+                                              logger=job.logger, progress=prog,
+                                              native=self.cfg.s3.native_transport)
+        n = sum(os.path.getsize(f) for f in files)
+        job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
+        self._count("bucket", n)
+
+    async def torrent(self, uri: str, job: Job, path: str) -> None:
+        from ..torrent.backend import download_torrent
+        short = uri[:25] + "..." if len(uri) > 25 else uri
+        job.logger.info("url", short)
+        n = await download_torrent(uri, job, path, self.cfg, self.sv)
+        job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
+        self._count("torrent", n)
+
+    async def close(self) -> None:
+        if self._torrent_client is not None:
+            await self._torrent_client.close()
+
+
+async def factory(cfg, services: Services) -> Stage:
+    return DownloadStage(cfg, services)

@@ -1,0 +1,33 @@
+"""Process stage (reference lib/process.js:101-122): select the media files to stage."""
+from __future__ import annotations
+
+import asyncio
+from typing import Any
+
+from .base import Job, Services, Stage
+from .select import MediaSelector, NoMediaFilesError, select_from_config
+
+
+class ProcessStage(Stage):
+    name = "process"
+
+    def __init__(self, cfg, services: Services):
+        self.cfg = cfg
+        self.sv = services
+
+    async def run(self, job: Job) -> Any:
+        last = job.last_stage or {}
+        root = last["path"]
+        job.logger.info("processing directory", root)
+        sel: MediaSelector = select_from_config(self.cfg, job.logger)
+        files = await asyncio.get_running_loop().run_in_executor(
+            None, sel.find, root, job.media.type)
+        if not files:
+            raise NoMediaFilesError()
+        job.logger.info("found", len(files), "media files")
+        job.logger.info({"files": files})
+        return {"files": files, "downloadPath": root}
+
+
+async def factory(cfg, services: Services) -> Stage:
+    return ProcessStage(cfg, services)

@@ -1,0 +1,223 @@
+"""Typed configuration (the reference's ``triton-core/config`` + env flags + constants).
+
+Reference behaviour:
+  * ``await Config('converter')`` loads a named YAML config (index.js:18; the name is a
+    copy/paste bug, App. A #1).  We load ``downloader`` and accept ``converter`` as an alias.
+  * keys used: ``instance.download_path`` (lib/download.js:235,240) and the S3 settings read
+    by ``minio.newClient(config)`` (lib/main.js:41).
+  * env: ``PORT`` (lib/main.js:194), ``ALLOW_FILE_URLS`` (lib/download.js:178).
+  * every hard-coded constant (TIMEOUT=240000 lib/download.js:21, 30 s ticker :88, bucket name
+    lib/upload.js:29, media extensions lib/process.js:15-20, prefetch 1 lib/main.js:46)
+    becomes a field here with the reference value as default.
+
+Precedence: defaults < YAML file < ``STAGER_<SECTION>__<FIELD>`` env < explicit overrides.
+``mode: reference`` pins the reference's throughput-relevant structure (one job in flight,
+sequential files, sequential parts, one HTTP stream) for A/B benchmarking.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from typing import Any, Dict, List, Literal, Mapping, Optional
+
+import yaml
+from pydantic import BaseModel, Field
+
+MiB = 1024 * 1024
+
+
+class InstanceConfig(BaseModel):
+    download_path: str = "downloads"
+    # App. A #18: concurrent duplicate deliveries must not share a directory.
+    per_attempt_dirs: bool = True
+
+
+class S3Config(BaseModel):
+    endpoint: str = "127.0.0.1:9000"
+    access_key: str = "minioadmin"
+    secret_key: str = "minioadmin"
+    region: str = "us-east-1"
+    secure: bool = False
+    bucket: str = "triton-staging"
+    part_size: int = 16 * MiB
+    multipart_threshold: int = 64 * MiB
+    max_inflight_parts: int = 8
+    concurrent_files: int = 4
+    # Sign with UNSIGNED-PAYLOAD (body never re-read for SHA-256); when False the
+    # native hasher computes the payload SHA-256 (minio-js over plain HTTP does that).
+    unsigned_payload: bool = True
+    # Use the native zero-copy HTTP transport for plain-http endpoints.
+    native_transport: bool = True
+    connect_timeout_s: float = 10.0
+    request_timeout_s: float = 300.0
+    retries: int = 3
+
+
+class BrokerConfig(BaseModel):
+    backend: Literal["amqp", "memory"] = "amqp"
+    url: str = ""  # empty -> dynamics('rabbitmq')
+    prefetch: int = 1          # lib/main.js:46 (AMQP arg 1)
+    max_retries: int = 2       # lib/main.js:46 (AMQP arg 2, INFERRED as retry budget)
+    download_queue: str = "v1.download"   # lib/main.js:172
+    convert_queue: str = "v1.convert"     # lib/main.js:164
+    dead_letter_queue: str = "v1.download.dead"
+    retry_backoff_s: float = 0.5
+    retry_backoff_max_s: float = 30.0
+    heartbeat_s: int = 30
+    reconnect_delay_s: float = 1.0
+
+
+class TelemetryConfig(BaseModel):
+    enabled: bool = True
+    status_queue: str = "v1.telemetry.status"
+    progress_queue: str = "v1.telemetry.progress"
+
+
+class DownloadConfig(BaseModel):
+    torrent_metadata_timeout_s: float = 240.0   # lib/download.js:21,47-50
+    torrent_stall_timeout_s: float = 240.0      # lib/download.js:90-101
+    progress_interval_s: float = 30.0           # lib/download.js:88
+    allow_file_urls: bool = False               # env ALLOW_FILE_URLS (lib/download.js:178)
+    http_streams: int = 4                       # parallel Range GETs per file (ref: 1)
+    http_min_split: int = 32 * MiB
+    http_timeout_s: float = 300.0
+    http_min_rate: float = 0.0                  # bytes/s stall floor, 0 = off
+    http_native: bool = True                    # native splice() transport for http://
+    bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
+    bucket_secure: bool = True                  # bucket:// is always TLS in the reference
+    verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
+    torrent_listen_port: int = 0
+    torrent_max_peers: int = 32
+    torrent_enable_dht: bool = True
+    torrent_enable_trackers: bool = True
+    torrent_enable_webseeds: bool = True
+    torrent_request_pipeline: int = 16
+    cleanup_on_stall: bool = True               # App. A #6 (reference leaves data behind)
+    emit_errored_on_stall: bool = False         # App. A #6 (reference: ack silently)
+
+
+class ProcessConfig(BaseModel):
+    media_exts: List[str] = Field(default_factory=lambda: [".mp4", ".mkv", ".mov", ".webm"])
+    case_insensitive_exts: bool = False         # App. A #15 (reference: case-sensitive)
+    legacy_full_path_extras: bool = False       # App. A #14
+    legacy_any_depth_sole_dir: bool = False     # App. A #16
+
+
+class HealthConfig(BaseModel):
+    enabled: bool = True
+    host: str = "0.0.0.0"
+    port: int = 3401                            # lib/main.js:194 (env PORT)
+    legacy_idle_500: bool = True                # App. A #9
+
+
+class MetricsConfig(BaseModel):
+    enabled: bool = True
+    # /metrics is served on the health port; a dedicated port may be set as well.
+    port: int = 0
+
+
+class TraceConfig(BaseModel):
+    enabled: bool = False
+    path: str = ""                              # JSONL span sink ("" -> stderr when enabled)
+
+
+class Config(BaseModel):
+    name: str = "downloader"
+    mode: Literal["tuned", "reference"] = "tuned"
+    concurrency: int = 2                        # jobs in flight per worker process
+    instance: InstanceConfig = Field(default_factory=InstanceConfig)
+    s3: S3Config = Field(default_factory=S3Config)
+    broker: BrokerConfig = Field(default_factory=BrokerConfig)
+    telemetry: TelemetryConfig = Field(default_factory=TelemetryConfig)
+    download: DownloadConfig = Field(default_factory=DownloadConfig)
+    process: ProcessConfig = Field(default_factory=ProcessConfig)
+    health: HealthConfig = Field(default_factory=HealthConfig)
+    metrics: MetricsConfig = Field(default_factory=MetricsConfig)
+    trace: TraceConfig = Field(default_factory=TraceConfig)
+    stages: List[str] = Field(default_factory=lambda: ["download", "process", "upload"])
+
+    def apply_mode(self) -> "Config":
+        """``mode: reference`` reproduces the reference's serial structure."""
+        if self.mode == "reference":
+            self.concurrency = 1
+            self.broker.prefetch = 1
+            self.s3.concurrent_files = 1
+            self.s3.max_inflight_parts = 1
+            self.download.http_streams = 1
+            self.download.bucket_concurrency = 1
+        else:
+            self.broker.prefetch = max(self.broker.prefetch, self.concurrency)
+        return self
+
+    def resolved_download_root(self, repo_root: Optional[Path] = None) -> Path:
+        """Relative ``download_path`` resolves against the project root (lib/download.js:234-240)."""
+        p = Path(self.instance.download_path)
+        if p.is_absolute():
+            return p
+        root = repo_root or Path(__file__).resolve().parents[2]
+        return root / p
+
+
+def _deep_merge(dst: Dict[str, Any], src: Mapping[str, Any]) -> Dict[str, Any]:
+    for k, v in src.items():
+        if isinstance(v, Mapping) and isinstance(dst.get(k), dict):
+            _deep_merge(dst[k], v)
+        else:
+            dst[k] = v
+    return dst
+
+
+def _parse_env_value(v: str) -> Any:
+    try:
+        return yaml.safe_load(v)
+    except yaml.YAMLError:
+        return v
+
+
+def env_overrides(env: Mapping[str, str]) -> Dict[str, Any]:
+    out: Dict[str, Any] = {}
+    for k, v in env.items():
+        if not k.startswith("STAGER_"):
+            continue
+        path = k[len("STAGER_"):].lower().split("__")
+        cur = out
+        for seg in path[:-1]:
+            cur = cur.setdefault(seg, {})
+        cur[path[-1]] = _parse_env_value(v)
+    # Reference env flags.
+    if "PORT" in env:
+        out.setdefault("health", {})["port"] = int(env["PORT"])
+    if "ALLOW_FILE_URLS" in env:
+        out.setdefault("download", {})["allow_file_urls"] = env["ALLOW_FILE_URLS"] == "true"
+    return out
+
+
+def find_config_file(name: str, search: Optional[List[Path]] = None) -> Optional[Path]:
+    dirs = search or [Path(os.environ.get("STAGER_CONFIG_DIR", "config")),
+                      Path(__file__).resolve().parents[2] / "config"]
+    for d in dirs:
+        for n in (name, "converter") if name == "downloader" else (name,):
+            for ext in (".yaml", ".yml"):
+                p = d / f"{n}{ext}"
+                if p.is_file():
+                    return p
+    return None
+
+
+def load_config(name: str = "downloader", path: Optional[str] = None,
+                env: Optional[Mapping[str, str]] = None,
+                overrides: Optional[Mapping[str, Any]] = None) -> Config:
+    env = os.environ if env is None else env
+    data: Dict[str, Any] = {}
+    fpath = Path(path) if path else find_config_file(name)
+    if fpath is not None:
+        with open(fpath, "r", encoding="utf-8") as f:
+            loaded = yaml.safe_load(f) or {}
+        if not isinstance(loaded, dict):
+            raise ValueError(f"config {fpath} must be a mapping")
+        _deep_merge(data, loaded)
+    _deep_merge(data, env_overrides(env))
+    if overrides:
+        _deep_merge(data, overrides)
+    data.setdefault("name", name)
+    return Config.model_validate(data).apply_mode()

@@ -1,0 +1,64 @@
+"""Prometheus metrics (the reference's ``triton-core/prom``).
+
+The reference creates ``Prom.new('downloader')`` and calls ``Prom.expose()`` (lib/main.js:43-44)
+but defines no service metrics of its own. Here each worker owns a registry with the
+staging metrics listed in SURVEY.md §5.5; the bench harness reads them back.
+"""
+from __future__ import annotations
+
+import time
+from contextlib import contextmanager
+from typing import Iterator, Optional
+
+from prometheus_client import (CollectorRegistry, Counter, Gauge, Histogram,
+                               generate_latest, start_http_server)
+from prometheus_client import CONTENT_TYPE_LATEST  # noqa: F401
+
+_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120, 300, 900, 3600)
+
+
+class Metrics:
+    def __init__(self, namespace: str = "downloader", registry: Optional[CollectorRegistry] = None):
+        self.registry = registry or CollectorRegistry(auto_describe=True)
+        ns = namespace
+        r = self.registry
+        self.bytes_downloaded = Counter("bytes_downloaded_total", "bytes fetched from sources",
+                                        ["proto"], namespace=ns, registry=r)
+        self.bytes_uploaded = Counter("bytes_uploaded_total", "bytes uploaded to staging",
+                                      namespace=ns, registry=r)
+        self.bytes_verified = Counter("bytes_verified_total", "bytes piece-hash verified",
+                                      ["backend"], namespace=ns, registry=r)
+        self.job_duration = Histogram("job_duration_seconds", "end-to-end job latency",
+                                      ["outcome"], namespace=ns, registry=r, buckets=_BUCKETS)
+        self.stage_duration = Histogram("stage_duration_seconds", "per-stage latency",
+                                        ["stage"], namespace=ns, registry=r, buckets=_BUCKETS)
+        self.inflight = Gauge("inflight_jobs", "jobs currently being processed",
+                              namespace=ns, registry=r)
+        self.jobs = Counter("jobs_total", "jobs by outcome", ["outcome"], namespace=ns, registry=r)
+        self.stalls = Counter("stall_total", "download stalls", namespace=ns, registry=r)
+        self.retries = Counter("retries_total", "job redeliveries scheduled", namespace=ns,
+                               registry=r)
+        self.key_collisions = Counter("key_collisions_total",
+                                      "files whose staging key collided within a job",
+                                      namespace=ns, registry=r)
+        self.messages = Counter("broker_messages_total", "broker traffic", ["queue", "op"],
+                                namespace=ns, registry=r)
+
+    @contextmanager
+    def time_stage(self, stage: str) -> Iterator[None]:
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.stage_duration.labels(stage).observe(time.perf_counter() - t0)
+
+    def exposition(self) -> bytes:
+        return generate_latest(self.registry)
+
+    def expose(self, port: int, addr: str = "0.0.0.0") -> None:
+        """``Prom.expose()`` equivalent: serve /metrics on a dedicated port."""
+        start_http_server(port, addr=addr, registry=self.registry)
+
+    def sample(self, name: str, **labels: str) -> float:
+        v = self.registry.get_sample_value(name, labels or None)
+        return 0.0 if v is None else v

@@ -1,0 +1,117 @@
+"""Shared fixtures: fake S3, a local HTTP origin, config factory, gpu marker."""
+from __future__ import annotations
+
+import asyncio
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+os.environ.setdefault("LOG_LEVEL", "error")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: multi-process or long-running test")
+
+
+@pytest.fixture
+def run():
+    """Run a coroutine to completion on a fresh loop."""
+    def _run(coro, timeout: float = 120.0):
+        return asyncio.run(asyncio.wait_for(coro, timeout))
+    return _run
+
+
+class Origin:
+    """aiohttp origin serving named blobs (Range + HEAD), optional faults."""
+
+    def __init__(self):
+        self.blobs = {}
+        self.runner = None
+        self.port = 0
+        self.requests = []
+        self.fail_status = {}   # path -> status
+        self.truncate = set()   # paths whose body is cut short
+        self.no_ranges = False
+        self.chunked = set()
+
+    async def start(self):
+        from aiohttp import web
+
+        async def handler(req: web.Request):
+            self.requests.append((req.method, req.path_qs, req.headers.get("Range")))
+            if req.path in self.fail_status:
+                return web.Response(status=self.fail_status[req.path], text="nope")
+            data = self.blobs.get(req.path)
+            if data is None:
+                return web.Response(status=404, text="not found")
+            hdrs = {} if self.no_ranges else {"Accept-Ranges": "bytes"}
+            rng = req.headers.get("Range")
+            if rng and not self.no_ranges:
+                a, _, b = rng[6:].partition("-")
+                s, e = int(a), int(b) if b else len(data) - 1
+                hdrs["Content-Range"] = f"bytes {s}-{e}/{len(data)}"
+                return web.Response(status=206, body=data[s:e + 1], headers=hdrs)
+            if req.method == "HEAD":
+                hdrs["Content-Length"] = str(len(data))
+                return web.Response(status=200, headers=hdrs)
+            if req.path in self.truncate:
+                resp = web.StreamResponse(status=200, headers={"Content-Length": str(len(data))})
+                await resp.prepare(req)
+                await resp.write(data[: len(data) // 2])
+                req.transport.close()
+                return resp
+            if req.path in self.chunked:
+                resp = web.StreamResponse(status=200)
+                resp.enable_chunked_encoding()
+                await resp.prepare(req)
+                for i in range(0, len(data), 7777):
+                    await resp.write(data[i:i + 7777])
+                await resp.write_eof()
+                return resp
+            return web.Response(body=data, headers=hdrs)
+
+        app = web.Application()
+        app.router.add_route("*", "/{tail:.*}", handler)
+        self.runner = web.AppRunner(app, access_log=None)
+        await self.runner.setup()
+        site = web.TCPSite(self.runner, "127.0.0.1", 0)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]
+        return self
+
+    def url(self, path: str) -> str:
+        return f"http://127.0.0.1:{self.port}{path}"
+
+    async def stop(self):
+        if self.runner is not None:
+            await self.runner.cleanup()
+
+
+@pytest.fixture
+def origin_cls():
+    return Origin
+
+
+@pytest.fixture
+def make_cfg(tmp_path):
+    from downloader_amd.utils.config import load_config
+
+    def _make(s3_endpoint: str = "127.0.0.1:9", **over):
+        base = {"instance": {"download_path": str(tmp_path / "dl")},
+                "s3": {"endpoint": s3_endpoint, "part_size": 5 << 20,
+                       "multipart_threshold": 6 << 20},
+                "broker": {"backend": "memory", "retry_backoff_s": 0.01},
+                "health": {"enabled": False}}
+        for k, v in over.items():
+            if isinstance(v, dict) and isinstance(base.get(k), dict):
+                base[k].update(v)
+            else:
+                base[k] = v
+        return load_config(overrides=base, env={})
+    return _make

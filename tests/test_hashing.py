@@ -1,0 +1,87 @@
+"""Native host hashing vs hashlib (SURVEY §4 rebuild plan item 5)."""
+from __future__ import annotations
+
+import hashlib
+import os
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from downloader_amd.ops import hashing, native
+
+
+@settings(max_examples=30, deadline=None)
+@given(st.binary(min_size=0, max_size=5000), st.sampled_from(["sha1", "sha256", "md5"]))
+def test_digest_matches_hashlib(data, algo):
+    assert native().digest(algo, data) == hashlib.new(algo, data).digest()
+
+
+@pytest.mark.parametrize("piece", [1, 63, 64, 65, 16384, 1 << 20])
+def test_hash_pieces(piece):
+    data = os.urandom(3 * 1048576 + 777)
+    want = b"".join(hashlib.sha1(data[i:i + piece]).digest() for i in range(0, len(data), piece))
+    if piece >= 64:
+        assert hashing.hash_pieces(data, piece, threads=4) == want
+
+
+def test_streaming_hasher_and_copy():
+    h = native().Hasher("sha256")
+    h.update(b"abc")
+    c = h.copy()
+    h.update(os.urandom(100000))
+    c.update(b"def")
+    assert c.digest() == hashlib.sha256(b"abcdef").digest()
+    assert c.hexdigest() == hashlib.sha256(b"abcdef").hexdigest()
+
+
+def _storage(tmp_path, sizes):
+    files, blob = [], b""
+    for i, n in enumerate(sizes):
+        d = os.urandom(n)
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(d)
+        files.append((str(p), n))
+        blob += d
+    return files, blob
+
+
+def test_verify_pieces_across_file_boundaries(tmp_path):
+    files, blob = _storage(tmp_path, [10000, 0, 70000, 3, 40000])
+    piece = 16384
+    hashes = b"".join(hashlib.sha1(blob[i:i + piece]).digest() for i in range(0, len(blob), piece))
+    assert hashing.hash_storage_pieces(files, piece) == hashes
+    ok = hashing.verify_pieces(files, piece, hashes, threads=3)
+    assert ok == b"\x01" * len(ok)
+    # corrupt one byte in the third file -> exactly the pieces covering it fail
+    p = files[2][0]
+    b = bytearray(open(p, "rb").read())
+    b[20000] ^= 0xFF
+    open(p, "wb").write(bytes(b))
+    bad_off = 10000 + 20000
+    ok = hashing.verify_pieces(files, piece, hashes)
+    assert [i for i, v in enumerate(ok) if not v] == [bad_off // piece]
+    # subset check
+    sub = hashing.verify_pieces(files, piece, hashes, which=[0, bad_off // piece])
+    assert sub == b"\x01\x00"
+
+
+def test_verify_missing_file_reports_false(tmp_path):
+    files, blob = _storage(tmp_path, [50000])
+    hashes = hashing.hash_storage_pieces(files, 16384)
+    os.unlink(files[0][0])
+    assert hashing.verify_pieces(files, 16384, hashes) == b"\x00" * 4
+
+
+def test_hash_file_ranges(tmp_path):
+    d = os.urandom(300000)
+    p = tmp_path / "x"
+    p.write_bytes(d)
+    rngs = [(0, 100), (100, 299900), (5, 0)]
+    out = hashing.hash_file_ranges(str(p), rngs, "md5", threads=2)
+    assert out == [hashlib.md5(d[o:o + n]).digest() for o, n in rngs]
+
+
+def test_choose_backend_cpu_without_gpu():
+    assert hashing.choose_backend("cpu", 1 << 40, 1 << 20) == "cpu"
+    assert hashing.choose_backend("auto", 100, 1) == "cpu"

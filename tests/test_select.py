@@ -1,0 +1,147 @@
+"""Media selector - golden cases ported from the reference's only unit tests
+(test/process/filter_dirs.js:17-82) plus the App. B truth table and property tests.
+
+The reference fixture trees hold zero-byte ``.mkv`` files; the same trees are recreated here.
+"""
+from __future__ import annotations
+
+import os
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from downloader_amd.models import api
+from downloader_amd.stages.select import MediaSelector, find_media_files, node_extname
+
+TV = api.string_to_enum("MediaType", "TV")
+MOVIE = api.string_to_enum("MediaType", "MOVIE")
+
+
+def make_tree(root, files):
+    for rel in files:
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        open(p, "wb").close()
+    return str(root)
+
+
+def test_should_filter_non_season_directories(tmp_path):
+    # reference: test/process/filter_dirs.js:21-41
+    root = make_tree(tmp_path / "should_filter_non_season_directories", [
+        "Season 1/KonoSuba S1E1.mkv", "Extras/KonoSuba OVA.mkv",
+        "Commentary/KonoSuba Season 1 Commentary.mkv", "S1/KonoSuba S1E1.mkv"])
+    files = find_media_files(root, TV)
+    assert len(files) == 2
+    assert files[0] == os.path.join(root, "S1/KonoSuba S1E1.mkv")
+    assert files[1] == os.path.join(root, "Season 1/KonoSuba S1E1.mkv")
+
+
+def test_should_read_all_dirs_when_processing_a_movie(tmp_path):
+    # reference: test/process/filter_dirs.js:43-61
+    root = make_tree(tmp_path / "movie", ["Some Movie Dir/Your Name.mkv"])
+    files = find_media_files(root, MOVIE)
+    assert files == [os.path.join(root, "Some Movie Dir/Your Name.mkv")]
+
+
+def test_should_read_with_top_level_dir(tmp_path):
+    # reference: test/process/filter_dirs.js:63-81 ("should real with top level dir")
+    root = make_tree(tmp_path / "top", ["Some Movie Dir/Your Name.mkv"])
+    files = find_media_files(root, TV)
+    assert files == [os.path.join(root, "Some Movie Dir/Your Name.mkv")]
+
+
+def test_movie_keeps_extras(tmp_path):
+    root = make_tree(tmp_path / "m", ["Extras/a.mkv", "Main/b.mp4", "c.webm", "d.txt"])
+    files = [os.path.relpath(f, root) for f in find_media_files(root, MOVIE)]
+    assert files == ["Extras/a.mkv", "Main/b.mp4", "c.webm"]
+
+
+def test_tv_season_regex_is_unanchored(tmp_path):
+    # App. B: /s\d+|season/i matches "Videos2" (s2) but not "Specials"
+    root = make_tree(tmp_path / "t", ["Videos2/a.mkv", "Specials/b.mkv", "x.mov"])
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    assert files == ["Videos2/a.mkv", "x.mov"]
+
+
+def test_extension_case_sensitive_by_default(tmp_path):
+    root = make_tree(tmp_path / "c", ["A.MKV", "b.mkv"])
+    assert [os.path.basename(f) for f in find_media_files(root, MOVIE)] == ["b.mkv"]
+    sel = MediaSelector(case_insensitive_exts=True)
+    assert [os.path.basename(f) for f in sel.find(root, MOVIE)] == ["A.MKV", "b.mkv"]
+
+
+def test_depth_first_lexicographic_order(tmp_path):
+    root = make_tree(tmp_path / "o", ["b/2.mkv", "b/1.mkv", "a/z.mkv", "a/S01/e.mkv", "0.mkv"])
+    files = [os.path.relpath(f, root) for f in find_media_files(root, MOVIE)]
+    assert files == ["0.mkv", "a/S01/e.mkv", "a/z.mkv", "b/1.mkv", "b/2.mkv"]
+
+
+def test_download_path_containing_extras_is_not_poisoned(tmp_path):
+    # App. A #14: reference tests the absolute path; we test the job-relative path.
+    root = make_tree(tmp_path / "extras-store" / "job", ["Season 1/a.mkv", "Other/b.mkv"])
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    assert files == ["Season 1/a.mkv"]
+    legacy = MediaSelector(legacy_full_path_extras=True).find(root, TV)
+    assert legacy == []
+
+
+def test_sole_dir_rule_depth_one_only(tmp_path):
+    # App. A #16: nested dir with the same name as the sole root entry is not auto-kept.
+    root = make_tree(tmp_path / "s", ["Show/Show/a.mkv", "Show/b.mkv"])
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    assert files == ["Show/b.mkv"]
+    legacy = MediaSelector(legacy_any_depth_sole_dir=True).find(root, TV)
+    assert [os.path.relpath(f, root) for f in legacy] == ["Show/Show/a.mkv", "Show/b.mkv"]
+
+
+def test_symlink_loop_terminates(tmp_path):
+    root = make_tree(tmp_path / "l", ["S1/a.mkv"])
+    os.symlink(os.path.join(root, "S1"), os.path.join(root, "S1", "S1loop"))
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    assert files[0] == "S1/a.mkv"
+    assert files == ["S1/a.mkv"]  # the symlinked dir is the same inode: cut
+
+
+@pytest.mark.parametrize("name,ext", [
+    ("index.html", ".html"), ("index.coffee.md", ".md"), ("index.", "."), ("index", ""),
+    (".index", ""), (".index.md", ".md"), ("..", ""), ("..md", ".md"), ("a.b.mkv", ".mkv"),
+    (".mkv", ""), ("x.torrent", ".torrent"),
+])
+def test_node_extname(name, ext):
+    assert node_extname(name) == ext
+
+
+_seg = st.text(alphabet="abcSs0123456789 _-eason", min_size=1, max_size=8)
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(st.tuples(st.lists(_seg, min_size=0, max_size=2),
+                          st.sampled_from(["a.mkv", "b.mp4", "c.txt", "d.MOV", "e.webm"])),
+                min_size=1, max_size=8),
+       st.booleans())
+def test_property_output_is_subset_and_media_only(tmp_path_factory, entries, movie):
+    root = tmp_path_factory.mktemp("p")
+    rels = set()
+    for dirs, fname in entries:
+        rel = os.path.join(*dirs, fname) if dirs else fname
+        rels.add(rel)
+    try:
+        make_tree(root, sorted(rels))
+    except (FileExistsError, NotADirectoryError, IsADirectoryError):
+        return
+    files = find_media_files(str(root), MOVIE if movie else TV)
+    for f in files:
+        assert os.path.isfile(f)
+        assert node_extname(os.path.basename(f)) in (".mp4", ".mkv", ".mov", ".webm")
+    assert len(files) == len(set(files))
+    if movie:
+        # MOVIE keeps every directory: all media files are selected.
+        want = sum(1 for r in rels if os.path.isfile(os.path.join(root, r))
+                   and node_extname(os.path.basename(r)) in (".mp4", ".mkv", ".mov", ".webm"))
+        assert len(files) == want
+    # top-level media files are always kept
+    top = [r for r in rels if os.sep not in r and r.endswith((".mkv", ".mp4", ".webm"))
+           and os.path.isfile(os.path.join(root, r))]
+    for t in top:
+        assert os.path.join(str(root), t) in files

@@ -1,0 +1,274 @@
+"""Service kernel end-to-end on in-process fakes (SURVEY §7.3 minimum slice + §3.4 failure
+paths): memory broker -> worker -> HTTP origin -> selector -> FakeS3 -> convert publish."""
+from __future__ import annotations
+
+import asyncio
+import base64
+import os
+
+import pytest
+
+from downloader_amd.broker.memory import MemoryBroker
+from downloader_amd.models import api, keys
+from downloader_amd.s3.fake_server import FakeS3, FaultRule
+from downloader_amd.service.worker import Worker
+from downloader_amd.stages.base import DownloadStalled, Stage
+
+
+async def _wait(w, n=1, timeout=30.0):
+    t = 0.0
+    while len(w.results) < n and t < timeout:
+        await asyncio.sleep(0.02)
+        t += 0.02
+    assert len(w.results) >= n, w.results
+
+
+async def _setup(make_cfg, origin_cls, **over):
+    s3 = FakeS3()
+    ep = await s3.start()
+    origin = await origin_cls().start()
+    cfg = make_cfg(ep, **over)
+    b = MemoryBroker()
+    w = Worker(cfg, broker=b)
+    await w.start(health=False)
+    return s3, origin, b, w
+
+
+def test_minimum_slice_http_to_s3(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls)
+        blob = os.urandom(10 * 1024 * 1024 + 3)
+        origin.blobs["/media/blob.mkv"] = blob
+        await w.submit(api.make_download("job1", "http", origin.url("/media/blob.mkv?x=1")))
+        await _wait(w)
+        r = w.results[0]
+        assert r.outcome == "staged" and r.bytes == len(blob)
+        key = "job1/original/" + base64.b64encode(b"blob.mkv").decode()
+        assert s3.get("triton-staging", key) == blob
+        assert s3.get("triton-staging", "job1/original/done") == b"true"
+        assert w.telemetry.statuses_of("job1") == [2]
+        assert w.telemetry.progress_of("job1") == [0, 50, 100]
+        conv = b.drain("v1.convert")
+        assert len(conv) == 1
+        c = api.decode(api.Convert, conv[0])
+        assert c.media.id == "job1" and c.media.sourceURI.endswith("blob.mkv?x=1")
+        # job directory cleaned up
+        assert not os.path.exists(os.path.join(w.cfg.instance.download_path, "job1", "x"))
+        code = await w.stop()
+        assert code == 0
+        await s3.stop()
+        await origin.stop()
+    run(go())
+
+
+def test_done_marker_skips_stages(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls)
+        s3.buckets["triton-staging"] = {}
+        s3.put("triton-staging", "job2/original/done", b"true")
+        await w.submit(api.make_download("job2", "http", origin.url("/nothing.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "skipped"
+        assert origin.requests == []
+        assert len(b.drain("v1.convert")) == 1
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_done_marker_probe_error_is_not_treated_as_missing(run, make_cfg, origin_cls):
+    # App. A #5: only NoSuchKey means "not staged"; an auth error must retry, not re-download
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0})
+        s3.faults.add(FaultRule(method="GET", path_contains="/done", status=403,
+                                code="AccessDenied", times=1))
+        origin.blobs["/a.mkv"] = b"x" * 100
+        await w.submit(api.make_download("job3", "http", origin.url("/a.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "dead"
+        assert origin.requests == []
+        assert w.telemetry.statuses_of("job3") == [2, 6]
+        assert len(b.drain("v1.download.dead")) == 1
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_http_error_status_fails_job_then_retries_then_dead_letters(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 2})
+        origin.fail_status["/bad.mkv"] = 500
+        await w.submit(api.make_download("job4", "http", origin.url("/bad.mkv")))
+        await _wait(w, 3)
+        assert [r.outcome for r in w.results] == ["retried", "retried", "dead"]
+        dead = b.drain("v1.download.dead")
+        assert len(dead) == 1
+        assert b.drain("v1.convert") == []
+        assert w.telemetry.statuses_of("job4") == [2, 6, 2, 6, 2, 6]
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_reference_mode_nacks_on_failure(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, mode="reference")
+        origin.fail_status["/bad.mkv"] = 404
+        await w.submit(api.make_download("job5", "http", origin.url("/bad.mkv")))
+        await _wait(w, 2)
+        assert w.results[0].outcome == "failed"
+        assert w.results[1].outcome == "failed"   # redelivered (nack requeue)
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_no_media_files_fails(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0})
+        origin.blobs["/notes.txt"] = b"hello"
+        await w.submit(api.make_download("job6", "http", origin.url("/notes.txt")))
+        await _wait(w)
+        assert w.results[0].outcome == "dead"
+        assert "suitable media" in w.results[0].error
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+class _StallStage(Stage):
+    async def run(self, job):
+        raise DownloadStalled()
+
+
+async def stall_factory(cfg, services):
+    return _StallStage()
+
+
+def test_stall_acks_and_drops(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(
+            make_cfg, origin_cls, stages=["tests.test_worker:stall_factory"])
+        await w.submit(api.make_download("job7", "http", origin.url("/x.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "stalled"
+        assert await b.queue_size("v1.download") == 0
+        assert w.telemetry.statuses_of("job7") == [2]      # reference: no ERRORED on stall
+        assert w.metrics.sample("downloader_stall_total") == 1
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_convert_publish_failure_nacks(run, make_cfg, origin_cls):
+    # App. A #8: a failed convert publish must not leave the delivery unacked forever.
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls)
+        origin.blobs["/m.mkv"] = b"m" * 1000
+        await w.submit(api.make_download("job8", "http", origin.url("/m.mkv")))
+        # fail only the convert publish (telemetry is disabled on a memory-broker? no: count)
+        orig = b.publish
+
+        async def flaky(queue, body, headers=None):
+            if queue == "v1.convert" and not getattr(flaky, "done", False):
+                flaky.done = True
+                raise ConnectionError("broker down")
+            return await orig(queue, body, headers)
+        b.publish = flaky
+        await _wait(w, 2)
+        assert w.results[0].outcome == "publish_failed"
+        assert w.results[1].outcome == "skipped"   # redelivered; done marker present
+        assert len(b.drain("v1.convert")) == 1
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_health_endpoint_semantics(run, make_cfg, origin_cls):
+    async def go():
+        import aiohttp
+        s3, origin, b, w = await _setup(make_cfg, origin_cls)
+        from downloader_amd.service.health import HealthServer
+        w.cfg.health.port = 0
+        hs = HealthServer(w, w.cfg.health)
+        port = await hs.start()
+        async with aiohttp.ClientSession() as sess:
+            async with sess.get(f"http://127.0.0.1:{port}/health") as r:
+                assert r.status == 500
+                assert await r.json() == {"message": "Not Running Jobs"}
+            from downloader_amd.service.worker import ActiveJob
+            w.active[99] = ActiveJob("j", "c")
+            async with sess.get(f"http://127.0.0.1:{port}/health") as r:
+                body = await r.json()
+                assert r.status == 200 and body["data"]["active"] == 1
+                assert body["metadata"]["success"] is True
+            async with sess.get(f"http://127.0.0.1:{port}/readyz") as r:
+                assert r.status == 200
+            async with sess.get(f"http://127.0.0.1:{port}/metrics") as r:
+                assert "downloader_jobs_total" in await r.text()
+        w.active.clear()
+        await hs.stop()
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_multi_file_bucket_source_with_collisions(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"bucket_secure": False})
+        s3.buckets["src"] = {}
+        s3.put("src", "show/S1/KonoSuba S1E1.mkv", b"one")
+        s3.put("src", "show/Season 1/KonoSuba S1E1.mkv", b"two")
+        s3.put("src", "show/Extras/ova.mkv", b"x")
+        uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,show"
+        await w.submit(api.make_download("job9", "bucket", uri, "TV"))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        k = keys.object_key("job9", "KonoSuba S1E1.mkv")
+        assert s3.get("triton-staging", k) == b"two"   # last in walk order wins (App. A #10)
+        assert w.metrics.sample("downloader_key_collisions_total") == 1
+        assert w.telemetry.progress_of("job9") == [0, 50, 75, 100]
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_file_urls_gated(run, make_cfg, origin_cls, tmp_path):
+    async def go():
+        src = tmp_path / "in.mkv"
+        src.write_bytes(b"f" * 12345)
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0})
+        await w.submit(api.make_download("j10", "file", f"file://{src}"))
+        await _wait(w)
+        assert w.results[0].outcome == "dead" and "not allowed" in w.results[0].error
+        await w.stop()
+        s3b, origin2, b2, w2 = s3, origin, MemoryBroker(), None
+        cfg = make_cfg(s3.endpoint, download={"allow_file_urls": True})
+        w2 = Worker(cfg, broker=b2)
+        await w2.start(health=False)
+        await w2.submit(api.make_download("j11", "file", f"file://{src}"))
+        await _wait(w2)
+        assert w2.results[0].outcome == "staged"
+        assert s3.get("triton-staging", keys.object_key("j11", "in.mkv")) == b"f" * 12345
+        await w2.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_concurrent_jobs_prefetch(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, concurrency=3)
+        for i in range(6):
+            origin.blobs[f"/c{i}.mp4"] = os.urandom(200_000)
+            await w.submit(api.make_download(f"cj{i}", "http", origin.url(f"/c{i}.mp4")))
+        await _wait(w, 6)
+        assert all(r.outcome == "staged" for r in w.results)
+        assert w.cfg.broker.prefetch == 3
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_unsupported_protocol_and_bad_message(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0})
+        d = api.make_download("j12", "http", "x")
+        d.media.source = 3  # BUCKET with a malformed URI
+        d.media.sourceURI = "bucket://nope"
+        await w.submit(d)
+        await b.publish("v1.download", b"\xff\xff\xff garbage")
+        await _wait(w, 2)
+        outs = sorted(r.outcome for r in w.results)
+        assert outs == ["dead", "dead"]
+        assert len(b.drain("v1.download.dead")) == 2
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
