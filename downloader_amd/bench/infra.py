@@ -17,7 +17,8 @@ PKG = Path(__file__).resolve().parents[1]
 
 class Blobd:
     def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
-                 host: str = "127.0.0.1"):
+                 host: str = "127.0.0.1", files_root: str = ""):
+        self.files_root = files_root
         self.keep_bytes = keep_bytes
         self.default_size = default_size
         self.host = host
@@ -30,7 +31,8 @@ class Blobd:
         pf = os.path.join(d, "port")
         self.proc = subprocess.Popen(
             [str(exe), "--host", self.host, "--port", "0", "--port-file", pf,
-             "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)],
+             "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)]
+            + (["--files-root", self.files_root] if self.files_root else []),
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         t0 = time.time()
         while not os.path.exists(pf):
@@ -49,6 +51,9 @@ class Blobd:
 
     def media_url(self, name: str, size: int, seed: int) -> str:
         return f"http://{self.endpoint}/media/{name}?size={size}&seed={seed}"
+
+    def files_url(self, rel: str = "") -> str:
+        return f"http://{self.endpoint}/files/{rel}"
 
     def stats(self) -> Dict[str, int]:
         with urllib.request.urlopen(f"http://{self.endpoint}/_stats", timeout=10) as r:

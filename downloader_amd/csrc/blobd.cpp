@@ -19,7 +19,10 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <signal.h>
+#include <fcntl.h>
+#include <sys/sendfile.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -56,6 +59,7 @@ std::unordered_map<std::string, Upload> g_uploads;
 std::atomic<uint64_t> g_rx{0}, g_tx{0}, g_reqs{0}, g_objects{0}, g_upload_seq{1};
 std::vector<uint8_t> g_pool;  // random pool the origin serves from
 size_t g_keep_bytes = 1 << 20;
+std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
 
 constexpr size_t kPool = 64ull << 20;
@@ -315,6 +319,60 @@ class Conn {
     return true;
   }
 
+  // Static files for BEP-19 webseeds: Range support, zero-copy sendfile from the page cache.
+  bool files(const Request& r) {
+    std::string rel = r.path.substr(7);
+    if (g_files_root.empty() || rel.find("..") != std::string::npos)
+      return respond(404, "Not Found", "no such file", "", "text/plain");
+    std::string full = g_files_root + "/" + rel;
+    int fd = ::open(full.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return respond(404, "Not Found", "no such file", "", "text/plain");
+    struct stat st;
+    fstat(fd, &st);
+    uint64_t size = (uint64_t)st.st_size, start = 0, end = size ? size - 1 : 0;
+    bool ranged = false;
+    auto it = r.h.find("range");
+    if (it != r.h.end() && it->second.rfind("bytes=", 0) == 0) {
+      std::string spec = it->second.substr(6);
+      size_t dash = spec.find('-');
+      std::string a = spec.substr(0, dash), b = spec.substr(dash + 1);
+      start = a.empty() ? (size > strtoull(b.c_str(), nullptr, 10) ? size - strtoull(b.c_str(), nullptr, 10) : 0)
+                        : strtoull(a.c_str(), nullptr, 10);
+      if (!a.empty() && !b.empty()) end = std::min<uint64_t>(strtoull(b.c_str(), nullptr, 10), size - 1);
+      ranged = true;
+      if (start > end || start >= size) {
+        ::close(fd);
+        return respond(416, "Range Not Satisfiable", "", "", "text/plain");
+      }
+    }
+    uint64_t len = size ? end - start + 1 : 0;
+    char hdr[512];
+    int n = snprintf(hdr, sizeof hdr,
+                     "HTTP/1.1 %d %s\r\nServer: blobd\r\nAccept-Ranges: bytes\r\nContent-Length: %" PRIu64 "\r\n",
+                     ranged ? 206 : 200, ranged ? "Partial Content" : "OK", len);
+    std::string out(hdr, (size_t)n);
+    if (ranged)
+      out += "Content-Range: bytes " + std::to_string(start) + "-" + std::to_string(end) + "/" +
+             std::to_string(size) + "\r\n";
+    out += "\r\n";
+    bool ok = send_all(out.data(), out.size());
+    if (ok && r.method != "HEAD") {
+      off_t o = (off_t)start;
+      uint64_t left = len;
+      while (ok && left) {
+        ssize_t w = ::sendfile(fd_, fd, &o, (size_t)std::min<uint64_t>(left, 8u << 20));
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) ok = false;
+        else {
+          left -= (uint64_t)w;
+          g_tx += (uint64_t)w;
+        }
+      }
+    }
+    ::close(fd);
+    return ok;
+  }
+
   bool s3(const Request& r) {
     std::string p = r.path.substr(1);
     size_t sl = p.find('/');
@@ -459,6 +517,7 @@ class Conn {
   bool dispatch(const Request& r) {
     if (r.path == "/_stats") return stats();
     if (r.path.rfind("/media/", 0) == 0 && (r.method == "GET" || r.method == "HEAD")) return origin(r);
+    if (r.path.rfind("/files/", 0) == 0 && (r.method == "GET" || r.method == "HEAD")) return files(r);
     return s3(r);
   }
 
@@ -481,6 +540,7 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = next();
     else if (a == "--keep-bytes") g_keep_bytes = strtoull(next(), nullptr, 10);
     else if (a == "--default-size") g_default_size = strtoull(next(), nullptr, 10);
+    else if (a == "--files-root") g_files_root = next();
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] [--default-size N]\n");
       return 2;

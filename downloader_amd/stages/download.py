@@ -35,7 +35,6 @@ class DownloadStage(Stage):
             "file": self.file,
             "bucket": self.bucket,
         }
-        self._torrent_client = None
 
     def job_dir(self, job: Job) -> str:
         d = os.path.join(str(self.root), job.id)
@@ -128,8 +127,9 @@ class DownloadStage(Stage):
         self._count("torrent", n)
 
     async def close(self) -> None:
-        if self._torrent_client is not None:
-            await self._torrent_client.close()
+        c = self.sv.extra.pop("torrent_client", None)
+        if c is not None:
+            await c.close()
 
 
 async def factory(cfg, services: Services) -> Stage:

@@ -1,0 +1,160 @@
+"""Torrent client: one per worker process (the reference keeps a module-level
+``new Webtorrent()`` singleton, lib/download.js:19, shared by every job). It owns the TCP
+listener for incoming peers, the optional DHT node and the transports; each job gets its own
+``TorrentSession`` (no shared ``torrents`` map keyed by magnet, App. A #3/#7)."""
+from __future__ import annotations
+
+import asyncio
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .magnet import Magnet
+from .metainfo import Metainfo
+from .peer import PeerConn, handshake_bytes, read_handshake
+from .session import TorrentError, TorrentSession
+from .tracker import random_peer_id
+
+Peer = Tuple[str, int]
+
+
+class TorrentClient:
+    def __init__(self, transports=None, peer_id: Optional[bytes] = None,
+                 listen_host: str = "0.0.0.0", listen_port: int = 0, public_host: str = "",
+                 max_peers: int = 32, max_uploads: int = 8, pipeline: int = 16,
+                 enable_dht: bool = False, dht_bootstrap: Sequence[Peer] = (),
+                 dht_port: int = 0, verify_backend: str = "auto", webseed_streams: int = 4,
+                 webseed_chunk: int = 32 << 20, webseed_max_failures: int = 5,
+                 idle_timeout: float = 120.0, connect_timeout: float = 10.0,
+                 seed_after_done: bool = False, listen: bool = True):
+        from ..net.http import make_transports
+        self._own_transports = transports is None
+        self.transports = transports or make_transports()
+        self.peer_id = peer_id or random_peer_id()
+        self.listen_host = listen_host
+        self.listen_port = listen_port
+        self.public_host = public_host
+        self.max_peers = max_peers
+        self.max_uploads = max_uploads
+        self.pipeline = pipeline
+        self.enable_dht = enable_dht
+        self.dht_bootstrap = list(dht_bootstrap)
+        self.dht_port = dht_port
+        self.dht = None
+        self.verify_backend = verify_backend
+        self.webseed_streams = webseed_streams
+        self.webseed_chunk = webseed_chunk
+        self.webseed_max_failures = webseed_max_failures
+        self.idle_timeout = idle_timeout
+        self.connect_timeout = connect_timeout
+        self.seed_after_done = seed_after_done
+        self.listen = listen
+        self.pex_interval = 60.0
+        self.dht_interval = 30.0
+        self.max_announce_interval = 300.0
+        self.sessions: Dict[bytes, TorrentSession] = {}
+        self._server: Optional[asyncio.AbstractServer] = None
+        self._conn_tasks: set = set()
+
+    @classmethod
+    def from_config(cls, cfg, transports=None, **kw) -> "TorrentClient":
+        d = cfg.download
+        boot = kw.pop("dht_bootstrap", None)
+        return cls(transports=transports, listen_port=d.torrent_listen_port,
+                   max_peers=d.torrent_max_peers, pipeline=d.torrent_request_pipeline,
+                   enable_dht=d.torrent_enable_dht, verify_backend=d.verify_backend,
+                   webseed_streams=max(1, d.http_streams),
+                   dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
+
+    async def start(self) -> "TorrentClient":
+        if self.listen:
+            self._server = await asyncio.start_server(self._incoming, self.listen_host,
+                                                      self.listen_port, reuse_address=True)
+            self.listen_port = self._server.sockets[0].getsockname()[1]
+        if self.enable_dht:
+            from .dht import DHTNode
+            self.dht = DHTNode(port=self.dht_port, bootstrap=self.dht_bootstrap)
+            await self.dht.start()
+        return self
+
+    async def close(self) -> None:
+        for s in list(self.sessions.values()):
+            await s.close()
+        self.sessions.clear()
+        if self._server is not None:
+            self._server.close()
+            await self._server.wait_closed()
+        for t in list(self._conn_tasks):
+            t.cancel()
+        if self.dht is not None:
+            await self.dht.close()
+        if self._own_transports:
+            await self.transports.close()
+
+    # ---------------------------------------------------------------- sessions
+    def _register(self, s: TorrentSession) -> TorrentSession:
+        if s.info_hash in self.sessions:
+            raise TorrentError("torrent already active in this worker")
+        self.sessions[s.info_hash] = s
+        return s
+
+    async def add_torrent(self, meta: Metainfo, root: str, peers: Sequence[Peer] = (),
+                          extra_webseeds: Sequence[str] = ()) -> TorrentSession:
+        s = self._register(TorrentSession(self, meta.info_hash, root, meta, peers=peers,
+                                          webseeds=extra_webseeds))
+        await s.start()
+        return s
+
+    async def add_magnet(self, m: Magnet, root: str) -> TorrentSession:
+        s = self._register(TorrentSession(self, m.info_hash, root, None, m.trackers, m.webseeds,
+                                          m.peers, m.name))
+        await s.start()
+        return s
+
+    async def remove(self, s: TorrentSession) -> None:
+        self.sessions.pop(s.info_hash, None)
+        await s.close()
+
+    # ---------------------------------------------------------------- peers
+    async def connect_peer(self, s: TorrentSession, addr: Peer) -> PeerConn:
+        r, w = await asyncio.wait_for(asyncio.open_connection(addr[0], addr[1]),
+                                      self.connect_timeout)
+        try:
+            w.write(handshake_bytes(s.info_hash, self.peer_id, True, self.dht is not None))
+            await w.drain()
+            reserved, ih, pid = await read_handshake(r, self.connect_timeout)
+            if ih != s.info_hash:
+                raise TorrentError("peer answered for another torrent")
+        except BaseException:
+            w.close()
+            raise
+        pc = PeerConn(s, r, w, addr, pid, reserved, outgoing=True)
+        if not s.register_peer(pc):
+            w.close()
+            raise TorrentError("peer rejected (duplicate or full)")
+        return pc
+
+    async def _incoming(self, r: asyncio.StreamReader, w: asyncio.StreamWriter) -> None:
+        t = asyncio.current_task()
+        self._conn_tasks.add(t)
+        try:
+            try:
+                reserved, ih, pid = await read_handshake(r, self.connect_timeout)
+            except Exception:
+                w.close()
+                return
+            s = self.sessions.get(ih)
+            if s is None or s._closed:
+                w.close()
+                return
+            w.write(handshake_bytes(ih, self.peer_id, True, self.dht is not None))
+            peer = w.get_extra_info("peername") or ("?", 0)
+            pc = PeerConn(s, r, w, (peer[0], peer[1]), pid, reserved, outgoing=False)
+            if not s.register_peer(pc):
+                w.close()
+                return
+            await pc.run()
+        finally:
+            self._conn_tasks.discard(t)
+
+
+DEFAULT_BOOTSTRAP: List[Peer] = [("router.bittorrent.com", 6881), ("dht.transmissionbt.com", 6881),
+                                 ("router.utorrent.com", 6881)]

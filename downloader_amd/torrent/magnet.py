@@ -1,0 +1,91 @@
+"""Magnet URIs (BEP-9) - replaces ``magnet-uri@5`` (yarn.lock:2040).
+
+``xt=urn:btih:<40 hex | 32 base32>``, ``dn`` display name, ``tr`` trackers, ``ws`` webseeds
+(BEP-19), ``x.pe`` peer addresses, ``xl`` exact length."""
+from __future__ import annotations
+
+import base64
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+from urllib.parse import parse_qsl, quote, urlsplit
+
+
+class MagnetError(ValueError):
+    pass
+
+
+@dataclass
+class Magnet:
+    info_hash: bytes
+    name: str = ""
+    trackers: List[str] = field(default_factory=list)
+    webseeds: List[str] = field(default_factory=list)
+    peers: List[Tuple[str, int]] = field(default_factory=list)
+    exact_length: Optional[int] = None
+
+    def to_uri(self) -> str:
+        parts = [f"xt=urn:btih:{self.info_hash.hex()}"]
+        if self.name:
+            parts.append("dn=" + quote(self.name))
+        parts += ["tr=" + quote(t, safe="") for t in self.trackers]
+        parts += ["ws=" + quote(w, safe="") for w in self.webseeds]
+        parts += [f"x.pe={h}:{p}" for h, p in self.peers]
+        return "magnet:?" + "&".join(parts)
+
+
+def parse_btih(v: str) -> bytes:
+    v = v.strip()
+    if len(v) == 40:
+        try:
+            return bytes.fromhex(v)
+        except ValueError as e:
+            raise MagnetError("bad hex infohash") from e
+    if len(v) == 32:
+        try:
+            return base64.b32decode(v.upper())
+        except ValueError as e:
+            raise MagnetError("bad base32 infohash") from e
+    raise MagnetError(f"infohash must be 40 hex or 32 base32 chars, got {len(v)}")
+
+
+def _hostport(s: str) -> Optional[Tuple[str, int]]:
+    if s.startswith("["):
+        h, _, rest = s[1:].partition("]")
+        port = rest.lstrip(":")
+    else:
+        h, _, port = s.rpartition(":")
+    try:
+        return h, int(port)
+    except ValueError:
+        return None
+
+
+def parse_magnet(uri: str) -> Magnet:
+    u = urlsplit(uri)
+    if u.scheme != "magnet":
+        raise MagnetError("not a magnet URI")
+    ih = None
+    m = Magnet(b"")
+    for k, v in parse_qsl(u.query, keep_blank_values=True):
+        k = k.split(".", 1)[0] if k.startswith(("xt.", "tr.", "ws.")) else k
+        if k == "xt" and v.lower().startswith("urn:btih:") and ih is None:
+            ih = parse_btih(v[9:])
+        elif k == "dn":
+            m.name = v
+        elif k == "tr":
+            m.trackers.append(v)
+        elif k == "ws":
+            m.webseeds.append(v)
+        elif k == "x.pe":
+            hp = _hostport(v)
+            if hp:
+                m.peers.append(hp)
+        elif k == "xl":
+            try:
+                m.exact_length = int(v)
+            except ValueError:
+                pass
+    if ih is None:
+        raise MagnetError("magnet URI has no urn:btih infohash")
+    m.info_hash = ih
+    return m

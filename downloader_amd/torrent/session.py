@@ -1,0 +1,660 @@
+"""One torrent being downloaded (and seeded while it runs).
+
+Replaces webtorrent's ``Torrent`` (reference: ``client.add(magnet, {path}, cb)`` lib/download.js:64,
+``torrent.progress`` :79, ``'done'`` :110, ``'error'`` :103). Sources of data:
+
+* peers (BEP-3) found through trackers, DHT (BEP-5), PEX (BEP-11), magnet ``x.pe`` and
+  incoming connections - rarest-first piece picking, 16 KiB block pipelining, endgame mode,
+  per-piece SHA-1 verification before anything is written;
+* webseeds (BEP-19 ``url-list`` / magnet ``ws``) - runs of whole pieces are fetched with HTTP
+  Range GETs spliced directly into the files (native transport), then verified in place by the
+  threaded native SHA-1; failed pieces are released back to the picker.
+
+Metadata for magnets is fetched with ut_metadata (BEP-9) and checked against the infohash.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import os
+import random
+import struct
+import time
+from typing import TYPE_CHECKING, Dict, List, Optional, Set, Tuple
+from urllib.parse import quote
+
+from ..net.http import FileSink, TransportError
+from .bencode import bencode
+from .metainfo import Metainfo, MetainfoError, parse_info
+from .peer import BLOCK, METADATA_PIECE, PIECE, PeerConn
+from .storage import Bitfield, Storage
+from .tracker import decode_compact, encode_compact
+
+if TYPE_CHECKING:  # pragma: no cover
+    from .client import TorrentClient
+
+Peer = Tuple[str, int]
+
+
+class TorrentError(Exception):
+    pass
+
+
+class _Active:
+    __slots__ = ("idx", "size", "nblocks", "buf", "state", "req", "got", "peers")
+
+    def __init__(self, idx: int, size: int):
+        self.idx = idx
+        self.size = size
+        self.nblocks = (size + BLOCK - 1) // BLOCK
+        self.buf = bytearray(size)
+        self.state = bytearray(self.nblocks)   # 0 free, 1 requested, 2 received
+        self.req: Dict[int, Set[int]] = {}     # block -> ids of peers that requested it
+        self.got = 0
+        self.peers: Set[int] = set()           # peers that contributed blocks
+
+    def block_len(self, b: int) -> int:
+        return min(BLOCK, self.size - b * BLOCK)
+
+
+class PiecePicker:
+    """Rarest-first picker over pieces; blocks inside active pieces; endgame duplicates."""
+
+    def __init__(self, meta: Metainfo, have: Bitfield):
+        self.meta = meta
+        self.have = have
+        self.n = meta.num_pieces
+        self.avail = [0] * self.n
+        self.active: Dict[int, _Active] = {}
+        self.claimed: Set[int] = set()       # pieces owned by webseed workers
+        self.failed: Dict[int, int] = {}
+
+    def add_peer(self, bf: Bitfield) -> None:
+        for i in range(self.n):
+            if i in bf:
+                self.avail[i] += 1
+
+    def remove_peer(self, bf: Bitfield) -> None:
+        for i in range(self.n):
+            if i in bf:
+                self.avail[i] -= 1
+
+    def inc(self, i: int) -> None:
+        self.avail[i] += 1
+
+    def wanted(self, i: int) -> bool:
+        return i not in self.have
+
+    def peer_has_wanted(self, bf: Bitfield) -> bool:
+        if self.have.complete:
+            return False
+        return any(i in bf and i not in self.have for i in range(self.n))
+
+    def next_block(self, peer_id: int, bf: Bitfield) -> Optional[Tuple[int, int, int]]:
+        # 1. a free block of an active piece this peer has
+        for ap in self.active.values():
+            if ap.idx in bf:
+                for b in range(ap.nblocks):
+                    if ap.state[b] == 0:
+                        ap.state[b] = 1
+                        ap.req.setdefault(b, set()).add(peer_id)
+                        return ap.idx, b * BLOCK, ap.block_len(b)
+        # 2. start the rarest piece this peer has
+        best, best_av, ties = -1, 1 << 30, 0
+        for i in range(self.n):
+            if i in self.have or i in self.active or i in self.claimed or i not in bf:
+                continue
+            a = self.avail[i]
+            if a < best_av:
+                best, best_av, ties = i, a, 1
+            elif a == best_av:
+                ties += 1
+                if random.randrange(ties) == 0:
+                    best = i
+        if best >= 0:
+            ap = _Active(best, self.meta.piece_size(best))
+            self.active[best] = ap
+            ap.state[0] = 1
+            ap.req[0] = {peer_id}
+            return best, 0, ap.block_len(0)
+        # 3. endgame: duplicate an outstanding block this peer has not requested yet
+        for ap in self.active.values():
+            if ap.idx in bf:
+                for b in range(ap.nblocks):
+                    if ap.state[b] == 1 and peer_id not in ap.req.get(b, ()):
+                        ap.req.setdefault(b, set()).add(peer_id)
+                        return ap.idx, b * BLOCK, ap.block_len(b)
+        return None
+
+    def release(self, peer_id: int, piece: int, begin: int) -> None:
+        ap = self.active.get(piece)
+        if ap is None:
+            return
+        b = begin // BLOCK
+        rs = ap.req.get(b)
+        if rs is not None:
+            rs.discard(peer_id)
+            if not rs and ap.state[b] == 1:
+                ap.state[b] = 0
+
+    def claim_run(self, max_bytes: int) -> Optional[Tuple[int, int]]:
+        """Claim the first run of contiguous free pieces (<= max_bytes) for a webseed."""
+        plen = self.meta.piece_length
+        maxp = max(1, max_bytes // plen)
+        i = 0
+        while i < self.n:
+            if i in self.have or i in self.active or i in self.claimed:
+                i += 1
+                continue
+            j = i
+            while j < self.n and j - i < maxp and j not in self.have and j not in self.active \
+                    and j not in self.claimed:
+                j += 1
+            for k in range(i, j):
+                self.claimed.add(k)
+            return i, j - i
+        return None
+
+    def unclaim(self, pieces) -> None:
+        for p in pieces:
+            self.claimed.discard(p)
+
+    def remaining(self) -> int:
+        return self.n - self.have.count
+
+
+class MetadataFetch:
+    def __init__(self, info_hash: bytes):
+        self.info_hash = info_hash
+        self.size = 0
+        self.pieces: Dict[int, bytes] = {}
+        self.pending: Dict[int, float] = {}
+
+    def n(self) -> int:
+        return (self.size + METADATA_PIECE - 1) // METADATA_PIECE
+
+    def next_piece(self) -> Optional[int]:
+        now = time.monotonic()
+        for i in range(self.n()):
+            if i not in self.pieces and now - self.pending.get(i, 0) > 5.0:
+                self.pending[i] = now
+                return i
+        return None
+
+    def assemble(self) -> Optional[bytes]:
+        if self.size == 0 or len(self.pieces) < self.n():
+            return None
+        data = b"".join(self.pieces[i] for i in range(self.n()))[: self.size]
+        if hashlib.sha1(data).digest() != self.info_hash:
+            self.pieces.clear()
+            self.pending.clear()
+            return None
+        return data
+
+
+class TorrentSession:
+    def __init__(self, client: "TorrentClient", info_hash: bytes, root: str,
+                 meta: Optional[Metainfo] = None, trackers=(), webseeds=(), peers=(), name: str = ""):
+        self.client = client
+        self.info_hash = info_hash
+        self.root = root
+        self.meta = meta
+        self.name = name
+        self.trackers: List[str] = list(trackers)
+        self.webseeds: List[str] = list(webseeds)
+        self.known: Dict[Peer, float] = {}
+        self.failed_peers: Dict[Peer, Tuple[int, float]] = {}
+        self.peers: Dict[int, PeerConn] = {}
+        self.storage: Optional[Storage] = None
+        self.have: Optional[Bitfield] = None
+        self.picker: Optional[PiecePicker] = None
+        self.metafetch = MetadataFetch(info_hash)
+        self.meta_ready = asyncio.Event()
+        self.done = asyncio.Event()
+        self.error: Optional[BaseException] = None
+        self.failed = asyncio.Event()
+        self.idle_timeout = client.idle_timeout
+        self.downloaded = 0
+        self.uploaded = 0
+        self.verified_bytes = 0
+        self.webseed_bytes = 0
+        self._tasks: List[asyncio.Task] = []
+        self._wake = asyncio.Event()
+        self._closed = False
+        self._ws_dead = 0
+        self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0}
+        self.add_peers(list(peers), "magnet")
+        if meta is not None:
+            self.trackers += [t for t in meta.trackers() if t not in self.trackers]
+            self.webseeds += [w for w in meta.url_list if w not in self.webseeds]
+
+    # ---------------------------------------------------------------- state
+    @property
+    def progress(self) -> float:
+        """Fraction of verified bytes, 0..1 (webtorrent ``torrent.progress``)."""
+        if self.meta is None or self.meta.total_length == 0:
+            return 1.0 if self.done.is_set() else 0.0
+        return self.verified_bytes / self.meta.total_length
+
+    @property
+    def left(self) -> int:
+        if self.meta is None:
+            return 1 << 40
+        return self.meta.total_length - self.verified_bytes
+
+    async def start(self) -> None:
+        if self.meta is not None:
+            await self._init_storage()
+        self._spawn(self._connector())
+        for t in self.trackers:
+            self._spawn(self._announce_loop(t))
+        if self.client.dht is not None and not (self.meta and self.meta.private):
+            self._spawn(self._dht_loop())
+        self._spawn(self._pex_loop())
+
+    def _spawn(self, coro) -> asyncio.Task:
+        t = asyncio.get_running_loop().create_task(coro)
+        self._tasks.append(t)
+        t.add_done_callback(self._task_done)
+        return t
+
+    def _task_done(self, t: asyncio.Task) -> None:
+        if t.cancelled():
+            return
+        e = t.exception()
+        if e is not None and not isinstance(e, (asyncio.CancelledError,)):
+            self.fail(e)
+
+    def fail(self, e: BaseException) -> None:
+        if self.error is None and not self.done.is_set():
+            self.error = e
+            self.failed.set()
+
+    async def _init_storage(self) -> None:
+        loop = asyncio.get_running_loop()
+        meta = self.meta
+        assert meta is not None
+        self.storage = await loop.run_in_executor(None, Storage, meta, self.root)
+        self.have = await loop.run_in_executor(None, self.storage.recheck,
+                                               self.client.verify_backend)
+        self.verified_bytes = sum(meta.piece_size(i) for i in range(meta.num_pieces)
+                                  if i in self.have)
+        self.picker = PiecePicker(meta, self.have)
+        self.meta_ready.set()
+        for p in list(self.peers.values()):
+            p.attach_meta()
+            await self.update_interest(p)
+            await p.send_bitfield()
+            await self.fill(p)
+        for url in self.webseeds:
+            for _ in range(self.client.webseed_streams):
+                self._spawn(self._webseed_worker(url))
+        if self.have.complete:
+            self._finish()
+
+    def _finish(self) -> None:
+        if not self.done.is_set():
+            if self.storage is not None:
+                self.storage.sync()
+            self.done.set()
+            for t in self.trackers:
+                self._spawn(self._announce_once(t, "completed"))
+
+    # ---------------------------------------------------------------- peers
+    def add_peers(self, peers: List[Peer], source: str = "") -> None:
+        new = False
+        for p in peers:
+            if p[1] <= 0 or p[1] > 65535:
+                continue
+            if p == (self.client.public_host, self.client.listen_port) or \
+                    (p[1] == self.client.listen_port and p[0] in ("127.0.0.1", "0.0.0.0", "::1")
+                     and self.client.listen_port):
+                continue
+            if p not in self.known:
+                self.known[p] = time.monotonic()
+                new = True
+        if new:
+            self._wake.set()
+
+    def connected_addrs(self) -> Set[Peer]:
+        return {p.addr for p in self.peers.values()}
+
+    async def _connector(self) -> None:
+        while not self._closed:
+            if not self.done.is_set() or self.client.seed_after_done:
+                conn = self.connected_addrs()
+                now = time.monotonic()
+                cands = [p for p in self.known if p not in conn and
+                         now >= self.failed_peers.get(p, (0, 0.0))[1]]
+                random.shuffle(cands)
+                room = self.client.max_peers - len(self.peers)
+                for p in cands[:max(0, room)]:
+                    self._spawn(self._connect(p))
+            self._wake.clear()
+            try:
+                await asyncio.wait_for(self._wake.wait(), 2.0)
+            except asyncio.TimeoutError:
+                pass
+
+    async def _connect(self, addr: Peer) -> None:
+        try:
+            pc = await self.client.connect_peer(self, addr)
+        except Exception:
+            n, _ = self.failed_peers.get(addr, (0, 0.0))
+            self.failed_peers[addr] = (n + 1, time.monotonic() + min(300.0, 2.0 * (2 ** n)))
+            return
+        self.failed_peers.pop(addr, None)
+        await pc.run()
+
+    def register_peer(self, pc: PeerConn) -> bool:
+        if len(self.peers) >= self.client.max_peers + 8 or self._closed:
+            return False
+        if pc.addr in self.connected_addrs() or pc.remote_id == self.client.peer_id:
+            return False
+        self.peers[id(pc)] = pc
+        self.stats["peers_connected"] += 1
+        if self.meta is not None and pc.bitfield is None:
+            pc.bitfield = Bitfield(self.meta.num_pieces)
+        return True
+
+    def peer_closed(self, pc: PeerConn) -> None:
+        if self.peers.pop(id(pc), None) is None:
+            return
+        self.release_inflight(pc)
+        if pc.bitfield is not None and self.picker is not None:
+            self.picker.remove_peer(pc.bitfield)
+        self._wake.set()
+
+    def release_inflight(self, pc: PeerConn) -> None:
+        if self.picker is not None:
+            for (piece, begin) in list(pc.inflight):
+                self.picker.release(id(pc), piece, begin)
+        pc.inflight.clear()
+
+    async def update_interest(self, pc: PeerConn) -> None:
+        if self.picker is None or pc.bitfield is None:
+            return
+        await pc.set_interested(self.picker.peer_has_wanted(pc.bitfield))
+
+    async def maybe_unchoke(self, pc: PeerConn) -> None:
+        unchoked = sum(1 for p in self.peers.values() if not p.am_choking)
+        if pc.am_choking and unchoked < self.client.max_uploads and self.have is not None:
+            await pc.set_choking(False)
+
+    async def fill(self, pc: PeerConn) -> None:
+        if self.picker is None or pc.peer_choking or not pc.am_interested or pc.bitfield is None:
+            return
+        while len(pc.inflight) < self.client.pipeline:
+            nb = self.picker.next_block(id(pc), pc.bitfield)
+            if nb is None:
+                break
+            await pc.request(*nb)
+
+    async def on_block(self, pc: PeerConn, idx: int, begin: int, data: bytes) -> None:
+        if self.picker is None or self.have is None:
+            return
+        ap = self.picker.active.get(idx)
+        if ap is None or begin % BLOCK or begin >= ap.size:
+            return
+        b = begin // BLOCK
+        if ap.state[b] == 2 or len(data) != ap.block_len(b):
+            return
+        ap.buf[begin:begin + len(data)] = data
+        ap.state[b] = 2
+        ap.got += 1
+        ap.peers.add(id(pc))
+        self.downloaded += len(data)
+        # endgame: cancel duplicates elsewhere
+        for other_id in ap.req.pop(b, set()):
+            if other_id != id(pc):
+                other = self.peers.get(other_id)
+                if other is not None:
+                    await other.cancel(idx, begin, len(data))
+        if ap.got < ap.nblocks:
+            return
+        del self.picker.active[idx]
+        buf = bytes(ap.buf)
+        loop = asyncio.get_running_loop()
+        from ..ops import hashing
+        digest = await loop.run_in_executor(None, hashing.sha1, buf) if len(buf) >= 262144 \
+            else hashing.sha1(buf)
+        if digest != self.meta.piece_hash(idx):
+            self.stats["hash_fails"] += 1
+            for pid in ap.peers:
+                p = self.peers.get(pid)
+                if p is not None:
+                    p.hash_fails += 1
+                    if p.hash_fails >= 3:
+                        p.close()
+            return
+        await loop.run_in_executor(None, self.storage.write, idx * self.meta.piece_length, buf)
+        await self._piece_complete(idx)
+
+    async def _piece_complete(self, idx: int) -> None:
+        if not self.have.set(idx):
+            return
+        self.verified_bytes += self.meta.piece_size(idx)
+        for p in list(self.peers.values()):
+            await p.send_have(idx)
+            if p.am_interested and p.bitfield is not None and not self.picker.peer_has_wanted(p.bitfield):
+                await p.set_interested(False)
+        if self.have.complete:
+            self._finish()
+
+    async def serve_request(self, pc: PeerConn, idx: int, begin: int, ln: int) -> None:
+        if pc.am_choking or self.have is None or idx >= self.have.n or idx not in self.have:
+            return
+        if ln > 131072 or begin + ln > self.meta.piece_size(idx):
+            return
+        data = await asyncio.get_running_loop().run_in_executor(
+            None, self.storage.read_block, idx, begin, ln)
+        pc.up_bytes += ln
+        self.uploaded += ln
+        await pc.send(PIECE, struct.pack(">II", idx, begin) + data)
+
+    # ---------------------------------------------------------------- metadata (BEP-9)
+    async def on_ext_handshake(self, pc: PeerConn) -> None:
+        if self.meta is None and pc.metadata_size and b"ut_metadata" in pc.ext:
+            if pc.metadata_size > 64 << 20:
+                return
+            if self.metafetch.size == 0:
+                self.metafetch.size = pc.metadata_size
+            await self._request_metadata(pc)
+
+    async def _request_metadata(self, pc: PeerConn) -> None:
+        if self.meta is not None or b"ut_metadata" not in pc.ext:
+            return
+        for _ in range(4):
+            i = self.metafetch.next_piece()
+            if i is None:
+                return
+            await pc.send_ext(b"ut_metadata", bencode({"msg_type": 0, "piece": i}))
+
+    async def on_metadata_msg(self, pc: PeerConn, d, tail: bytes) -> None:
+        if not isinstance(d, dict):
+            return
+        t = d.get(b"msg_type")
+        piece = int(d.get(b"piece", -1))
+        if t == 0:  # request
+            if self.meta is None:
+                await pc.send_ext(b"ut_metadata", bencode({"msg_type": 2, "piece": piece}))
+                return
+            raw = self.meta.raw_info
+            chunk = raw[piece * METADATA_PIECE:(piece + 1) * METADATA_PIECE]
+            if not chunk:
+                await pc.send_ext(b"ut_metadata", bencode({"msg_type": 2, "piece": piece}))
+                return
+            await pc.send_ext(b"ut_metadata", bencode({"msg_type": 1, "piece": piece,
+                                                       "total_size": len(raw)}) + chunk)
+        elif t == 1 and self.meta is None:
+            if 0 <= piece < self.metafetch.n():
+                self.metafetch.pieces[piece] = tail
+            data = self.metafetch.assemble()
+            if data is not None:
+                await self.set_metadata(data)
+            else:
+                await self._request_metadata(pc)
+        elif t == 2:
+            self.metafetch.pending.pop(piece, None)
+
+    async def set_metadata(self, info_bytes: bytes) -> None:
+        if self.meta is not None:
+            return
+        try:
+            m = parse_info(info_bytes, self.info_hash)
+        except MetainfoError as e:
+            self.fail(TorrentError(f"bad metadata: {e}"))
+            return
+        self.meta = m
+        self.name = m.name
+        await self._init_storage()
+
+    # ---------------------------------------------------------------- PEX (BEP-11)
+    def on_pex(self, pc: PeerConn, d) -> None:
+        if not isinstance(d, dict) or (self.meta is not None and self.meta.private):
+            return
+        added = d.get(b"added", b"")
+        if isinstance(added, bytes):
+            self.add_peers(decode_compact(added), "pex")
+
+    async def _pex_loop(self) -> None:
+        while not self._closed:
+            await asyncio.sleep(self.client.pex_interval)
+            if self.meta is not None and self.meta.private:
+                continue
+            addrs = [p.addr if p.outgoing else (p.addr[0], p.listen_port)
+                     for p in self.peers.values() if p.outgoing or p.listen_port]
+            msg = bencode({"added": encode_compact(addrs[:50]), "added.f": b"\x00" * min(50, len(addrs)),
+                           "dropped": b""})
+            for p in list(self.peers.values()):
+                await p.send_ext(b"ut_pex", msg)
+
+    # ---------------------------------------------------------------- trackers / DHT
+    async def _announce_once(self, url: str, event: str = "") -> int:
+        from .tracker import announce
+        try:
+            r = await announce(url, self.info_hash, self.client.peer_id, self.client.listen_port,
+                               self.uploaded, self.downloaded, self.left, event,
+                               transports=self.client.transports)
+        except Exception:
+            return 30
+        self.add_peers(r.peers, "tracker")
+        return max(5, min(r.interval, 1800))
+
+    async def _announce_loop(self, url: str) -> None:
+        interval = await self._announce_once(url, "started")
+        while not self._closed:  # keep announcing while seeding too
+            await asyncio.sleep(min(interval, self.client.max_announce_interval))
+            interval = await self._announce_once(url)
+
+    async def _dht_loop(self) -> None:
+        dht = self.client.dht
+        while not self._closed:  # a complete session keeps announcing itself as a seed
+            try:
+                peers = await dht.get_peers(self.info_hash, announce_port=self.client.listen_port)
+                self.add_peers(peers, "dht")
+            except Exception:
+                pass
+            await asyncio.sleep(self.client.dht_interval)
+
+    # ---------------------------------------------------------------- webseeds (BEP-19)
+    def _webseed_url(self, base: str, file_idx: int) -> str:
+        m = self.meta
+        assert m is not None
+        if not m.multi_file:
+            return base + quote(m.name) if base.endswith("/") else base
+        f = m.files[file_idx]
+        return base.rstrip("/") + "/" + "/".join(quote(x) for x in [m.name] + f.path)
+
+    async def _webseed_worker(self, base: str) -> None:
+        failures = 0
+        loop = asyncio.get_running_loop()
+        while not self._closed and not self.done.is_set():
+            run = self.picker.claim_run(self.client.webseed_chunk)
+            if run is None:
+                return
+            first, count = run
+            pieces = list(range(first, first + count))
+            off = first * self.meta.piece_length
+            length = sum(self.meta.piece_size(i) for i in pieces)
+            try:
+                for fd, foff, ln, fidx in self.storage.segments(off, length):
+                    url = self._webseed_url(base, fidx)
+                    flen = self.meta.files[fidx].length
+                    hdrs = [] if (foff == 0 and ln == flen) else \
+                        [("Range", f"bytes={foff}-{foff + ln - 1}")]
+                    r = await self.client.transports.request("GET", url, headers=hdrs,
+                                                             sink=FileSink(fd, foff, ln))
+                    if r.status not in (200, 206) or (r.status == 200 and hdrs) or r.written != ln:
+                        raise TransportError(f"webseed {url}: HTTP {r.status}, {r.written}/{ln} B",
+                                             r.status)
+                    self.webseed_bytes += ln
+                    self.downloaded += ln
+                ok = await loop.run_in_executor(None, self.storage.verify, pieces)
+            except (TransportError, OSError) as e:
+                self.picker.unclaim(pieces)
+                failures += 1
+                self.stats["webseed_failures"] += 1
+                if failures >= self.client.webseed_max_failures:
+                    self._webseed_gave_up(e)
+                    return
+                await asyncio.sleep(min(10.0, 0.2 * (2 ** failures)))
+                continue
+            for i, good in zip(pieces, ok):
+                self.picker.claimed.discard(i)
+                if good:
+                    await self._piece_complete(i)
+                else:
+                    self.stats["hash_fails"] += 1
+            if not all(ok):
+                failures += 1
+                if failures >= self.client.webseed_max_failures:
+                    self._webseed_gave_up(TorrentError("webseed served corrupt pieces"))
+                    return
+
+    def _webseed_gave_up(self, e: BaseException) -> None:
+        self._ws_dead += 1
+        if self._ws_dead >= len(self.webseeds) * self.client.webseed_streams and not self.peers \
+                and not self.known and not self.trackers and self.client.dht is None:
+            self.fail(TorrentError(f"webseed failed: {e}"))
+
+    # ---------------------------------------------------------------- shutdown
+    async def wait(self) -> None:
+        """Wait until complete; raise the session error if one happens first."""
+        d = asyncio.ensure_future(self.done.wait())
+        f = asyncio.ensure_future(self.failed.wait())
+        try:
+            await asyncio.wait({d, f}, return_when=asyncio.FIRST_COMPLETED)
+        finally:
+            d.cancel()
+            f.cancel()
+        if not self.done.is_set() and self.error is not None:
+            raise self.error
+
+    async def close(self) -> None:
+        if self._closed:
+            return
+        self._closed = True
+        for t in self._tasks:
+            t.cancel()
+        for p in list(self.peers.values()):
+            p.close()
+        await asyncio.gather(*self._tasks, return_exceptions=True)
+        if self.storage is not None:
+            self.storage.close()
+        stop = [self._announce_once(t, "stopped") for t in self.trackers]
+        if stop:
+            try:
+                await asyncio.wait_for(asyncio.gather(*stop, return_exceptions=True), 2.0)
+            except asyncio.TimeoutError:
+                pass
+
+    def local_files(self) -> List[str]:
+        return [p for p, _ in self.meta.local_files(self.root)] if self.meta else []
+
+    def total_bytes(self) -> int:
+        return self.meta.total_length if self.meta else 0
+
+
+def webseed_file_size(path: str) -> int:
+    return os.path.getsize(path)

@@ -1,0 +1,141 @@
+"""Piece storage (replaces ``fs-chunk-store`` + ``torrent-piece`` in webtorrent, yarn.lock:1407,3543).
+
+The torrent's files are treated as one concatenated byte space split into pieces. Writes of
+verified pieces go straight to the files with ``pwrite``; webseed bodies are spliced into the
+files by the native transport (``segments()`` gives the fd/offset pairs). Piece verification
+uses the native SHA-1 (``ops.hashing``); a full recheck can run on the MI355X.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+from ..ops import hashing
+from .metainfo import Metainfo
+
+
+class Bitfield:
+    __slots__ = ("n", "bits", "count")
+
+    def __init__(self, n: int, data: Optional[bytes] = None):
+        self.n = n
+        self.bits = bytearray((n + 7) // 8)
+        self.count = 0
+        if data is not None:
+            self.load(data)
+
+    def load(self, data: bytes) -> None:
+        need = (self.n + 7) // 8
+        if len(data) < need:
+            raise ValueError("bitfield too short")
+        self.bits = bytearray(data[:need])
+        spare = need * 8 - self.n
+        if spare and self.bits:
+            self.bits[-1] &= (0xFF << spare) & 0xFF
+        self.count = sum(bin(b).count("1") for b in self.bits)
+
+    def __contains__(self, i: int) -> bool:
+        return bool(self.bits[i >> 3] & (0x80 >> (i & 7)))
+
+    def set(self, i: int) -> bool:
+        m = 0x80 >> (i & 7)
+        if self.bits[i >> 3] & m:
+            return False
+        self.bits[i >> 3] |= m
+        self.count += 1
+        return True
+
+    def clear(self, i: int) -> None:
+        m = 0x80 >> (i & 7)
+        if self.bits[i >> 3] & m:
+            self.bits[i >> 3] &= ~m & 0xFF
+            self.count -= 1
+
+    @property
+    def complete(self) -> bool:
+        return self.count == self.n
+
+    def to_bytes(self) -> bytes:
+        return bytes(self.bits)
+
+    def missing(self) -> List[int]:
+        return [i for i in range(self.n) if i not in self]
+
+
+class Storage:
+    def __init__(self, meta: Metainfo, root: str, preallocate: bool = True):
+        self.meta = meta
+        self.root = root
+        self.paths = meta.local_files(root)
+        self.fds: List[int] = []
+        for p, n in self.paths:
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            fd = os.open(p, os.O_RDWR | os.O_CREAT | getattr(os, "O_CLOEXEC", 0), 0o644)
+            if preallocate and os.fstat(fd).st_size != n:
+                os.ftruncate(fd, n)
+            self.fds.append(fd)
+
+    def piece_range(self, i: int) -> Tuple[int, int]:
+        return i * self.meta.piece_length, self.meta.piece_size(i)
+
+    def segments(self, offset: int, length: int) -> List[Tuple[int, int, int, int]]:
+        """(fd, file_offset, length, file_index) for a storage byte range."""
+        return [(self.fds[idx], foff, ln, idx) for idx, foff, ln in self.meta.file_spans(offset, length)]
+
+    def write(self, offset: int, data: bytes) -> None:
+        mv = memoryview(data)
+        pos = 0
+        for fd, foff, ln, _ in self.segments(offset, len(data)):
+            chunk = mv[pos:pos + ln]
+            while chunk:
+                w = os.pwrite(fd, chunk, foff)
+                chunk = chunk[w:]
+                foff += w
+            pos += ln
+
+    def read(self, offset: int, length: int) -> bytes:
+        out = bytearray()
+        for fd, foff, ln, _ in self.segments(offset, length):
+            while ln > 0:
+                b = os.pread(fd, ln, foff)
+                if not b:
+                    raise OSError("short read from torrent storage")
+                out += b
+                foff += len(b)
+                ln -= len(b)
+        return bytes(out)
+
+    def read_block(self, piece: int, begin: int, length: int) -> bytes:
+        return self.read(piece * self.meta.piece_length + begin, length)
+
+    def verify(self, pieces: Sequence[int], threads: int = 0) -> List[bool]:
+        ok = hashing.verify_pieces(self.paths, self.meta.piece_length, self.meta.pieces,
+                                   which=list(pieces), threads=threads)
+        return [bool(b) for b in ok]
+
+    def recheck(self, backend: str = "auto", threads: int = 0) -> Bitfield:
+        """Verify every piece already on disk (resume after a crash)."""
+        bf = Bitfield(self.meta.num_pieces)
+        if not any(os.path.exists(p) and os.path.getsize(p) for p, _ in self.paths):
+            return bf
+        ok = hashing.verify_pieces(self.paths, self.meta.piece_length, self.meta.pieces,
+                                   threads=threads, backend=backend)
+        for i, v in enumerate(ok):
+            if v:
+                bf.set(i)
+        return bf
+
+    def sync(self) -> None:
+        for fd in self.fds:
+            try:
+                os.fsync(fd)
+            except OSError:
+                pass
+
+    def close(self) -> None:
+        for fd in self.fds:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+        self.fds = []

@@ -1,0 +1,389 @@
+"""BitTorrent subsystem: bencode, metainfo, magnet, trackers, swarm, ut_metadata, webseeds,
+DHT, resume, and the worker-level torrent job with the reference watchdogs."""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import os
+import shutil
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from downloader_amd.torrent.bencode import BencodeError, bdecode, bencode, decode_torrent
+from downloader_amd.torrent.client import TorrentClient
+from downloader_amd.torrent.magnet import Magnet, MagnetError, parse_magnet
+from downloader_amd.torrent.metainfo import MetainfoError, make_torrent, parse_torrent
+from downloader_amd.torrent.tracker import announce
+from downloader_amd.torrent.tracker_server import Tracker
+
+_bval = st.recursive(
+    st.one_of(st.integers(-10**12, 10**12), st.binary(max_size=20)),
+    lambda ch: st.one_of(st.lists(ch, max_size=4),
+                         st.dictionaries(st.binary(max_size=6), ch, max_size=4)),
+    max_leaves=12)
+
+
+@settings(max_examples=60, deadline=None)
+@given(_bval)
+def test_bencode_roundtrip(v):
+    assert bdecode(bencode(v)) == v
+
+
+@pytest.mark.parametrize("bad", [b"i01e", b"i-0e", b"ie", b"5:abc", b"l", b"d1:ae", b"x", b"i1ei2e"])
+def test_bdecode_rejects(bad):
+    with pytest.raises(BencodeError):
+        bdecode(bad)
+
+
+def test_info_span_is_exact():
+    raw = b"d8:announce3:abc4:infod6:lengthi5e4:name1:x12:piece lengthi16384e6:pieces20:" + \
+        b"A" * 20 + b"ee"
+    top, info = decode_torrent(raw)
+    assert info.startswith(b"d6:length") and info.endswith(b"e")
+    assert parse_torrent(raw).info_hash == hashlib.sha1(info).digest()
+
+
+def _tree(root, sizes):
+    data = {}
+    for rel, n in sizes.items():
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        d = os.urandom(n)
+        with open(p, "wb") as f:
+            f.write(d)
+        data[rel] = d
+    return data
+
+
+def test_make_and_parse_multi_file(tmp_path):
+    _tree(tmp_path / "src" / "Show", {"S1/a.mkv": 100_000, "S1/b.mkv": 1, "c.txt": 70_000})
+    t = make_torrent(str(tmp_path / "src" / "Show"), 16384, trackers=["http://t/a", "udp://u:1"],
+                     url_list=["http://ws/"])
+    m = parse_torrent(t)
+    assert m.multi_file and m.name == "Show" and m.total_length == 170_001
+    assert [f.path for f in m.files] == [["S1", "a.mkv"], ["S1", "b.mkv"], ["c.txt"]]
+    assert m.num_pieces == (170_001 + 16383) // 16384
+    assert m.trackers() == ["http://t/a", "udp://u:1"] and m.url_list == ["http://ws/"]
+    lf = m.local_files("/dl")
+    assert lf[0] == ("/dl/Show/S1/a.mkv", 100_000)
+    assert m.file_spans(99_999, 3) == [(0, 99_999, 1), (1, 0, 1), (2, 0, 1)]
+
+
+def test_metainfo_rejects_bad_piece_count():
+    raw = bencode({"info": {"name": "x", "length": 100000, "piece length": 16384,
+                            "pieces": b"A" * 20}})
+    with pytest.raises(MetainfoError):
+        parse_torrent(raw)
+
+
+def test_path_traversal_is_neutralised(tmp_path):
+    raw = bencode({"info": {"name": "..", "piece length": 16384, "pieces": b"A" * 20,
+                            "files": [{"path": ["..", "etc", "passwd"], "length": 5}]}})
+    m = parse_torrent(raw)
+    for p, _ in m.local_files(str(tmp_path)):
+        assert os.path.abspath(p).startswith(str(tmp_path))
+
+
+def test_magnet_parse():
+    ih = bytes(range(20))
+    m = parse_magnet(f"magnet:?xt=urn:btih:{ih.hex()}&dn=My%20Show&tr=udp%3A%2F%2Ft%3A1"
+                     f"&ws=http%3A%2F%2Fw%2F&x.pe=1.2.3.4:5&xl=99")
+    assert m.info_hash == ih and m.name == "My Show" and m.trackers == ["udp://t:1"]
+    assert m.webseeds == ["http://w/"] and m.peers == [("1.2.3.4", 5)] and m.exact_length == 99
+    import base64
+    b32 = base64.b32encode(ih).decode()
+    assert parse_magnet(f"magnet:?xt=urn:btih:{b32}").info_hash == ih
+    assert parse_magnet(Magnet(ih, "n", ["http://t"]).to_uri()).trackers == ["http://t"]
+    with pytest.raises(MagnetError):
+        parse_magnet("magnet:?dn=x")
+
+
+def test_http_and_udp_tracker(run):
+    async def go():
+        tr = await Tracker().start()
+        ih, a, b = b"I" * 20, b"A" * 20, b"B" * 20
+        r1 = await announce(tr.http_url, ih, a, 1111, 0, 0, 10, "started")
+        assert r1.peers == []
+        r2 = await announce(tr.udp_url, ih, b, 2222, 0, 0, 0, "started")
+        assert ("127.0.0.1", 1111) in r2.peers and r2.interval == 5
+        r3 = await announce(tr.http_url, ih, a, 1111, 0, 0, 10)
+        assert ("127.0.0.1", 2222) in r3.peers and r3.seeders == 1
+        await tr.stop()
+    run(go())
+
+
+async def _seed(tmp_path, sizes, piece=32768, **mk):
+    src = tmp_path / "seed"
+    data = _tree(src / "Pack", sizes)
+    raw = make_torrent(str(src / "Pack"), piece, **mk)
+    seeder = await TorrentClient().start()
+    await seeder.add_torrent(parse_torrent(raw), str(src))
+    return raw, data, seeder, src
+
+
+def _check(dst, data, name="Pack"):
+    for rel, d in data.items():
+        with open(os.path.join(dst, name, rel), "rb") as f:
+            assert f.read() == d, rel
+
+
+def test_swarm_download_from_seeder(run, tmp_path):
+    async def go():
+        tr = await Tracker().start()
+        raw, data, seeder, _ = await _seed(tmp_path, {"a.mkv": 700_000, "S1/b.mkv": 123_457},
+                                           trackers=[tr.http_url])
+        leech = await TorrentClient().start()
+        s = await leech.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        await asyncio.wait_for(s.wait(), 30)
+        assert s.progress == 1.0 and s.stats["hash_fails"] == 0
+        _check(tmp_path / "dl", data)
+        await leech.close(); await seeder.close(); await tr.stop()
+    run(go())
+
+
+def test_magnet_metadata_over_peers(run, tmp_path):
+    async def go():
+        raw, data, seeder, _ = await _seed(tmp_path, {"x.mkv": 400_000})
+        m = parse_torrent(raw)
+        leech = await TorrentClient().start()
+        mag = Magnet(m.info_hash, peers=[("127.0.0.1", seeder.listen_port)])
+        s = await leech.add_magnet(parse_magnet(mag.to_uri()), str(tmp_path / "dl"))
+        await asyncio.wait_for(s.wait(), 30)
+        assert s.meta.info_hash == m.info_hash
+        _check(tmp_path / "dl", data)
+        await leech.close(); await seeder.close()
+    run(go())
+
+
+def test_bad_peer_data_is_rejected_and_refetched(run, tmp_path):
+    async def go():
+        raw, data, seeder, src = await _seed(tmp_path, {"x.mkv": 300_000})
+        # corrupt the seeder's file AFTER it verified: it will serve a bad piece 0
+        p = src / "Pack" / "x.mkv"
+        b = bytearray(p.read_bytes())
+        b[10] ^= 0xFF
+        p.write_bytes(bytes(b))
+        good = await TorrentClient().start()
+        gdir = tmp_path / "good"
+        _tree(gdir / "Pack", {})
+        shutil.copytree(src / "Pack", gdir / "Pack", dirs_exist_ok=True)
+        (gdir / "Pack" / "x.mkv").write_bytes(data["x.mkv"])
+        await good.add_torrent(parse_torrent(raw), str(gdir))
+        leech = await TorrentClient().start()
+        s = await leech.add_torrent(parse_torrent(raw), str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", seeder.listen_port),
+                                           ("127.0.0.1", good.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        await leech.close(); await seeder.close(); await good.close()
+    run(go(), timeout=90)
+
+
+def test_webseed_single_and_multi_file(run, tmp_path, origin_cls):
+    async def go():
+        origin = await origin_cls().start()
+        src = tmp_path / "ws"
+        data = _tree(src / "Pack", {"a.mkv": 1_000_003, "dir/b.mkv": 77_777, "dir/c.mp4": 5})
+        for rel, d in data.items():
+            origin.blobs["/seed/Pack/" + rel] = d
+        raw = make_torrent(str(src / "Pack"), 65536, url_list=[origin.url("/seed/")])
+        c = TorrentClient(webseed_chunk=200_000, webseed_streams=3)
+        await c.start()
+        s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        await asyncio.wait_for(s.wait(), 30)
+        _check(tmp_path / "dl", data)
+        assert s.webseed_bytes == sum(len(d) for d in data.values())
+        # single-file torrent with a URL pointing at the file itself
+        one = os.urandom(333_333)
+        (src / "one.mkv").write_bytes(one)
+        origin.blobs["/direct/one.mkv"] = one
+        raw1 = make_torrent(str(src / "one.mkv"), 16384, url_list=[origin.url("/direct/one.mkv")])
+        s1 = await c.add_torrent(parse_torrent(raw1), str(tmp_path / "dl1"))
+        await asyncio.wait_for(s1.wait(), 30)
+        assert (tmp_path / "dl1" / "one.mkv").read_bytes() == one
+        await c.close(); await origin.stop()
+    run(go())
+
+
+def test_resume_rechecks_existing_data(run, tmp_path, origin_cls):
+    async def go():
+        origin = await origin_cls().start()
+        src = tmp_path / "ws"
+        data = _tree(src / "Pack", {"a.mkv": 500_000})
+        origin.blobs["/s/Pack/a.mkv"] = data["a.mkv"]
+        raw = make_torrent(str(src / "Pack"), 16384, url_list=[origin.url("/s/")])
+        dl = tmp_path / "dl" / "Pack"
+        dl.mkdir(parents=True)
+        partial = bytearray(data["a.mkv"])
+        partial[400_000:] = b"\x00" * 100_000
+        (dl / "a.mkv").write_bytes(bytes(partial))
+        c = await TorrentClient().start()
+        s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        have0 = s.have.count
+        await asyncio.wait_for(s.wait(), 30)
+        assert have0 == 400_000 // 16384
+        assert s.webseed_bytes < 150_000
+        _check(tmp_path / "dl", data)
+        await c.close(); await origin.stop()
+    run(go())
+
+
+def test_dht_peer_discovery(run, tmp_path):
+    async def go():
+        from downloader_amd.torrent.dht import DHTNode
+        boot = await DHTNode(host="127.0.0.1").start()
+        nodes = [await DHTNode(host="127.0.0.1", bootstrap=[("127.0.0.1", boot.port)]).start()
+                 for _ in range(6)]
+        ih = hashlib.sha1(b"x").digest()
+        assert await nodes[0].get_peers(ih, announce_port=4242) == []
+        found = await nodes[5].get_peers(ih)
+        assert ("127.0.0.1", 4242) in found
+        # full client path: seeder announces via DHT, leecher finds it with no tracker
+        raw, data, _, src = await _seed(tmp_path, {"d.mkv": 200_000})
+        seeder = TorrentClient(enable_dht=True, dht_bootstrap=[("127.0.0.1", boot.port)])
+        seeder.dht_interval = 0.5
+        await seeder.start()
+        await seeder.add_torrent(parse_torrent(raw), str(src))
+        leech = TorrentClient(enable_dht=True, dht_bootstrap=[("127.0.0.1", boot.port)])
+        leech.dht_interval = 0.5
+        await leech.start()
+        await asyncio.sleep(1.0)
+        s = await leech.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        await asyncio.wait_for(s.wait(), 30)
+        _check(tmp_path / "dl", data)
+        await leech.close(); await seeder.close()
+        for n in nodes + [boot]:
+            await n.close()
+    run(go(), timeout=60)
+
+
+def test_pex_spreads_peers(run, tmp_path):
+    async def go():
+        raw, data, seeder, _ = await _seed(tmp_path, {"p.mkv": 100_000})
+        a = await TorrentClient().start()
+        a.pex_interval = 0.3
+        sa = await a.add_torrent(parse_torrent(raw), str(tmp_path / "a"),
+                                 peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(sa.wait(), 30)
+        b = await TorrentClient().start()
+        sb = await b.add_torrent(parse_torrent(raw), str(tmp_path / "b"),
+                                 peers=[("127.0.0.1", a.listen_port)])
+        await asyncio.wait_for(sb.wait(), 30)
+        for _ in range(30):
+            if ("127.0.0.1", seeder.listen_port) in sb.known:
+                break
+            await asyncio.sleep(0.1)
+        assert ("127.0.0.1", seeder.listen_port) in sb.known
+        await a.close(); await b.close(); await seeder.close()
+    run(go())
+
+
+# ------------------------------------------------------------------ worker-level torrent jobs
+def _worker(make_cfg, s3_ep, **over):
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.service.worker import Worker
+    d = {"torrent_enable_dht": False, "progress_interval_s": 0.05}
+    d.update(over.pop("download", {}))
+    cfg = make_cfg(s3_ep, download=d, **over)
+    return Worker(cfg, broker=MemoryBroker())
+
+
+async def _wait_results(w, n=1, timeout=30.0):
+    for _ in range(int(timeout / 0.02)):
+        if len(w.results) >= n:
+            return
+        await asyncio.sleep(0.02)
+    raise AssertionError(w.results)
+
+
+def test_worker_torrent_over_http_with_webseed(run, tmp_path, make_cfg, origin_cls):
+    """Reference path lib/download.js:143-155: a .torrent URL chains to the torrent backend."""
+    async def go():
+        from downloader_amd.models import api, keys
+        from downloader_amd.s3.fake_server import FakeS3
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src"
+        data = _tree(src / "My Show", {"Season 1/e1.mkv": 400_000, "Season 1/e2.mkv": 300_000,
+                                       "Extras/x.mkv": 1000, "readme.txt": 10})
+        for rel, d in data.items():
+            origin.blobs["/ws/My Show/" + rel] = d
+        raw = make_torrent(str(src / "My Show"), 32768, url_list=[origin.url("/ws/")])
+        origin.blobs["/t/show.torrent"] = raw
+        w = _worker(make_cfg, ep)
+        await w.start(health=False)
+        await w.submit(api.make_download("tj1", "http", origin.url("/t/show.torrent"), "TV"))
+        await _wait_results(w)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        for rel in ("Season 1/e1.mkv", "Season 1/e2.mkv"):
+            assert s3.get("triton-staging", keys.object_key("tj1", rel)) == data[rel]
+        assert s3.get("triton-staging", keys.object_key("tj1", "x.mkv")) is None  # extras dropped
+        prog = w.telemetry.progress_of("tj1")
+        assert prog[0] == 0 and 50 in prog and prog[-1] == 100
+        assert all(p <= 50 for p in prog[:prog.index(50)])
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_worker_magnet_job(run, tmp_path, make_cfg):
+    async def go():
+        from downloader_amd.models import api, keys
+        from downloader_amd.s3.fake_server import FakeS3
+        s3 = FakeS3()
+        ep = await s3.start()
+        tr = await Tracker().start()
+        raw, data, seeder, _ = await _seed(tmp_path, {"movie.mkv": 250_000}, trackers=[tr.http_url])
+        m = parse_torrent(raw)
+        w = _worker(make_cfg, ep)
+        await w.start(health=False)
+        await w.submit(api.make_download("tj2", "torrent", Magnet(m.info_hash, "Pack",
+                                                                  [tr.udp_url]).to_uri()))
+        await _wait_results(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert s3.get("triton-staging", keys.object_key("tj2", "movie.mkv")) == data["movie.mkv"]
+        await w.stop(); await seeder.close(); await tr.stop(); await s3.stop()
+    run(go())
+
+
+def test_worker_metadata_stall_fails_job(run, tmp_path, make_cfg):
+    async def go():
+        from downloader_amd.models import api
+        from downloader_amd.s3.fake_server import FakeS3
+        s3 = FakeS3()
+        ep = await s3.start()
+        w = _worker(make_cfg, ep, download={"torrent_metadata_timeout_s": 0.3},
+                    broker={"max_retries": 0})
+        await w.start(health=False)
+        await w.submit(api.make_download("tj3", "torrent", Magnet(b"\x01" * 20).to_uri()))
+        await _wait_results(w)
+        assert w.results[0].outcome == "dead"
+        assert "Metadata fetch stalled" in w.results[0].error
+        assert w.telemetry.statuses_of("tj3") == [2, 6]
+        await w.stop(); await s3.stop()
+    run(go())
+
+
+def test_worker_progress_stall_acks(run, tmp_path, make_cfg, origin_cls):
+    """A torrent whose only source never delivers -> ERRDLSTALL -> acked and dropped."""
+    async def go():
+        from downloader_amd.models import api
+        from downloader_amd.s3.fake_server import FakeS3
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src"
+        _tree(src / "P", {"a.mkv": 100_000})
+        raw = make_torrent(str(src / "P"), 16384, url_list=[origin.url("/missing/")])
+        origin.blobs["/t.torrent"] = raw
+        w = _worker(make_cfg, ep, download={"torrent_stall_timeout_s": 0.4})
+        await w.start(health=False)
+        await w.submit(api.make_download("tj4", "http", origin.url("/t.torrent")))
+        await _wait_results(w)
+        assert w.results[0].outcome == "stalled"
+        assert w.telemetry.statuses_of("tj4") == [2]
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
