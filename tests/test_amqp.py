@@ -1,0 +1,232 @@
+"""AMQP 0-9-1 codec, client and bundled broker: prefetch, ack/nack, redelivery, confirms,
+reconnect, and the full worker over AMQP."""
+from __future__ import annotations
+
+import asyncio
+import os
+from decimal import Decimal
+
+import pytest
+
+from downloader_amd.broker import amqp_codec as C
+from downloader_amd.broker.amqp import AmqpBroker, Connection, parse_url
+from downloader_amd.broker.server import BrokerServer
+
+
+def test_field_table_roundtrip():
+    t = {"a": 1, "b": "x", "c": True, "d": 1.5, "e": b"\x00\x01", "f": {"g": [1, "two", None]},
+         "h": Decimal("1.25"), "i": -7}
+    r = C.Reader(C.enc_table(t))
+    assert r.table() == t
+
+
+def test_method_and_bits_roundtrip():
+    f = C.method_frame(3, C.QUEUE_DECLARE, 0, "q", False, True, False, True, False, {"x": 1})
+    assert f[0] == C.FRAME_METHOD and f[-1] == C.FRAME_END
+    m, a = C.decode_method(f[7:-1])
+    assert m == C.QUEUE_DECLARE and a == [0, "q", False, True, False, True, False, {"x": 1}]
+    m, a = C.decode_method(C.method_frame(1, C.BASIC_NACK, 2**40, True, False)[7:-1])
+    assert a == [2**40, True, False]
+
+
+def test_properties_roundtrip():
+    p = C.Properties(content_type="x/y", headers={"x-attempt": 2}, delivery_mode=2,
+                     timestamp=123, message_id="m")
+    q = C.Properties.decode(C.Reader(p.encode()))
+    assert q == p
+
+
+def test_parse_url():
+    assert parse_url("amqp://u:p%40ss@h:1234/v%2Fx") == ("h", 1234, "u", "p@ss", "v/x")
+    assert parse_url("amqp://h") == ("h", 5672, "guest", "guest", "/")
+
+
+def test_publish_consume_ack_nack_redelivery(run):
+    async def go():
+        srv = await BrokerServer().start()
+        b = AmqpBroker(srv.url)
+        await b.connect()
+        await b.declare("q")
+        got = []
+        ev = asyncio.Event()
+
+        async def h(d):
+            got.append((d.body, d.redelivered, d.headers.get("x-attempt")))
+            if len(got) == 1:
+                await d.nack(requeue=True)
+            else:
+                await d.ack()
+                ev.set()
+        await b.publish("q", b"hello", {"x-attempt": 3})
+        await b.consume("q", h, prefetch=1)
+        await asyncio.wait_for(ev.wait(), 5)
+        assert got == [(b"hello", False, 3), (b"hello", True, 3)]
+        assert srv.depth("q") == 0
+        await b.close(); await srv.stop()
+    run(go())
+
+
+def test_prefetch_bounds_unacked(run):
+    async def go():
+        srv = await BrokerServer().start()
+        b = AmqpBroker(srv.url)
+        await b.connect()
+        await b.declare("p")
+        held = []
+        inflight = {"n": 0, "max": 0}
+        release = asyncio.Event()
+
+        async def h(d):
+            inflight["n"] += 1
+            inflight["max"] = max(inflight["max"], inflight["n"])
+            held.append(d)
+            await release.wait()
+            inflight["n"] -= 1
+            await d.ack()
+        await b.consume("p", h, prefetch=2)
+        for i in range(6):
+            await b.publish("p", b"%d" % i)
+        await asyncio.sleep(0.3)
+        assert len(held) == 2 and srv.depth("p") == 4
+        release.set()
+        for _ in range(100):
+            if len(held) == 6:
+                break
+            await asyncio.sleep(0.02)
+        assert len(held) == 6 and inflight["max"] == 2
+        await b.close(); await srv.stop()
+    run(go())
+
+
+def test_round_robin_two_consumers(run):
+    async def go():
+        srv = await BrokerServer().start()
+        b1, b2 = AmqpBroker(srv.url), AmqpBroker(srv.url)
+        await b1.connect(); await b2.connect()
+        seen = {1: 0, 2: 0}
+
+        def mk(k):
+            async def h(d):
+                seen[k] += 1
+                await asyncio.sleep(0.01)
+                await d.ack()
+            return h
+        await b1.consume("rr", mk(1), 1)
+        await b2.consume("rr", mk(2), 1)
+        for i in range(20):
+            await b1.publish("rr", b"x")
+        for _ in range(200):
+            if seen[1] + seen[2] == 20:
+                break
+            await asyncio.sleep(0.02)
+        assert seen[1] + seen[2] == 20 and seen[1] >= 5 and seen[2] >= 5
+        await b1.close(); await b2.close(); await srv.stop()
+    run(go())
+
+
+def test_unacked_requeued_when_consumer_dies(run):
+    async def go():
+        srv = await BrokerServer().start()
+        b1 = AmqpBroker(srv.url)
+        await b1.connect()
+        started = asyncio.Event()
+
+        async def stuck(d):
+            started.set()
+            await asyncio.sleep(3600)
+        await b1.consume("d", stuck, 1)
+        await b1.publish("d", b"job")
+        await asyncio.wait_for(started.wait(), 5)
+        await b1.close()
+        b2 = AmqpBroker(srv.url)
+        await b2.connect()
+        await asyncio.sleep(0.1)
+        d = await b2.get("d")
+        assert d is not None and d.body == b"job" and d.redelivered
+        await d.ack()
+        assert await b2.get("d") is None
+        await b2.close(); await srv.stop()
+    run(go())
+
+
+def test_reconnect_resubscribes(run):
+    async def go():
+        srv = await BrokerServer().start()
+        b = AmqpBroker(srv.url, reconnect_delay=0.05)
+        await b.connect()
+        got = []
+
+        async def h(d):
+            got.append(d.body)
+            await d.ack()
+        await b.consume("r", h, 1)
+        await b.publish("r", b"1")
+        for _ in range(50):
+            if got:
+                break
+            await asyncio.sleep(0.02)
+        srv.drop_connections()
+        await asyncio.sleep(0.3)
+        await b.publish("r", b"2")
+        for _ in range(100):
+            if len(got) == 2:
+                break
+            await asyncio.sleep(0.02)
+        assert got == [b"1", b"2"] and b.reconnects >= 1
+        await b.close(); await srv.stop()
+    run(go())
+
+
+def test_auth_refused(run):
+    async def go():
+        srv = await BrokerServer().start()
+        with pytest.raises(C.AMQPError):
+            await Connection(f"amqp://bad:creds@127.0.0.1:{srv.port}/").connect()
+        await srv.stop()
+    run(go())
+
+
+def test_large_message_spans_frames(run):
+    async def go():
+        srv = await BrokerServer(frame_max=4096).start()
+        b = AmqpBroker(srv.url)
+        await b.connect()
+        await b.declare("big")
+        body = os.urandom(100_000)
+        await b.publish("big", body)
+        d = await b.get("big")
+        assert d.body == body
+        await d.ack()
+        await b.close(); await srv.stop()
+    run(go())
+
+
+def test_worker_over_amqp(run, make_cfg, origin_cls):
+    async def go():
+        from downloader_amd.models import api, keys
+        from downloader_amd.s3.fake_server import FakeS3
+        from downloader_amd.service.worker import Worker
+        srv = await BrokerServer().start()
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        origin.blobs["/a.mkv"] = os.urandom(50_000)
+        cfg = make_cfg(ep, broker={"backend": "amqp", "url": srv.url})
+        w = Worker(cfg)
+        await w.start(health=False)
+        client = AmqpBroker(srv.url)
+        await client.connect()
+        await client.publish("v1.download", api.encode(api.make_download("aj", "http", origin.url("/a.mkv"))))
+        for _ in range(250):
+            if w.results:
+                break
+            await asyncio.sleep(0.02)
+        assert w.results[0].outcome == "staged"
+        d = await client.get("v1.convert")
+        assert api.decode(api.Convert, d.body).media.id == "aj"
+        assert "traceparent" in d.headers
+        st = await client.get("v1.telemetry.status")
+        assert api.decode(api.TelemetryStatus, st.body).status == 2
+        assert s3.get("triton-staging", keys.object_key("aj", "a.mkv")) == origin.blobs["/a.mkv"]
+        await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()
+    run(go())
