@@ -1,0 +1,165 @@
+"""Command line (the reference's process entrypoint, index.js:1-40, plus operational tools).
+
+  python -m downloader_amd worker      [--config F]   consume v1.download (index.js init())
+  python -m downloader_amd supervisor  -n 8           N workers on one host, auto-restart
+  python -m downloader_amd broker      [--port 5672]  bundled AMQP 0-9-1 broker
+  python -m downloader_amd submit      ID SOURCE URI [--type TV]   publish an api.Download
+  python -m downloader_amd make-torrent PATH -o F [--webseed URL] [--tracker URL]
+  python -m downloader_amd verify      TORRENT DIR [--backend gpu|cpu|auto]
+  python -m downloader_amd config                     print the effective config
+
+Worker lifecycle mirrors index.js: logger + tracer, load config (named ``downloader``; the
+reference's ``'converter'`` is accepted as an alias), start the service, and on SIGINT/SIGTERM
+or an unhandled error run the termination handler and exit 0 when idle / 1 when jobs were in
+flight (lib/main.js:197-204; App. A #2 fixed so that "idle" is real).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import signal
+import sys
+import time
+
+
+def _worker(args) -> int:
+    from .service.worker import Worker
+    from .utils.config import load_config
+    from .utils.log import get_logger
+    log = get_logger("index.py")
+    cfg = load_config(path=args.config or None)
+    if args.mode:
+        cfg.mode = args.mode
+        cfg.apply_mode()
+
+    async def main() -> int:
+        w = Worker(cfg, logger=get_logger("main"))
+        await w.start()
+        log.info("initialized")
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(sig, stop.set)
+
+        def on_error(loop, ctx):
+            log.error("Unhandled exception", str(ctx.get("exception") or ctx.get("message")))
+            stop.set()
+        loop.set_exception_handler(on_error)
+        await stop.wait()
+        code = await w.stop(drain_timeout=args.drain_timeout)
+        log.info("exiting", code=code)
+        return code
+    return asyncio.run(main())
+
+
+def _supervisor(args) -> int:
+    from .parallel.supervisor import Supervisor, worker_argv
+    extra = ["--mode", args.mode] if args.mode else []
+    sup = Supervisor(args.n, worker_argv(args.config, extra), cpus_per_worker=args.cpus_per_worker,
+                     base_port=args.base_port)
+    return sup.run_forever()
+
+
+def _broker(args) -> int:
+    from .broker.server import run_broker
+    try:
+        asyncio.run(run_broker(args.host, args.port))
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
+def _submit(args) -> int:
+    from .broker.amqp import AmqpBroker
+    from .models import api
+    from .utils.config import load_config
+    from .utils.dynamics import dyn
+    cfg = load_config(path=args.config or None)
+
+    async def main() -> None:
+        b = AmqpBroker(cfg.broker.url or dyn("rabbitmq"))
+        await b.connect()
+        msg = api.make_download(args.id, args.source, args.uri, args.type, args.creator)
+        await b.publish(cfg.broker.download_queue, api.encode(msg))
+        await b.close()
+    asyncio.run(main())
+    return 0
+
+
+def _make_torrent(args) -> int:
+    from .torrent.metainfo import make_torrent, parse_torrent
+    raw = make_torrent(args.path, args.piece_length, args.tracker or [], args.webseed or [])
+    with open(args.output, "wb") as f:
+        f.write(raw)
+    m = parse_torrent(raw)
+    print(json.dumps({"info_hash": m.info_hash.hex(), "pieces": m.num_pieces,
+                      "piece_length": m.piece_length, "bytes": m.total_length}))
+    return 0
+
+
+def _verify(args) -> int:
+    from .ops import hashing
+    from .torrent.metainfo import parse_torrent
+    with open(args.torrent, "rb") as f:
+        m = parse_torrent(f.read())
+    files = m.local_files(args.dir)
+    t0 = time.perf_counter()
+    ok = hashing.verify_pieces(files, m.piece_length, m.pieces, backend=args.backend)
+    dt = time.perf_counter() - t0
+    good = sum(ok)
+    print(json.dumps({"pieces": len(ok), "good": good, "seconds": round(dt, 4),
+                      "GBps": round(m.total_length / dt / 1e9, 3) if dt else None,
+                      "backend": hashing.choose_backend(args.backend, m.total_length, len(ok))}))
+    return 0 if good == len(ok) else 1
+
+
+def _config(args) -> int:
+    from .utils.config import load_config
+    print(load_config(path=args.config or None).model_dump_json(indent=2))
+    return 0
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(prog="downloader_amd")
+    sub = p.add_subparsers(dest="cmd", required=True)
+    w = sub.add_parser("worker")
+    w.add_argument("--config", default="")
+    w.add_argument("--mode", choices=["tuned", "reference"], default="")
+    w.add_argument("--drain-timeout", type=float, default=30.0)
+    s = sub.add_parser("supervisor")
+    s.add_argument("-n", type=int, default=os.cpu_count() or 1)
+    s.add_argument("--config", default="")
+    s.add_argument("--mode", choices=["tuned", "reference"], default="")
+    s.add_argument("--cpus-per-worker", type=int, default=0)
+    s.add_argument("--base-port", type=int, default=0)
+    b = sub.add_parser("broker")
+    b.add_argument("--host", default="0.0.0.0")
+    b.add_argument("--port", type=int, default=5672)
+    su = sub.add_parser("submit")
+    su.add_argument("id")
+    su.add_argument("source", choices=["http", "torrent", "file", "bucket"])
+    su.add_argument("uri")
+    su.add_argument("--type", default="MOVIE", choices=["MOVIE", "TV"])
+    su.add_argument("--creator", default="")
+    su.add_argument("--config", default="")
+    mt = sub.add_parser("make-torrent")
+    mt.add_argument("path")
+    mt.add_argument("-o", "--output", required=True)
+    mt.add_argument("--piece-length", type=int, default=0)
+    mt.add_argument("--tracker", action="append")
+    mt.add_argument("--webseed", action="append")
+    v = sub.add_parser("verify")
+    v.add_argument("torrent")
+    v.add_argument("dir")
+    v.add_argument("--backend", default="auto", choices=["auto", "cpu", "gpu"])
+    c = sub.add_parser("config")
+    c.add_argument("--config", default="")
+    args = p.parse_args(argv)
+    return {"worker": _worker, "supervisor": _supervisor, "broker": _broker, "submit": _submit,
+            "make-torrent": _make_torrent, "verify": _verify, "config": _config}[args.cmd](args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -394,8 +394,9 @@ class _AmqpDelivery(Delivery):
 
 class AmqpBroker(Broker):
     def __init__(self, url: str, heartbeat: int = 30, reconnect_delay: float = 1.0,
-                 max_reconnect_delay: float = 30.0, metrics=None):
+                 max_reconnect_delay: float = 30.0, metrics=None, connect_retry_s: float = 0.0):
         self.url = url
+        self.connect_retry_s = connect_retry_s
         self.heartbeat = heartbeat
         self.reconnect_delay = reconnect_delay
         self.max_reconnect_delay = max_reconnect_delay
@@ -415,10 +416,21 @@ class AmqpBroker(Broker):
         self.reconnects = 0
 
     async def connect(self) -> None:
-        async with self._lock:
-            if self.connected:
-                return
-            await self._open()
+        deadline = asyncio.get_running_loop().time() + self.connect_retry_s
+        delay = self.reconnect_delay
+        while True:
+            try:
+                async with self._lock:
+                    if self.connected:
+                        return
+                    await self._open()
+                break
+            except (OSError, C.AMQPError, asyncio.TimeoutError, ConnectionError):
+                # amqp-connection-manager semantics: keep trying while the broker comes up
+                if asyncio.get_running_loop().time() + delay > deadline:
+                    raise
+                await asyncio.sleep(delay)
+                delay = min(self.max_reconnect_delay, delay * 2)
         self._watch = asyncio.get_running_loop().create_task(self._watchdog())
 
     async def _open(self) -> None:

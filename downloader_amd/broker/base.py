@@ -97,4 +97,5 @@ def make_broker(cfg, metrics=None) -> Broker:
     from .amqp import AmqpBroker
     url = cfg.broker.url or dyn("rabbitmq")
     return AmqpBroker(url, heartbeat=cfg.broker.heartbeat_s,
-                      reconnect_delay=cfg.broker.reconnect_delay_s, metrics=metrics)
+                      reconnect_delay=cfg.broker.reconnect_delay_s, metrics=metrics,
+                      connect_retry_s=cfg.broker.connect_retry_s)

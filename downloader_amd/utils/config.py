@@ -65,6 +65,7 @@ class BrokerConfig(BaseModel):
     retry_backoff_max_s: float = 30.0
     heartbeat_s: int = 30
     reconnect_delay_s: float = 1.0
+    connect_retry_s: float = 60.0               # keep retrying the first connect this long
 
 
 class TelemetryConfig(BaseModel):

@@ -1,0 +1,91 @@
+"""Multi-process: the supervisor runs N worker processes (CLI entrypoint) against the bundled
+AMQP broker; jobs are spread across workers; SIGTERM drains them cleanly. Plus the bench
+contract on 2 ranks over gloo (torch.distributed.run)."""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.slow
+def test_supervisor_two_workers_over_amqp(run, tmp_path, origin_cls):
+    async def go():
+        from downloader_amd.broker.amqp import AmqpBroker
+        from downloader_amd.broker.server import BrokerServer
+        from downloader_amd.models import api, keys
+        from downloader_amd.parallel.supervisor import Supervisor, worker_argv
+        from downloader_amd.s3.fake_server import FakeS3
+        srv = await BrokerServer().start()
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error",
+                   STAGER_BROKER__URL=srv.url, STAGER_BROKER__BACKEND="amqp",
+                   STAGER_S3__ENDPOINT=ep, STAGER_INSTANCE__DOWNLOAD_PATH=str(tmp_path / "dl"),
+                   STAGER_HEALTH__ENABLED="false", STAGER_DOWNLOAD__TORRENT_ENABLE_DHT="false",
+                   STAGER_CONCURRENCY="1")
+        sup = Supervisor(2, worker_argv(), env=env)
+        sup.start()
+        client = AmqpBroker(srv.url)
+        await client.connect()
+        await client.declare("v1.download")   # unroutable publishes are dropped, like RabbitMQ
+        n = 8
+        for i in range(n):
+            origin.blobs[f"/m{i}.mkv"] = os.urandom(30_000 + i)
+            await client.publish("v1.download", api.encode(
+                api.make_download(f"mp{i}", "http", origin.url(f"/m{i}.mkv"))))
+        got = []
+        for _ in range(1500):
+            d = await client.get("v1.convert")
+            if d is not None:
+                got.append(api.decode(api.Convert, d.body).media.id)
+                await d.ack()
+                if len(got) == n:
+                    break
+            else:
+                await asyncio.sleep(0.02)
+        assert sorted(got) == sorted(f"mp{i}" for i in range(n))
+        for i in range(n):
+            assert s3.get("triton-staging", keys.object_key(f"mp{i}", f"m{i}.mkv")) == \
+                origin.blobs[f"/m{i}.mkv"]
+        # both workers consumed (prefetch=1 round-robin)
+        assert len(srv.queues["v1.download"].consumers) == 2
+        codes = await asyncio.get_running_loop().run_in_executor(None, sup.stop)
+        assert codes == [0, 0]
+        await client.close(); await srv.stop(); await s3.stop(); await origin.stop()
+    run(go(), timeout=120)
+
+
+@pytest.mark.slow
+def test_bench_contract_two_ranks_gloo(tmp_path):
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    j = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in j
+    assert j["n_gpus"] == 2 and j["steps"] == 2 and j["value"] > 0
+    assert j["config"]["jobs_timed"] == 4
+
+
+def test_bench_single_rank_defaults_are_valid(tmp_path):
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
+                        "--warmup", "1", "--size-mb", "2"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["n_gpus"] == 1 and j["higher_is_better"] is True and j["scaling"] == "weak"
