@@ -4,7 +4,9 @@
 BASELINE.json names the metric "MB/s staged end-to-end (download->S3) + p50 job latency at
 1/2/4/8 workers" and config 2 "100x100 MB HTTP URLs, N concurrent workers -> MinIO multipart".
 One rank = one worker process (the reference's scaling unit: one consumer per container,
-SURVEY §2.6). One "step" = every worker stages one 100 MB random-byte media blob:
+SURVEY §2.6). One "step" = every worker stages a batch of ``--jobs-per-step`` 100 MB
+random-byte media blobs (default 8; like a training batch, it keeps the timed region long
+enough to be stable), each job being:
 HTTP GET from the origin -> staging dir on disk -> media selection -> multipart PUT to the
 S3 endpoint -> done marker -> api.Convert published -> ack. Weak scaling: per-worker work is
 fixed as N grows.
@@ -39,8 +41,14 @@ def parse() -> argparse.Namespace:
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--size-mb", type=float, default=100.0, help="object size in MB (1e6 B)")
     p.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
-    p.add_argument("--concurrency", type=int, default=2, help="jobs in flight per worker")
+    p.add_argument("--concurrency", type=int, default=4, help="jobs in flight per worker")
+    p.add_argument("--jobs-per-step", type=int, default=8, help="jobs per worker per step")
     p.add_argument("--stage-dir", default="", help="download_path (default: a temp dir)")
+    p.add_argument("--http-streams", type=int, default=0, help="override download.http_streams")
+    p.add_argument("--part-mb", type=int, default=0, help="override s3.part_size (MiB)")
+    p.add_argument("--inflight-parts", type=int, default=0, help="override s3.max_inflight_parts")
+    p.add_argument("--staging", choices=["stream", "disk"], default="stream",
+                   help="stream: single-file HTTP jobs relay origin->S3; disk: stage on disk first")
     p.add_argument("--compare-reference", action="store_true",
                    help="also time reference-equivalent mode and report the ratio")
     return p.parse_args()
@@ -121,14 +129,24 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
     from downloader_amd.utils.config import load_config
 
     size = int(args.size_mb * 1e6)
-    cfg = load_config(overrides={
+    over = {
         "mode": mode,
         "concurrency": args.concurrency,
         "instance": {"download_path": stage_root},
         "s3": {"endpoint": endpoint},
+        "download": {},
         "broker": {"backend": "memory"},
         "health": {"enabled": False},
-    })
+    }
+    if mode == "tuned":
+        if args.http_streams:
+            over["download"]["http_streams"] = args.http_streams
+        if args.part_mb:
+            over["s3"]["part_size"] = args.part_mb << 20
+        if args.inflight_parts:
+            over["s3"]["max_inflight_parts"] = args.inflight_parts
+        over["download"]["stream_http"] = args.staging == "stream"
+    cfg = load_config(overrides=over, env={})
     worker = Worker(cfg, broker=MemoryBroker())
     await worker.start(health=False)
     host, port = endpoint.split(":")
@@ -136,14 +154,15 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
     def url(name, sz, seed):
         return f"http://{host}:{port}/media/{name}?size={sz}&seed={seed}"
 
-    _, wres = await run_phase(worker, url, dist.rank, 0, args.warmup, size, mode)
+    B = args.jobs_per_step
+    _, wres = await run_phase(worker, url, dist.rank, 0, args.warmup * B, size, mode)
     bad = [r for r in wres if r.outcome != "staged"]
     if bad:
         raise RuntimeError(f"warmup job failed: {bad[0]}")
     dist.barrier()
     cuda_sync()
     t0 = time.perf_counter()
-    dt, res = await run_phase(worker, url, dist.rank, args.warmup, args.steps, size, mode)
+    dt, res = await run_phase(worker, url, dist.rank, args.warmup * B, args.steps * B, size, mode)
     cuda_sync()
     t1 = time.perf_counter()
     bad = [r for r in res if r.outcome != "staged"]
@@ -208,14 +227,16 @@ def main() -> int:
             "p50_job_latency_s": round(tuned["p50"], 4),
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
+            "staging": args.staging if args.mode == "tuned" else "disk",
             "concurrency_per_worker": args.concurrency if args.mode == "tuned" else 1,
             "config": {
                 "model": "BASELINE.json config 2: HTTP media blob -> S3 multipart staging",
-                "global_batch": n,
+                "global_batch": n * args.jobs_per_step,
+                "jobs_per_step_per_worker": args.jobs_per_step,
                 "seq_len": int(args.size_mb * 1e6),
                 "parallelism": f"workers{n}",
                 "object_bytes": int(args.size_mb * 1e6),
-                "jobs_timed": n * args.steps,
+                "jobs_timed": n * args.steps * args.jobs_per_step,
             },
         }
         if ref is not None:

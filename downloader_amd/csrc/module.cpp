@@ -4,6 +4,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+
 #include "native.h"
 
 namespace py = pybind11;
@@ -234,6 +238,45 @@ PYBIND11_MODULE(_native, m) {
           py::arg("max_bytes") = (int64_t)1 << 50, py::arg("progress") = nullptr,
           py::arg("max_err_body") = (int64_t)1 << 20,
           "Send a body-less request; a 2xx body is spliced into `fd` at `offset`.")
+      .def(
+          "relay_to",
+          [](HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
+             int64_t length, Progress* prog, int64_t max_body) {
+            std::string gh = get_head, ph = put_head;
+            ResponseHead g, p;
+            std::string gerr, pbody;
+            int64_t moved = 0;
+            {
+              py::gil_scoped_release rel;
+              src.send_request(gh, nullptr, 0);
+              g = src.read_head();
+              bool ok = (g.status == 200 || g.status == 206) && !g.chunked && g.content_length == length;
+              if (!ok) {
+                gerr = src.read_body(g, 1 << 20);
+              } else {
+                int cork = 1;
+                setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+                dst.send_raw(ph);
+                moved = src.relay_body_to(dst, length, prog);
+                cork = 0;
+                setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+                p = dst.read_head();
+                pbody = dst.read_body(p, max_body);
+              }
+            }
+            py::dict d;
+            d["get"] = head_to_dict(g);
+            d["get_body"] = py::bytes(gerr);
+            d["put"] = p.status ? (py::object)head_to_dict(p) : py::none();
+            d["put_body"] = py::bytes(pbody);
+            d["moved"] = moved;
+            return d;
+          },
+          py::arg("get_head"), py::arg("dst"), py::arg("put_head"), py::arg("length"),
+          py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)1 << 20,
+          "GET on this connection and stream exactly `length` body bytes as the body of the "
+          "PUT sent on `dst` (socket->pipe->socket splice). The GET must answer 200/206 with "
+          "that Content-Length, otherwise nothing is sent on `dst`.")
       .def("close", &HttpConn::close)
       .def_property_readonly("is_open", &HttpConn::is_open)
       .def_property_readonly("reusable", &HttpConn::reusable)

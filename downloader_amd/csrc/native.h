@@ -101,6 +101,12 @@ class HttpConn {
                           Progress* prog);
   // Drain and discard a body (keeps the connection reusable).
   void discard_body(const ResponseHead& h);
+  // Move exactly `n` body bytes of the response being read on *this to `dst`'s socket
+  // (bytes already buffered first, then socket -> pipe -> socket with splice).
+  int64_t relay_body_to(HttpConn& dst, int64_t n, Progress* prog);
+  void send_raw(const std::string& s) { send_all((const uint8_t*)s.data(), s.size()); }
+  int fd() const { return fd_; }
+  void mark_unusable() { reusable_ = false; }
   void close();
   bool is_open() const { return fd_ >= 0; }
   bool reusable() const { return fd_ >= 0 && reusable_; }

@@ -421,6 +421,59 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
   return written;
 }
 
+int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog) {
+  int64_t moved = 0;
+  if (rpos_ < rend_) {
+    int64_t k = std::min<int64_t>(n, (int64_t)(rend_ - rpos_));
+    dst.send_all(rbuf_.data() + rpos_, (size_t)k);
+    rpos_ += (size_t)k;
+    moved += k;
+    if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
+  }
+  if (moved == n) return moved;
+  if (pipe_[0] < 0) {
+    if (pipe2(pipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
+    int got = fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
+    pipe_sz_ = got > 0 ? (size_t)got : 65536;
+  }
+  while (moved < n) {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("cancelled");
+    }
+    size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)pipe_sz_);
+    ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+    if (in < 0) {
+      if (errno == EINTR) continue;
+      reusable_ = false;
+      dst.reusable_ = false;
+      if (errno == EAGAIN) throw IoError("recv timeout");
+      throw IoError(errstr("splice(src)"));
+    }
+    if (in == 0) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("source closed mid-body");
+    }
+    ssize_t left = in;
+    while (left > 0) {
+      ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)left,
+                             SPLICE_F_MOVE | SPLICE_F_MORE);
+      if (out < 0) {
+        if (errno == EINTR) continue;
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError(errstr("splice(dst)"));
+      }
+      left -= out;
+    }
+    moved += in;
+    if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
+  }
+  return moved;
+}
+
 void HttpConn::discard_body(const ResponseHead& h) {
   if (h.chunked || h.content_length > 0) {
     read_body(h, (int64_t)1 << 40);

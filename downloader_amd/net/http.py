@@ -208,6 +208,55 @@ class NativeTransport(Transport):
                 nprog.cancel()
             raise
 
+    def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
+               length: int, nprog) -> Tuple[Response, Optional[Response], int]:
+        _, sh, sp, spath = split_host(src_url)
+        _, dh, dp, dpath = split_host(dst_url)
+        get_head = _build_head("GET", sh if sp == 80 else f"{sh}:{sp}", spath, src_headers, None)
+        put_head = _build_head("PUT", dh if dp == 80 else f"{dh}:{dp}", dpath, dst_headers, length)
+        src, _ = self._acquire(sh, sp)
+        try:
+            dst, _ = self._acquire(dh, dp)
+        except BaseException:
+            self._release(src)
+            raise
+        try:
+            d = src.relay_to(get_head, dst, put_head, length, nprog)
+        except RuntimeError as e:
+            src.close()
+            dst.close()
+            raise TransportError(f"relay {spath} -> {dpath}: {e}") from e
+        self._release(src)
+        self._release(dst)
+        g = d["get"]
+        get = Response(g["status"], list(g["headers"]), d["get_body"], 0, g.get("reason", ""))
+        put = None
+        if d["put"] is not None:
+            p = d["put"]
+            put = Response(p["status"], list(p["headers"]), d["put_body"], 0, p.get("reason", ""))
+        return get, put, d["moved"]
+
+    async def relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
+                    length: int, progress: Optional[Progress] = None
+                    ) -> Tuple[Response, Optional[Response], int]:
+        """GET ``src_url`` and stream exactly ``length`` body bytes as the body of a PUT to
+        ``dst_url`` without touching user space (socket -> pipe -> socket splice). The PUT is
+        only sent when the GET answers 2xx with exactly that Content-Length."""
+        nprog = None
+        if progress is not None:
+            if progress.native is None:
+                progress.native = self._n.Progress()
+            nprog = progress.native
+        loop = asyncio.get_running_loop()
+        fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
+                                   dst_headers, length, nprog)
+        try:
+            return await asyncio.shield(fut)
+        except asyncio.CancelledError:
+            if nprog is not None:
+                nprog.cancel()
+            raise
+
     async def close(self) -> None:
         with self._lock:
             conns = [c for v in self._pool.values() for c in v]

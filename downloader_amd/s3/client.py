@@ -294,6 +294,78 @@ class S3Client:
                                           [(o, ln) for _, o, ln in cand], "md5")
         return {n: remote[n][0] for (n, _, _), d in zip(cand, md5s) if d.hex() == remote[n][0]}
 
+    # ------------------------------------------------------------------ streaming relay
+    def can_relay(self, src_url: str) -> bool:
+        nt = getattr(self.t, "native", None)
+        return nt is not None and src_url.startswith("http://") and self.base.startswith("http://")
+
+    def _signed(self, method: str, bucket: str, key: str, query: Sequence[Tuple[str, str]],
+                headers: Optional[Dict[str, str]] = None) -> Tuple[str, List[Tuple[str, str]]]:
+        path = "/" + bucket + ("/" + key if key else "")
+        qs = sigv4.canonical_query(query)
+        url = self.base + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
+        hdrs = {"host": self.endpoint}
+        if headers:
+            hdrs.update({k.lower(): v for k, v in headers.items()})
+        sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
+                   self.region, sigv4.UNSIGNED)
+        return url, list(hdrs.items())
+
+    async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
+                         src_url: str, offset: int, length: int, whole: bool,
+                         progress: Optional[Progress]) -> str:
+        src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
+        attempt = 0
+        while True:
+            url, hdrs = self._signed("PUT", bucket, key, query)
+            try:
+                get, put, _ = await self.t.native.relay(src_url, src_hdrs, url, hdrs, length,
+                                                        progress)
+            except TransportError as e:
+                err: Exception = e
+                retry = True
+            else:
+                if put is None:
+                    raise TransportError(f"source {src_url} answered HTTP {get.status} "
+                                         f"(Content-Length {get.header('content-length')}) "
+                                         f"for {length} bytes at {offset}", get.status)
+                if put.ok:
+                    return (put.header("etag") or "").strip('"')
+                err = parse_error(put, bucket, key)
+                retry = err.retryable
+            if not retry or attempt >= self.retries:
+                raise err
+            attempt += 1
+            await asyncio.sleep(min(5.0, 0.1 * (2 ** attempt)) * (0.5 + random.random()))
+
+    async def relay_object(self, bucket: str, key: str, src_url: str, size: int,
+                           progress: Optional[Progress] = None,
+                           concurrency: Optional[int] = None) -> str:
+        """Stage ``src_url`` (``size`` bytes, Range-capable origin) straight into S3: each
+        multipart part is one Range GET relayed socket->socket into one UploadPart."""
+        if size <= self.multipart_threshold:
+            return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress)
+        parts = self.plan_parts(size)
+        upload_id = await self.create_multipart_upload(bucket, key)
+        sem = asyncio.Semaphore(concurrency or self.max_inflight_parts)
+        etags: Dict[int, str] = {}
+
+        async def one(num: int, off: int, ln: int) -> None:
+            async with sem:
+                etags[num] = await self._relay_put(
+                    bucket, key, [("partNumber", str(num)), ("uploadId", upload_id)], src_url,
+                    off, ln, False, progress)
+        try:
+            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts))
+            return await self.complete_multipart_upload(bucket, key, upload_id,
+                                                        [(n, etags[n]) for n, _, _ in parts])
+        except BaseException:
+            try:
+                await asyncio.shield(self.abort_multipart_upload(bucket, key, upload_id))
+            except Exception:
+                pass
+            raise
+
     async def create_multipart_upload(self, bucket: str, key: str) -> str:
         r = await self._request("POST", bucket, key, query=[("uploads", "")])
         return _text(ET.fromstring(r.body), "UploadId")

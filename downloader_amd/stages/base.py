@@ -107,3 +107,14 @@ class Services:
 
 
 DOWNLOADING = api.STATUS_DOWNLOADING
+
+
+async def ensure_staging_bucket(sv: Services) -> None:
+    """``bucketExists``/``makeBucket('triton-staging')`` (lib/upload.js:29-31), once per worker."""
+    if sv.extra.get("bucket_ready"):
+        return
+    lock = sv.extra.setdefault("bucket_lock", asyncio.Lock())
+    async with lock:
+        if not sv.extra.get("bucket_ready"):
+            await sv.s3.ensure_bucket(sv.config.s3.bucket)
+            sv.extra["bucket_ready"] = True

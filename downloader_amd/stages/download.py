@@ -15,9 +15,11 @@ from typing import Any, Awaitable, Callable, Dict
 from ..fetch import bucket as bucket_src
 from ..fetch import http as http_src
 from ..fetch import local as file_src
-from ..models import api
+from ..models import api, keys
 from ..net.http import Progress
-from .base import DOWNLOADING, Job, ProtocolNotSupported, Services, Stage
+from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
+                   ensure_staging_bucket)
+from .select import select_from_config
 
 Backend = Callable[[str, Job, str], Awaitable[None]]
 
@@ -70,7 +72,10 @@ class DownloadStage(Stage):
             raise
         job.logger.info("finished download")
         await self.sv.telemetry.emit_progress(job.id, DOWNLOADING, 50)
-        return {"path": path}
+        out: Dict[str, Any] = {"path": path}
+        if job.stats.get("streamed"):
+            out["streamed"] = job.stats["streamed"]
+        return out
 
     @staticmethod
     def _redact(uri: str, protocol: str) -> str:
@@ -88,14 +93,40 @@ class DownloadStage(Stage):
             job.logger.info("downloading a .torrent, chaining to torrent downloader")
             await self.torrent(url, job, path)
             return
-        out = os.path.join(path, http_src.output_name(url))
         d = self.cfg.download
+        name = http_src.output_name(url)
+        if d.stream_http and await self._stream_http(url, name, job, path):
+            return
+        out = os.path.join(path, name)
         prog = Progress()
         n = await http_src.download_to(self.sv.transports, url, out, d.http_streams,
                                        d.http_min_split, prog, d.http_min_rate,
                                        min(60.0, d.http_timeout_s), job.logger)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("http", n)
+
+    async def _stream_http(self, url: str, name: str, job: Job, path: str) -> bool:
+        """Streaming fast path for a single-file HTTP source: origin -> S3 with no disk hop.
+
+        Applies only when the outcome of the process stage is already known - one top-level
+        file whose name the media selector accepts - and the origin reports its size (and
+        supports Range for multipart sizes). The object lands under the same key, the
+        progress curve and done marker are unchanged; otherwise the disk path runs."""
+        s3 = self.sv.s3
+        if not s3.can_relay(url) or not select_from_config(self.cfg).accepts_single_file(name):
+            return False
+        size, ranges = await http_src.probe(self.sv.transports, url)
+        if size <= 0 or (size > s3.multipart_threshold and not ranges):
+            return False
+        await ensure_staging_bucket(self.sv)
+        key = keys.object_key(job.id, name)
+        job.logger.info("streaming http source straight to staging", key=key, size=size)
+        await s3.relay_object(self.cfg.s3.bucket, key, url, size, Progress())
+        job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
+        job.stats.setdefault("streamed", []).append(
+            {"file": os.path.join(path, name), "key": key, "size": size})
+        self._count("http", size)
+        return True
 
     async def file(self, url: str, job: Job, path: str) -> None:
         if not self.cfg.download.allow_file_urls:

@@ -18,6 +18,12 @@ class ProcessStage(Stage):
     async def run(self, job: Job) -> Any:
         last = job.last_stage or {}
         root = last["path"]
+        if last.get("streamed"):
+            # The download stage streamed a single selector-approved file straight to staging
+            # (no disk hop); the walk result is that file.
+            files = [s["file"] for s in last["streamed"]]
+            job.logger.info("found", len(files), "media files (streamed)")
+            return {"files": files, "downloadPath": root, "streamed": last["streamed"]}
         job.logger.info("processing directory", root)
         sel: MediaSelector = select_from_config(self.cfg, job.logger)
         files = await asyncio.get_running_loop().run_in_executor(

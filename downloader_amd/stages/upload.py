@@ -20,7 +20,7 @@ from typing import Any, Dict, List
 
 from ..models import keys
 from ..net.http import Progress
-from .base import DOWNLOADING, Job, Services, Stage
+from .base import DOWNLOADING, Job, Services, Stage, ensure_staging_bucket
 
 
 class UploadStage(Stage):
@@ -29,21 +29,15 @@ class UploadStage(Stage):
     def __init__(self, cfg, services: Services):
         self.cfg = cfg
         self.sv = services
-        self._bucket_ready = False
-        self._bucket_lock = asyncio.Lock()
 
     async def ensure_bucket(self) -> None:
-        if self._bucket_ready:
-            return
-        async with self._bucket_lock:
-            if not self._bucket_ready:
-                await self.sv.s3.ensure_bucket(self.cfg.s3.bucket)
-                self._bucket_ready = True
+        await ensure_staging_bucket(self.sv)
 
     async def run(self, job: Job) -> Any:
         last = job.last_stage or {}
         files = last.get("files")
         download_path = last.get("downloadPath")
+        streamed = {s["file"]: s for s in last.get("streamed", [])}
         if not isinstance(files, list):
             raise TypeError(f"Invalid files data type, expected array, got '{type(files).__name__}'")
         job.logger.info("starting file upload")
@@ -63,7 +57,7 @@ class UploadStage(Stage):
                     self.sv.metrics.key_collisions.inc()
             owner[k] = i
         for f in files:
-            if not os.path.exists(f):
+            if f not in streamed and not os.path.exists(f):
                 job.logger.error("failed to upload file, not found")
                 raise FileNotFoundError(f"{f} not found.")
 
@@ -79,8 +73,11 @@ class UploadStage(Stage):
                 if owner[k] == i:
                     job.logger.info("upload", os.path.basename(f))
                     prog = Progress()
-                    await self.sv.s3.fput_object(bucket, k, f, progress=prog)
-                    size = os.path.getsize(f)
+                    if f in streamed:   # already staged by the streaming download path
+                        size = streamed[f]["size"]
+                    else:
+                        await self.sv.s3.fput_object(bucket, k, f, progress=prog)
+                        size = os.path.getsize(f)
                     uploaded.append(size)
                     if self.sv.metrics is not None:
                         self.sv.metrics.bytes_uploaded.inc(size)

@@ -84,6 +84,8 @@ class DownloadConfig(BaseModel):
     http_timeout_s: float = 300.0
     http_min_rate: float = 0.0                  # bytes/s stall floor, 0 = off
     http_native: bool = True                    # native splice() transport for http://
+    # Single selector-approved HTTP file -> relayed origin->S3 socket-to-socket (no disk hop).
+    stream_http: bool = True
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
@@ -125,7 +127,7 @@ class TraceConfig(BaseModel):
 class Config(BaseModel):
     name: str = "downloader"
     mode: Literal["tuned", "reference"] = "tuned"
-    concurrency: int = 2                        # jobs in flight per worker process
+    concurrency: int = 4                        # jobs in flight per worker process
     instance: InstanceConfig = Field(default_factory=InstanceConfig)
     s3: S3Config = Field(default_factory=S3Config)
     broker: BrokerConfig = Field(default_factory=BrokerConfig)
@@ -146,6 +148,7 @@ class Config(BaseModel):
             self.s3.max_inflight_parts = 1
             self.download.http_streams = 1
             self.download.bucket_concurrency = 1
+            self.download.stream_http = False
         else:
             self.broker.prefetch = max(self.broker.prefetch, self.concurrency)
         return self

@@ -68,7 +68,7 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4", "--jobs-per-step", "2"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -78,7 +78,7 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in j
     assert j["n_gpus"] == 2 and j["steps"] == 2 and j["value"] > 0
-    assert j["config"]["jobs_timed"] == 4
+    assert j["config"]["jobs_timed"] == 2 * 2 * 2   # ranks x steps x jobs-per-step
 
 
 def test_bench_single_rank_defaults_are_valid(tmp_path):

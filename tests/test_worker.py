@@ -272,3 +272,53 @@ def test_unsupported_protocol_and_bad_message(run, make_cfg, origin_cls):
         assert len(b.drain("v1.download.dead")) == 2
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_stream_path_and_disk_fallback(run, make_cfg, origin_cls):
+    """Single selector-approved HTTP file -> relayed origin->S3 (no disk); without Range
+    support (multipart size) or with stream_http off it falls back to the disk path."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls)
+        blob = os.urandom(13 * 1024 * 1024 + 11)
+        origin.blobs["/v/big.mkv"] = blob
+        await w.submit(api.make_download("st1", "http", origin.url("/v/big.mkv")))
+        await _wait(w)
+        key = keys.object_key("st1", "big.mkv")
+        assert w.results[0].outcome == "staged" and s3.get("triton-staging", key) == blob
+        ranged = [r for r in origin.requests if r[2]]
+        assert len(ranged) == 3                     # 5 MiB parts -> 3 Range GETs relayed
+        assert w.telemetry.progress_of("st1") == [0, 50, 100]
+        # no Range support -> disk path (single GET)
+        origin.no_ranges = True
+        origin.requests.clear()
+        await w.submit(api.make_download("st2", "http", origin.url("/v/big.mkv")))
+        await _wait(w, 2)
+        assert w.results[1].outcome == "staged"
+        assert s3.get("triton-staging", keys.object_key("st2", "big.mkv")) == blob
+        assert [r for r in origin.requests if r[0] == "GET" and r[2]] == []
+        # non-media name -> never streamed, job fails in the process stage
+        origin.no_ranges = False
+        origin.blobs["/v/readme.txt"] = b"x" * 100
+        w.cfg.broker.max_retries = 0
+        await w.submit(api.make_download("st3", "http", origin.url("/v/readme.txt")))
+        await _wait(w, 3)
+        assert w.results[2].outcome == "dead"
+        assert s3.get("triton-staging", keys.object_key("st3", "readme.txt")) is None
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_stream_source_failure_retries_cleanly(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 1})
+        origin.blobs["/f.mkv"] = os.urandom(8 * 1024 * 1024)
+        # part 2 fails 5 times: the client's 4 tries fail the first job attempt, the retry passes
+        s3.faults.add(FaultRule(method="PUT", query_contains="partNumber=2", times=5,
+                                status=500, code="InternalError"))
+        await w.submit(api.make_download("st4", "http", origin.url("/f.mkv")))
+        await _wait(w, 2)
+        assert [r.outcome for r in w.results] == ["retried", "staged"]
+        assert s3.get("triton-staging", keys.object_key("st4", "f.mkv")) == origin.blobs["/f.mkv"]
+        assert not s3.uploads.get("triton-staging")   # failed attempt's upload was aborted
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
