@@ -49,6 +49,10 @@ def parse() -> argparse.Namespace:
     p.add_argument("--inflight-parts", type=int, default=0, help="override s3.max_inflight_parts")
     p.add_argument("--staging", choices=["stream", "disk"], default="stream",
                    help="stream: single-file HTTP jobs relay origin->S3; disk: stage on disk first")
+    p.add_argument("--peers", choices=["per-rank", "shared"], default="per-rank",
+                   help="one blobd origin+S3 peer per worker, or one shared on rank 0")
+    p.add_argument("--sink", choices=["discard", "checksum"], default="discard",
+                   help="blobd S3 sink: splice bodies to /dev/null, or checksum every byte")
     p.add_argument("--compare-reference", action="store_true",
                    help="also time reference-equivalent mode and report the ratio")
     return p.parse_args()
@@ -172,40 +176,49 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
             "err": bad[0].error if bad else ""}
 
 
-def measure(args, dist: Dist, endpoint: str, mode: str):
+def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
     stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
+    rx0 = blob.stats()["bytes_received"] if blob is not None else 0
     try:
         out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root))
     finally:
         if not args.stage_dir:
             shutil.rmtree(stage_root, ignore_errors=True)
     dist.barrier()
+    # The S3 peer's own byte counter must cover every byte the workers claim to have staged.
+    out["sink_bytes"] = (blob.stats()["bytes_received"] - rx0) if blob is not None else 0
     allr = dist.gather(out)
     elapsed = max(r["elapsed"] for r in allr)
     total_bytes = sum(r["bytes"] for r in allr)
+    sink = sum(r["sink_bytes"] for r in allr)
     lats = [x for r in allr for x in r["latencies"]]
     failed = sum(r["failed"] for r in allr)
     if failed:
         raise RuntimeError(f"{failed} timed jobs failed: {[r['err'] for r in allr if r['err']][:1]}")
+    if sink < total_bytes:
+        raise RuntimeError(f"S3 peer received {sink} bytes < {total_bytes} claimed staged")
     return {"mbps": total_bytes / elapsed / 1e6, "elapsed": elapsed,
             "p50": statistics.median(lats) if lats else 0.0,
             "p90": sorted(lats)[int(0.9 * (len(lats) - 1))] if lats else 0.0,
-            "bytes": total_bytes}
+            "bytes": total_bytes, "sink_bytes": sink}
 
 
 def main() -> int:
     args = parse()
     dist = Dist(args.gpus)
+    from downloader_amd.bench.infra import Blobd
     blob = None
     endpoint = None
-    if dist.rank == 0:
-        from downloader_amd.bench.infra import Blobd
-        blob = Blobd(default_size=int(args.size_mb * 1e6)).start()
+    if args.peers == "per-rank" or dist.rank == 0:
+        # Native origin + S3 sink. per-rank: every worker gets its own peer (the external world
+        # is not the bottleneck being measured); shared: one peer on rank 0 for all workers.
+        blob = Blobd(default_size=int(args.size_mb * 1e6), sink=args.sink).start()
         endpoint = blob.endpoint
-    endpoint = dist.bcast(endpoint)
+    if args.peers == "shared":
+        endpoint = dist.bcast(endpoint)
     try:
-        tuned = measure(args, dist, endpoint, args.mode)
-        ref = measure(args, dist, endpoint, "reference") if args.compare_reference else None
+        tuned = measure(args, dist, endpoint, args.mode, blob)
+        ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
     finally:
         if blob is not None:
             blob.stop()
@@ -225,6 +238,8 @@ def main() -> int:
             "dtype": "bytes",
             "data": "synthetic random-byte media blobs served by the native blobd origin",
             "p50_job_latency_s": round(tuned["p50"], 4),
+            "s3_peer_bytes_received": tuned["sink_bytes"],
+            "peers": args.peers,
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
             "staging": args.staging if args.mode == "tuned" else "disk",

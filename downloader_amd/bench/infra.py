@@ -17,8 +17,9 @@ PKG = Path(__file__).resolve().parents[1]
 
 class Blobd:
     def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
-                 host: str = "127.0.0.1", files_root: str = ""):
+                 host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum"):
         self.files_root = files_root
+        self.sink = sink
         self.keep_bytes = keep_bytes
         self.default_size = default_size
         self.host = host
@@ -32,7 +33,8 @@ class Blobd:
         self.proc = subprocess.Popen(
             [str(exe), "--host", self.host, "--port", "0", "--port-file", pf,
              "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)]
-            + (["--files-root", self.files_root] if self.files_root else []),
+            + (["--files-root", self.files_root] if self.files_root else [])
+            + ["--sink", self.sink],
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         t0 = time.time()
         while not os.path.exists(pf):

@@ -22,6 +22,7 @@
 #include <fcntl.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -59,6 +60,9 @@ std::unordered_map<std::string, Upload> g_uploads;
 std::atomic<uint64_t> g_rx{0}, g_tx{0}, g_reqs{0}, g_objects{0}, g_upload_seq{1};
 std::vector<uint8_t> g_pool;  // random pool the origin serves from
 size_t g_keep_bytes = 1 << 20;
+bool g_discard = false;     // --sink discard
+int g_devnull = -1;
+int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
 
@@ -138,7 +142,13 @@ struct Request {
 class Conn {
  public:
   explicit Conn(int fd) : fd_(fd), buf_(1 << 20) {}
-  ~Conn() { ::close(fd_); }
+  ~Conn() {
+    ::close(fd_);
+    if (pipe_[0] >= 0) {
+      ::close(pipe_[0]);
+      ::close(pipe_[1]);
+    }
+  }
 
   void serve() {
     for (;;) {
@@ -222,6 +232,7 @@ class Conn {
 
   // Consume the request body, folding it into `s`; keep up to `keep` bytes in `out`.
   bool read_body(int64_t n, Summer& s, std::string* out, size_t keep) {
+    if (g_discard && n > (int64_t)keep) return discard_body(n, s);
     while (n > 0) {
       if (pos_ == end_ && !fill()) return false;
       size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
@@ -230,6 +241,38 @@ class Conn {
       pos_ += k;
       n -= (int64_t)k;
       g_rx += k;
+    }
+    return true;
+  }
+
+  // --sink discard: large bodies go socket -> pipe -> /dev/null (no user-space copy); the
+  // checksum then covers only the bytes that were already buffered with the header.
+  bool discard_body(int64_t n, Summer& s) {
+    if (pos_ < end_) {
+      size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
+      s.feed(buf_.data() + pos_, k);
+      pos_ += k;
+      n -= (int64_t)k;
+      g_rx += k;
+    }
+    if (pipe_[0] < 0) {
+      if (pipe2(pipe_, O_CLOEXEC) != 0) return false;
+      fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
+    }
+    while (n > 0) {
+      ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, (size_t)std::min<int64_t>(n, 1 << 20),
+                            SPLICE_F_MOVE | SPLICE_F_MORE);
+      if (in < 0 && errno == EINTR) continue;
+      if (in <= 0) return false;
+      ssize_t left = in;
+      while (left > 0) {
+        ssize_t out = ::splice(pipe_[0], nullptr, g_devnull, nullptr, (size_t)left, SPLICE_F_MOVE);
+        if (out < 0 && errno == EINTR) continue;
+        if (out <= 0) return false;
+        left -= out;
+      }
+      n -= in;
+      g_rx += (uint64_t)in;
     }
     return true;
   }
@@ -306,12 +349,24 @@ class Conn {
     out += "\r\n";
     if (!send_all(out.data(), out.size())) return false;
     if (r.method == "HEAD") return true;
-    // Object byte at offset o = pool[(o + seed * 7919) % kPool]
+    // Object byte at offset o = pool[(o + seed * 7919) % kPool]; the pool lives in a memfd so
+    // the body goes out with sendfile (page references, no user-space copy).
     uint64_t o = start, left = len;
     while (left) {
       uint64_t po = (o + seed * 7919ull) % kPool;
       size_t k = (size_t)std::min<uint64_t>(left, std::min<uint64_t>(kPool - po, 4ull << 20));
-      if (!send_all(g_pool.data() + po, k)) return false;
+      if (g_pool_fd >= 0) {
+        off_t fo = (off_t)po;
+        size_t sent = 0;
+        while (sent < k) {
+          ssize_t w = ::sendfile(fd_, g_pool_fd, &fo, k - sent);
+          if (w < 0 && errno == EINTR) continue;
+          if (w <= 0) return false;
+          sent += (size_t)w;
+        }
+      } else if (!send_all(g_pool.data() + po, k)) {
+        return false;
+      }
       g_tx += k;
       o += k;
       left -= k;
@@ -524,6 +579,7 @@ class Conn {
   int fd_;
   std::vector<uint8_t> buf_;
   size_t pos_ = 0, end_ = 0;
+  int pipe_[2] = {-1, -1};
 };
 
 }  // namespace
@@ -541,8 +597,10 @@ int main(int argc, char** argv) {
     else if (a == "--keep-bytes") g_keep_bytes = strtoull(next(), nullptr, 10);
     else if (a == "--default-size") g_default_size = strtoull(next(), nullptr, 10);
     else if (a == "--files-root") g_files_root = next();
+    else if (a == "--sink") g_discard = std::string(next()) == "discard";
     else {
-      fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] [--default-size N]\n");
+      fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
+                      "[--default-size N] [--files-root DIR] [--sink checksum|discard]\n");
       return 2;
     }
   }
@@ -552,6 +610,20 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < kPool; i += 8) {
     uint64_t v = rng();
     memcpy(g_pool.data() + i, &v, 8);
+  }
+  g_devnull = ::open("/dev/null", O_WRONLY | O_CLOEXEC);
+  g_pool_fd = memfd_create("blobd-pool", MFD_CLOEXEC);
+  if (g_pool_fd >= 0) {
+    size_t off = 0;
+    while (off < kPool) {
+      ssize_t w = ::write(g_pool_fd, g_pool.data() + off, kPool - off);
+      if (w <= 0) {
+        ::close(g_pool_fd);
+        g_pool_fd = -1;
+        break;
+      }
+      off += (size_t)w;
+    }
   }
   int ls = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   int one = 1;
