@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cstring>
 #include <fcntl.h>
@@ -50,6 +51,22 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
 }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
+// gfx950 (CDNA4) V_BITOP3_B32: any 3-input bitwise function in one VALU op, selected by an
+// 8-bit truth table. Only symmetric tables are used here (operand order cannot matter):
+//   0x96 = a ^ b ^ c (SHA-1 parity rounds, message schedule), 0xE8 = majority(a, b, c).
+// hipcc does not form these from plain C (no v_xor3 on gfx950 either), so they are emitted
+// directly; this removes ~1/6 of the VALU ops per 64-byte block.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 struct Sha1State {
   uint32_t h0, h1, h2, h3, h4;
 };
@@ -64,19 +81,33 @@ struct Sha1State {
     a = tmp;                                                             \
   }
 
+// B3 = true: gfx950 v_bitop3 forms; false: plain C (kept for the in-process A/B benchmark).
+template <bool B3>
+__device__ __forceinline__ uint32_t par3(uint32_t a, uint32_t b, uint32_t c) {
+  if constexpr (B3) return xor3(a, b, c);
+  return a ^ b ^ c;
+}
+template <bool B3>
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+  if constexpr (B3) return maj(a, b, c);
+  return (a & b) | (a & c) | (b & c);
+}
+
+template <bool B3>
 __device__ __forceinline__ void sha1_block(Sha1State& s, uint32_t w[16]) {
   uint32_t a = s.h0, b = s.h1, c = s.h2, d = s.h3, e = s.h4;
 #pragma unroll
   for (int t = 0; t < 80; ++t) {
-    if (t >= 16) w[t & 15] = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+    if (t >= 16)
+      w[t & 15] = rotl(par3<B3>(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
     if (t < 20) {
-      SHA1_ROUND(t, (b & c) | (~b & d), 0x5A827999u);
+      SHA1_ROUND(t, (b & c) | (~b & d), 0x5A827999u);  // -> v_bfi_b32
     } else if (t < 40) {
-      SHA1_ROUND(t, b ^ c ^ d, 0x6ED9EBA1u);
+      SHA1_ROUND(t, par3<B3>(b, c, d), 0x6ED9EBA1u);
     } else if (t < 60) {
-      SHA1_ROUND(t, (b & c) | (b & d) | (c & d), 0x8F1BBCDCu);
+      SHA1_ROUND(t, maj3<B3>(b, c, d), 0x8F1BBCDCu);
     } else {
-      SHA1_ROUND(t, b ^ c ^ d, 0xCA62C1D6u);
+      SHA1_ROUND(t, par3<B3>(b, c, d), 0xCA62C1D6u);
     }
   }
   s.h0 += a;
@@ -114,7 +145,7 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t w[16]) {
 // One lane hashes one piece. data holds n_pieces consecutive pieces of piece_len bytes,
 // the last one possibly `last_len` bytes. If `expected` is non-null, ok[i] = digest matches,
 // otherwise digests are written to `out` (5 words, big-endian byte order as bytes).
-template <int ALIGN>
+template <int ALIGN, bool B3 = true>
 __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ data,
                                                    int64_t piece_len, int64_t last_len,
                                                    int n_pieces,
@@ -130,24 +161,31 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
   const int64_t nfull = len >> 6;
   for (int64_t blk = 0; blk < nfull; ++blk) {
     load_block<ALIGN>(p + (blk << 6), w);
-    sha1_block(s, w);
+    sha1_block<B3>(s, w);
   }
-  // Tail + padding (one or two blocks).
+  // Tail + padding (one or two blocks), built word by word straight into w[] - no byte
+  // array, so the padding logic costs no extra registers or scratch.
   const int rem = (int)(len & 63);
   const uint8_t* tail = p + (nfull << 6);
-  uint8_t buf[128];
-#pragma unroll 4
-  for (int k = 0; k < 128; ++k) buf[k] = 0;
-  for (int k = 0; k < rem; ++k) buf[k] = tail[k];
-  buf[rem] = 0x80;
-  const int nb = rem >= 56 ? 2 : 1;
   const uint64_t bits = (uint64_t)len * 8ull;
-  uint8_t* lb = buf + nb * 64 - 8;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) lb[k] = (uint8_t)(bits >> (56 - 8 * k));
+  const int nb = rem >= 56 ? 2 : 1;
   for (int b = 0; b < nb; ++b) {
-    load_block<1>(buf + 64 * b, w);
-    sha1_block(s, w);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int idx = b * 64 + 4 * i + k;
+        uint32_t byte = idx < rem ? (uint32_t)tail[idx] : (idx == rem ? 0x80u : 0u);
+        v |= byte << (24 - 8 * k);
+      }
+      w[i] = v;
+    }
+    if (b == nb - 1) {
+      w[14] = (uint32_t)(bits >> 32);
+      w[15] = (uint32_t)bits;
+    }
+    sha1_block<B3>(s, w);
   }
   uint32_t hv[5] = {s.h0, s.h1, s.h2, s.h3, s.h4};
   if (expected) {
@@ -170,6 +208,79 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
       o[4 * k + 3] = (uint8_t)hv[k];
     }
   }
+}
+
+// Chunk-streamed variant: lane k owns piece (first + k) of a window and advances it by one
+// CH-byte chunk per launch; the SHA-1 state lives in `state` between launches. The chunk of
+// lane k sits at data + k * CH. On the launch that reaches the end of the piece the lane pads,
+// finalises and writes ok[first + k]. Per-launch latency is CH / lane-rate (~1.6 ms for 64 KiB)
+// instead of piece_len / lane-rate, so copies and hashing overlap at a fine grain whatever the
+// piece size.
+template <bool B3>
+__global__ __launch_bounds__(256) void sha1_chunk(uint32_t* __restrict__ state,
+                                                  const uint8_t* __restrict__ data, int64_t CH,
+                                                  int n, int64_t piece_len, int64_t last_len,
+                                                  int first, int n_total, int64_t chunk_off,
+                                                  const uint8_t* __restrict__ expected,
+                                                  uint8_t* __restrict__ ok) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int gi = first + k;
+  const int64_t len = (gi == n_total - 1) ? last_len : piece_len;
+  const int64_t valid = len - chunk_off;          // bytes of this piece at/after this chunk
+  if (valid < 0 || (valid == 0 && chunk_off > 0)) return;  // finished in an earlier launch
+  uint32_t* st = state + 5 * (int64_t)k;
+  Sha1State s;
+  if (chunk_off == 0) {
+    s = Sha1State{0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  } else {
+    s = Sha1State{st[0], st[1], st[2], st[3], st[4]};
+  }
+  const uint8_t* p = data + (int64_t)k * CH;
+  const bool last_chunk = valid <= CH;
+  const int64_t here = last_chunk ? valid : CH;
+  uint32_t w[16];
+  const int64_t nfull = here >> 6;
+  for (int64_t blk = 0; blk < nfull; ++blk) {
+    load_block<16>(p + (blk << 6), w);
+    sha1_block<B3>(s, w);
+  }
+  if (!last_chunk) {
+    st[0] = s.h0; st[1] = s.h1; st[2] = s.h2; st[3] = s.h3; st[4] = s.h4;
+    return;
+  }
+  const int rem = (int)(here & 63);
+  const uint8_t* tail = p + (nfull << 6);
+  const uint64_t bits = (uint64_t)len * 8ull;
+  const int nb = rem >= 56 ? 2 : 1;
+  for (int b = 0; b < nb; ++b) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = b * 64 + 4 * i + q;
+        uint32_t byte = idx < rem ? (uint32_t)tail[idx] : (idx == rem ? 0x80u : 0u);
+        v |= byte << (24 - 8 * q);
+      }
+      w[i] = v;
+    }
+    if (b == nb - 1) {
+      w[14] = (uint32_t)(bits >> 32);
+      w[15] = (uint32_t)bits;
+    }
+    sha1_block<B3>(s, w);
+  }
+  const uint32_t hv[5] = {s.h0, s.h1, s.h2, s.h3, s.h4};
+  const uint8_t* ex = expected + (int64_t)gi * 20;
+  bool good = true;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    uint32_t e = ((uint32_t)ex[4 * q] << 24) | ((uint32_t)ex[4 * q + 1] << 16) |
+                 ((uint32_t)ex[4 * q + 2] << 8) | (uint32_t)ex[4 * q + 3];
+    good = good && (e == hv[q]);
+  }
+  ok[gi] = good ? 1 : 0;
 }
 
 void launch(hipStream_t st, const uint8_t* d_data, int64_t piece_len, int64_t last_len, int n,
@@ -318,6 +429,131 @@ class GpuVerifier {
 
   int64_t batch_bytes() const { return batch_bytes_; }
 
+  // Chunk-streamed verification (see sha1_chunk). Pieces are processed in windows of W lanes;
+  // each round fills one pinned slot with chunk c of every piece of the window (reader
+  // threads, pread from the page cache), copies it on the slot's stream and launches the
+  // chunk kernel. Kernels are ordered across the two streams with events (state carries
+  // over); the host refills a slot only after its previous copy completed.
+  std::vector<uint8_t> verify_files_streamed(
+      const std::vector<std::pair<std::string, int64_t>>& files, int64_t piece_len,
+      const std::string& hashes, int64_t chunk, std::vector<double>* timing) {
+    HIP_CHECK(hipSetDevice(device_));
+    Files fs(files);
+    const int64_t np = fs.total == 0 ? 0 : (fs.total + piece_len - 1) / piece_len;
+    if ((int64_t)hashes.size() != np * 20) throw std::invalid_argument("hash list / piece count mismatch");
+    std::vector<uint8_t> ok((size_t)np, 0);
+    if (np == 0) return ok;
+    const int64_t CH = std::max<int64_t>(64, std::min<int64_t>(chunk, piece_len) & ~(int64_t)63);
+    const int64_t W = std::max<int64_t>(1, std::min<int64_t>(np, batch_bytes_ / CH));
+    const int64_t last_len = fs.total - (np - 1) * piece_len;
+    uint8_t *d_exp = nullptr, *d_ok = nullptr;
+    uint32_t* d_state = nullptr;
+    HIP_CHECK(hipMalloc((void**)&d_exp, (size_t)np * 20));
+    HIP_CHECK(hipMalloc((void**)&d_ok, (size_t)np));
+    HIP_CHECK(hipMalloc((void**)&d_state, (size_t)W * 20));
+    HIP_CHECK(hipMemcpy(d_exp, hashes.data(), (size_t)np * 20, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemset(d_ok, 0, (size_t)np));
+    std::vector<uint8_t> readable((size_t)np, 1);
+    hipEvent_t copied[2], kdone[2];
+    for (int s = 0; s < 2; ++s) {
+      HIP_CHECK(hipEventCreateWithFlags(&copied[s], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&kdone[s], hipEventDisableTiming));
+    }
+    bool slot_busy[2] = {false, false};
+    bool have_prev_kernel = false;
+    int prev_slot = 0;
+    double t_fill = 0, t_wait = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    int s = 0;
+    for (int64_t first = 0; first < np; first += W) {
+      const int64_t n = std::min(W, np - first);
+      const int64_t maxlen = (first + n == np) ? std::max(piece_len, last_len) : piece_len;
+      const int64_t rounds = (maxlen + CH - 1) / CH;
+      for (int64_t c = 0; c < rounds; ++c, s ^= 1) {
+        auto t0 = now();
+        if (slot_busy[s]) HIP_CHECK(hipEventSynchronize(copied[s]));
+        auto t1 = now();
+        uint8_t* dst = h_buf_[s];
+        const int64_t coff = c * CH;
+        parallel_for((size_t)n, readers_, [&](size_t k) {
+          const int64_t gi = first + (int64_t)k;
+          const int64_t len = gi == np - 1 ? last_len : piece_len;
+          const int64_t here = std::min<int64_t>(CH, len - coff);
+          if (here <= 0) return;
+          if (!fs.read(gi * piece_len + coff, here, dst + (int64_t)k * CH)) readable[(size_t)gi] = 0;
+        });
+        auto t2 = now();
+        t_wait += std::chrono::duration<double>(t1 - t0).count();
+        t_fill += std::chrono::duration<double>(t2 - t1).count();
+        HIP_CHECK(hipMemcpyAsync(d_buf_[s], dst, (size_t)(n * CH), hipMemcpyHostToDevice, stream_[s]));
+        HIP_CHECK(hipEventRecord(copied[s], stream_[s]));
+        slot_busy[s] = true;
+        if (have_prev_kernel) HIP_CHECK(hipStreamWaitEvent(stream_[s], kdone[prev_slot], 0));
+        const int block = 64, grid = (int)((n + block - 1) / block);
+        hipLaunchKernelGGL((sha1_chunk<true>), dim3(grid), dim3(block), 0, stream_[s], d_state,
+                           d_buf_[s], CH, (int)n, piece_len, last_len, (int)first, (int)np, coff,
+                           d_exp, d_ok);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(kdone[s], stream_[s]));
+        have_prev_kernel = true;
+        prev_slot = s;
+      }
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_[0]));
+    HIP_CHECK(hipStreamSynchronize(stream_[1]));
+    HIP_CHECK(hipMemcpy(ok.data(), d_ok, (size_t)np, hipMemcpyDeviceToHost));
+    for (int q = 0; q < 2; ++q) {
+      hipEventDestroy(copied[q]);
+      hipEventDestroy(kdone[q]);
+    }
+    hipFree(d_exp);
+    hipFree(d_ok);
+    hipFree(d_state);
+    for (int64_t i = 0; i < np; ++i)
+      if (!readable[(size_t)i]) ok[(size_t)i] = 0;
+    if (timing) *timing = {t_fill, t_wait};
+    return ok;
+  }
+
+  // Kernel-only timing (device-resident data, hipEvents): ms per launch hashing `n_pieces`
+  // pieces of `piece_len` bytes; `bitop3` selects the v_bitop3 or the plain-C round forms
+  // so both variants are A/B-timed interleaved in one process.
+  std::vector<double> kernel_bench(int64_t piece_len, int n_pieces, int iters) {
+    HIP_CHECK(hipSetDevice(device_));
+    size_t bytes = (size_t)piece_len * (size_t)n_pieces;
+    uint8_t *d = nullptr, *dout = nullptr;
+    HIP_CHECK(hipMalloc((void**)&d, bytes));
+    HIP_CHECK(hipMalloc((void**)&dout, (size_t)n_pieces * 20));
+    HIP_CHECK(hipMemset(d, 0x5a, bytes));
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    const int block = 64, grid = (n_pieces + block - 1) / block;
+    double t[2] = {0, 0};
+    for (int it = 0; it < iters + 1; ++it) {
+      for (int v = 0; v < 2; ++v) {
+        HIP_CHECK(hipEventRecord(e0, stream_[0]));
+        if (v == 0)
+          hipLaunchKernelGGL((sha1_pieces<16, true>), dim3(grid), dim3(block), 0, stream_[0], d,
+                             piece_len, piece_len, n_pieces, nullptr, nullptr, dout);
+        else
+          hipLaunchKernelGGL((sha1_pieces<16, false>), dim3(grid), dim3(block), 0, stream_[0], d,
+                             piece_len, piece_len, n_pieces, nullptr, nullptr, dout);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(e1, stream_[0]));
+        HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (it > 0) t[v] += ms;  // first round is warm-up
+      }
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipFree(d);
+    hipFree(dout);
+    return {t[0] / iters, t[1] / iters};
+  }
+
  private:
   template <class Fill>
   void run_batches(int64_t np, int64_t piece_len, int64_t total, const uint8_t* expected,
@@ -451,5 +687,36 @@ PYBIND11_MODULE(_gpuhash, m) {
             return py::bytes((const char*)ok.data(), ok.size());
           },
           py::arg("files"), py::arg("piece_len"), py::arg("hashes"))
+      .def(
+          "verify_files_streamed",
+          [](GpuVerifier& g, const std::vector<std::pair<std::string, int64_t>>& files,
+             int64_t piece_len, const py::bytes& hashes, int64_t chunk) {
+            std::string hs = hashes;
+            if (piece_len <= 0) throw std::invalid_argument("piece_len must be > 0");
+            std::vector<uint8_t> ok;
+            std::vector<double> timing;
+            {
+              py::gil_scoped_release rel;
+              ok = g.verify_files_streamed(files, piece_len, hs, chunk, &timing);
+            }
+            return py::make_tuple(py::bytes((const char*)ok.data(), ok.size()),
+                                  py::make_tuple(timing[0], timing[1]));
+          },
+          py::arg("files"), py::arg("piece_len"), py::arg("hashes"), py::arg("chunk") = 65536,
+          "Chunk-streamed SHA-1 verification: returns (ok bytes, (host_fill_s, host_wait_s)).")
+      .def(
+          "kernel_bench",
+          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters) {
+            if (piece_len <= 0 || piece_len % 16 || n_pieces <= 0 || iters <= 0)
+              throw std::invalid_argument("piece_len must be a positive multiple of 16");
+            std::vector<double> r;
+            {
+              py::gil_scoped_release rel;
+              r = g.kernel_bench(piece_len, n_pieces, iters);
+            }
+            return py::make_tuple(r[0], r[1]);
+          },
+          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 5,
+          "(ms_bitop3, ms_plain): kernel time per launch, device-resident data")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
 }

@@ -90,5 +90,6 @@ def verify_pieces(files: FileList, piece_len: int, hashes: bytes,
     n_pieces = (total + piece_len - 1) // piece_len if total else 0
     be = choose_backend(backend, total, n_pieces) if which is None else "cpu"
     if be == "gpu":
-        return _verifier().verify_files(files, piece_len, hashes)
+        ok, _timing = _verifier().verify_files_streamed(files, piece_len, hashes)
+        return ok
     return native().verify_pieces(files, piece_len, hashes, list(which or []), threads)

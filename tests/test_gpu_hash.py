@@ -65,6 +65,48 @@ def test_verify_files_detects_corruption(gv, tmp_path):
     assert [i for i, v in enumerate(ok) if not v] == [bad]
 
 
+@pytest.mark.parametrize("piece,sizes,chunk", [
+    (1 << 20, [3_000_000, 1, 5_000_000, 777_777], 65536),   # short last piece, file spans
+    (65536, [200_000, 333_333], 65536),                     # chunk == piece
+    (262144, [1_048_576], 65536),                           # exact multiple, no tail
+    (100_000, [950_001], 65536),                            # piece not a multiple of the chunk
+    (1 << 20, [4_500_000], 4096),                           # many rounds per piece
+])
+def test_streamed_verify_matches_cpu(gv, tmp_path, piece, sizes, chunk):
+    from downloader_amd.ops import hashing
+    files, blob = [], b""
+    for i, n in enumerate(sizes):
+        d = os.urandom(n)
+        p = tmp_path / f"s{i}"
+        p.write_bytes(d)
+        files.append((str(p), n))
+        blob += d
+    hashes = ref(blob, piece)
+    ok, _ = gv.verify_files_streamed(files, piece, hashes, chunk)
+    assert ok == b"\x01" * (len(hashes) // 20)
+    assert hashing.verify_pieces(files, piece, hashes, backend="gpu") == ok
+    # corrupt the last byte of the storage -> only the last piece fails
+    last = files[-1][0]
+    b = bytearray(open(last, "rb").read())
+    b[-1] ^= 0x01
+    open(last, "wb").write(bytes(b))
+    ok, _ = gv.verify_files_streamed(files, piece, hashes, chunk)
+    n = len(hashes) // 20
+    assert [i for i, v in enumerate(ok) if not v] == [n - 1]
+
+
+def test_streamed_window_smaller_than_piece_count(gv, tmp_path):
+    """A tiny pinned slot forces several windows of lanes (W < pieces)."""
+    from downloader_amd.ops import gpuhash
+    g = gpuhash().GpuVerifier(0, 1 << 20, 4)   # 1 MiB slot / 64 KiB chunk -> 16 lanes/window
+    d = os.urandom(70 * 65536 + 123)
+    p = tmp_path / "w"
+    p.write_bytes(d)
+    hashes = ref(d, 65536)
+    ok, _ = g.verify_files_streamed([(str(p), len(d))], 65536, hashes, 65536)
+    assert ok == b"\x01" * 71
+
+
 def test_gpu_matches_cpu_backend_and_reports_throughput(gv, tmp_path):
     from downloader_amd.ops import hashing
     piece = 1 << 20
