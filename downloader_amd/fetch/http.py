@@ -14,6 +14,7 @@ file through the native transport.
 from __future__ import annotations
 
 import asyncio
+import json
 import os
 import posixpath
 import time
@@ -69,17 +70,31 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                       min_split: int = 32 << 20, progress: Optional[Progress] = None,
                       min_rate: float = 0.0, stall_window: float = 30.0,
                       logger: Optional[Logger] = None) -> int:
+    """Download ``url`` to ``path`` through ``path + '.part'`` (renamed when complete).
+
+    Resume (the reference restarts from byte 0): completed byte ranges are
+    recorded in ``path + '.part.ranges'``; a later attempt with the same job directory skips
+    them, and a single-stream transfer continues from the ``.part`` length when the origin
+    supports ``Range``. A complete ``path`` of the advertised size is reused as is."""
     log = logger or NullLogger()
     progress = progress or Progress()
-    size, ranges = (-1, False)
-    if streams > 1:
-        size, ranges = await probe(t, url)
-    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | getattr(os, "O_CLOEXEC", 0), 0o644)
+    size, ranges = await probe(t, url)
+    if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
+        log.info("resume: file already complete", path=path)
+        return 0
+    part_path, state_path = path + ".part", path + ".part.ranges"
+    done = _load_ranges(state_path) if os.path.exists(part_path) else []
+    fd = os.open(part_path, os.O_WRONLY | os.O_CREAT | getattr(os, "O_CLOEXEC", 0), 0o644)
+    written = 0
     try:
         if streams > 1 and ranges and size >= 2 * min_split:
             n = int(min(streams, size // min_split))
             step = (size + n - 1) // n
             os.ftruncate(fd, size)
+            plan = [(o, min(step, size - o)) for o in range(0, size, step)]
+            todo = [(o, ln) for o, ln in plan if [o, ln] not in done]
+            if len(todo) < len(plan):
+                log.info("resume: skipping completed ranges", done=len(plan) - len(todo))
             log.debug("parallel range download", streams=n, size=size)
 
             async def part(off: int, ln: int) -> int:
@@ -89,24 +104,53 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                     raise HttpDownloadError(f"range request got HTTP {r.status}")
                 if r.written != ln:
                     raise HttpDownloadError(f"short range body {r.written} != {ln}")
+                done.append([off, ln])
+                _save_ranges(state_path, done)
                 return r.written
 
-            coro = asyncio.gather(*(part(o, min(step, size - o)) for o in range(0, size, step)))
-            task = asyncio.ensure_future(coro)
+            task = asyncio.ensure_future(asyncio.gather(*(part(o, ln) for o, ln in todo)))
             written = sum(await _guard(task, progress, min_rate, stall_window))
         else:
-            task = asyncio.ensure_future(t.request("GET", url, sink=FileSink(fd, 0),
-                                                   progress=progress))
+            have = os.fstat(fd).st_size if (ranges and size > 0 and not done) else 0
+            if not (0 < have < size):
+                have = 0
+                os.ftruncate(fd, 0)
+            hdrs = [("Range", f"bytes={have}-")] if have else []
+            if have:
+                log.info("resume: continuing partial download", offset=have, size=size)
+            task = asyncio.ensure_future(t.request("GET", url, headers=hdrs,
+                                                   sink=FileSink(fd, have), progress=progress))
             r = await _guard(task, progress, min_rate, stall_window)
-            if not r.ok:
+            if not r.ok or (have and r.status != 206):
                 raise HttpDownloadError(f"GET {url} -> HTTP {r.status} {r.reason}")
             cl = r.header("content-length")
             if cl and cl.isdigit() and int(cl) != r.written:
                 raise HttpDownloadError(f"truncated body: {r.written} of {cl} bytes")
             written = r.written
+            if size >= 0 and have + written != size:
+                raise HttpDownloadError(f"size mismatch: {have + written} != {size}")
     finally:
         os.close(fd)
+    os.replace(part_path, path)
+    if os.path.exists(state_path):
+        os.unlink(state_path)
     return written
+
+
+def _load_ranges(p: str) -> list:
+    try:
+        with open(p, "r", encoding="utf-8") as f:
+            v = json.load(f)
+        return [list(x) for x in v] if isinstance(v, list) else []
+    except (OSError, ValueError):
+        return []
+
+
+def _save_ranges(p: str, done: list) -> None:
+    tmp = p + ".tmp"
+    with open(tmp, "w", encoding="utf-8") as f:
+        json.dump(done, f)
+    os.replace(tmp, p)
 
 
 async def _guard(task: asyncio.Future, progress: Progress, min_rate: float, window: float):

@@ -147,7 +147,7 @@ class Worker:
         except Exception as e:
             self.log.error("undecodable message dropped to dead-letter", err=str(e))
             await self._dead_letter(d, f"decode: {e}")
-            return self._finish(JobResult("", "dead", time.perf_counter() - t0, error=str(e)))
+            return self._finish(None, JobResult("", "dead", time.perf_counter() - t0, error=str(e)))
         media = msg.media
         job_id, creator = media.id, media.creatorId
         attempt = int(d.headers.get("x-attempt", 0) or 0)
@@ -177,11 +177,11 @@ class Worker:
                             if self.cfg.download.emit_errored_on_stall:
                                 await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
                             await d.ack()
-                            return self._finish(JobResult(job_id, "stalled",
+                            return self._finish(job, JobResult(job_id, "stalled",
                                                           time.perf_counter() - t0, error=str(e)))
                         await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
                         outcome = await self._retry(d, attempt, str(e))
-                        return self._finish(JobResult(job_id, outcome, time.perf_counter() - t0,
+                        return self._finish(job, JobResult(job_id, outcome, time.perf_counter() - t0,
                                                       error=str(e)))
                     child.info("creating convert job")
                 else:
@@ -195,22 +195,38 @@ class Worker:
                 except Exception as e:
                     child.error("failed to create job:", str(e))
                     await d.nack(requeue=True)
-                    return self._finish(JobResult(job_id, "publish_failed",
+                    return self._finish(job, JobResult(job_id, "publish_failed",
                                                   time.perf_counter() - t0, error=str(e)))
                 await d.ack()
-                return self._finish(JobResult(job_id, outcome, time.perf_counter() - t0,
+                return self._finish(job, JobResult(job_id, outcome, time.perf_counter() - t0,
                                               job.stats.get("uploaded_bytes", 0)))
         except Exception as e:  # infrastructure error outside the stage loop (e.g. S3 down)
             err = str(e)
             child.error("job failed outside stages", err=err)
             await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
             outcome = await self._retry(d, attempt, err)
-            return self._finish(JobResult(job_id, outcome, time.perf_counter() - t0, error=err))
+            return self._finish(job, JobResult(job_id, outcome, time.perf_counter() - t0, error=err))
         finally:
             self.active.pop(slot, None)
             self.metrics.inflight.dec()
+            await self._release_jobdir(job, job.stats.get("outcome", ""))
 
-    def _finish(self, r: JobResult) -> JobResult:
+    async def _release_jobdir(self, job: Job, outcome: str) -> None:
+        """Keep a failed attempt's partial data for the retry (resume); drop it when the job
+        is finished for good (dead-lettered, or stalled with cleanup_on_stall, App. A #6)."""
+        jd = job.jobdir
+        if jd is None:
+            return
+        drop = outcome == "dead" or (outcome == "stalled" and self.cfg.download.cleanup_on_stall)
+        loop = asyncio.get_running_loop()
+        if drop or not jd.exclusive:
+            await loop.run_in_executor(None, jd.remove)
+        jd.release()
+        job.jobdir = None
+
+    def _finish(self, job: Optional[Job], r: JobResult) -> JobResult:
+        if job is not None:
+            job.stats["outcome"] = r.outcome
         self.results.append(r)
         self.metrics.jobs.labels(r.outcome).inc()
         self.metrics.job_duration.labels(r.outcome).observe(r.seconds)

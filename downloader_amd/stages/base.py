@@ -66,6 +66,7 @@ class Job:
     headers: Dict[str, Any] = field(default_factory=dict)
     cancel: asyncio.Event = field(default_factory=asyncio.Event)
     stats: Dict[str, Any] = field(default_factory=dict)
+    jobdir: Any = None            # stages.jobdir.JobDir claimed by the download stage
 
     @property
     def id(self) -> str:

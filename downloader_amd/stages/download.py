@@ -19,6 +19,7 @@ from ..models import api, keys
 from ..net.http import Progress
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket)
+from .jobdir import JobDir
 from .select import select_from_config
 
 Backend = Callable[[str, Job, str], Awaitable[None]]
@@ -39,11 +40,12 @@ class DownloadStage(Stage):
         }
 
     def job_dir(self, job: Job) -> str:
-        d = os.path.join(str(self.root), job.id)
-        if self.cfg.instance.per_attempt_dirs:
-            job.attempt_id = job.attempt_id or secrets.token_hex(4)
-            d = os.path.join(d, job.attempt_id)
-        return d
+        if not self.cfg.instance.per_attempt_dirs:
+            return os.path.join(str(self.root), job.id)   # reference layout, no locking
+        if job.jobdir is None:
+            job.jobdir = JobDir(str(self.root), job.id)
+            job.jobdir.acquire()
+        return job.jobdir.path
 
     def _count(self, proto: str, n: int) -> None:
         if self.sv.metrics is not None and n:
@@ -51,9 +53,9 @@ class DownloadStage(Stage):
 
     async def run(self, job: Job) -> Any:
         media = job.media
-        path = self.job_dir(job)
         protocol = api.enum_to_string("SourceType", media.source)
         try:
+            path = await asyncio.get_running_loop().run_in_executor(None, self.job_dir, job)
             await asyncio.get_running_loop().run_in_executor(
                 None, lambda: os.makedirs(path, exist_ok=True))
             job.logger.info("created downloadPath", path)

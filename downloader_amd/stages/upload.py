@@ -76,7 +76,8 @@ class UploadStage(Stage):
                     if f in streamed:   # already staged by the streaming download path
                         size = streamed[f]["size"]
                     else:
-                        await self.sv.s3.fput_object(bucket, k, f, progress=prog)
+                        await self.sv.s3.fput_object(bucket, k, f, progress=prog,
+                                                     resume=self.cfg.s3.resume_uploads)
                         size = os.path.getsize(f)
                     uploaded.append(size)
                     if self.sv.metrics is not None:

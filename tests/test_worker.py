@@ -322,3 +322,91 @@ def test_stream_source_failure_retries_cleanly(run, make_cfg, origin_cls):
         assert not s3.uploads.get("triton-staging")   # failed attempt's upload was aborted
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_http_resume_after_truncated_transfer(run, make_cfg, origin_cls):
+    """Attempt 1 is cut mid-body; the retry re-uses the job directory and continues with a
+    Range request from the partial length (the reference restarts from 0)."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"stream_http": False,
+                                                                         "http_streams": 1})
+        blob = os.urandom(3 * 1024 * 1024 + 5)
+        origin.blobs["/r.mkv"] = blob
+        origin.truncate.add("/r.mkv")
+        await w.submit(api.make_download("rs1", "http", origin.url("/r.mkv")))
+        await _wait(w, 1)
+        assert w.results[0].outcome == "retried"
+        origin.truncate.discard("/r.mkv")
+        await _wait(w, 2)
+        assert w.results[1].outcome == "staged"
+        gets = [r for r in origin.requests if r[0] == "GET"]
+        assert gets[-1][2] and gets[-1][2].startswith("bytes=") and gets[-1][2] != "bytes=0-"
+        assert s3.get("triton-staging", keys.object_key("rs1", "r.mkv")) == blob
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_parallel_range_resume_skips_done_ranges(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={
+            "stream_http": False, "http_streams": 4, "http_min_split": 1 << 20})
+        blob = os.urandom(8 * 1024 * 1024)
+        origin.blobs["/p.mkv"] = blob
+        # make the last range fail once: 3 of 4 ranges complete in attempt 1
+        orig_handler_fail = {"n": 0}
+
+        def hook(method, path):
+            pass
+        origin.fail_status["/p.mkv"] = None
+        del origin.fail_status["/p.mkv"]
+        step = 2 * 1024 * 1024
+        bad = f"bytes={3 * step}-{len(blob) - 1}"
+        calls = []
+        orig_start = origin.requests
+
+        class FailLast(list):
+            def append(self, item):
+                super().append(item)
+                calls.append(item)
+        origin.requests = FailLast()
+        import aiohttp.web as web
+
+        real = origin.blobs
+
+        class Blobs(dict):
+            def get(self, k, d=None):
+                if calls and calls[-1][2] == bad and orig_handler_fail["n"] == 0:
+                    orig_handler_fail["n"] += 1
+                    return None          # -> 404 for that one range request
+                return dict.get(self, k, d)
+        origin.blobs = Blobs(real)
+        await w.submit(api.make_download("rs2", "http", origin.url("/p.mkv")))
+        await _wait(w, 2)
+        assert [r.outcome for r in w.results] == ["retried", "staged"]
+        ranged = [c[2] for c in calls if c[0] == "GET" and c[2]]
+        assert ranged.count("bytes=0-2097151") == 1       # done in attempt 1, skipped after
+        assert ranged.count(bad) == 2
+        assert s3.get("triton-staging", keys.object_key("rs2", "p.mkv")) == blob
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_multipart_upload_resume_reuses_parts(run, make_cfg, origin_cls):
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"stream_http": False})
+        blob = os.urandom(16 * 1024 * 1024 + 7)
+        origin.blobs["/u.mkv"] = blob
+        # part 3 fails on every try of attempt 1 (client retries 3 -> 4 faults)
+        s3.faults.add(FaultRule(method="PUT", query_contains="partNumber=3", times=4,
+                                status=500, code="InternalError"))
+        part_puts = []
+        s3.hooks.append(lambda m, p: part_puts.append(m))
+        await w.submit(api.make_download("rs3", "http", origin.url("/u.mkv")))
+        await _wait(w, 2)
+        assert [r.outcome for r in w.results] == ["retried", "staged"]
+        assert s3.get("triton-staging", keys.object_key("rs3", "u.mkv")) == blob
+        # attempt 2 listed the open upload and only re-sent the missing part(s)
+        assert any(m == "GET" for m in part_puts)
+        assert not s3.uploads.get("triton-staging")
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
