@@ -1,0 +1,278 @@
+"""Runner for the BASELINE.json benchmark configs (config 2 is the headline ``bench.py``).
+
+  1  single 10 MB HTTP URL -> S3, 1 worker: per-job latency (p50/p90 over sequential jobs)
+  3  single-file 4 GB torrent fetched from a BEP-19 webseed, piece-hash verification on
+  4  multi-file 20 GB torrent (50 files), full piece verification, one S3 object per file
+  5  mixed steady-state queue: HTTP + torrent jobs published at a fixed rate to the AMQP
+     broker, consumed by N worker processes, 5% of HTTP jobs fail once (retry path)
+
+Every config runs the real worker (stages, S3 client, telemetry) against the native ``blobd``
+peer (origin, webseed file server and S3 sink); ``--mode reference`` runs the reference-
+equivalent structure (prefetch 1, sequential parts/files, single stream, disk staging).
+
+  python -m downloader_amd.bench.configs --config 3 [--scale 0.25] [--mode tuned|reference]
+
+``--scale`` shrinks configs 3/4/5 proportionally for quick runs; results report the actual
+sizes. Output: one JSON line per config.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import shutil
+import statistics
+import sys
+import tempfile
+import time
+from typing import Dict, List
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+from downloader_amd.bench.infra import Blobd  # noqa: E402
+from downloader_amd.broker.memory import MemoryBroker  # noqa: E402
+from downloader_amd.models import api  # noqa: E402
+from downloader_amd.service.worker import Worker  # noqa: E402
+from downloader_amd.utils.config import load_config  # noqa: E402
+
+MB = 1_000_000
+
+
+def _pct(xs: List[float], q: float) -> float:
+    if not xs:
+        return 0.0
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * (len(xs) - 1) + 0.5))]
+
+
+def _cfg(mode: str, endpoint: str, stage: str, **over) -> object:
+    o: Dict = {"mode": mode, "instance": {"download_path": stage}, "s3": {"endpoint": endpoint},
+               "broker": {"backend": "memory"}, "health": {"enabled": False},
+               "download": {"torrent_enable_dht": False, "progress_interval_s": 5.0}}
+    for k, v in over.items():
+        if isinstance(v, dict):
+            o.setdefault(k, {}).update(v)
+        else:
+            o[k] = v
+    return load_config(overrides=o, env={})
+
+
+async def _run_jobs(w: Worker, msgs, timeout: float = 3600.0):
+    done = asyncio.Event()
+    res = []
+
+    def cb(r):
+        res.append(r)
+        if len(res) >= len(msgs):
+            done.set()
+    w.on_result = cb
+    t0 = time.perf_counter()
+    for m in msgs:
+        await w.submit(m)
+    await asyncio.wait_for(done.wait(), timeout)
+    return time.perf_counter() - t0, res
+
+
+def _write_random(path: str, n: int, seed: int) -> None:
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "wb") as f:
+        left = n
+        while left:
+            k = min(left, 256 << 20)
+            f.write(rng.bytes(k))
+            left -= k
+
+
+# ---------------------------------------------------------------------------- config 1
+async def config1(a) -> Dict:
+    stage = tempfile.mkdtemp(prefix="cfg1-")
+    with Blobd(sink="discard") as b:
+        w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1), broker=MemoryBroker())
+        await w.start(health=False)
+        lat = []
+        for i in range(a.jobs):
+            m = api.make_download(f"c1-{a.mode}-{i}", "http",
+                                  b.media_url(f"c1-{i}.mkv", 10 * MB, i))
+            _, r = await _run_jobs(w, [m])
+            assert r[0].outcome == "staged", r[0]
+            lat.append(r[0].seconds)
+        await w.stop()
+    shutil.rmtree(stage, ignore_errors=True)
+    lat = lat[1:] or lat   # first job warms connections
+    return {"config": 1, "mode": a.mode, "jobs": len(lat), "object_MB": 10,
+            "p50_latency_s": round(statistics.median(lat), 4),
+            "p90_latency_s": round(_pct(lat, 0.9), 4),
+            "MBps_sequential": round(10 / statistics.mean(lat), 1)}
+
+
+# ---------------------------------------------------------------------------- configs 3/4
+def _make_torrent_tree(root: str, name: str, sizes: List[int], url: str, plen: int) -> bytes:
+    from downloader_amd.torrent.metainfo import make_torrent
+    if len(sizes) == 1:
+        p = os.path.join(root, name)
+        _write_random(p, sizes[0], 7)
+        return make_torrent(p, plen, url_list=[url + name])
+    for i, n in enumerate(sizes):
+        _write_random(os.path.join(root, name, f"Season 1/{name} E{i + 1:02d}.mkv"), n, 100 + i)
+    return make_torrent(os.path.join(root, name), plen, url_list=[url])
+
+
+async def config_torrent(a, cfg_no: int) -> Dict:
+    if cfg_no == 3:
+        sizes = [int(4e9 * a.scale)]
+        name = "movie.mkv"
+    else:
+        total = int(20e9 * a.scale)
+        sizes = [total // 50 + (i * 7919) % 1000 for i in range(50)]
+        name = "Show"
+    total = sum(sizes)
+    src = tempfile.mkdtemp(prefix=f"cfg{cfg_no}-src-", dir=a.src_dir)
+    stage = tempfile.mkdtemp(prefix=f"cfg{cfg_no}-stage-", dir=a.stage_dir or None)
+    try:
+        with Blobd(sink="discard", files_root=src) as b:
+            t0 = time.perf_counter()
+            raw = _make_torrent_tree(src, name, sizes, b.files_url(), a.piece_mb << 20)
+            setup_s = time.perf_counter() - t0
+            with open(os.path.join(src, "job.torrent"), "wb") as f:
+                f.write(raw)
+            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1,
+                            download={"verify_backend": a.verify_backend}),
+                       broker=MemoryBroker())
+            await w.start(health=False)
+            m = api.make_download(f"c{cfg_no}-{a.mode}", "http", b.files_url("job.torrent"),
+                                  "TV" if cfg_no == 4 else "MOVIE")
+            dt, r = await _run_jobs(w, [m])
+            await w.stop()
+            assert r[0].outcome == "staged", r[0]
+            st = b.stats()
+    finally:
+        shutil.rmtree(src, ignore_errors=True)
+        shutil.rmtree(stage, ignore_errors=True)
+    return {"config": cfg_no, "mode": a.mode, "bytes": total, "files": len(sizes),
+            "piece_len": a.piece_mb << 20, "job_s": round(dt, 3),
+            "MBps": round(total / dt / MB, 1), "setup_s": round(setup_s, 2),
+            "s3_bytes_received": st["bytes_received"], "uploaded_bytes": r[0].bytes}
+
+
+# ---------------------------------------------------------------------------- config 5
+async def config5(a) -> Dict:
+    from downloader_amd.broker.amqp import AmqpBroker
+    from downloader_amd.broker.server import BrokerServer
+    from downloader_amd.parallel.supervisor import Supervisor, worker_argv
+    from downloader_amd.torrent.metainfo import make_torrent
+    n_jobs = max(20, int(1000 * a.scale))
+    src = tempfile.mkdtemp(prefix="cfg5-src-", dir=a.src_dir)
+    stage = tempfile.mkdtemp(prefix="cfg5-stage-", dir=a.stage_dir or None)
+    srv = await BrokerServer(heartbeat=0).start()
+    with Blobd(sink="discard", files_root=src) as b:
+        # 4 distinct torrents re-used by the torrent jobs (50 MB each, webseed)
+        torrents = []
+        for t in range(4):
+            p = os.path.join(src, f"t{t}.mkv")
+            _write_random(p, 50 * MB, 500 + t)
+            raw = make_torrent(p, 1 << 20, url_list=[b.files_url(f"t{t}.mkv")])
+            with open(os.path.join(src, f"t{t}.torrent"), "wb") as f:
+                f.write(raw)
+            torrents.append(b.files_url(f"t{t}.torrent"))
+        env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error",
+                   STAGER_BROKER__URL=srv.url, STAGER_BROKER__BACKEND="amqp",
+                   STAGER_S3__ENDPOINT=b.endpoint, STAGER_INSTANCE__DOWNLOAD_PATH=stage,
+                   STAGER_HEALTH__ENABLED="false", STAGER_DOWNLOAD__TORRENT_ENABLE_DHT="false",
+                   STAGER_BROKER__RETRY_BACKOFF_S="0.05", STAGER_MODE=a.mode,
+                   STAGER_CONCURRENCY=str(a.concurrency))
+        sup = Supervisor(a.workers, worker_argv(), env=env)
+        client = AmqpBroker(srv.url)
+        await client.connect()
+        for q in ("v1.download", "v1.convert"):
+            await client.declare(q)
+        sup.start()
+        rng = random.Random(5)
+        published: Dict[str, float] = {}
+        lat: List[float] = []
+        kinds: Dict[str, str] = {}
+        done = asyncio.Event()
+
+        async def on_convert(d):
+            mid = api.decode(api.Convert, d.body).media.id
+            if mid in published and mid not in kinds.get("_seen", ""):
+                lat.append(time.perf_counter() - published[mid])
+            await d.ack()
+            if len(lat) >= n_jobs:
+                done.set()
+        await client.consume("v1.convert", on_convert, prefetch=64)
+        t0 = time.perf_counter()
+        fails = 0
+        for i in range(n_jobs):
+            target = t0 + i / a.qps
+            now = time.perf_counter()
+            if target > now:
+                await asyncio.sleep(target - now)
+            jid = f"c5-{a.mode}-{i}"
+            if rng.random() < 0.2:
+                m = api.make_download(jid, "http", torrents[i % 4])
+                kinds[jid] = "torrent"
+            else:
+                url = b.media_url(f"c5-{i}.mkv", 10 * MB, i)
+                if rng.random() < 0.05:
+                    url += "&fail=1"
+                    fails += 1
+                m = api.make_download(jid, "http", url)
+                kinds[jid] = "http"
+            published[jid] = time.perf_counter()
+            await client.publish("v1.download", api.encode(m))
+        publish_s = time.perf_counter() - t0
+        try:
+            await asyncio.wait_for(done.wait(), 1800)
+        finally:
+            wall = time.perf_counter() - t0
+            codes = await asyncio.get_running_loop().run_in_executor(None, sup.stop)
+            await client.close()
+            await srv.stop()
+            shutil.rmtree(src, ignore_errors=True)
+            shutil.rmtree(stage, ignore_errors=True)
+    n_torrent = sum(1 for k in kinds.values() if k == "torrent")
+    total_bytes = (n_jobs - n_torrent) * 10 * MB + n_torrent * 50 * MB
+    return {"config": 5, "mode": a.mode, "jobs": n_jobs, "workers": a.workers,
+            "qps_offered": a.qps, "publish_s": round(publish_s, 2), "wall_s": round(wall, 2),
+            "jobs_per_s": round(n_jobs / wall, 1), "MBps": round(total_bytes / wall / MB, 1),
+            "p50_latency_s": round(statistics.median(lat), 4),
+            "p99_latency_s": round(_pct(lat, 0.99), 4), "injected_failures": fails,
+            "torrent_jobs": n_torrent, "worker_exit_codes": codes}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, action="append", required=True)
+    ap.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")
+    ap.add_argument("--piece-mb", type=int, default=4)
+    ap.add_argument("--verify-backend", choices=["cpu", "gpu", "auto"], default="auto")
+    ap.add_argument("--workers", type=int, default=4, help="config 5 worker processes")
+    ap.add_argument("--concurrency", type=int, default=4, help="config 5 jobs per worker")
+    ap.add_argument("--qps", type=float, default=50.0, help="config 5 offered job rate")
+    ap.add_argument("--src-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    ap.add_argument("--stage-dir", default="")
+    a = ap.parse_args(argv)
+    os.environ.setdefault("LOG_LEVEL", "error")
+    for c in a.config:
+        if c == 1:
+            out = asyncio.run(config1(a))
+        elif c in (3, 4):
+            out = asyncio.run(config_torrent(a, c))
+        elif c == 5:
+            out = asyncio.run(config5(a))
+        else:
+            raise SystemExit(f"config {c}: use bench.py for config 2")
+        print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -57,6 +57,7 @@ struct Upload {
 std::mutex g_mu;
 std::unordered_map<std::string, std::map<std::string, Object>> g_buckets;
 std::unordered_map<std::string, Upload> g_uploads;
+std::unordered_map<std::string, int> g_fail_counts;
 std::atomic<uint64_t> g_rx{0}, g_tx{0}, g_reqs{0}, g_objects{0}, g_upload_seq{1};
 std::vector<uint8_t> g_pool;  // random pool the origin serves from
 size_t g_keep_bytes = 1 << 20;
@@ -314,6 +315,16 @@ class Conn {
 
   bool origin(const Request& r) {
     uint64_t size = g_default_size, seed = 0;
+    // ?fail=N : the first N GETs of this exact URL answer 503 (retry-path fault injection)
+    auto fit = r.q.find("fail");
+    if (fit != r.q.end() && r.method == "GET") {
+      std::lock_guard<std::mutex> lk(g_mu);
+      int& seen = g_fail_counts[r.path + "?" + r.query];
+      if (seen < atoi(fit->second.c_str())) {
+        ++seen;
+        return respond(503, "Service Unavailable", "injected", "", "text/plain");
+      }
+    }
     auto it = r.q.find("size");
     if (it != r.q.end()) size = strtoull(it->second.c_str(), nullptr, 10);
     it = r.q.find("seed");

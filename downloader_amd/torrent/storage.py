@@ -68,6 +68,9 @@ class Storage:
         self.root = root
         self.paths = meta.local_files(root)
         self.fds: List[int] = []
+        # Only data that was on disk before we created/preallocated the files can be resumed;
+        # a fresh (sparse) layout needs no recheck pass at all.
+        self.preexisting = any(os.path.isfile(p) and os.path.getsize(p) > 0 for p, _ in self.paths)
         for p, n in self.paths:
             os.makedirs(os.path.dirname(p), exist_ok=True)
             fd = os.open(p, os.O_RDWR | os.O_CREAT | getattr(os, "O_CLOEXEC", 0), 0o644)
@@ -116,7 +119,7 @@ class Storage:
     def recheck(self, backend: str = "auto", threads: int = 0) -> Bitfield:
         """Verify every piece already on disk (resume after a crash)."""
         bf = Bitfield(self.meta.num_pieces)
-        if not any(os.path.exists(p) and os.path.getsize(p) for p, _ in self.paths):
+        if not self.preexisting:
             return bf
         ok = hashing.verify_pieces(self.paths, self.meta.piece_length, self.meta.pieces,
                                    threads=threads, backend=backend)
