@@ -126,7 +126,7 @@ class DownloadStage(Stage):
         await s3.relay_object(self.cfg.s3.bucket, key, url, size, Progress())
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
         job.stats.setdefault("streamed", []).append(
-            {"file": os.path.join(path, name), "key": key, "size": size})
+            {"file": os.path.join(path, name), "key": key, "size": size, "virtual": True})
         self._count("http", size)
         return True
 

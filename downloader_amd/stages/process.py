@@ -18,7 +18,7 @@ class ProcessStage(Stage):
     async def run(self, job: Job) -> Any:
         last = job.last_stage or {}
         root = last["path"]
-        if last.get("streamed"):
+        if last.get("streamed") and all(s.get("virtual") for s in last["streamed"]):
             # The download stage streamed a single selector-approved file straight to staging
             # (no disk hop); the walk result is that file.
             files = [s["file"] for s in last["streamed"]]
@@ -32,7 +32,10 @@ class ProcessStage(Stage):
             raise NoMediaFilesError()
         job.logger.info("found", len(files), "media files")
         job.logger.info({"files": files})
-        return {"files": files, "downloadPath": root}
+        out = {"files": files, "downloadPath": root}
+        if last.get("streamed"):   # eagerly staged torrent files: the upload stage skips them
+            out["streamed"] = [s for s in last["streamed"] if s["file"] in set(files)]
+        return out
 
 
 async def factory(cfg, services: Services) -> Stage:

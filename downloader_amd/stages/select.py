@@ -159,6 +159,43 @@ class MediaSelector:
         """Whether a lone top-level file with this name would be selected (stream fast path)."""
         return self._is_media(filename)
 
+    def find_virtual(self, root: str, rel_files: Sequence[str], media_type: int) -> List[str]:
+        """The same walk over a tree that does not exist yet - e.g. the file list of a torrent
+        before its data arrives - given as paths relative to ``root``. Returns the absolute
+        paths ``find(root, ...)`` will return once exactly those files are on disk."""
+        root = os.path.abspath(root)
+        movie = media_type == api.string_to_enum("MediaType", "MOVIE")
+        tree: dict = {}
+        for rel in rel_files:
+            node = tree
+            parts = [p for p in rel.split("/") if p]
+            for d in parts[:-1]:
+                node = node.setdefault(d, {})
+                if node is None:
+                    break
+            if parts:
+                node.setdefault(parts[-1], None)
+
+        def entries(node: dict) -> List[str]:
+            return sorted(node, key=os.fsencode)
+
+        root_entries = entries(tree)
+        files: List[str] = []
+        stack = [(root, tree, 0)]
+        while stack:
+            path, node, depth = stack.pop()
+            if node is None:
+                files.append(path)
+                continue
+            keep = []
+            for name in (root_entries if depth == 0 else entries(node)):
+                child = os.path.join(path, name)
+                sub = node[name]
+                if self._keep(root, root_entries, child, sub is not None, depth + 1, movie):
+                    keep.append((child, sub, depth + 1))
+            stack.extend(reversed(keep))
+        return files
+
 
 def find_media_files(root: str, media_type: int, logger: Optional[Logger] = None,
                      **kw) -> List[str]:

@@ -59,6 +59,28 @@ async def open_session(client: TorrentClient, uri: str, path: str, sv: Services)
     return await client.add_torrent(parse_torrent(data), path)
 
 
+async def _start_eager(session: TorrentSession, job: Job, path: str, cfg, sv: Services):
+    """Start staging selected files while downloading (torrent.eager) when the job directory
+    holds nothing but this torrent's files, so the virtual walk equals the later disk walk."""
+    from ..stages.base import ensure_staging_bucket
+    from ..stages.select import select_from_config
+    from .eager import EagerUploader
+    mine = {os.path.abspath(p) for p, _ in session.meta.local_files(path)}
+    for dp, _, fns in os.walk(path):
+        for fn in fns:
+            if os.path.abspath(os.path.join(dp, fn)) not in mine:
+                return None
+    rels = [os.path.relpath(p, path) for p, _ in session.meta.local_files(path)]
+    selected = select_from_config(cfg).find_virtual(path, rels, job.media.type)
+    if not selected:
+        return None
+    await ensure_staging_bucket(sv)
+    eager = EagerUploader(session, job, cfg, sv, selected)
+    session.piece_listeners.append(eager.on_piece)
+    eager.start()
+    return eager
+
+
 async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
                            client: Optional[TorrentClient] = None) -> int:
     d = cfg.download
@@ -82,6 +104,7 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
             raise MetadataStalled()
         job.logger.debug("hash", session.info_hash.hex())
         job.logger.debug("files", len(session.meta.files))
+        eager = await _start_eager(session, job, path, cfg, sv) if d.eager_upload else None
 
         # 2) progress ticker + stall watchdog around the transfer
         state = {"last_int": None, "last_progress": None}
@@ -111,6 +134,13 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
             done, _ = await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
             for t in done:
                 t.result()  # propagate DownloadStalled / session errors
+            if eager is not None:
+                job.stats.setdefault("streamed", []).extend(await eager.finish())
+                job.stats["eager_uploaded_bytes"] = eager.uploaded_bytes
+        except BaseException:
+            if eager is not None:
+                await eager.abort()
+            raise
         finally:
             for t in tasks:
                 t.cancel()

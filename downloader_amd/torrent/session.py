@@ -222,6 +222,7 @@ class TorrentSession:
         self._wake = asyncio.Event()
         self._closed = False
         self._ws_dead = 0
+        self.piece_listeners: List = []   # callbacks(piece index) after a piece is verified
         self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0}
         self.add_peers(list(peers), "magnet")
         if meta is not None:
@@ -434,6 +435,8 @@ class TorrentSession:
         if not self.have.set(idx):
             return
         self.verified_bytes += self.meta.piece_size(idx)
+        for cb in self.piece_listeners:
+            cb(idx)
         for p in list(self.peers.values()):
             await p.send_have(idx)
             if p.am_interested and p.bitfield is not None and not self.picker.peer_has_wanted(p.bitfield):

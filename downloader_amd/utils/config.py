@@ -89,6 +89,8 @@ class DownloadConfig(BaseModel):
     http_native: bool = True                    # native splice() transport for http://
     # Single selector-approved HTTP file -> relayed origin->S3 socket-to-socket (no disk hop).
     stream_http: bool = True
+    # Torrents: stage selected files part by part while the torrent is still downloading.
+    eager_upload: bool = True
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
@@ -152,6 +154,7 @@ class Config(BaseModel):
             self.download.http_streams = 1
             self.download.bucket_concurrency = 1
             self.download.stream_http = False
+            self.download.eager_upload = False
         else:
             self.broker.prefetch = max(self.broker.prefetch, self.concurrency)
         return self

@@ -145,3 +145,29 @@ def test_property_output_is_subset_and_media_only(tmp_path_factory, entries, mov
            and os.path.isfile(os.path.join(root, r))]
     for t in top:
         assert os.path.join(str(root), t) in files
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(st.tuples(st.lists(_seg, min_size=0, max_size=2),
+                          st.sampled_from(["a.mkv", "b.mp4", "c.txt", "S1.mkv", "e.webm"])),
+                min_size=1, max_size=8),
+       st.booleans())
+def test_virtual_walk_matches_disk_walk(tmp_path_factory, entries, movie):
+    """find_virtual (torrent file list before download) == find (tree on disk)."""
+    root = tmp_path_factory.mktemp("v")
+    rels = sorted({os.path.join(*d, f) if d else f for d, f in entries})
+    try:
+        make_tree(root, rels)
+    except (FileExistsError, NotADirectoryError, IsADirectoryError):
+        return
+    rels = [r for r in rels if os.path.isfile(os.path.join(root, r))]
+    sel = MediaSelector()
+    mt = MOVIE if movie else TV
+    assert sel.find_virtual(str(root), rels, mt) == sel.find(str(root), mt)
+
+
+def test_virtual_walk_reference_fixture(tmp_path):
+    rels = ["Season 1/KonoSuba S1E1.mkv", "Extras/KonoSuba OVA.mkv",
+            "Commentary/KonoSuba Season 1 Commentary.mkv", "S1/KonoSuba S1E1.mkv"]
+    got = MediaSelector().find_virtual("/job", rels, TV)
+    assert got == ["/job/S1/KonoSuba S1E1.mkv", "/job/Season 1/KonoSuba S1E1.mkv"]

@@ -387,3 +387,33 @@ def test_worker_progress_stall_acks(run, tmp_path, make_cfg, origin_cls):
         assert w.telemetry.statuses_of("tj4") == [2]
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_worker_torrent_eager_upload_collision_and_parts(run, tmp_path, make_cfg, origin_cls):
+    """Eager staging while downloading keeps the reference's key-collision rule (the later
+    file in walk order owns the key) and multipart objects are complete and correct."""
+    async def go():
+        from downloader_amd.models import api, keys
+        from downloader_amd.s3.fake_server import FakeS3
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src"
+        data = _tree(src / "Show", {"S1/ep.mkv": 9_000_001, "Season 1/ep.mkv": 7_000_003,
+                                    "Extras/ep.mkv": 1000})
+        for rel, d in data.items():
+            origin.blobs["/ws/Show/" + rel] = d
+        raw = make_torrent(str(src / "Show"), 65536, url_list=[origin.url("/ws/")])
+        origin.blobs["/t/s.torrent"] = raw
+        w = _worker(make_cfg, ep)
+        await w.start(health=False)
+        await w.submit(api.make_download("eg1", "http", origin.url("/t/s.torrent"), "TV"))
+        await _wait_results(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        k = keys.object_key("eg1", "ep.mkv")
+        assert s3.get("triton-staging", k) == data["Season 1/ep.mkv"]
+        assert s3.objects("triton-staging")[k].etag.endswith("-2")   # multipart (5 MiB parts)
+        assert w.metrics.sample("downloader_key_collisions_total") == 1
+        assert not s3.uploads.get("triton-staging")
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
