@@ -83,6 +83,23 @@ def build_blobd(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def build_selftest(kind: str, force: bool = False, verbose: bool = True) -> Path:
+    """Host-only sanitizer build of the native code's self-test."""
+    srcs = [CSRC / "selftest.cpp", CSRC / "hashing.cpp", CSRC / "transfer.cpp"]
+    BIN.mkdir(exist_ok=True)
+    out = BIN / f"selftest_{kind}"
+    if force or _stale(out, srcs + [CSRC / "native.h"]):
+        cxx = os.environ.get("CXX", "g++")
+        cmd = [cxx, "-O1", "-g", "-std=c++17", *SANITIZERS[kind], *[str(s) for s in srcs],
+               "-lcrypto", "-lpthread", "-o", str(out)]
+        _run(cmd, verbose)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = True, gpu: bool = True) -> None:
     build_native(force, verbose)
     if (CSRC / "blobd.cpp").exists():

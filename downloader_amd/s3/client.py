@@ -23,7 +23,7 @@ from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import quote
 
-from ..net.http import (FileRange, FileSink, HttpError, Progress, Response, TransportError,
+from ..net.http import (FileRange, FileSink, Progress, Response, TransportError,
                         TransportSet, make_transports)
 from . import sigv4
 

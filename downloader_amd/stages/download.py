@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import asyncio
 import os
-import secrets
 from typing import Any, Awaitable, Callable, Dict
 
 from ..fetch import bucket as bucket_src

@@ -38,6 +38,7 @@ class Origin:
         self.fail_status = {}   # path -> status
         self.truncate = set()   # paths whose body is cut short
         self.no_ranges = False
+        self.fail_ranges = {}   # Range header value -> remaining injected 503s
         self.chunked = set()
 
     async def start(self):
@@ -52,6 +53,9 @@ class Origin:
                 return web.Response(status=404, text="not found")
             hdrs = {} if self.no_ranges else {"Accept-Ranges": "bytes"}
             rng = req.headers.get("Range")
+            if rng and self.fail_ranges.get(rng, 0) > 0:
+                self.fail_ranges[rng] -= 1
+                return web.Response(status=503, text="injected range failure")
             if rng and not self.no_ranges:
                 a, _, b = rng[6:].partition("-")
                 s, e = int(a), int(b) if b else len(data) - 1
