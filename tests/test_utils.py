@@ -1,0 +1,108 @@
+"""Config (triton-core/config), dynamics, pino-style logging, tracing, metrics."""
+from __future__ import annotations
+
+import io
+import json
+import os
+
+from downloader_amd.utils.config import load_config
+from downloader_amd.utils.dynamics import dyn
+from downloader_amd.utils.log import Logger, ListSink, Sink
+from downloader_amd.utils.metrics import Metrics
+from downloader_amd.utils.trace import Tracer, parse_traceparent
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_defaults_pin_reference_constants():
+    c = load_config(env={})
+    assert c.download.torrent_metadata_timeout_s == 240        # lib/download.js:21
+    assert c.download.torrent_stall_timeout_s == 240
+    assert c.download.progress_interval_s == 30                # lib/download.js:88
+    assert c.s3.bucket == "triton-staging"                     # lib/upload.js:29
+    assert c.process.media_exts == [".mp4", ".mkv", ".mov", ".webm"]   # lib/process.js:15-20
+    assert c.broker.download_queue == "v1.download" and c.broker.convert_queue == "v1.convert"
+    assert c.health.port == 3401                               # lib/main.js:194
+    assert c.stages == ["download", "process", "upload"]       # lib/main.js:28-32
+
+
+def test_env_overrides_and_reference_env_flags():
+    env = {"STAGER_S3__ENDPOINT": "s3:9", "STAGER_CONCURRENCY": "7", "PORT": "4000",
+           "ALLOW_FILE_URLS": "true", "STAGER_DOWNLOAD__HTTP_STREAMS": "2"}
+    c = load_config(env=env)
+    assert c.s3.endpoint == "s3:9" and c.concurrency == 7 and c.broker.prefetch == 7
+    assert c.health.port == 4000 and c.download.allow_file_urls is True
+    assert c.download.http_streams == 2
+    assert load_config(env={"ALLOW_FILE_URLS": "1"}).download.allow_file_urls is False
+
+
+def test_reference_mode_is_serial():
+    c = load_config(env={}, overrides={"mode": "reference"})
+    assert (c.concurrency, c.broker.prefetch, c.s3.max_inflight_parts, c.s3.concurrent_files,
+            c.download.http_streams) == (1, 1, 1, 1, 1)
+    assert not c.download.stream_http and not c.download.eager_upload
+
+
+def test_yaml_file_and_converter_alias(tmp_path):
+    d = tmp_path / "config"
+    d.mkdir()
+    (d / "converter.yaml").write_text("instance:\n  download_path: /data/dl\n")
+    from downloader_amd.utils import config as cfgmod
+    p = cfgmod.find_config_file("downloader", [d])
+    assert p is not None and p.name == "converter.yaml"        # index.js:18 legacy name
+    c = load_config(path=str(p), env={})
+    assert str(c.resolved_download_root()) == "/data/dl"
+    ex = load_config(path=os.path.join(REPO, "config", "downloader.example.yaml"), env={})
+    assert ex.s3.bucket == "triton-staging"
+
+
+def test_relative_download_path_resolves_against_project_root():
+    c = load_config(env={}, overrides={"instance": {"download_path": "dl"}})
+    assert str(c.resolved_download_root()) == os.path.join(REPO, "dl")
+
+
+def test_dynamics_lookup_order():
+    assert dyn("rabbitmq", {"RABBITMQ_URL": "amqp://x"}) == "amqp://x"
+    assert dyn("rabbitmq", {"RABBITMQ_SERVICE_HOST": "10.0.0.1",
+                            "RABBITMQ_SERVICE_PORT": "5673"}) == "amqp://guest:guest@10.0.0.1:5673/"
+    assert dyn("rabbitmq", {}).startswith("amqp://")
+
+
+def test_pino_line_format_and_child_bindings():
+    buf = io.StringIO()
+    lg = Logger("main.js", sink=Sink(buf), level=20)
+    lg.child(jobId="j", fileId="f").info("hello", "world", extra=1)
+    rec = json.loads(buf.getvalue())
+    assert rec["level"] == 30 and rec["name"] == "main.js" and rec["msg"] == "hello world"
+    assert rec["jobId"] == "j" and rec["fileId"] == "f" and rec["extra"] == 1
+    assert {"time", "pid", "hostname"} <= set(rec)
+    sink = ListSink()
+    Logger("x", sink=sink, level=40).info("dropped")
+    assert sink.records == []
+
+
+def test_trace_spans_nest_and_propagate():
+    t = Tracer("downloader", enabled=False)
+    t.keep = True
+    with t.span("job") as job:
+        with t.span("stage.download"):
+            pass
+        tp = job.traceparent()
+    assert [s.name for s in t.finished] == ["stage.download", "job"]
+    assert t.finished[0].parent_id == t.finished[1].span_id
+    trace_id, span_id = parse_traceparent(tp)
+    with t.span("convert", traceparent=tp) as c:
+        pass
+    assert c.trace_id == trace_id and c.parent_id == span_id
+    assert parse_traceparent("garbage") is None
+
+
+def test_metrics_registry_exposition():
+    m = Metrics()
+    m.bytes_downloaded.labels("http").inc(10)
+    with m.time_stage("download"):
+        pass
+    text = m.exposition().decode()
+    assert 'downloader_bytes_downloaded_total{proto="http"} 10.0' in text
+    assert "downloader_stage_duration_seconds_count" in text
+    assert m.sample("downloader_bytes_downloaded_total", proto="http") == 10
