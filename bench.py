@@ -179,11 +179,17 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
     stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
     rx0 = blob.stats()["bytes_received"] if blob is not None else 0
+    peer_cpu0 = blob.cpu_seconds() if blob is not None else 0.0
+    t = os.times()
+    cpu0 = t.user + t.system
     try:
         out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root))
     finally:
         if not args.stage_dir:
             shutil.rmtree(stage_root, ignore_errors=True)
+    t = os.times()
+    out["worker_cpu_s"] = t.user + t.system - cpu0          # warmup + timed jobs
+    out["peer_cpu_s"] = (blob.cpu_seconds() - peer_cpu0) if blob is not None else 0.0
     dist.barrier()
     # The S3 peer's own byte counter must cover every byte the workers claim to have staged.
     out["sink_bytes"] = (blob.stats()["bytes_received"] - rx0) if blob is not None else 0
@@ -197,10 +203,13 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
         raise RuntimeError(f"{failed} timed jobs failed: {[r['err'] for r in allr if r['err']][:1]}")
     if sink < total_bytes:
         raise RuntimeError(f"S3 peer received {sink} bytes < {total_bytes} claimed staged")
+    gb_all = max(1e-9, sink / 1e9)
     return {"mbps": total_bytes / elapsed / 1e6, "elapsed": elapsed,
             "p50": statistics.median(lats) if lats else 0.0,
             "p90": sorted(lats)[int(0.9 * (len(lats) - 1))] if lats else 0.0,
-            "bytes": total_bytes, "sink_bytes": sink}
+            "bytes": total_bytes, "sink_bytes": sink,
+            "worker_cpu_s_per_GB": sum(r["worker_cpu_s"] for r in allr) / gb_all,
+            "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all}
 
 
 def main() -> int:
@@ -239,6 +248,8 @@ def main() -> int:
             "data": "synthetic random-byte media blobs served by the native blobd origin",
             "p50_job_latency_s": round(tuned["p50"], 4),
             "s3_peer_bytes_received": tuned["sink_bytes"],
+            "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
+            "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
             "peers": args.peers,
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,

@@ -57,6 +57,17 @@ class Blobd:
     def files_url(self, rel: str = "") -> str:
         return f"http://{self.endpoint}/files/{rel}"
 
+    def cpu_seconds(self) -> float:
+        """user+sys CPU time of the blobd process (from /proc/<pid>/stat)."""
+        if self.proc is None:
+            return 0.0
+        try:
+            with open(f"/proc/{self.proc.pid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            return 0.0
+
     def stats(self) -> Dict[str, int]:
         with urllib.request.urlopen(f"http://{self.endpoint}/_stats", timeout=10) as r:
             return json.loads(r.read())
