@@ -99,7 +99,7 @@ def cuda_sync() -> None:
     # not use the device for HTTP jobs, so this is a no-op unless torch already initialised it.
     try:
         import torch
-        if torch.cuda.is_available() and torch.cuda.is_initialized():
+        if torch.cuda.is_initialized():   # never initialise HIP just to synchronise
             torch.cuda.synchronize()
     except Exception:
         pass

@@ -246,9 +246,46 @@ async def config5(a) -> Dict:
             "torrent_jobs": n_torrent, "worker_exit_codes": codes}
 
 
+async def config_swarm(a) -> Dict:
+    """Extra (not in BASELINE.json): a peer-wire-only download from ``--seeders`` seeders
+    over loopback (no webseed), measuring the BEP-3 block pipeline + SHA-1 verification."""
+    from downloader_amd.torrent.client import TorrentClient
+    from downloader_amd.torrent.metainfo import make_torrent, parse_torrent
+    total = int(2e9 * a.scale)
+    src = tempfile.mkdtemp(prefix="swarm-src-", dir=a.src_dir)
+    dst = tempfile.mkdtemp(prefix="swarm-dst-", dir=a.stage_dir or None)
+    try:
+        p = os.path.join(src, "swarm.mkv")
+        _write_random(p, total, 99)
+        meta = parse_torrent(make_torrent(p, a.piece_mb << 20))
+        seeders = []
+        for _ in range(a.seeders):
+            c = await TorrentClient(max_uploads=64).start()
+            await c.add_torrent(meta, src)
+            seeders.append(c)
+        leech = await TorrentClient(max_peers=64, pipeline=a.pipeline).start()
+        t0 = time.perf_counter()
+        s = await leech.add_torrent(meta, dst, peers=[("127.0.0.1", c.listen_port) for c in seeders])
+        await asyncio.wait_for(s.wait(), 1800)
+        dt = time.perf_counter() - t0
+        out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
+               "piece_len": a.piece_mb << 20, "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
+               "hash_fails": s.stats["hash_fails"]}
+        await leech.close()
+        for c in seeders:
+            await c.close()
+        return out
+    finally:
+        shutil.rmtree(src, ignore_errors=True)
+        shutil.rmtree(dst, ignore_errors=True)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, action="append", required=True)
+    ap.add_argument("--config", type=int, action="append", required=True,
+                    help="1, 3, 4, 5 (BASELINE.json) or 6 (peer-wire swarm, extra)")
+    ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")
+    ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
     ap.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")
@@ -268,6 +305,8 @@ def main(argv=None) -> int:
             out = asyncio.run(config_torrent(a, c))
         elif c == 5:
             out = asyncio.run(config5(a))
+        elif c == 6:
+            out = asyncio.run(config_swarm(a))
         else:
             raise SystemExit(f"config {c}: use bench.py for config 2")
         print(json.dumps(out), flush=True)

@@ -48,6 +48,7 @@ class TorrentClient:
         self.seed_after_done = seed_after_done
         self.listen = listen
         self.pex_interval = 60.0
+        self.piece_cache_bytes = 64 << 20   # per-session LRU of pieces being served to peers
         self.dht_interval = 30.0
         self.max_announce_interval = 300.0
         self.sessions: Dict[bytes, TorrentSession] = {}

@@ -78,6 +78,7 @@ class PeerConn:
         self.up_bytes = 0
         self.hash_fails = 0
         self.connected_at = time.monotonic()
+        self.last_rx = self.connected_at
         self._wlock = asyncio.Lock()
 
     # ---------------------------------------------------------------- sending
@@ -127,6 +128,19 @@ class PeerConn:
         self.inflight[(piece, begin)] = time.monotonic()
         await self.send(REQUEST, struct.pack(">III", piece, begin, length))
 
+    async def request_many(self, blocks) -> None:
+        now = time.monotonic()
+        frames = []
+        for piece, begin, length in blocks:
+            self.inflight[(piece, begin)] = now
+            frames.append(self._frame(REQUEST, struct.pack(">III", piece, begin, length)))
+        if self.closed:
+            return
+        self.writer.write(b"".join(frames))
+        if self.writer.transport.get_write_buffer_size() > 1 << 20:
+            async with self._wlock:
+                await self.writer.drain()
+
     async def cancel(self, piece: int, begin: int, length: int) -> None:
         if self.inflight.pop((piece, begin), None) is not None:
             await self.send(CANCEL, struct.pack(">III", piece, begin, length))
@@ -141,7 +155,19 @@ class PeerConn:
         except Exception:
             pass
 
+    async def _idle_watchdog(self) -> None:
+        # One timer per connection instead of a wait_for() around every read (which costs a
+        # task + timer handle per message on the hot path).
+        period = max(1.0, self.s.idle_timeout / 4)
+        while not self.closed:
+            await asyncio.sleep(period)
+            if time.monotonic() - self.last_rx > self.s.idle_timeout:
+                self.close()
+                return
+
     async def run(self) -> None:
+        wd = asyncio.get_running_loop().create_task(self._idle_watchdog())
+        read = self.reader.readexactly
         try:
             if self.supports_ext:
                 await self.send_ext_handshake()
@@ -149,18 +175,19 @@ class PeerConn:
             if self.s.client.dht is not None and self.supports_dht:
                 await self.send(PORT, struct.pack(">H", self.s.client.dht.port))
             while not self.closed:
-                hdr = await asyncio.wait_for(self.reader.readexactly(4), self.s.idle_timeout)
-                n = struct.unpack(">I", hdr)[0]
+                n = struct.unpack(">I", await read(4))[0]
+                self.last_rx = time.monotonic()
                 if n == 0:
                     continue
                 if n > MAX_MSG:
                     raise ProtocolError(f"message too large ({n})")
-                body = await asyncio.wait_for(self.reader.readexactly(n), self.s.idle_timeout)
+                body = await read(n)
                 await self._dispatch(body[0], memoryview(body)[1:])
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError, OSError,
                 ProtocolError):
             pass
         finally:
+            wd.cancel()
             self.close()
             self.s.peer_closed(self)
 

@@ -20,6 +20,7 @@ import os
 import random
 import struct
 import time
+from collections import OrderedDict
 from typing import TYPE_CHECKING, Dict, List, Optional, Set, Tuple
 from urllib.parse import quote
 
@@ -126,6 +127,38 @@ class PiecePicker:
                         return ap.idx, b * BLOCK, ap.block_len(b)
         return None
 
+    def next_blocks(self, peer_id: int, bf: Bitfield, k: int) -> List[Tuple[int, int, int]]:
+        """Up to ``k`` blocks for one peer in one pass: free blocks of active pieces first,
+        then whole new (rarest) pieces, then endgame duplicates."""
+        out: List[Tuple[int, int, int]] = []
+        for ap in self.active.values():
+            if len(out) >= k:
+                return out
+            if ap.idx not in bf or ap.got + len(ap.req) >= ap.nblocks and 0 not in ap.state:
+                continue
+            for b in range(ap.nblocks):
+                if ap.state[b] == 0:
+                    ap.state[b] = 1
+                    ap.req.setdefault(b, set()).add(peer_id)
+                    out.append((ap.idx, b * BLOCK, ap.block_len(b)))
+                    if len(out) >= k:
+                        return out
+        while len(out) < k:
+            nb = self.next_block(peer_id, bf)
+            if nb is None:
+                break
+            out.append(nb)
+            ap = self.active.get(nb[0])
+            if ap is not None and nb[1] == 0:      # a fresh piece: take its remaining blocks
+                for b in range(1, ap.nblocks):
+                    if len(out) >= k:
+                        break
+                    if ap.state[b] == 0:
+                        ap.state[b] = 1
+                        ap.req.setdefault(b, set()).add(peer_id)
+                        out.append((ap.idx, b * BLOCK, ap.block_len(b)))
+        return out
+
     def release(self, peer_id: int, piece: int, begin: int) -> None:
         ap = self.active.get(piece)
         if ap is None:
@@ -223,6 +256,8 @@ class TorrentSession:
         self._closed = False
         self._ws_dead = 0
         self.piece_listeners: List = []   # callbacks(piece index) after a piece is verified
+        self._piece_cache: "OrderedDict[int, bytes]" = OrderedDict()   # LRU of served pieces
+        self._piece_cache_bytes = 0
         self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0}
         self.add_peers(list(peers), "magnet")
         if meta is not None:
@@ -385,11 +420,14 @@ class TorrentSession:
     async def fill(self, pc: PeerConn) -> None:
         if self.picker is None or pc.peer_choking or not pc.am_interested or pc.bitfield is None:
             return
-        while len(pc.inflight) < self.client.pipeline:
-            nb = self.picker.next_block(id(pc), pc.bitfield)
-            if nb is None:
-                break
-            await pc.request(*nb)
+        room = self.client.pipeline - len(pc.inflight)
+        # Refill in batches (at least a quarter of the pipeline) so one write carries many
+        # REQUEST messages instead of one syscall per 17-byte message.
+        if room < max(1, self.client.pipeline // 4):
+            return
+        blocks = self.picker.next_blocks(id(pc), pc.bitfield, room)
+        if blocks:
+            await pc.request_many(blocks)
 
     async def on_block(self, pc: PeerConn, idx: int, begin: int, data: bytes) -> None:
         if self.picker is None or self.have is None:
@@ -449,11 +487,21 @@ class TorrentSession:
             return
         if ln > 131072 or begin + ln > self.meta.piece_size(idx):
             return
-        data = await asyncio.get_running_loop().run_in_executor(
-            None, self.storage.read_block, idx, begin, ln)
+        piece = self._piece_cache.get(idx)
+        if piece is None:
+            # Read the whole piece once (one thread-pool hop) and serve its blocks from memory.
+            piece = await asyncio.get_running_loop().run_in_executor(
+                None, self.storage.read, idx * self.meta.piece_length, self.meta.piece_size(idx))
+            self._piece_cache[idx] = piece
+            self._piece_cache_bytes += len(piece)
+            while self._piece_cache_bytes > self.client.piece_cache_bytes and self._piece_cache:
+                old = next(iter(self._piece_cache))
+                self._piece_cache_bytes -= len(self._piece_cache.pop(old))
+        else:
+            self._piece_cache.move_to_end(idx)
         pc.up_bytes += ln
         self.uploaded += ln
-        await pc.send(PIECE, struct.pack(">II", idx, begin) + data)
+        await pc.send(PIECE, struct.pack(">II", idx, begin) + piece[begin:begin + ln])
 
     # ---------------------------------------------------------------- metadata (BEP-9)
     async def on_ext_handshake(self, pc: PeerConn) -> None:
