@@ -212,9 +212,27 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
             "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all}
 
 
+def pin_rank(dist: Dist) -> list:
+    """With N>1 ranks on one node, give each rank (worker threads + its blobd, which inherits
+    the mask) a disjoint, contiguous slice of the allowed CPUs: no cross-rank cache thrash and
+    sockets/threads stay on one CCD/NUMA domain. Returns the slice ([] = unpinned)."""
+    if dist.world <= 1 or os.environ.get("STAGER_BENCH_NO_PIN") == "1":
+        return []
+    cpus = sorted(os.sched_getaffinity(0))
+    local = int(os.environ.get("LOCAL_RANK", dist.rank))
+    nlocal = int(os.environ.get("LOCAL_WORLD_SIZE", dist.world))
+    per = len(cpus) // max(1, nlocal)
+    if per < 2:
+        return []
+    mine = cpus[local * per:(local + 1) * per]
+    os.sched_setaffinity(0, mine)
+    return mine
+
+
 def main() -> int:
     args = parse()
     dist = Dist(args.gpus)
+    pinned = pin_rank(dist)
     from downloader_amd.bench.infra import Blobd
     blob = None
     endpoint = None
@@ -251,6 +269,7 @@ def main() -> int:
             "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
             "peers": args.peers,
+            "cpus_per_rank": len(pinned) if pinned else len(os.sched_getaffinity(0)),
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
             "staging": args.staging if args.mode == "tuned" else "disk",
