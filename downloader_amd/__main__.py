@@ -35,13 +35,13 @@ def _worker(args) -> int:
         cfg.apply_mode()
 
     async def main() -> int:
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGINT, signal.SIGTERM):   # before start(): no startup window
+            loop.add_signal_handler(sig, stop.set)
         w = Worker(cfg, logger=get_logger("main"))
         await w.start()
         log.info("initialized")
-        stop = asyncio.Event()
-        loop = asyncio.get_running_loop()
-        for sig in (signal.SIGINT, signal.SIGTERM):
-            loop.add_signal_handler(sig, stop.set)
 
         def on_error(loop, ctx):
             log.error("Unhandled exception", str(ctx.get("exception") or ctx.get("message")))

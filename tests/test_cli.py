@@ -1,0 +1,89 @@
+"""Command-line entrypoint (reference index.js + operational tools)."""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cli(*args, env=None, timeout=120):
+    e = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    e.update(env or {})
+    return subprocess.run([sys.executable, "-m", "downloader_amd", *args], capture_output=True,
+                          text=True, timeout=timeout, env=e, cwd=REPO)
+
+
+def test_make_torrent_and_verify_roundtrip(tmp_path):
+    src = tmp_path / "Show"
+    (src / "S1").mkdir(parents=True)
+    (src / "S1" / "a.mkv").write_bytes(os.urandom(300_000))
+    (src / "b.mkv").write_bytes(os.urandom(5))
+    out = tmp_path / "show.torrent"
+    r = _cli("make-torrent", str(src), "-o", str(out), "--piece-length", "16384",
+             "--webseed", "http://ws/", "--tracker", "udp://t:1")
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout)
+    assert info["bytes"] == 300_005 and info["pieces"] == (300_005 + 16383) // 16384
+    r = _cli("verify", str(out), str(tmp_path), "--backend", "cpu")
+    assert r.returncode == 0, r.stderr
+    v = json.loads(r.stdout)
+    assert v["good"] == v["pieces"] and v["backend"] == "cpu"
+    with open(src / "S1" / "a.mkv", "r+b") as f:
+        f.write(b"\x00\x01")
+    r = _cli("verify", str(out), str(tmp_path), "--backend", "cpu")
+    assert r.returncode == 1 and json.loads(r.stdout)["good"] == v["pieces"] - 1
+
+
+def test_config_command_prints_effective_config():
+    r = _cli("config", env={"STAGER_S3__BUCKET": "other", "PORT": "4123"})
+    assert r.returncode == 0, r.stderr
+    c = json.loads(r.stdout)
+    assert c["s3"]["bucket"] == "other" and c["health"]["port"] == 4123
+
+
+def test_submit_publishes_download(run):
+    async def go():
+        from downloader_amd.broker.amqp import AmqpBroker
+        from downloader_amd.broker.server import BrokerServer
+        from downloader_amd.models import api
+        srv = await BrokerServer().start()
+        c = AmqpBroker(srv.url)
+        await c.connect()
+        await c.declare("v1.download")
+        r = await asyncio.get_running_loop().run_in_executor(None, lambda: _cli(
+            "submit", "m42", "http", "http://o/x.mkv", "--type", "TV", "--creator", "card7",
+            env={"STAGER_BROKER__URL": srv.url}))
+        assert r.returncode == 0, r.stderr
+        d = await c.get("v1.download")
+        m = api.decode(api.Download, d.body)
+        assert (m.media.id, m.media.creatorId, m.media.sourceURI) == ("m42", "card7", "http://o/x.mkv")
+        assert m.media.type == api.string_to_enum("MediaType", "TV")
+        await c.close()
+        await srv.stop()
+    run(go())
+
+
+def test_worker_exits_zero_on_sigterm_when_idle(run, tmp_path):
+    async def go():
+        import signal
+        from downloader_amd.broker.server import BrokerServer
+        srv = await BrokerServer().start()
+        env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error", STAGER_BROKER__URL=srv.url,
+                   STAGER_HEALTH__PORT="0", STAGER_INSTANCE__DOWNLOAD_PATH=str(tmp_path),
+                   STAGER_DOWNLOAD__TORRENT_ENABLE_DHT="false")
+        p = await asyncio.create_subprocess_exec(sys.executable, "-m", "downloader_amd", "worker",
+                                                 env=env, cwd=REPO)
+        for _ in range(200):
+            q = srv.queues.get("v1.download")
+            if q is not None and q.consumers:
+                break
+            await asyncio.sleep(0.05)
+        p.send_signal(signal.SIGTERM)
+        code = await asyncio.wait_for(p.wait(), 30)
+        assert code == 0            # termHandler: exit(0) when no job is in flight
+        await srv.stop()
+    run(go(), timeout=60)
