@@ -5,7 +5,7 @@ BASELINE.json names the metric "MB/s staged end-to-end (download->S3) + p50 job 
 1/2/4/8 workers" and config 2 "100x100 MB HTTP URLs, N concurrent workers -> MinIO multipart".
 One rank = one worker process (the reference's scaling unit: one consumer per container,
 SURVEY §2.6). One "step" = every worker stages a batch of ``--jobs-per-step`` 100 MB
-random-byte media blobs (default 8; like a training batch, it keeps the timed region long
+random-byte media blobs (default 16; like a training batch, it keeps the timed region long
 enough to be stable), each job being:
 HTTP GET from the origin -> staging dir on disk -> media selection -> multipart PUT to the
 S3 endpoint -> done marker -> api.Convert published -> ack. Weak scaling: per-worker work is
@@ -42,7 +42,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--size-mb", type=float, default=100.0, help="object size in MB (1e6 B)")
     p.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
     p.add_argument("--concurrency", type=int, default=4, help="jobs in flight per worker")
-    p.add_argument("--jobs-per-step", type=int, default=8, help="jobs per worker per step")
+    p.add_argument("--jobs-per-step", type=int, default=16, help="jobs per worker per step")
     p.add_argument("--stage-dir", default="", help="download_path (default: a temp dir)")
     p.add_argument("--http-streams", type=int, default=0, help="override download.http_streams")
     p.add_argument("--part-mb", type=int, default=0, help="override s3.part_size (MiB)")
