@@ -6,14 +6,17 @@ BASELINE.json names the metric "MB/s staged end-to-end (download->S3) + p50 job 
 One rank = one worker process (the reference's scaling unit: one consumer per container,
 SURVEY §2.6). One "step" = every worker stages a batch of ``--jobs-per-step`` 100 MB
 random-byte media blobs (default 16; like a training batch, it keeps the timed region long
-enough to be stable), each job being:
-HTTP GET from the origin -> staging dir on disk -> media selection -> multipart PUT to the
-S3 endpoint -> done marker -> api.Convert published -> ack. Weak scaling: per-worker work is
-fixed as N grows.
+enough to be stable), each job being the worker's full path: done-marker probe -> HTTP
+origin -> (default ``--staging stream``: each multipart part relayed origin->S3 by splice;
+``--staging disk``: download to the job dir first) -> media selection -> S3 multipart upload
+-> done marker -> api.Convert published -> ack. Weak scaling: per-worker work is fixed as N
+grows.
 
 Launch: ``python bench.py`` (N=1) or ``python -m torch.distributed.run --nproc-per-node N
-bench.py --gpus N``. Rank 0 starts the native ``blobd`` peer (origin + S3 sink) and shares its
-port; ranks synchronise over gloo (the workload is host-side: there is no tensor compute).
+bench.py --gpus N``. Each rank starts its own native ``blobd`` peer (origin + S3 sink;
+``--peers shared`` = one on rank 0) and, for N>1, pins itself to a disjoint CPU slice; ranks
+synchronise over gloo (the workload is host-side: there is no tensor compute). The run fails
+if the S3 peer received fewer bytes than the workers claim to have staged.
 """
 from __future__ import annotations
 

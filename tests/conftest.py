@@ -39,6 +39,7 @@ class Origin:
         self.truncate = set()   # paths whose body is cut short
         self.no_ranges = False
         self.fail_ranges = {}   # Range header value -> remaining injected 503s
+        self.slow = {}          # path -> bytes/s trickle rate
         self.chunked = set()
 
     async def start(self):
@@ -69,6 +70,15 @@ class Origin:
                 await resp.prepare(req)
                 await resp.write(data[: len(data) // 2])
                 req.transport.close()
+                return resp
+            if req.path in self.slow:            # trickle the body at `slow[path]` bytes/s
+                rate = self.slow[req.path]
+                resp = web.StreamResponse(status=200, headers={"Content-Length": str(len(data))})
+                await resp.prepare(req)
+                step = max(1, int(rate / 20))
+                for i in range(0, len(data), step):
+                    await resp.write(data[i:i + step])
+                    await asyncio.sleep(0.05)
                 return resp
             if req.path in self.chunked:
                 resp = web.StreamResponse(status=200)

@@ -230,3 +230,43 @@ def test_worker_over_amqp(run, make_cfg, origin_cls):
         assert s3.get("triton-staging", keys.object_key("aj", "a.mkv")) == origin.blobs["/a.mkv"]
         await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_broker_drop_mid_job_redelivers_and_dedups(run, make_cfg, origin_cls):
+    """The broker connection dies while a job is running: the ack of the dead connection is
+    moot, the broker requeues the delivery, the reconnected worker sees it again and the
+    done marker turns the redelivery into a skip (no duplicate upload)."""
+    async def go():
+        from downloader_amd.models import api
+        from downloader_amd.s3.fake_server import FakeS3
+        from downloader_amd.service.worker import Worker
+        srv = await BrokerServer().start()
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        origin.blobs["/slow.mkv"] = os.urandom(200_000)
+        gate = asyncio.Event()
+
+        def hook(method, path):
+            if path.endswith("/done") and method == "PUT" and not gate.is_set():
+                srv.drop_connections()          # kill AMQP right before the job completes
+                gate.set()
+        s3.hooks.append(hook)
+        cfg = make_cfg(ep, broker={"backend": "amqp", "url": srv.url, "reconnect_delay_s": 0.05})
+        w = Worker(cfg)
+        await w.start(health=False)
+        client = AmqpBroker(srv.url, reconnect_delay=0.05)
+        await client.connect()
+        await client.publish("v1.download", api.encode(api.make_download("bd1", "http",
+                                                                          origin.url("/slow.mkv"))))
+        for _ in range(500):
+            if len(w.results) >= 2:
+                break
+            await asyncio.sleep(0.02)
+        # the redelivered copy may finish first (it only probes the marker and publishes)
+        outcomes = sorted(r.outcome for r in w.results)
+        assert outcomes == ["skipped", "staged"], outcomes
+        puts = [p for m, p in s3.requests if m == "PUT" and p.endswith("/done")]
+        assert len(puts) == 1
+        await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()
+    run(go(), timeout=60)

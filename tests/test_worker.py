@@ -384,3 +384,20 @@ def test_multipart_upload_resume_reuses_parts(run, make_cfg, origin_cls):
         assert not s3.uploads.get("triton-staging")
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_http_stall_floor_fails_slow_transfer(run, make_cfg, origin_cls):
+    """A bytes/s floor (``download.http_min_rate``) turns a crawling origin into a failure the
+    retry policy can handle (the reference has no HTTP stall detection at all)."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0},
+                                        download={"stream_http": False, "http_streams": 1,
+                                                  "http_min_rate": 1e6, "http_timeout_s": 0.5})
+        origin.blobs["/crawl.mkv"] = os.urandom(4 * 1024 * 1024)
+        origin.slow["/crawl.mkv"] = 100_000          # 100 kB/s < the 1 MB/s floor
+        await w.submit(api.make_download("sl1", "http", origin.url("/crawl.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "dead"
+        assert "B/s" in w.results[0].error
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
