@@ -329,9 +329,9 @@ class TorrentSession:
             self._finish()
 
     def _finish(self) -> None:
+        # No fsync here: staged files are uploaded and deleted right after, and a crashed
+        # attempt is recovered by re-verifying what is on disk (recheck), not by durability.
         if not self.done.is_set():
-            if self.storage is not None:
-                self.storage.sync()
             self.done.set()
             for t in self.trackers:
                 self._spawn(self._announce_once(t, "completed"))
