@@ -141,8 +141,12 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             setup_s = time.perf_counter() - t0
             with open(os.path.join(src, "job.torrent"), "wb") as f:
                 f.write(raw)
-            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1,
-                            download={"verify_backend": a.verify_backend}),
+            dl = {"verify_backend": a.verify_backend}
+            if a.webseed_streams:
+                dl["webseed_streams"] = a.webseed_streams
+            if a.webseed_chunk_mb:
+                dl["webseed_chunk"] = a.webseed_chunk_mb << 20
+            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl),
                        broker=MemoryBroker())
             await w.start(health=False)
             m = api.make_download(f"c{cfg_no}-{a.mode}", "http", b.files_url("job.torrent"),
@@ -291,6 +295,8 @@ def main(argv=None) -> int:
     ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")
     ap.add_argument("--piece-mb", type=int, default=4)
     ap.add_argument("--verify-backend", choices=["cpu", "gpu", "auto"], default="auto")
+    ap.add_argument("--webseed-streams", type=int, default=0)
+    ap.add_argument("--webseed-chunk-mb", type=int, default=0)
     ap.add_argument("--workers", type=int, default=4, help="config 5 worker processes")
     ap.add_argument("--concurrency", type=int, default=4, help="config 5 jobs per worker")
     ap.add_argument("--qps", type=float, default=50.0, help="config 5 offered job rate")

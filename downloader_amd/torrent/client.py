@@ -62,7 +62,8 @@ class TorrentClient:
         return cls(transports=transports, listen_port=d.torrent_listen_port,
                    max_peers=d.torrent_max_peers, pipeline=d.torrent_request_pipeline,
                    enable_dht=d.torrent_enable_dht, verify_backend=d.verify_backend,
-                   webseed_streams=max(1, d.http_streams),
+                   webseed_streams=max(1, d.webseed_streams or d.http_streams),
+                   webseed_chunk=d.webseed_chunk,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":
