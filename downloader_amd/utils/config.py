@@ -100,8 +100,8 @@ class DownloadConfig(BaseModel):
     torrent_enable_trackers: bool = True
     torrent_enable_webseeds: bool = True
     torrent_request_pipeline: int = 16
-    webseed_streams: int = 0                    # concurrent Range GETs per webseed (0: http_streams)
-    webseed_chunk: int = 32 * MiB               # bytes of whole pieces per webseed request run
+    webseed_streams: int = 8                    # concurrent Range GETs per webseed (0: http_streams)
+    webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     cleanup_on_stall: bool = True               # App. A #6 (reference leaves data behind)
     emit_errored_on_stall: bool = False         # App. A #6 (reference: ack silently)
 
@@ -155,6 +155,7 @@ class Config(BaseModel):
             self.s3.max_inflight_parts = 1
             self.download.http_streams = 1
             self.download.bucket_concurrency = 1
+            self.download.webseed_streams = 1
             self.download.stream_http = False
             self.download.eager_upload = False
         else:
