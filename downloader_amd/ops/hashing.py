@@ -5,6 +5,7 @@ torrent creation (bench fixtures), S3 SigV4 payload hashes and Content-MD5 / ETa
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import List, Optional, Sequence, Tuple
 
@@ -58,14 +59,38 @@ def hash_file_ranges(path: str, ranges: Sequence[Tuple[int, int]], algo: str,
 
 _gpu_lock = threading.Lock()
 _gpu_verifier = None
+# A cold verifier pays HIP init + 2 pinned staging slots (~0.3-1 s): "auto" uses the GPU for
+# a cold start only when the recheck is big enough to amortise it.
+GPU_COLD_MIN_BYTES = 32 << 30
+
+
+def gpu_device() -> int:
+    """One worker per GPU: ``STAGER_GPU_DEVICE``, else worker index / LOCAL_RANK modulo the
+    visible device count."""
+    if os.environ.get("STAGER_GPU_DEVICE"):
+        return int(os.environ["STAGER_GPU_DEVICE"])
+    idx = int(os.environ.get("STAGER_WORKER_INDEX", os.environ.get("LOCAL_RANK", "0")) or 0)
+    try:
+        n = gpuhash().device_count()
+    except Exception:
+        n = 1
+    return idx % max(1, n)
 
 
 def _verifier():
     global _gpu_verifier
     with _gpu_lock:
         if _gpu_verifier is None:
-            _gpu_verifier = gpuhash().GpuVerifier(0, 256 << 20, 8)
+            _gpu_verifier = gpuhash().GpuVerifier(gpu_device(), 256 << 20, 8)
         return _gpu_verifier
+
+
+def prewarm_gpu() -> bool:
+    """Create the verifier now (worker start-up) so later rechecks see a warm device."""
+    if not gpu_available():
+        return False
+    _verifier()
+    return True
 
 
 def choose_backend(requested: str, total_bytes: int, n_pieces: int) -> str:
@@ -75,7 +100,10 @@ def choose_backend(requested: str, total_bytes: int, n_pieces: int) -> str:
         if not gpu_available():
             raise RuntimeError("verify_backend=gpu but no HIP device is available")
         return "gpu"
-    if total_bytes >= GPU_MIN_BYTES and n_pieces >= GPU_MIN_PIECES and gpu_available():
+    if total_bytes < GPU_MIN_BYTES or n_pieces < GPU_MIN_PIECES:
+        return "cpu"
+    warm = _gpu_verifier is not None
+    if (warm or total_bytes >= GPU_COLD_MIN_BYTES) and gpu_available():
         return "gpu"
     return "cpu"
 

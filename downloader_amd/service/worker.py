@@ -93,6 +93,13 @@ class Worker:
             await self.broker.declare(q)
         if not self.stages:
             self.stages = await build_stages(self.cfg.stages, self.cfg, self.services)
+        if self.cfg.download.gpu_prewarm and self.cfg.download.verify_backend != "cpu":
+            from ..ops.hashing import prewarm_gpu
+            try:
+                warm = await asyncio.get_running_loop().run_in_executor(None, prewarm_gpu)
+                self.log.info({"gpu_verifier": warm}, "gpu verifier prewarm")
+            except Exception as e:  # a missing device must not stop the worker
+                self.log.warn({"err": str(e)}, "gpu verifier prewarm failed")
 
     async def start(self, health: bool = True) -> None:
         await self.init()

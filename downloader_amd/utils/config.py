@@ -94,6 +94,9 @@ class DownloadConfig(BaseModel):
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
+    # Initialise the GPU verifier at worker start (device = worker index % GPUs) so "auto"
+    # rechecks of >=256 MiB go to the GPU instead of paying the cold start per job.
+    gpu_prewarm: bool = False
     torrent_listen_port: int = 0
     torrent_max_peers: int = 32
     torrent_enable_dht: bool = True

@@ -122,3 +122,9 @@ def test_gpu_matches_cpu_backend_and_reports_throughput(gv, tmp_path):
     tc = time.perf_counter() - t0
     assert g == c == b"\x01" * 256
     print(f"verify 256 MiB: gpu {len(data) / tg / 1e9:.2f} GB/s, cpu {len(data) / tc / 1e9:.2f} GB/s")
+
+
+def test_prewarm_makes_auto_pick_gpu():
+    from downloader_amd.ops import hashing
+    assert hashing.prewarm_gpu() is True
+    assert hashing.choose_backend("auto", hashing.GPU_MIN_BYTES, 1024) == "gpu"

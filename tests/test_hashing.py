@@ -85,3 +85,30 @@ def test_hash_file_ranges(tmp_path):
 def test_choose_backend_cpu_without_gpu():
     assert hashing.choose_backend("cpu", 1 << 40, 1 << 20) == "cpu"
     assert hashing.choose_backend("auto", 100, 1) == "cpu"
+
+
+def test_auto_backend_accounts_for_cold_start(monkeypatch):
+    monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    monkeypatch.setattr(hashing, "_gpu_verifier", None)
+    big, cold = hashing.GPU_MIN_BYTES, hashing.GPU_COLD_MIN_BYTES
+    # Cold device: only a recheck large enough to amortise HIP init goes to the GPU.
+    assert hashing.choose_backend("auto", big, 1024) == "cpu"
+    assert hashing.choose_backend("auto", cold, 1024) == "gpu"
+    # Few pieces never pay off, warm or not.
+    assert hashing.choose_backend("auto", cold, 8) == "cpu"
+    monkeypatch.setattr(hashing, "_gpu_verifier", object())
+    assert hashing.choose_backend("auto", big, 1024) == "gpu"
+    assert hashing.choose_backend("auto", big - 1, 1024) == "cpu"
+
+
+def test_gpu_device_from_worker_index(monkeypatch):
+    class _G:
+        @staticmethod
+        def device_count():
+            return 8
+    monkeypatch.setattr(hashing, "gpuhash", lambda: _G)
+    monkeypatch.delenv("STAGER_GPU_DEVICE", raising=False)
+    monkeypatch.setenv("STAGER_WORKER_INDEX", "11")
+    assert hashing.gpu_device() == 3
+    monkeypatch.setenv("STAGER_GPU_DEVICE", "5")
+    assert hashing.gpu_device() == 5
