@@ -132,3 +132,9 @@ class NullLogger(Logger):
 
     def child(self, **bindings: Any) -> "Logger":
         return self
+
+
+def make_test_logger(name: str = "test") -> Logger:
+    """Logger for tests: silent unless ``USE_REAL_LOGGER`` is set (the reference's test switch,
+    test/process/filter_dirs.js:19)."""
+    return get_logger(name) if os.environ.get("USE_REAL_LOGGER") else NullLogger()

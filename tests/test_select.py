@@ -13,9 +13,11 @@ from hypothesis import strategies as st
 
 from downloader_amd.models import api
 from downloader_amd.stages.select import MediaSelector, find_media_files, node_extname
+from downloader_amd.utils.log import NullLogger, make_test_logger
 
 TV = api.string_to_enum("MediaType", "TV")
 MOVIE = api.string_to_enum("MediaType", "MOVIE")
+LOG = make_test_logger("process")  # USE_REAL_LOGGER=1 shows the selector's decisions
 
 
 def make_tree(root, files):
@@ -31,7 +33,7 @@ def test_should_filter_non_season_directories(tmp_path):
     root = make_tree(tmp_path / "should_filter_non_season_directories", [
         "Season 1/KonoSuba S1E1.mkv", "Extras/KonoSuba OVA.mkv",
         "Commentary/KonoSuba Season 1 Commentary.mkv", "S1/KonoSuba S1E1.mkv"])
-    files = find_media_files(root, TV)
+    files = find_media_files(root, TV, LOG)
     assert len(files) == 2
     assert files[0] == os.path.join(root, "S1/KonoSuba S1E1.mkv")
     assert files[1] == os.path.join(root, "Season 1/KonoSuba S1E1.mkv")
@@ -40,47 +42,47 @@ def test_should_filter_non_season_directories(tmp_path):
 def test_should_read_all_dirs_when_processing_a_movie(tmp_path):
     # reference: test/process/filter_dirs.js:43-61
     root = make_tree(tmp_path / "movie", ["Some Movie Dir/Your Name.mkv"])
-    files = find_media_files(root, MOVIE)
+    files = find_media_files(root, MOVIE, LOG)
     assert files == [os.path.join(root, "Some Movie Dir/Your Name.mkv")]
 
 
 def test_should_read_with_top_level_dir(tmp_path):
     # reference: test/process/filter_dirs.js:63-81 ("should real with top level dir")
     root = make_tree(tmp_path / "top", ["Some Movie Dir/Your Name.mkv"])
-    files = find_media_files(root, TV)
+    files = find_media_files(root, TV, LOG)
     assert files == [os.path.join(root, "Some Movie Dir/Your Name.mkv")]
 
 
 def test_movie_keeps_extras(tmp_path):
     root = make_tree(tmp_path / "m", ["Extras/a.mkv", "Main/b.mp4", "c.webm", "d.txt"])
-    files = [os.path.relpath(f, root) for f in find_media_files(root, MOVIE)]
+    files = [os.path.relpath(f, root) for f in find_media_files(root, MOVIE, LOG)]
     assert files == ["Extras/a.mkv", "Main/b.mp4", "c.webm"]
 
 
 def test_tv_season_regex_is_unanchored(tmp_path):
     # App. B: /s\d+|season/i matches "Videos2" (s2) but not "Specials"
     root = make_tree(tmp_path / "t", ["Videos2/a.mkv", "Specials/b.mkv", "x.mov"])
-    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV, LOG)]
     assert files == ["Videos2/a.mkv", "x.mov"]
 
 
 def test_extension_case_sensitive_by_default(tmp_path):
     root = make_tree(tmp_path / "c", ["A.MKV", "b.mkv"])
-    assert [os.path.basename(f) for f in find_media_files(root, MOVIE)] == ["b.mkv"]
+    assert [os.path.basename(f) for f in find_media_files(root, MOVIE, LOG)] == ["b.mkv"]
     sel = MediaSelector(case_insensitive_exts=True)
     assert [os.path.basename(f) for f in sel.find(root, MOVIE)] == ["A.MKV", "b.mkv"]
 
 
 def test_depth_first_lexicographic_order(tmp_path):
     root = make_tree(tmp_path / "o", ["b/2.mkv", "b/1.mkv", "a/z.mkv", "a/S01/e.mkv", "0.mkv"])
-    files = [os.path.relpath(f, root) for f in find_media_files(root, MOVIE)]
+    files = [os.path.relpath(f, root) for f in find_media_files(root, MOVIE, LOG)]
     assert files == ["0.mkv", "a/S01/e.mkv", "a/z.mkv", "b/1.mkv", "b/2.mkv"]
 
 
 def test_download_path_containing_extras_is_not_poisoned(tmp_path):
     # App. A #14: reference tests the absolute path; we test the job-relative path.
     root = make_tree(tmp_path / "extras-store" / "job", ["Season 1/a.mkv", "Other/b.mkv"])
-    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV, LOG)]
     assert files == ["Season 1/a.mkv"]
     legacy = MediaSelector(legacy_full_path_extras=True).find(root, TV)
     assert legacy == []
@@ -89,7 +91,7 @@ def test_download_path_containing_extras_is_not_poisoned(tmp_path):
 def test_sole_dir_rule_depth_one_only(tmp_path):
     # App. A #16: nested dir with the same name as the sole root entry is not auto-kept.
     root = make_tree(tmp_path / "s", ["Show/Show/a.mkv", "Show/b.mkv"])
-    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV, LOG)]
     assert files == ["Show/b.mkv"]
     legacy = MediaSelector(legacy_any_depth_sole_dir=True).find(root, TV)
     assert [os.path.relpath(f, root) for f in legacy] == ["Show/Show/a.mkv", "Show/b.mkv"]
@@ -98,7 +100,7 @@ def test_sole_dir_rule_depth_one_only(tmp_path):
 def test_symlink_loop_terminates(tmp_path):
     root = make_tree(tmp_path / "l", ["S1/a.mkv"])
     os.symlink(os.path.join(root, "S1"), os.path.join(root, "S1", "S1loop"))
-    files = [os.path.relpath(f, root) for f in find_media_files(root, TV)]
+    files = [os.path.relpath(f, root) for f in find_media_files(root, TV, LOG)]
     assert files[0] == "S1/a.mkv"
     assert files == ["S1/a.mkv"]  # the symlinked dir is the same inode: cut
 
@@ -171,3 +173,10 @@ def test_virtual_walk_reference_fixture(tmp_path):
             "Commentary/KonoSuba Season 1 Commentary.mkv", "S1/KonoSuba S1E1.mkv"]
     got = MediaSelector().find_virtual("/job", rels, TV)
     assert got == ["/job/S1/KonoSuba S1E1.mkv", "/job/Season 1/KonoSuba S1E1.mkv"]
+
+
+def test_use_real_logger_switch(monkeypatch):
+    monkeypatch.delenv("USE_REAL_LOGGER", raising=False)
+    assert isinstance(make_test_logger(), NullLogger)
+    monkeypatch.setenv("USE_REAL_LOGGER", "1")
+    assert not isinstance(make_test_logger(), NullLogger)
