@@ -38,6 +38,7 @@ from downloader_amd.broker.memory import MemoryBroker  # noqa: E402
 from downloader_amd.models import api  # noqa: E402
 from downloader_amd.service.worker import Worker  # noqa: E402
 from downloader_amd.utils.config import load_config  # noqa: E402
+from downloader_amd.stages.jobdir import get_reaper  # noqa: E402
 
 MB = 1_000_000
 
@@ -47,6 +48,12 @@ def _pct(xs: List[float], q: float) -> float:
         return 0.0
     xs = sorted(xs)
     return xs[min(len(xs) - 1, int(q * (len(xs) - 1) + 0.5))]
+
+
+def _self_cpu() -> float:
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
 
 
 def _cfg(mode: str, endpoint: str, stage: str, **over) -> object:
@@ -151,7 +158,15 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             await w.start(health=False)
             m = api.make_download(f"c{cfg_no}-{a.mode}", "http", b.files_url("job.torrent"),
                                   "TV" if cfg_no == 4 else "MOVIE")
+            cpu0, peer0 = _self_cpu(), b.cpu_seconds()
             dt, r = await _run_jobs(w, [m])
+            cpu_s, peer_cpu_s = _self_cpu() - cpu0, b.cpu_seconds() - peer0
+            # job_s ends at the convert publish; the background unlink of the staged files
+            # (instance.background_cleanup) is timed separately here.
+            tc = time.perf_counter()
+            await asyncio.get_running_loop().run_in_executor(
+                None, get_reaper(w.services).drain, 600.0)
+            cleanup_s = time.perf_counter() - tc
             await w.stop()
             assert r[0].outcome == "staged", r[0]
             st = b.stats()
@@ -161,7 +176,11 @@ async def config_torrent(a, cfg_no: int) -> Dict:
     return {"config": cfg_no, "mode": a.mode, "bytes": total, "files": len(sizes),
             "piece_len": a.piece_mb << 20, "job_s": round(dt, 3),
             "MBps": round(total / dt / MB, 1), "setup_s": round(setup_s, 2),
-            "s3_bytes_received": st["bytes_received"], "uploaded_bytes": r[0].bytes}
+            "s3_bytes_received": st["bytes_received"], "uploaded_bytes": r[0].bytes,
+            "torrent": r[0].stats.get("torrent", {}), "stage_s": r[0].stats.get("stage_s", {}),
+            "eager_upload_s": r[0].stats.get("eager_upload_s"),
+            "cleanup_after_job_s": round(cleanup_s, 3),
+            "worker_cpu_s": round(cpu_s, 2), "peer_cpu_s": round(peer_cpu_s, 2)}
 
 
 # ---------------------------------------------------------------------------- config 5

@@ -30,6 +30,7 @@ from ..net.http import TransportSet, make_transports
 from ..s3.client import S3Client, S3Error
 from ..stages import build_stages
 from ..stages.base import EventEmitter, Job, Services, Stage
+from ..stages.jobdir import get_reaper
 from ..utils.config import Config
 from ..utils.log import Logger, get_logger
 from ..utils.metrics import Metrics
@@ -52,6 +53,7 @@ class JobResult:
     seconds: float
     bytes: int = 0
     error: str = ""
+    stats: dict = field(default_factory=dict)   # the job's stats (stage timings, torrent, ...)
 
 
 class Worker:
@@ -93,6 +95,7 @@ class Worker:
             await self.broker.declare(q)
         if not self.stages:
             self.stages = await build_stages(self.cfg.stages, self.cfg, self.services)
+        get_reaper(self.services).sweep()   # trash left by a crashed predecessor
         if self.cfg.download.gpu_prewarm and self.cfg.download.verify_backend != "cpu":
             from ..ops.hashing import prewarm_gpu
             try:
@@ -131,6 +134,8 @@ class Worker:
             await self._health.stop()
         for _, st in self.stages:
             await st.close()
+        await asyncio.get_running_loop().run_in_executor(None, get_reaper(self.services).close,
+                                                         drain_timeout)
         try:
             await self.broker.close()
         except Exception:
@@ -228,13 +233,18 @@ class Worker:
         drop = outcome == "dead" or (outcome == "stalled" and self.cfg.download.cleanup_on_stall)
         loop = asyncio.get_running_loop()
         if drop or not jd.exclusive:
-            await loop.run_in_executor(None, jd.remove)
+            reaper = get_reaper(self.services)
+            if reaper.background:
+                reaper.reap(jd.path)
+            else:
+                await loop.run_in_executor(None, jd.remove)
         jd.release()
         job.jobdir = None
 
     def _finish(self, job: Optional[Job], r: JobResult) -> JobResult:
         if job is not None:
             job.stats["outcome"] = r.outcome
+            r.stats = job.stats
         self.results.append(r)
         self.metrics.jobs.labels(r.outcome).inc()
         self.metrics.job_duration.labels(r.outcome).observe(r.seconds)
@@ -259,8 +269,10 @@ class Worker:
             job.logger.info(f"invoking stage '{name}'")
             self.active[slot].stage = name
             job.last_stage = last
+            ts = time.perf_counter()
             with self.tracer.span(f"stage.{name}"), self.metrics.time_stage(name):
                 last = await fn(job)
+            job.stats.setdefault("stage_s", {})[name] = round(time.perf_counter() - ts, 4)
             job.emitter.emit("progress", 0)
 
     async def _retry(self, d: Delivery, attempt: int, err: str) -> str:

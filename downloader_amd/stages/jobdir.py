@@ -16,7 +16,9 @@ import fcntl
 import os
 import secrets
 import shutil
-from typing import Optional
+import threading
+from concurrent.futures import Future, ThreadPoolExecutor, wait
+from typing import Optional, Set
 
 
 class JobDir:
@@ -56,3 +58,93 @@ class JobDir:
     def remove(self) -> None:
         if self.path:
             shutil.rmtree(self.path, ignore_errors=True)
+
+
+class Reaper:
+    """Removes finished job directories off the job's critical path.
+
+    The reference deletes the job directory inline before the convert message goes out
+    (lib/upload.js:60-64). Unlinking multi-GB staged files frees their page-cache pages and
+    extents, which costs 0.3 s for 4 GB and 1.5 s for 20 GB on the build box - as long as the
+    whole eager-staged upload. Here the directory is renamed into ``<root>/.trash`` (one
+    syscall, so the job id's path is free again at once) and unlinked by one background thread.
+    ``sweep()`` removes whatever a crashed worker left in the trash; ``drain()`` waits for the
+    queue at shutdown. ``background=False`` (``mode: reference``) deletes inline.
+    """
+
+    def __init__(self, root: str, background: bool = True):
+        self.root = root
+        self.background = background
+        self.trash = os.path.join(root, ".trash")
+        self._pool: Optional[ThreadPoolExecutor] = None
+        self._pending: Set[Future] = set()
+        self._lock = threading.Lock()
+        self.reaped = 0
+
+    def _submit(self, path: str) -> Future:
+        with self._lock:
+            if self._pool is None:
+                self._pool = ThreadPoolExecutor(1, thread_name_prefix="reaper")
+            fut = self._pool.submit(shutil.rmtree, path, True)
+            self._pending.add(fut)
+        fut.add_done_callback(self._done)
+        return fut
+
+    def _done(self, fut: Future) -> None:
+        with self._lock:
+            self._pending.discard(fut)
+            self.reaped += 1
+
+    def reap(self, path: str) -> Optional[Future]:
+        if not path or not os.path.lexists(path):
+            return None
+        if not self.background:
+            shutil.rmtree(path, ignore_errors=True)
+            return None
+        dst = path
+        try:
+            os.makedirs(self.trash, exist_ok=True)
+            cand = os.path.join(self.trash, f"{os.path.basename(path)}.{secrets.token_hex(4)}")
+            os.rename(path, cand)
+            dst = cand
+        except OSError:
+            pass   # other filesystem or already gone: delete in place
+        return self._submit(dst)
+
+    def sweep(self) -> int:
+        n = 0
+        try:
+            names = os.listdir(self.trash)
+        except OSError:
+            return 0
+        for name in names:
+            self._submit(os.path.join(self.trash, name))
+            n += 1
+        return n
+
+    def pending(self) -> int:
+        with self._lock:
+            return len(self._pending)
+
+    def drain(self, timeout: Optional[float] = None) -> bool:
+        with self._lock:
+            futs = list(self._pending)
+        done, not_done = wait(futs, timeout=timeout)
+        return not not_done
+
+    def close(self, timeout: Optional[float] = 30.0) -> None:
+        self.drain(timeout)
+        with self._lock:
+            pool, self._pool = self._pool, None
+        if pool is not None:
+            pool.shutdown(wait=False)
+
+
+def get_reaper(sv) -> Reaper:
+    """Per-worker reaper for ``instance.download_path`` (kept in ``Services.extra``)."""
+    r = sv.extra.get("reaper")
+    if r is None:
+        cfg = sv.config
+        r = Reaper(str(cfg.resolved_download_root()), cfg.instance.background_cleanup)
+        sv.extra["reaper"] = r
+    return r

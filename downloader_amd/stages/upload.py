@@ -21,6 +21,7 @@ from typing import Any, Dict, List
 from ..models import keys
 from ..net.http import Progress
 from .base import DOWNLOADING, Job, Services, Stage, ensure_staging_bucket
+from .jobdir import get_reaper
 
 
 class UploadStage(Stage):
@@ -95,8 +96,12 @@ class UploadStage(Stage):
         job.logger.info("finished uploading all files")
         if download_path:
             try:
-                await asyncio.get_running_loop().run_in_executor(
-                    None, shutil.rmtree, download_path)
+                reaper = get_reaper(self.sv)
+                if reaper.background:
+                    reaper.reap(download_path)    # rename now, unlink in the background
+                else:
+                    await asyncio.get_running_loop().run_in_executor(
+                        None, shutil.rmtree, download_path)
             except OSError as e:
                 job.logger.warn("err", f"failed to clean up directory: {e}")
         return {"files": files, "keys": sorted(owner), "bytes": sum(uploaded)}

@@ -17,6 +17,7 @@ from __future__ import annotations
 import asyncio
 import math
 import os
+import time
 from typing import Optional
 
 from ..fetch.http import fetch_bytes
@@ -84,8 +85,12 @@ async def _start_eager(session: TorrentSession, job: Job, path: str, cfg, sv: Se
 async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
                            client: Optional[TorrentClient] = None) -> int:
     d = cfg.download
+    t0 = time.perf_counter()
     client = client or await get_client(cfg, sv)
     session = await open_session(client, uri, path, sv)
+    # Seconds since the backend was entered: open (metainfo fetched, storage ready), metadata,
+    # payload complete and verified, eager staging drained.
+    tl = {"open": time.perf_counter() - t0}
     try:
         # 1) metadata stall timer
         meta_wait = asyncio.ensure_future(session.meta_ready.wait())
@@ -102,6 +107,7 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
         if not session.meta_ready.is_set():
             job.logger.warn("download failed to progress, killing")
             raise MetadataStalled()
+        tl["metadata"] = time.perf_counter() - t0
         job.logger.debug("hash", session.info_hash.hex())
         job.logger.debug("files", len(session.meta.files))
         eager = await _start_eager(session, job, path, cfg, sv) if d.eager_upload else None
@@ -134,9 +140,12 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
             done, _ = await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
             for t in done:
                 t.result()  # propagate DownloadStalled / session errors
+            tl["complete"] = time.perf_counter() - t0
             if eager is not None:
                 job.stats.setdefault("streamed", []).extend(await eager.finish())
                 job.stats["eager_uploaded_bytes"] = eager.uploaded_bytes
+                job.stats["eager_upload_s"] = round(eager.upload_s, 4)
+                tl["eager_drained"] = time.perf_counter() - t0
         except BaseException:
             if eager is not None:
                 await eager.abort()
@@ -148,7 +157,10 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
         job.logger.debug("finished, clearing watchers")
         job.stats["torrent"] = {"webseed_bytes": session.webseed_bytes,
                                 "peers": session.stats["peers_connected"],
-                                "hash_fails": session.stats["hash_fails"]}
+                                "hash_fails": session.stats["hash_fails"],
+                                "webseed_fetch_s": round(session.stats["webseed_fetch_s"], 4),
+                                "webseed_verify_s": round(session.stats["webseed_verify_s"], 4),
+                                "timeline_s": {k: round(v, 4) for k, v in tl.items()}}
         return session.total_bytes()
     finally:
         await client.remove(session)

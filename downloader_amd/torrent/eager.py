@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import asyncio
 import os
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set, Tuple
 
@@ -64,6 +65,7 @@ class EagerUploader:
         self.tasks: List[asyncio.Task] = []
         self.error: Optional[BaseException] = None
         self.uploaded_bytes = 0
+        self.upload_s = 0.0          # summed part-upload time (with the semaphore held)
 
     # ---------------------------------------------------------------- readiness
     def _ready(self, f: _File, off: int, ln: int) -> bool:
@@ -100,6 +102,7 @@ class EagerUploader:
     async def _upload(self, f: _File, num: int, off: int, ln: int) -> None:
         try:
             async with self.sem:
+                t0 = time.perf_counter()
                 if f.fd < 0:
                     f.fd = os.open(f.path, os.O_RDONLY | getattr(os, "O_CLOEXEC", 0))
                 if f.single:
@@ -113,6 +116,7 @@ class EagerUploader:
                     f.etags[num] = await self.s3.upload_part(self.bucket, f.key, f.upload_id, num,
                                                              FileRange(f.fd, off, ln))
                 self.uploaded_bytes += ln
+                self.upload_s += time.perf_counter() - t0
         except BaseException as e:  # surfaced by finish()
             if self.error is None:
                 self.error = e

@@ -258,7 +258,9 @@ class TorrentSession:
         self.piece_listeners: List = []   # callbacks(piece index) after a piece is verified
         self._piece_cache: "OrderedDict[int, bytes]" = OrderedDict()   # LRU of served pieces
         self._piece_cache_bytes = 0
-        self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0}
+        self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0,
+                      # summed over webseed streams: time in Range GETs / in piece verification
+                      "webseed_fetch_s": 0.0, "webseed_verify_s": 0.0}
         self.add_peers(list(peers), "magnet")
         if meta is not None:
             self.trackers += [t for t in meta.trackers() if t not in self.trackers]
@@ -628,6 +630,7 @@ class TorrentSession:
             pieces = list(range(first, first + count))
             off = first * self.meta.piece_length
             length = sum(self.meta.piece_size(i) for i in pieces)
+            t_fetch = time.perf_counter()
             try:
                 for fd, foff, ln, fidx in self.storage.segments(off, length):
                     url = self._webseed_url(base, fidx)
@@ -641,7 +644,10 @@ class TorrentSession:
                                              r.status)
                     self.webseed_bytes += ln
                     self.downloaded += ln
+                t_verify = time.perf_counter()
+                self.stats["webseed_fetch_s"] += t_verify - t_fetch
                 ok = await loop.run_in_executor(None, self.storage.verify, pieces)
+                self.stats["webseed_verify_s"] += time.perf_counter() - t_verify
             except (TransportError, OSError) as e:
                 self.picker.unclaim(pieces)
                 failures += 1

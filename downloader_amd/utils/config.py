@@ -30,6 +30,9 @@ class InstanceConfig(BaseModel):
     download_path: str = "downloads"
     # App. A #18: concurrent duplicate deliveries must not share a directory.
     per_attempt_dirs: bool = True
+    # Finished job dirs are renamed into <download_path>/.trash and unlinked by a background
+    # thread instead of inline before the convert publish (reference: inline rm, upload.js:60).
+    background_cleanup: bool = True
 
 
 class S3Config(BaseModel):
@@ -161,6 +164,7 @@ class Config(BaseModel):
             self.download.webseed_streams = 1
             self.download.stream_http = False
             self.download.eager_upload = False
+            self.instance.background_cleanup = False
         else:
             self.broker.prefetch = max(self.broker.prefetch, self.concurrency)
         return self

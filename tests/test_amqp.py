@@ -263,9 +263,12 @@ def test_broker_drop_mid_job_redelivers_and_dedups(run, make_cfg, origin_cls):
             if len(w.results) >= 2:
                 break
             await asyncio.sleep(0.02)
-        # the redelivered copy may finish first (it only probes the marker and publishes)
+        # the redelivered copy may finish first (it only probes the marker and publishes); the
+        # first copy's convert publish either lands after the reconnect ("staged") or hits the
+        # dead connection ("publish_failed") - either way the redelivery converts it once more.
         outcomes = sorted(r.outcome for r in w.results)
-        assert outcomes == ["skipped", "staged"], outcomes
+        assert outcomes in (["skipped", "staged"], ["publish_failed", "skipped"]), outcomes
+        assert srv.depth("v1.convert") >= 1
         puts = [p for m, p in s3.requests if m == "PUT" and p.endswith("/done")]
         assert len(puts) == 1
         await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()

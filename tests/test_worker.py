@@ -51,10 +51,12 @@ def test_minimum_slice_http_to_s3(run, make_cfg, origin_cls):
         assert len(conv) == 1
         c = api.decode(api.Convert, conv[0])
         assert c.media.id == "job1" and c.media.sourceURI.endswith("blob.mkv?x=1")
-        # job directory cleaned up
-        assert not os.path.exists(os.path.join(w.cfg.instance.download_path, "job1", "x"))
+        # job directory released at once (renamed into .trash), unlinked by the reaper
+        root = w.cfg.instance.download_path
+        assert not os.path.exists(os.path.join(root, "job1"))
         code = await w.stop()
         assert code == 0
+        assert os.listdir(os.path.join(root, ".trash")) == []
         await s3.stop()
         await origin.stop()
     run(go())
@@ -401,3 +403,26 @@ def test_http_stall_floor_fails_slow_transfer(run, make_cfg, origin_cls):
         assert "B/s" in w.results[0].error
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_reaper_renames_then_unlinks_and_sweeps(tmp_path):
+    from downloader_amd.stages.jobdir import Reaper
+    root = tmp_path / "dl"
+    job = root / "j1" / "Season 1"
+    job.mkdir(parents=True)
+    (job / "e1.mkv").write_bytes(os.urandom(1 << 20))
+    r = Reaper(str(root))
+    fut = r.reap(str(root / "j1"))
+    assert not (root / "j1").exists()           # path free before the unlink finished
+    fut.result(10)
+    assert r.drain(10) and os.listdir(root / ".trash") == []
+    # leftovers of a crashed worker are swept
+    (root / ".trash" / "old.abcd" / "x").mkdir(parents=True)
+    assert r.sweep() == 1 and r.drain(10)
+    assert os.listdir(root / ".trash") == []
+    r.close()
+    # reference mode: inline removal, no trash
+    (root / "j2").mkdir()
+    inline = Reaper(str(root), background=False)
+    assert inline.reap(str(root / "j2")) is None and not (root / "j2").exists()
+    assert inline.reap(str(root / "missing")) is None
