@@ -7,6 +7,7 @@ single-file torrent lands at ``<path>/<name>``, a multi-file torrent under ``<pa
 """
 from __future__ import annotations
 
+import bisect
 import hashlib
 import os
 from dataclasses import dataclass, field
@@ -72,6 +73,16 @@ class Metainfo:
             base = os.path.join(root, _safe(self.name))
             return [(os.path.join(base, *[_safe(p) for p in f.path]), f.length) for f in self.files]
         return [(os.path.join(root, _safe(self.name)), self.total_length)]
+
+    def file_at(self, offset: int) -> int:
+        """Index of the (non-empty) file holding storage byte ``offset``."""
+        ends = self.__dict__.get("_ends")
+        if ends is None:
+            ends = self.__dict__["_ends"] = [f.offset + f.length for f in self.files]
+        i = bisect.bisect_right(ends, offset)
+        while i < len(self.files) - 1 and self.files[i].length == 0:
+            i += 1
+        return min(i, len(self.files) - 1)
 
     def file_spans(self, offset: int, length: int) -> List[Tuple[int, int, int]]:
         """Split a storage byte range into (file_index, file_offset, length) segments."""

@@ -170,10 +170,15 @@ class PiecePicker:
             if not rs and ap.state[b] == 1:
                 ap.state[b] = 0
 
-    def claim_run(self, max_bytes: int) -> Optional[Tuple[int, int]]:
-        """Claim the first run of contiguous free pieces (<= max_bytes) for a webseed."""
+    def claim_run(self, max_bytes: int, busy_files: Optional[Dict[int, int]] = None
+                  ) -> Optional[Tuple[int, int]]:
+        """Claim a run of contiguous free pieces (<= max_bytes) for a webseed stream. With
+        ``busy_files`` (file index -> streams writing it) the first run that starts in a file
+        no other stream is writing wins: page-cache writes into ONE file serialise on its
+        inode (~10 GB/s per file on the build box), so streams spread over files."""
         plen = self.meta.piece_length
         maxp = max(1, max_bytes // plen)
+        fallback = None
         i = 0
         while i < self.n:
             if i in self.have or i in self.active or i in self.claimed:
@@ -183,10 +188,25 @@ class PiecePicker:
             while j < self.n and j - i < maxp and j not in self.have and j not in self.active \
                     and j not in self.claimed:
                 j += 1
-            for k in range(i, j):
-                self.claimed.add(k)
-            return i, j - i
-        return None
+            if not busy_files or not busy_files.get(self.meta.file_at(i * plen), 0):
+                fallback = (i, j)
+                break
+            if fallback is None:
+                fallback = (i, j)
+            i = self._next_file_piece(i, j)
+        if fallback is None:
+            return None
+        i, j = fallback
+        for k in range(i, j):
+            self.claimed.add(k)
+        return i, j - i
+
+    def _next_file_piece(self, i: int, j: int) -> int:
+        """First piece index at or after j that starts beyond the file holding piece i."""
+        m = self.meta
+        f = m.files[m.file_at(i * m.piece_length)]
+        end = f.offset + f.length
+        return max(j, end // m.piece_length)
 
     def unclaim(self, pieces) -> None:
         for p in pieces:
@@ -255,6 +275,7 @@ class TorrentSession:
         self._wake = asyncio.Event()
         self._closed = False
         self._ws_dead = 0
+        self._ws_files: Dict[int, int] = {}   # file index -> webseed streams writing into it
         self.piece_listeners: List = []   # callbacks(piece index) after a piece is verified
         self._piece_cache: "OrderedDict[int, bytes]" = OrderedDict()   # LRU of served pieces
         self._piece_cache_bytes = 0
@@ -620,54 +641,90 @@ class TorrentSession:
         return base.rstrip("/") + "/" + "/".join(quote(x) for x in [m.name] + f.path)
 
     async def _webseed_worker(self, base: str) -> None:
-        failures = 0
+        """One BEP-19 stream: claim a run of whole pieces (``webseed_chunk`` bytes), GET it
+        straight into the storage files (splice), hand the run to verification and go on with
+        the next run while it is hashed - fetch and SHA-1 overlap within the stream, so a few
+        streams saturate the path (parallel writers into one file contend on its inode lock)."""
+        st = {"failures": 0}
+        verifying: Set[asyncio.Task] = set()
         loop = asyncio.get_running_loop()
-        while not self._closed and not self.done.is_set():
-            run = self.picker.claim_run(self.client.webseed_chunk)
-            if run is None:
-                return
-            first, count = run
-            pieces = list(range(first, first + count))
-            off = first * self.meta.piece_length
-            length = sum(self.meta.piece_size(i) for i in pieces)
-            t_fetch = time.perf_counter()
-            try:
-                for fd, foff, ln, fidx in self.storage.segments(off, length):
-                    url = self._webseed_url(base, fidx)
-                    flen = self.meta.files[fidx].length
-                    hdrs = [] if (foff == 0 and ln == flen) else \
-                        [("Range", f"bytes={foff}-{foff + ln - 1}")]
-                    r = await self.client.transports.request("GET", url, headers=hdrs,
-                                                             sink=FileSink(fd, foff, ln))
-                    if r.status not in (200, 206) or (r.status == 200 and hdrs) or r.written != ln:
-                        raise TransportError(f"webseed {url}: HTTP {r.status}, {r.written}/{ln} B",
-                                             r.status)
-                    self.webseed_bytes += ln
-                    self.downloaded += ln
-                t_verify = time.perf_counter()
-                self.stats["webseed_fetch_s"] += t_verify - t_fetch
-                ok = await loop.run_in_executor(None, self.storage.verify, pieces)
-                self.stats["webseed_verify_s"] += time.perf_counter() - t_verify
-            except (TransportError, OSError) as e:
-                self.picker.unclaim(pieces)
-                failures += 1
-                self.stats["webseed_failures"] += 1
-                if failures >= self.client.webseed_max_failures:
-                    self._webseed_gave_up(e)
-                    return
-                await asyncio.sleep(min(10.0, 0.2 * (2 ** failures)))
-                continue
-            for i, good in zip(pieces, ok):
-                self.picker.claimed.discard(i)
-                if good:
-                    await self._piece_complete(i)
-                else:
-                    self.stats["hash_fails"] += 1
-            if not all(ok):
-                failures += 1
-                if failures >= self.client.webseed_max_failures:
+        depth = max(1, self.client.webseed_verify_depth)
+        try:
+            while not self._closed and not self.done.is_set():
+                if st["failures"] >= self.client.webseed_max_failures:
                     self._webseed_gave_up(TorrentError("webseed served corrupt pieces"))
                     return
+                run = self.picker.claim_run(self.client.webseed_chunk, self._ws_files)
+                if run is None:
+                    if not verifying:
+                        return
+                    # a failing verification hands its pieces back: wait, then look again
+                    await asyncio.wait(verifying, return_when=asyncio.FIRST_COMPLETED)
+                    continue
+                first, count = run
+                pieces = list(range(first, first + count))
+                fidx = self.meta.file_at(first * self.meta.piece_length)
+                self._ws_files[fidx] = self._ws_files.get(fidx, 0) + 1
+                try:
+                    await self._webseed_fetch(base, first, pieces)
+                except (TransportError, OSError) as e:
+                    self.picker.unclaim(pieces)
+                    st["failures"] += 1
+                    self.stats["webseed_failures"] += 1
+                    if st["failures"] >= self.client.webseed_max_failures:
+                        self._webseed_gave_up(e)
+                        return
+                    await asyncio.sleep(min(10.0, 0.2 * (2 ** st["failures"])))
+                    continue
+                finally:
+                    self._ws_files[fidx] -= 1
+                t = loop.create_task(self._webseed_verify(pieces, st))
+                verifying.add(t)
+                t.add_done_callback(verifying.discard)
+                while len(verifying) >= depth:
+                    await asyncio.wait(verifying, return_when=asyncio.FIRST_COMPLETED)
+            if verifying:
+                await asyncio.gather(*verifying)
+        finally:
+            for t in verifying:
+                t.cancel()
+
+    async def _webseed_fetch(self, base: str, first: int, pieces: List[int]) -> None:
+        off = first * self.meta.piece_length
+        length = sum(self.meta.piece_size(i) for i in pieces)
+        t_fetch = time.perf_counter()
+        for fd, foff, ln, fidx in self.storage.segments(off, length):
+            url = self._webseed_url(base, fidx)
+            flen = self.meta.files[fidx].length
+            hdrs = [] if (foff == 0 and ln == flen) else \
+                [("Range", f"bytes={foff}-{foff + ln - 1}")]
+            r = await self.client.transports.request("GET", url, headers=hdrs,
+                                                     sink=FileSink(fd, foff, ln))
+            if r.status not in (200, 206) or (r.status == 200 and hdrs) or r.written != ln:
+                raise TransportError(f"webseed {url}: HTTP {r.status}, {r.written}/{ln} B",
+                                     r.status)
+            self.webseed_bytes += ln
+            self.downloaded += ln
+        self.stats["webseed_fetch_s"] += time.perf_counter() - t_fetch
+
+    async def _webseed_verify(self, pieces: List[int], st: Dict[str, int]) -> None:
+        t_verify = time.perf_counter()
+        try:
+            ok = await asyncio.get_running_loop().run_in_executor(None, self.storage.verify,
+                                                                  pieces)
+        except OSError:
+            self.picker.unclaim(pieces)
+            st["failures"] += 1
+            return
+        self.stats["webseed_verify_s"] += time.perf_counter() - t_verify
+        for i, good in zip(pieces, ok):
+            self.picker.claimed.discard(i)
+            if good:
+                await self._piece_complete(i)
+            else:
+                self.stats["hash_fails"] += 1
+        if not all(ok):
+            st["failures"] += 1
 
     def _webseed_gave_up(self, e: BaseException) -> None:
         self._ws_dead += 1

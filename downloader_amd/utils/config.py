@@ -108,6 +108,7 @@ class DownloadConfig(BaseModel):
     torrent_request_pipeline: int = 16
     webseed_streams: int = 8                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
+    webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on
     cleanup_on_stall: bool = True               # App. A #6 (reference leaves data behind)
     emit_errored_on_stall: bool = False         # App. A #6 (reference: ack silently)
 

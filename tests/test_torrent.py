@@ -417,3 +417,28 @@ def test_worker_torrent_eager_upload_collision_and_parts(run, tmp_path, make_cfg
         assert not s3.uploads.get("triton-staging")
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_webseed_claims_spread_over_files():
+    """Streams prefer runs in files no other stream is writing (one file's page-cache write
+    path serialises), and fall back to any free run."""
+    from downloader_amd.torrent.metainfo import FileEntry, Metainfo
+    from downloader_amd.torrent.session import PiecePicker
+    from downloader_amd.torrent.storage import Bitfield
+    files, off = [], 0
+    for i, n in enumerate([16, 0, 16, 16]):
+        files.append(FileEntry([f"f{i}"], n, off))
+        off += n
+    m = Metainfo(b"x" * 20, "t", 4, b"\0" * 20 * (off // 4), files, off, multi_file=True)
+    assert [m.file_at(o) for o in (0, 15, 16, 31, 32, 47)] == [0, 0, 2, 2, 3, 3]
+    pp = PiecePicker(m, Bitfield(m.num_pieces))
+    busy = {}
+    got = []
+    for _ in range(6):
+        first, count = pp.claim_run(8, busy)
+        f = m.file_at(first * 4)
+        busy[f] = busy.get(f, 0) + 1
+        got.append((first, count, f))
+    assert [g[2] for g in got[:3]] == [0, 2, 3]            # one stream per file first
+    assert sorted(p for g in got for p in range(g[0], g[0] + g[1])) == list(range(12))
+    assert pp.claim_run(8, busy) is None
