@@ -23,6 +23,8 @@ import signal
 import sys
 import time
 
+from .utils.cpus import effective_cpus
+
 
 def _worker(args) -> int:
     from .service.worker import Worker
@@ -129,7 +131,8 @@ def main(argv=None) -> int:
     w.add_argument("--mode", choices=["tuned", "reference"], default="")
     w.add_argument("--drain-timeout", type=float, default=30.0)
     s = sub.add_parser("supervisor")
-    s.add_argument("-n", type=int, default=os.cpu_count() or 1)
+    # one worker (4 jobs in flight, native threads for hashing/relay) per 4 usable CPUs
+    s.add_argument("-n", type=int, default=max(1, effective_cpus() // 4))
     s.add_argument("--config", default="")
     s.add_argument("--mode", choices=["tuned", "reference"], default="")
     s.add_argument("--cpus-per-worker", type=int, default=0)

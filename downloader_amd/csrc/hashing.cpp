@@ -10,7 +10,10 @@
 #include <openssl/evp.h>
 
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <sched.h>
 #include <fcntl.h>
 #include <stdexcept>
 #include <string>
@@ -35,12 +38,35 @@ void digest_into(const EVP_MD* md, const uint8_t* p, size_t n, uint8_t* out) {
   if (EVP_Digest(p, n, out, &len, md, nullptr) != 1) throw std::runtime_error("EVP_Digest failed");
 }
 
+// CPUs this process may actually use: the affinity mask, capped by a cgroup v2 CPU quota
+// (cpu.max "quota period"). Containers commonly expose hundreds of CPUs in the mask but grant
+// a 16-CPU quota; spawning a thread per visible CPU would only add run-queue contention.
+int effective_cpus() {
+  static const int cached = [] {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) {
+      unsigned hc = std::thread::hardware_concurrency();
+      n = hc ? (int)hc : 4;
+    }
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32] = {0};
+      long period = 0;
+      if (fscanf(f, "%31s %ld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+        long q = atol(quota);
+        int lim = (int)((q + period - 1) / period);
+        if (lim > 0 && lim < n) n = lim;
+      }
+      fclose(f);
+    }
+    return n;
+  }();
+  return cached;
+}
+
 int resolve_threads(int threads, size_t work_items) {
-  if (threads <= 0) {
-    unsigned hc = std::thread::hardware_concurrency();
-    threads = hc ? (int)hc : 4;
-    if (threads > 16) threads = 16;  // box CPU share is 16 (gpurun); callers may raise it
-  }
+  if (threads <= 0) threads = effective_cpus();
   if ((size_t)threads > work_items) threads = (int)(work_items ? work_items : 1);
   return threads;
 }

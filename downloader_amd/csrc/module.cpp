@@ -57,6 +57,8 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "stager host-native byte paths: hashing (OpenSSL EVP, threaded) and zero-copy HTTP";
 
   m.def("digest_size", &digest_size);
+  m.def("effective_cpus", &effective_cpus,
+        "CPUs usable by this process: affinity mask capped by the cgroup v2 cpu.max quota");
   m.def(
       "digest",
       [](const std::string& algo, const py::buffer& data) {

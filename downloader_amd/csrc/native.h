@@ -16,6 +16,7 @@ namespace stager {
 // ---- hashing.cpp -----------------------------------------------------------------------
 const EVP_MD* md_for(const std::string& algo);
 size_t digest_size(const std::string& algo);
+int effective_cpus();
 int resolve_threads(int threads, size_t work_items);
 
 class Hasher {

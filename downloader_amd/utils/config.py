@@ -106,7 +106,7 @@ class DownloadConfig(BaseModel):
     torrent_enable_trackers: bool = True
     torrent_enable_webseeds: bool = True
     torrent_request_pipeline: int = 16
-    webseed_streams: int = 8                    # concurrent Range GETs per webseed (0: http_streams)
+    webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on
     cleanup_on_stall: bool = True               # App. A #6 (reference leaves data behind)

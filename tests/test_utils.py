@@ -106,3 +106,23 @@ def test_metrics_registry_exposition():
     assert 'downloader_bytes_downloaded_total{proto="http"} 10.0' in text
     assert "downloader_stage_duration_seconds_count" in text
     assert m.sample("downloader_bytes_downloaded_total", proto="http") == 10
+
+
+def test_effective_cpus_respects_cgroup_quota(tmp_path, monkeypatch):
+    from downloader_amd.utils import cpus
+    f = tmp_path / "cpu.max"
+    f.write_text("1600000 100000\n")
+    assert cpus.cgroup_cpu_quota(str(f)) == 16
+    f.write_text("max 100000\n")
+    assert cpus.cgroup_cpu_quota(str(f)) == float("inf")
+    assert cpus.cgroup_cpu_quota(str(tmp_path / "missing")) == float("inf")
+    cpus.effective_cpus.cache_clear()
+    monkeypatch.setattr(cpus, "cgroup_cpu_quota", lambda path="": 2.5)
+    assert cpus.effective_cpus() == min(3, len(os.sched_getaffinity(0)))
+    cpus.effective_cpus.cache_clear()
+
+
+def test_native_effective_cpus_matches_python():
+    from downloader_amd.ops import native
+    from downloader_amd.utils.cpus import effective_cpus
+    assert native().effective_cpus() == effective_cpus()
