@@ -210,22 +210,23 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
   }
 }
 
-// Chunk-streamed variant: lane k owns piece (first + k) of a window and advances it by one
-// CH-byte chunk per launch; the SHA-1 state lives in `state` between launches. The chunk of
-// lane k sits at data + k * CH. On the launch that reaches the end of the piece the lane pads,
-// finalises and writes ok[first + k]. Per-launch latency is CH / lane-rate (~1.6 ms for 64 KiB)
-// instead of piece_len / lane-rate, so copies and hashing overlap at a fine grain whatever the
-// piece size.
+// Chunk-streamed variant: lane k owns piece (first + k) of a window - or, with a piece list,
+// piece lane_piece[first + k] - and advances it by one CH-byte chunk per launch; the SHA-1
+// state lives in `state` between launches. The chunk of lane k sits at data + k * CH. On the
+// launch that reaches the end of the piece the lane pads, finalises and writes ok[gi].
+// Per-launch latency is CH / lane-rate (~1.6 ms for 64 KiB) instead of piece_len / lane-rate,
+// so copies and hashing overlap at a fine grain whatever the piece size.
 template <bool B3>
 __global__ __launch_bounds__(256) void sha1_chunk(uint32_t* __restrict__ state,
                                                   const uint8_t* __restrict__ data, int64_t CH,
                                                   int n, int64_t piece_len, int64_t last_len,
                                                   int first, int n_total, int64_t chunk_off,
                                                   const uint8_t* __restrict__ expected,
-                                                  uint8_t* __restrict__ ok) {
+                                                  uint8_t* __restrict__ ok,
+                                                  const int* __restrict__ lane_piece) {
   int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const int gi = first + k;
+  const int gi = lane_piece ? lane_piece[first + k] : first + k;
   const int64_t len = (gi == n_total - 1) ? last_len : piece_len;
   const int64_t valid = len - chunk_off;          // bytes of this piece at/after this chunk
   if (valid < 0 || (valid == 0 && chunk_off > 0)) return;  // finished in an earlier launch
@@ -434,25 +435,39 @@ class GpuVerifier {
   // threads, pread from the page cache), copies it on the slot's stream and launches the
   // chunk kernel. Kernels are ordered across the two streams with events (state carries
   // over); the host refills a slot only after its previous copy completed.
+  // `which` (optional) restricts the check to those piece indices: the result then holds one
+  // byte per listed piece, in list order (incremental verification of downloaded runs).
   std::vector<uint8_t> verify_files_streamed(
       const std::vector<std::pair<std::string, int64_t>>& files, int64_t piece_len,
-      const std::string& hashes, int64_t chunk, std::vector<double>* timing) {
+      const std::string& hashes, int64_t chunk, std::vector<double>* timing,
+      const std::vector<int>& which = {}) {
     HIP_CHECK(hipSetDevice(device_));
     Files fs(files);
     const int64_t np = fs.total == 0 ? 0 : (fs.total + piece_len - 1) / piece_len;
     if ((int64_t)hashes.size() != np * 20) throw std::invalid_argument("hash list / piece count mismatch");
+    for (int w : which)
+      if (w < 0 || (int64_t)w >= np) throw std::invalid_argument("piece index out of range");
+    const bool subset = !which.empty();
+    const int64_t m = subset ? (int64_t)which.size() : np;   // lanes to run
+    auto piece_of = [&](int64_t j) -> int64_t { return subset ? (int64_t)which[(size_t)j] : j; };
     std::vector<uint8_t> ok((size_t)np, 0);
+    if (timing) *timing = {0.0, 0.0};
     if (np == 0) return ok;
     const int64_t CH = std::max<int64_t>(64, std::min<int64_t>(chunk, piece_len) & ~(int64_t)63);
-    const int64_t W = std::max<int64_t>(1, std::min<int64_t>(np, batch_bytes_ / CH));
+    const int64_t W = std::max<int64_t>(1, std::min<int64_t>(m, batch_bytes_ / CH));
     const int64_t last_len = fs.total - (np - 1) * piece_len;
     uint8_t *d_exp = nullptr, *d_ok = nullptr;
     uint32_t* d_state = nullptr;
+    int* d_lanes = nullptr;
     HIP_CHECK(hipMalloc((void**)&d_exp, (size_t)np * 20));
     HIP_CHECK(hipMalloc((void**)&d_ok, (size_t)np));
     HIP_CHECK(hipMalloc((void**)&d_state, (size_t)W * 20));
     HIP_CHECK(hipMemcpy(d_exp, hashes.data(), (size_t)np * 20, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemset(d_ok, 0, (size_t)np));
+    if (subset) {
+      HIP_CHECK(hipMalloc((void**)&d_lanes, (size_t)m * sizeof(int)));
+      HIP_CHECK(hipMemcpy(d_lanes, which.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice));
+    }
     std::vector<uint8_t> readable((size_t)np, 1);
     hipEvent_t copied[2], kdone[2];
     for (int s = 0; s < 2; ++s) {
@@ -465,9 +480,11 @@ class GpuVerifier {
     double t_fill = 0, t_wait = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
     int s = 0;
-    for (int64_t first = 0; first < np; first += W) {
-      const int64_t n = std::min(W, np - first);
-      const int64_t maxlen = (first + n == np) ? std::max(piece_len, last_len) : piece_len;
+    for (int64_t first = 0; first < m; first += W) {
+      const int64_t n = std::min(W, m - first);
+      int64_t maxlen = piece_len;
+      for (int64_t k = 0; k < n; ++k)
+        if (piece_of(first + k) == np - 1) maxlen = std::max(piece_len, last_len);
       const int64_t rounds = (maxlen + CH - 1) / CH;
       for (int64_t c = 0; c < rounds; ++c, s ^= 1) {
         auto t0 = now();
@@ -476,7 +493,7 @@ class GpuVerifier {
         uint8_t* dst = h_buf_[s];
         const int64_t coff = c * CH;
         parallel_for((size_t)n, readers_, [&](size_t k) {
-          const int64_t gi = first + (int64_t)k;
+          const int64_t gi = piece_of(first + (int64_t)k);
           const int64_t len = gi == np - 1 ? last_len : piece_len;
           const int64_t here = std::min<int64_t>(CH, len - coff);
           if (here <= 0) return;
@@ -492,7 +509,7 @@ class GpuVerifier {
         const int block = 64, grid = (int)((n + block - 1) / block);
         hipLaunchKernelGGL((sha1_chunk<true>), dim3(grid), dim3(block), 0, stream_[s], d_state,
                            d_buf_[s], CH, (int)n, piece_len, last_len, (int)first, (int)np, coff,
-                           d_exp, d_ok);
+                           d_exp, d_ok, d_lanes);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipEventRecord(kdone[s], stream_[s]));
         have_prev_kernel = true;
@@ -509,10 +526,14 @@ class GpuVerifier {
     hipFree(d_exp);
     hipFree(d_ok);
     hipFree(d_state);
+    if (d_lanes) hipFree(d_lanes);
     for (int64_t i = 0; i < np; ++i)
       if (!readable[(size_t)i]) ok[(size_t)i] = 0;
     if (timing) *timing = {t_fill, t_wait};
-    return ok;
+    if (!subset) return ok;
+    std::vector<uint8_t> sub((size_t)m);
+    for (int64_t j = 0; j < m; ++j) sub[(size_t)j] = ok[(size_t)which[(size_t)j]];
+    return sub;
   }
 
   // Kernel-only timing (device-resident data, hipEvents): ms per launch hashing `n_pieces`
@@ -690,20 +711,23 @@ PYBIND11_MODULE(_gpuhash, m) {
       .def(
           "verify_files_streamed",
           [](GpuVerifier& g, const std::vector<std::pair<std::string, int64_t>>& files,
-             int64_t piece_len, const py::bytes& hashes, int64_t chunk) {
+             int64_t piece_len, const py::bytes& hashes, int64_t chunk,
+             const std::vector<int>& which) {
             std::string hs = hashes;
             if (piece_len <= 0) throw std::invalid_argument("piece_len must be > 0");
             std::vector<uint8_t> ok;
             std::vector<double> timing;
             {
               py::gil_scoped_release rel;
-              ok = g.verify_files_streamed(files, piece_len, hs, chunk, &timing);
+              ok = g.verify_files_streamed(files, piece_len, hs, chunk, &timing, which);
             }
             return py::make_tuple(py::bytes((const char*)ok.data(), ok.size()),
                                   py::make_tuple(timing[0], timing[1]));
           },
           py::arg("files"), py::arg("piece_len"), py::arg("hashes"), py::arg("chunk") = 65536,
-          "Chunk-streamed SHA-1 verification: returns (ok bytes, (host_fill_s, host_wait_s)).")
+          py::arg("which") = std::vector<int>{},
+          "Chunk-streamed SHA-1 verification: returns (ok bytes, (host_fill_s, host_wait_s)); "
+          "with `which`, one ok byte per listed piece in list order.")
       .def(
           "kernel_bench",
           [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters) {

@@ -111,13 +111,103 @@ def choose_backend(requested: str, total_bytes: int, n_pieces: int) -> str:
 def verify_pieces(files: FileList, piece_len: int, hashes: bytes,
                   which: Optional[Sequence[int]] = None, threads: int = 0,
                   backend: str = "cpu") -> bytes:
-    """One byte per piece (1 = SHA-1 matches). ``which`` restricts the CPU check to a subset;
-    the GPU backend always checks the full storage (recheck use case)."""
+    """One byte per piece (1 = SHA-1 matches). With ``which``, one byte per listed piece in
+    list order. ``backend="auto"`` picks the GPU only for a whole-storage recheck; a subset
+    goes to the GPU when asked for explicitly (see ``GpuBatcher`` for the batched path)."""
     files = [(str(p), int(n)) for p, n in files]
     total = sum(n for _, n in files)
     n_pieces = (total + piece_len - 1) // piece_len if total else 0
-    be = choose_backend(backend, total, n_pieces) if which is None else "cpu"
+    if which is None:
+        be = choose_backend(backend, total, n_pieces)
+    else:
+        be = "gpu" if backend == "gpu" and choose_backend("gpu", total, n_pieces) == "gpu" \
+            else "cpu"
     if be == "gpu":
-        ok, _timing = _verifier().verify_files_streamed(files, piece_len, hashes)
+        v = _verifier()
+        with _gpu_call_lock:
+            ok, _timing = v.verify_files_streamed(files, piece_len, hashes,
+                                                  which=list(which or []))
         return ok
     return native().verify_pieces(files, piece_len, hashes, list(which or []), threads)
+
+
+# One GpuVerifier per process owns two pinned slots and two streams: calls are serialised.
+_gpu_call_lock = threading.Lock()
+
+
+class GpuBatcher:
+    """Coalesces incremental piece checks (webseed runs, peer pieces) into few GPU launches.
+
+    A lane hashes ~41 MB/s (SHA-1 is serial within a piece), so the GPU pays off only with
+    hundreds of pieces in flight: every caller submits its pieces and gets a future; one
+    thread takes everything pending for the same storage, verifies the union in ONE
+    chunk-streamed call and resolves the futures. While a batch runs, the next one fills.
+    Host cost per byte is a pread into pinned memory instead of a SHA-1 pass on a core.
+    """
+
+    def __init__(self, max_pieces: int = 8192):
+        self.max_pieces = max_pieces
+        self._cv = threading.Condition()
+        self._pending: List[tuple] = []
+        self._thread: Optional[threading.Thread] = None
+        self.batches = 0
+        self.pieces = 0
+
+    def submit(self, files: FileList, piece_len: int, hashes: bytes, pieces: Sequence[int]):
+        from concurrent.futures import Future
+        fut: Future = Future()
+        key = (tuple((str(p), int(n)) for p, n in files), int(piece_len), hashes)
+        with self._cv:
+            self._pending.append((key, list(pieces), fut))
+            if self._thread is None:
+                self._thread = threading.Thread(target=self._loop, name="gpu-verify",
+                                                daemon=True)
+                self._thread.start()
+            self._cv.notify()
+        return fut
+
+    def _take(self):
+        with self._cv:
+            while not self._pending:
+                self._cv.wait()
+            key = self._pending[0][0]
+            batch, rest, n = [], [], 0
+            for item in self._pending:
+                if item[0] == key and (n == 0 or n + len(item[1]) <= self.max_pieces):
+                    batch.append(item)
+                    n += len(item[1])
+                else:
+                    rest.append(item)
+            self._pending = rest
+            return key, batch
+
+    def _loop(self) -> None:
+        while True:
+            key, batch = self._take()
+            files, piece_len, hashes = key
+            union = sorted({i for _, ps, _ in batch for i in ps})
+            try:
+                v = _verifier()
+                with _gpu_call_lock:
+                    ok, _t = v.verify_files_streamed(list(files), piece_len, hashes, which=union)
+                pos = {p: ok[j] for j, p in enumerate(union)}
+                self.batches += 1
+                self.pieces += len(union)
+                for _, ps, fut in batch:
+                    if fut.set_running_or_notify_cancel():
+                        fut.set_result([bool(pos[i]) for i in ps])
+            except BaseException as e:  # surface to every waiter, keep serving
+                for _, _, fut in batch:
+                    if not fut.done():
+                        fut.set_exception(e)
+
+
+_batcher: Optional[GpuBatcher] = None
+
+
+def gpu_batcher() -> GpuBatcher:
+    global _batcher
+    with _gpu_lock:
+        if _batcher is None:
+            _batcher = GpuBatcher()
+        return _batcher

@@ -25,11 +25,16 @@ from typing import TYPE_CHECKING, Dict, List, Optional, Set, Tuple
 from urllib.parse import quote
 
 from ..net.http import FileSink, TransportError
+from ..ops import hashing
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
 from .peer import BLOCK, METADATA_PIECE, PIECE, PeerConn
 from .storage import Bitfield, Storage
 from .tracker import decode_compact, encode_compact
+
+# Below this torrent size "auto" keeps incremental verification on the host: a GPU batch needs
+# hundreds of pieces in flight to beat a few SHA-NI cores.
+GPU_INCREMENTAL_MIN_BYTES = 1 << 30
 
 if TYPE_CHECKING:  # pragma: no cover
     from .client import TorrentClient
@@ -275,7 +280,10 @@ class TorrentSession:
         self._wake = asyncio.Event()
         self._closed = False
         self._ws_dead = 0
+        self._ws_live = 0                      # webseed stream tasks still running
+        self._ws_error: Optional[BaseException] = None
         self._ws_files: Dict[int, int] = {}   # file index -> webseed streams writing into it
+        self._gpu_verify: Optional[bool] = None
         self.piece_listeners: List = []   # callbacks(piece index) after a piece is verified
         self._piece_cache: "OrderedDict[int, bytes]" = OrderedDict()   # LRU of served pieces
         self._piece_cache_bytes = 0
@@ -477,7 +485,6 @@ class TorrentSession:
         del self.picker.active[idx]
         buf = bytes(ap.buf)
         loop = asyncio.get_running_loop()
-        from ..ops import hashing
         digest = await loop.run_in_executor(None, hashing.sha1, buf) if len(buf) >= 262144 \
             else hashing.sha1(buf)
         if digest != self.meta.piece_hash(idx):
@@ -645,15 +652,20 @@ class TorrentSession:
         straight into the storage files (splice), hand the run to verification and go on with
         the next run while it is hashed - fetch and SHA-1 overlap within the stream, so a few
         streams saturate the path (parallel writers into one file contend on its inode lock)."""
-        st = {"failures": 0}
+        st = {"failures": 0, "seen": 0}
         verifying: Set[asyncio.Task] = set()
         loop = asyncio.get_running_loop()
         depth = max(1, self.client.webseed_verify_depth)
+        self._ws_live += 1
         try:
             while not self._closed and not self.done.is_set():
                 if st["failures"] >= self.client.webseed_max_failures:
                     self._webseed_gave_up(TorrentError("webseed served corrupt pieces"))
                     return
+                if st["failures"] > st["seen"]:       # a run failed its hash check: back off
+                    st["seen"] = st["failures"]
+                    await asyncio.sleep(min(10.0, 0.2 * (2 ** st["failures"])))
+                    continue
                 run = self.picker.claim_run(self.client.webseed_chunk, self._ws_files)
                 if run is None:
                     if not verifying:
@@ -670,6 +682,7 @@ class TorrentSession:
                 except (TransportError, OSError) as e:
                     self.picker.unclaim(pieces)
                     st["failures"] += 1
+                    st["seen"] = st["failures"]
                     self.stats["webseed_failures"] += 1
                     if st["failures"] >= self.client.webseed_max_failures:
                         self._webseed_gave_up(e)
@@ -688,6 +701,7 @@ class TorrentSession:
         finally:
             for t in verifying:
                 t.cancel()
+            self._webseed_exit()
 
     async def _webseed_fetch(self, base: str, first: int, pieces: List[int]) -> None:
         off = first * self.meta.piece_length
@@ -707,11 +721,32 @@ class TorrentSession:
             self.downloaded += ln
         self.stats["webseed_fetch_s"] += time.perf_counter() - t_fetch
 
+    def _use_gpu_verify(self) -> bool:
+        """Incremental (per-run) verification on the GPU: always for ``verify_backend=gpu``;
+        for ``auto`` only when the verifier is already warm (``download.gpu_prewarm``) and the
+        torrent is big enough to keep hundreds of pieces in flight."""
+        if self._gpu_verify is None:
+            be = self.client.verify_backend
+            if be == "gpu":
+                self._gpu_verify = True
+            elif be == "auto":
+                self._gpu_verify = (hashing._gpu_verifier is not None and
+                                    self.meta.total_length >= GPU_INCREMENTAL_MIN_BYTES and
+                                    hashing.gpu_available())
+            else:
+                self._gpu_verify = False
+        return self._gpu_verify
+
     async def _webseed_verify(self, pieces: List[int], st: Dict[str, int]) -> None:
         t_verify = time.perf_counter()
         try:
-            ok = await asyncio.get_running_loop().run_in_executor(None, self.storage.verify,
-                                                                  pieces)
+            if self._use_gpu_verify():
+                fut = hashing.gpu_batcher().submit(self.storage.paths, self.meta.piece_length,
+                                                   self.meta.pieces, pieces)
+                ok = await asyncio.wrap_future(fut)
+            else:
+                ok = await asyncio.get_running_loop().run_in_executor(None, self.storage.verify,
+                                                                      pieces)
         except OSError:
             self.picker.unclaim(pieces)
             st["failures"] += 1
@@ -728,9 +763,17 @@ class TorrentSession:
 
     def _webseed_gave_up(self, e: BaseException) -> None:
         self._ws_dead += 1
-        if self._ws_dead >= len(self.webseeds) * self.client.webseed_streams and not self.peers \
-                and not self.known and not self.trackers and self.client.dht is None:
-            self.fail(TorrentError(f"webseed failed: {e}"))
+        self._ws_error = e
+
+    def _webseed_exit(self) -> None:
+        """A stream ended. Streams that found nothing left to claim end normally, so when the
+        LAST one ends after another gave up, pieces may be left that nobody fetches: with no
+        other source (peers, trackers, DHT) the session fails instead of waiting forever."""
+        self._ws_live -= 1
+        if self._ws_live == 0 and self._ws_error is not None and not self.done.is_set() \
+                and not self.peers and not self.known and not self.trackers \
+                and self.client.dht is None:
+            self.fail(TorrentError(f"webseed failed: {self._ws_error}"))
 
     # ---------------------------------------------------------------- shutdown
     async def wait(self) -> None:

@@ -15,6 +15,7 @@ from downloader_amd.torrent.bencode import BencodeError, bdecode, bencode, decod
 from downloader_amd.torrent.client import TorrentClient
 from downloader_amd.torrent.magnet import Magnet, MagnetError, parse_magnet
 from downloader_amd.torrent.metainfo import MetainfoError, make_torrent, parse_torrent
+from downloader_amd.torrent.session import TorrentError
 from downloader_amd.torrent.tracker import announce
 from downloader_amd.torrent.tracker_server import Tracker
 
@@ -442,3 +443,61 @@ def test_webseed_claims_spread_over_files():
     assert [g[2] for g in got[:3]] == [0, 2, 3]            # one stream per file first
     assert sorted(p for g in got for p in range(g[0], g[0] + g[1])) == list(range(12))
     assert pp.claim_run(8, busy) is None
+
+
+def test_webseed_gpu_verify_path_through_batcher(run, tmp_path, origin_cls, monkeypatch):
+    """verify_backend=gpu routes every fetched run through GpuBatcher. The device is stood in
+    for by the host verifier here (the real kernel: tests/test_gpu_hash.py), so the CPU tier
+    covers the batching, result mapping and a corrupt-run refetch."""
+    from downloader_amd.ops import hashing, native
+
+    class HostVerifier:
+        def verify_files_streamed(self, files, plen, hashes, chunk=65536, which=()):
+            return native().verify_pieces(files, plen, hashes, list(which), 0), (0.0, 0.0)
+
+    monkeypatch.setattr(hashing, "_verifier", lambda: HostVerifier())
+    monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    batcher = hashing.GpuBatcher()
+    monkeypatch.setattr(hashing, "gpu_batcher", lambda: batcher)
+
+    async def go():
+        origin = await origin_cls().start()
+        src = tmp_path / "ws"
+        data = _tree(src / "Pack", {"a.mkv": 1_000_003, "dir/b.mkv": 377_777})
+        raw = make_torrent(str(src / "Pack"), 65536, url_list=[origin.url("/seed/")])
+        for rel, d in data.items():
+            origin.blobs["/seed/Pack/" + rel] = d
+        # the first GET of a.mkv's head serves a corrupt byte -> hash fail -> refetch
+        good = data["a.mkv"]
+        origin.blobs["/seed/Pack/a.mkv"] = b"\xff" + good[1:]
+        c = TorrentClient(webseed_chunk=200_000, webseed_streams=3, verify_backend="gpu")
+        await c.start()
+        s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        await asyncio.sleep(0.3)
+        origin.blobs["/seed/Pack/a.mkv"] = good
+        await asyncio.wait_for(s.wait(), 30)
+        _check(tmp_path / "dl", data)
+        assert s._gpu_verify is True and batcher.pieces >= s.meta.num_pieces
+        assert s.stats["hash_fails"] >= 1
+        await c.close(); await origin.stop()
+    run(go())
+
+
+def test_webseed_serving_corrupt_data_fails_session(run, tmp_path, origin_cls):
+    """A webseed that keeps serving a bad piece: the owning stream backs off, gives up after
+    webseed_max_failures, and - with no peers/trackers/DHT - the session fails instead of
+    waiting forever for a piece nobody fetches."""
+    async def go():
+        origin = await origin_cls().start()
+        src = tmp_path / "ws"
+        data = _tree(src / "Pack", {"a.mkv": 300_000})
+        raw = make_torrent(str(src / "Pack"), 65536, url_list=[origin.url("/seed/")])
+        origin.blobs["/seed/Pack/a.mkv"] = data["a.mkv"][:70_000] + b"\x00" + data["a.mkv"][70_001:]
+        c = TorrentClient(webseed_chunk=65536, webseed_streams=2, webseed_max_failures=2)
+        await c.start()
+        s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        with pytest.raises(TorrentError, match="webseed failed"):
+            await asyncio.wait_for(s.wait(), 30)
+        assert s.stats["hash_fails"] >= 2 and 1 not in s.have
+        await c.close(); await origin.stop()
+    run(go())
