@@ -155,6 +155,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["webseed_chunk"] = a.webseed_chunk_mb << 20
             if a.webseed_verify_depth:
                 dl["webseed_verify_depth"] = a.webseed_verify_depth
+            if getattr(a, "no_gpu_prewarm", False):
+                dl["gpu_prewarm"] = False
             w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl),
                        broker=MemoryBroker())
             await w.start(health=False)
@@ -319,6 +321,8 @@ def main(argv=None) -> int:
     ap.add_argument("--webseed-streams", type=int, default=0)
     ap.add_argument("--webseed-chunk-mb", type=int, default=0)
     ap.add_argument("--webseed-verify-depth", type=int, default=0)
+    ap.add_argument("--no-gpu-prewarm", action="store_true",
+                    help="do not init the GPU verifier at worker start (download.gpu_prewarm)")
     ap.add_argument("--workers", type=int, default=4, help="config 5 worker processes")
     ap.add_argument("--concurrency", type=int, default=4, help="config 5 jobs per worker")
     ap.add_argument("--qps", type=float, default=50.0, help="config 5 offered job rate")

@@ -97,9 +97,10 @@ class DownloadConfig(BaseModel):
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
-    # Initialise the GPU verifier at worker start (device = worker index % GPUs) so "auto"
-    # rechecks of >=256 MiB go to the GPU instead of paying the cold start per job.
-    gpu_prewarm: bool = False
+    # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
+    # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of
+    # torrents >= 8 GiB to the GPU instead of paying the cold start inside a job.
+    gpu_prewarm: bool = True
     torrent_listen_port: int = 0
     torrent_max_peers: int = 32
     torrent_enable_dht: bool = True
@@ -109,6 +110,7 @@ class DownloadConfig(BaseModel):
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on
+    webseed_verify_depth_gpu: int = 32          # same when runs are verified by the GPU batcher
     cleanup_on_stall: bool = True               # App. A #6 (reference leaves data behind)
     emit_errored_on_stall: bool = False         # App. A #6 (reference: ack silently)
 
