@@ -141,7 +141,8 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
         "concurrency": args.concurrency,
         "instance": {"download_path": stage_root},
         "s3": {"endpoint": endpoint},
-        "download": {},
+        # HTTP staging never verifies torrent pieces: no GPU verifier (HIP init, pinned slots)
+        "download": {"gpu_prewarm": False},
         "broker": {"backend": "memory"},
         "health": {"enabled": False},
     }

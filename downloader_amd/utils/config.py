@@ -165,6 +165,7 @@ class Config(BaseModel):
             self.download.http_streams = 1
             self.download.bucket_concurrency = 1
             self.download.webseed_streams = 1
+            self.download.webseed_verify_depth = 1   # fetch -> verify -> fetch, one thread
             self.download.stream_http = False
             self.download.eager_upload = False
             self.instance.background_cleanup = False
