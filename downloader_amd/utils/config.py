@@ -166,6 +166,8 @@ class Config(BaseModel):
             self.download.bucket_concurrency = 1
             self.download.webseed_streams = 1
             self.download.webseed_verify_depth = 1   # fetch -> verify -> fetch, one thread
+            self.download.verify_backend = "cpu"     # webtorrent hashes on the host
+            self.download.gpu_prewarm = False
             self.download.stream_http = False
             self.download.eager_upload = False
             self.instance.background_cleanup = False
