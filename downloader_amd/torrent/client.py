@@ -23,7 +23,7 @@ class TorrentClient:
                  enable_dht: bool = False, dht_bootstrap: Sequence[Peer] = (),
                  dht_port: int = 0, verify_backend: str = "auto", webseed_streams: int = 4,
                  webseed_chunk: int = 32 << 20, webseed_verify_depth: int = 2,
-                 webseed_verify_depth_gpu: int = 32,
+                 webseed_verify_depth_gpu: int = 32, verify_threads: int = 0,
                  webseed_max_failures: int = 5,
                  idle_timeout: float = 120.0, connect_timeout: float = 10.0,
                  seed_after_done: bool = False, listen: bool = True):
@@ -46,6 +46,7 @@ class TorrentClient:
         self.webseed_chunk = webseed_chunk
         self.webseed_verify_depth = webseed_verify_depth
         self.webseed_verify_depth_gpu = webseed_verify_depth_gpu
+        self.verify_threads = verify_threads
         self.webseed_max_failures = webseed_max_failures
         self.idle_timeout = idle_timeout
         self.connect_timeout = connect_timeout
@@ -69,6 +70,7 @@ class TorrentClient:
                    webseed_streams=max(1, d.webseed_streams or d.http_streams),
                    webseed_chunk=d.webseed_chunk, webseed_verify_depth=d.webseed_verify_depth,
                    webseed_verify_depth_gpu=d.webseed_verify_depth_gpu,
+                   verify_threads=d.verify_threads,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

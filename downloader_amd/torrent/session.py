@@ -748,8 +748,8 @@ class TorrentSession:
                                                    self.meta.pieces, pieces)
                 ok = await asyncio.wrap_future(fut)
             else:
-                ok = await asyncio.get_running_loop().run_in_executor(None, self.storage.verify,
-                                                                      pieces)
+                ok = await asyncio.get_running_loop().run_in_executor(
+                    None, self.storage.verify, pieces, self.client.verify_threads)
         except OSError:
             self.picker.unclaim(pieces)
             st["failures"] += 1

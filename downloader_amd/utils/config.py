@@ -97,6 +97,7 @@ class DownloadConfig(BaseModel):
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
+    verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
     # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of
     # torrents >= 8 GiB to the GPU instead of paying the cold start inside a job.
@@ -162,11 +163,15 @@ class Config(BaseModel):
             self.broker.prefetch = 1
             self.s3.concurrent_files = 1
             self.s3.max_inflight_parts = 1
+            # minio-js over plain HTTP signs every PUT/part with its payload SHA-256
+            # (SURVEY §2.5); over TLS it would send UNSIGNED-PAYLOAD + Content-MD5 instead.
+            self.s3.unsigned_payload = self.s3.secure
             self.download.http_streams = 1
             self.download.bucket_concurrency = 1
             self.download.webseed_streams = 1
             self.download.webseed_verify_depth = 1   # fetch -> verify -> fetch, one thread
-            self.download.verify_backend = "cpu"     # webtorrent hashes on the host
+            self.download.verify_backend = "cpu"     # webtorrent hashes on the host,
+            self.download.verify_threads = 1         # on its one JS thread (simple-sha1)
             self.download.gpu_prewarm = False
             self.download.stream_http = False
             self.download.eager_upload = False

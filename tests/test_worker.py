@@ -426,3 +426,21 @@ def test_reaper_renames_then_unlinks_and_sweeps(tmp_path):
     inline = Reaper(str(root), background=False)
     assert inline.reap(str(root / "j2")) is None and not (root / "j2").exists()
     assert inline.reap(str(root / "missing")) is None
+
+
+def test_signed_payload_staging(run, make_cfg, origin_cls):
+    """s3.unsigned_payload=False (minio-js over plain HTTP; reference mode): every PUT and
+    part carries its SHA-256, which FakeS3 checks against the body it received."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls,
+                                        s3={"unsigned_payload": False},
+                                        download={"stream_http": False})
+        blob = os.urandom(13 * 1024 * 1024 + 7)           # > threshold: multipart, 3 parts
+        origin.blobs["/m/signed.mkv"] = blob
+        await w.submit(api.make_download("sig1", "http", origin.url("/m/signed.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        key = "sig1/original/" + base64.b64encode(b"signed.mkv").decode()
+        assert s3.get("triton-staging", key) == blob
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
