@@ -501,3 +501,29 @@ def test_webseed_serving_corrupt_data_fails_session(run, tmp_path, origin_cls):
         assert s.stats["hash_fails"] >= 2 and 1 not in s.have
         await c.close(); await origin.stop()
     run(go())
+
+
+def test_auto_incremental_verify_policy(monkeypatch):
+    """auto: GPU batches only with a warm verifier AND a torrent big enough to amortise the
+    ~100 ms batch latency; reference mode never (host, one thread)."""
+    from downloader_amd.ops import hashing
+    from downloader_amd.torrent import session as S
+    from downloader_amd.torrent.metainfo import FileEntry, Metainfo
+    monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+
+    def sess(backend, total):
+        c = TorrentClient(verify_backend=backend, listen=False)
+        m = Metainfo(b"y" * 20, "t", 1 << 22, b"\0" * 20, [FileEntry(["t"], total, 0)], total)
+        return S.TorrentSession(c, m.info_hash, "/nonexistent", m)
+    big, small = S.GPU_INCREMENTAL_MIN_BYTES, S.GPU_INCREMENTAL_MIN_BYTES - 1
+    monkeypatch.setattr(hashing, "_gpu_verifier", None)
+    assert sess("auto", big)._use_gpu_verify() is False          # cold device
+    monkeypatch.setattr(hashing, "_gpu_verifier", object())
+    assert sess("auto", big)._use_gpu_verify() is True
+    assert sess("auto", small)._use_gpu_verify() is False
+    assert sess("cpu", big)._use_gpu_verify() is False
+    assert sess("gpu", 1)._use_gpu_verify() is True
+    from downloader_amd.utils.config import load_config
+    ref = load_config(overrides={"mode": "reference"}, env={})
+    assert ref.download.verify_backend == "cpu" and ref.download.verify_threads == 1
+    assert ref.download.webseed_verify_depth == 1 and not ref.s3.unsigned_payload
