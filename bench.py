@@ -56,6 +56,9 @@ def parse() -> argparse.Namespace:
                    help="one blobd origin+S3 peer per worker, or one shared on rank 0")
     p.add_argument("--sink", choices=["discard", "checksum"], default="discard",
                    help="blobd S3 sink: splice bodies to /dev/null, or checksum every byte")
+    p.add_argument("--cpus-per-rank", type=int, default=0,
+                   help="pin each rank (worker + its peer) to this many CPUs; 0: node CPUs / "
+                        "ranks, -1: no pinning")
     p.add_argument("--compare-reference", action="store_true",
                    help="also time reference-equivalent mode and report the ratio")
     return p.parse_args()
@@ -216,17 +219,20 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
             "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all}
 
 
-def pin_rank(dist: Dist) -> list:
-    """With N>1 ranks on one node, give each rank (worker threads + its blobd, which inherits
-    the mask) a disjoint, contiguous slice of the allowed CPUs: no cross-rank cache thrash and
-    sockets/threads stay on one CCD/NUMA domain. Returns the slice ([] = unpinned)."""
-    if dist.world <= 1 or os.environ.get("STAGER_BENCH_NO_PIN") == "1":
+def pin_rank(dist: Dist, per_rank: int = 0) -> list:
+    """Give each rank (worker threads + its blobd, which inherits the mask) a disjoint,
+    contiguous slice of the allowed CPUs: no cross-rank cache thrash and sockets/threads stay
+    on one CCD/NUMA domain. ``per_rank`` 0 = allowed CPUs / local ranks (N>1 only), -1 = off,
+    K = exactly K CPUs per rank (also for N=1). Returns the slice ([] = unpinned)."""
+    if per_rank < 0 or os.environ.get("STAGER_BENCH_NO_PIN") == "1":
+        return []
+    if dist.world <= 1 and per_rank == 0:
         return []
     cpus = sorted(os.sched_getaffinity(0))
     local = int(os.environ.get("LOCAL_RANK", dist.rank))
     nlocal = int(os.environ.get("LOCAL_WORLD_SIZE", dist.world))
-    per = len(cpus) // max(1, nlocal)
-    if per < 2:
+    per = per_rank or len(cpus) // max(1, nlocal)
+    if per < 2 or per * nlocal > len(cpus):
         return []
     mine = cpus[local * per:(local + 1) * per]
     os.sched_setaffinity(0, mine)
@@ -236,7 +242,7 @@ def pin_rank(dist: Dist) -> list:
 def main() -> int:
     args = parse()
     dist = Dist(args.gpus)
-    pinned = pin_rank(dist)
+    pinned = pin_rank(dist, args.cpus_per_rank)
     from downloader_amd.bench.infra import Blobd
     blob = None
     endpoint = None
