@@ -280,6 +280,7 @@ PYBIND11_MODULE(_native, m) {
           "PUT sent on `dst` (socket->pipe->socket splice). The GET must answer 200/206 with "
           "that Content-Length, otherwise nothing is sent on `dst`.")
       .def("close", &HttpConn::close)
+      .def("abort", &HttpConn::abort)
       .def_property_readonly("is_open", &HttpConn::is_open)
       .def_property_readonly("reusable", &HttpConn::reusable)
       .def_property_readonly("host", &HttpConn::host)

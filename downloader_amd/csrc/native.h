@@ -109,6 +109,10 @@ class HttpConn {
   int fd() const { return fd_; }
   void mark_unusable() { reusable_ = false; }
   void close();
+  // Unblock a transfer running on another thread (cancelled job, shutdown): shut the
+  // socket down in both directions; the owner's recv/splice/send then fails fast and
+  // the owner closes the fd as usual.
+  void abort();
   bool is_open() const { return fd_ >= 0; }
   bool reusable() const { return fd_ >= 0 && reusable_; }
   const std::string& host() const { return host_; }

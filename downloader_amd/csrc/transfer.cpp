@@ -114,6 +114,12 @@ void HttpConn::close() {
     }
 }
 
+void HttpConn::abort() {
+  reusable_ = false;
+  const int fd = fd_;
+  if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
+}
+
 void HttpConn::send_all(const uint8_t* p, size_t n) {
   while (n) {
     ssize_t w = ::send(fd_, p, n, MSG_NOSIGNAL);

@@ -18,7 +18,7 @@ import os
 import threading
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
+from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
 from urllib.parse import urlsplit
 
 Headers = Sequence[Tuple[str, str]]
@@ -134,6 +134,10 @@ class NativeTransport(Transport):
         self._pool: Dict[Tuple[str, int], List[object]] = {}
         self._lock = threading.Lock()
         self._exec = ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="xfer")
+        # connections of requests in flight (one list per request), so a cancelled request or
+        # close() can abort() the socket a blocked native transfer sits on
+        self._inflight: Set[int] = set()
+        self._slots: Dict[int, List[object]] = {}
         self.connect_timeout = connect_timeout
         self.io_timeout = io_timeout
         self.max_idle = max_idle_per_host
@@ -159,14 +163,32 @@ class NativeTransport(Transport):
                 return
         conn.close()
 
+    def _track(self, slot: int, conn) -> None:
+        with self._lock:
+            self._slots.setdefault(slot, []).append(conn)
+
+    def _untrack(self, slot: int, conn) -> None:
+        """Before the owner releases or closes ``conn``: afterwards an abort must not reach it
+        (pooled for another request, or its fd number reused)."""
+        with self._lock:
+            lst = self._slots.get(slot)
+            if lst is not None and conn in lst:
+                lst.remove(conn)
+
+    def _abort_slot(self, slot: int) -> None:
+        with self._lock:   # under the lock: the owner cannot close the fd meanwhile
+            for c in self._slots.pop(slot, []):
+                c.abort()
+
     def _do(self, method: str, host: str, port: int, host_hdr: str, path: str,
             headers: Headers, body, sink: Optional[FileSink], nprog,
-            expect_body: bool) -> Response:
+            expect_body: bool, slot: int = 0) -> Response:
         blen = body.length if isinstance(body, FileRange) else (len(body) if body else 0)
         head = _build_head(method, host_hdr, path, headers, blen if body is not None else
                            (0 if method in ("PUT", "POST") else None))
         for attempt in (0, 1):
             conn, reused = self._acquire(host, port)
+            self._track(slot, conn)
             try:
                 if isinstance(body, FileRange):
                     d = conn.request_fd(head, body.fd, body.offset, body.length, nprog)
@@ -175,12 +197,14 @@ class NativeTransport(Transport):
                 else:
                     d = conn.request(head, body, expect_body and method != "HEAD")
             except RuntimeError as e:
+                self._untrack(slot, conn)
                 conn.close()
                 # A pooled keep-alive socket may have been closed by the peer: retry once on
                 # a fresh connection (the whole request is re-sent; bodies are re-readable).
                 if reused and attempt == 0 and not (nprog is not None and nprog.cancelled):
                     continue
                 raise TransportError(f"{method} {host}:{port}{path}: {e}") from e
+            self._untrack(slot, conn)
             self._release(conn)
             return Response(d["status"], list(d["headers"]), d.get("body", b""),
                             d.get("written", 0), d.get("reason", ""))
@@ -199,33 +223,55 @@ class NativeTransport(Transport):
                 progress.native = self._n.Progress()
             nprog = progress.native
         loop = asyncio.get_running_loop()
+        slot = self._new_slot()
         fut = loop.run_in_executor(self._exec, self._do, method, host, port, host_hdr, path,
-                                   headers, body, sink, nprog, expect_body)
+                                   headers, body, sink, nprog, expect_body, slot)
         try:
             return await asyncio.shield(fut)
         except asyncio.CancelledError:
             if nprog is not None:
                 nprog.cancel()
+            self._abort_slot(slot)
             raise
+        finally:
+            self._end_slot(slot)
+
+    def _new_slot(self) -> int:
+        with self._lock:
+            self._seq = getattr(self, "_seq", 0) + 1
+            self._inflight.add(self._seq)
+            return self._seq
+
+    def _end_slot(self, slot: int) -> None:
+        with self._lock:
+            self._inflight.discard(slot)
+            self._slots.pop(slot, None)
 
     def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
-               length: int, nprog) -> Tuple[Response, Optional[Response], int]:
+               length: int, nprog, slot: int = 0) -> Tuple[Response, Optional[Response], int]:
         _, sh, sp, spath = split_host(src_url)
         _, dh, dp, dpath = split_host(dst_url)
         get_head = _build_head("GET", sh if sp == 80 else f"{sh}:{sp}", spath, src_headers, None)
         put_head = _build_head("PUT", dh if dp == 80 else f"{dh}:{dp}", dpath, dst_headers, length)
         src, _ = self._acquire(sh, sp)
+        self._track(slot, src)
         try:
             dst, _ = self._acquire(dh, dp)
         except BaseException:
+            self._untrack(slot, src)
             self._release(src)
             raise
+        self._track(slot, dst)
         try:
             d = src.relay_to(get_head, dst, put_head, length, nprog)
         except RuntimeError as e:
+            self._untrack(slot, src)
+            self._untrack(slot, dst)
             src.close()
             dst.close()
             raise TransportError(f"relay {spath} -> {dpath}: {e}") from e
+        self._untrack(slot, src)
+        self._untrack(slot, dst)
         self._release(src)
         self._release(dst)
         g = d["get"]
@@ -248,19 +294,27 @@ class NativeTransport(Transport):
                 progress.native = self._n.Progress()
             nprog = progress.native
         loop = asyncio.get_running_loop()
+        slot = self._new_slot()
         fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
-                                   dst_headers, length, nprog)
+                                   dst_headers, length, nprog, slot)
         try:
             return await asyncio.shield(fut)
         except asyncio.CancelledError:
             if nprog is not None:
                 nprog.cancel()
+            self._abort_slot(slot)
             raise
+        finally:
+            self._end_slot(slot)
 
     async def close(self) -> None:
         with self._lock:
             conns = [c for v in self._pool.values() for c in v]
             self._pool.clear()
+            for v in self._slots.values():
+                for c in v:
+                    c.abort()   # transfers still running on executor threads fail fast
+            self._slots.clear()
         for c in conns:
             c.close()
         self._exec.shutdown(wait=False)

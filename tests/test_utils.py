@@ -126,3 +126,28 @@ def test_native_effective_cpus_matches_python():
     from downloader_amd.ops import native
     from downloader_amd.utils.cpus import effective_cpus
     assert native().effective_cpus() == effective_cpus()
+
+
+def test_cancelled_native_request_frees_its_thread(run):
+    """A request stuck on a silent server: cancelling it aborts the socket, so the single
+    executor thread is free again at once instead of after io_timeout."""
+    import asyncio
+    import socket
+    import time
+    from downloader_amd.net.http import NativeTransport
+
+    async def go():
+        srv = socket.socket()
+        srv.bind(("127.0.0.1", 0))
+        srv.listen(4)
+        port = srv.getsockname()[1]
+        t = NativeTransport(max_workers=1, connect_timeout=5, io_timeout=60)
+        task = asyncio.ensure_future(t.request("GET", f"http://127.0.0.1:{port}/x"))
+        await asyncio.sleep(0.3)
+        task.cancel()
+        t0 = time.perf_counter()
+        await asyncio.get_running_loop().run_in_executor(t._exec, lambda: None)
+        assert time.perf_counter() - t0 < 5
+        await t.close()
+        srv.close()
+    run(go(), timeout=30)
