@@ -134,7 +134,8 @@ def main(argv=None) -> int:
     s.add_argument("-n", type=int, default=max(1, effective_cpus() // 4))
     s.add_argument("--config", default="")
     s.add_argument("--mode", choices=["tuned", "reference"], default="")
-    s.add_argument("--cpus-per-worker", type=int, default=0)
+    s.add_argument("--cpus-per-worker", type=int, default=0,
+                   help="K: pin each worker to K CPUs; 0: share of the cgroup quota; -1: off")
     s.add_argument("--base-port", type=int, default=0)
     b = sub.add_parser("broker")
     b.add_argument("--host", default="0.0.0.0")

@@ -9,6 +9,7 @@ worker stays on one CCD of the host EPYC.
 """
 from __future__ import annotations
 
+import math
 import os
 import signal
 import subprocess
@@ -28,9 +29,24 @@ class Slot:
     exit_codes: List[int] = field(default_factory=list)
 
 
+def auto_cpus_per_worker(n_workers: int, available: Sequence[int], quota: float) -> int:
+    """Each worker's share of the CPU quota (contiguous pinning measured +40 % on the build box,
+    where the mask spans 256 CPUs but the quota is 16); 0 (no pinning) without a quota or when
+    the share would be the whole mask."""
+    if quota == float("inf") or n_workers <= 0:
+        return 0
+    per = min(len(available) // n_workers, max(2, math.ceil(quota / n_workers)))
+    return per if per < len(available) else 0
+
+
 def cpu_slices(n_workers: int, cpus_per_worker: int, available: Optional[Sequence[int]] = None
                ) -> List[List[int]]:
+    """``cpus_per_worker``: K > 0 pins every worker to K contiguous CPUs, 0 = auto (quota
+    share, ``auto_cpus_per_worker``), < 0 = no pinning."""
     cpus = sorted(available if available is not None else os.sched_getaffinity(0))
+    if cpus_per_worker == 0:
+        from ..utils.cpus import cgroup_cpu_quota
+        cpus_per_worker = auto_cpus_per_worker(n_workers, cpus, cgroup_cpu_quota())
     if cpus_per_worker <= 0:
         return [[] for _ in range(n_workers)]
     out = []

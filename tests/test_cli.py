@@ -87,3 +87,32 @@ def test_worker_exits_zero_on_sigterm_when_idle(run, tmp_path):
         assert code == 0            # termHandler: exit(0) when no job is in flight
         await srv.stop()
     run(go(), timeout=60)
+
+
+def test_bench_pin_rank_quota_share(monkeypatch):
+    """bench.py pins each rank to its share of the CPU quota (contiguous, disjoint)."""
+    import os
+    import types
+
+    import bench
+    from downloader_amd.utils import cpus
+    got = {}
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, s: got.setdefault("mask", list(s)))
+    monkeypatch.delenv("STAGER_BENCH_NO_PIN", raising=False)
+    monkeypatch.setattr(cpus, "cgroup_cpu_quota", lambda path="": 16.0)
+    one = types.SimpleNamespace(world=1, rank=0)
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    assert bench.pin_rank(one) == list(range(16))
+    assert bench.pin_rank(one, -1) == []
+    monkeypatch.setattr(cpus, "cgroup_cpu_quota", lambda path="": 128.0)
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    eight = types.SimpleNamespace(world=8, rank=3)
+    assert bench.pin_rank(eight) == list(range(48, 64))
+    monkeypatch.setattr(cpus, "cgroup_cpu_quota", lambda path="": float("inf"))
+    assert bench.pin_rank(eight) == list(range(96, 128))        # no quota: 256 / 8
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert bench.pin_rank(one) == []                            # no quota, N=1: leave it

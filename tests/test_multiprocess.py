@@ -89,3 +89,14 @@ def test_bench_single_rank_defaults_are_valid(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["n_gpus"] == 1 and j["higher_is_better"] is True and j["scaling"] == "weak"
+
+
+def test_supervisor_auto_pinning_quota_share():
+    from downloader_amd.parallel.supervisor import auto_cpus_per_worker, cpu_slices
+    mask = list(range(256))
+    assert auto_cpus_per_worker(4, mask, 16.0) == 4
+    assert auto_cpus_per_worker(1, mask, 16.0) == 16
+    assert auto_cpus_per_worker(4, mask, float("inf")) == 0
+    assert auto_cpus_per_worker(1, list(range(8)), 16.0) == 0     # share = whole mask
+    assert cpu_slices(2, 3, list(range(8))) == [[0, 1, 2], [3, 4, 5]]
+    assert cpu_slices(2, -1, list(range(8))) == [[], []]
