@@ -23,7 +23,6 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
-import math
 import os
 import shutil
 import statistics
@@ -231,21 +230,14 @@ def pin_rank(dist: Dist, per_rank: int = 0) -> list:
     Returns the slice ([] = unpinned)."""
     if per_rank < 0 or os.environ.get("STAGER_BENCH_NO_PIN") == "1":
         return []
-    from downloader_amd.utils.cpus import cgroup_cpu_quota
-    cpus = sorted(os.sched_getaffinity(0))
+    from downloader_amd.utils import cpus
     local = int(os.environ.get("LOCAL_RANK", dist.rank))
     nlocal = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", dist.world)))
-    per = per_rank
-    if per == 0:
-        per = len(cpus) // nlocal
-        quota = cgroup_cpu_quota()
-        if quota != float("inf"):
-            per = min(per, max(2, math.ceil(quota / nlocal)))
-    if per < 2 or per * nlocal > len(cpus) or (nlocal == 1 and per >= len(cpus)):
-        return []
-    mine = cpus[local * per:(local + 1) * per]
-    os.sched_setaffinity(0, mine)
-    return mine
+    if per_rank == 0 and cpus.cgroup_cpu_quota() == float("inf"):
+        if nlocal == 1:
+            return []
+        per_rank = len(os.sched_getaffinity(0)) // nlocal
+    return cpus.pin_share(local, nlocal, per_rank)
 
 
 def main() -> int:

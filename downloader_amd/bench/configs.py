@@ -328,8 +328,14 @@ def main(argv=None) -> int:
     ap.add_argument("--qps", type=float, default=50.0, help="config 5 offered job rate")
     ap.add_argument("--src-dir", default="/dev/shm" if os.path.isdir("/dev/shm") else None)
     ap.add_argument("--stage-dir", default="")
+    ap.add_argument("--cpus", type=int, default=0,
+                    help="pin the bench (worker, blobd, config-5 workers) to this many CPUs; "
+                         "0: the cgroup quota share, -1: no pinning")
     a = ap.parse_args(argv)
     os.environ.setdefault("LOG_LEVEL", "error")
+    if a.cpus >= 0:
+        from downloader_amd.utils.cpus import pin_share
+        pin_share(0, 1, a.cpus)
     for c in a.config:
         if c == 1:
             out = asyncio.run(config1(a))

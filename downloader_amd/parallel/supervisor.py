@@ -9,7 +9,6 @@ worker stays on one CCD of the host EPYC.
 """
 from __future__ import annotations
 
-import math
 import os
 import signal
 import subprocess
@@ -30,13 +29,9 @@ class Slot:
 
 
 def auto_cpus_per_worker(n_workers: int, available: Sequence[int], quota: float) -> int:
-    """Each worker's share of the CPU quota (contiguous pinning measured +40 % on the build box,
-    where the mask spans 256 CPUs but the quota is 16); 0 (no pinning) without a quota or when
-    the share would be the whole mask."""
-    if quota == float("inf") or n_workers <= 0:
-        return 0
-    per = min(len(available) // n_workers, max(2, math.ceil(quota / n_workers)))
-    return per if per < len(available) else 0
+    """Each worker's share of the CPU quota (``utils.cpus.quota_share``)."""
+    from ..utils.cpus import quota_share
+    return quota_share(available, n_workers, quota) if n_workers > 0 else 0
 
 
 def cpu_slices(n_workers: int, cpus_per_worker: int, available: Optional[Sequence[int]] = None
