@@ -50,6 +50,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--http-streams", type=int, default=0, help="override download.http_streams")
     p.add_argument("--part-mb", type=int, default=0, help="override s3.part_size (MiB)")
     p.add_argument("--inflight-parts", type=int, default=0, help="override s3.max_inflight_parts")
+    p.add_argument("--threshold-mb", type=int, default=0,
+                   help="override s3.multipart_threshold (MiB; objects up to it go in one PUT)")
     p.add_argument("--staging", choices=["stream", "disk"], default="stream",
                    help="stream: single-file HTTP jobs relay origin->S3; disk: stage on disk first")
     p.add_argument("--peers", choices=["per-rank", "shared"], default="per-rank",
@@ -156,6 +158,8 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
             over["s3"]["part_size"] = args.part_mb << 20
         if args.inflight_parts:
             over["s3"]["max_inflight_parts"] = args.inflight_parts
+        if args.threshold_mb:
+            over["s3"]["multipart_threshold"] = args.threshold_mb << 20
         over["download"]["stream_http"] = args.staging == "stream"
     cfg = load_config(overrides=over, env={})
     worker = Worker(cfg, broker=MemoryBroker())

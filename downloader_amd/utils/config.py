@@ -42,7 +42,9 @@ class S3Config(BaseModel):
     region: str = "us-east-1"
     secure: bool = False
     bucket: str = "triton-staging"
-    part_size: int = 16 * MiB
+    # minio-js 7 default; per-request Python cost (SigV4, executor hop) makes fewer, larger
+    # parts faster even for the socket relay: 100 MB jobs 37 GB/s @16 MiB -> 47.5 GB/s @64 MiB
+    part_size: int = 64 * MiB
     multipart_threshold: int = 64 * MiB
     max_inflight_parts: int = 8
     concurrent_files: int = 4
