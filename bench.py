@@ -177,14 +177,17 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
     dist.barrier()
     cuda_sync()
     t0 = time.perf_counter()
+    loop_cpu0 = time.thread_time()
     dt, res = await run_phase(worker, url, dist.rank, args.warmup * B, args.steps * B, size, mode)
+    loop_cpu = time.thread_time() - loop_cpu0
     cuda_sync()
     t1 = time.perf_counter()
     bad = [r for r in res if r.outcome != "staged"]
     await worker.stop()
+    # event-loop thread CPU / wall: ~1.0 means the Python side (one thread) is the limit
     return {"elapsed": t1 - t0, "latencies": [r.seconds for r in res],
             "bytes": sum(r.bytes for r in res), "failed": len(bad),
-            "err": bad[0].error if bad else ""}
+            "err": bad[0].error if bad else "", "loop_busy": loop_cpu / max(1e-9, t1 - t0)}
 
 
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
@@ -220,7 +223,8 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
             "p90": sorted(lats)[int(0.9 * (len(lats) - 1))] if lats else 0.0,
             "bytes": total_bytes, "sink_bytes": sink,
             "worker_cpu_s_per_GB": sum(r["worker_cpu_s"] for r in allr) / gb_all,
-            "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all}
+            "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all,
+            "loop_busy": max(r["loop_busy"] for r in allr)}
 
 
 def pin_rank(dist: Dist, per_rank: int = 0) -> list:
@@ -282,6 +286,7 @@ def main() -> int:
             "p50_job_latency_s": round(tuned["p50"], 4),
             "s3_peer_bytes_received": tuned["sink_bytes"],
             "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
+            "event_loop_busy": round(tuned["loop_busy"], 3),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
             "peers": args.peers,
             "cpus_per_rank": len(pinned) if pinned else len(os.sched_getaffinity(0)),
