@@ -30,6 +30,7 @@ import statistics
 import sys
 import tempfile
 import time
+from typing import Optional
 
 os.environ.setdefault("LOG_LEVEL", "warn")
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -64,6 +65,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--cpus-per-rank", type=int, default=0,
                    help="pin each rank (worker + its peer) to this many CPUs; 0: allowed CPUs / "
                         "ranks capped by the cgroup quota share, -1: no pinning")
+    p.add_argument("--procs-per-rank", type=int, default=0,
+                   help="worker processes per rank; 0: one per 8 CPUs of the rank's slice")
     p.add_argument("--compare-reference", action="store_true",
                    help="also time reference-equivalent mode and report the ratio")
     return p.parse_args()
@@ -154,12 +157,11 @@ async def run_phase(worker, blob_ep_url, rank: int, first: int, count: int, size
     return dt, results
 
 
-async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str):
+async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
     from downloader_amd.broker.memory import MemoryBroker
     from downloader_amd.service.worker import Worker
     from downloader_amd.utils.config import load_config
 
-    size = int(args.size_mb * 1e6)
     over = {
         "mode": mode,
         "concurrency": args.concurrency,
@@ -187,41 +189,141 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str)
 
     def url(name, sz, seed):
         return f"http://{host}:{port}/media/{name}?size={sz}&seed={seed}"
+    return worker, url
 
-    B = args.jobs_per_step
-    _, wres = await run_phase(worker, url, dist.rank, 0, args.warmup * B, size, mode)
+
+async def _warmup(args, worker, url, wid: int, mode: str) -> None:
+    _, wres = await run_phase(worker, url, wid, 0, args.warmup * args.jobs_per_step,
+                              int(args.size_mb * 1e6), mode)
     bad = [r for r in wres if r.outcome != "staged"]
     if bad:
         raise RuntimeError(f"warmup job failed: {bad[0]}")
-    dist.barrier()
-    cuda_sync()
+
+
+async def _timed(args, worker, url, wid: int, mode: str, count: int) -> dict:
+    """The timed jobs of one worker process; ``elapsed`` is this process' own view."""
+    B = args.jobs_per_step
     t0 = time.perf_counter()
     loop_cpu0 = time.thread_time()
-    dt, res = await run_phase(worker, url, dist.rank, args.warmup * B, args.steps * B, size, mode)
+    dt, res = await run_phase(worker, url, wid, args.warmup * B, count,
+                              int(args.size_mb * 1e6), mode)
     loop_cpu = time.thread_time() - loop_cpu0
-    cuda_sync()
     t1 = time.perf_counter()
     bad = [r for r in res if r.outcome != "staged"]
-    await worker.stop()
     # event-loop thread CPU / wall: ~1.0 means the Python side (one thread) is the limit
     return {"elapsed": t1 - t0, "latencies": [r.seconds for r in res],
             "bytes": sum(r.bytes for r in res), "failed": len(bad),
             "err": bad[0].error if bad else "", "loop_busy": loop_cpu / max(1e-9, t1 - t0)}
 
 
-def measure(args, dist: Dist, endpoint: str, mode: str, blob=None):
+async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str):
+    worker, url = await _start_worker(args, endpoint, mode, stage_root)
+    await _warmup(args, worker, url, dist.rank, mode)
+    dist.barrier()
+    cuda_sync()
+    t0 = time.perf_counter()
+    out = await _timed(args, worker, url, dist.rank, mode, args.steps * args.jobs_per_step)
+    cuda_sync()
+    out["elapsed"] = time.perf_counter() - t0
+    await worker.stop()
+    return out
+
+
+def _proc_main(conn, args, endpoint: str, mode: str, stage_root: str, wid: int, cpus: list,
+               count: int) -> None:
+    """One worker process of a rank (``--procs-per-rank``): warm up, report ready, wait for
+    the rank's go, run its share of the timed jobs, report."""
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    os.environ.setdefault("LOG_LEVEL", "error")
+
+    async def go():
+        worker, url = await _start_worker(args, endpoint, mode, stage_root)
+        await _warmup(args, worker, url, wid, mode)
+        conn.send(("ready", None))
+        if conn.recv() != "go":
+            await worker.stop()
+            return
+        out = await _timed(args, worker, url, wid, mode, count)
+        await worker.stop()
+        t = os.times()
+        out["worker_cpu_s"] = t.user + t.system
+        conn.send(("done", out))
+    try:
+        asyncio.run(go())
+    except BaseException as e:   # the rank turns this into a failed run
+        conn.send(("error", repr(e)))
+        raise
+
+
+def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, nproc: int,
+               cpus: list) -> dict:
+    """Run a rank as ``nproc`` worker processes (like ``downloader_amd supervisor -n`` does for
+    a GPU slot): one asyncio worker saturates its event loop + GIL long before the rank's CPU
+    share (two single-process ranks on one 16-CPU box: 82 GB/s vs 55 GB/s for one). Each
+    process gets a contiguous sub-slice of the rank's CPUs and an equal share of the jobs; the
+    rank's clock brackets "go" to the last "done"."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")            # fresh interpreters: no fork after gloo threads
+    total = args.steps * args.jobs_per_step
+    shares = [total // nproc + (1 if i < total % nproc else 0) for i in range(nproc)]
+    per = len(cpus) // nproc if cpus else 0
+    procs, conns = [], []
+    for i in range(nproc):
+        a, b = ctx.Pipe()
+        sub = cpus[i * per:(i + 1) * per] if per >= 1 else []
+        p = ctx.Process(target=_proc_main, args=(b, args, endpoint, mode, stage_root,
+                                                 dist.rank * 64 + i, sub, shares[i]),
+                        daemon=True)
+        p.start()
+        procs.append(p)
+        conns.append(a)
+
+    def recv(c):
+        kind, val = c.recv()
+        if kind == "error":
+            raise RuntimeError(f"bench worker process failed: {val}")
+        return val
+    try:
+        for c in conns:
+            recv(c)                           # all warmed up
+        dist.barrier()
+        cuda_sync()
+        t0 = time.perf_counter()
+        for c in conns:
+            c.send("go")
+        outs = [recv(c) for c in conns]
+        cuda_sync()
+        elapsed = time.perf_counter() - t0
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return {"elapsed": elapsed, "latencies": [x for o in outs for x in o["latencies"]],
+            "bytes": sum(o["bytes"] for o in outs), "failed": sum(o["failed"] for o in outs),
+            "err": next((o["err"] for o in outs if o["err"]), ""),
+            "loop_busy": max(o["loop_busy"] for o in outs),
+            "child_cpu_s": sum(o["worker_cpu_s"] for o in outs)}
+
+
+def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 1,
+            cpus: Optional[list] = None):
     stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
     rx0 = blob.stats()["bytes_received"] if blob is not None else 0
     peer_cpu0 = blob.cpu_seconds() if blob is not None else 0.0
     t = os.times()
     cpu0 = t.user + t.system
     try:
-        out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root))
+        if nproc > 1:
+            out = rank_procs(args, dist, endpoint, mode, stage_root, nproc, cpus or [])
+        else:
+            out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root))
     finally:
         if not args.stage_dir:
             shutil.rmtree(stage_root, ignore_errors=True)
     t = os.times()
-    out["worker_cpu_s"] = t.user + t.system - cpu0          # warmup + timed jobs
+    out["worker_cpu_s"] = t.user + t.system - cpu0 + out.pop("child_cpu_s", 0.0)
     out["peer_cpu_s"] = (blob.cpu_seconds() - peer_cpu0) if blob is not None else 0.0
     dist.barrier()
     # The S3 peer's own byte counter must cover every byte the workers claim to have staged.
@@ -281,8 +383,13 @@ def main() -> int:
         endpoint = blob.endpoint
     if args.peers == "shared":
         endpoint = dist.bcast(endpoint)
+    nproc = args.procs_per_rank
+    if nproc <= 0:   # auto: one worker process per 8 CPUs of the rank's slice, at most 8
+        nproc = max(1, min(8, len(pinned or os.sched_getaffinity(0)) // 8))
+    if args.mode == "reference":
+        nproc = 1    # the reference is one serial consumer per container
     try:
-        tuned = measure(args, dist, endpoint, args.mode, blob)
+        tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
         ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
     finally:
         if blob is not None:
@@ -313,12 +420,13 @@ def main() -> int:
             "mode": args.mode,
             "staging": args.staging if args.mode == "tuned" else "disk",
             "concurrency_per_worker": args.concurrency if args.mode == "tuned" else 1,
+            "procs_per_rank": nproc,
             "config": {
                 "model": "BASELINE.json config 2: HTTP media blob -> S3 multipart staging",
                 "global_batch": n * args.jobs_per_step,
                 "jobs_per_step_per_worker": args.jobs_per_step,
                 "seq_len": int(args.size_mb * 1e6),
-                "parallelism": f"workers{n}",
+                "parallelism": f"ranks{n}x{nproc}procs",
                 "object_bytes": int(args.size_mb * 1e6),
                 "jobs_timed": n * args.steps * args.jobs_per_step,
             },

@@ -100,3 +100,20 @@ def test_supervisor_auto_pinning_quota_share():
     assert auto_cpus_per_worker(1, list(range(8)), 16.0) == 0     # share = whole mask
     assert cpu_slices(2, 3, list(range(8))) == [[0, 1, 2], [3, 4, 5]]
     assert cpu_slices(2, -1, list(range(8))) == [[], []]
+
+
+@pytest.mark.slow
+def test_bench_rank_with_two_worker_processes(tmp_path):
+    """--procs-per-rank 2: the rank spawns two worker processes, splits the timed jobs, and
+    still prints exactly one JSON line whose byte count the S3 peer confirmed."""
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
+                        "--warmup", "1", "--jobs-per-step", "3", "--size-mb", "4",
+                        "--procs-per-rank", "2"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    j = json.loads(lines[0])
+    assert j["procs_per_rank"] == 2 and j["config"]["jobs_timed"] == 6
+    assert j["s3_peer_bytes_received"] >= 6 * 4_000_000 and j["value"] > 0
