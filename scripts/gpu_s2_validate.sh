@@ -1,0 +1,20 @@
+#!/bin/bash
+# Re-validate the tree after the multi-process-per-rank bench change: GPU tier, smoke, bench
+# with the new default (auto worker processes per rank) A/B against one process, and N=2.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+F=gpurun_out/s2
+mkdir -p $F
+export LOG_LEVEL=error
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $F/pytest_gpu.txt 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $F/smoke.txt 2>&1 && \
+timeout -k 10 300 python bench.py > $F/bench_default.json 2> $F/bench.err && \
+timeout -k 10 300 python bench.py --procs-per-rank 1 > $F/bench_p1.json 2>> $F/bench.err && \
+timeout -k 10 300 python bench.py --procs-per-rank 4 > $F/bench_p4.json 2>> $F/bench.err && \
+timeout -k 10 300 python bench.py > $F/bench_default2.json 2>> $F/bench.err && \
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 > $F/bench_n2.json 2>> $F/bench.err
+rc=$?
+tail -3 $F/pytest_gpu.txt
+cat $F/smoke.txt | tail -2
+cat $F/bench_*.json
+exit $rc
