@@ -5,7 +5,7 @@ BASELINE.json names the metric "MB/s staged end-to-end (download->S3) + p50 job 
 1/2/4/8 workers" and config 2 "100x100 MB HTTP URLs, N concurrent workers -> MinIO multipart".
 One rank = one worker process (the reference's scaling unit: one consumer per container,
 SURVEY §2.6). One "step" = every worker stages a batch of ``--jobs-per-step`` 100 MB
-random-byte media blobs (default 16; like a training batch, it keeps the timed region long
+random-byte media blobs (default 64; like a training batch, it keeps the timed region long
 enough to be stable), each job being the worker's full path: done-marker probe -> HTTP
 origin -> (default ``--staging stream``: each multipart part relayed origin->S3 by splice;
 ``--staging disk``: download to the job dir first) -> media selection -> S3 multipart upload
@@ -14,7 +14,8 @@ grows.
 
 Launch: ``python bench.py`` (N=1) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Each rank starts its own native ``blobd`` peer (origin + S3 sink;
-``--peers shared`` = one on rank 0) and, for N>1, pins itself to a disjoint CPU slice; ranks
+``--peers shared`` = one on rank 0) and pins itself to its GPU slot's CPU share (the same
+at every N, so the 1/2/4/8 curve is weak scaling of one slot's host resources); ranks
 synchronise over gloo (the workload is host-side: there is no tensor compute). The run fails
 if the S3 peer received fewer bytes than the workers claim to have staged.
 """
@@ -49,7 +50,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--concurrency", type=int, default=8,
                    help="jobs in flight per worker (8: best MB/s on the build box, p50 +4 ms vs 4: "
                         "profiles/bench_defaults_r1.jsonl)")
-    p.add_argument("--jobs-per-step", type=int, default=16, help="jobs per worker per step")
+    p.add_argument("--jobs-per-step", type=int, default=64,
+                   help="jobs per worker per step (64: ~1 s timed at N=1 for 10 steps; 16/32/64 "
+                        "give the same MB/s, profiles/s2_r1/jobs_ab.jsonl)")
     p.add_argument("--stage-dir", default="", help="download_path (default: a temp dir)")
     p.add_argument("--http-streams", type=int, default=0, help="override download.http_streams")
     p.add_argument("--part-mb", type=int, default=0, help="override s3.part_size (MiB)")
@@ -63,8 +66,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--sink", choices=["discard", "checksum"], default="discard",
                    help="blobd S3 sink: splice bodies to /dev/null, or checksum every byte")
     p.add_argument("--cpus-per-rank", type=int, default=0,
-                   help="pin each rank (worker + its peer) to this many CPUs; 0: allowed CPUs / "
-                        "ranks capped by the cgroup quota share, -1: no pinning")
+                   help="pin each rank (worker + its peer) to this many CPUs; 0: its GPU slot's "
+                        "share, min(mask, cgroup quota) / visible GPUs; -1: no pinning")
     p.add_argument("--procs-per-rank", type=int, default=0,
                    help="worker processes per rank; 0: one per 8 CPUs of the rank's slice")
     p.add_argument("--compare-reference", action="store_true",
@@ -349,23 +352,24 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
 
 
 def pin_rank(dist: Dist, per_rank: int = 0) -> list:
-    """Give each rank (worker threads + its blobd, which inherits the mask) a disjoint,
-    contiguous slice of the allowed CPUs: no cross-rank cache thrash, and sockets/threads stay
-    on a few CCDs of one NUMA node instead of migrating over the whole mask.
+    """Give each rank (worker threads + its blobd, which inherits the mask) a disjoint slice
+    of the allowed CPUs: no cross-rank cache thrash, and sockets/threads stay on a few CCDs
+    of one NUMA node instead of migrating over the whole mask (build box: 256 CPUs in the
+    mask, 16-CPU quota; 35.8 - 37.6 GB/s pinned vs 23.5 - 28.7 GB/s unpinned,
+    profiles/bench_pinning_r1.jsonl).
 
-    ``per_rank`` 0 = auto: allowed CPUs / local ranks, capped by the cgroup CPU quota share
-    (build box: 256 CPUs in the mask, 16-CPU quota -> 16 CPUs; measured 35.8 - 37.6 GB/s pinned
-    vs 23.5 - 28.7 GB/s unpinned, profiles/bench_pinning_r1.jsonl); -1 = off; K = exactly K.
-    Returns the slice ([] = unpinned)."""
+    ``per_rank`` 0 = auto: the rank's GPU slot share, min(mask, quota) / visible GPUs
+    (``utils.cpus.pin_slot``) - NOT divided by the number of ranks, so a rank owns the same
+    CPUs at N=1 as at N=8 and the driver's 1/2/4/8 curve is a weak-scaling curve (one GPU
+    slot's worth of host per worker) rather than "the whole node at N=1"; -1 = off; K = K
+    contiguous CPUs per local rank. Returns the slice ([] = unpinned)."""
     if per_rank < 0 or os.environ.get("STAGER_BENCH_NO_PIN") == "1":
         return []
     from downloader_amd.utils import cpus
     local = int(os.environ.get("LOCAL_RANK", dist.rank))
     nlocal = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", dist.world)))
-    if per_rank == 0 and cpus.cgroup_cpu_quota() == float("inf"):
-        if nlocal == 1:
-            return []
-        per_rank = len(os.sched_getaffinity(0)) // nlocal
+    if per_rank == 0:
+        return cpus.pin_slot(local, max(nlocal, cpus.gpu_slots()))
     return cpus.pin_share(local, nlocal, per_rank)
 
 

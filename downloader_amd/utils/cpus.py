@@ -47,6 +47,80 @@ def quota_share(available, n: int, quota: float) -> int:
     return per if per < len(available) else 0
 
 
+def gpu_slots() -> int:
+    """GPUs this process may use = worker slots of the node: ``STAGER_GPU_SLOTS``, else the
+    ``ROCR_VISIBLE_DEVICES`` / ``HIP_VISIBLE_DEVICES`` list, else the DRM render nodes the
+    container can open (the build pool's 1-GPU boxes show one of the host's eight). Never
+    initialises HIP."""
+    env = os.environ.get("STAGER_GPU_SLOTS", "")
+    if env.strip().isdigit() and int(env) > 0:
+        return int(env)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        ids = [x for x in os.environ.get(var, "").split(",") if x.strip()]
+        if ids:
+            return len(ids)
+    try:
+        n = sum(1 for d in os.listdir("/dev/dri") if d.startswith("renderD"))
+    except OSError:
+        n = 0
+    return max(1, n)
+
+
+def _core_of(cpu: int, root: str) -> tuple:
+    base = f"{root}/cpu{cpu}/topology"
+    try:
+        with open(f"{base}/physical_package_id", encoding="ascii") as f:
+            pkg = int(f.read())
+        with open(f"{base}/core_id", encoding="ascii") as f:
+            core = int(f.read())
+        return (pkg, core)
+    except (OSError, ValueError):
+        return (-1, cpu)          # unknown topology: every CPU is its own core
+
+
+def cores(cpus, root: str = "/sys/devices/system/cpu") -> list:
+    """CPUs grouped by physical core (SMT siblings together), cores ordered by (package,
+    core id), threads within a core ascending."""
+    by = {}
+    for c in sorted(cpus):
+        by.setdefault(_core_of(c, root), []).append(c)
+    return [by[k] for k in sorted(by)]
+
+
+def slot_cpus(index: int, slots: int, budget: int, cpus, root: str = "/sys/devices/system/cpu") -> list:
+    """CPUs of worker slot ``index`` of ``slots``: the slot owns a contiguous run of
+    ``len(cores) // slots`` physical cores (so no two slots share SMT siblings or, when the
+    run fits, a package) and uses ``budget // slots`` of their threads, first threads of each
+    core before second ones (under a quota a thread per core beats two threads on one)."""
+    groups = cores(cpus, root)
+    per_core = len(groups) // max(1, slots)
+    want = budget // max(1, slots)
+    if per_core < 1 or want < 1:
+        return []
+    mine = groups[index * per_core:(index + 1) * per_core]
+    depth = max(len(g) for g in mine)
+    order = [g[t] for t in range(depth) for g in mine if t < len(g)]
+    return sorted(order[:want])
+
+
+def pin_slot(index: int, slots: int) -> list:
+    """Pin this process to GPU slot ``index`` of ``slots``' share of the CPU budget
+    (min(mask, cgroup quota) / slots). The share does not depend on how many slots are busy,
+    so one worker sees the same CPUs whether it runs alone or next to seven others (weak
+    scaling). Returns the slice ([] = unpinned: no quota and one slot = the whole machine)."""
+    avail = sorted(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    if quota == math.inf and slots <= 1:
+        return []
+    budget = len(avail) if quota == math.inf else min(len(avail), max(1, math.ceil(quota)))
+    mine = slot_cpus(index, slots, budget, avail)
+    if not mine:
+        return []
+    os.sched_setaffinity(0, mine)
+    effective_cpus.cache_clear()
+    return mine
+
+
 def pin_share(index: int, n: int, per: int = 0) -> list:
     """Pin this process to slice ``index`` of ``n`` contiguous slices of its CPU mask
     (``per`` CPUs each; 0 = ``quota_share``). Children inherit the mask. Returns the slice

@@ -104,15 +104,37 @@ def test_bench_pin_rank_quota_share(monkeypatch):
     one = types.SimpleNamespace(world=1, rank=0)
     monkeypatch.delenv("LOCAL_RANK", raising=False)
     monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    # the build pool's EPYC 9575F: CPU c and c+128 are SMT siblings, cores 0-63 on package 0
+    monkeypatch.setattr(cpus, "_core_of", lambda c, root: (c % 128 // 64, c % 64))
+    monkeypatch.setenv("STAGER_GPU_SLOTS", "1")                  # 1-GPU box
     assert bench.pin_rank(one) == list(range(16))
     assert bench.pin_rank(one, -1) == []
+    # 8-GPU node, quota 128: 16 CPUs per GPU slot whatever the number of ranks
+    monkeypatch.setenv("STAGER_GPU_SLOTS", "8")
     monkeypatch.setattr(cpus, "cgroup_cpu_quota", lambda path="": 128.0)
+    assert bench.pin_rank(one) == list(range(16))               # N=1: slot 0, not the node
     monkeypatch.setenv("LOCAL_RANK", "3")
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     eight = types.SimpleNamespace(world=8, rank=3)
     assert bench.pin_rank(eight) == list(range(48, 64))
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert bench.pin_rank(eight) == list(range(80, 96))         # package 1
+    # no quota: 32 CPUs per slot = 16 cores with both SMT threads, never shared across slots
     monkeypatch.setattr(cpus, "cgroup_cpu_quota", lambda path="": float("inf"))
-    assert bench.pin_rank(eight) == list(range(96, 128))        # no quota: 256 / 8
+    assert bench.pin_rank(eight) == list(range(80, 96)) + list(range(208, 224))
     monkeypatch.setenv("LOCAL_RANK", "0")
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
-    assert bench.pin_rank(one) == []                            # no quota, N=1: leave it
+    monkeypatch.setenv("STAGER_GPU_SLOTS", "1")
+    assert bench.pin_rank(one) == []                            # no quota, one slot: leave it
+    assert bench.pin_rank(one, 4) == [0, 1, 2, 3]               # K > 0: K contiguous per rank
+
+
+def test_gpu_slots_from_env(monkeypatch):
+    from downloader_amd.utils import cpus
+    monkeypatch.delenv("STAGER_GPU_SLOTS", raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    assert cpus.gpu_slots() == 8
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3")
+    assert cpus.gpu_slots() == 1
+    monkeypatch.setenv("STAGER_GPU_SLOTS", "4")
+    assert cpus.gpu_slots() == 4
