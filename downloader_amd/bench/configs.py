@@ -148,7 +148,9 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             setup_s = time.perf_counter() - t0
             with open(os.path.join(src, "job.torrent"), "wb") as f:
                 f.write(raw)
-            dl = {"verify_backend": a.verify_backend}
+            dl = {"verify_backend": a.verify_backend, "torrent_stream": a.torrent_stream}
+            if a.stream_parallel:
+                dl["torrent_stream_parallel"] = a.stream_parallel
             if a.webseed_streams:
                 dl["webseed_streams"] = a.webseed_streams
             if a.webseed_chunk_mb:
@@ -321,6 +323,10 @@ def main(argv=None) -> int:
     ap.add_argument("--webseed-streams", type=int, default=0)
     ap.add_argument("--webseed-chunk-mb", type=int, default=0)
     ap.add_argument("--webseed-verify-depth", type=int, default=0)
+    ap.add_argument("--torrent-stream", choices=["auto", "always", "off"], default="auto",
+                    help="download.torrent_stream: webseed->S3 relay (auto) or disk staging (off)")
+    ap.add_argument("--stream-parallel", type=int, default=0,
+                    help="download.torrent_stream_parallel (parts in flight per job)")
     ap.add_argument("--no-gpu-prewarm", action="store_true",
                     help="do not init the GPU verifier at worker start (download.gpu_prewarm)")
     ap.add_argument("--workers", type=int, default=4, help="config 5 worker processes")

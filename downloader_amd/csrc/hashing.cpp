@@ -122,6 +122,13 @@ std::string Hasher::digest() const {
   EVP_MD_CTX_free(c);
   return std::string((const char*)out, len);
 }
+std::string Hasher::finish_and_reset() {
+  unsigned char out[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  if (EVP_DigestFinal_ex(ctx_, out, &len) != 1 || EVP_DigestInit_ex(ctx_, md_for(algo_), nullptr) != 1)
+    throw std::runtime_error("EVP_DigestFinal failed");
+  return std::string((const char*)out, len);
+}
 std::unique_ptr<Hasher> Hasher::copy() const {
   auto h = std::make_unique<Hasher>(algo_);
   EVP_MD_CTX_copy_ex(h->ctx_, ctx_);

@@ -53,6 +53,53 @@ ResponseHead dict_to_head(const py::dict& d) {
 
 }  // namespace
 
+struct PieceSplit {
+  int64_t skip, full_len, piece_len;
+};
+
+// GET on `src`, then (only on 200/206 with exactly `length` bytes) the PUT head on `dst`
+// followed by the body: spliced socket->pipe->socket, or - with `split` - through a hashed
+// user-space chunk (HttpConn::relay_body_hashed).
+py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
+               int64_t length, Progress* prog, int64_t max_body, const PieceSplit* split) {
+  std::string gh = get_head, ph = put_head;
+  ResponseHead g, p;
+  std::string gerr, pbody, digests, head, tail;
+  int64_t moved = 0;
+  {
+    py::gil_scoped_release rel;
+    src.send_request(gh, nullptr, 0);
+    g = src.read_head();
+    bool ok = (g.status == 200 || g.status == 206) && !g.chunked && g.content_length == length;
+    if (!ok) {
+      gerr = src.read_body(g, 1 << 20);
+    } else {
+      int cork = 1;
+      setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+      dst.send_raw(ph);
+      moved = split ? src.relay_body_hashed(dst, length, split->skip, split->full_len,
+                                            split->piece_len, prog, &digests, &head, &tail)
+                    : src.relay_body_to(dst, length, prog);
+      cork = 0;
+      setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+      p = dst.read_head();
+      pbody = dst.read_body(p, max_body);
+    }
+  }
+  py::dict d;
+  d["get"] = head_to_dict(g);
+  d["get_body"] = py::bytes(gerr);
+  d["put"] = p.status ? (py::object)head_to_dict(p) : py::none();
+  d["put_body"] = py::bytes(pbody);
+  d["moved"] = moved;
+  if (split) {
+    d["digests"] = py::bytes(digests);
+    d["head"] = py::bytes(head);
+    d["tail"] = py::bytes(tail);
+  }
+  return d;
+}
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "stager host-native byte paths: hashing (OpenSSL EVP, threaded) and zero-copy HTTP";
 
@@ -244,41 +291,27 @@ PYBIND11_MODULE(_native, m) {
           "relay_to",
           [](HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
              int64_t length, Progress* prog, int64_t max_body) {
-            std::string gh = get_head, ph = put_head;
-            ResponseHead g, p;
-            std::string gerr, pbody;
-            int64_t moved = 0;
-            {
-              py::gil_scoped_release rel;
-              src.send_request(gh, nullptr, 0);
-              g = src.read_head();
-              bool ok = (g.status == 200 || g.status == 206) && !g.chunked && g.content_length == length;
-              if (!ok) {
-                gerr = src.read_body(g, 1 << 20);
-              } else {
-                int cork = 1;
-                setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
-                dst.send_raw(ph);
-                moved = src.relay_body_to(dst, length, prog);
-                cork = 0;
-                setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
-                p = dst.read_head();
-                pbody = dst.read_body(p, max_body);
-              }
-            }
-            py::dict d;
-            d["get"] = head_to_dict(g);
-            d["get_body"] = py::bytes(gerr);
-            d["put"] = p.status ? (py::object)head_to_dict(p) : py::none();
-            d["put_body"] = py::bytes(pbody);
-            d["moved"] = moved;
-            return d;
+            return relay(src, get_head, dst, put_head, length, prog, max_body, nullptr);
           },
           py::arg("get_head"), py::arg("dst"), py::arg("put_head"), py::arg("length"),
           py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)1 << 20,
           "GET on this connection and stream exactly `length` body bytes as the body of the "
           "PUT sent on `dst` (socket->pipe->socket splice). The GET must answer 200/206 with "
           "that Content-Length, otherwise nothing is sent on `dst`.")
+      .def(
+          "relay_hashed_to",
+          [](HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
+             int64_t length, int64_t skip, int64_t full_len, int64_t piece_len, Progress* prog,
+             int64_t max_body) {
+            PieceSplit ps{skip, full_len, piece_len};
+            return relay(src, get_head, dst, put_head, length, prog, max_body, &ps);
+          },
+          py::arg("get_head"), py::arg("dst"), py::arg("put_head"), py::arg("length"),
+          py::arg("skip"), py::arg("full_len"), py::arg("piece_len"),
+          py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)1 << 20,
+          "relay_to through a user-space chunk that is SHA-1'd on the way: body bytes "
+          "[skip, skip+full_len) as consecutive `piece_len` pieces (last may be short). Adds "
+          "`digests` (20 B per piece), `head` (bytes before skip) and `tail` (bytes after).")
       .def("close", &HttpConn::close)
       .def("abort", &HttpConn::abort)
       .def_property_readonly("is_open", &HttpConn::is_open)

@@ -28,6 +28,8 @@ class Hasher {
   void update(const uint8_t* p, size_t n);
   void update_fd(int fd, int64_t offset, int64_t length);
   std::string digest() const;
+  // Digest of everything fed so far, then start over (one EVP final, no context copy).
+  std::string finish_and_reset();
   std::unique_ptr<Hasher> copy() const;
   const std::string& algo() const { return algo_; }
 
@@ -105,6 +107,13 @@ class HttpConn {
   // Move exactly `n` body bytes of the response being read on *this to `dst`'s socket
   // (bytes already buffered first, then socket -> pipe -> socket with splice).
   int64_t relay_body_to(HttpConn& dst, int64_t n, Progress* prog);
+  // Same relay, but through a user-space chunk that is also hashed: body bytes [skip,
+  // skip + full_len) are SHA-1'd as consecutive pieces of `piece_len` (the last may be
+  // short) into `digests`; bytes before `skip` go to `head`, bytes after to `tail` (the
+  // fragments of pieces that straddle the body's ends). One pass, L2-resident chunks.
+  int64_t relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
+                            int64_t piece_len, Progress* prog, std::string* digests,
+                            std::string* head, std::string* tail);
   void send_raw(const std::string& s) { send_all((const uint8_t*)s.data(), s.size()); }
   int fd() const { return fd_; }
   void mark_unusable() { reusable_ = false; }

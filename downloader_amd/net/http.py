@@ -248,7 +248,8 @@ class NativeTransport(Transport):
             self._slots.pop(slot, None)
 
     def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
-               length: int, nprog, slot: int = 0) -> Tuple[Response, Optional[Response], int]:
+               length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None
+               ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         _, sh, sp, spath = split_host(src_url)
         _, dh, dp, dpath = split_host(dst_url)
         get_head = _build_head("GET", sh if sp == 80 else f"{sh}:{sp}", spath, src_headers, None)
@@ -263,7 +264,10 @@ class NativeTransport(Transport):
             raise
         self._track(slot, dst)
         try:
-            d = src.relay_to(get_head, dst, put_head, length, nprog)
+            if split is None:
+                d = src.relay_to(get_head, dst, put_head, length, nprog)
+            else:
+                d = src.relay_hashed_to(get_head, dst, put_head, length, *split, nprog)
         except RuntimeError as e:
             self._untrack(slot, src)
             self._untrack(slot, dst)
@@ -280,14 +284,20 @@ class NativeTransport(Transport):
         if d["put"] is not None:
             p = d["put"]
             put = Response(p["status"], list(p["headers"]), d["put_body"], 0, p.get("reason", ""))
-        return get, put, d["moved"]
+        hashed = {k: d[k] for k in ("digests", "head", "tail")} if split is not None else None
+        return get, put, d["moved"], hashed
 
     async def relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
-                    length: int, progress: Optional[Progress] = None
-                    ) -> Tuple[Response, Optional[Response], int]:
+                    length: int, progress: Optional[Progress] = None,
+                    split: Optional[Tuple[int, int, int]] = None
+                    ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         """GET ``src_url`` and stream exactly ``length`` body bytes as the body of a PUT to
         ``dst_url`` without touching user space (socket -> pipe -> socket splice). The PUT is
-        only sent when the GET answers 2xx with exactly that Content-Length."""
+        only sent when the GET answers 2xx with exactly that Content-Length.
+
+        ``split=(skip, full_len, piece_len)``: relay through L2-sized user-space chunks and
+        SHA-1 body bytes [skip, skip+full_len) as consecutive pieces on the way; the 4th
+        result is then ``{"digests", "head", "tail"}`` (``HttpConn.relay_hashed_to``)."""
         nprog = None
         if progress is not None:
             if progress.native is None:
@@ -296,7 +306,7 @@ class NativeTransport(Transport):
         loop = asyncio.get_running_loop()
         slot = self._new_slot()
         fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
-                                   dst_headers, length, nprog, slot)
+                                   dst_headers, length, nprog, slot, split)
         try:
             return await asyncio.shield(fut)
         except asyncio.CancelledError:

@@ -313,14 +313,16 @@ class S3Client:
 
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                          src_url: str, offset: int, length: int, whole: bool,
-                         progress: Optional[Progress]) -> str:
+                         progress: Optional[Progress], split=None):
+        """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
+        (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``."""
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
         attempt = 0
         while True:
             url, hdrs = self._signed("PUT", bucket, key, query)
             try:
-                get, put, _ = await self.t.native.relay(src_url, src_hdrs, url, hdrs, length,
-                                                        progress)
+                get, put, _, hashed = await self.t.native.relay(src_url, src_hdrs, url, hdrs,
+                                                                length, progress, split)
             except TransportError as e:
                 err: Exception = e
                 retry = True
@@ -330,7 +332,8 @@ class S3Client:
                                          f"(Content-Length {get.header('content-length')}) "
                                          f"for {length} bytes at {offset}", get.status)
                 if put.ok:
-                    return (put.header("etag") or "").strip('"')
+                    etag = (put.header("etag") or "").strip('"')
+                    return etag if split is None else (etag, hashed)
                 err = parse_error(put, bucket, key)
                 retry = err.retryable
             if not retry or attempt >= self.retries:
@@ -365,6 +368,17 @@ class S3Client:
             except Exception:
                 pass
             raise
+
+    async def relay_hashed(self, bucket: str, key: str, src_url: str, offset: int, length: int,
+                           whole: bool, split: Tuple[int, int, int],
+                           part: Optional[Tuple[int, str]] = None,
+                           progress: Optional[Progress] = None):
+        """Relay ``length`` bytes of ``src_url`` at ``offset`` into the object ``key`` (or its
+        multipart ``part=(number, upload_id)``) while SHA-1-ing the torrent pieces inside it
+        (``split``); returns ``(etag, {"digests", "head", "tail"})``."""
+        query = [] if part is None else [("partNumber", str(part[0])), ("uploadId", part[1])]
+        return await self._relay_put(bucket, key, query, src_url, offset, length, whole,
+                                     progress, split)
 
     async def create_multipart_upload(self, bucket: str, key: str) -> str:
         r = await self._request("POST", bucket, key, query=[("uploads", "")])

@@ -11,6 +11,10 @@
 
 ``uri`` may be a magnet link, an http(s) URL of a ``.torrent`` (the reference's
 ``.torrent``-over-HTTP chain, lib/download.js:143-155) or a local ``.torrent`` path.
+
+A ``.torrent`` whose only source is webseeds is staged by ``torrent/stream.py`` (webseed ->
+S3 relay with in-flight piece verification, no disk) under the same watchdogs; everything
+else runs a ``TorrentSession`` into the job directory, with eager staging of selected files.
 """
 from __future__ import annotations
 
@@ -18,13 +22,13 @@ import asyncio
 import math
 import os
 import time
-from typing import Optional
+from typing import Awaitable, Callable, List, Optional
 
 from ..fetch.http import fetch_bytes
 from ..stages.base import DOWNLOADING, DownloadStalled, Job, Services
 from .client import TorrentClient
 from .magnet import parse_magnet
-from .metainfo import parse_torrent
+from .metainfo import Metainfo, parse_torrent
 from .session import TorrentSession
 
 
@@ -47,9 +51,10 @@ async def get_client(cfg, sv: Services) -> TorrentClient:
     return c
 
 
-async def open_session(client: TorrentClient, uri: str, path: str, sv: Services) -> TorrentSession:
+async def load_metainfo(uri: str, sv: Services) -> Optional[Metainfo]:
+    """The metainfo of a ``.torrent`` source (URL or path); None for a magnet link."""
     if uri.startswith("magnet:"):
-        return await client.add_magnet(parse_magnet(uri), path)
+        return None
     if uri.startswith(("http://", "https://")):
         data = await fetch_bytes(sv.transports, uri)
     elif os.path.isfile(uri):
@@ -57,22 +62,47 @@ async def open_session(client: TorrentClient, uri: str, path: str, sv: Services)
             data = f.read()
     else:
         raise ValueError(f"unsupported torrent source {uri[:40]!r}")
-    return await client.add_torrent(parse_torrent(data), path)
+    return parse_torrent(data)
 
 
-async def _start_eager(session: TorrentSession, job: Job, path: str, cfg, sv: Services):
-    """Start staging selected files while downloading (torrent.eager) when the job directory
-    holds nothing but this torrent's files, so the virtual walk equals the later disk walk."""
-    from ..stages.base import ensure_staging_bucket
+async def open_session(client: TorrentClient, uri: str, path: str, sv: Services,
+                       meta: Optional[Metainfo] = None) -> TorrentSession:
+    if uri.startswith("magnet:"):
+        return await client.add_magnet(parse_magnet(uri), path)
+    return await client.add_torrent(meta or await load_metainfo(uri, sv), path)
+
+
+def virtual_selection(meta: Metainfo, job: Job, path: str, cfg) -> Optional[List[str]]:
+    """The process stage's answer from the metainfo alone (``find_virtual``), when the job
+    directory holds nothing but this torrent's files - so it equals the later disk walk."""
     from ..stages.select import select_from_config
-    from .eager import EagerUploader
-    mine = {os.path.abspath(p) for p, _ in session.meta.local_files(path)}
+    mine = {os.path.abspath(p) for p, _ in meta.local_files(path)}
     for dp, _, fns in os.walk(path):
         for fn in fns:
             if os.path.abspath(os.path.join(dp, fn)) not in mine:
                 return None
-    rels = [os.path.relpath(p, path) for p, _ in session.meta.local_files(path)]
-    selected = select_from_config(cfg).find_virtual(path, rels, job.media.type)
+    rels = [os.path.relpath(p, path) for p, _ in meta.local_files(path)]
+    return select_from_config(cfg).find_virtual(path, rels, job.media.type) or None
+
+
+def stream_webseeds(meta: Metainfo, job: Job, cfg, sv: Services) -> List[str]:
+    """Webseeds to stage from with ``torrent/stream.py``; [] = use a session."""
+    d = cfg.download
+    if cfg.mode != "tuned" or d.torrent_stream == "off" or not d.eager_upload \
+            or not d.torrent_enable_webseeds:
+        return []
+    if d.torrent_stream == "auto" and ((d.torrent_enable_trackers and meta.trackers())
+                                       or job.attempt > 0):
+        return []
+    seeds = [u for u in meta.url_list if sv.s3.can_relay(u)]
+    return seeds if seeds and len(seeds) == len(meta.url_list) else []
+
+
+async def _start_eager(session: TorrentSession, job: Job, path: str, cfg, sv: Services):
+    """Start staging selected files while downloading (torrent.eager)."""
+    from ..stages.base import ensure_staging_bucket
+    from .eager import EagerUploader
+    selected = virtual_selection(session.meta, job, path, cfg)
     if not selected:
         return None
     await ensure_staging_bucket(sv)
@@ -82,12 +112,81 @@ async def _start_eager(session: TorrentSession, job: Job, path: str, cfg, sv: Se
     return eager
 
 
+async def _watched(job: Job, sv: Services, d, progress: Callable[[], float],
+                   work: Awaitable) -> None:
+    """Run ``work`` under the reference's progress ticker (30 s, floor(pct/2) when changed,
+    lib/download.js:78-88) and stall watchdog (240 s without progress -> ERRDLSTALL,
+    lib/download.js:90-101)."""
+    state = {"last_int": None, "last_progress": None}
+
+    async def ticker() -> None:
+        while True:
+            await asyncio.sleep(d.progress_interval_s)
+            pct = progress() * 100
+            job.logger.info("download progress", pct)
+            pint = math.floor(pct / 2)
+            if pint != state["last_int"]:
+                await sv.telemetry.emit_progress(job.id, DOWNLOADING, pint)
+            state["last_int"] = pint
+
+    async def watchdog() -> None:
+        while True:
+            await asyncio.sleep(d.torrent_stall_timeout_s)
+            pct = progress() * 100
+            job.logger.info("stall check", pct, state["last_progress"])
+            if pct == state["last_progress"]:
+                raise DownloadStalled()
+            state["last_progress"] = pct
+
+    tasks = [asyncio.ensure_future(work), asyncio.ensure_future(ticker()),
+             asyncio.ensure_future(watchdog())]
+    try:
+        done, _ = await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
+        for t in done:
+            t.result()  # propagate DownloadStalled / session errors
+    finally:
+        for t in tasks:
+            t.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
+
+
+async def _stream_torrent(meta: Metainfo, seeds: List[str], selected: List[str], job: Job,
+                          path: str, cfg, sv: Services, t0: float) -> int:
+    from ..stages.base import ensure_staging_bucket
+    from .stream import StreamStager
+    d = cfg.download
+    await ensure_staging_bucket(sv)
+    st = StreamStager(meta, job, cfg, sv, selected, path, seeds, d.torrent_stream_parallel)
+    job.logger.info("streaming webseed torrent straight to staging", files=len(st.targets),
+                    skipped_bytes=st.skipped_bytes())
+    out: dict = {}
+
+    async def work() -> None:
+        out["streamed"] = await st.run()
+    await _watched(job, sv, d, lambda: st.progress, work())
+    job.stats.setdefault("streamed", []).extend(out["streamed"])
+    job.stats["eager_uploaded_bytes"] = st.total
+    job.stats["torrent"] = {"staging": "stream", "webseed_bytes": st.fetched_bytes,
+                            "peers": 0, "hash_fails": st.hash_fails,
+                            "webseed_fetch_s": round(st.stats["relay_s"], 4),
+                            "webseed_verify_s": 0.0, "gap_bytes": st.stats["gap_bytes"],
+                            "skipped_bytes": st.skipped_bytes(),
+                            "timeline_s": {"complete": round(time.perf_counter() - t0, 4)}}
+    return st.fetched_bytes
+
+
 async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
                            client: Optional[TorrentClient] = None) -> int:
     d = cfg.download
     t0 = time.perf_counter()
+    meta = await load_metainfo(uri, sv)
+    if meta is not None and client is None:
+        seeds = stream_webseeds(meta, job, cfg, sv)
+        selected = virtual_selection(meta, job, path, cfg) if seeds else None
+        if selected:
+            return await _stream_torrent(meta, seeds, selected, job, path, cfg, sv, t0)
     client = client or await get_client(cfg, sv)
-    session = await open_session(client, uri, path, sv)
+    session = await open_session(client, uri, path, sv, meta)
     # Seconds since the backend was entered: open (metainfo fetched, storage ready), metadata,
     # payload complete and verified, eager staging drained.
     tl = {"open": time.perf_counter() - t0}
@@ -113,33 +212,8 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
         eager = await _start_eager(session, job, path, cfg, sv) if d.eager_upload else None
 
         # 2) progress ticker + stall watchdog around the transfer
-        state = {"last_int": None, "last_progress": None}
-
-        async def ticker() -> None:
-            while True:
-                await asyncio.sleep(d.progress_interval_s)
-                progress = session.progress * 100
-                job.logger.info("download progress", progress)
-                pint = math.floor(progress / 2)
-                if pint != state["last_int"]:
-                    await sv.telemetry.emit_progress(job.id, DOWNLOADING, pint)
-                state["last_int"] = pint
-
-        async def watchdog() -> None:
-            while True:
-                await asyncio.sleep(d.torrent_stall_timeout_s)
-                progress = session.progress * 100
-                job.logger.info("stall check", progress, state["last_progress"])
-                if progress == state["last_progress"]:
-                    raise DownloadStalled()
-                state["last_progress"] = progress
-
-        tasks = [asyncio.ensure_future(session.wait()), asyncio.ensure_future(ticker()),
-                 asyncio.ensure_future(watchdog())]
         try:
-            done, _ = await asyncio.wait(tasks, return_when=asyncio.FIRST_COMPLETED)
-            for t in done:
-                t.result()  # propagate DownloadStalled / session errors
+            await _watched(job, sv, d, lambda: session.progress, session.wait())
             tl["complete"] = time.perf_counter() - t0
             if eager is not None:
                 job.stats.setdefault("streamed", []).extend(await eager.finish())
@@ -150,12 +224,8 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
             if eager is not None:
                 await eager.abort()
             raise
-        finally:
-            for t in tasks:
-                t.cancel()
-            await asyncio.gather(*tasks, return_exceptions=True)
         job.logger.debug("finished, clearing watchers")
-        job.stats["torrent"] = {"webseed_bytes": session.webseed_bytes,
+        job.stats["torrent"] = {"staging": "disk", "webseed_bytes": session.webseed_bytes,
                                 "peers": session.stats["peers_connected"],
                                 "hash_fails": session.stats["hash_fails"],
                                 "webseed_fetch_s": round(session.stats["webseed_fetch_s"], 4),

@@ -642,12 +642,8 @@ class TorrentSession:
 
     # ---------------------------------------------------------------- webseeds (BEP-19)
     def _webseed_url(self, base: str, file_idx: int) -> str:
-        m = self.meta
-        assert m is not None
-        if not m.multi_file:
-            return base + quote(m.name) if base.endswith("/") else base
-        f = m.files[file_idx]
-        return base.rstrip("/") + "/" + "/".join(quote(x) for x in [m.name] + f.path)
+        assert self.meta is not None
+        return webseed_url(self.meta, base, file_idx)
 
     async def _webseed_worker(self, base: str) -> None:
         """One BEP-19 stream: claim a run of whole pieces (``webseed_chunk`` bytes), GET it
@@ -814,6 +810,16 @@ class TorrentSession:
 
     def total_bytes(self) -> int:
         return self.meta.total_length if self.meta else 0
+
+
+def webseed_url(m: Metainfo, base: str, file_idx: int) -> str:
+    """BEP-19 URL of file ``file_idx``: a single-file torrent's url-list entry is the file
+    itself (or a directory, when it ends in ``/``); multi-file entries are the parent of
+    ``<name>/<path...>``."""
+    if not m.multi_file:
+        return base + quote(m.name) if base.endswith("/") else base
+    f = m.files[file_idx]
+    return base.rstrip("/") + "/" + "/".join(quote(x) for x in [m.name] + f.path)
 
 
 def webseed_file_size(path: str) -> int:

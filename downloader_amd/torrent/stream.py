@@ -1,0 +1,355 @@
+"""Streamed staging of webseed-only torrents: webseed -> S3, pieces verified on the way, no disk.
+
+The reference downloads the whole torrent into ``<download_path>/<id>`` with webtorrent
+(lib/download.js:43-123), walks it (lib/process.js) and uploads the media files
+(lib/upload.js:34-52). When the torrent's only source is BEP-19 webseeds and the process
+stage's answer is already known from the metainfo (``MediaSelector.find_virtual``), the
+bytes need not land on disk at all:
+
+* every multipart part of every selected file is ONE Range GET on the file's webseed URL,
+  relayed into its UploadPart through L2-sized user-space chunks that are SHA-1'd in flight
+  (``HttpConn::relay_body_hashed``): whole pieces inside the part are verified by the relay
+  itself;
+* a piece that straddles a part's end (or a file boundary) is assembled from the neighbouring
+  parts' edge fragments plus - where it reaches into a file the selector drops - "gap" bytes
+  fetched into memory, and verified once complete;
+* a part whose pieces fail is fetched and uploaded again (S3 replaces a part number); a file
+  becomes visible only at ``CompleteMultipartUpload``, issued after every piece covering it
+  verified - and the job's commit point stays the done marker written by the upload stage.
+
+Files the selector drops are never fetched (apart from gap bytes). Measured on the build box:
+page-cache writes of ONE file top out at ~8 GB/s (inode lock, page allocation; tmpfs is
+slower still, ``profiles/s2_r1/stage_fs.jsonl``), which capped the 4 GB single-file config.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Set, Tuple
+
+from ..models import keys
+from ..net.http import TransportError
+from .metainfo import Metainfo
+from .session import TorrentError, webseed_url
+
+
+@dataclass(eq=False)
+class _Target:
+    """One selected file and its staging object."""
+    path: str
+    key: str
+    index: int                  # file index in the metainfo
+    offset: int                 # torrent offset of the file's first byte
+    size: int
+    single: bool                # one PUT (<= multipart threshold) instead of multipart
+    upload_id: str = ""
+    etags: Dict[int, str] = field(default_factory=dict)
+
+
+@dataclass(eq=False)
+class _Unit:
+    """A contiguous torrent byte range fetched in one go: an S3 part of a target (relayed
+    and hashed) or a gap (bytes of unselected files, fetched into memory for a boundary
+    piece)."""
+    uid: int
+    start: int
+    length: int
+    target: Optional[_Target] = None
+    num: int = 0                # part number (multipart targets)
+    file_off: int = 0           # offset of the part inside its file
+    skip: int = 0               # bytes before the first whole piece
+    full: int = 0               # bytes of whole pieces
+    attempts: int = 0
+    done: bool = False
+
+    @property
+    def end(self) -> int:
+        return self.start + self.length
+
+    def fragments(self) -> List[Tuple[int, int]]:
+        """Torrent ranges of this unit that belong to boundary pieces (head, tail; a gap is
+        one fragment)."""
+        if self.target is None:
+            return [(self.start, self.end)]
+        out = []
+        if self.skip:
+            out.append((self.start, self.start + self.skip))
+        t0 = self.start + self.skip + self.full
+        if t0 < self.end:
+            out.append((t0, self.end))
+        return out
+
+
+def piece_split(meta: Metainfo, start: int, length: int) -> Tuple[int, int]:
+    """(skip, full) of the torrent range [start, start+length): ``skip`` bytes before the
+    first whole piece, then ``full`` bytes of whole pieces (the torrent's short last piece
+    counts as whole when the range reaches the end)."""
+    plen, end = meta.piece_length, start + length
+    ps = -(-start // plen) * plen
+    pe = end if end == meta.total_length else (end // plen) * plen
+    if pe <= ps:
+        return min(ps - start, length), 0
+    return ps - start, pe - ps
+
+
+class StreamStager:
+    def __init__(self, meta: Metainfo, job, cfg, sv, selected: List[str], root: str,
+                 webseeds: List[str], parallel: int = 16, max_failures: int = 5):
+        self.meta = meta
+        self.job = job
+        self.sv = sv
+        self.s3 = sv.s3
+        self.bucket = cfg.s3.bucket
+        self.webseeds = list(webseeds)
+        self.plen = meta.piece_length
+        self.parallel = max(1, parallel)
+        self.max_failures = max(1, max_failures)
+        index = {os.path.abspath(p): i for i, (p, _) in enumerate(meta.local_files(root))}
+        self.selected = [os.path.abspath(f) for f in selected]
+        self.sizes = {f: meta.files[index[f]].length for f in self.selected}
+        owner: Dict[str, str] = {}
+        for f in self.selected:
+            owner[keys.object_key(job.id, f)] = f       # the later file wins the key (App. A #10)
+        self.targets: List[_Target] = []
+        self.units: List[_Unit] = []
+        for key, f in owner.items():
+            fe = meta.files[index[f]]
+            t = _Target(f, key, index[f], fe.offset, fe.length,
+                        fe.length <= self.s3.multipart_threshold)
+            self.targets.append(t)
+            if t.size == 0:
+                continue
+            parts = [(0, 0, t.size)] if t.single else self.s3.plan_parts(t.size)
+            for num, off, ln in parts:
+                skip, full = piece_split(meta, t.offset + off, ln)
+                self.units.append(_Unit(len(self.units), t.offset + off, ln, t, num, off,
+                                        skip, full))
+        # boundary pieces: piece -> {torrent offset: fragment}, and the units supplying them
+        self.frags: Dict[int, Dict[int, bytes]] = {}
+        self.suppliers: Dict[int, Set[int]] = {}
+        self._plan_gaps()
+        self.verified: Set[int] = set()
+        self.piece_fails: Dict[int, int] = {}
+        self.total = sum(t.size for t in self.targets)
+        self.fetched_bytes = 0
+        self.done_bytes = 0
+        self.hash_fails = 0
+        self.error: Optional[BaseException] = None
+        self._outstanding = 0
+        self._finished = asyncio.Event()
+        self.stats = {"relay_s": 0.0, "gap_bytes": 0, "units": 0}
+
+    # ---------------------------------------------------------------- planning
+    def _piece_range(self, p: int) -> Tuple[int, int]:
+        return p * self.plen, p * self.plen + self.meta.piece_size(p)
+
+    def _plan_gaps(self) -> None:
+        covered: Dict[int, List[Tuple[int, int]]] = {}
+        for u in self.units:
+            for a, b in u.fragments():
+                p = a // self.plen
+                covered.setdefault(p, []).append((a, b))
+                self.suppliers.setdefault(p, set()).add(u.uid)
+        for p in sorted(covered):
+            lo, hi = self._piece_range(p)
+            pos = lo
+            for a, b in sorted(covered[p]) + [(hi, hi)]:
+                if a > pos:
+                    g = _Unit(len(self.units), pos, a - pos)
+                    self.units.append(g)
+                    self.suppliers[p].add(g.uid)
+                pos = max(pos, b)
+            self.frags[p] = {}
+
+    @property
+    def progress(self) -> float:
+        """Fraction of the selected bytes relayed and verified (the ticker / stall watchdog
+        of lib/download.js:78-101 sample it like webtorrent's ``torrent.progress``)."""
+        return 1.0 if self.total == 0 else min(1.0, self.done_bytes / self.total)
+
+    def skipped_bytes(self) -> int:
+        """Torrent bytes never fetched (files the selector drops)."""
+        return self.meta.total_length - sum(u.length for u in self.units)
+
+    # ---------------------------------------------------------------- execution
+    async def run(self) -> List[dict]:
+        """Stage every selected file; return the ``streamed`` entries (walk order, every
+        selected file - the upload stage resolves key ownership) for the later stages."""
+        multi = [t for t in self.targets if not t.single and t.size]
+        try:
+            for t in self.targets:
+                if t.size == 0:
+                    await self.s3.put_object(self.bucket, t.key, b"")
+            ids = await asyncio.gather(*(self.s3.create_multipart_upload(self.bucket, t.key)
+                                         for t in multi))
+            for t, uid in zip(multi, ids):
+                t.upload_id = uid
+            queue: "asyncio.Queue[_Unit]" = asyncio.Queue()
+            for u in self.units:
+                queue.put_nowait(u)
+            self._outstanding = len(self.units)
+            if not self.units:
+                self._finished.set()
+            workers = [asyncio.ensure_future(self._worker(queue)) for _ in range(self.parallel)]
+            try:
+                await self._finished.wait()
+            finally:
+                for w in workers:
+                    w.cancel()
+                await asyncio.gather(*workers, return_exceptions=True)
+            if self.error is not None:
+                raise self.error
+            unverified = [p for p in self.frags if p not in self.verified]
+            if unverified:
+                raise TorrentError(f"pieces {unverified[:5]} never verified")
+            await asyncio.gather(*(self.s3.complete_multipart_upload(
+                self.bucket, t.key, t.upload_id, sorted(t.etags.items())) for t in multi))
+        except BaseException:
+            await asyncio.shield(self.abort())
+            raise
+        return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
+                 "virtual": True} for f in self.selected]
+
+    async def _worker(self, queue: "asyncio.Queue[_Unit]") -> None:
+        while True:
+            u = await queue.get()
+            try:
+                requeue = await self._process(u)
+            except (TransportError, OSError) as e:
+                u.attempts += 1
+                if u.attempts >= self.max_failures:
+                    self._fail(TorrentError(f"webseed failed: {e}"))
+                    return
+                await asyncio.sleep(min(5.0, 0.1 * (2 ** u.attempts)))
+                requeue = [u]
+            except BaseException as e:
+                self._fail(e)
+                return
+            if self.error is not None:
+                return
+            self._settle(u, requeue, queue)
+
+    def _settle(self, u: _Unit, requeue: List[_Unit], queue: "asyncio.Queue[_Unit]") -> None:
+        if u not in requeue:
+            u.done = True
+            self._outstanding -= 1
+        for r in requeue:
+            if r.done:
+                r.done = False
+                self._outstanding += 1
+                if r.target is not None:
+                    self.done_bytes -= r.length
+            for a, _ in r.fragments():               # its fragments are fetched again
+                p = a // self.plen
+                self.frags[p].pop(a, None)
+                self.verified.discard(p)
+            queue.put_nowait(r)
+        if self._outstanding == 0:
+            self._finished.set()
+
+    def _fail(self, e: BaseException) -> None:
+        if self.error is None:
+            self.error = e
+        self._finished.set()
+
+    def _base(self, u: _Unit) -> str:
+        return self.webseeds[(u.uid + u.attempts) % len(self.webseeds)]
+
+    async def _process(self, u: _Unit) -> List[_Unit]:
+        """Fetch one unit; return the units that must be fetched again (bad pieces)."""
+        if u.target is None:
+            pieces = [(u.start, await self._fetch_gap(u))]
+        else:
+            got = await self._relay(u)
+            if got is None:                          # a whole piece inside failed its hash
+                u.attempts += 1
+                if u.attempts >= self.max_failures:
+                    raise TorrentError("webseed served corrupt pieces")
+                return [u]
+            pieces = got
+        self.stats["units"] += 1
+        requeue: List[_Unit] = []
+        for a, data in pieces:
+            p = a // self.plen
+            self.frags[p][a] = data
+            if await self._check_piece(p):
+                requeue += [self.units[i] for i in sorted(self.suppliers[p])]
+        return requeue
+
+    async def _relay(self, u: _Unit) -> Optional[List[Tuple[int, bytes]]]:
+        t = u.target
+        url = webseed_url(self.meta, self._base(u), t.index)
+        whole = u.file_off == 0 and u.length == t.size
+        t0 = time.perf_counter()
+        etag, h = await self.s3.relay_hashed(
+            self.bucket, t.key, url, u.file_off, u.length, whole, (u.skip, u.full, self.plen),
+            part=None if t.single else (u.num, t.upload_id))
+        self.stats["relay_s"] += time.perf_counter() - t0
+        self.fetched_bytes += u.length
+        digests = h["digests"]
+        first = (u.start + u.skip) // self.plen
+        for k in range(len(digests) // 20):
+            if digests[20 * k:20 * k + 20] != self.meta.piece_hash(first + k):
+                self.hash_fails += 1
+                return None
+        if not t.single:
+            t.etags[u.num] = etag
+        self.done_bytes += u.length
+        out = []
+        if u.skip:
+            out.append((u.start, h["head"]))
+        if h["tail"]:
+            out.append((u.start + u.skip + u.full, h["tail"]))
+        return out
+
+    async def _fetch_gap(self, u: _Unit) -> bytes:
+        buf = bytearray()
+        for fi, foff, ln in self.meta.file_spans(u.start, u.length):
+            url = webseed_url(self.meta, self._base(u), fi)
+            r = await self.sv.transports.request(
+                "GET", url, headers=[("Range", f"bytes={foff}-{foff + ln - 1}")])
+            if r.status != 206 or len(r.body) != ln:
+                raise TransportError(f"webseed {url}: HTTP {r.status}, {len(r.body)}/{ln} B",
+                                     r.status)
+            buf += r.body
+        self.fetched_bytes += u.length
+        self.stats["gap_bytes"] += u.length
+        return bytes(buf)
+
+    async def _check_piece(self, p: int) -> bool:
+        """Verify boundary piece ``p`` once all its fragments are in; True = it failed."""
+        got = self.frags[p]
+        lo, hi = self._piece_range(p)
+        if p in self.verified or sum(len(b) for b in got.values()) != hi - lo:
+            return False
+        data = b"".join(got[a] for a in sorted(got))
+        if len(data) >= 1 << 20:
+            digest = await asyncio.get_running_loop().run_in_executor(None, _sha1, data)
+        else:
+            digest = _sha1(data)
+        if digest == self.meta.piece_hash(p):
+            self.verified.add(p)
+            return False
+        self.hash_fails += 1
+        self.piece_fails[p] = self.piece_fails.get(p, 0) + 1
+        if self.piece_fails[p] >= self.max_failures:
+            raise TorrentError(f"webseed served corrupt data for piece {p}")
+        return True
+
+    async def abort(self) -> None:
+        """Drop what a failed attempt staged: open multipart uploads, single-PUT objects."""
+        for t in self.targets:
+            try:
+                if t.upload_id:
+                    await self.s3.abort_multipart_upload(self.bucket, t.key, t.upload_id)
+                elif t.single:
+                    await self.s3.delete_object(self.bucket, t.key)
+            except Exception:
+                pass
+
+
+def _sha1(b: bytes) -> bytes:
+    return hashlib.sha1(b).digest()

@@ -99,6 +99,11 @@ class DownloadConfig(BaseModel):
     stream_http: bool = True
     # Torrents: stage selected files part by part while the torrent is still downloading.
     eager_upload: bool = True
+    # Webseed-only .torrent jobs: relay each S3 part webseed->S3 with in-flight SHA-1 and no
+    # disk hop (torrent/stream.py). auto: when the metainfo lists no trackers, first attempt
+    # only (a retry takes the disk path with every source); always: whenever webseeds exist.
+    torrent_stream: Literal["auto", "always", "off"] = "auto"
+    torrent_stream_parallel: int = 16           # parts (Range GETs) in flight per job
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
@@ -182,6 +187,7 @@ class Config(BaseModel):
             self.download.gpu_prewarm = False
             self.download.stream_http = False
             self.download.eager_upload = False
+            self.download.torrent_stream = "off"
             self.instance.background_cleanup = False
         else:
             self.broker.prefetch = max(self.broker.prefetch, self.concurrency)

@@ -41,6 +41,17 @@ class Origin:
         self.fail_ranges = {}   # Range header value -> remaining injected 503s
         self.slow = {}          # path -> bytes/s trickle rate
         self.chunked = set()
+        self.corrupt = {}       # path -> [file offset, responses left]: flip that byte
+
+    def _body(self, path: str, data: bytes, s: int, e: int) -> bytes:
+        """data[s:e+1], with the byte of an armed ``corrupt`` fault flipped if covered."""
+        body = data[s:e + 1]
+        c = self.corrupt.get(path)
+        if c and c[1] > 0 and s <= c[0] <= e:
+            c[1] -= 1
+            i = c[0] - s
+            body = body[:i] + bytes([body[i] ^ 0xFF]) + body[i + 1:]
+        return body
 
     async def start(self):
         from aiohttp import web
@@ -61,7 +72,8 @@ class Origin:
                 a, _, b = rng[6:].partition("-")
                 s, e = int(a), int(b) if b else len(data) - 1
                 hdrs["Content-Range"] = f"bytes {s}-{e}/{len(data)}"
-                return web.Response(status=206, body=data[s:e + 1], headers=hdrs)
+                return web.Response(status=206, body=self._body(req.path, data, s, e),
+                                    headers=hdrs)
             if req.method == "HEAD":
                 hdrs["Content-Length"] = str(len(data))
                 return web.Response(status=200, headers=hdrs)
@@ -88,7 +100,7 @@ class Origin:
                     await resp.write(data[i:i + 7777])
                 await resp.write_eof()
                 return resp
-            return web.Response(body=data, headers=hdrs)
+            return web.Response(body=self._body(req.path, data, 0, len(data) - 1), headers=hdrs)
 
         app = web.Application()
         app.router.add_route("*", "/{tail:.*}", handler)

@@ -1,0 +1,178 @@
+"""Streamed staging of webseed-only torrents (torrent/stream.py): webseed -> S3 relay with
+in-flight piece verification, boundary pieces assembled from neighbouring parts and gap
+fetches, refetch of corrupt data, clean abort, and the gate that picks this path."""
+from __future__ import annotations
+
+import asyncio
+import os
+import types
+
+import pytest
+
+from downloader_amd.models import api, keys
+from downloader_amd.s3.fake_server import FakeS3
+from downloader_amd.torrent.metainfo import FileEntry, Metainfo, make_torrent, parse_torrent
+from downloader_amd.torrent.stream import piece_split
+
+
+def _tree(root, sizes):
+    data = {}
+    for rel, n in sizes.items():
+        p = os.path.join(root, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        d = os.urandom(n)
+        with open(p, "wb") as f:
+            f.write(d)
+        data[rel] = d
+    return data
+
+
+def _worker(make_cfg, s3_ep, **over):
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.service.worker import Worker
+    d = {"torrent_enable_dht": False, "progress_interval_s": 0.05}
+    d.update(over.pop("download", {}))
+    return Worker(make_cfg(s3_ep, download=d, **over), broker=MemoryBroker())
+
+
+async def _wait(w, n=1, timeout=30.0):
+    for _ in range(int(timeout / 0.02)):
+        if len(w.results) >= n:
+            return
+        await asyncio.sleep(0.02)
+    raise AssertionError(w.results)
+
+
+def test_piece_split():
+    m = Metainfo(b"x" * 20, "t", 4, b"\0" * 100, [FileEntry(["t"], 18, 0)], 18)
+    assert piece_split(m, 0, 8) == (0, 8)        # aligned: two whole pieces
+    assert piece_split(m, 1, 8) == (3, 4)        # head 1..4, piece 4..8, tail 8..9
+    assert piece_split(m, 5, 2) == (2, 0)        # inside one piece: all head
+    assert piece_split(m, 6, 4) == (2, 0)        # straddles 8 without a whole piece
+    assert piece_split(m, 14, 4) == (2, 2)       # reaches the end: short last piece is whole
+    assert piece_split(m, 17, 1) == (1, 0)
+
+
+SHOW = {"Extras/x.mkv": 150_000, "Season 1/e1.mkv": 6_500_001, "Season 1/e2.mkv": 300_007,
+        "readme.txt": 1_000}
+
+
+async def _show(tmp_path, origin, plen=131072):
+    src = tmp_path / "src"
+    data = _tree(src / "Show", SHOW)
+    for rel, d in data.items():
+        origin.blobs["/ws/Show/" + rel] = d
+    raw = make_torrent(str(src / "Show"), plen, url_list=[origin.url("/ws/")])
+    origin.blobs["/t/show.torrent"] = raw
+    return data, parse_torrent(raw)
+
+
+def test_stream_job_unaligned_files_gaps_and_refetch(run, tmp_path, make_cfg, origin_cls):
+    """Selected files start and end mid-piece; the pieces they share with dropped files
+    (Extras, readme) are completed with gap fetches. One corrupt byte inside a part's whole
+    pieces and one inside a gap are both caught and refetched; the result is byte-exact and
+    the dropped files are (almost) never fetched."""
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        data, meta = await _show(tmp_path, origin)
+        origin.corrupt["/ws/Show/Season 1/e1.mkv"] = [3_000_000, 1]    # whole piece, part 1
+        origin.corrupt["/ws/Show/Extras/x.mkv"] = [140_000, 1]          # gap of a boundary piece
+        w = _worker(make_cfg, ep)
+        await w.start(health=False)
+        await w.submit(api.make_download("st1", "http", origin.url("/t/show.torrent"), "TV"))
+        await _wait(w)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        t = r.stats["torrent"]
+        assert t["staging"] == "stream" and t["hash_fails"] >= 2
+        for rel in ("Season 1/e1.mkv", "Season 1/e2.mkv"):
+            assert s3.get("triton-staging", keys.object_key("st1", rel)) == data[rel]
+        assert s3.objects("triton-staging")[keys.object_key("st1", "e1.mkv")].etag.endswith("-2")
+        assert s3.get("triton-staging", keys.object_key("st1", "x.mkv")) is None
+        assert not s3.uploads.get("triton-staging")
+        # dropped bytes: only the gap slices of the two boundary pieces were fetched
+        assert t["gap_bytes"] < 2 * meta.piece_length
+        assert t["skipped_bytes"] >= SHOW["Extras/x.mkv"] - meta.piece_length
+        ranges = [rg for _, p, rg in origin.requests if p.startswith("/ws/Show/Extras")]
+        assert ranges and all(rg and rg.startswith("bytes=") for rg in ranges)
+        prog = w.telemetry.progress_of("st1")
+        assert prog[0] == 0 and 50 in prog and prog[-1] == 100
+        for dp, _, fns in os.walk(tmp_path / "dl"):
+            assert not [f for f in fns if f.endswith(".mkv")], (dp, fns)   # nothing on disk
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_stream_job_persistent_corruption_aborts_cleanly(run, tmp_path, make_cfg, origin_cls):
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        data, _ = await _show(tmp_path, origin)
+        origin.corrupt["/ws/Show/Season 1/e1.mkv"] = [6_000_000, 1000]   # part 2, always bad
+        w = _worker(make_cfg, ep, broker={"max_retries": 0})
+        await w.start(health=False)
+        await w.submit(api.make_download("st2", "http", origin.url("/t/show.torrent"), "TV"))
+        await _wait(w)
+        r = w.results[0]
+        assert r.outcome == "dead" and "corrupt" in r.error, r
+        assert s3.get("triton-staging", keys.object_key("st2", "e1.mkv")) is None
+        assert s3.get("triton-staging", keys.object_key("st2", "e2.mkv")) is None   # deleted
+        assert s3.get("triton-staging", keys.done_key("st2")) is None
+        assert not s3.uploads.get("triton-staging")
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+@pytest.mark.parametrize("plen", [16384, 1 << 20])
+def test_stream_matches_disk_path(run, tmp_path, make_cfg, origin_cls, plen):
+    """Same job through both staging paths -> identical objects and progress endpoints."""
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        data, _ = await _show(tmp_path, origin, plen)
+        got = {}
+        for mode in ("auto", "off"):
+            w = _worker(make_cfg, ep, download={"torrent_stream": mode})
+            await w.start(health=False)
+            jid = f"cmp-{mode}"
+            await w.submit(api.make_download(jid, "http", origin.url("/t/show.torrent"), "TV"))
+            await _wait(w)
+            r = w.results[0]
+            assert r.outcome == "staged", r
+            assert r.stats["torrent"]["staging"] == ("stream" if mode == "auto" else "disk")
+            got[mode] = {rel: s3.get("triton-staging", keys.object_key(jid, rel))
+                         for rel in ("Season 1/e1.mkv", "Season 1/e2.mkv", "Extras/x.mkv")}
+            await w.stop()
+        assert got["auto"] == got["off"]
+        assert got["auto"]["Season 1/e1.mkv"] == data["Season 1/e1.mkv"]
+        await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_stream_gate():
+    from downloader_amd.torrent.backend import stream_webseeds
+    from downloader_amd.utils.config import load_config
+
+    class S3:
+        def can_relay(self, u):
+            return u.startswith("http://")
+    sv = types.SimpleNamespace(s3=S3())
+    m = Metainfo(b"x" * 20, "t", 4, b"\0" * 20, [FileEntry(["t"], 4, 0)], 4,
+                 url_list=["http://a/t"])
+    job = types.SimpleNamespace(attempt=0)
+    cfg = load_config(env={})
+    assert stream_webseeds(m, job, cfg, sv) == ["http://a/t"]
+    assert stream_webseeds(m, types.SimpleNamespace(attempt=1), cfg, sv) == []  # retry: disk
+    m.announce = [["http://tracker/announce"]]
+    assert stream_webseeds(m, job, cfg, sv) == []                # peers may be the source
+    cfg.download.torrent_stream = "always"
+    assert stream_webseeds(m, job, cfg, sv) == ["http://a/t"]
+    m.url_list.append("https://b/t")                              # TLS seed: no native relay
+    assert stream_webseeds(m, job, cfg, sv) == []
+    ref = load_config(overrides={"mode": "reference"}, env={})
+    m.url_list.pop()
+    assert stream_webseeds(m, job, ref, sv) == []
