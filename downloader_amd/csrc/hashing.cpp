@@ -166,6 +166,21 @@ std::string hash_pieces(const std::string& algo, const uint8_t* p, size_t n, siz
   size_t ds = (size_t)EVP_MD_get_size(md);
   size_t np = (n + piece_len - 1) / piece_len;
   std::string out(np * ds, '\0');
+  if (algo == "sha1" && sha1_mb_supported() && np >= 8) {
+    // 16 pieces per task in the lanes of one AVX-512 multi-buffer SHA-1
+    parallel_for((np + 15) / 16, threads, [&](size_t g, int) {
+      const uint8_t* ptrs[16];
+      size_t lens[16];
+      size_t k = std::min<size_t>(16, np - g * 16);
+      for (size_t l = 0; l < k; ++l) {
+        size_t off = (g * 16 + l) * piece_len;
+        ptrs[l] = p + off;
+        lens[l] = std::min(piece_len, n - off);
+      }
+      sha1_mb(ptrs, lens, k, (uint8_t*)&out[g * 16 * ds]);
+    });
+    return out;
+  }
   parallel_for(np, threads, [&](size_t i, int) {
     size_t off = i * piece_len;
     size_t len = std::min(piece_len, n - off);
@@ -173,6 +188,41 @@ std::string hash_pieces(const std::string& algo, const uint8_t* p, size_t n, siz
   });
   return out;
 }
+
+namespace {
+
+// SHA-1 of up to 16 storage pieces of equal length `len` (starting at offs[l]) in the lanes of
+// one multi-buffer state, reading `chunk` bytes per lane per step into `buf` (16 * chunk).
+// present[l] = false for a lane whose bytes are (partly) missing; its digest is not written.
+void mb_storage_group(const Storage& st, const int64_t* offs, size_t k, int64_t len,
+                      size_t chunk, uint8_t* buf, bool* present, uint8_t* out20) {
+  uint32_t state[5][16];
+  sha1x16_init(state);
+  uint16_t active = (uint16_t)((1u << k) - 1);
+  const uint8_t* ptr[16];
+  for (int l = 0; l < 16; ++l) ptr[l] = buf + (size_t)l * chunk;
+  int64_t off = 0;
+  for (;;) {
+    const int64_t n = std::min<int64_t>((int64_t)chunk, len - off);
+    for (size_t l = 0; l < k; ++l)
+      if ((active >> l) & 1 && !st.read(offs[l] + off, n, buf + l * chunk))
+        active &= (uint16_t)~(1u << l);
+    const size_t whole = (size_t)n / 64;
+    if (active && whole) sha1_mb16_blocks(state, ptr, whole, active);
+    off += n;
+    if (off >= len) {
+      const uint8_t* tails[16];
+      for (int l = 0; l < 16; ++l) tails[l] = ptr[l] + whole * 64;
+      if (active) sha1x16_finish(state, tails, (size_t)n % 64, (uint64_t)len, active, out20);
+      break;
+    }
+  }
+  for (size_t l = 0; l < k; ++l) present[l] = (active >> l) & 1;
+}
+
+constexpr size_t kMbChunk = 256 * 1024;   // per lane per step: 16 lanes = 4 MiB per thread
+
+}  // namespace
 
 // ---------------------------------------------------------------------------------------
 // Torrent storage: a list of files concatenated in order, split into fixed pieces.
@@ -248,6 +298,47 @@ std::vector<uint8_t> verify_pieces(const std::vector<std::pair<std::string, int6
     for (int64_t i = 0; i < np; ++i) idx[(size_t)i] = i;
   }
   std::vector<uint8_t> ok(idx.size(), 0);
+  if (sha1_mb_supported() && idx.size() >= 8) {
+    // Full-length pieces go 16 per task through the multi-buffer SHA-1 (streamed in 256 KiB
+    // steps per lane); the torrent's short last piece and out-of-range entries one by one.
+    std::vector<size_t> full, odd;
+    for (size_t k = 0; k < idx.size(); ++k) {
+      const int64_t i = idx[k];
+      if (i < 0 || i >= np) continue;
+      (std::min<int64_t>(piece_len, st.total - i * piece_len) == piece_len ? full : odd)
+          .push_back(k);
+    }
+    const size_t chunk = std::min<size_t>(kMbChunk, (size_t)piece_len);
+    const size_t groups = (full.size() + 15) / 16;
+    int nt = resolve_threads(threads, groups + odd.size());
+    std::vector<std::vector<uint8_t>> bufs(nt, std::vector<uint8_t>(16 * chunk));
+    parallel_for(groups + odd.size(), nt, [&](size_t task, int t) {
+      if (task < groups) {
+        int64_t offs[16];
+        bool present[16];
+        uint8_t d[16 * 20];
+        const size_t k = std::min<size_t>(16, full.size() - task * 16);
+        for (size_t l = 0; l < k; ++l) offs[l] = idx[full[task * 16 + l]] * piece_len;
+        mb_storage_group(st, offs, k, piece_len, chunk, bufs[t].data(), present, d);
+        for (size_t l = 0; l < k; ++l) {
+          const size_t kk = full[task * 16 + l];
+          ok[kk] = present[l] &&
+                   memcmp(d + 20 * l, hashes.data() + (size_t)idx[kk] * ds, ds) == 0;
+        }
+        return;
+      }
+      const size_t kk = odd[task - groups];
+      const int64_t i = idx[kk];
+      const int64_t off = i * piece_len;
+      const int64_t len = st.total - off;
+      std::vector<uint8_t> b((size_t)len);
+      if (!st.read(off, len, b.data())) return;
+      uint8_t d[20];
+      digest_into(md, b.data(), (size_t)len, d);
+      ok[kk] = memcmp(d, hashes.data() + (size_t)i * ds, ds) == 0;
+    });
+    return ok;
+  }
   int nt = resolve_threads(threads, idx.size());
   std::vector<std::vector<uint8_t>> bufs(nt, std::vector<uint8_t>((size_t)piece_len));
   parallel_for(idx.size(), nt, [&](size_t k, int t) {
@@ -272,6 +363,33 @@ std::string hash_storage_pieces(const std::vector<std::pair<std::string, int64_t
   size_t ds = (size_t)EVP_MD_get_size(md);
   int64_t np = (st.total + piece_len - 1) / piece_len;
   std::string out((size_t)np * ds, '\0');
+  const int64_t nfull = st.total / piece_len;   // pieces of full length
+  if (algo == "sha1" && sha1_mb_supported() && nfull >= 8) {
+    const size_t chunk = std::min<size_t>(kMbChunk, (size_t)piece_len);
+    const size_t groups = (size_t)(nfull + 15) / 16;
+    const size_t tasks = groups + (size_t)(np - nfull);
+    int nt = resolve_threads(threads, tasks);
+    std::vector<std::vector<uint8_t>> bufs(nt, std::vector<uint8_t>(16 * chunk));
+    parallel_for(tasks, nt, [&](size_t task, int t) {
+      if (task < groups) {
+        int64_t offs[16];
+        bool present[16];
+        const size_t k = (size_t)std::min<int64_t>(16, nfull - (int64_t)task * 16);
+        for (size_t l = 0; l < k; ++l) offs[l] = ((int64_t)task * 16 + (int64_t)l) * piece_len;
+        mb_storage_group(st, offs, k, piece_len, chunk, bufs[t].data(), present,
+                         (uint8_t*)&out[task * 16 * ds]);
+        for (size_t l = 0; l < k; ++l)
+          if (!present[l]) throw std::runtime_error("short read while hashing");
+        return;
+      }
+      const int64_t off = nfull * piece_len;    // the short last piece
+      std::vector<uint8_t> b((size_t)(st.total - off));
+      if (!st.read(off, (int64_t)b.size(), b.data()))
+        throw std::runtime_error("short read while hashing");
+      digest_into(md, b.data(), b.size(), (uint8_t*)&out[(size_t)nfull * ds]);
+    });
+    return out;
+  }
   int nt = resolve_threads(threads, (size_t)np);
   std::vector<std::vector<uint8_t>> bufs(nt, std::vector<uint8_t>((size_t)piece_len));
   parallel_for((size_t)np, nt, [&](size_t i, int t) {

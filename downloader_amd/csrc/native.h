@@ -42,6 +42,19 @@ std::string digest(const std::string& algo, const uint8_t* p, size_t n);
 std::string hash_pieces(const std::string& algo, const uint8_t* p, size_t n, size_t piece_len,
                         int threads);
 
+// ---- sha1_mb.cpp (AVX-512 16-lane multi-buffer SHA-1) --------------------------------
+bool sha1_mb_supported();
+// SHA-1 of n independent messages, 20 bytes each into out (16 lanes per group).
+void sha1_mb(const uint8_t* const* msgs, const size_t* lens, size_t n, uint8_t* out);
+// Streaming form for 16 messages of EQUAL length: init, absorb whole blocks (lanes whose
+// `active` bit is clear are untouched), finish with each lane's last tail_len (< 64) bytes;
+// digests of active lanes go to out + 20 * lane.
+void sha1x16_init(uint32_t st[5][16]);
+void sha1_mb16_blocks(uint32_t state[5][16], const uint8_t* const ptr[16], size_t nblocks,
+                      uint16_t active);
+void sha1x16_finish(uint32_t st[5][16], const uint8_t* const tails[16], size_t tail_len,
+                    uint64_t total_len, uint16_t active, uint8_t* out);
+
 struct Storage {
   struct Entry {
     std::string path;
@@ -114,6 +127,10 @@ class HttpConn {
   int64_t relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                             int64_t piece_len, Progress* prog, std::string* digests,
                             std::string* head, std::string* tail);
+  // relay_body_hashed for parts of >= 8 pieces: buffer the part, then multi-buffer SHA-1.
+  int64_t relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
+                               int64_t piece_len, Progress* prog, std::string* digests,
+                               std::string* head, std::string* tail);
   void send_raw(const std::string& s) { send_all((const uint8_t*)s.data(), s.size()); }
   int fd() const { return fd_; }
   void mark_unusable() { reusable_ = false; }

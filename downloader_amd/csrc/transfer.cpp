@@ -486,6 +486,9 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
                                     std::string* head, std::string* tail) {
   if (skip < 0 || full_len < 0 || skip + full_len > n || piece_len <= 0)
     throw IoError("relay_body_hashed: bad piece split");
+  const int64_t npieces = (full_len + piece_len - 1) / piece_len;
+  if (npieces >= 8 && n <= ((int64_t)256 << 20) && sha1_mb_supported())
+    return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail);
   // Chunk size: 512 KiB stays in a Zen 5 core's 1 MiB L2 between the recv copy, the send
   // copy and the SHA-1 pass, so the payload is read from DRAM once.
   thread_local std::vector<uint8_t> buf(512 * 1024);
@@ -548,6 +551,64 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
     consume(buf.data(), k);
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
+  return pos;
+}
+
+int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
+                                       int64_t full_len, int64_t piece_len, Progress* prog,
+                                       std::string* digests, std::string* head,
+                                       std::string* tail) {
+  // The whole part lands in a per-thread buffer on its way to `dst` (recv into it, send from
+  // it: the same two copies as the chunked path), then its pieces are hashed 16 at a time in
+  // the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the per-core rate of a single SHA-NI
+  // chain, which bounds the chunked path once many parts are in flight.
+  thread_local std::vector<uint8_t> part;
+  if ((int64_t)part.size() < n) part.resize((size_t)n);
+  uint8_t* b = part.data();
+  int64_t pos = 0;
+  while (pos < n) {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("cancelled");
+    }
+    const int64_t want = std::min<int64_t>(n - pos, 1 << 20);
+    int64_t k = take_buffered(b + pos, want);
+    if (k == 0) {
+      size_t r;
+      try {
+        r = recv_some(b + pos, (size_t)want);
+      } catch (...) {
+        dst.reusable_ = false;
+        throw;
+      }
+      if (r == 0) {
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError("source closed mid-body");
+      }
+      k = (int64_t)r;
+    }
+    try {
+      dst.send_all(b + pos, (size_t)k);
+    } catch (...) {
+      reusable_ = false;
+      throw;
+    }
+    pos += k;
+    if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
+  }
+  const int64_t np = (full_len + piece_len - 1) / piece_len;
+  std::vector<const uint8_t*> ptrs((size_t)np);
+  std::vector<size_t> lens((size_t)np);
+  for (int64_t i = 0; i < np; ++i) {
+    ptrs[(size_t)i] = b + skip + i * piece_len;
+    lens[(size_t)i] = (size_t)std::min<int64_t>(piece_len, full_len - i * piece_len);
+  }
+  digests->resize((size_t)np * 20);
+  sha1_mb(ptrs.data(), lens.data(), (size_t)np, (uint8_t*)&(*digests)[0]);
+  head->assign((const char*)b, (size_t)skip);
+  tail->assign((const char*)b + skip + full_len, (size_t)(n - skip - full_len));
   return pos;
 }
 

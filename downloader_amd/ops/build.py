@@ -48,7 +48,7 @@ def _run(cmd: List[str], verbose: bool) -> None:
 
 
 def build_native(force: bool = False, verbose: bool = True) -> Path:
-    srcs = [CSRC / "module.cpp", CSRC / "hashing.cpp", CSRC / "transfer.cpp"]
+    srcs = [CSRC / "module.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp"]
     out = OPS / f"_native{EXT}"
     if force or _stale(out, srcs + [CSRC / "native.h"]):
         cxx = os.environ.get("CXX", "g++")
@@ -89,7 +89,7 @@ SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"
 
 def build_selftest(kind: str, force: bool = False, verbose: bool = True) -> Path:
     """Host-only sanitizer build of the native code's self-test."""
-    srcs = [CSRC / "selftest.cpp", CSRC / "hashing.cpp", CSRC / "transfer.cpp"]
+    srcs = [CSRC / "selftest.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp"]
     BIN.mkdir(exist_ok=True)
     out = BIN / f"selftest_{kind}"
     if force or _stale(out, srcs + [CSRC / "native.h"]):

@@ -112,3 +112,31 @@ def test_gpu_device_from_worker_index(monkeypatch):
     assert hashing.gpu_device() == 3
     monkeypatch.setenv("STAGER_GPU_DEVICE", "5")
     assert hashing.gpu_device() == 5
+
+
+@pytest.mark.parametrize("piece", [300_001, 262_144, 4096 + 64])
+def test_multibuffer_verify_and_hash_storage(tmp_path, piece):
+    """The AVX-512 16-lane path (``csrc/sha1_mb.cpp``): pieces longer than one 256 KiB lane
+    step with a sub-block tail, groups of 16 plus a remainder, a file missing mid-torrent,
+    corrupt pieces, the short last piece and an arbitrary ``which`` list - vs hashlib."""
+    files, blob = _storage(tmp_path, [1_234_567, 2_000_000, 777_777, 0, 3_000_001])
+    want = b"".join(hashlib.sha1(blob[i:i + piece]).digest() for i in range(0, len(blob), piece))
+    n = len(want) // 20
+    assert hashing.hash_storage_pieces(files, piece, threads=3) == want
+    assert hashing.verify_pieces(files, piece, want, threads=2) == b"\x01" * n
+    p = files[4][0]
+    b = bytearray(open(p, "rb").read())
+    for off in (5, 1_500_000, len(b) - 1):          # incl. the torrent's short last piece
+        b[off] ^= 1
+    open(p, "wb").write(bytes(b))
+    base = sum(f[1] for f in files[:4])
+    bad = sorted({(base + off) // piece for off in (5, 1_500_000, len(b) - 1)})
+    os.unlink(files[2][0])                          # 777_777 bytes missing mid-torrent
+    lost = set(range(sum(f[1] for f in files[:2]) // piece,
+                     (sum(f[1] for f in files[:3]) - 1) // piece + 1))
+    ok = hashing.verify_pieces(files, piece, want)
+    assert [i for i in range(n) if not ok[i]] == sorted(lost | set(bad))
+    which = [n - 1, 0, bad[0], n - 1, n + 5] + sorted(lost)[:1]
+    sub = hashing.verify_pieces(files, piece, want, which=which)
+    expect = [i not in lost and i not in bad and 0 <= i < n for i in which]
+    assert list(sub) == [int(x) for x in expect]
