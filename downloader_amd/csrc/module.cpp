@@ -104,6 +104,8 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "stager host-native byte paths: hashing (OpenSSL EVP, threaded) and zero-copy HTTP";
 
   m.def("digest_size", &digest_size);
+  m.def("sha1_mb_supported", &sha1_mb_supported,
+        "True when the host runs the AVX-512 16-lane multi-buffer SHA-1 (csrc/sha1_mb.cpp)");
   m.def("effective_cpus", &effective_cpus,
         "CPUs usable by this process: affinity mask capped by the cgroup v2 cpu.max quota");
   m.def(

@@ -96,8 +96,13 @@ class Worker:
         if not self.stages:
             self.stages = await build_stages(self.cfg.stages, self.cfg, self.services)
         get_reaper(self.services).sweep()   # trash left by a crashed predecessor
-        if self.cfg.download.gpu_prewarm and self.cfg.download.verify_backend != "cpu":
-            from ..ops.hashing import prewarm_gpu
+        d = self.cfg.download
+        if d.gpu_prewarm and d.verify_backend != "cpu":
+            from ..ops import hashing
+            # auto never picks the GPU on a host with the multi-buffer SHA-1: no HIP init
+            if d.verify_backend == "auto" and not hashing.auto_may_use_gpu():
+                return
+            prewarm_gpu = hashing.prewarm_gpu
             try:
                 warm = await asyncio.get_running_loop().run_in_executor(None, prewarm_gpu)
                 self.log.info({"gpu_verifier": warm}, "gpu verifier prewarm")

@@ -34,8 +34,10 @@ from .tracker import decode_compact, encode_compact
 
 # Below this torrent size "auto" keeps incremental verification on the host: a GPU batch takes
 # ~100 ms whatever its size (a lane hashes a 4 MiB piece serially), so a short job pays that as
-# a tail. Measured on the build box: 4 GB single file 6.7 GB/s host vs 5.0 GB/s GPU; 20 GB /
-# 50 files 12.1 GB/s host vs 14.7 GB/s GPU with 40 % less worker CPU.
+# a tail. Measured on the build box with OpenSSL host hashing: 4 GB single file 6.7 GB/s host
+# vs 5.0 GB/s GPU; 20 GB / 50 files 12.1 vs 14.7 GB/s. With the AVX-512 multi-buffer SHA-1
+# the host wins both (20 GB: 13.1-13.8 vs 12.3-13.0 GB/s, profiles/s2_r1/verify_ab.jsonl), so
+# auto uses the GPU only on hosts without it (``hashing.auto_may_use_gpu``).
 GPU_INCREMENTAL_MIN_BYTES = 8 << 30
 
 if TYPE_CHECKING:  # pragma: no cover
@@ -731,7 +733,7 @@ class TorrentSession:
             elif be == "auto":
                 self._gpu_verify = (hashing._gpu_verifier is not None and
                                     self.meta.total_length >= GPU_INCREMENTAL_MIN_BYTES and
-                                    hashing.gpu_available())
+                                    hashing.auto_may_use_gpu())
             else:
                 self._gpu_verify = False
         return self._gpu_verify

@@ -124,9 +124,11 @@ def test_gpu_matches_cpu_backend_and_reports_throughput(gv, tmp_path):
     print(f"verify 256 MiB: gpu {len(data) / tg / 1e9:.2f} GB/s, cpu {len(data) / tc / 1e9:.2f} GB/s")
 
 
-def test_prewarm_makes_auto_pick_gpu():
+def test_prewarm_makes_auto_pick_gpu(monkeypatch):
+    """On a host without the AVX-512 multi-buffer SHA-1 a warm device takes auto rechecks."""
     from downloader_amd.ops import hashing
     assert hashing.prewarm_gpu() is True
+    monkeypatch.setattr(hashing, "host_multibuffer", lambda: False)
     assert hashing.choose_backend("auto", hashing.GPU_MIN_BYTES, 1024) == "gpu"
 
 

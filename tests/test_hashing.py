@@ -89,6 +89,13 @@ def test_choose_backend_cpu_without_gpu():
 
 def test_auto_backend_accounts_for_cold_start(monkeypatch):
     monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    monkeypatch.setattr(hashing, "_gpu_verifier", object())
+    # a host with the AVX-512 multi-buffer SHA-1 out-runs the device: auto stays on the host
+    monkeypatch.setattr(hashing, "host_multibuffer", lambda: True)
+    assert hashing.choose_backend("auto", hashing.GPU_COLD_MIN_BYTES, 1 << 20) == "cpu"
+    assert not hashing.auto_may_use_gpu()
+    assert hashing.choose_backend("gpu", 1, 1) == "gpu"
+    monkeypatch.setattr(hashing, "host_multibuffer", lambda: False)
     monkeypatch.setattr(hashing, "_gpu_verifier", None)
     big, cold = hashing.GPU_MIN_BYTES, hashing.GPU_COLD_MIN_BYTES
     # Cold device: only a recheck large enough to amortise HIP init goes to the GPU.

@@ -510,6 +510,7 @@ def test_auto_incremental_verify_policy(monkeypatch):
     from downloader_amd.torrent import session as S
     from downloader_amd.torrent.metainfo import FileEntry, Metainfo
     monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    monkeypatch.setattr(hashing, "host_multibuffer", lambda: False)   # host without AVX-512
 
     def sess(backend, total):
         c = TorrentClient(verify_backend=backend, listen=False)
@@ -522,6 +523,9 @@ def test_auto_incremental_verify_policy(monkeypatch):
     assert sess("auto", big)._use_gpu_verify() is True
     assert sess("auto", small)._use_gpu_verify() is False
     assert sess("cpu", big)._use_gpu_verify() is False
+    assert sess("gpu", 1)._use_gpu_verify() is True
+    monkeypatch.setattr(hashing, "host_multibuffer", lambda: True)    # AVX-512 host: CPU wins
+    assert sess("auto", big)._use_gpu_verify() is False
     assert sess("gpu", 1)._use_gpu_verify() is True
     from downloader_amd.utils.config import load_config
     ref = load_config(overrides={"mode": "reference"}, env={})
