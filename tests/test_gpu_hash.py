@@ -171,16 +171,17 @@ def test_gpu_batcher_coalesces_concurrent_runs(tmp_path):
 
 
 def test_torrent_job_with_gpu_piece_verification(run):
-    """Config-3 shape at 1/50 scale: webseed torrent -> eager S3 staging, every downloaded run
-    verified by the gfx950 kernel through the batcher."""
+    """Config-4 shape at 1/50 scale, disk staging (the stream path hashes in the relay):
+    webseed torrent -> eager S3 staging, every downloaded run verified by the gfx950 kernel
+    through the batcher."""
     import argparse
     from downloader_amd.bench import configs
     from downloader_amd.ops import hashing
     a = argparse.Namespace(mode="tuned", scale=0.02, piece_mb=1, verify_backend="gpu",
                            webseed_streams=4, webseed_chunk_mb=8, webseed_verify_depth=4,
-                           src_dir=None, stage_dir="")
+                           src_dir=None, stage_dir="", torrent_stream="off", stream_parallel=0)
     before = hashing.gpu_batcher().pieces
     r = run(configs.config_torrent(a, 4), timeout=300)
     assert r["uploaded_bytes"] == r["bytes"] and r["s3_bytes_received"] >= r["bytes"]
-    assert r["torrent"]["hash_fails"] == 0
+    assert r["torrent"]["hash_fails"] == 0 and r["torrent"]["staging"] == "disk"
     assert hashing.gpu_batcher().pieces - before >= r["bytes"] // (1 << 20)
