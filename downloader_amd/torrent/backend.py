@@ -172,6 +172,8 @@ async def _stream_torrent(meta: Metainfo, seeds: List[str], selected: List[str],
                             "webseed_verify_s": 0.0, "gap_bytes": st.stats["gap_bytes"],
                             "skipped_bytes": st.skipped_bytes(),
                             "timeline_s": {"complete": round(time.perf_counter() - t0, 4)}}
+    if sv.metrics is not None:
+        sv.metrics.bytes_verified.labels("host").inc(st.fetched_bytes)
     return st.fetched_bytes
 
 
@@ -231,6 +233,9 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
                                 "webseed_fetch_s": round(session.stats["webseed_fetch_s"], 4),
                                 "webseed_verify_s": round(session.stats["webseed_verify_s"], 4),
                                 "timeline_s": {k: round(v, 4) for k, v in tl.items()}}
+        if sv.metrics is not None:
+            sv.metrics.bytes_verified.labels("gpu" if session._gpu_verify else "host").inc(
+                session.verified_bytes)
         return session.total_bytes()
     finally:
         await client.remove(session)

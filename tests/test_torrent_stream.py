@@ -97,6 +97,8 @@ def test_stream_job_unaligned_files_gaps_and_refetch(run, tmp_path, make_cfg, or
         assert t["skipped_bytes"] >= SHOW["Extras/x.mkv"] - meta.piece_length
         ranges = [rg for _, p, rg in origin.requests if p.startswith("/ws/Show/Extras")]
         assert ranges and all(rg and rg.startswith("bytes=") for rg in ranges)
+        assert w.metrics.sample("downloader_bytes_verified_total", backend="host") == \
+            t["webseed_bytes"] >= SHOW["Season 1/e1.mkv"] + SHOW["Season 1/e2.mkv"]
         prog = w.telemetry.progress_of("st1")
         assert prog[0] == 0 and 50 in prog and prog[-1] == 100
         for dp, _, fns in os.walk(tmp_path / "dl"):
@@ -144,6 +146,9 @@ def test_stream_matches_disk_path(run, tmp_path, make_cfg, origin_cls, plen):
             r = w.results[0]
             assert r.outcome == "staged", r
             assert r.stats["torrent"]["staging"] == ("stream" if mode == "auto" else "disk")
+            if mode == "off":   # the whole torrent was downloaded and verified
+                assert w.metrics.sample("downloader_bytes_verified_total", backend="host") == \
+                    sum(SHOW.values())
             got[mode] = {rel: s3.get("triton-staging", keys.object_key(jid, rel))
                          for rel in ("Season 1/e1.mkv", "Season 1/e2.mkv", "Extras/x.mkv")}
             await w.stop()
