@@ -63,7 +63,9 @@ class _Unit:
     skip: int = 0               # bytes before the first whole piece
     full: int = 0               # bytes of whole pieces
     attempts: int = 0
-    done: bool = False
+    state: str = "queued"       # queued | running | done - a unit is in the queue at most once
+    again: bool = False         # fetch once more when the running fetch ends (bad neighbour piece)
+    counted: bool = False       # its bytes are in StreamStager.done_bytes
 
     @property
     def end(self) -> int:
@@ -132,6 +134,7 @@ class StreamStager:
         self.suppliers: Dict[int, Set[int]] = {}
         self._plan_gaps()
         self.verified: Set[int] = set()
+        self._checking: Set[int] = set()
         self.piece_fails: Dict[int, int] = {}
         self.total = sum(t.size for t in self.targets)
         self.fetched_bytes = 0
@@ -216,6 +219,7 @@ class StreamStager:
     async def _worker(self, queue: "asyncio.Queue[_Unit]") -> None:
         while True:
             u = await queue.get()
+            u.state = "running"
             try:
                 requeue = await self._process(u)
             except (TransportError, OSError) as e:
@@ -233,20 +237,37 @@ class StreamStager:
             self._settle(u, requeue, queue)
 
     def _settle(self, u: _Unit, requeue: List[_Unit], queue: "asyncio.Queue[_Unit]") -> None:
-        if u not in requeue:
-            u.done = True
-            self._outstanding -= 1
-        for r in requeue:
-            if r.done:
-                r.done = False
-                self._outstanding += 1
-                if r.target is not None:
-                    self.done_bytes -= r.length
+        """``u``'s fetch ended; ``requeue`` = units whose bytes must be fetched again. A unit
+        is never queued twice: a queued one stays as it is, a running one is flagged
+        ``again`` (it goes back to the queue when its fetch ends), a done one returns to the
+        queue and counts as outstanding again."""
+        redo = {r.uid: r for r in requeue}
+        if u.again:
+            u.again = False
+            redo[u.uid] = u
+        for r in redo.values():
             for a, _ in r.fragments():               # its fragments are fetched again
                 p = a // self.plen
                 self.frags[p].pop(a, None)
                 self.verified.discard(p)
-            queue.put_nowait(r)
+            if r.counted:
+                r.counted = False
+                self.done_bytes -= r.length
+        for r in redo.values():
+            if r is u:
+                continue
+            if r.state == "done":
+                r.state = "queued"
+                self._outstanding += 1
+                queue.put_nowait(r)
+            elif r.state == "running":
+                r.again = True
+        if u.uid in redo:
+            u.state = "queued"
+            queue.put_nowait(u)
+        else:
+            u.state = "done"
+            self._outstanding -= 1
         if self._outstanding == 0:
             self._finished.set()
 
@@ -297,7 +318,9 @@ class StreamStager:
                 return None
         if not t.single:
             t.etags[u.num] = etag
-        self.done_bytes += u.length
+        if not u.counted:
+            u.counted = True
+            self.done_bytes += u.length
         out = []
         if u.skip:
             out.append((u.start, h["head"]))
@@ -320,16 +343,22 @@ class StreamStager:
         return bytes(buf)
 
     async def _check_piece(self, p: int) -> bool:
-        """Verify boundary piece ``p`` once all its fragments are in; True = it failed."""
+        """Verify boundary piece ``p`` once all its fragments are in; True = it failed. A
+        piece already being hashed (its last fragment arrived twice) is not checked again."""
         got = self.frags[p]
         lo, hi = self._piece_range(p)
-        if p in self.verified or sum(len(b) for b in got.values()) != hi - lo:
+        if p in self.verified or p in self._checking or \
+                sum(len(b) for b in got.values()) != hi - lo:
             return False
         data = b"".join(got[a] for a in sorted(got))
-        if len(data) >= 1 << 20:
-            digest = await asyncio.get_running_loop().run_in_executor(None, _sha1, data)
-        else:
-            digest = _sha1(data)
+        self._checking.add(p)
+        try:
+            if len(data) >= 1 << 20:
+                digest = await asyncio.get_running_loop().run_in_executor(None, _sha1, data)
+            else:
+                digest = _sha1(data)
+        finally:
+            self._checking.discard(p)
         if digest == self.meta.piece_hash(p):
             self.verified.add(p)
             return False

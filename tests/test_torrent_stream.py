@@ -181,3 +181,43 @@ def test_stream_gate():
     ref = load_config(overrides={"mode": "reference"}, env={})
     m.url_list.pop()
     assert stream_webseeds(m, job, ref, sv) == []
+
+
+def test_settle_never_queues_a_unit_twice(tmp_path):
+    """Boundary piece 2 ([8, 12)) is supplied by file a's tail and file b's head. When it
+    fails while a neighbour is still being fetched, the neighbour is flagged and re-fetched
+    once its current fetch ends - it is never in the queue twice, and the outstanding count
+    that ends the job stays exact."""
+    from downloader_amd.torrent.stream import StreamStager
+    files = [FileEntry(["a.mkv"], 10, 0), FileEntry(["b.mkv"], 10, 10)]
+    m = Metainfo(b"x" * 20, "P", 4, b"\0" * 100, files, 20, multi_file=True)
+    s3 = types.SimpleNamespace(multipart_threshold=1 << 20, plan_parts=lambda n: [(1, 0, n)])
+    root = str(tmp_path)
+    sel = [os.path.join(root, "P", "a.mkv"), os.path.join(root, "P", "b.mkv")]
+    st = StreamStager(m, types.SimpleNamespace(id="j"),
+                      types.SimpleNamespace(s3=types.SimpleNamespace(bucket="b")),
+                      types.SimpleNamespace(s3=s3), sel, root, ["http://x/"])
+    a, b = st.units
+    assert len(st.units) == 2 and st.suppliers[2] == {a.uid, b.uid}   # no gaps needed
+    q = asyncio.Queue()
+    st._outstanding = 2
+    a.state = b.state = "running"
+    for u in (a, b):
+        u.counted = True
+        st.done_bytes += u.length
+    st._settle(a, [], q)                      # a done
+    assert (a.state, st._outstanding, q.qsize()) == ("done", 1, 0)
+    st._settle(b, [a, b], q)                  # piece 2 failed when b delivered: both again
+    assert (a.state, b.state, st._outstanding, q.qsize()) == ("queued", "queued", 2, 2)
+    assert st.done_bytes == 0 and not a.counted
+    q.get_nowait(), q.get_nowait()
+    a.state = b.state = "running"
+    st._settle(a, [a, b], q)                  # fails again while b is still running
+    assert (a.state, b.again, q.qsize(), st._outstanding) == ("queued", True, 1, 2)
+    st._settle(b, [], q)                      # b's stale fetch ends: re-queued, not done
+    assert (b.state, b.again, q.qsize(), st._outstanding) == ("queued", False, 2, 2)
+    q.get_nowait(), q.get_nowait()
+    a.state = b.state = "running"
+    st._settle(a, [], q)
+    st._settle(b, [], q)
+    assert st._outstanding == 0 and st._finished.is_set() and q.qsize() == 0
