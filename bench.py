@@ -390,8 +390,8 @@ def main() -> int:
     nproc = args.procs_per_rank
     if nproc <= 0:   # auto: one worker process per 8 CPUs of the rank's slice, at most 8
         nproc = max(1, min(8, len(pinned or os.sched_getaffinity(0)) // 8))
-    if args.mode == "reference":
-        nproc = 1    # the reference is one serial consumer per container
+    if args.mode == "reference" and args.procs_per_rank <= 0:
+        nproc = 1    # the reference is one serial consumer per container (explicit N: N of them)
     try:
         tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
         ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
