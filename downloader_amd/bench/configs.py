@@ -159,7 +159,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["webseed_verify_depth"] = a.webseed_verify_depth
             if getattr(a, "no_gpu_prewarm", False):
                 dl["gpu_prewarm"] = False
-            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl),
+            s3o = {"part_size": a.part_mb << 20} if a.part_mb else {}
+            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl, s3=s3o),
                        broker=MemoryBroker())
             await w.start(health=False)
             m = api.make_download(f"c{cfg_no}-{a.mode}", "http", b.files_url("job.torrent"),
@@ -327,6 +328,8 @@ def main(argv=None) -> int:
                     help="download.torrent_stream: webseed->S3 relay (auto) or disk staging (off)")
     ap.add_argument("--stream-parallel", type=int, default=0,
                     help="download.torrent_stream_parallel (parts in flight per job)")
+    ap.add_argument("--part-mb", type=int, default=0,
+                    help="configs 3/4: override s3.part_size (MiB; one relayed part per unit)")
     ap.add_argument("--no-gpu-prewarm", action="store_true",
                     help="do not init the GPU verifier at worker start (download.gpu_prewarm)")
     ap.add_argument("--workers", type=int, default=4, help="config 5 worker processes")
