@@ -159,7 +159,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["webseed_verify_depth"] = a.webseed_verify_depth
             if getattr(a, "no_gpu_prewarm", False):
                 dl["gpu_prewarm"] = False
-            s3o = {"part_size": a.part_mb << 20} if a.part_mb else {}
+            part_mb = getattr(a, "part_mb", 0)
+            s3o = {"part_size": part_mb << 20} if part_mb else {}
             w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl, s3=s3o),
                        broker=MemoryBroker())
             await w.start(health=False)

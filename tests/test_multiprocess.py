@@ -117,3 +117,18 @@ def test_bench_rank_with_two_worker_processes(tmp_path):
     j = json.loads(lines[0])
     assert j["procs_per_rank"] == 2 and j["config"]["jobs_timed"] == 6
     assert j["s3_peer_bytes_received"] >= 6 * 4_000_000 and j["value"] > 0
+
+
+@pytest.mark.slow
+def test_bench_reference_mode_worker_count():
+    """Reference mode defaults to one serial consumer per rank; an explicit --procs-per-rank N
+    runs N of them (N reference containers, the worker sweep's reference column)."""
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    base = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1", "--warmup", "0",
+            "--jobs-per-step", "2", "--size-mb", "2", "--mode", "reference"]
+    for extra, want in (([], 1), (["--procs-per-rank", "2"], 2)):
+        r = subprocess.run(base + extra, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        assert j["mode"] == "reference" and j["procs_per_rank"] == want
+        assert j["config"]["jobs_timed"] == 2        # jobs per step are per rank, split over procs
