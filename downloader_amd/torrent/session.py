@@ -30,7 +30,7 @@ from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
 from .peer import BLOCK, METADATA_PIECE, PIECE, PeerConn
 from .storage import Bitfield, Storage
-from .tracker import decode_compact, encode_compact
+from .tracker import decode_compact, encode_compact, supported as tracker_supported
 
 # Below this torrent size "auto" keeps incremental verification on the host: a GPU batch takes
 # ~100 ms whatever its size (a lane hashes a 4 MiB piece serially), so a short job pays that as
@@ -262,7 +262,7 @@ class TorrentSession:
         self.root = root
         self.meta = meta
         self.name = name
-        self.trackers: List[str] = list(trackers)
+        self.trackers: List[str] = [t for t in trackers if tracker_supported(t)]
         self.webseeds: List[str] = list(webseeds)
         self.known: Dict[Peer, float] = {}
         self.failed_peers: Dict[Peer, Tuple[int, float]] = {}
@@ -296,7 +296,8 @@ class TorrentSession:
                       "webseed_fetch_s": 0.0, "webseed_verify_s": 0.0}
         self.add_peers(list(peers), "magnet")
         if meta is not None:
-            self.trackers += [t for t in meta.trackers() if t not in self.trackers]
+            self.trackers += [t for t in meta.trackers()
+                              if t not in self.trackers and tracker_supported(t)]
             self.webseeds += [w for w in meta.url_list if w not in self.webseeds]
 
     # ---------------------------------------------------------------- state

@@ -1,7 +1,9 @@
 """Tracker clients: HTTP (BEP-3, compact peers BEP-23) and UDP (BEP-15).
 
-Replaces ``bittorrent-tracker@9`` (yarn.lock:402-430). WebSocket trackers are not implemented
-(no WebRTC peers in Node without ``wrtc``).
+Replaces ``bittorrent-tracker@9`` (yarn.lock:402-430). WebSocket trackers (``ws://``,
+``wss://``) only hand out WebRTC peers; bittorrent-tracker in Node without ``wrtc`` drops them
+from the announce list, and so does ``supported`` here: a torrent whose only
+trackers are WebSocket ones is treated as tracker-less instead of announcing to them forever.
 """
 from __future__ import annotations
 
@@ -144,6 +146,17 @@ async def announce_udp(url: str, info_hash: bytes, peer_id: bytes, port: int, up
         return AnnounceResult(interval, decode_compact(data[20:]), seeders, leechers)
     finally:
         tr.close()
+
+
+SCHEMES = ("http", "https", "udp")
+
+
+def supported(url: str) -> bool:
+    """True for tracker URLs this client can announce to (HTTP(S) and UDP)."""
+    try:
+        return urlsplit(url).scheme in SCHEMES
+    except ValueError:
+        return False
 
 
 async def announce(url: str, *a, transports=None, **kw) -> AnnounceResult:

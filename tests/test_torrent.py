@@ -531,3 +531,27 @@ def test_auto_incremental_verify_policy(monkeypatch):
     ref = load_config(overrides={"mode": "reference"}, env={})
     assert ref.download.verify_backend == "cpu" and ref.download.verify_threads == 1
     assert ref.download.webseed_verify_depth == 1 and not ref.s3.unsigned_payload
+
+
+def test_websocket_only_trackers_are_dropped(run, tmp_path):
+    """ws:// / wss:// trackers hand out WebRTC peers only; like bittorrent-tracker in Node
+    without wrtc they are dropped, so a torrent whose only trackers are WebSocket ones and
+    whose webseed is dead fails instead of waiting for the 240 s stall watchdog."""
+    from downloader_amd.torrent.tracker import supported
+    assert supported("http://t/a") and supported("udp://u:1") and supported("https://t/a")
+    assert not supported("wss://tracker.example/announce") and not supported("ws://t")
+    _tree(tmp_path / "src", {"movie.mkv": 100_000})
+    meta = parse_torrent(make_torrent(str(tmp_path / "src" / "movie.mkv"), 16384,
+                                      trackers=["wss://tracker.example/announce", "ws://t/a"],
+                                      url_list=["http://127.0.0.1:1/"]))
+
+    async def go():
+        c = await TorrentClient(listen=False, webseed_max_failures=2).start()
+        try:
+            s = await c.add_torrent(meta, str(tmp_path / "dl"))
+            assert s.trackers == []
+            with pytest.raises(TorrentError):
+                await asyncio.wait_for(s.wait(), 60)
+        finally:
+            await c.close()
+    run(go())
