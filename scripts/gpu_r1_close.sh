@@ -2,7 +2,7 @@
 # End-of-round re-validation of the committed tree: GPU tier, smoke, headline bench x2, N=2.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=gpurun_out/close
+F=${OUT:-gpurun_out/close}
 mkdir -p $F
 export LOG_LEVEL=error
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $F/pytest_gpu.txt 2>&1 && \
