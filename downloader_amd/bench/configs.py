@@ -164,19 +164,28 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl, s3=s3o),
                        broker=MemoryBroker())
             await w.start(health=False)
-            m = api.make_download(f"c{cfg_no}-{a.mode}", "http", b.files_url("job.torrent"),
-                                  "TV" if cfg_no == 4 else "MOVIE")
-            cpu0, peer0 = _self_cpu(), b.cpu_seconds()
-            dt, r = await _run_jobs(w, [m])
-            cpu_s, peer_cpu_s = _self_cpu() - cpu0, b.cpu_seconds() - peer0
-            # job_s ends at the convert publish; the background unlink of the staged files
-            # (instance.background_cleanup) is timed separately here.
-            tc = time.perf_counter()
-            await asyncio.get_running_loop().run_in_executor(
-                None, get_reaper(w.services).drain, 600.0)
-            cleanup_s = time.perf_counter() - tc
+            # --reps: the same torrent staged again under a fresh media id (no done marker,
+            # so every rep does the full job); one job is a sub-second sample on this box.
+            reps = []
+            for k in range(max(1, getattr(a, "reps", 1))):
+                suffix = f"-r{k}" if k else ""
+                m = api.make_download(f"c{cfg_no}-{a.mode}{suffix}", "http",
+                                      b.files_url("job.torrent"), "TV" if cfg_no == 4 else "MOVIE")
+                cpu0, peer0 = _self_cpu(), b.cpu_seconds()
+                dt_k, r_k = await _run_jobs(w, [m])
+                cpu_k, peer_k = _self_cpu() - cpu0, b.cpu_seconds() - peer0
+                # job_s ends at the convert publish; the background unlink of the staged
+                # files (instance.background_cleanup) is timed separately here.
+                tc = time.perf_counter()
+                await asyncio.get_running_loop().run_in_executor(
+                    None, get_reaper(w.services).drain, 600.0)
+                cleanup_k = time.perf_counter() - tc
+                assert r_k[0].outcome == "staged", r_k[0]
+                reps.append((dt_k, r_k, cpu_k, peer_k, cleanup_k))
             await w.stop()
-            assert r[0].outcome == "staged", r[0]
+            # the median rep is the one reported in full
+            reps_sorted = sorted(reps, key=lambda x: x[0])
+            dt, r, cpu_s, peer_cpu_s, cleanup_s = reps_sorted[len(reps_sorted) // 2]
             st = b.stats()
     finally:
         shutil.rmtree(src, ignore_errors=True)
@@ -188,7 +197,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "torrent": r[0].stats.get("torrent", {}), "stage_s": r[0].stats.get("stage_s", {}),
             "eager_upload_s": r[0].stats.get("eager_upload_s"),
             "cleanup_after_job_s": round(cleanup_s, 3),
-            "worker_cpu_s": round(cpu_s, 2), "peer_cpu_s": round(peer_cpu_s, 2)}
+            "worker_cpu_s": round(cpu_s, 2), "peer_cpu_s": round(peer_cpu_s, 2),
+            "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps]}
 
 
 # ---------------------------------------------------------------------------- config 5
@@ -321,6 +331,8 @@ def main(argv=None) -> int:
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")
     ap.add_argument("--piece-mb", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=1,
+                    help="configs 3/4: stage the torrent this many times, report the median")
     ap.add_argument("--verify-backend", choices=["cpu", "gpu", "auto"], default="auto")
     ap.add_argument("--webseed-streams", type=int, default=0)
     ap.add_argument("--webseed-chunk-mb", type=int, default=0)

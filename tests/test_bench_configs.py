@@ -1,0 +1,30 @@
+"""BASELINE config benches on the CPU: the torrent configs (3/4) through the native blobd
+peer at a tiny scale, including ``--reps`` (same torrent staged again under fresh media ids,
+median reported)."""
+import argparse
+
+from downloader_amd.bench import configs
+
+
+def _ns(**over):
+    a = argparse.Namespace(mode="tuned", scale=0.002, piece_mb=1, verify_backend="cpu",
+                           webseed_streams=0, webseed_chunk_mb=0, webseed_verify_depth=0,
+                           src_dir=None, stage_dir="", torrent_stream="auto", stream_parallel=0)
+    vars(a).update(over)
+    return a
+
+
+def test_config3_reps_report_median(run):
+    r = run(configs.config_torrent(_ns(reps=3), 3), timeout=120)
+    assert r["reps"] == 3 and len(r["MBps_reps"]) == 3
+    assert sorted(r["MBps_reps"])[1] == r["MBps"]
+    assert r["uploaded_bytes"] == r["bytes"]
+    assert r["s3_bytes_received"] >= 3 * r["bytes"]      # every rep re-staged the object
+    assert r["torrent"]["hash_fails"] == 0
+
+
+def test_config4_single_rep_default(run):
+    """Namespace callers without ``reps`` (e.g. older scripts) still get one job."""
+    r = run(configs.config_torrent(_ns(), 4), timeout=120)
+    assert r["reps"] == 1 and r["files"] == 50
+    assert r["uploaded_bytes"] == r["bytes"]
