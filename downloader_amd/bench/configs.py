@@ -157,6 +157,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["webseed_chunk"] = a.webseed_chunk_mb << 20
             if a.webseed_verify_depth:
                 dl["webseed_verify_depth"] = a.webseed_verify_depth
+            if getattr(a, "webseed_verify_depth_gpu", 0):
+                dl["webseed_verify_depth_gpu"] = a.webseed_verify_depth_gpu
             if getattr(a, "no_gpu_prewarm", False):
                 dl["gpu_prewarm"] = False
             part_mb = getattr(a, "part_mb", 0)
@@ -337,6 +339,8 @@ def main(argv=None) -> int:
     ap.add_argument("--webseed-streams", type=int, default=0)
     ap.add_argument("--webseed-chunk-mb", type=int, default=0)
     ap.add_argument("--webseed-verify-depth", type=int, default=0)
+    ap.add_argument("--webseed-verify-depth-gpu", type=int, default=0,
+                    help="fetched runs queued per stream when the GPU batcher verifies them")
     ap.add_argument("--torrent-stream", choices=["auto", "always", "off"], default="auto",
                     help="download.torrent_stream: webseed->S3 relay (auto) or disk staging (off)")
     ap.add_argument("--stream-parallel", type=int, default=0,
