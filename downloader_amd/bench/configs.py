@@ -50,6 +50,18 @@ def _pct(xs: List[float], q: float) -> float:
     return xs[min(len(xs) - 1, int(q * (len(xs) - 1) + 0.5))]
 
 
+def _rss_mb() -> Dict[str, float]:
+    """This (worker) process: current RSS (/proc/self/statm) and peak RSS (ru_maxrss)."""
+    import resource
+    try:
+        with open("/proc/self/statm") as f:
+            cur = int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE")
+    except OSError:
+        cur = 0
+    peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+    return {"rss_MB": round(cur / MB, 1), "rss_peak_MB": round(peak / MB, 1)}
+
+
 def _self_cpu() -> float:
     import resource
     ru = resource.getrusage(resource.RUSAGE_SELF)
@@ -184,6 +196,12 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 cleanup_k = time.perf_counter() - tc
                 assert r_k[0].outcome == "staged", r_k[0]
                 reps.append((dt_k, r_k, cpu_k, peer_k, cleanup_k))
+            rss = _rss_mb()
+            try:
+                from downloader_amd.ops import native
+                pool = native().relay_pool_stats()
+            except Exception:
+                pool = {}
             await w.stop()
             # the median rep is the one reported in full
             reps_sorted = sorted(reps, key=lambda x: x[0])
@@ -200,6 +218,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "eager_upload_s": r[0].stats.get("eager_upload_s"),
             "cleanup_after_job_s": round(cleanup_s, 3),
             "worker_cpu_s": round(cpu_s, 2), "peer_cpu_s": round(peer_cpu_s, 2),
+            "worker_rss_after_MB": rss["rss_MB"], "worker_rss_peak_MB": rss["rss_peak_MB"],
+            "relay_pool_after": pool,
             "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps]}
 
 

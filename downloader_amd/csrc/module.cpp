@@ -108,6 +108,19 @@ PYBIND11_MODULE(_native, m) {
         "True when the host runs the AVX-512 16-lane multi-buffer SHA-1 (csrc/sha1_mb.cpp)");
   m.def("effective_cpus", &effective_cpus,
         "CPUs usable by this process: affinity mask capped by the cgroup v2 cpu.max quota");
+  m.def("relay_pool_trim", &relay_pool_trim,
+        "Unmap every idle hashed-relay part buffer; returns the bytes freed");
+  m.def("relay_pool_set_max_idle", &relay_pool_set_max_idle, py::arg("n"),
+        "Keep at most n idle part buffers (the rest are unmapped on release)");
+  m.def("relay_pool_stats", []() {
+    RelayPoolStats s = relay_pool_stats();
+    py::dict d;
+    d["idle_buffers"] = s.idle_buffers;
+    d["idle_bytes"] = s.idle_bytes;
+    d["in_use"] = s.in_use;
+    d["max_idle"] = s.max_idle;
+    return d;
+  });
   m.def(
       "digest",
       [](const std::string& algo, const py::buffer& data) {

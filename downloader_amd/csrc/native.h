@@ -81,6 +81,18 @@ std::vector<std::string> hash_file_ranges(const std::string& path,
                                           const std::string& algo, int threads);
 
 // ---- transfer.cpp ----------------------------------------------------------------------
+// Parts up to this size are relayed through a pooled buffer and hashed with the multi-buffer
+// SHA-1; larger ones take the chunked (L2-sized, single-chain) path.
+constexpr int64_t kMaxBufferedPart = (int64_t)64 << 20;
+
+struct RelayPoolStats {
+  size_t idle_buffers, idle_bytes, in_use, max_idle;
+};
+// Idle part buffers are unmapped (returns the bytes freed); max_idle bounds the idle list.
+size_t relay_pool_trim();
+void relay_pool_set_max_idle(size_t n);
+RelayPoolStats relay_pool_stats();
+
 // Byte counter shared between a transfer running on a worker thread and the asyncio side
 // (progress telemetry, stall watchdog, cancellation).
 struct Progress {

@@ -17,6 +17,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <sys/mman.h>
@@ -489,7 +490,7 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
   if (skip < 0 || full_len < 0 || skip + full_len > n || piece_len <= 0)
     throw IoError("relay_body_hashed: bad piece split");
   const int64_t npieces = (full_len + piece_len - 1) / piece_len;
-  if (npieces >= 8 && n <= ((int64_t)256 << 20) && sha1_mb_supported())
+  if (npieces >= 8 && n <= kMaxBufferedPart && sha1_mb_supported())
     return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail);
   // Chunk size: 512 KiB stays in a Zen 5 core's 1 MiB L2 between the recv copy, the send
   // copy and the SHA-1 pass, so the payload is read from DRAM once.
@@ -557,7 +558,7 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
 }
 
 namespace {
-// Per-thread part buffer for relay_body_hashed_mb: anonymous memory on 2 MiB boundaries with
+// Part buffers for relay_body_hashed_mb: anonymous memory on 2 MiB boundaries with
 // MADV_HUGEPAGE and no value-initialisation. A std::vector resize zero-filled every 4 KiB page
 // of a 64 MiB part and faulted them one by one: ~280k minor faults (0.7 CPU-s) the first time
 // 16 relay threads ran, i.e. the first torrent a worker staged ran at half speed.
@@ -566,14 +567,7 @@ struct PartBuffer {
   uint8_t* base = nullptr;
   size_t mapped = 0, cap = 0;
   uint8_t* data = nullptr;
-  ~PartBuffer() {
-    if (base) munmap(base, mapped);
-  }
-  uint8_t* get(size_t n) {
-    if (n <= cap) return data;
-    if (base) munmap(base, mapped);
-    base = data = nullptr;
-    mapped = cap = 0;
+  explicit PartBuffer(size_t n) {
     const size_t c = (n + kHuge - 1) & ~(kHuge - 1);
     void* m = mmap(nullptr, c + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m == MAP_FAILED) throw std::bad_alloc();
@@ -582,10 +576,98 @@ struct PartBuffer {
     data = (uint8_t*)(((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
     madvise(data, c, MADV_HUGEPAGE);  // best effort: THP "never" just keeps 4 KiB pages
     cap = c;
-    return data;
   }
+  ~PartBuffer() { munmap(base, mapped); }
+  PartBuffer(const PartBuffer&) = delete;
+  PartBuffer& operator=(const PartBuffer&) = delete;
+};
+
+// One process-wide pool instead of a buffer per transfer thread: a thread_local buffer as
+// large as the biggest part ever relayed stayed resident on each of the 32 transfer threads
+// (up to 4-8 GiB per worker after one torrent job). Buffers in use are bounded by the
+// caller's relays in flight (torrent_stream_parallel per job); at most `max_idle` idle
+// buffers are kept for the next part, the rest are unmapped on release, and trim() unmaps
+// every idle one (the stream stager calls it when a job's relays are done).
+class PartPool {
+ public:
+  std::unique_ptr<PartBuffer> acquire(size_t n) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      size_t best = idle_.size();
+      for (size_t i = 0; i < idle_.size(); ++i)
+        if (idle_[i]->cap >= n && (best == idle_.size() || idle_[i]->cap < idle_[best]->cap))
+          best = i;
+      if (best < idle_.size()) {
+        std::unique_ptr<PartBuffer> b = std::move(idle_[best]);
+        idle_.erase(idle_.begin() + (ptrdiff_t)best);
+        idle_bytes_ -= b->cap;
+        in_use_ += 1;
+        return b;
+      }
+      in_use_ += 1;
+    }
+    try {
+      return std::unique_ptr<PartBuffer>(new PartBuffer(n));
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu_);
+      in_use_ -= 1;
+      throw;
+    }
+  }
+  void release(std::unique_ptr<PartBuffer> b) {
+    std::unique_ptr<PartBuffer> drop;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      in_use_ -= 1;
+      if (idle_.size() < max_idle_) {
+        idle_bytes_ += b->cap;
+        idle_.push_back(std::move(b));
+      } else {
+        drop = std::move(b);
+      }
+    }
+  }  // `drop` unmapped outside the lock
+  size_t trim() {
+    std::vector<std::unique_ptr<PartBuffer>> drop;
+    size_t freed;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      drop.swap(idle_);
+      freed = idle_bytes_;
+      idle_bytes_ = 0;
+    }
+    return freed;
+  }
+  void set_max_idle(size_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    max_idle_ = n;
+  }
+  RelayPoolStats stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    return RelayPoolStats{idle_.size(), idle_bytes_, in_use_, max_idle_};
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<std::unique_ptr<PartBuffer>> idle_;
+  size_t idle_bytes_ = 0, in_use_ = 0, max_idle_ = 16;
+};
+
+PartPool& part_pool() {
+  static PartPool* p = new PartPool();  // never destroyed: transfer threads may outlive exit
+  return *p;
+}
+
+struct PartLease {
+  std::unique_ptr<PartBuffer> b;
+  explicit PartLease(size_t n) : b(part_pool().acquire(n)) {}
+  ~PartLease() { part_pool().release(std::move(b)); }
 };
 }  // namespace
+
+size_t relay_pool_trim() { return part_pool().trim(); }
+void relay_pool_set_max_idle(size_t n) { part_pool().set_max_idle(n); }
+RelayPoolStats relay_pool_stats() { return part_pool().stats(); }
 
 int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
                                        int64_t full_len, int64_t piece_len, Progress* prog,
@@ -595,8 +677,8 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
   // it: the same two copies as the chunked path), then its pieces are hashed 16 at a time in
   // the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the per-core rate of a single SHA-NI
   // chain, which bounds the chunked path once many parts are in flight.
-  thread_local PartBuffer part;
-  uint8_t* b = part.get((size_t)n);
+  PartLease lease((size_t)n);
+  uint8_t* b = lease.b->data;
   int64_t pos = 0;
   while (pos < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {

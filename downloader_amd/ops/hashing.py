@@ -131,7 +131,13 @@ def verify_pieces(files: FileList, piece_len: int, hashes: bytes,
                   backend: str = "cpu") -> bytes:
     """One byte per piece (1 = SHA-1 matches). With ``which``, one byte per listed piece in
     list order. ``backend="auto"`` picks the GPU only for a whole-storage recheck; a subset
-    goes to the GPU when asked for explicitly (see ``GpuBatcher`` for the batched path)."""
+    goes to the GPU when asked for explicitly (see ``GpuBatcher`` for the batched path).
+    Only ``which=None`` asks for a full recheck: an empty ``which`` verifies nothing (the
+    native calls read an empty list as "every piece")."""
+    if which is not None:
+        which = [int(i) for i in which]
+        if not which:
+            return b""
     files = [(str(p), int(n)) for p, n in files]
     total = sum(n for _, n in files)
     n_pieces = (total + piece_len - 1) // piece_len if total else 0
@@ -144,9 +150,9 @@ def verify_pieces(files: FileList, piece_len: int, hashes: bytes,
         v = _verifier()
         with _gpu_call_lock:
             ok, _timing = v.verify_files_streamed(files, piece_len, hashes,
-                                                  which=list(which or []))
+                                                  which=which or [])
         return ok
-    return native().verify_pieces(files, piece_len, hashes, list(which or []), threads)
+    return native().verify_pieces(files, piece_len, hashes, which or [], threads)
 
 
 # One GpuVerifier per process owns two pinned slots and two streams: calls are serialised.
@@ -204,6 +210,11 @@ class GpuBatcher:
             key, batch = self._take()
             files, piece_len, hashes = key
             union = sorted({i for _, ps, _ in batch for i in ps})
+            if not union:           # nothing to verify (never a whole-storage recheck)
+                for _, _, fut in batch:
+                    if fut.set_running_or_notify_cancel():
+                        fut.set_result([])
+                continue
             try:
                 v = _verifier()
                 with _gpu_call_lock:

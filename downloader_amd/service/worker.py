@@ -240,7 +240,10 @@ class Worker:
         if drop or not jd.exclusive:
             reaper = get_reaper(self.services)
             if reaper.background:
-                reaper.reap(jd.path)
+                try:
+                    reaper.reap(jd.path)
+                except ValueError as e:
+                    job.logger.error("job dir not removed", err=str(e))
             else:
                 await loop.run_in_executor(None, jd.remove)
         jd.release()

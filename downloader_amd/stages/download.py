@@ -18,7 +18,7 @@ from ..models import api, keys
 from ..net.http import Progress
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket)
-from .jobdir import JobDir
+from .jobdir import JobDir, dir_name
 from .select import select_from_config
 
 Backend = Callable[[str, Job, str], Awaitable[None]]
@@ -40,7 +40,7 @@ class DownloadStage(Stage):
 
     def job_dir(self, job: Job) -> str:
         if not self.cfg.instance.per_attempt_dirs:
-            return os.path.join(str(self.root), job.id)   # reference layout, no locking
+            return os.path.join(str(self.root), dir_name(job.id))   # no locking
         if job.jobdir is None:
             job.jobdir = JobDir(str(self.root), job.id)
             job.jobdir.acquire()

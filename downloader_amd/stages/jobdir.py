@@ -13,6 +13,7 @@ take the lock works in a private ``<root>/<id>.<token>`` directory instead.
 from __future__ import annotations
 
 import fcntl
+import hashlib
 import os
 import secrets
 import shutil
@@ -20,11 +21,39 @@ import threading
 from concurrent.futures import Future, ThreadPoolExecutor, wait
 from typing import Optional, Set
 
+_NAME_MAX = 200          # bytes; leaves room for ".<token>" / ".lock" under NAME_MAX = 255
+
+
+def dir_name(job_id: str) -> str:
+    """Directory name of a job under the download root. ``media.id`` arrives in the queue
+    message, so it is untrusted: the reference's ``<root>/<id>`` layout is kept for plain ids,
+    while ids that could name the root itself, its parent, a nested path or one of our own
+    dot-directories (``''``, ``'.'``, ``'..'``, anything with ``/``, ``os.sep`` or NUL, or a
+    leading ``.``) - and over-long ids - get an encoded name (``%`` + hex of the UTF-8, or of
+    its SHA-256 when too long) that always stays one component strictly inside the root.
+    Plain ids never start with ``%``, so the two spaces cannot collide."""
+    raw = job_id.encode("utf-8", "surrogatepass")
+    plain = (job_id and not job_id.startswith((".", "%")) and "/" not in job_id
+             and os.sep not in job_id and "\0" not in job_id and len(raw) <= _NAME_MAX)
+    if plain:
+        return job_id
+    enc = raw.hex()
+    if len(enc) + 1 > _NAME_MAX:
+        enc = "h" + hashlib.sha256(raw).hexdigest()
+    return "%" + enc
+
+
+def inside(root: str, path: str) -> bool:
+    """True when ``path`` lies strictly below ``root`` (symlinks resolved)."""
+    r = os.path.realpath(root)
+    p = os.path.realpath(path)
+    return p != r and os.path.commonpath([r, p]) == r
+
 
 class JobDir:
     def __init__(self, root: str, job_id: str):
         self.root = root
-        self.job_id = job_id.replace("/", "_") or "_"
+        self.job_id = dir_name(job_id)
         self.path = ""
         self.exclusive = False
         self._fd: Optional[int] = None
@@ -56,7 +85,7 @@ class JobDir:
                 self._fd = None
 
     def remove(self) -> None:
-        if self.path:
+        if self.path and inside(self.root, self.path):
             shutil.rmtree(self.path, ignore_errors=True)
 
 
@@ -96,8 +125,15 @@ class Reaper:
             self.reaped += 1
 
     def reap(self, path: str) -> Optional[Future]:
+        """Remove one job directory. Only paths strictly inside the download root (and not
+        our own ``.trash`` / ``.locks``) are ever removed - never the root or anything above
+        it, whatever a job's id or a stage's result says."""
         if not path or not os.path.lexists(path):
             return None
+        if not inside(self.root, path) or os.path.realpath(path) in (
+                os.path.realpath(self.trash), os.path.realpath(os.path.join(self.root, ".locks"))):
+            raise ValueError(f"refusing to remove {path!r}: not a job directory under "
+                             f"{self.root!r}")
         if not self.background:
             shutil.rmtree(path, ignore_errors=True)
             return None

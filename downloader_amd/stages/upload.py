@@ -15,7 +15,6 @@ from __future__ import annotations
 
 import asyncio
 import os
-import shutil
 from typing import Any, Dict, List
 
 from ..models import keys
@@ -101,8 +100,8 @@ class UploadStage(Stage):
                     reaper.reap(download_path)    # rename now, unlink in the background
                 else:
                     await asyncio.get_running_loop().run_in_executor(
-                        None, shutil.rmtree, download_path)
-            except OSError as e:
+                        None, reaper.reap, download_path)
+            except (OSError, ValueError) as e:
                 job.logger.warn("err", f"failed to clean up directory: {e}")
         return {"files": files, "keys": sorted(owner), "bytes": sum(uploaded)}
 

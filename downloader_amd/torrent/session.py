@@ -739,19 +739,40 @@ class TorrentSession:
                 self._gpu_verify = False
         return self._gpu_verify
 
+    async def _host_verify(self, pieces: List[int]) -> List[bool]:
+        return await asyncio.get_running_loop().run_in_executor(
+            None, self.storage.verify, pieces, self.client.verify_threads)
+
     async def _webseed_verify(self, pieces: List[int], st: Dict[str, int]) -> None:
+        """Verify one fetched run. It runs as a plain task next to its stream, so nothing may
+        escape it: every error hands the pieces back to the picker (otherwise they stay
+        claimed and nobody fetches them again). A transient read error counts as a stream
+        failure; a verifier fault (HIP error, OOM, no device) falls back to the host under
+        ``verify_backend=auto`` and fails the session under an explicit ``gpu``."""
         t_verify = time.perf_counter()
         try:
             if self._use_gpu_verify():
-                fut = hashing.gpu_batcher().submit(self.storage.paths, self.meta.piece_length,
-                                                   self.meta.pieces, pieces)
-                ok = await asyncio.wrap_future(fut)
+                try:
+                    fut = hashing.gpu_batcher().submit(self.storage.paths, self.meta.piece_length,
+                                                       self.meta.pieces, pieces)
+                    ok = await asyncio.wrap_future(fut)
+                except OSError:
+                    raise
+                except Exception:
+                    if self.client.verify_backend == "gpu":
+                        raise
+                    self._gpu_verify = False          # auto: this session stays on the host
+                    ok = await self._host_verify(pieces)
             else:
-                ok = await asyncio.get_running_loop().run_in_executor(
-                    None, self.storage.verify, pieces, self.client.verify_threads)
+                ok = await self._host_verify(pieces)
         except OSError:
             self.picker.unclaim(pieces)
             st["failures"] += 1
+            return
+        except Exception as e:
+            self.picker.unclaim(pieces)
+            st["failures"] += 1
+            self.fail(TorrentError(f"piece verification failed: {e!r}"))
             return
         self.stats["webseed_verify_s"] += time.perf_counter() - t_verify
         for i, good in zip(pieces, ok):

@@ -85,6 +85,19 @@ class _Unit:
         return out
 
 
+_active_stagers = 0
+
+
+def _trim_relay_buffers() -> None:
+    """Unmap the idle pooled part buffers of the hashed relay once no stream staging runs in
+    this process (they are as large as a part, 64 MiB, one per relay that was in flight)."""
+    try:
+        from ..ops import native
+        native().relay_pool_trim()
+    except Exception:
+        pass
+
+
 def piece_split(meta: Metainfo, start: int, length: int) -> Tuple[int, int]:
     """(skip, full) of the torrent range [start, start+length): ``skip`` bytes before the
     first whole piece, then ``full`` bytes of whole pieces (the torrent's short last piece
@@ -135,6 +148,9 @@ class StreamStager:
         self._plan_gaps()
         self.verified: Set[int] = set()
         self._checking: Set[int] = set()
+        # boundary piece -> version of its fragment set, bumped whenever a fragment is
+        # stored, replaced or dropped: a check whose snapshot is stale does not count
+        self.frag_ver: Dict[int, int] = {}
         self.piece_fails: Dict[int, int] = {}
         self.total = sum(t.size for t in self.targets)
         self.fetched_bytes = 0
@@ -181,7 +197,9 @@ class StreamStager:
     async def run(self) -> List[dict]:
         """Stage every selected file; return the ``streamed`` entries (walk order, every
         selected file - the upload stage resolves key ownership) for the later stages."""
+        global _active_stagers
         multi = [t for t in self.targets if not t.single and t.size]
+        _active_stagers += 1
         try:
             for t in self.targets:
                 if t.size == 0:
@@ -213,6 +231,10 @@ class StreamStager:
         except BaseException:
             await asyncio.shield(self.abort())
             raise
+        finally:
+            _active_stagers -= 1
+            if _active_stagers == 0:
+                _trim_relay_buffers()         # munmap of <= max_idle parts: milliseconds
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
                  "virtual": True} for f in self.selected]
 
@@ -249,6 +271,7 @@ class StreamStager:
             for a, _ in r.fragments():               # its fragments are fetched again
                 p = a // self.plen
                 self.frags[p].pop(a, None)
+                self.frag_ver[p] = self.frag_ver.get(p, 0) + 1
                 self.verified.discard(p)
             if r.counted:
                 r.counted = False
@@ -296,6 +319,7 @@ class StreamStager:
         for a, data in pieces:
             p = a // self.plen
             self.frags[p][a] = data
+            self.frag_ver[p] = self.frag_ver.get(p, 0) + 1
             if await self._check_piece(p):
                 requeue += [self.units[i] for i in sorted(self.suppliers[p])]
         return requeue
@@ -344,29 +368,36 @@ class StreamStager:
 
     async def _check_piece(self, p: int) -> bool:
         """Verify boundary piece ``p`` once all its fragments are in; True = it failed. A
-        piece already being hashed (its last fragment arrived twice) is not checked again."""
-        got = self.frags[p]
-        lo, hi = self._piece_range(p)
-        if p in self.verified or p in self._checking or \
-                sum(len(b) for b in got.values()) != hi - lo:
-            return False
-        data = b"".join(got[a] for a in sorted(got))
-        self._checking.add(p)
-        try:
-            if len(data) >= 1 << 20:
-                digest = await asyncio.get_running_loop().run_in_executor(None, _sha1, data)
-            else:
-                digest = _sha1(data)
-        finally:
-            self._checking.discard(p)
-        if digest == self.meta.piece_hash(p):
-            self.verified.add(p)
-            return False
-        self.hash_fails += 1
-        self.piece_fails[p] = self.piece_fails.get(p, 0) + 1
-        if self.piece_fails[p] >= self.max_failures:
-            raise TorrentError(f"webseed served corrupt data for piece {p}")
-        return True
+        piece already being hashed (its last fragment arrived twice) is not checked again
+        here: the running check sees the version bump and re-checks. Large pieces are hashed
+        in an executor while the loop runs on, so ``_settle`` may drop or replace a fragment
+        meanwhile; the verdict only counts if the fragment set is still the hashed one."""
+        while True:
+            got = self.frags[p]
+            lo, hi = self._piece_range(p)
+            if p in self.verified or p in self._checking or \
+                    sum(len(b) for b in got.values()) != hi - lo:
+                return False
+            ver = self.frag_ver.get(p, 0)
+            data = b"".join(got[a] for a in sorted(got))
+            self._checking.add(p)
+            try:
+                if len(data) >= 1 << 20:
+                    digest = await asyncio.get_running_loop().run_in_executor(None, _sha1, data)
+                else:
+                    digest = _sha1(data)
+            finally:
+                self._checking.discard(p)
+            if self.frag_ver.get(p, 0) != ver:
+                continue                     # fragments changed while hashing: check again
+            if digest == self.meta.piece_hash(p):
+                self.verified.add(p)
+                return False
+            self.hash_fails += 1
+            self.piece_fails[p] = self.piece_fails.get(p, 0) + 1
+            if self.piece_fails[p] >= self.max_failures:
+                raise TorrentError(f"webseed served corrupt data for piece {p}")
+            return True
 
     async def abort(self) -> None:
         """Drop what a failed attempt staged: open multipart uploads, single-PUT objects."""

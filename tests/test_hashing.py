@@ -64,6 +64,24 @@ def test_verify_pieces_across_file_boundaries(tmp_path):
     # subset check
     sub = hashing.verify_pieces(files, piece, hashes, which=[0, bad_off // piece])
     assert sub == b"\x01\x00"
+    # an explicit empty subset verifies nothing (only which=None is a full recheck)
+    assert hashing.verify_pieces(files, piece, hashes, which=[]) == b""
+    assert hashing.verify_pieces(files, piece, hashes, which=(), backend="gpu") == b""
+
+
+def test_gpu_batcher_empty_batch_never_rechecks(monkeypatch):
+    calls = []
+
+    class V:
+        def verify_files_streamed(self, files, plen, hashes, which=()):
+            calls.append(list(which))
+            return b"\x01" * len(which), (0.0, 0.0)
+
+    monkeypatch.setattr(hashing, "_verifier", lambda: V())
+    b = hashing.GpuBatcher()
+    assert b.submit([("x", 10)], 4, b"\0" * 60, []).result(5) == []
+    assert b.submit([("x", 10)], 4, b"\0" * 60, [2]).result(5) == [True]
+    assert calls == [[2]]
 
 
 def test_verify_missing_file_reports_false(tmp_path):

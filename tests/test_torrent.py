@@ -483,6 +483,51 @@ def test_webseed_gpu_verify_path_through_batcher(run, tmp_path, origin_cls, monk
     run(go())
 
 
+@pytest.mark.parametrize("backend", ["gpu", "auto"])
+def test_webseed_verifier_fault_is_never_lost(run, tmp_path, origin_cls, monkeypatch, backend):
+    """The GPU verifier raises (HIP fault, OOM, no device) inside a run's verify task. Under
+    an explicit ``gpu`` the session fails at once with that error - the pieces are handed
+    back, nothing waits for the 240 s stall watchdog; under ``auto`` the run is verified on
+    the host instead and the job completes."""
+    from concurrent.futures import Future
+
+    from downloader_amd.ops import hashing
+
+    class Broken:
+        submitted = 0
+
+        def submit(self, files, plen, hashes, pieces):
+            Broken.submitted += 1
+            f: Future = Future()
+            f.set_exception(RuntimeError("hipErrorIllegalAddress"))
+            return f
+
+    monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    monkeypatch.setattr(hashing, "gpu_batcher", lambda: Broken())
+    monkeypatch.setattr(hashing, "_gpu_verifier", object())
+
+    async def go():
+        origin = await origin_cls().start()
+        src = tmp_path / "ws"
+        data = _tree(src / "Pack", {"a.mkv": 400_000})
+        raw = make_torrent(str(src / "Pack"), 65536, url_list=[origin.url("/seed/")])
+        origin.blobs["/seed/Pack/a.mkv"] = data["a.mkv"]
+        c = TorrentClient(webseed_chunk=131072, webseed_streams=2, verify_backend=backend)
+        await c.start()
+        s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
+        if backend == "auto":
+            s._gpu_verify = True          # as if the warm-verifier policy had picked the GPU
+            await asyncio.wait_for(s.wait(), 30)
+            _check(tmp_path / "dl", data)
+            assert s._gpu_verify is False and Broken.submitted >= 1
+        else:
+            with pytest.raises(TorrentError, match="hipErrorIllegalAddress"):
+                await asyncio.wait_for(s.wait(), 10)
+            assert not s.picker.claimed or all(i not in s.have for i in s.picker.claimed)
+        await c.close(); await origin.stop()
+    run(go())
+
+
 def test_webseed_serving_corrupt_data_fails_session(run, tmp_path, origin_cls):
     """A webseed that keeps serving a bad piece: the owning stream backs off, gives up after
     webseed_max_failures, and - with no peers/trackers/DHT - the session fails instead of

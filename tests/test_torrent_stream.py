@@ -154,6 +154,10 @@ def test_stream_matches_disk_path(run, tmp_path, make_cfg, origin_cls, plen):
             await w.stop()
         assert got["auto"] == got["off"]
         assert got["auto"]["Season 1/e1.mkv"] == data["Season 1/e1.mkv"]
+        # the hashed relay's pooled part buffers are all back and unmapped after the job
+        from downloader_amd.ops import native
+        pool = native().relay_pool_stats()
+        assert pool["in_use"] == 0 and pool["idle_bytes"] == 0, pool
         await s3.stop(); await origin.stop()
     run(go())
 
@@ -221,3 +225,63 @@ def test_settle_never_queues_a_unit_twice(tmp_path):
     st._settle(a, [], q)
     st._settle(b, [], q)
     assert st._outstanding == 0 and st._finished.is_set() and q.qsize() == 0
+
+
+def test_check_piece_discards_stale_verdict(run, tmp_path, monkeypatch):
+    """A 1 MiB boundary piece is hashed in an executor. While that hash runs, ``_settle``
+    requeues one supplier (dropping its fragment). The in-flight verdict is stale and must
+    not mark the piece verified: otherwise the supplier's re-fetched - here corrupt - bytes
+    would never be checked (version counter per piece)."""
+    import hashlib
+    import threading
+
+    from downloader_amd.torrent import stream as stream_mod
+    from downloader_amd.torrent.stream import StreamStager
+
+    plen = 1 << 20
+    data = os.urandom(3 * plen)
+    half = 3 * plen // 2
+    files = [FileEntry(["a.mkv"], half, 0), FileEntry(["b.mkv"], half, half)]
+    pieces = b"".join(hashlib.sha1(data[i:i + plen]).digest() for i in range(0, 3 * plen, plen))
+    m = Metainfo(b"x" * 20, "P", plen, pieces, files, 3 * plen, multi_file=True)
+    s3 = types.SimpleNamespace(multipart_threshold=1 << 30, plan_parts=lambda n: [(1, 0, n)])
+    root = str(tmp_path)
+    sel = [os.path.join(root, "P", "a.mkv"), os.path.join(root, "P", "b.mkv")]
+    st = StreamStager(m, types.SimpleNamespace(id="j"),
+                      types.SimpleNamespace(s3=types.SimpleNamespace(bucket="b")),
+                      types.SimpleNamespace(s3=s3), sel, root, ["http://x/"])
+    a, b = st.units
+    assert st.suppliers[1] == {a.uid, b.uid}
+    gate, entered = threading.Event(), threading.Event()
+    real = stream_mod._sha1
+
+    def slow_sha1(buf):
+        entered.set()
+        gate.wait(10)
+        return real(buf)
+
+    async def go():
+        q = asyncio.Queue()
+        st._outstanding = 2
+        a.state, b.state = "done", "running"
+        st.frags[1][plen] = data[plen:half]                 # a's tail
+        st.frags[1][half] = data[half:2 * plen]             # b's head
+        st.frag_ver[1] = 2
+        monkeypatch.setattr(stream_mod, "_sha1", slow_sha1)
+        chk = asyncio.ensure_future(st._check_piece(1))
+        while not entered.is_set():
+            await asyncio.sleep(0.005)
+        st._settle(b, [b], q)                               # b's fragment dropped mid-hash
+        gate.set()
+        assert await chk is False and 1 not in st.verified
+        monkeypatch.setattr(stream_mod, "_sha1", real)
+        bad = bytearray(data[half:2 * plen])
+        bad[7] ^= 0xFF
+        st.frags[1][half] = bytes(bad)                      # the re-fetch brings bad bytes
+        st.frag_ver[1] += 1
+        assert await st._check_piece(1) is True             # ... and they ARE checked
+        assert 1 not in st.verified and st.hash_fails == 1
+        st.frags[1][half] = data[half:2 * plen]
+        st.frag_ver[1] += 1
+        assert await st._check_piece(1) is False and 1 in st.verified
+    run(go())

@@ -6,6 +6,7 @@ import asyncio
 import base64
 import os
 
+import pytest
 
 from downloader_amd.broker.memory import MemoryBroker
 from downloader_amd.models import api, keys
@@ -442,5 +443,60 @@ def test_signed_payload_staging(run, make_cfg, origin_cls):
         assert w.results[0].outcome == "staged", w.results[0]
         key = "sig1/original/" + base64.b64encode(b"signed.mkv").decode()
         assert s3.get("triton-staging", key) == blob
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_job_dir_names_stay_inside_the_root(tmp_path):
+    """media.id comes from the queue: '', '.', '..', ids with '/' or NUL, dot-ids (which
+    could hit .locks / .trash) and over-long ids get an encoded single component; plain ids
+    keep the reference layout <root>/<id>."""
+    from downloader_amd.stages.jobdir import JobDir, Reaper, dir_name, inside
+    root = tmp_path / "dl"
+    root.mkdir()
+    assert dir_name("job1") == "job1" and dir_name("Some Movie (2019)") == "Some Movie (2019)"
+    seen = set()
+    for bad in ("", ".", "..", "../x", "a/b", "/", "x\0y", ".trash", ".locks", "%41",
+                "é" * 300):
+        n = dir_name(bad)
+        assert n.startswith("%") and "/" not in n and "\0" not in n and len(n) <= 200, n
+        assert n not in seen
+        seen.add(n)
+        jd = JobDir(str(root), bad)
+        p = jd.acquire()
+        assert inside(str(root), p) and os.path.dirname(p) == str(root)
+        jd.release()
+    # the reaper never removes the root, its parent or its own bookkeeping dirs
+    (root / "other").mkdir()
+    r = Reaper(str(root), background=False)
+    for p in (str(root), str(tmp_path), str(root / "."), str(root / ".."),
+              str(root / ".locks"), str(root / ".trash")):
+        os.makedirs(root / ".trash", exist_ok=True)
+        with pytest.raises(ValueError):
+            r.reap(p)
+    assert (root / "other").is_dir() and (root / ".locks").is_dir()
+    jd = JobDir(str(root), "..")
+    jd.path = str(root)          # a corrupted path is still not removed
+    jd.remove()
+    assert (root / "other").is_dir()
+
+
+def test_dotdot_job_id_does_not_wipe_other_jobs(run, make_cfg, origin_cls, tmp_path):
+    """A job whose id is '..' stages normally and its cleanup removes only its own dir."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls)
+        keep = tmp_path / "dl" / "other-job"
+        keep.mkdir(parents=True)
+        (keep / "x.mkv").write_bytes(b"x")
+        origin.blobs["/d.mkv"] = os.urandom(100_000)
+        for jid in ("..", "."):
+            await w.submit(api.make_download(jid, "http", origin.url("/d.mkv")))
+        await _wait(w, 2)
+        assert [r.outcome for r in w.results] == ["staged", "staged"], w.results
+        reaper = w.services.extra.get("reaper")
+        if reaper is not None:
+            assert reaper.drain(10)
+        assert (keep / "x.mkv").read_bytes() == b"x"
+        assert (tmp_path / "dl").is_dir()
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
