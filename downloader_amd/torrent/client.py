@@ -114,7 +114,7 @@ class TorrentClient:
 
     async def add_magnet(self, m: Magnet, root: str) -> TorrentSession:
         s = self._register(TorrentSession(self, m.info_hash, root, None, m.trackers, m.webseeds,
-                                          m.peers, m.name))
+                                          m.peers, m.name, m.exact_sources))
         await s.start()
         return s
 

@@ -1,7 +1,9 @@
 """Magnet URIs (BEP-9) - replaces ``magnet-uri@5`` (yarn.lock:2040).
 
-``xt=urn:btih:<40 hex | 32 base32>``, ``dn`` display name, ``tr`` trackers, ``ws`` webseeds
-(BEP-19), ``x.pe`` peer addresses, ``xl`` exact length."""
+``xt=urn:btih:<40 hex | 32 base32>``, ``dn`` display name, ``tr`` trackers, ``ws`` and ``as``
+webseeds (BEP-19; magnet-uri folds both into ``urlList``), ``xs`` exact sources (URLs of the
+``.torrent`` itself, which webtorrent fetches for the metadata before asking peers), ``x.pe``
+peer addresses, ``xl`` exact length, ``kt`` keywords."""
 from __future__ import annotations
 
 import base64
@@ -22,6 +24,8 @@ class Magnet:
     webseeds: List[str] = field(default_factory=list)
     peers: List[Tuple[str, int]] = field(default_factory=list)
     exact_length: Optional[int] = None
+    exact_sources: List[str] = field(default_factory=list)
+    keywords: List[str] = field(default_factory=list)
 
     def to_uri(self) -> str:
         parts = [f"xt=urn:btih:{self.info_hash.hex()}"]
@@ -29,6 +33,7 @@ class Magnet:
             parts.append("dn=" + quote(self.name))
         parts += ["tr=" + quote(t, safe="") for t in self.trackers]
         parts += ["ws=" + quote(w, safe="") for w in self.webseeds]
+        parts += ["xs=" + quote(x, safe="") for x in self.exact_sources]
         parts += [f"x.pe={h}:{p}" for h, p in self.peers]
         return "magnet:?" + "&".join(parts)
 
@@ -67,15 +72,20 @@ def parse_magnet(uri: str) -> Magnet:
     ih = None
     m = Magnet(b"")
     for k, v in parse_qsl(u.query, keep_blank_values=True):
-        k = k.split(".", 1)[0] if k.startswith(("xt.", "tr.", "ws.")) else k
+        k = k.split(".", 1)[0] if k.startswith(("xt.", "tr.", "ws.", "as.", "xs.")) else k
         if k == "xt" and v.lower().startswith("urn:btih:") and ih is None:
             ih = parse_btih(v[9:])
         elif k == "dn":
             m.name = v
         elif k == "tr":
             m.trackers.append(v)
-        elif k == "ws":
-            m.webseeds.append(v)
+        elif k in ("ws", "as"):
+            if v not in m.webseeds:
+                m.webseeds.append(v)
+        elif k == "xs":
+            m.exact_sources.append(v)
+        elif k == "kt":
+            m.keywords += v.replace("+", " ").split()
         elif k == "x.pe":
             hp = _hostport(v)
             if hp:

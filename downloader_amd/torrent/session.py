@@ -10,7 +10,8 @@ Replaces webtorrent's ``Torrent`` (reference: ``client.add(magnet, {path}, cb)``
   Range GETs spliced directly into the files (native transport), then verified in place by the
   threaded native SHA-1; failed pieces are released back to the picker.
 
-Metadata for magnets is fetched with ut_metadata (BEP-9) and checked against the infohash.
+Metadata for magnets is fetched with ut_metadata (BEP-9) - or from the magnet's ``xs`` exact
+sources over HTTP, as webtorrent does - and checked against the infohash.
 """
 from __future__ import annotations
 
@@ -256,7 +257,8 @@ class MetadataFetch:
 
 class TorrentSession:
     def __init__(self, client: "TorrentClient", info_hash: bytes, root: str,
-                 meta: Optional[Metainfo] = None, trackers=(), webseeds=(), peers=(), name: str = ""):
+                 meta: Optional[Metainfo] = None, trackers=(), webseeds=(), peers=(), name: str = "",
+                 exact_sources=()):
         self.client = client
         self.info_hash = info_hash
         self.root = root
@@ -264,6 +266,8 @@ class TorrentSession:
         self.name = name
         self.trackers: List[str] = [t for t in trackers if tracker_supported(t)]
         self.webseeds: List[str] = list(webseeds)
+        self.exact_sources: List[str] = [x for x in exact_sources
+                                          if x.startswith(("http://", "https://"))]
         self.known: Dict[Peer, float] = {}
         self.failed_peers: Dict[Peer, Tuple[int, float]] = {}
         self.peers: Dict[int, PeerConn] = {}
@@ -318,6 +322,8 @@ class TorrentSession:
         if self.meta is not None:
             await self._init_storage()
         self._spawn(self._connector())
+        if self.meta is None and self.exact_sources:
+            self._spawn(self._xs_fetch())
         for t in self.trackers:
             self._spawn(self._announce_loop(t))
         if self.client.dht is not None and not (self.meta and self.meta.private):
@@ -594,6 +600,31 @@ class TorrentSession:
         self.meta = m
         self.name = m.name
         await self._init_storage()
+
+    async def _xs_fetch(self) -> None:
+        """Magnet ``xs``: fetch the ``.torrent`` from each exact source in turn while peers
+        are asked over ut_metadata; the first file whose info dict hashes to the magnet's
+        infohash wins. A source that fails or serves another torrent is skipped."""
+        from ..fetch.http import fetch_bytes
+        from .metainfo import parse_torrent
+        for url in self.exact_sources:
+            if self.meta is not None or self._closed:
+                return
+            try:
+                m = parse_torrent(await fetch_bytes(self.client.transports, url))
+            except Exception:
+                continue
+            if m.info_hash == self.info_hash and self.meta is None:
+                # the .torrent may carry trackers / webseeds the magnet did not list
+                new = [t for t in m.trackers() if t not in self.trackers and tracker_supported(t)]
+                self.trackers += new
+                for t in new:
+                    self._spawn(self._announce_loop(t))
+                for w in m.url_list:
+                    if w not in self.webseeds:
+                        self.webseeds.append(w)
+                await self.set_metadata(m.raw_info)
+                return
 
     # ---------------------------------------------------------------- PEX (BEP-11)
     def on_pex(self, pc: PeerConn, d) -> None:

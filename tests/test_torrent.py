@@ -99,6 +99,12 @@ def test_magnet_parse():
     assert parse_magnet(Magnet(ih, "n", ["http://t"]).to_uri()).trackers == ["http://t"]
     with pytest.raises(MagnetError):
         parse_magnet("magnet:?dn=x")
+    # magnet-uri folds ``as`` into the webseed list; ``xs`` = .torrent exact sources
+    m = parse_magnet(f"magnet:?xt=urn:btih:{ih.hex()}&as=http%3A%2F%2Fa%2F&ws=http%3A%2F%2Fa%2F"
+                     f"&xs=http%3A%2F%2Fo%2Fx.torrent&kt=movie+2019")
+    assert m.webseeds == ["http://a/"] and m.exact_sources == ["http://o/x.torrent"]
+    assert m.keywords == ["movie", "2019"]
+    assert parse_magnet(m.to_uri()).exact_sources == ["http://o/x.torrent"]
 
 
 def test_http_and_udp_tracker(run):
@@ -155,6 +161,32 @@ def test_magnet_metadata_over_peers(run, tmp_path):
         assert s.meta.info_hash == m.info_hash
         _check(tmp_path / "dl", data)
         await leech.close(); await seeder.close()
+    run(go())
+
+
+def test_magnet_metadata_from_exact_source(run, tmp_path, origin_cls):
+    """A magnet with no peers, trackers or DHT but an ``xs`` URL: the .torrent is fetched over
+    HTTP (a first source serving ANOTHER torrent is skipped), its webseeds are adopted, and
+    the payload arrives from them (webtorrent's exact-source path)."""
+    async def go():
+        origin = await origin_cls().start()
+        src = tmp_path / "ws"
+        data = _tree(src / "Pack", {"a.mkv": 300_000})
+        raw = make_torrent(str(src / "Pack"), 65536, url_list=[origin.url("/seed/")])
+        other = make_torrent(str(src / "Pack"), 32768)
+        origin.blobs["/seed/Pack/a.mkv"] = data["a.mkv"]
+        origin.blobs["/t/other.torrent"] = other
+        origin.blobs["/t/pack.torrent"] = raw
+        m = parse_torrent(raw)
+        c = await TorrentClient(webseed_chunk=65536, webseed_streams=2).start()
+        mag = Magnet(m.info_hash, exact_sources=[origin.url("/t/missing.torrent"),
+                                                 origin.url("/t/other.torrent"),
+                                                 origin.url("/t/pack.torrent")])
+        s = await c.add_magnet(parse_magnet(mag.to_uri()), str(tmp_path / "dl"))
+        await asyncio.wait_for(s.wait(), 30)
+        assert s.meta.info_hash == m.info_hash and s.webseed_bytes == 300_000
+        _check(tmp_path / "dl", data)
+        await c.close(); await origin.stop()
     run(go())
 
 
