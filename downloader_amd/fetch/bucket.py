@@ -15,6 +15,7 @@ from dataclasses import dataclass
 from typing import List, Optional
 
 from ..models.keys import node_join
+from ..stages.jobdir import inside
 from ..utils.log import Logger, NullLogger
 
 
@@ -60,7 +61,7 @@ async def fetch_bucket(uri: str, download_dir: str, secure: bool = True, concurr
 
         async def one(name: str) -> None:
             dst = local_name(download_dir, name, src.sub_folder)
-            if not os.path.abspath(dst).startswith(os.path.abspath(download_dir)):
+            if not inside(download_dir, dst):   # '../job2/x' must not reach a sibling dir
                 raise ValueError(f"object {name!r} escapes the download directory")
             async with sem:
                 log.info(f"Downloading file '{name}' from bucket '{src.bucket}' to '{dst}'")

@@ -31,7 +31,12 @@ class HttpDownloadError(Exception):
 
 
 def output_name(url: str) -> str:
+    """``basename(new URL(url).pathname)`` (lib/download.js:139-141). The WHATWG parser drops
+    ``.`` / ``..`` segments (also as ``%2e``), so Node never yields them as a basename: a path
+    that ends in one resolves to a directory, i.e. an empty name -> ``index`` here."""
     name = posixpath.basename(urlsplit(url).path)
+    if name.lower().replace("%2e", ".") in (".", ".."):
+        name = ""
     return name or "index"
 
 

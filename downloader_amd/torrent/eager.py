@@ -117,9 +117,15 @@ class EagerUploader:
                                                              FileRange(f.fd, off, ln))
                 self.uploaded_bytes += ln
                 self.upload_s += time.perf_counter() - t0
-        except BaseException as e:  # surfaced by finish()
+        except asyncio.CancelledError:
+            raise                     # abort(): the job is being torn down already
+        except BaseException as e:
+            # Surfaced by finish(), and at once through the session: without that a part
+            # that failed early (S3 down, 4xx) would only fail the job after the rest of a
+            # possibly multi-GB torrent had been downloaded for nothing.
             if self.error is None:
                 self.error = e
+                self.s.fail(e)
 
     async def finish(self) -> List[dict]:
         """After the download completed: send whatever is left, complete every multipart

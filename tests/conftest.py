@@ -53,6 +53,18 @@ class Origin:
             body = body[:i] + bytes([body[i] ^ 0xFF]) + body[i + 1:]
         return body
 
+    async def _trickle(self, req, status, body, hdrs):
+        from aiohttp import web
+        rate = self.slow[req.path]
+        resp = web.StreamResponse(status=status,
+                                  headers=dict(hdrs, **{"Content-Length": str(len(body))}))
+        await resp.prepare(req)
+        step = max(1, int(rate / 20))
+        for i in range(0, len(body), step):
+            await resp.write(body[i:i + step])
+            await asyncio.sleep(0.05)
+        return resp
+
     async def start(self):
         from aiohttp import web
 
@@ -72,8 +84,10 @@ class Origin:
                 a, _, b = rng[6:].partition("-")
                 s, e = int(a), int(b) if b else len(data) - 1
                 hdrs["Content-Range"] = f"bytes {s}-{e}/{len(data)}"
-                return web.Response(status=206, body=self._body(req.path, data, s, e),
-                                    headers=hdrs)
+                body = self._body(req.path, data, s, e)
+                if req.path in self.slow:
+                    return await self._trickle(req, 206, body, hdrs)
+                return web.Response(status=206, body=body, headers=hdrs)
             if req.method == "HEAD":
                 hdrs["Content-Length"] = str(len(data))
                 return web.Response(status=200, headers=hdrs)
@@ -84,14 +98,7 @@ class Origin:
                 req.transport.close()
                 return resp
             if req.path in self.slow:            # trickle the body at `slow[path]` bytes/s
-                rate = self.slow[req.path]
-                resp = web.StreamResponse(status=200, headers={"Content-Length": str(len(data))})
-                await resp.prepare(req)
-                step = max(1, int(rate / 20))
-                for i in range(0, len(data), step):
-                    await resp.write(data[i:i + step])
-                    await asyncio.sleep(0.05)
-                return resp
+                return await self._trickle(req, 200, data, {})
             if req.path in self.chunked:
                 resp = web.StreamResponse(status=200)
                 resp.enable_chunked_encoding()

@@ -452,6 +452,40 @@ def test_worker_torrent_eager_upload_collision_and_parts(run, tmp_path, make_cfg
     run(go())
 
 
+def test_eager_upload_failure_fails_the_job_before_the_download_ends(run, tmp_path, make_cfg,
+                                                                     origin_cls):
+    """An eager part upload that fails for good (S3 403) fails the job at once; the rest of
+    the torrent is not downloaded first (ADVICE-style audit: errors were only surfaced by
+    finish(), after the whole payload had arrived)."""
+    async def go():
+        import time as _time
+
+        from downloader_amd.models import api
+        from downloader_amd.s3.fake_server import FakeS3, FaultRule
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src"
+        data = _tree(src / "Show", {"Season 1/a.mkv": 1_000_000, "Season 1/b.mkv": 8_000_000})
+        for rel, d in data.items():
+            origin.blobs["/ws/Show/" + rel] = d
+        origin.slow["/ws/Show/Season 1/b.mkv"] = 200_000       # b alone takes ~10 s
+        raw = make_torrent(str(src / "Show"), 65536, url_list=[origin.url("/ws/")])
+        origin.blobs["/t/s.torrent"] = raw
+        s3.faults.add(FaultRule(method="PUT", path_contains="/eg2/", times=100, status=403,
+                                code="AccessDenied"))
+        w = _worker(make_cfg, ep, download={"torrent_stream": "off", "webseed_chunk": 262144},
+                    broker={"max_retries": 0})
+        await w.start(health=False)
+        t0 = _time.perf_counter()
+        await w.submit(api.make_download("eg2", "http", origin.url("/t/s.torrent"), "TV"))
+        await _wait_results(w)
+        assert w.results[0].outcome == "dead", w.results[0]
+        assert _time.perf_counter() - t0 < 3.0
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
 def test_webseed_claims_spread_over_files():
     """Streams prefer runs in files no other stream is writing (one file's page-cache write
     path serialises), and fall back to any free run."""

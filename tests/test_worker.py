@@ -500,3 +500,29 @@ def test_dotdot_job_id_does_not_wipe_other_jobs(run, make_cfg, origin_cls, tmp_p
         assert (tmp_path / "dl").is_dir()
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_source_names_cannot_leave_the_job_dir(run, tmp_path):
+    """bucket:// object names are joined under the job dir: '../<sibling>/x' passes a plain
+    string-prefix check ('/dl/job' is a prefix of '/dl/job2') and must still be refused. An
+    HTTP URL path ending in '..' names no file (Node's URL parser drops the segment)."""
+    from downloader_amd.fetch.bucket import fetch_bucket
+    from downloader_amd.fetch.http import output_name
+
+    assert output_name("http://h/a/..") == "index" and output_name("http://h/a/%2E%2e") == "index"
+    assert output_name("http://h/a/.") == "index" and output_name("http://h/x/m.mkv?q") == "m.mkv"
+
+    async def go():
+        s3 = FakeS3()
+        await s3.start()
+        s3.buckets["src"] = {}
+        s3.put("src", "show/../job2/evil.mkv", b"evil")
+        job = tmp_path / "dl" / "job"
+        (tmp_path / "dl" / "job2").mkdir(parents=True)
+        job.mkdir()
+        uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,show"
+        with pytest.raises(ValueError, match="escapes"):
+            await fetch_bucket(uri, str(job), secure=False)
+        assert not (tmp_path / "dl" / "job2" / "evil.mkv").exists()
+        await s3.stop()
+    run(go())
