@@ -10,7 +10,6 @@ first occurrence only). The reference fetches objects one by one; here up to
 from __future__ import annotations
 
 import asyncio
-import os
 from dataclasses import dataclass
 from typing import List, Optional
 
