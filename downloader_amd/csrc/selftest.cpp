@@ -20,6 +20,7 @@
 #include <functional>
 #include <random>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -232,6 +233,52 @@ int main() {
     CHECK(moved == (int64_t)body.size() && p.status == 200);
     dst.read_body(p, 16);
     CHECK(sunk == (int64_t)body.size());
+  }
+  // ---- hashed relay, 4 threads at once: the chunked single-chain path (< 8 pieces) and the
+  // pooled multi-buffer path (>= 8 pieces; buffers shared through the process-wide pool)
+  for (int64_t plen : {(int64_t)1 << 18, (int64_t)1 << 16}) {
+    const int64_t skip = 1000, n = (int64_t)body.size();
+    const int64_t full = ((n - skip) / plen) * plen;   // whole pieces, then a tail fragment
+    std::string want = hash_pieces("sha1", body.data() + skip, (size_t)full, (size_t)plen, 1);
+    std::vector<std::thread> ths;
+    std::atomic<int> good{0};
+    for (int t = 0; t < 4; ++t) {
+      ths.emplace_back([&] {
+        Server origin([&](int fd) {
+          read_head(fd);
+          send_str(fd, "HTTP/1.1 206 Partial Content\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+          send_str(fd, std::string((const char*)body.data(), body.size()));
+        });
+        int64_t sunk = 0;
+        Server sink([&](int fd) {
+          read_head(fd);
+          sunk = drain_body(fd, n);
+          send_str(fd, "HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n");
+        });
+        HttpConn src("127.0.0.1", origin.port, 5, 5), dst("127.0.0.1", sink.port, 5, 5);
+        src.send_request("GET /h HTTP/1.1\r\nHost: x\r\n\r\n", nullptr, 0);
+        ResponseHead g = src.read_head();
+        dst.send_raw("PUT /h HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+        std::string digests, head, tail;
+        int64_t moved = src.relay_body_hashed(dst, g.content_length, skip, full, plen, nullptr,
+                                              &digests, &head, &tail);
+        ResponseHead p = dst.read_head();
+        dst.read_body(p, 16);
+        bool ok = moved == n && p.status == 200 && digests == want &&
+                  head == std::string((const char*)body.data(), (size_t)skip) &&
+                  tail == std::string((const char*)body.data() + skip + full, (size_t)(n - skip - full));
+        if (ok) good.fetch_add(1);
+        (void)sunk;
+      });
+    }
+    for (auto& th : ths) th.join();
+    CHECK(good.load() == 4);
+  }
+  {
+    RelayPoolStats st = relay_pool_stats();
+    CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);
+    relay_pool_trim();
+    CHECK(relay_pool_stats().idle_bytes == 0);
   }
   unlink(fa.c_str());
   unlink(fb.c_str());

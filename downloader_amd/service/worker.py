@@ -56,6 +56,16 @@ class JobResult:
     stats: dict = field(default_factory=dict)   # the job's stats (stage timings, torrent, ...)
 
 
+def _attempt(headers: Dict[str, Any]) -> int:
+    """``x-attempt`` of a delivery. Headers come from whoever published the message: a value
+    that is not a small non-negative integer counts as attempt 0 instead of raising before
+    the delivery is acked or nacked (which would leave it stuck unacked)."""
+    try:
+        return max(0, min(1 << 20, int(headers.get("x-attempt", 0) or 0)))
+    except (TypeError, ValueError, OverflowError):
+        return 0
+
+
 class Worker:
     def __init__(self, cfg: Config, broker: Optional[Broker] = None,
                  s3: Optional[S3Client] = None, transports: Optional[TransportSet] = None,
@@ -168,7 +178,7 @@ class Worker:
             return self._finish(None, JobResult("", "dead", time.perf_counter() - t0, error=str(e)))
         media = msg.media
         job_id, creator = media.id, media.creatorId
-        attempt = int(d.headers.get("x-attempt", 0) or 0)
+        attempt = _attempt(d.headers)
         child = self.log.child(jobId=job_id, fileId=creator)
         self._seq += 1
         slot = self._seq

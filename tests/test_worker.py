@@ -268,9 +268,13 @@ def test_unsupported_protocol_and_bad_message(run, make_cfg, origin_cls):
         d.media.sourceURI = "bucket://nope"
         await w.submit(d)
         await b.publish("v1.download", b"\xff\xff\xff garbage")
-        await _wait(w, 2)
+        # a publisher's junk x-attempt header is attempt 0, not a stuck unacked delivery
+        origin.blobs["/ok.mkv"] = b"m" * 1000
+        await w.submit(api.make_download("j13", "http", origin.url("/ok.mkv")),
+                       {"x-attempt": "not-a-number"})
+        await _wait(w, 3)
         outs = sorted(r.outcome for r in w.results)
-        assert outs == ["dead", "dead"]
+        assert outs == ["dead", "dead", "staged"]
         assert len(b.drain("v1.download.dead")) == 2
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
