@@ -86,16 +86,34 @@ class _Unit:
 
 
 _active_stagers = 0
+_trim_handle: Optional[asyncio.TimerHandle] = None
 
 
 def _trim_relay_buffers() -> None:
-    """Unmap the idle pooled part buffers of the hashed relay once no stream staging runs in
-    this process (they are as large as a part, 64 MiB, one per relay that was in flight)."""
+    """Unmap the idle pooled part buffers of the hashed relay (as large as a part, one per
+    relay that was in flight) - unless stream staging started again meanwhile."""
+    global _trim_handle
+    _trim_handle = None
+    if _active_stagers:
+        return
     try:
         from ..ops import native
         native().relay_pool_trim()
     except Exception:
         pass
+
+
+def _schedule_trim(idle_s: float) -> None:
+    """Last stream stager of the process finished: trim after ``idle_s`` quiet seconds (0 =
+    now), so back-to-back jobs keep reusing warm buffers while an idle worker holds none."""
+    global _trim_handle
+    if _trim_handle is not None:
+        _trim_handle.cancel()
+        _trim_handle = None
+    if idle_s <= 0:
+        _trim_relay_buffers()
+    else:
+        _trim_handle = asyncio.get_running_loop().call_later(idle_s, _trim_relay_buffers)
 
 
 def piece_split(meta: Metainfo, start: int, length: int) -> Tuple[int, int]:
@@ -122,6 +140,8 @@ class StreamStager:
         self.plen = meta.piece_length
         self.parallel = max(1, parallel)
         self.max_failures = max(1, max_failures)
+        self.trim_idle_s = float(getattr(getattr(cfg, "download", None),
+                                         "relay_pool_idle_trim_s", 0.0) or 0.0)
         index = {os.path.abspath(p): i for i, (p, _) in enumerate(meta.local_files(root))}
         self.selected = [os.path.abspath(f) for f in selected]
         self.sizes = {f: meta.files[index[f]].length for f in self.selected}
@@ -234,7 +254,7 @@ class StreamStager:
         finally:
             _active_stagers -= 1
             if _active_stagers == 0:
-                _trim_relay_buffers()         # munmap of <= max_idle parts: milliseconds
+                _schedule_trim(self.trim_idle_s)
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
                  "virtual": True} for f in self.selected]
 

@@ -104,6 +104,10 @@ class DownloadConfig(BaseModel):
     # only (a retry takes the disk path with every source); always: whenever webseeds exist.
     torrent_stream: Literal["auto", "always", "off"] = "auto"
     torrent_stream_parallel: int = 16           # parts (Range GETs) in flight per job
+    # idle seconds after the last stream-staged job before the hashed relay's pooled part
+    # buffers (one per part in flight, up to 64 MiB each) are unmapped; back-to-back jobs
+    # reuse them without re-faulting ~1 GiB
+    relay_pool_idle_trim_s: float = 5.0
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"

@@ -138,7 +138,8 @@ def test_stream_matches_disk_path(run, tmp_path, make_cfg, origin_cls, plen):
         data, _ = await _show(tmp_path, origin, plen)
         got = {}
         for mode in ("auto", "off"):
-            w = _worker(make_cfg, ep, download={"torrent_stream": mode})
+            w = _worker(make_cfg, ep, download={"torrent_stream": mode,
+                                                "relay_pool_idle_trim_s": 0.3})
             await w.start(health=False)
             jid = f"cmp-{mode}"
             await w.submit(api.make_download(jid, "http", origin.url("/t/show.torrent"), "TV"))
@@ -154,10 +155,13 @@ def test_stream_matches_disk_path(run, tmp_path, make_cfg, origin_cls, plen):
             await w.stop()
         assert got["auto"] == got["off"]
         assert got["auto"]["Season 1/e1.mkv"] == data["Season 1/e1.mkv"]
-        # the hashed relay's pooled part buffers are all back and unmapped after the job
+        # the hashed relay's pooled part buffers are all back after the job, and unmapped
+        # once the worker has been idle for relay_pool_idle_trim_s
         from downloader_amd.ops import native
         pool = native().relay_pool_stats()
-        assert pool["in_use"] == 0 and pool["idle_bytes"] == 0, pool
+        assert pool["in_use"] == 0, pool
+        await asyncio.sleep(0.5)
+        assert native().relay_pool_stats()["idle_bytes"] == 0
         await s3.stop(); await origin.stop()
     run(go())
 
