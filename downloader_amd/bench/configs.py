@@ -181,6 +181,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             # --reps: the same torrent staged again under a fresh media id (no done marker,
             # so every rep does the full job); one job is a sub-second sample on this box.
             reps = []
+            rss0 = _rss_mb()["rss_MB"]
             for k in range(max(1, getattr(a, "reps", 1))):
                 suffix = f"-r{k}" if k else ""
                 m = api.make_download(f"c{cfg_no}-{a.mode}{suffix}", "http",
@@ -218,7 +219,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "eager_upload_s": r[0].stats.get("eager_upload_s"),
             "cleanup_after_job_s": round(cleanup_s, 3),
             "worker_cpu_s": round(cpu_s, 2), "peer_cpu_s": round(peer_cpu_s, 2),
-            "worker_rss_after_MB": rss["rss_MB"], "worker_rss_peak_MB": rss["rss_peak_MB"],
+            "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"], "worker_rss_peak_MB": rss["rss_peak_MB"],
             "relay_pool_after": pool,
             "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps]}
 
