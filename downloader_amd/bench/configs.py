@@ -219,7 +219,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "eager_upload_s": r[0].stats.get("eager_upload_s"),
             "cleanup_after_job_s": round(cleanup_s, 3),
             "worker_cpu_s": round(cpu_s, 2), "peer_cpu_s": round(peer_cpu_s, 2),
-            "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"], "worker_rss_peak_MB": rss["rss_peak_MB"],
+            "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"],
+            "worker_rss_peak_MB": rss["rss_peak_MB"],
             "relay_pool_after": pool,
             "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps]}
 

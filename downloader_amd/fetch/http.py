@@ -58,17 +58,17 @@ async def _watch(progress: Progress, min_rate: float, window: float, task: async
             last_b, last_t = b, now
 
 
-async def probe(t: TransportSet, url: str) -> Tuple[int, bool]:
-    """HEAD -> (content_length or -1, accepts byte ranges)."""
+async def probe(t: TransportSet, url: str) -> Tuple[int, bool, str]:
+    """HEAD (redirects followed) -> (content_length or -1, accepts byte ranges, final URL)."""
     try:
         r = await t.request("HEAD", url, expect_body=False)
     except Exception:
-        return -1, False
+        return -1, False, url
     if not r.ok:
-        return -1, False
+        return -1, False, url
     cl = r.header("content-length")
     return (int(cl) if cl and cl.isdigit() else -1,
-            (r.header("accept-ranges") or "").lower() == "bytes")
+            (r.header("accept-ranges") or "").lower() == "bytes", r.url or url)
 
 
 async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
@@ -83,7 +83,7 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     supports ``Range``. A complete ``path`` of the advertised size is reused as is."""
     log = logger or NullLogger()
     progress = progress or Progress()
-    size, ranges = await probe(t, url)
+    size, ranges, url = await probe(t, url)    # later GETs go straight to the final URL
     if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
         log.info("resume: file already complete", path=path)
         return 0

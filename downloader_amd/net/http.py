@@ -10,6 +10,11 @@ Two implementations behind one async interface:
 
 A request body is ``bytes`` or a ``FileRange``; a response body is returned in memory or
 written into a ``FileSink``.
+
+Redirects: the reference fetches with ``request`` (npm), which follows up to 10 redirects of a
+GET/HEAD (``followRedirect``; other methods are not redirected) and drops ``Authorization``
+when the host changes. ``TransportSet.request`` and ``NativeTransport.relay`` do the same;
+``Response.url`` is the URL that finally answered. A 3xx body is never written into a sink.
 """
 from __future__ import annotations
 
@@ -19,9 +24,12 @@ import threading
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
-from urllib.parse import urlsplit
+from urllib.parse import quote, urljoin, urlsplit
 
 Headers = Sequence[Tuple[str, str]]
+
+REDIRECTS = (301, 302, 303, 307, 308)
+MAX_REDIRECTS = 10          # request@2 maxRedirects
 
 
 class HttpError(Exception):
@@ -56,6 +64,7 @@ class Response:
     body: bytes = b""
     written: int = 0
     reason: str = ""
+    url: str = ""                # the URL that produced this response (after redirects)
 
     def header(self, name: str, default: Optional[str] = None) -> Optional[str]:
         name = name.lower()
@@ -87,6 +96,27 @@ class Progress:
         self.cancelled = True
         if self.native is not None:
             self.native.cancel()
+
+
+def redirect_target(url: str, r: "Response") -> Optional[str]:
+    """Absolute URL a 3xx response points to (None: not a usable redirect)."""
+    if r.status not in REDIRECTS:
+        return None
+    loc = r.header("location")
+    if not loc:
+        return None
+    # Like the WHATWG URL parser: resolve against the current URL and percent-encode what
+    # may not appear raw in a request line (spaces, non-ASCII), keeping existing escapes.
+    nxt = quote(urljoin(url, loc.strip()), safe=":/?#[]@!$&'()*+,;=%~")
+    return nxt if urlsplit(nxt).scheme in ("http", "https") else None
+
+
+def redirect_headers(url: str, nxt: str, headers: Headers) -> List[Tuple[str, str]]:
+    """Headers for the next hop: ``Authorization`` (and a stale ``Host``) is dropped when the
+    host changes, as request@2 does; everything else (``Range``!) is kept."""
+    same = urlsplit(url).netloc == urlsplit(nxt).netloc
+    return [(k, v) for k, v in headers
+            if k.lower() != "host" and (same or k.lower() != "authorization")]
 
 
 def split_host(url: str) -> Tuple[str, str, int, str]:
@@ -304,18 +334,30 @@ class NativeTransport(Transport):
                 progress.native = self._n.Progress()
             nprog = progress.native
         loop = asyncio.get_running_loop()
-        slot = self._new_slot()
-        fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
-                                   dst_headers, length, nprog, slot, split)
-        try:
-            return await asyncio.shield(fut)
-        except asyncio.CancelledError:
-            if nprog is not None:
-                nprog.cancel()
-            self._abort_slot(slot)
-            raise
-        finally:
-            self._end_slot(slot)
+        for _ in range(MAX_REDIRECTS + 1):
+            slot = self._new_slot()
+            fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
+                                       dst_headers, length, nprog, slot, split)
+            try:
+                out = await asyncio.shield(fut)
+            except asyncio.CancelledError:
+                if nprog is not None:
+                    nprog.cancel()
+                self._abort_slot(slot)
+                raise
+            finally:
+                self._end_slot(slot)
+            get, put = out[0], out[1]
+            get.url = src_url
+            nxt = redirect_target(src_url, get) if put is None else None
+            if nxt is None:
+                return out
+            if not nxt.startswith("http://"):
+                raise TransportError(f"relay source {src_url} redirects to {nxt}: the "
+                                     f"socket relay needs plain http", get.status)
+            src_headers = redirect_headers(src_url, nxt, src_headers)
+            src_url = nxt
+        raise TransportError(f"relay source: more than {MAX_REDIRECTS} redirects", 310)
 
     async def close(self) -> None:
         with self._lock:
@@ -338,6 +380,7 @@ class AiohttpTransport(Transport):
         self.io_timeout = io_timeout
         self.limit = limit
         self.ssl_verify = ssl_verify
+        self.max_body = 64 << 20
 
     async def _sess(self):
         import aiohttp
@@ -362,8 +405,9 @@ class AiohttpTransport(Transport):
         loop = asyncio.get_running_loop()
         try:
             async with sess.request(method, url, headers=hdrs, data=data,
-                                    allow_redirects=True, compress=None) as resp:
+                                    allow_redirects=False, compress=None) as resp:
                 rh = [(k.lower(), v) for k, v in resp.headers.items()]
+                final = str(resp.url)
                 if sink is not None and 200 <= resp.status < 300:
                     written = 0
                     async for chunk in resp.content.iter_chunked(1 << 20):
@@ -376,9 +420,16 @@ class AiohttpTransport(Transport):
                         written += len(chunk)
                         if progress is not None:
                             progress.add(len(chunk))
-                    return Response(resp.status, rh, b"", written, resp.reason or "")
-                payload = b"" if method == "HEAD" or not expect_body else await resp.read()
-                return Response(resp.status, rh, payload, 0, resp.reason or "")
+                    return Response(resp.status, rh, b"", written, resp.reason or "", final)
+                payload = b""
+                if method != "HEAD" and expect_body:
+                    buf = bytearray()       # bounded like the native transport (64 MiB)
+                    async for chunk in resp.content.iter_chunked(1 << 20):
+                        if len(buf) + len(chunk) > self.max_body:
+                            raise HttpError("response body exceeds limit", resp.status)
+                        buf += chunk
+                    payload = bytes(buf)
+                return Response(resp.status, rh, payload, 0, resp.reason or "", final)
         except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError,
                 asyncio.TimeoutError) as e:
             raise TransportError(f"{method} {url}: {type(e).__name__}: {e}") from e
@@ -422,8 +473,21 @@ class TransportSet:
             return self.native
         return self.fallback
 
-    async def request(self, method: str, url: str, **kw) -> Response:
-        return await self.for_url(url).request(method, url, **kw)
+    async def request(self, method: str, url: str, follow_redirects: bool = True,
+                      **kw) -> Response:
+        if method not in ("GET", "HEAD") or not follow_redirects:
+            r = await self.for_url(url).request(method, url, **kw)
+            r.url = r.url or url
+            return r
+        for _ in range(MAX_REDIRECTS + 1):
+            r = await self.for_url(url).request(method, url, **kw)
+            r.url = r.url or url
+            nxt = redirect_target(r.url, r)
+            if nxt is None:
+                return r
+            kw["headers"] = redirect_headers(r.url, nxt, kw.get("headers") or ())
+            url = nxt
+        raise TransportError(f"{method} {url}: more than {MAX_REDIRECTS} redirects", 310)
 
     async def close(self) -> None:
         if self.native is not None:

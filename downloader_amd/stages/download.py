@@ -116,13 +116,13 @@ class DownloadStage(Stage):
         s3 = self.sv.s3
         if not s3.can_relay(url) or not select_from_config(self.cfg).accepts_single_file(name):
             return False
-        size, ranges = await http_src.probe(self.sv.transports, url)
-        if size <= 0 or (size > s3.multipart_threshold and not ranges):
+        size, ranges, final = await http_src.probe(self.sv.transports, url)
+        if size <= 0 or (size > s3.multipart_threshold and not ranges) or not s3.can_relay(final):
             return False
         await ensure_staging_bucket(self.sv)
         key = keys.object_key(job.id, name)
         job.logger.info("streaming http source straight to staging", key=key, size=size)
-        await s3.relay_object(self.cfg.s3.bucket, key, url, size, Progress())
+        await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress())
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
         job.stats.setdefault("streamed", []).append(
             {"file": os.path.join(path, name), "key": key, "size": size, "virtual": True})

@@ -42,6 +42,7 @@ class Origin:
         self.slow = {}          # path -> bytes/s trickle rate
         self.chunked = set()
         self.corrupt = {}       # path -> [file offset, responses left]: flip that byte
+        self.redirect = {}      # path -> (status, Location): answered before anything else
 
     def _body(self, path: str, data: bytes, s: int, e: int) -> bytes:
         """data[s:e+1], with the byte of an armed ``corrupt`` fault flipped if covered."""
@@ -70,6 +71,9 @@ class Origin:
 
         async def handler(req: web.Request):
             self.requests.append((req.method, req.path_qs, req.headers.get("Range")))
+            if req.path in self.redirect:
+                st, loc = self.redirect[req.path]
+                return web.Response(status=st, headers={"Location": loc}, text="moved")
             if req.path in self.fail_status:
                 return web.Response(status=self.fail_status[req.path], text="nope")
             data = self.blobs.get(req.path)

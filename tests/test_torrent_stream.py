@@ -289,3 +289,28 @@ def test_check_piece_discards_stale_verdict(run, tmp_path, monkeypatch):
         st.frag_ver[1] += 1
         assert await st._check_piece(1) is False and 1 in st.verified
     run(go())
+
+
+@pytest.mark.parametrize("mode", ["auto", "off"])
+def test_webseeds_that_redirect(run, tmp_path, make_cfg, origin_cls, mode):
+    """Webseed file URLs answering 302 to a mirror: the hashed relay (stream staging) and the
+    session's spliced Range GETs (disk staging) both follow to the mirror."""
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        data, _ = await _show(tmp_path, origin)
+        for rel in SHOW:
+            origin.blobs["/mirror/Show/" + rel] = origin.blobs.pop("/ws/Show/" + rel)
+            origin.redirect["/ws/Show/" + rel] = (302, origin.url("/mirror/Show/" + rel))
+        w = _worker(make_cfg, ep, download={"torrent_stream": mode})
+        await w.start(health=False)
+        await w.submit(api.make_download("rdt", "http", origin.url("/t/show.torrent"), "TV"))
+        await _wait(w)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        assert r.stats["torrent"]["staging"] == ("stream" if mode == "auto" else "disk")
+        for rel in ("Season 1/e1.mkv", "Season 1/e2.mkv"):
+            assert s3.get("triton-staging", keys.object_key("rdt", rel)) == data[rel]
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())

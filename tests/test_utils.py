@@ -151,3 +151,16 @@ def test_cancelled_native_request_frees_its_thread(run):
         await t.close()
         srv.close()
     run(go(), timeout=30)
+
+
+def test_redirect_target_and_headers():
+    from downloader_amd.net.http import Response, redirect_headers, redirect_target
+    r = Response(302, [("location", "../b/c d.mkv?x=1")])
+    assert redirect_target("http://h:1/a/x/y.mkv", r) == "http://h:1/a/b/c%20d.mkv?x=1"
+    assert redirect_target("http://h/a", Response(200, [("location", "/x")])) is None
+    assert redirect_target("http://h/a", Response(301, [])) is None
+    assert redirect_target("http://h/a", Response(302, [("location", "ftp://x/y")])) is None
+    assert redirect_target("http://h/a", Response(302, [("location", "/p%20q")])) == "http://h/p%20q"
+    hdrs = [("Range", "bytes=0-9"), ("Authorization", "AWS4 x"), ("Host", "h")]
+    assert redirect_headers("http://h/a", "http://h/b", hdrs) == hdrs[:2]
+    assert redirect_headers("http://h/a", "http://other/b", hdrs) == hdrs[:1]

@@ -530,3 +530,41 @@ def test_source_names_cannot_leave_the_job_dir(run, tmp_path):
         assert not (tmp_path / "dl" / "job2" / "evil.mkv").exists()
         await s3.stop()
     run(go())
+
+
+def test_http_sources_follow_redirects(run, make_cfg, origin_cls):
+    """request@2 follows up to 10 GET redirects (relative Locations too, Range kept). The
+    stream relay, the disk path (parallel Range GETs) and .torrent URLs all land on the final
+    URL; an 11-hop loop fails the job."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0})
+        big = os.urandom(13 * 1024 * 1024 + 5)          # multipart: relayed in Range parts
+        origin.blobs["/cdn/real/big.mkv"] = big
+        origin.redirect["/v/big.mkv"] = (302, "/cdn/hop.mkv")
+        origin.redirect["/cdn/hop.mkv"] = (307, "real/big.mkv")          # relative
+        await w.submit(api.make_download("rd1", "http", origin.url("/v/big.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert w.results[0].stats.get("streamed")                  # relayed, no disk hop
+        assert s3.get("triton-staging", keys.object_key("rd1", "big.mkv")) == big
+        # disk path with parallel ranges: every Range GET carries its Range through the hops
+        await w.stop()
+        cfg = make_cfg(s3.endpoint, download={"stream_http": False, "http_streams": 3,
+                                              "http_min_split": 4 << 20},
+                       broker={"max_retries": 0})
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        await w.submit(api.make_download("rd2", "http", origin.url("/v/big.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert s3.get("triton-staging", keys.object_key("rd2", "big.mkv")) == big
+        ranged = [rg for m, p, rg in origin.requests if p == "/cdn/real/big.mkv" and m == "GET"]
+        assert ranged and all(rg for rg in ranged)
+        # a redirect loop is an error, not a hang
+        for i in range(12):
+            origin.redirect[f"/loop/{i}.mkv"] = (302, f"/loop/{i + 1}.mkv")
+        await w.submit(api.make_download("rd3", "http", origin.url("/loop/0.mkv")))
+        await _wait(w, 2)
+        assert w.results[1].outcome == "dead" and "redirect" in w.results[1].error
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
