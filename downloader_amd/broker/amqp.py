@@ -208,13 +208,22 @@ class Channel:
             finally:
                 self._get_waiter = None
 
-    def basic_ack(self, tag: int, multiple: bool = False) -> None:
-        if not self.closed:
-            self.conn.send(C.method_frame(self.id, C.BASIC_ACK, tag, multiple))
+    def basic_ack(self, tag: int, multiple: bool = False) -> bool:
+        """False when the channel or its connection is gone: the broker requeues every
+        unacked delivery of a dead channel, so there is nothing left to settle."""
+        return self._settle(C.method_frame(self.id, C.BASIC_ACK, tag, multiple))
 
-    def basic_nack(self, tag: int, requeue: bool = True, multiple: bool = False) -> None:
-        if not self.closed:
-            self.conn.send(C.method_frame(self.id, C.BASIC_NACK, tag, multiple, requeue))
+    def basic_nack(self, tag: int, requeue: bool = True, multiple: bool = False) -> bool:
+        return self._settle(C.method_frame(self.id, C.BASIC_NACK, tag, multiple, requeue))
+
+    def _settle(self, frame: bytes) -> bool:
+        if self.closed:
+            return False
+        try:
+            self.conn.send(frame)
+        except ConnectionError:
+            return False
+        return True
 
     async def close(self) -> None:
         if self.closed:

@@ -273,3 +273,19 @@ def test_broker_drop_mid_job_redelivers_and_dedups(run, make_cfg, origin_cls):
         assert len(puts) == 1
         await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()
     run(go(), timeout=60)
+
+
+def test_settling_on_a_dead_connection_is_a_noop():
+    """An ack/nack racing a dropped connection (before the reconnect bumps the generation)
+    must not raise into the job: the broker requeues unacked deliveries of a dead channel,
+    and the done marker makes the redelivery a skip."""
+    from downloader_amd.broker.amqp import Channel
+
+    class DeadConn:
+        def send(self, data):
+            raise ConnectionError("AMQP connection is closed")
+
+    ch = Channel(DeadConn(), 1)
+    assert ch.basic_ack(7) is False and ch.basic_nack(7) is False
+    ch.closed = True
+    assert ch.basic_ack(8) is False
