@@ -161,6 +161,10 @@ class TorrentClient:
                 w.close()
                 return
             await pc.run()
+        except Exception:
+            # never let a remote connection's failure reach the loop's exception handler
+            # (it stops the worker): drop the connection
+            w.close()
         finally:
             self._conn_tasks.discard(t)
 

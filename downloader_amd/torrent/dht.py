@@ -23,6 +23,8 @@ from .bencode import BencodeError, bdecode, bencode
 Addr = Tuple[str, int]
 K = 8
 ALPHA = 3
+STORE_MAX_TORRENTS = 10000      # announce_peer store bounds (any node can announce)
+STORE_MAX_PEERS = 200
 
 
 def distance(a: bytes, b: bytes) -> int:
@@ -117,6 +119,7 @@ class DHTNode(asyncio.DatagramProtocol):
         self._secret_t = time.monotonic()
         self.transport: Optional[asyncio.DatagramTransport] = None
         self.queries_served = 0
+        self.bad_packets = 0
 
     # ---------------------------------------------------------------- lifecycle
     async def start(self) -> "DHTNode":
@@ -182,14 +185,27 @@ class DHTNode(asyncio.DatagramProtocol):
         return r
 
     def datagram_received(self, data: bytes, addr) -> None:
+        # Anything may arrive on a public UDP port: a packet that does not parse or that
+        # breaks a handler is dropped. An exception escaping a protocol callback would reach
+        # the event loop's exception handler, which stops the worker process.
+        try:
+            self._datagram(data, addr)
+        except Exception:
+            self.bad_packets += 1
+
+    def _datagram(self, data: bytes, addr) -> None:
         try:
             msg = bdecode(data)
         except BencodeError:
+            self.bad_packets += 1
             return
         if not isinstance(msg, dict):
             return
         y = msg.get(b"y")
         t = msg.get(b"t", b"")
+        if not isinstance(t, bytes):
+            self.bad_packets += 1
+            return
         addr = (addr[0], addr[1])
         if y == b"r" or y == b"e":
             f = self._pending.get(t)
@@ -205,6 +221,9 @@ class DHTNode(asyncio.DatagramProtocol):
     def _handle_query(self, msg: dict, t: bytes, addr: Addr) -> None:
         q = msg.get(b"q")
         a = msg.get(b"a") or {}
+        if not isinstance(a, dict):
+            self._send({"t": t, "y": "e", "e": [203, "bad arguments"]}, addr)
+            return
         nid = a.get(b"id")
         if not isinstance(nid, bytes) or len(nid) != 20:
             self._send({"t": t, "y": "e", "e": [203, "bad id"]}, addr)
@@ -230,8 +249,19 @@ class DHTNode(asyncio.DatagramProtocol):
             if not self._valid_token(addr[0], a.get(b"token", b"")):
                 self._send({"t": t, "y": "e", "e": [203, "bad token"]}, addr)
                 return
-            port = addr[1] if a.get(b"implied_port") else int(a.get(b"port", 0))
-            self.store.setdefault(ih, {})[(addr[0], port)] = time.monotonic()
+            port = addr[1] if a.get(b"implied_port") else a.get(b"port", 0)
+            if not isinstance(ih, bytes) or len(ih) != 20 or not isinstance(port, int) \
+                    or not 0 < port < 65536:
+                self._send({"t": t, "y": "e", "e": [203, "bad announce"]}, addr)
+                return
+            peers = self.store.get(ih)
+            if peers is None:
+                if len(self.store) >= STORE_MAX_TORRENTS:      # bounded: forget the oldest
+                    self.store.pop(next(iter(self.store)))
+                peers = self.store[ih] = {}
+            peers[(addr[0], port)] = time.monotonic()
+            while len(peers) > STORE_MAX_PEERS:
+                peers.pop(min(peers, key=peers.get))
         else:
             self._send({"t": t, "y": "e", "e": [204, "method unknown"]}, addr)
             return

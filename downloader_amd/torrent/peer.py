@@ -186,6 +186,12 @@ class PeerConn:
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError, OSError,
                 ProtocolError):
             pass
+        except Exception:
+            # A malformed message from the remote (short REQUEST/HAVE -> struct.error, a bad
+            # bitfield, odd bencoding) ends this connection only. Escaping run() it would fail
+            # the whole torrent session (outgoing peers) or reach the event loop's exception
+            # handler and stop the worker (incoming peers).
+            self.s.stats["peer_protocol_errors"] = self.s.stats.get("peer_protocol_errors", 0) + 1
         finally:
             wd.cancel()
             self.close()

@@ -507,7 +507,12 @@ class TorrentSession:
                     if p.hash_fails >= 3:
                         p.close()
             return
-        await loop.run_in_executor(None, self.storage.write, idx * self.meta.piece_length, buf)
+        try:
+            await loop.run_in_executor(None, self.storage.write, idx * self.meta.piece_length,
+                                       buf)
+        except OSError as e:   # our disk, not the peer: ENOSPC/EIO fail the job (retried)
+            self.fail(TorrentError(f"storage write of piece {idx} failed: {e}"))
+            return
         await self._piece_complete(idx)
 
     async def _piece_complete(self, idx: int) -> None:

@@ -36,6 +36,13 @@ def test_supervisor_two_workers_over_amqp(run, tmp_path, origin_cls):
         client = AmqpBroker(srv.url)
         await client.connect()
         await client.declare("v1.download")   # unroutable publishes are dropped, like RabbitMQ
+        # both worker processes subscribed before the jobs go out (a loaded CI box may start
+        # the second interpreter after the first has drained all 8 jobs)
+        for _ in range(3000):
+            q = srv.queues.get("v1.download")
+            if q is not None and len(q.consumers) == 2:
+                break
+            await asyncio.sleep(0.02)
         n = 8
         for i in range(n):
             origin.blobs[f"/m{i}.mkv"] = os.urandom(30_000 + i)

@@ -6,6 +6,7 @@ import asyncio
 import hashlib
 import os
 import shutil
+import struct
 
 import pytest
 from hypothesis import given, settings
@@ -665,4 +666,49 @@ def test_websocket_only_trackers_are_dropped(run, tmp_path):
                 await asyncio.wait_for(s.wait(), 60)
         finally:
             await c.close()
+    run(go())
+
+
+def test_malformed_remote_input_never_escapes(run, tmp_path):
+    """Garbage from the network ends one connection / drops one packet and nothing else:
+    a peer's short REQUEST (struct.error) and a DHT query whose ``a`` is a list / whose ``t``
+    is a dict. Escaping, they would fail the session or hit the event loop's exception
+    handler, which stops the worker."""
+    from downloader_amd.torrent.bencode import bencode
+    from downloader_amd.torrent.dht import DHTNode
+    from downloader_amd.torrent.peer import handshake_bytes, read_handshake
+
+    async def go():
+        loop_errors = []
+        asyncio.get_running_loop().set_exception_handler(lambda lp, ctx: loop_errors.append(ctx))
+        raw, data, seeder, _ = await _seed(tmp_path, {"x.mkv": 200_000})
+        m = parse_torrent(raw)
+        sess = seeder.sessions[m.info_hash]
+        r, w = await asyncio.open_connection("127.0.0.1", seeder.listen_port)
+        w.write(handshake_bytes(m.info_hash, b"-XX0001-" + b"0" * 12, True))
+        await read_handshake(r)
+        w.write(struct.pack(">IB", 5, 6) + b"\0\0\0\0")       # REQUEST with 4 of 12 bytes
+        await w.drain()
+        await asyncio.wait_for(r.read(), 5)                    # the seeder hangs up on us
+        w.close()
+        assert sess.error is None and not sess.failed.is_set()
+        assert sess.stats.get("peer_protocol_errors", 0) >= 1
+        # the seeder still serves a well-behaved leecher
+        leech = await TorrentClient().start()
+        s = await leech.add_torrent(m, str(tmp_path / "dl"), peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 30)
+        _check(tmp_path / "dl", data)
+        await leech.close(); await seeder.close()
+        node = await DHTNode(host="127.0.0.1").start()
+        probe = await DHTNode(host="127.0.0.1").start()
+        for pkt in (bencode({"t": "aa", "y": "q", "q": "ping", "a": [1, 2]}),
+                    bencode({"t": {"x": 1}, "y": "r", "r": {}}),
+                    bencode({"t": "ab", "y": "q", "q": "announce_peer",
+                             "a": {"id": b"i" * 20, "info_hash": [1], "port": "x", "token": b""}}),
+                    b"d1:y1:qe", b"\xff" * 40):
+            probe.transport.sendto(pkt, ("127.0.0.1", node.port))
+        await asyncio.sleep(0.2)
+        assert await probe.ping(("127.0.0.1", node.port)) == node.id    # still answering
+        await node.close(); await probe.close()
+        assert not loop_errors, loop_errors
     run(go())
