@@ -245,11 +245,33 @@ class S3Client:
         finally:
             os.close(fd)
 
-    def plan_parts(self, size: int) -> List[Tuple[int, int, int]]:
+    def plan_parts(self, size: int, align_offset: int = 0,
+                   align: int = 0) -> List[Tuple[int, int, int]]:
+        """(part number, offset, length) of a multipart upload of ``size`` bytes.
+
+        ``align``/``align_offset``: the object is bytes [align_offset, align_offset + size) of
+        a larger stream cut into ``align``-sized units (torrent pieces). When the part size is
+        a multiple of ``align``, the first part is shortened so every interior part boundary
+        falls on a unit boundary: a torrent piece then never straddles two parts, so only
+        pieces at the file's two ends need assembling from fragments. S3 allows unequal
+        parts (all but the last >= 5 MiB)."""
         ps = self.part_size
         while (size + ps - 1) // ps > MAX_PARTS:
             ps *= 2
-        return [(i + 1, off, min(ps, size - off)) for i, off in enumerate(range(0, size, ps))]
+        first = ps
+        if align > 0 and ps % align == 0 and size > ps:
+            first = ps - align_offset % align
+            while first < MIN_PART:            # part size close to the 5 MiB floor
+                first += align
+        out, off, num = [], 0, 1
+        while off < size:
+            ln = min(first if num == 1 else ps, size - off)
+            out.append((num, off, ln))
+            off += ln
+            num += 1
+        if len(out) > MAX_PARTS:               # the shortened first part added one: fall back
+            return [(i + 1, o, min(ps, size - o)) for i, o in enumerate(range(0, size, ps))]
+        return out
 
     async def _multipart(self, bucket: str, key: str, fd: int, size: int, path: str,
                          progress: Optional[Progress], resume: bool, concurrency: int) -> str:

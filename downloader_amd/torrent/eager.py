@@ -59,7 +59,9 @@ class EagerUploader:
             fi = index[os.path.abspath(f)]
             size = meta.files[fi].length
             single = size <= self.s3.multipart_threshold
-            parts = [(1, 0, size)] if single else self.s3.plan_parts(size)
+            # piece-aligned parts: a part is ready as soon as ITS pieces are verified
+            parts = [(1, 0, size)] if single else \
+                self.s3.plan_parts(size, meta.files[fi].offset, self.plen)
             self.files.append(_File(f, key, meta.files[fi].offset, size, parts, single=single))
         self.sem = asyncio.Semaphore(max(1, cfg.s3.max_inflight_parts * 2))
         self.tasks: List[asyncio.Task] = []

@@ -157,7 +157,8 @@ class StreamStager:
             self.targets.append(t)
             if t.size == 0:
                 continue
-            parts = [(0, 0, t.size)] if t.single else self.s3.plan_parts(t.size)
+            parts = [(0, 0, t.size)] if t.single else \
+                self.s3.plan_parts(t.size, fe.offset, meta.piece_length)
             for num, off, ln in parts:
                 skip, full = piece_split(meta, t.offset + off, ln)
                 self.units.append(_Unit(len(self.units), t.offset + off, ln, t, num, off,

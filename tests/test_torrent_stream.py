@@ -199,7 +199,7 @@ def test_settle_never_queues_a_unit_twice(tmp_path):
     from downloader_amd.torrent.stream import StreamStager
     files = [FileEntry(["a.mkv"], 10, 0), FileEntry(["b.mkv"], 10, 10)]
     m = Metainfo(b"x" * 20, "P", 4, b"\0" * 100, files, 20, multi_file=True)
-    s3 = types.SimpleNamespace(multipart_threshold=1 << 20, plan_parts=lambda n: [(1, 0, n)])
+    s3 = types.SimpleNamespace(multipart_threshold=1 << 20, plan_parts=lambda n, *a: [(1, 0, n)])
     root = str(tmp_path)
     sel = [os.path.join(root, "P", "a.mkv"), os.path.join(root, "P", "b.mkv")]
     st = StreamStager(m, types.SimpleNamespace(id="j"),
@@ -248,7 +248,7 @@ def test_check_piece_discards_stale_verdict(run, tmp_path, monkeypatch):
     files = [FileEntry(["a.mkv"], half, 0), FileEntry(["b.mkv"], half, half)]
     pieces = b"".join(hashlib.sha1(data[i:i + plen]).digest() for i in range(0, 3 * plen, plen))
     m = Metainfo(b"x" * 20, "P", plen, pieces, files, 3 * plen, multi_file=True)
-    s3 = types.SimpleNamespace(multipart_threshold=1 << 30, plan_parts=lambda n: [(1, 0, n)])
+    s3 = types.SimpleNamespace(multipart_threshold=1 << 30, plan_parts=lambda n, *a: [(1, 0, n)])
     root = str(tmp_path)
     sel = [os.path.join(root, "P", "a.mkv"), os.path.join(root, "P", "b.mkv")]
     st = StreamStager(m, types.SimpleNamespace(id="j"),
@@ -314,3 +314,23 @@ def test_webseeds_that_redirect(run, tmp_path, make_cfg, origin_cls, mode):
             assert s3.get("triton-staging", keys.object_key("rdt", rel)) == data[rel]
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_piece_aligned_part_plan():
+    """Interior part boundaries of a file at an unaligned torrent offset land on piece
+    boundaries (only the file's two end pieces straddle a part/file edge); parts stay >= 5 MiB
+    except the last, and cover the file exactly."""
+    from downloader_amd.s3.client import MIN_PART, S3Client
+    c = S3Client("127.0.0.1:9", "a", "b", part_size=64 << 20)
+    plen = 4 << 20
+    for off, size in ((12345, 300 << 20), (0, 200 << 20), (plen - 1, 129 << 20),
+                      (7 << 20, (64 << 20) + 1), (123, 64 << 20)):
+        parts = c.plan_parts(size, off, plen)
+        assert parts[0][1] == 0 and sum(ln for _, _, ln in parts) == size
+        assert all(o1 + l1 == o2 for (_, o1, l1), (_, o2, _) in zip(parts, parts[1:]))
+        assert [n for n, _, _ in parts] == list(range(1, len(parts) + 1))
+        assert all(ln >= MIN_PART for _, _, ln in parts[:-1])
+        for _, o, _ in parts[1:]:
+            assert (off + o) % plen == 0, (off, size, parts)
+    # part size not a multiple of the piece length: the plain plan
+    assert c.plan_parts(200 << 20, 5, 3 << 20) == c.plan_parts(200 << 20)
