@@ -6,11 +6,12 @@
 //
 //   * SHA-1 is a serial chain over 64-byte blocks inside one piece, so the unit of
 //     parallelism is the piece: ONE LANE PER PIECE, 64 pieces per wavefront. Per-lane work is
-//     ~670 VALU ops per 64-byte block (80 rounds using v_alignbit rotates, v_bfi for Ch,
-//     v_add3/v_xor3, plus the message schedule), i.e. ~110 MB/s per lane and ~4.9 TB/s for the
-//     full chip - far above the PCIe Gen5 x16 host link (63 GB/s spec) that feeds it. The
-//     design is therefore link-bound as soon as a batch holds >~1k pieces, and the kernel's
-//     job is to never be the bottleneck while keeping host CPUs free for network I/O.
+//     ~616 VALU ops per 64-byte block (80 rounds with v_alignbit rotates, v_bfi for Ch and
+//     v_bitop3 for parity/majority, plus the message schedule). Measured (profiles/verify,
+//     profiles/r2_validate): ~41 MB/s per lane - one wave per SIMD leaves dependent-issue
+//     gaps - so throughput is pieces-in-flight x 41 MB/s: ~680 GB/s at 16k pieces, ~170 GB/s
+//     at 4k. Real torrents have 1k-20k pieces, and the host path that feeds the kernel
+//     (pread into pinned slots + PCIe Gen5 x16, ~57 GB/s DMA measured) is the bound.
 //   * Each lane streams its own piece with 16-byte global loads (4 x dwordx4 per block). The
 //     64 lanes of a wave touch 64 different lines per load, but each line is fully consumed
 //     by the lane's next load, so the L1/L2 absorb it (no LDS staging needed: the kernel is
