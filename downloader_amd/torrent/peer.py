@@ -212,7 +212,7 @@ class PeerConn:
                 self.bitfield.set(i)
         self._raw_bitfield = None
         self._early_haves.clear()
-        self.s.picker.add_peer(self.bitfield)
+        self.s.picker.add_peer(self.bitfield, id(self))
 
     # ---------------------------------------------------------------- receiving
     async def _dispatch(self, mid: int, p: memoryview) -> None:
@@ -233,7 +233,7 @@ class PeerConn:
             if self.bitfield is None:
                 self._early_haves.add(idx)
             elif idx < self.bitfield.n and self.bitfield.set(idx):
-                s.picker.inc(idx)
+                s.picker.inc(idx, id(self))
                 await s.update_interest(self)
                 await s.fill(self)
         elif mid == BITFIELD:
@@ -241,10 +241,10 @@ class PeerConn:
                 self._raw_bitfield = bytes(p)
             else:
                 if self.bitfield is not None:
-                    s.picker.remove_peer(self.bitfield)
+                    s.picker.remove_peer(self.bitfield, id(self))
                 self.bitfield = Bitfield(s.meta.num_pieces)
                 self.bitfield.load(bytes(p))
-                s.picker.add_peer(self.bitfield)
+                s.picker.add_peer(self.bitfield, id(self))
                 await s.update_interest(self)
                 await s.fill(self)
         elif mid == UNCHOKE:

@@ -69,7 +69,15 @@ class _Active:
 
 
 class PiecePicker:
-    """Rarest-first picker over pieces; blocks inside active pieces; endgame duplicates."""
+    """Rarest-first picker over pieces; blocks inside active pieces; endgame duplicates.
+
+    Candidates (pieces not had, not active, not being verified, not claimed by a webseed
+    stream) sit in availability buckets, so starting a new piece costs O(1) expected instead
+    of a scan over every piece (quadratic over a 20k-piece torrent). Buckets are maintained
+    lazily: an entry whose piece changed availability or stopped being a candidate is
+    dropped when met. Each peer's count of pieces it has that we still want is kept up to
+    date too, so "is this peer interesting?" is O(1) instead of a scan per completed piece
+    per peer."""
 
     def __init__(self, meta: Metainfo, have: Bitfield):
         self.meta = meta
@@ -78,29 +86,110 @@ class PiecePicker:
         self.avail = [0] * self.n
         self.active: Dict[int, _Active] = {}
         self.claimed: Set[int] = set()       # pieces owned by webseed workers
+        self.verifying: Set[int] = set()     # all blocks in, SHA-1 / write in progress
         self.failed: Dict[int, int] = {}
+        self._buckets: Dict[int, List[int]] = {}
+        self._slot = [-1] * self.n            # bucket a piece's live entry sits in (-1: none)
+        self._peers: Dict[int, Bitfield] = {}
+        self.want_count: Dict[int, int] = {}      # peer id -> pieces it has that we lack
+        for i in range(self.n):
+            self._push(i)
 
-    def add_peer(self, bf: Bitfield) -> None:
+    # ---------------------------------------------------------------- candidates
+    def _cand(self, i: int) -> bool:
+        return not (i in self.have or i in self.active or i in self.claimed
+                    or i in self.verifying)
+
+    def _push(self, i: int) -> None:
+        a = self.avail[i]
+        if self._slot[i] == a or not self._cand(i):
+            return
+        self._slot[i] = a
+        b = self._buckets.get(a)
+        if b is None:
+            b = self._buckets[a] = []
+        b.append(i)
+
+    def requeue(self, i: int) -> None:
+        """Piece ``i`` is wanted again (failed its hash check, or a claim was released)."""
+        self.verifying.discard(i)
+        self._slot[i] = -1
+        self._push(i)
+
+    def _take_rarest(self, bf: Bitfield) -> int:
+        """Remove and return a random piece of the lowest availability that ``bf`` has."""
+        for a in sorted(self._buckets):
+            if a <= 0:
+                continue                      # nobody has those
+            lst = self._buckets[a]
+            misses = 0
+            while lst:
+                r = random.randrange(len(lst)) if len(lst) > 1 else 0
+                i = lst[r]
+                stale = self._slot[i] != a or not self._cand(i)
+                if stale or i in bf:
+                    lst[r] = lst[-1]
+                    lst.pop()
+                    if self._slot[i] == a:
+                        self._slot[i] = -1
+                    if stale:
+                        continue
+                    return i
+                misses += 1
+                if misses >= 16:             # a sparse peer: scan this bucket once
+                    for r, i in enumerate(lst):
+                        if self._slot[i] == a and self._cand(i) and i in bf:
+                            lst[r] = lst[-1]
+                            lst.pop()
+                            self._slot[i] = -1
+                            return i
+                    break
+        return -1
+
+    # ---------------------------------------------------------------- peers
+    def add_peer(self, bf: Bitfield, pid: Optional[int] = None) -> None:
+        want = 0
         for i in range(self.n):
             if i in bf:
                 self.avail[i] += 1
+                self._push(i)
+                if i not in self.have:
+                    want += 1
+        if pid is not None:
+            self._peers[pid] = bf
+            self.want_count[pid] = want
 
-    def remove_peer(self, bf: Bitfield) -> None:
+    def remove_peer(self, bf: Bitfield, pid: Optional[int] = None) -> None:
         for i in range(self.n):
             if i in bf:
                 self.avail[i] -= 1
+                self._push(i)
+        if pid is not None:
+            self._peers.pop(pid, None)
+            self.want_count.pop(pid, None)
 
-    def inc(self, i: int) -> None:
+    def inc(self, i: int, pid: Optional[int] = None) -> None:
+        """A peer announced piece ``i`` (HAVE)."""
         self.avail[i] += 1
+        self._push(i)
+        if pid is not None and pid in self.want_count and i not in self.have:
+            self.want_count[pid] += 1
 
-    def wanted(self, i: int) -> bool:
-        return i not in self.have
+    def piece_done(self, i: int) -> None:
+        """``i`` was just added to ``have``: peers holding it are less interesting."""
+        self.verifying.discard(i)
+        for pid, bf in self._peers.items():
+            if i in bf:
+                self.want_count[pid] -= 1
 
-    def peer_has_wanted(self, bf: Bitfield) -> bool:
+    def peer_has_wanted(self, bf: Bitfield, pid: Optional[int] = None) -> bool:
         if self.have.complete:
             return False
+        if pid is not None and pid in self.want_count:
+            return self.want_count[pid] > 0
         return any(i in bf and i not in self.have for i in range(self.n))
 
+    # ---------------------------------------------------------------- blocks
     def next_block(self, peer_id: int, bf: Bitfield) -> Optional[Tuple[int, int, int]]:
         # 1. a free block of an active piece this peer has
         for ap in self.active.values():
@@ -111,17 +200,7 @@ class PiecePicker:
                         ap.req.setdefault(b, set()).add(peer_id)
                         return ap.idx, b * BLOCK, ap.block_len(b)
         # 2. start the rarest piece this peer has
-        best, best_av, ties = -1, 1 << 30, 0
-        for i in range(self.n):
-            if i in self.have or i in self.active or i in self.claimed or i not in bf:
-                continue
-            a = self.avail[i]
-            if a < best_av:
-                best, best_av, ties = i, a, 1
-            elif a == best_av:
-                ties += 1
-                if random.randrange(ties) == 0:
-                    best = i
+        best = self._take_rarest(bf)
         if best >= 0:
             ap = _Active(best, self.meta.piece_size(best))
             self.active[best] = ap
@@ -168,6 +247,12 @@ class PiecePicker:
                         ap.req.setdefault(b, set()).add(peer_id)
                         out.append((ap.idx, b * BLOCK, ap.block_len(b)))
         return out
+
+    def complete_blocks(self, idx: int) -> None:
+        """All blocks of active piece ``idx`` arrived: it leaves ``active`` for ``verifying``
+        (not a candidate again unless its hash check fails -> ``requeue``)."""
+        self.verifying.add(idx)
+        self.active.pop(idx, None)
 
     def release(self, peer_id: int, piece: int, begin: int) -> None:
         ap = self.active.get(piece)
@@ -221,6 +306,13 @@ class PiecePicker:
     def unclaim(self, pieces) -> None:
         for p in pieces:
             self.claimed.discard(p)
+            self.requeue(p)
+
+    def settle_claim(self, p: int, good: bool) -> None:
+        """A claimed webseed piece was verified: done (caller sets ``have``) or wanted again."""
+        self.claimed.discard(p)
+        if not good:
+            self.requeue(p)
 
     def remaining(self) -> int:
         return self.n - self.have.count
@@ -440,7 +532,7 @@ class TorrentSession:
             return
         self.release_inflight(pc)
         if pc.bitfield is not None and self.picker is not None:
-            self.picker.remove_peer(pc.bitfield)
+            self.picker.remove_peer(pc.bitfield, id(pc))
         self._wake.set()
 
     def release_inflight(self, pc: PeerConn) -> None:
@@ -452,7 +544,7 @@ class TorrentSession:
     async def update_interest(self, pc: PeerConn) -> None:
         if self.picker is None or pc.bitfield is None:
             return
-        await pc.set_interested(self.picker.peer_has_wanted(pc.bitfield))
+        await pc.set_interested(self.picker.peer_has_wanted(pc.bitfield, id(pc)))
 
     async def maybe_unchoke(self, pc: PeerConn) -> None:
         unchoked = sum(1 for p in self.peers.values() if not p.am_choking)
@@ -493,13 +585,14 @@ class TorrentSession:
                     await other.cancel(idx, begin, len(data))
         if ap.got < ap.nblocks:
             return
-        del self.picker.active[idx]
+        self.picker.complete_blocks(idx)
         buf = bytes(ap.buf)
         loop = asyncio.get_running_loop()
         digest = await loop.run_in_executor(None, hashing.sha1, buf) if len(buf) >= 262144 \
             else hashing.sha1(buf)
         if digest != self.meta.piece_hash(idx):
             self.stats["hash_fails"] += 1
+            self.picker.requeue(idx)
             for pid in ap.peers:
                 p = self.peers.get(pid)
                 if p is not None:
@@ -511,6 +604,7 @@ class TorrentSession:
             await loop.run_in_executor(None, self.storage.write, idx * self.meta.piece_length,
                                        buf)
         except OSError as e:   # our disk, not the peer: ENOSPC/EIO fail the job (retried)
+            self.picker.requeue(idx)
             self.fail(TorrentError(f"storage write of piece {idx} failed: {e}"))
             return
         await self._piece_complete(idx)
@@ -518,12 +612,14 @@ class TorrentSession:
     async def _piece_complete(self, idx: int) -> None:
         if not self.have.set(idx):
             return
+        self.picker.piece_done(idx)
         self.verified_bytes += self.meta.piece_size(idx)
         for cb in self.piece_listeners:
             cb(idx)
         for p in list(self.peers.values()):
             await p.send_have(idx)
-            if p.am_interested and p.bitfield is not None and not self.picker.peer_has_wanted(p.bitfield):
+            if p.am_interested and p.bitfield is not None and \
+                    not self.picker.peer_has_wanted(p.bitfield, id(p)):
                 await p.set_interested(False)
         if self.have.complete:
             self._finish()
@@ -812,7 +908,7 @@ class TorrentSession:
             return
         self.stats["webseed_verify_s"] += time.perf_counter() - t_verify
         for i, good in zip(pieces, ok):
-            self.picker.claimed.discard(i)
+            self.picker.settle_claim(i, bool(good))
             if good:
                 await self._piece_complete(i)
             else:

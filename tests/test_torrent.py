@@ -712,3 +712,87 @@ def test_malformed_remote_input_never_escapes(run, tmp_path):
         await node.close(); await probe.close()
         assert not loop_errors, loop_errors
     run(go())
+
+
+def test_piece_picker_buckets_and_interest_counts():
+    """Randomised check of the bucketed rarest-first picker against brute force: every piece
+    started is a candidate of minimal availability among those the peer has; per-peer
+    interest counts match a full recount; a 20k-piece torrent is picked in O(1) per piece."""
+    import random as _r
+    import time as _t
+
+    from downloader_amd.torrent.metainfo import FileEntry, Metainfo
+    from downloader_amd.torrent.session import PiecePicker
+    from downloader_amd.torrent.storage import Bitfield
+
+    rng = _r.Random(7)
+    n = 300
+    m = Metainfo(b"x" * 20, "t", 16384, b"\0" * 20 * n, [FileEntry(["t"], n * 16384, 0)],
+                 n * 16384)
+    have = Bitfield(n)
+    pk = PiecePicker(m, have)
+    peers = {}
+    for step in range(1500):
+        op = rng.random()
+        if op < 0.08 or not peers:
+            bf = Bitfield(n)
+            for i in rng.sample(range(n), rng.randrange(1, n)):
+                bf.set(i)
+            pid = step
+            peers[pid] = bf
+            pk.add_peer(bf, pid)
+        elif op < 0.12 and len(peers) > 1:
+            pid = rng.choice(list(peers))
+            pk.remove_peer(peers.pop(pid), pid)
+        elif op < 0.3:
+            pid = rng.choice(list(peers))
+            i = rng.randrange(n)
+            if peers[pid].set(i):
+                pk.inc(i, pid)
+        elif op < 0.8:
+            pid = rng.choice(list(peers))
+            bf = peers[pid]
+            cands = [i for i in range(n) if i in bf and i not in have and i not in pk.active
+                     and i not in pk.verifying and i not in pk.claimed]
+            got = pk._take_rarest(bf)
+            if not cands:
+                assert got == -1
+                continue
+            assert got in cands and pk.avail[got] == min(pk.avail[i] for i in cands)
+            pk.active[got] = object()          # started
+        elif op < 0.95 and pk.active:
+            i = rng.choice(list(pk.active))
+            pk.complete_blocks(i)
+            if rng.random() < 0.2:
+                pk.requeue(i)                   # hash failure
+            else:
+                have.set(i)
+                pk.piece_done(i)
+        else:
+            i = rng.randrange(n)
+            if pk._cand(i):
+                pk.claimed.add(i)
+                pk.unclaim([i]) if rng.random() < 0.5 else None
+        for pid, bf in peers.items():
+            assert pk.want_count[pid] == sum(1 for i in range(n) if i in bf and i not in have)
+    # scale: 20k pieces, 32 full seeders
+    n = 20000
+    m = Metainfo(b"x" * 20, "t", 16384, b"\0" * 20 * n, [FileEntry(["t"], n * 16384, 0)],
+                 n * 16384)
+    have = Bitfield(n)
+    pk = PiecePicker(m, have)
+    full = Bitfield(n, b"\xff" * ((n + 7) // 8))
+    for pid in range(32):
+        pk.add_peer(full, pid)
+    t0 = _t.perf_counter()
+    seen = set()
+    for _ in range(n):
+        i = pk._take_rarest(full)
+        assert i >= 0 and i not in seen
+        seen.add(i)
+        pk.active[i] = object()
+        pk.complete_blocks(i)
+        have.set(i)
+        pk.piece_done(i)
+    assert pk._take_rarest(full) == -1 and not pk.peer_has_wanted(full, 0)
+    assert _t.perf_counter() - t0 < 2.0
