@@ -93,6 +93,18 @@ class PeerConn:
             async with self._wlock:
                 await self.writer.drain()
 
+    async def send_block(self, idx: int, begin: int, block: memoryview) -> None:
+        """PIECE message with the block taken as a view of the cached piece: the header and
+        the block go out in one write without the two intermediate 16 KiB copies that
+        ``send(PIECE, header + block)`` makes."""
+        if self.closed:
+            return
+        self.writer.write(b"".join((struct.pack(">IBII", len(block) + 9, PIECE, idx, begin),
+                                    block)))
+        if self.writer.transport.get_write_buffer_size() > 1 << 20:
+            async with self._wlock:
+                await self.writer.drain()
+
     async def send_ext(self, name: bytes, payload: bytes) -> None:
         mid = self.ext.get(name)
         if mid:
@@ -223,7 +235,7 @@ class PeerConn:
             idx, begin = struct.unpack(">II", p[:8])
             if self.inflight.pop((idx, begin), None) is not None or s.picker is not None:
                 self.down_bytes += len(p) - 8
-                await s.on_block(self, idx, begin, bytes(p[8:]))
+                await s.on_block(self, idx, begin, p[8:])   # copied once, into the piece
             await s.fill(self)
         elif mid == REQUEST:
             idx, begin, ln = struct.unpack(">III", p[:12])

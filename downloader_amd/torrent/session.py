@@ -19,7 +19,6 @@ import asyncio
 import hashlib
 import os
 import random
-import struct
 import time
 from collections import OrderedDict
 from typing import TYPE_CHECKING, Dict, List, Optional, Set, Tuple
@@ -29,7 +28,7 @@ from ..net.http import FileSink, TransportError
 from ..ops import hashing
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
-from .peer import BLOCK, METADATA_PIECE, PIECE, PeerConn
+from .peer import BLOCK, METADATA_PIECE, PeerConn
 from .storage import Bitfield, Storage
 from .tracker import decode_compact, encode_compact, supported as tracker_supported
 
@@ -563,7 +562,9 @@ class TorrentSession:
         if blocks:
             await pc.request_many(blocks)
 
-    async def on_block(self, pc: PeerConn, idx: int, begin: int, data: bytes) -> None:
+    async def on_block(self, pc: PeerConn, idx: int, begin: int, data) -> None:
+        """``data``: the block (bytes or a memoryview of the receive buffer - it is copied
+        into the piece before anything awaits)."""
         if self.picker is None or self.have is None:
             return
         ap = self.picker.active.get(idx)
@@ -643,7 +644,7 @@ class TorrentSession:
             self._piece_cache.move_to_end(idx)
         pc.up_bytes += ln
         self.uploaded += ln
-        await pc.send(PIECE, struct.pack(">II", idx, begin) + piece[begin:begin + ln])
+        await pc.send_block(idx, begin, memoryview(piece)[begin:begin + ln])
 
     # ---------------------------------------------------------------- metadata (BEP-9)
     async def on_ext_handshake(self, pc: PeerConn) -> None:
