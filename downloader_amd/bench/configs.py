@@ -311,36 +311,79 @@ async def config5(a) -> Dict:
             "torrent_jobs": n_torrent, "worker_exit_codes": codes}
 
 
+def _seed_proc(conn, raw: bytes, src: str, n: int) -> None:
+    """Seeding clients in their own process (remote peers are not on our event loop)."""
+    from downloader_amd.torrent.client import TorrentClient
+    from downloader_amd.torrent.metainfo import parse_torrent
+
+    async def go():
+        meta = parse_torrent(raw)
+        cs = []
+        for _ in range(n):
+            c = await TorrentClient(max_uploads=64).start()
+            await c.add_torrent(meta, src)
+            cs.append(c)
+        conn.send([c.listen_port for c in cs])
+        await asyncio.get_running_loop().run_in_executor(None, conn.recv)
+        for c in cs:
+            await c.close()
+    asyncio.run(go())
+
+
 async def config_swarm(a) -> Dict:
     """Extra (not in BASELINE.json): a peer-wire-only download from ``--seeders`` seeders
-    over loopback (no webseed), measuring the BEP-3 block pipeline + SHA-1 verification."""
+    over loopback (no webseed), measuring the BEP-3 block pipeline + SHA-1 verification of
+    the downloading client. The seeders run in a separate process (``--seed-inproc``: on the
+    same event loop, as in round 1)."""
+    import multiprocessing as mp
+
     from downloader_amd.torrent.client import TorrentClient
     from downloader_amd.torrent.metainfo import make_torrent, parse_torrent
     total = int(2e9 * a.scale)
     src = tempfile.mkdtemp(prefix="swarm-src-", dir=a.src_dir)
     dst = tempfile.mkdtemp(prefix="swarm-dst-", dir=a.stage_dir or None)
+    proc = conn = None
+    seeders = []
     try:
         p = os.path.join(src, "swarm.mkv")
         _write_random(p, total, 99)
-        meta = parse_torrent(make_torrent(p, a.piece_mb << 20))
-        seeders = []
-        for _ in range(a.seeders):
-            c = await TorrentClient(max_uploads=64).start()
-            await c.add_torrent(meta, src)
-            seeders.append(c)
+        raw = make_torrent(p, a.piece_mb << 20)
+        meta = parse_torrent(raw)
+        if getattr(a, "seed_inproc", False):
+            for _ in range(a.seeders):
+                c = await TorrentClient(max_uploads=64).start()
+                await c.add_torrent(meta, src)
+                seeders.append(c)
+            ports = [c.listen_port for c in seeders]
+        else:
+            ctx = mp.get_context("spawn")
+            conn, child = ctx.Pipe()
+            proc = ctx.Process(target=_seed_proc, args=(child, raw, src, a.seeders), daemon=True)
+            proc.start()
+            ports = await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline).start()
+        cpu0 = _self_cpu()
         t0 = time.perf_counter()
-        s = await leech.add_torrent(meta, dst, peers=[("127.0.0.1", c.listen_port) for c in seeders])
+        s = await leech.add_torrent(meta, dst, peers=[("127.0.0.1", port) for port in ports])
         await asyncio.wait_for(s.wait(), 1800)
         dt = time.perf_counter() - t0
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
-               "piece_len": a.piece_mb << 20, "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
-               "hash_fails": s.stats["hash_fails"]}
+               "seeders_in_process": bool(seeders), "piece_len": a.piece_mb << 20,
+               "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
+               "leech_cpu_s": round(_self_cpu() - cpu0, 2), "hash_fails": s.stats["hash_fails"]}
         await leech.close()
-        for c in seeders:
-            await c.close()
         return out
     finally:
+        for c in seeders:
+            await c.close()
+        if proc is not None:
+            try:
+                conn.send("stop")
+            except (OSError, ValueError):
+                pass
+            proc.join(timeout=30)
+            if proc.is_alive():
+                proc.kill()
         shutil.rmtree(src, ignore_errors=True)
         shutil.rmtree(dst, ignore_errors=True)
 
@@ -351,6 +394,8 @@ def main(argv=None) -> int:
                     help="1, 3, 4, 5 (BASELINE.json) or 6 (peer-wire swarm, extra)")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
+    ap.add_argument("--seed-inproc", action="store_true",
+                    help="config 6: seeders on the measuring process's event loop (round 1)")
     ap.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")

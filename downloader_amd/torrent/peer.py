@@ -211,14 +211,7 @@ class PeerConn:
             if self.s.client.dht is not None and self.supports_dht:
                 await self.send(PORT, struct.pack(">H", self.s.client.dht.port))
             while not self.closed:
-                n = struct.unpack(">I", await read(4))[0]
-                self.last_rx = time.monotonic()
-                if n == 0:
-                    continue
-                if n > MAX_MSG:
-                    raise ProtocolError(f"message too large ({n})")
-                body = await read(n)
-                await self._dispatch(body[0], memoryview(body)[1:])
+                await self._read_batch(read)
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError, OSError,
                 ProtocolError):
             pass
@@ -232,6 +225,41 @@ class PeerConn:
             wd.cancel()
             self.close()
             self.s.peer_closed(self)
+
+    async def _read_batch(self, readexactly) -> None:
+        """Read whatever the socket has (up to 1 MiB) and dispatch every message in it as a
+        view of that one immutable chunk: no await and no copy per message (a 16 KiB block
+        is copied once, into its piece). A message cut by the chunk's end is completed with
+        ``readexactly`` and copied once."""
+        data = await self.reader.read(1 << 20)
+        if not data:
+            raise asyncio.IncompleteReadError(b"", 4)
+        self.last_rx = time.monotonic()
+        mv = memoryview(data)
+        end, pos = len(data), 0
+        while pos < end:
+            if end - pos < 4:                              # a cut length prefix
+                hdr = bytes(mv[pos:]) + await readexactly(4 - (end - pos))
+                n = int.from_bytes(hdr, "big")
+                if n > MAX_MSG:
+                    raise ProtocolError(f"message too large ({n})")
+                if n:
+                    body = await readexactly(n)
+                    await self._dispatch(body[0], memoryview(body)[1:])
+                return
+            n = int.from_bytes(mv[pos:pos + 4], "big")
+            if n > MAX_MSG:
+                raise ProtocolError(f"message too large ({n})")
+            pos += 4
+            if n == 0:                                     # keep-alive
+                continue
+            if end - pos >= n:
+                await self._dispatch(mv[pos], mv[pos + 1:pos + n])
+                pos += n
+            else:                                          # a cut message body
+                body = bytes(mv[pos:]) + await readexactly(n - (end - pos))
+                await self._dispatch(body[0], memoryview(body)[1:])
+                return
 
     def attach_meta(self) -> None:
         """Called when metadata becomes known (magnet): materialise the bitfield."""
