@@ -796,3 +796,41 @@ def test_piece_picker_buckets_and_interest_counts():
         pk.piece_done(i)
     assert pk._take_rarest(full) == -1 and not pk.peer_has_wanted(full, 0)
     assert _t.perf_counter() - t0 < 2.0
+
+
+def test_peer_read_batch_handles_every_split(run):
+    """Messages cut anywhere by the socket (inside the length prefix, inside the body,
+    keep-alives in between) come out whole and in order from the chunk parser."""
+    from downloader_amd.torrent.peer import PeerConn
+
+    msgs = [(7, b"\x00\x00\x00\x01\x00\x00\x40\x00" + bytes(range(256)) * 64), (4, b"\x00\x00\x00\x09"),
+            (1, b""), (20, b"\x00d1:md11:ut_metadatai1eee"), (7, b"\x00" * 8 + b"z" * 100)]
+    wire = b""
+    for mid, body in msgs:
+        wire += len(body + b"x").to_bytes(4, "big") + bytes([mid]) + body
+        wire += b"\x00\x00\x00\x00"                                  # keep-alive
+
+    async def go():
+        for cut in list(range(1, 12)) + [4096, 16393, 16400, len(wire) - 3]:
+            reader = asyncio.StreamReader(limit=1 << 22)
+            pc = PeerConn.__new__(PeerConn)
+            pc.reader = reader
+            got = []
+
+            async def disp(mid, p, got=got):
+                got.append((mid, bytes(p)))
+            pc._dispatch = disp
+            parts = [wire[i:i + cut] for i in range(0, len(wire), cut)]
+
+            async def feed():
+                for part in parts:
+                    reader.feed_data(part)
+                    await asyncio.sleep(0)
+                reader.feed_eof()
+            f = asyncio.ensure_future(feed())
+            with pytest.raises(asyncio.IncompleteReadError):
+                while True:
+                    await pc._read_batch(reader.readexactly)
+            await f
+            assert got == msgs, cut
+    run(go())
