@@ -22,6 +22,7 @@ from typing import Optional, Tuple
 from urllib.parse import urlsplit
 
 from ..net.http import FileSink, HttpError, Progress, TransportSet
+from ..net.proxy import ProxyConfig
 from ..stages.select import node_extname
 from ..utils.log import Logger, NullLogger
 
@@ -58,10 +59,11 @@ async def _watch(progress: Progress, min_rate: float, window: float, task: async
             last_b, last_t = b, now
 
 
-async def probe(t: TransportSet, url: str) -> Tuple[int, bool, str]:
+async def probe(t: TransportSet, url: str, proxy: Optional[ProxyConfig] = None
+                ) -> Tuple[int, bool, str]:
     """HEAD (redirects followed) -> (content_length or -1, accepts byte ranges, final URL)."""
     try:
-        r = await t.request("HEAD", url, expect_body=False)
+        r = await t.request("HEAD", url, expect_body=False, proxy=proxy)
     except Exception:
         return -1, False, url
     if not r.ok:
@@ -74,7 +76,8 @@ async def probe(t: TransportSet, url: str) -> Tuple[int, bool, str]:
 async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                       min_split: int = 32 << 20, progress: Optional[Progress] = None,
                       min_rate: float = 0.0, stall_window: float = 30.0,
-                      logger: Optional[Logger] = None) -> int:
+                      logger: Optional[Logger] = None,
+                      proxy: Optional[ProxyConfig] = None) -> int:
     """Download ``url`` to ``path`` through ``path + '.part'`` (renamed when complete).
 
     Resume (the reference restarts from byte 0): completed byte ranges are
@@ -83,7 +86,7 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     supports ``Range``. A complete ``path`` of the advertised size is reused as is."""
     log = logger or NullLogger()
     progress = progress or Progress()
-    size, ranges, url = await probe(t, url)    # later GETs go straight to the final URL
+    size, ranges, url = await probe(t, url, proxy)    # later GETs go to the final URL
     if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
         log.info("resume: file already complete", path=path)
         return 0
@@ -104,7 +107,7 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
 
             async def part(off: int, ln: int) -> int:
                 r = await t.request("GET", url, headers=[("Range", f"bytes={off}-{off + ln - 1}")],
-                                    sink=FileSink(fd, off, ln), progress=progress)
+                                    sink=FileSink(fd, off, ln), progress=progress, proxy=proxy)
                 if r.status != 206:
                     raise HttpDownloadError(f"range request got HTTP {r.status}")
                 if r.written != ln:
@@ -123,7 +126,7 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
             hdrs = [("Range", f"bytes={have}-")] if have else []
             if have:
                 log.info("resume: continuing partial download", offset=have, size=size)
-            task = asyncio.ensure_future(t.request("GET", url, headers=hdrs,
+            task = asyncio.ensure_future(t.request("GET", url, headers=hdrs, proxy=proxy,
                                                    sink=FileSink(fd, have), progress=progress))
             r = await _guard(task, progress, min_rate, stall_window)
             if not r.ok or (have and r.status != 206):

@@ -26,6 +26,8 @@ from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
 from urllib.parse import quote, urljoin, urlsplit
 
+from .proxy import Proxy, ProxyConfig
+
 Headers = Sequence[Tuple[str, str]]
 
 REDIRECTS = (301, 302, 303, 307, 308)
@@ -119,6 +121,17 @@ def redirect_headers(url: str, nxt: str, headers: Headers) -> List[Tuple[str, st
             if k.lower() != "host" and (same or k.lower() != "authorization")]
 
 
+def _via_proxy(proxy: Proxy, url: str, headers: Headers
+               ) -> Tuple[str, int, str, List[Tuple[str, str]]]:
+    """Connect target, absolute-form request target and headers for a plain-http request
+    through a forward proxy (RFC 7230 5.3.2)."""
+    target = url.split("#", 1)[0]
+    hdrs = list(headers)
+    if proxy.auth:
+        hdrs.append(("Proxy-Authorization", proxy.auth))
+    return proxy.host, proxy.port, target, hdrs
+
+
 def split_host(url: str) -> Tuple[str, str, int, str]:
     u = urlsplit(url)
     scheme = u.scheme or "http"
@@ -149,7 +162,8 @@ def _build_head(method: str, host_hdr: str, path: str, headers: Headers,
 class Transport:
     async def request(self, method: str, url: str, headers: Headers = (),
                       body: Union[None, bytes, FileRange] = None, sink: Optional[FileSink] = None,
-                      progress: Optional[Progress] = None, expect_body: bool = True) -> Response:
+                      progress: Optional[Progress] = None, expect_body: bool = True,
+                      proxy: Optional[Proxy] = None) -> Response:
         raise NotImplementedError
 
     async def close(self) -> None:
@@ -242,11 +256,14 @@ class NativeTransport(Transport):
 
     async def request(self, method: str, url: str, headers: Headers = (),
                       body: Union[None, bytes, FileRange] = None, sink: Optional[FileSink] = None,
-                      progress: Optional[Progress] = None, expect_body: bool = True) -> Response:
+                      progress: Optional[Progress] = None, expect_body: bool = True,
+                      proxy: Optional[Proxy] = None) -> Response:
         scheme, host, port, path = split_host(url)
         if scheme != "http":
             raise ValueError("NativeTransport handles plain http:// only")
         host_hdr = host if port == 80 else f"{host}:{port}"
+        if proxy is not None:      # absolute-form request target to the forward proxy
+            host, port, path, headers = _via_proxy(proxy, url, headers)
         nprog = None
         if progress is not None:
             if progress.native is None:
@@ -278,11 +295,15 @@ class NativeTransport(Transport):
             self._slots.pop(slot, None)
 
     def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
-               length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None
+               length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None,
+               src_proxy: Optional[Proxy] = None
                ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         _, sh, sp, spath = split_host(src_url)
         _, dh, dp, dpath = split_host(dst_url)
-        get_head = _build_head("GET", sh if sp == 80 else f"{sh}:{sp}", spath, src_headers, None)
+        src_host_hdr = sh if sp == 80 else f"{sh}:{sp}"
+        if src_proxy is not None:
+            sh, sp, spath, src_headers = _via_proxy(src_proxy, src_url, src_headers)
+        get_head = _build_head("GET", src_host_hdr, spath, src_headers, None)
         put_head = _build_head("PUT", dh if dp == 80 else f"{dh}:{dp}", dpath, dst_headers, length)
         src, _ = self._acquire(sh, sp)
         self._track(slot, src)
@@ -319,7 +340,8 @@ class NativeTransport(Transport):
 
     async def relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
                     length: int, progress: Optional[Progress] = None,
-                    split: Optional[Tuple[int, int, int]] = None
+                    split: Optional[Tuple[int, int, int]] = None,
+                    src_proxy: Optional[ProxyConfig] = None
                     ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         """GET ``src_url`` and stream exactly ``length`` body bytes as the body of a PUT to
         ``dst_url`` without touching user space (socket -> pipe -> socket splice). The PUT is
@@ -336,8 +358,9 @@ class NativeTransport(Transport):
         loop = asyncio.get_running_loop()
         for _ in range(MAX_REDIRECTS + 1):
             slot = self._new_slot()
+            px = src_proxy.for_url(src_url) if src_proxy is not None else None
             fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
-                                       dst_headers, length, nprog, slot, split)
+                                       dst_headers, length, nprog, slot, split, px)
             try:
                 out = await asyncio.shield(fut)
             except asyncio.CancelledError:
@@ -394,7 +417,8 @@ class AiohttpTransport(Transport):
 
     async def request(self, method: str, url: str, headers: Headers = (),
                       body: Union[None, bytes, FileRange] = None, sink: Optional[FileSink] = None,
-                      progress: Optional[Progress] = None, expect_body: bool = True) -> Response:
+                      progress: Optional[Progress] = None, expect_body: bool = True,
+                      proxy: Optional[Proxy] = None) -> Response:
         import aiohttp
         sess = await self._sess()
         hdrs = [(k, v) for k, v in headers if k.lower() != "host"]
@@ -405,7 +429,8 @@ class AiohttpTransport(Transport):
         loop = asyncio.get_running_loop()
         try:
             async with sess.request(method, url, headers=hdrs, data=data,
-                                    allow_redirects=False, compress=None) as resp:
+                                    allow_redirects=False, compress=None,
+                                    proxy=proxy.url if proxy is not None else None) as resp:
                 rh = [(k.lower(), v) for k, v in resp.headers.items()]
                 final = str(resp.url)
                 if sink is not None and 200 <= resp.status < 300:
@@ -474,13 +499,15 @@ class TransportSet:
         return self.fallback
 
     async def request(self, method: str, url: str, follow_redirects: bool = True,
-                      **kw) -> Response:
+                      proxy: Optional[ProxyConfig] = None, **kw) -> Response:
+        """``proxy``: the source-fetch proxy policy (``net/proxy.py``), resolved per hop;
+        S3 and torrent traffic pass none."""
         if method not in ("GET", "HEAD") or not follow_redirects:
-            r = await self.for_url(url).request(method, url, **kw)
+            r = await self._one(method, url, proxy, kw)
             r.url = r.url or url
             return r
         for _ in range(MAX_REDIRECTS + 1):
-            r = await self.for_url(url).request(method, url, **kw)
+            r = await self._one(method, url, proxy, kw)
             r.url = r.url or url
             nxt = redirect_target(r.url, r)
             if nxt is None:
@@ -488,6 +515,12 @@ class TransportSet:
             kw["headers"] = redirect_headers(r.url, nxt, kw.get("headers") or ())
             url = nxt
         raise TransportError(f"{method} {url}: more than {MAX_REDIRECTS} redirects", 310)
+
+    async def _one(self, method: str, url: str, proxy: Optional[ProxyConfig], kw) -> Response:
+        px = proxy.for_url(url) if proxy is not None else None
+        if px is not None:
+            return await self.for_url(url).request(method, url, proxy=px, **kw)
+        return await self.for_url(url).request(method, url, **kw)
 
     async def close(self) -> None:
         if self.native is not None:

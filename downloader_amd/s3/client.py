@@ -335,7 +335,7 @@ class S3Client:
 
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                          src_url: str, offset: int, length: int, whole: bool,
-                         progress: Optional[Progress], split=None):
+                         progress: Optional[Progress], split=None, src_proxy=None):
         """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
         (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``."""
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
@@ -344,7 +344,8 @@ class S3Client:
             url, hdrs = self._signed("PUT", bucket, key, query)
             try:
                 get, put, _, hashed = await self.t.native.relay(src_url, src_hdrs, url, hdrs,
-                                                                length, progress, split)
+                                                                length, progress, split,
+                                                                src_proxy=src_proxy)
             except TransportError as e:
                 err: Exception = e
                 retry = True
@@ -365,11 +366,13 @@ class S3Client:
 
     async def relay_object(self, bucket: str, key: str, src_url: str, size: int,
                            progress: Optional[Progress] = None,
-                           concurrency: Optional[int] = None) -> str:
+                           concurrency: Optional[int] = None, src_proxy=None) -> str:
         """Stage ``src_url`` (``size`` bytes, Range-capable origin) straight into S3: each
-        multipart part is one Range GET relayed socket->socket into one UploadPart."""
+        multipart part is one Range GET relayed socket->socket into one UploadPart.
+        ``src_proxy``: the source-fetch proxy policy (``net/proxy.ProxyConfig``)."""
         if size <= self.multipart_threshold:
-            return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress)
+            return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
+                                         src_proxy=src_proxy)
         parts = self.plan_parts(size)
         upload_id = await self.create_multipart_upload(bucket, key)
         sem = asyncio.Semaphore(concurrency or self.max_inflight_parts)
@@ -379,7 +382,7 @@ class S3Client:
             async with sem:
                 etags[num] = await self._relay_put(
                     bucket, key, [("partNumber", str(num)), ("uploadId", upload_id)], src_url,
-                    off, ln, False, progress)
+                    off, ln, False, progress, src_proxy=src_proxy)
         try:
             await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts))
             return await self.complete_multipart_upload(bucket, key, upload_id,

@@ -16,6 +16,7 @@ from ..fetch import http as http_src
 from ..fetch import local as file_src
 from ..models import api, keys
 from ..net.http import Progress
+from ..net.proxy import ProxyConfig
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket)
 from .jobdir import JobDir, dir_name
@@ -31,6 +32,7 @@ class DownloadStage(Stage):
         self.cfg = cfg
         self.sv = services
         self.root = cfg.resolved_download_root()
+        self.proxy = ProxyConfig(cfg.download.http_proxy)
         self.methods: Dict[str, Backend] = {
             "torrent": self.torrent,
             "http": self.http,
@@ -102,7 +104,7 @@ class DownloadStage(Stage):
         prog = Progress()
         n = await http_src.download_to(self.sv.transports, url, out, d.http_streams,
                                        d.http_min_split, prog, d.http_min_rate,
-                                       min(60.0, d.http_timeout_s), job.logger)
+                                       min(60.0, d.http_timeout_s), job.logger, self.proxy)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("http", n)
 
@@ -116,13 +118,14 @@ class DownloadStage(Stage):
         s3 = self.sv.s3
         if not s3.can_relay(url) or not select_from_config(self.cfg).accepts_single_file(name):
             return False
-        size, ranges, final = await http_src.probe(self.sv.transports, url)
+        size, ranges, final = await http_src.probe(self.sv.transports, url, self.proxy)
         if size <= 0 or (size > s3.multipart_threshold and not ranges) or not s3.can_relay(final):
             return False
         await ensure_staging_bucket(self.sv)
         key = keys.object_key(job.id, name)
         job.logger.info("streaming http source straight to staging", key=key, size=size)
-        await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress())
+        await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress(),
+                              src_proxy=self.proxy)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
         job.stats.setdefault("streamed", []).append(
             {"file": os.path.join(path, name), "key": key, "size": size, "virtual": True})

@@ -95,6 +95,9 @@ class DownloadConfig(BaseModel):
     http_timeout_s: float = 300.0
     http_min_rate: float = 0.0                  # bytes/s stall floor, 0 = off
     http_native: bool = True                    # native splice() transport for http://
+    # Forward proxy for http(s) SOURCE fetches, as request@2 does: "env" = HTTP_PROXY /
+    # HTTPS_PROXY / NO_PROXY, "" = never, or http://[user:pass@]host:port (net/proxy.py).
+    http_proxy: str = "env"
     # Single selector-approved HTTP file -> relayed origin->S3 socket-to-socket (no disk hop).
     stream_http: bool = True
     # Torrents: stage selected files part by part while the torrent is still downloading.

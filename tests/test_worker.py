@@ -568,3 +568,102 @@ def test_http_sources_follow_redirects(run, make_cfg, origin_cls):
         assert w.results[1].outcome == "dead" and "redirect" in w.results[1].error
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+class _ForwardProxy:
+    """Minimal HTTP/1.1 forward proxy for tests: absolute-form requests only, one request
+    per client connection (answers with Connection: close), records what it forwarded."""
+
+    def __init__(self):
+        self.seen = []          # (request line, Proxy-Authorization)
+        self.server = None
+        self.port = 0
+
+    async def start(self):
+        self.server = await asyncio.start_server(self._client, "127.0.0.1", 0)
+        self.port = self.server.sockets[0].getsockname()[1]
+        return self
+
+    async def _client(self, r, w):
+        from urllib.parse import urlsplit
+        try:
+            head = await r.readuntil(b"\r\n\r\n")
+            lines = head.decode("latin-1").split("\r\n")
+            method, target, ver = lines[0].split(" ")
+            auth = next((ln.split(":", 1)[1].strip() for ln in lines[1:]
+                         if ln.lower().startswith("proxy-authorization:")), "")
+            self.seen.append((lines[0], auth))
+            u = urlsplit(target)
+            keep = [ln for ln in lines[1:] if ln and not ln.lower().startswith(
+                ("proxy-authorization:", "connection:"))]
+            path = (u.path or "/") + ("?" + u.query if u.query else "")
+            req = "\r\n".join([f"{method} {path} {ver}"] + keep + ["Connection: close", "", ""])
+            orr, ow = await asyncio.open_connection(u.hostname, u.port or 80)
+            ow.write(req.encode("latin-1"))
+            await ow.drain()
+            while True:
+                chunk = await orr.read(1 << 16)
+                if not chunk:
+                    break
+                w.write(chunk)
+                await w.drain()
+            ow.close()
+        except Exception:
+            pass
+        finally:
+            w.close()
+
+    async def stop(self):
+        self.server.close()
+        await self.server.wait_closed()
+
+
+def test_http_source_through_forward_proxy(run, make_cfg, origin_cls):
+    """download.http_proxy (request@2 honours HTTP_PROXY): source GETs - stream relay and
+    disk path - go through the proxy in absolute form with Proxy-Authorization; S3 traffic
+    does not."""
+    async def go():
+        proxy = await _ForwardProxy().start()
+        purl = f"http://user:pw@127.0.0.1:{proxy.port}"
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"http_proxy": purl})
+        big = os.urandom(13 * 1024 * 1024 + 1)
+        origin.blobs["/p/big.mkv"] = big
+        await w.submit(api.make_download("px1", "http", origin.url("/p/big.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert w.results[0].stats.get("streamed")
+        assert s3.get("triton-staging", keys.object_key("px1", "big.mkv")) == big
+        await w.stop()
+        cfg = make_cfg(s3.endpoint, download={"http_proxy": purl, "stream_http": False})
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        await w.submit(api.make_download("px2", "http", origin.url("/p/big.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert s3.get("triton-staging", keys.object_key("px2", "big.mkv")) == big
+        lines = [ln for ln, _ in proxy.seen]
+        assert lines and all(f"http://127.0.0.1:{origin.port}/p/big.mkv" in ln for ln in lines)
+        assert {a for _, a in proxy.seen} == {"Basic dXNlcjpwdw=="}
+        assert any(ln.startswith("HEAD ") for ln in lines) and any(ln.startswith("GET ") for ln in lines)
+        assert not any("triton-staging" in ln for ln in lines)
+        await w.stop(); await proxy.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_proxy_env_selection():
+    from downloader_amd.net.proxy import ProxyConfig, proxy_from_env
+    env = {"HTTP_PROXY": "http://p:3128", "NO_PROXY": ".internal, cdn.example.com:8080,x.org"}
+    assert proxy_from_env("http://a.example.com/x", env).port == 3128
+    assert proxy_from_env("http://h.internal/x", env) is None
+    assert proxy_from_env("http://internal/x", env) is None
+    assert proxy_from_env("http://cdn.example.com:8080/x", env) is None
+    assert proxy_from_env("http://cdn.example.com/x", env) is not None        # port differs
+    assert proxy_from_env("http://sub.x.org/x", env) is None
+    assert proxy_from_env("http://127.0.0.1:9/x", env) is None                 # loopback
+    assert proxy_from_env("https://a.example.com/x", env).host == "p"          # https -> HTTP_PROXY
+    assert proxy_from_env("https://a.b/x", {"HTTPS_PROXY": "s:1", "HTTP_PROXY": "p:2"}).host == "s"
+    assert proxy_from_env("http://a.b/x", {"http_proxy": "p:2", "NO_PROXY": "*"}) is None
+    assert proxy_from_env("http://a.b/x", {}) is None
+    assert ProxyConfig("").for_url("http://a.b/") is None
+    assert ProxyConfig("http://u:p@q:8").for_url("http://127.0.0.1/").auth.startswith("Basic ")
+    assert ProxyConfig("env", {"HTTP_PROXY": "p:1"}).for_url("http://a.b/").port == 1
