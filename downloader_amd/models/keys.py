@@ -13,6 +13,7 @@ reproduced exactly here.
 from __future__ import annotations
 
 import base64
+import mimetypes
 import os
 
 STAGING_BUCKET = "triton-staging"
@@ -62,3 +63,19 @@ def object_key(media_id: str, file_path: str) -> str:
 
 def done_key(media_id: str) -> str:
     return node_join(media_id, "original/", "done")
+
+
+# mime-db types of the media the selector keeps (lib/process.js:15-20): minio-js 7's
+# fPutObject looks the Content-Type up from the file name with mime-types (yarn.lock:2162).
+_MEDIA_TYPES = {".mkv": "video/x-matroska", ".mp4": "video/mp4", ".mov": "video/quicktime",
+                ".webm": "video/webm"}
+DEFAULT_CONTENT_TYPE = "application/octet-stream"
+
+
+def content_type(file_path: str) -> str:
+    """Content-Type minio-js would send for ``file_path`` (by extension, lower-cased)."""
+    ext = os.path.splitext(file_path)[1].lower()
+    if ext in _MEDIA_TYPES:
+        return _MEDIA_TYPES[ext]
+    return mimetypes.guess_type("x" + ext)[0] or DEFAULT_CONTENT_TYPE if ext else \
+        DEFAULT_CONTENT_TYPE

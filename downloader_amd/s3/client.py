@@ -232,16 +232,19 @@ class S3Client:
 
     async def fput_object(self, bucket: str, key: str, path: str,
                           progress: Optional[Progress] = None, resume: bool = False,
-                          concurrency: Optional[int] = None) -> str:
+                          concurrency: Optional[int] = None, content_type: str = "") -> str:
+        """minio-js ``fPutObject``: one PUT up to the multipart threshold, else a multipart
+        upload; ``content_type`` goes on the PUT / the multipart initiation."""
         size = os.path.getsize(path)
         fd = os.open(path, os.O_RDONLY | getattr(os, "O_CLOEXEC", 0))
+        hdrs = {"content-type": content_type} if content_type else None
         try:
             if size <= self.multipart_threshold:
                 r = await self._request("PUT", bucket, key, body=FileRange(fd, 0, size),
-                                        progress=progress)
+                                        progress=progress, headers=hdrs)
                 return (r.header("etag") or "").strip('"')
             return await self._multipart(bucket, key, fd, size, path, progress, resume,
-                                         concurrency or self.max_inflight_parts)
+                                         concurrency or self.max_inflight_parts, content_type)
         finally:
             os.close(fd)
 
@@ -274,7 +277,8 @@ class S3Client:
         return out
 
     async def _multipart(self, bucket: str, key: str, fd: int, size: int, path: str,
-                         progress: Optional[Progress], resume: bool, concurrency: int) -> str:
+                         progress: Optional[Progress], resume: bool, concurrency: int,
+                         content_type: str = "") -> str:
         parts = self.plan_parts(size)
         upload_id = None
         done: Dict[int, str] = {}
@@ -283,7 +287,7 @@ class S3Client:
             if upload_id:
                 done = await self._reusable_parts(bucket, key, upload_id, path, parts)
         if not upload_id:
-            upload_id = await self.create_multipart_upload(bucket, key)
+            upload_id = await self.create_multipart_upload(bucket, key, content_type)
         sem = asyncio.Semaphore(concurrency)
         etags: Dict[int, str] = dict(done)
 
@@ -335,13 +339,15 @@ class S3Client:
 
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                          src_url: str, offset: int, length: int, whole: bool,
-                         progress: Optional[Progress], split=None, src_proxy=None):
+                         progress: Optional[Progress], split=None, src_proxy=None,
+                         content_type: str = ""):
         """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
         (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``."""
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
         attempt = 0
         while True:
-            url, hdrs = self._signed("PUT", bucket, key, query)
+            url, hdrs = self._signed("PUT", bucket, key, query,
+                                     {"content-type": content_type} if content_type else None)
             try:
                 get, put, _, hashed = await self.t.native.relay(src_url, src_hdrs, url, hdrs,
                                                                 length, progress, split,
@@ -366,15 +372,16 @@ class S3Client:
 
     async def relay_object(self, bucket: str, key: str, src_url: str, size: int,
                            progress: Optional[Progress] = None,
-                           concurrency: Optional[int] = None, src_proxy=None) -> str:
+                           concurrency: Optional[int] = None, src_proxy=None,
+                           content_type: str = "") -> str:
         """Stage ``src_url`` (``size`` bytes, Range-capable origin) straight into S3: each
         multipart part is one Range GET relayed socket->socket into one UploadPart.
         ``src_proxy``: the source-fetch proxy policy (``net/proxy.ProxyConfig``)."""
         if size <= self.multipart_threshold:
             return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
-                                         src_proxy=src_proxy)
+                                         src_proxy=src_proxy, content_type=content_type)
         parts = self.plan_parts(size)
-        upload_id = await self.create_multipart_upload(bucket, key)
+        upload_id = await self.create_multipart_upload(bucket, key, content_type)
         sem = asyncio.Semaphore(concurrency or self.max_inflight_parts)
         etags: Dict[int, str] = {}
 
@@ -397,16 +404,18 @@ class S3Client:
     async def relay_hashed(self, bucket: str, key: str, src_url: str, offset: int, length: int,
                            whole: bool, split: Tuple[int, int, int],
                            part: Optional[Tuple[int, str]] = None,
-                           progress: Optional[Progress] = None):
+                           progress: Optional[Progress] = None, content_type: str = ""):
         """Relay ``length`` bytes of ``src_url`` at ``offset`` into the object ``key`` (or its
         multipart ``part=(number, upload_id)``) while SHA-1-ing the torrent pieces inside it
         (``split``); returns ``(etag, {"digests", "head", "tail"})``."""
         query = [] if part is None else [("partNumber", str(part[0])), ("uploadId", part[1])]
         return await self._relay_put(bucket, key, query, src_url, offset, length, whole,
-                                     progress, split)
+                                     progress, split,
+                                     content_type=content_type if part is None else "")
 
-    async def create_multipart_upload(self, bucket: str, key: str) -> str:
-        r = await self._request("POST", bucket, key, query=[("uploads", "")])
+    async def create_multipart_upload(self, bucket: str, key: str, content_type: str = "") -> str:
+        r = await self._request("POST", bucket, key, query=[("uploads", "")],
+                                headers={"content-type": content_type} if content_type else None)
         return _text(ET.fromstring(r.body), "UploadId")
 
     async def upload_part(self, bucket: str, key: str, upload_id: str, num: int, body,

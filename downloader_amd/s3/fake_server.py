@@ -39,6 +39,7 @@ class StoredObject:
 @dataclass
 class Upload:
     key: str
+    content_type: str = "application/octet-stream"
     parts: Dict[int, Tuple[bytes, str]] = field(default_factory=dict)
     initiated: float = field(default_factory=time.time)
 
@@ -277,7 +278,7 @@ class FakeS3:
         m = req.method
         if m == "POST" and "uploads" in q:
             uid = secrets.token_hex(16)
-            ups[uid] = Upload(key)
+            ups[uid] = Upload(key, req.headers.get("Content-Type", "application/octet-stream"))
             return _xml(f'<InitiateMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
                         f"<Key>{escape(key)}</Key><UploadId>{uid}</UploadId>"
                         "</InitiateMultipartUploadResult>")
@@ -331,7 +332,7 @@ class FakeS3:
                     md5s += bytes.fromhex(got[1])
                 data = b"".join(datas)
                 etag = f"{hashlib.md5(md5s).hexdigest()}-{len(want)}"
-                objs[key] = StoredObject(data, etag)
+                objs[key] = StoredObject(data, etag, content_type=up.content_type)
                 del ups[q["uploadId"]]
                 return _xml(f'<CompleteMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}'
                             f"</Bucket><Key>{escape(key)}</Key><ETag>&quot;{etag}&quot;</ETag>"

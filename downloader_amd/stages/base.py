@@ -16,7 +16,7 @@ import asyncio
 from dataclasses import dataclass, field
 from typing import Any, Awaitable, Callable, Dict, List
 
-from ..models import api
+from ..models import api, keys
 from ..utils.log import Logger, NullLogger
 
 
@@ -119,3 +119,9 @@ async def ensure_staging_bucket(sv: Services) -> None:
         if not sv.extra.get("bucket_ready"):
             await sv.s3.ensure_bucket(sv.config.s3.bucket)
             sv.extra["bucket_ready"] = True
+
+
+def media_type(cfg, path: str) -> str:
+    """Content-Type for a staged file: by extension like minio-js ``fPutObject``
+    (``s3.content_type_by_extension``), else "" (S3 then stores application/octet-stream)."""
+    return keys.content_type(path) if cfg.s3.content_type_by_extension else ""

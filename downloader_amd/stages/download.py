@@ -18,7 +18,7 @@ from ..models import api, keys
 from ..net.http import Progress
 from ..net.proxy import ProxyConfig
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
-                   ensure_staging_bucket)
+                   ensure_staging_bucket, media_type)
 from .jobdir import JobDir, dir_name
 from .select import select_from_config
 
@@ -125,7 +125,7 @@ class DownloadStage(Stage):
         key = keys.object_key(job.id, name)
         job.logger.info("streaming http source straight to staging", key=key, size=size)
         await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress(),
-                              src_proxy=self.proxy)
+                              src_proxy=self.proxy, content_type=media_type(self.cfg, name))
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
         job.stats.setdefault("streamed", []).append(
             {"file": os.path.join(path, name), "key": key, "size": size, "virtual": True})

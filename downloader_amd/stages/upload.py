@@ -19,7 +19,7 @@ from typing import Any, Dict, List
 
 from ..models import keys
 from ..net.http import Progress
-from .base import DOWNLOADING, Job, Services, Stage, ensure_staging_bucket
+from .base import DOWNLOADING, Job, Services, Stage, ensure_staging_bucket, media_type
 from .jobdir import get_reaper
 
 
@@ -77,7 +77,8 @@ class UploadStage(Stage):
                         size = streamed[f]["size"]
                     else:
                         await self.sv.s3.fput_object(bucket, k, f, progress=prog,
-                                                     resume=self.cfg.s3.resume_uploads)
+                                                     resume=self.cfg.s3.resume_uploads,
+                                                     content_type=media_type(self.cfg, f))
                         size = os.path.getsize(f)
                     uploaded.append(size)
                     if self.sv.metrics is not None:

@@ -22,6 +22,7 @@ from typing import Dict, List, Optional, Set, Tuple
 
 from ..models import keys
 from ..net.http import FileRange
+from ..stages.base import media_type
 
 
 @dataclass
@@ -109,12 +110,15 @@ class EagerUploader:
                     f.fd = os.open(f.path, os.O_RDONLY | getattr(os, "O_CLOEXEC", 0))
                 if f.single:
                     body = FileRange(f.fd, 0, f.size) if f.size else b""
-                    await self.s3._request("PUT", self.bucket, f.key, body=body)
+                    ct = media_type(self.cfg, f.path)
+                    await self.s3._request("PUT", self.bucket, f.key, body=body,
+                                           headers={"content-type": ct} if ct else None)
                     f.etags[num] = "single"
                 else:
                     async with f.lock:
                         if not f.upload_id:
-                            f.upload_id = await self.s3.create_multipart_upload(self.bucket, f.key)
+                            f.upload_id = await self.s3.create_multipart_upload(
+                                self.bucket, f.key, media_type(self.cfg, f.path))
                     f.etags[num] = await self.s3.upload_part(self.bucket, f.key, f.upload_id, num,
                                                              FileRange(f.fd, off, ln))
                 self.uploaded_bytes += ln

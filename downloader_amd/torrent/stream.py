@@ -31,6 +31,7 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set, Tuple
 
 from ..models import keys
+from ..stages.base import media_type
 from ..net.http import TransportError
 from .metainfo import Metainfo
 from .session import TorrentError, webseed_url
@@ -140,6 +141,7 @@ class StreamStager:
         self.plen = meta.piece_length
         self.parallel = max(1, parallel)
         self.max_failures = max(1, max_failures)
+        self.cfg = cfg
         self.trim_idle_s = float(getattr(getattr(cfg, "download", None),
                                          "relay_pool_idle_trim_s", 0.0) or 0.0)
         index = {os.path.abspath(p): i for i, (p, _) in enumerate(meta.local_files(root))}
@@ -224,8 +226,9 @@ class StreamStager:
         try:
             for t in self.targets:
                 if t.size == 0:
-                    await self.s3.put_object(self.bucket, t.key, b"")
-            ids = await asyncio.gather(*(self.s3.create_multipart_upload(self.bucket, t.key)
+                    await self.s3.put_object(self.bucket, t.key, b"", self._ctype(t))
+            ids = await asyncio.gather(*(self.s3.create_multipart_upload(self.bucket, t.key,
+                                                                         self._ctype(t))
                                          for t in multi))
             for t, uid in zip(multi, ids):
                 t.upload_id = uid
@@ -320,6 +323,9 @@ class StreamStager:
             self.error = e
         self._finished.set()
 
+    def _ctype(self, t: _Target) -> str:
+        return media_type(self.cfg, t.path)
+
     def _base(self, u: _Unit) -> str:
         return self.webseeds[(u.uid + u.attempts) % len(self.webseeds)]
 
@@ -352,7 +358,7 @@ class StreamStager:
         t0 = time.perf_counter()
         etag, h = await self.s3.relay_hashed(
             self.bucket, t.key, url, u.file_off, u.length, whole, (u.skip, u.full, self.plen),
-            part=None if t.single else (u.num, t.upload_id))
+            part=None if t.single else (u.num, t.upload_id), content_type=self._ctype(t))
         self.stats["relay_s"] += time.perf_counter() - t0
         self.fetched_bytes += u.length
         digests = h["digests"]

@@ -54,6 +54,9 @@ class S3Config(BaseModel):
     # Sign with UNSIGNED-PAYLOAD (body never re-read for SHA-256); when False the
     # native hasher computes the payload SHA-256 (minio-js over plain HTTP does that).
     unsigned_payload: bool = True
+    # Content-Type of staged media from the file extension (minio-js fPutObject looks it up
+    # with mime-types: .mkv -> video/x-matroska, ...); False: application/octet-stream.
+    content_type_by_extension: bool = True
     # Keep a failed multipart upload open and, on the retry, re-use the parts whose ETag
     # equals the local MD5 of the same range.
     resume_uploads: bool = True

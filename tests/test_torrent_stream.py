@@ -334,3 +334,45 @@ def test_piece_aligned_part_plan():
             assert (off + o) % plen == 0, (off, size, parts)
     # part size not a multiple of the piece length: the plain plan
     assert c.plan_parts(200 << 20, 5, 3 << 20) == c.plan_parts(200 << 20)
+
+
+def test_staged_objects_carry_media_content_types(run, tmp_path, make_cfg, origin_cls):
+    """minio-js fPutObject sets Content-Type from the file name (mime-types): every staging
+    path - HTTP stream relay, HTTP disk + upload stage, torrent stream staging, torrent eager
+    staging - stores video/x-matroska for .mkv (and octet-stream with the flag off)."""
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        data, _ = await _show(tmp_path, origin)
+        origin.blobs["/h/movie.mkv"] = os.urandom(7 << 20)
+        origin.blobs["/h/clip.mp4"] = os.urandom(1 << 20)
+        jobs = [("ct1", {}, "/h/movie.mkv", "MOVIE"),
+                ("ct2", {"stream_http": False}, "/h/clip.mp4", "MOVIE"),
+                ("ct3", {}, "/t/show.torrent", "TV"),
+                ("ct4", {"torrent_stream": "off"}, "/t/show.torrent", "TV")]
+        for jid, dl, path, typ in jobs:
+            w = _worker(make_cfg, ep, download=dl)
+            await w.start(health=False)
+            await w.submit(api.make_download(jid, "http", origin.url(path), typ))
+            await _wait(w)
+            assert w.results[0].outcome == "staged", w.results[0]
+            await w.stop()
+        objs = s3.objects("triton-staging")
+        assert objs[keys.object_key("ct1", "movie.mkv")].content_type == "video/x-matroska"
+        assert objs[keys.object_key("ct2", "clip.mp4")].content_type == "video/mp4"
+        for jid in ("ct3", "ct4"):
+            assert objs[keys.object_key(jid, "e1.mkv")].content_type == "video/x-matroska"
+            assert objs[keys.object_key(jid, "e2.mkv")].content_type == "video/x-matroska"
+        w = _worker(make_cfg, ep, s3={"content_type_by_extension": False})
+        await w.start(health=False)
+        await w.submit(api.make_download("ct5", "http", origin.url("/h/movie.mkv")))
+        await _wait(w)
+        await w.stop()
+        assert objs is not None and s3.objects("triton-staging")[
+            keys.object_key("ct5", "movie.mkv")].content_type == "application/octet-stream"
+        assert keys.content_type("a/B.MKV") == "video/x-matroska"
+        assert keys.content_type("x.webm") == "video/webm" and keys.content_type("x") == \
+            "application/octet-stream"
+        await s3.stop(); await origin.stop()
+    run(go())
