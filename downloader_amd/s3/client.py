@@ -427,10 +427,26 @@ class S3Client:
 
     async def complete_multipart_upload(self, bucket: str, key: str, upload_id: str,
                                         parts: Sequence[Tuple[int, str]]) -> str:
+        """CompleteMultipartUpload. A lost reply makes the transport retry, and the retry
+        answers NoSuchUpload because the first attempt DID complete: then the object's
+        multipart ETag ("<md5 of part md5s>-<n>") is checked against the parts sent, and a
+        match counts as success instead of failing a job whose object is in place."""
         xml = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>\"{e}\"</ETag></Part>"
                       for n, e in parts)
         body = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
-        r = await self._request("POST", bucket, key, query=[("uploadId", upload_id)], body=body)
+        try:
+            r = await self._request("POST", bucket, key, query=[("uploadId", upload_id)],
+                                    body=body)
+        except S3Error as e:
+            if e.code != "NoSuchUpload":
+                raise
+            try:
+                info = await self.head_object(bucket, key)
+            except S3Error:
+                raise e from None
+            if info.etag != multipart_etag([t for _, t in parts]):
+                raise
+            return info.etag
         root = ET.fromstring(r.body)
         if _strip(root.tag) == "Error":
             raise S3Error(_text(root, "Code"), _text(root, "Message"), 200, key, bucket)
@@ -518,6 +534,17 @@ class S3Client:
             if _text(root, "IsTruncated") != "true":
                 return out
             token = _text(root, "NextContinuationToken")
+            if not token:    # truncated without a continuation token: would loop forever
+                raise S3Error("InvalidResponse", "IsTruncated without NextContinuationToken",
+                              200, "", bucket)
+
+
+def multipart_etag(part_etags: Sequence[str]) -> str:
+    """S3's ETag of a completed multipart object: MD5 of the concatenated binary part MD5s,
+    then ``-<part count>``."""
+    import hashlib
+    md5s = b"".join(bytes.fromhex(e.strip('"')) for e in part_etags)
+    return f"{hashlib.md5(md5s).hexdigest()}-{len(part_etags)}"
 
 
 def object_url_path(bucket: str, key: str) -> str:

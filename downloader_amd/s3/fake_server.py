@@ -54,6 +54,9 @@ class FaultRule:
     code: str = "SlowDown"
     delay_s: float = 0.0
     drop_connection: bool = False
+    # process the request, then drop the connection before the response (a lost reply:
+    # the client cannot tell whether e.g. CompleteMultipartUpload happened)
+    drop_after: bool = False
 
     def matches(self, method: str, path: str, query: str) -> bool:
         return ((self.method == "*" or self.method == method)
@@ -178,8 +181,16 @@ class FakeS3:
                 if req.transport is not None:
                     req.transport.close()
                 raise web.HTTPInternalServerError()
-            if rule.status:
+            if rule.status and not rule.drop_after:
                 return _err(rule.status, rule.code, "injected fault", path)
+        resp = await self._dispatch(req, path, query)
+        if rule is not None and rule.drop_after:
+            if req.transport is not None:
+                req.transport.close()
+            raise web.HTTPInternalServerError()
+        return resp
+
+    async def _dispatch(self, req: web.Request, path: str, query) -> web.StreamResponse:
         body = await req.read() if req.can_read_body else b""
         if self.verify_signatures:
             hdrs = {k.lower(): v for k, v in req.headers.items()}

@@ -667,3 +667,23 @@ def test_proxy_env_selection():
     assert ProxyConfig("").for_url("http://a.b/") is None
     assert ProxyConfig("http://u:p@q:8").for_url("http://127.0.0.1/").auth.startswith("Basic ")
     assert ProxyConfig("env", {"HTTP_PROXY": "p:1"}).for_url("http://a.b/").port == 1
+
+
+def test_complete_multipart_with_lost_reply(run, make_cfg, origin_cls):
+    """CompleteMultipartUpload succeeds on the server but its reply is lost: the client's
+    retry gets NoSuchUpload, finds the object with the matching multipart ETag, and the job
+    is staged instead of failing (and retrying a job whose object is already in place)."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0},
+                                        download={"stream_http": False})
+        blob = os.urandom(13 * 1024 * 1024 + 9)
+        origin.blobs["/lost/reply.mkv"] = blob
+        s3.faults.add(FaultRule(method="POST", query_contains="uploadId", times=1,
+                                drop_after=True))
+        await w.submit(api.make_download("lr1", "http", origin.url("/lost/reply.mkv")))
+        await _wait(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        o = s3.objects("triton-staging")[keys.object_key("lr1", "reply.mkv")]
+        assert o.data == blob and o.etag.endswith("-3")
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
