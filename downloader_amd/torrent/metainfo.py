@@ -122,7 +122,21 @@ def parse_info(info_bytes: bytes, info_hash: Optional[bytes] = None) -> Metainfo
     return _from_info(info, info_bytes, info_hash or hashlib.sha1(info_bytes).digest())
 
 
+MAX_PIECE_LENGTH = 256 << 20     # a piece is buffered whole on the peer path
+
+
 def _from_info(info: Dict[bytes, Any], raw: bytes, ih: bytes) -> Metainfo:
+    """Metainfo from a decoded info dict. The dict comes from a .torrent URL or from peers
+    (ut_metadata): anything malformed is a MetainfoError, never another exception type."""
+    try:
+        return _from_info_checked(info, raw, ih)
+    except MetainfoError:
+        raise
+    except (KeyError, TypeError, ValueError, AttributeError, OverflowError) as e:
+        raise MetainfoError(f"malformed info dict: {type(e).__name__}: {e}") from e
+
+
+def _from_info_checked(info: Dict[bytes, Any], raw: bytes, ih: bytes) -> Metainfo:
     if not isinstance(info, dict):
         raise MetainfoError("info is not a dictionary")
     try:
@@ -132,6 +146,8 @@ def _from_info(info: Dict[bytes, Any], raw: bytes, ih: bytes) -> Metainfo:
         raise MetainfoError(f"info dict missing field: {e}") from e
     if plen <= 0 or len(pieces) % 20:
         raise MetainfoError("bad piece length or pieces field")
+    if plen > MAX_PIECE_LENGTH:
+        raise MetainfoError(f"piece length {plen} above {MAX_PIECE_LENGTH}")
     name = _s(info.get(b"name.utf-8", info.get(b"name")), "torrent")
     files: List[FileEntry] = []
     multi = b"files" in info
@@ -164,11 +180,14 @@ def parse_torrent(data: bytes) -> Metainfo:
         top, info_bytes = decode_torrent(data)
     except BencodeError as e:
         raise MetainfoError(f"not a torrent: {e}") from e
+    if not isinstance(top, dict) or b"info" not in top:
+        raise MetainfoError("not a torrent: no info dictionary")
     m = _from_info(top[b"info"], info_bytes, hashlib.sha1(info_bytes).digest())
     tiers: List[List[str]] = []
-    if b"announce-list" in top:
-        for tier in top[b"announce-list"]:
-            t = [_s(u) for u in tier if u]
+    al = top.get(b"announce-list")
+    if isinstance(al, list):            # a malformed list is ignored, like parse-torrent
+        for tier in al:
+            t = [_s(u) for u in tier if u] if isinstance(tier, list) else []
             if t:
                 tiers.append(t)
     if b"announce" in top and not tiers:

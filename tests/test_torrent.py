@@ -80,6 +80,26 @@ def test_metainfo_rejects_bad_piece_count():
         parse_torrent(raw)
 
 
+@pytest.mark.parametrize("bad", [
+    {"announce": "x"},                                                       # no info
+    {"info": {"name": "x", "piece length": 16384, "pieces": b"A" * 20, "files": [1, 2]}},
+    {"info": {"name": "x", "piece length": 16384, "pieces": b"A" * 20, "files": [{"path": ["a"]}]}},
+    {"info": {"name": "x", "piece length": 16384, "pieces": b"A" * 20, "length": "big"}},
+    {"info": {"name": "x", "piece length": 1 << 30, "pieces": b"A" * 20, "length": 10}},
+    {"info": {"name": "x", "piece length": 16384, "pieces": 7, "length": 10}},
+])
+def test_malformed_metainfo_is_a_metainfo_error(bad):
+    """.torrent files and ut_metadata come from the network: every malformation is a
+    MetainfoError (the job fails cleanly / the peer's metadata is dropped), and a piece
+    length that would make the peer path buffer gigabytes per piece is refused."""
+    with pytest.raises(MetainfoError):
+        parse_torrent(bencode(bad))
+    good = {"info": {"name": "x", "piece length": 16384, "pieces": b"A" * 20, "length": 10},
+            "announce-list": [5, ["http://t/a"]], "url-list": 3}
+    m = parse_torrent(bencode(good))
+    assert m.announce == [["http://t/a"]] and m.url_list == []
+
+
 def test_path_traversal_is_neutralised(tmp_path):
     raw = bencode({"info": {"name": "..", "piece length": 16384, "pieces": b"A" * 20,
                             "files": [{"path": ["..", "etc", "passwd"], "length": 5}]}})
