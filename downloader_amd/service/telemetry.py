@@ -5,12 +5,14 @@ Reference calls: ``telem.emitStatus(jobId, 2)`` on receipt (lib/main.js:68), ``e
 floor(pct/2) every 30 s -> 50 -> floor(50 + 50*i/n) per uploaded file (lib/download.js:255,
 78-88,272; lib/upload.js:48-51). The wire format inside triton-core is INFERRED to be protobuf
 over the broker; here ``api.TelemetryStatus`` / ``api.TelemetryProgress`` are published on
-two queues. ``history`` keeps the emitted sequence for tests and the bench.
+two queues. ``history`` keeps the most recent emitted events (bounded: a long-running worker
+must not grow with every job) for tests, the bench and debugging.
 """
 from __future__ import annotations
 
 import time
-from typing import List, Optional, Tuple
+from collections import deque
+from typing import Deque, List, Optional, Tuple
 
 from ..broker.base import Broker
 from ..models import api
@@ -20,14 +22,16 @@ from ..utils.log import Logger, NullLogger
 class Telemetry:
     def __init__(self, broker: Optional[Broker], status_queue: str = "v1.telemetry.status",
                  progress_queue: str = "v1.telemetry.progress", enabled: bool = True,
-                 logger: Optional[Logger] = None, keep_history: bool = True):
+                 logger: Optional[Logger] = None, keep_history: bool = True,
+                 history_max: int = 100_000):
         self.broker = broker
         self.status_queue = status_queue
         self.progress_queue = progress_queue
         self.enabled = enabled and broker is not None
         self.log = logger or NullLogger()
         self.keep_history = keep_history
-        self.history: List[Tuple[str, str, int, Optional[int], float]] = []
+        self.history: Deque[Tuple[str, str, int, Optional[int], float]] = \
+            deque(maxlen=history_max)
 
     @classmethod
     def from_config(cls, cfg, broker: Optional[Broker], logger: Optional[Logger] = None):

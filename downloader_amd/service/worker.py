@@ -21,8 +21,9 @@ from __future__ import annotations
 
 import asyncio
 import time
+from collections import deque
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Deque, Dict, List, Optional, Tuple
 
 from ..broker.base import Broker, Delivery, make_broker
 from ..models import api, keys
@@ -56,6 +57,9 @@ class JobResult:
     stats: dict = field(default_factory=dict)   # the job's stats (stage timings, torrent, ...)
 
 
+RESULTS_MAX = 10_000
+
+
 def _attempt(headers: Dict[str, Any]) -> int:
     """``x-attempt`` of a delivery. Headers come from whoever published the message: a value
     that is not a small non-negative integer counts as attempt 0 instead of raising before
@@ -87,7 +91,8 @@ class Worker:
                                  self.tracer, self.log)
         self.stages: List[Tuple[str, Stage]] = []
         self.active: Dict[int, ActiveJob] = {}
-        self.results: List[JobResult] = []
+        # most recent outcomes (tests, bench, debugging); bounded for long-running workers
+        self.results: Deque[JobResult] = deque(maxlen=RESULTS_MAX)
         self._consumer: Optional[str] = None
         self._inflight: set = set()
         self._stopping = False

@@ -164,3 +164,21 @@ def test_redirect_target_and_headers():
     hdrs = [("Range", "bytes=0-9"), ("Authorization", "AWS4 x"), ("Host", "h")]
     assert redirect_headers("http://h/a", "http://h/b", hdrs) == hdrs[:2]
     assert redirect_headers("http://h/a", "http://other/b", hdrs) == hdrs[:1]
+
+
+def test_long_running_worker_state_is_bounded(make_cfg):
+    """Per-job records a worker keeps for tests and debugging (results, telemetry history)
+    are bounded, so a worker staging millions of jobs does not grow without limit."""
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.service import worker as wmod
+    from downloader_amd.service.telemetry import Telemetry
+    w = wmod.Worker(make_cfg(), broker=MemoryBroker())
+    assert w.results.maxlen == wmod.RESULTS_MAX
+    for i in range(wmod.RESULTS_MAX + 5):
+        w.results.append(i)
+    assert len(w.results) == wmod.RESULTS_MAX and w.results[0] == 5
+    t = Telemetry(None, history_max=3)
+    import asyncio as _a
+    for i in range(5):
+        _a.run(t.emit_progress("m", 2, i))
+    assert t.progress_of("m") == [2, 3, 4]
