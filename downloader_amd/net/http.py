@@ -21,6 +21,7 @@ from __future__ import annotations
 import asyncio
 import os
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
@@ -172,10 +173,18 @@ class Transport:
 
 class NativeTransport(Transport):
     def __init__(self, max_workers: int = 32, connect_timeout: float = 10.0,
-                 io_timeout: float = 300.0, max_idle_per_host: int = 64):
+                 io_timeout: float = 300.0, max_idle_per_host: int = 64,
+                 idle_ttl: float = 30.0, max_idle_total: int = 512):
         from ..ops import native
         self._n = native()
-        self._pool: Dict[Tuple[str, int], List[object]] = {}
+        # (host, port) -> [(conn, released at)], most recently released last. Idle sockets
+        # expire after idle_ttl (servers drop keep-alive connections anyway) and at most
+        # max_idle_total stay open over all hosts: a long-running worker that fetched from
+        # many origins must not sit on hosts x 64 idle file descriptors.
+        self._pool: Dict[Tuple[str, int], List[Tuple[object, float]]] = {}
+        self.idle_ttl = idle_ttl
+        self.max_idle_total = max_idle_total
+        self._idle_total = 0
         self._lock = threading.Lock()
         self._exec = ThreadPoolExecutor(max_workers=max_workers, thread_name_prefix="xfer")
         # connections of requests in flight (one list per request), so a cancelled request or
@@ -187,10 +196,23 @@ class NativeTransport(Transport):
         self.max_idle = max_idle_per_host
 
     def _acquire(self, host: str, port: int) -> Tuple[object, bool]:
-        with self._lock:
-            idle = self._pool.get((host, port))
-            if idle:
-                return idle.pop(), True
+        stale = []
+        try:
+            with self._lock:
+                idle = self._pool.get((host, port))
+                now = time.monotonic()
+                while idle:
+                    conn, t = idle.pop()
+                    self._idle_total -= 1
+                    if now - t <= self.idle_ttl:
+                        return conn, True
+                    stale.append(conn)         # older ones below it are staler: drop all
+                    stale.extend(c for c, _ in idle)
+                    self._idle_total -= len(idle)
+                    idle.clear()
+        finally:
+            for c in stale:
+                c.close()
         try:
             return self._n.HttpConn(host, port, self.connect_timeout, self.io_timeout), False
         except RuntimeError as e:
@@ -200,12 +222,45 @@ class NativeTransport(Transport):
         if not conn.reusable:
             conn.close()
             return
+        drop = []
         with self._lock:
             idle = self._pool.setdefault((conn.host, conn.port), [])
             if len(idle) < self.max_idle:
-                idle.append(conn)
-                return
-        conn.close()
+                idle.append((conn, time.monotonic()))
+                self._idle_total += 1
+                conn = None
+                if self._idle_total > self.max_idle_total:
+                    drop = self._evict_locked()
+        if conn is not None:
+            conn.close()
+        for c in drop:
+            c.close()
+
+    def _evict_locked(self) -> List[object]:
+        """Over the global idle cap: drop expired sockets everywhere, then the oldest."""
+        now = time.monotonic()
+        out = []
+        for key in list(self._pool):
+            lst = self._pool[key]
+            keep = [(c, t) for c, t in lst if now - t <= self.idle_ttl]
+            out += [c for c, t in lst if now - t > self.idle_ttl]
+            if keep:
+                self._pool[key] = keep
+            else:
+                del self._pool[key]
+        self._idle_total = sum(len(v) for v in self._pool.values())
+        while self._idle_total > self.max_idle_total:
+            key = min(self._pool, key=lambda k: self._pool[k][0][1])
+            c, _ = self._pool[key].pop(0)
+            out.append(c)
+            self._idle_total -= 1
+            if not self._pool[key]:
+                del self._pool[key]
+        return out
+
+    def idle_connections(self) -> int:
+        with self._lock:
+            return self._idle_total
 
     def _track(self, slot: int, conn) -> None:
         with self._lock:
@@ -384,8 +439,9 @@ class NativeTransport(Transport):
 
     async def close(self) -> None:
         with self._lock:
-            conns = [c for v in self._pool.values() for c in v]
+            conns = [c for v in self._pool.values() for c, _ in v]
             self._pool.clear()
+            self._idle_total = 0
             for v in self._slots.values():
                 for c in v:
                     c.abort()   # transfers still running on executor threads fail fast

@@ -1,6 +1,7 @@
 """Config (triton-core/config), dynamics, pino-style logging, tracing, metrics."""
 from __future__ import annotations
 
+import asyncio
 import io
 import json
 import os
@@ -182,3 +183,27 @@ def test_long_running_worker_state_is_bounded(make_cfg):
     for i in range(5):
         _a.run(t.emit_progress("m", 2, i))
     assert t.progress_of("m") == [2, 3, 4]
+
+
+def test_native_pool_idle_ttl_and_global_cap(run, origin_cls):
+    """Idle keep-alive sockets are capped over all hosts and expire after idle_ttl."""
+    from downloader_amd.net.http import NativeTransport
+
+    async def go():
+        origins = [await origin_cls().start() for _ in range(3)]
+        for o in origins:
+            o.blobs["/x"] = b"y" * 100
+        t = NativeTransport(max_workers=4, idle_ttl=0.3, max_idle_total=2)
+        for o in origins:
+            r = await t.request("GET", o.url("/x"))
+            assert r.status == 200 and r.body == b"y" * 100
+        assert t.idle_connections() == 2                    # global cap
+        r = await t.request("GET", origins[2].url("/x"))    # reuses a pooled socket
+        assert r.status == 200 and t.idle_connections() == 2
+        await asyncio.sleep(0.4)
+        r = await t.request("GET", origins[2].url("/x"))    # expired: dropped, fresh socket
+        assert r.status == 200 and t.idle_connections() <= 2
+        await t.close()
+        for o in origins:
+            await o.stop()
+    run(go())
