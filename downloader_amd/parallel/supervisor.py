@@ -25,6 +25,8 @@ class Slot:
     restarts: int = 0
     started: float = 0.0
     backoff: float = 1.0
+    restart_at: float = 0.0          # > 0: respawn due at this monotonic time
+    done: bool = False               # exited 0, or out of restarts: not respawned
     exit_codes: List[int] = field(default_factory=list)
 
 
@@ -53,14 +55,16 @@ def cpu_slices(n_workers: int, cpus_per_worker: int, available: Optional[Sequenc
 
 class Supervisor:
     def __init__(self, n: int, argv: Sequence[str], env: Optional[Dict[str, str]] = None,
-                 cpus_per_worker: int = 0, max_restarts: int = 10, base_port: int = 0):
+                 cpus_per_worker: int = 0, max_restarts: int = 10, base_port: int = 0,
+                 backoff: float = 1.0):
         self.n = n
         self.argv = list(argv)
         self.env = dict(env or os.environ)
         self.cpus = cpu_slices(n, cpus_per_worker)
         self.max_restarts = max_restarts
         self.base_port = base_port
-        self.slots = [Slot(i) for i in range(n)]
+        self.initial_backoff = backoff
+        self.slots = [Slot(i, backoff=backoff) for i in range(n)]
         self.stopping = False
 
     def _spawn(self, s: Slot) -> None:
@@ -82,22 +86,30 @@ class Supervisor:
             self._spawn(s)
 
     def poll(self) -> None:
-        """Restart exited workers (exponential backoff, reset after 60 s of healthy uptime)."""
+        """Reap exited workers once each and respawn crashed ones after an exponential
+        backoff (reset after 60 s of healthy uptime). Never sleeps: a crash-looping worker
+        does not delay the others' restarts or the reaction to SIGTERM."""
+        now = time.monotonic()
         for s in self.slots:
-            if s.proc is None or s.proc.poll() is None or self.stopping:
+            if self.stopping or s.done:
                 continue
-            rc = s.proc.returncode
-            s.exit_codes.append(rc)
-            if rc == 0:
-                continue
-            if s.restarts >= self.max_restarts:
-                continue
-            if time.monotonic() - s.started > 60:
-                s.backoff = 1.0
-            time.sleep(min(s.backoff, 30.0))
-            s.backoff *= 2
-            s.restarts += 1
-            self._spawn(s)
+            if s.proc is not None:
+                if s.proc.poll() is None:
+                    continue
+                rc = s.proc.returncode
+                s.exit_codes.append(rc)
+                s.proc = None
+                if rc == 0 or s.restarts >= self.max_restarts:
+                    s.done = True
+                    continue
+                if now - s.started > 60:
+                    s.backoff = self.initial_backoff
+                s.restart_at = now + min(s.backoff, 30.0)
+                s.backoff *= 2
+            if s.proc is None and s.restart_at and now >= s.restart_at:
+                s.restart_at = 0.0
+                s.restarts += 1
+                self._spawn(s)
 
     def stop(self, timeout: float = 30.0) -> List[int]:
         self.stopping = True
@@ -132,9 +144,7 @@ class Supervisor:
         self.start()
         while not stop["flag"]:
             self.poll()
-            if self.alive() == 0 and all(
-                    s.exit_codes and (s.exit_codes[-1] == 0 or s.restarts >= self.max_restarts)
-                    for s in self.slots):
+            if all(s.done for s in self.slots):
                 break
             time.sleep(0.5)
         codes = self.stop()

@@ -139,3 +139,28 @@ def test_bench_reference_mode_worker_count():
         j = json.loads(r.stdout.strip().splitlines()[-1])
         assert j["mode"] == "reference" and j["procs_per_rank"] == want
         assert j["config"]["jobs_timed"] == 2        # jobs per step are per rank, split over procs
+
+
+def test_supervisor_restarts_crashed_workers_without_blocking():
+    """A worker that keeps crashing is respawned with exponential backoff up to max_restarts
+    and then left down, each exit is recorded once, and a healthy sibling is untouched;
+    poll() never sleeps (the old loop slept through the backoff)."""
+    import time as _t
+
+    from downloader_amd.parallel.supervisor import Supervisor
+    code = ("import os, sys, time\n"
+            "if os.environ['STAGER_WORKER_INDEX'] == '1': time.sleep(30)\n"
+            "sys.exit(3)\n")
+    sup = Supervisor(2, [sys.executable, "-c", code], cpus_per_worker=-1, max_restarts=2,
+                     backoff=0.05)
+    sup.start()
+    t0 = _t.monotonic()
+    while not sup.slots[0].done and _t.monotonic() - t0 < 20:
+        t1 = _t.monotonic()
+        sup.poll()
+        assert _t.monotonic() - t1 < 0.5
+        _t.sleep(0.02)
+    s0, s1 = sup.slots
+    assert s0.done and s0.restarts == 2 and s0.exit_codes == [3, 3, 3]
+    assert s1.proc is not None and s1.proc.poll() is None and not s1.exit_codes
+    assert sup.stop(timeout=10) != []
