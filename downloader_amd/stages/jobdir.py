@@ -44,9 +44,13 @@ def dir_name(job_id: str) -> str:
 
 
 def inside(root: str, path: str) -> bool:
-    """True when ``path`` lies strictly below ``root`` (symlinks resolved)."""
-    r = os.path.realpath(root)
-    p = os.path.realpath(path)
+    """True when ``path`` lies strictly below ``root`` after normalisation (``..``, ``.``,
+    repeated slashes). Lexical on purpose - ``realpath`` costs an lstat per path component
+    on every job - which is sound here: the components under the root are names this
+    module or the job's own stages made (``dir_name``), and a symlink where a job dir should
+    be is never followed by the removal (``shutil.rmtree`` refuses symlinks)."""
+    r = os.path.abspath(root)
+    p = os.path.abspath(path)
     return p != r and os.path.commonpath([r, p]) == r
 
 
@@ -105,6 +109,7 @@ class Reaper:
         self.root = root
         self.background = background
         self.trash = os.path.join(root, ".trash")
+        self._trash_ready = False
         self._pool: Optional[ThreadPoolExecutor] = None
         self._pending: Set[Future] = set()
         self._lock = threading.Lock()
@@ -130,22 +135,26 @@ class Reaper:
         it, whatever a job's id or a stage's result says."""
         if not path or not os.path.lexists(path):
             return None
-        if not inside(self.root, path) or os.path.realpath(path) in (
-                os.path.realpath(self.trash), os.path.realpath(os.path.join(self.root, ".locks"))):
+        if not inside(self.root, path) or os.path.abspath(path) in (
+                os.path.abspath(self.trash), os.path.abspath(os.path.join(self.root, ".locks"))):
             raise ValueError(f"refusing to remove {path!r}: not a job directory under "
                              f"{self.root!r}")
         if not self.background:
             shutil.rmtree(path, ignore_errors=True)
             return None
-        dst = path
         try:
-            os.makedirs(self.trash, exist_ok=True)
+            if not self._trash_ready:
+                os.makedirs(self.trash, exist_ok=True)
+                self._trash_ready = True
             cand = os.path.join(self.trash, f"{os.path.basename(path)}.{secrets.token_hex(4)}")
             os.rename(path, cand)
-            dst = cand
         except OSError:
-            pass   # other filesystem or already gone: delete in place
-        return self._submit(dst)
+            # other filesystem, trash gone, ...: delete in place NOW - a background delete
+            # of the job's own path could remove the directory of a retry that reuses it
+            self._trash_ready = False
+            shutil.rmtree(path, ignore_errors=True)
+            return None
+        return self._submit(cand)
 
     def sweep(self) -> int:
         n = 0

@@ -96,12 +96,11 @@ class UploadStage(Stage):
         job.logger.info("finished uploading all files")
         if download_path:
             try:
-                reaper = get_reaper(self.sv)
-                if reaper.background:
-                    reaper.reap(download_path)    # rename now, unlink in the background
-                else:
-                    await asyncio.get_running_loop().run_in_executor(
-                        None, reaper.reap, download_path)
+                # background: rename into .trash now (the job id's path is free when the
+                # stage returns), unlink later; reference mode: delete inline. Either way
+                # the syscalls run off the event loop.
+                await asyncio.get_running_loop().run_in_executor(
+                    None, get_reaper(self.sv).reap, download_path)
             except (OSError, ValueError) as e:
                 job.logger.warn("err", f"failed to clean up directory: {e}")
         return {"files": files, "keys": sorted(owner), "bytes": sum(uploaded)}
