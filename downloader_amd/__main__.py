@@ -117,8 +117,21 @@ def _verify(args) -> int:
 
 
 def _config(args) -> int:
+    """Print the effective config. Secrets (S3 secret key, broker URL password) are masked
+    unless ``--show-secrets`` (App. A #19: the reference logged bucket:// credentials)."""
+    from urllib.parse import urlsplit, urlunsplit
+
     from .utils.config import load_config
-    print(load_config(path=args.config or None).model_dump_json(indent=2))
+    d = load_config(path=args.config or None).model_dump(mode="json")
+    if not args.show_secrets:
+        if d.get("s3", {}).get("secret_key"):
+            d["s3"]["secret_key"] = "***"
+        url = d.get("broker", {}).get("url") or ""
+        u = urlsplit(url)
+        if u.password:
+            netloc = f"{u.username}:***@{u.hostname}" + (f":{u.port}" if u.port else "")
+            d["broker"]["url"] = urlunsplit(u._replace(netloc=netloc))
+    print(json.dumps(d, indent=2))
     return 0
 
 
@@ -159,6 +172,7 @@ def main(argv=None) -> int:
     v.add_argument("--backend", default="auto", choices=["auto", "cpu", "gpu"])
     c = sub.add_parser("config")
     c.add_argument("--config", default="")
+    c.add_argument("--show-secrets", action="store_true", help="do not mask credentials")
     args = p.parse_args(argv)
     return {"worker": _worker, "supervisor": _supervisor, "broker": _broker, "submit": _submit,
             "make-torrent": _make_torrent, "verify": _verify, "config": _config}[args.cmd](args)

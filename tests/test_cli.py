@@ -39,10 +39,16 @@ def test_make_torrent_and_verify_roundtrip(tmp_path):
 
 
 def test_config_command_prints_effective_config():
-    r = _cli("config", env={"STAGER_S3__BUCKET": "other", "PORT": "4123"})
+    r = _cli("config", env={"STAGER_S3__BUCKET": "other", "PORT": "4123",
+                            "STAGER_S3__SECRET_KEY": "hunter2",
+                            "STAGER_BROKER__URL": "amqp://u:pw@mq:5672/"})
     assert r.returncode == 0, r.stderr
     c = json.loads(r.stdout)
     assert c["s3"]["bucket"] == "other" and c["health"]["port"] == 4123
+    assert "hunter2" not in r.stdout and ":pw@" not in r.stdout     # masked by default
+    assert c["broker"]["url"] == "amqp://u:***@mq:5672/"
+    r = _cli("config", "--show-secrets", env={"STAGER_S3__SECRET_KEY": "hunter2"})
+    assert json.loads(r.stdout)["s3"]["secret_key"] == "hunter2"
 
 
 def test_submit_publishes_download(run):
