@@ -17,6 +17,7 @@ from ..fetch import local as file_src
 from ..models import api, keys
 from ..net.http import Progress
 from ..net.proxy import ProxyConfig
+from ..utils.log import redact_url
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket, media_type)
 from .jobdir import JobDir, dir_name
@@ -82,16 +83,18 @@ class DownloadStage(Stage):
 
     @staticmethod
     def _redact(uri: str, protocol: str) -> str:
+        """The source URI as logged: bucket:// secret keys (App. A #19), URL passwords and
+        signature/token query values of presigned URLs are masked."""
         if protocol.lower() == "bucket":
             try:
                 return bucket_src.parse_bucket_uri(uri).redacted()
             except ValueError:
                 return "bucket://<invalid>"
-        return uri
+        return redact_url(uri)
 
     # ------------------------------------------------------------------ backends
     async def http(self, url: str, job: Job, path: str) -> None:
-        job.logger.info("http", url)
+        job.logger.info("http", redact_url(url))
         if http_src.is_torrent_url(url):
             job.logger.info("downloading a .torrent, chaining to torrent downloader")
             await self.torrent(url, job, path)
@@ -155,7 +158,8 @@ class DownloadStage(Stage):
 
     async def torrent(self, uri: str, job: Job, path: str) -> None:
         from ..torrent.backend import download_torrent
-        short = uri[:25] + "..." if len(uri) > 25 else uri
+        uri_log = redact_url(uri)
+        short = uri_log[:25] + "..." if len(uri_log) > 25 else uri_log
         job.logger.info("url", short)
         n = await download_torrent(uri, job, path, self.cfg, self.sv)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n

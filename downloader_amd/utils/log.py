@@ -9,11 +9,13 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import socket
 import sys
 import threading
 import time
 from typing import Any, Callable, Dict, List, Optional, TextIO
+from urllib.parse import urlsplit, urlunsplit
 
 LEVELS = {"trace": 10, "debug": 20, "info": 30, "warn": 40, "error": 50, "fatal": 60}
 _HOST = socket.gethostname()
@@ -138,3 +140,31 @@ def make_test_logger(name: str = "test") -> Logger:
     """Logger for tests: silent unless ``USE_REAL_LOGGER`` is set (the reference's test switch,
     test/process/filter_dirs.js:19)."""
     return get_logger(name) if os.environ.get("USE_REAL_LOGGER") else NullLogger()
+
+
+_SECRET_PARAM = re.compile(r"(sig|signature|token|secret|password|passwd|credential|auth|key)",
+                           re.IGNORECASE)
+
+
+def redact_url(url: str) -> str:
+    """``url`` for logs: a userinfo password and the values of query parameters that look
+    like secrets (``X-Amz-Signature``, ``X-Amz-Credential``, ``token``, ``sig``, ...) become
+    ``***``; magnets and anything unparsable pass through unchanged."""
+    try:
+        u = urlsplit(url)
+    except ValueError:
+        return url
+    if u.scheme not in ("http", "https"):
+        return url
+    netloc = u.netloc
+    if u.password is not None:
+        host = u.hostname or ""
+        netloc = f"{u.username}:***@{host}" + (f":{u.port}" if u.port else "")
+    query = u.query
+    if query:
+        parts = []
+        for kv in query.split("&"):
+            k, eq, v = kv.partition("=")
+            parts.append(f"{k}=***" if eq and _SECRET_PARAM.search(k) else kv)
+        query = "&".join(parts)
+    return urlunsplit((u.scheme, netloc, u.path, query, u.fragment))

@@ -207,3 +207,15 @@ def test_native_pool_idle_ttl_and_global_cap(run, origin_cls):
         for o in origins:
             await o.stop()
     run(go())
+
+
+def test_redact_url_for_logs():
+    from downloader_amd.utils.log import redact_url
+    u = ("https://u:pw@cdn.example.com:8443/m/x.mkv?X-Amz-Algorithm=AWS4-HMAC-SHA256"
+         "&X-Amz-Credential=AKIA%2F2024&X-Amz-Signature=abc123&partNumber=2&token=t0k")
+    r = redact_url(u)
+    assert "pw" not in r and "abc123" not in r and "AKIA" not in r and "t0k" not in r
+    assert r.startswith("https://u:***@cdn.example.com:8443/m/x.mkv?")
+    assert "X-Amz-Algorithm=AWS4-HMAC-SHA256" in r and "partNumber=2" in r
+    assert redact_url("http://o/x.mkv?size=1") == "http://o/x.mkv?size=1"
+    assert redact_url("magnet:?xt=urn:btih:abc") == "magnet:?xt=urn:btih:abc"
