@@ -187,9 +187,10 @@ class Channel:
             raise C.AMQPError("channel closed")
         fut = None
         if self.confirming:
-            self._publish_seq += 1
-            fut = asyncio.get_running_loop().create_future()
-            self._confirms[self._publish_seq] = fut
+            self._publish_seq += 1            # the broker numbers every publish
+            if wait_confirm:                  # fire-and-forget: no future to leave unread
+                fut = asyncio.get_running_loop().create_future()
+                self._confirms[self._publish_seq] = fut
         data = C.content_frames(self.id, C.method_frame(self.id, C.BASIC_PUBLISH, 0, exchange,
                                                         routing_key, False, False),
                                 bytes(body), props or C.Properties(), self.conn.frame_max)
@@ -494,11 +495,12 @@ class AmqpBroker(Broker):
         await self._ready()
         await self._cons_ch.queue_declare(queue)
 
-    async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None) -> None:
+    async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
+                      confirm: bool = True) -> None:
         await self._ready()
         props = C.Properties(content_type="application/octet-stream", delivery_mode=2,
                              headers=_to_headers(headers))
-        await self._pub_ch.basic_publish("", queue, body, props)
+        await self._pub_ch.basic_publish("", queue, body, props, wait_confirm=confirm)
         if self.metrics is not None:
             self.metrics.messages.labels(queue, "publish").inc()
 

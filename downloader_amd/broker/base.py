@@ -67,7 +67,10 @@ class Broker(abc.ABC):
     async def declare(self, queue: str) -> None: ...
 
     @abc.abstractmethod
-    async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None) -> None: ...
+    async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
+                      confirm: bool = True) -> None:
+        """Publish to ``queue``. ``confirm=False``: do not wait for the broker's publisher
+        confirm (telemetry: a lost progress event must not cost a round trip per event)."""
 
     @abc.abstractmethod
     async def consume(self, queue: str, handler: Handler, prefetch: int = 1) -> str:

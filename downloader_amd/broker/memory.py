@@ -77,7 +77,8 @@ class MemoryBroker(Broker):
     async def declare(self, queue: str) -> None:
         self.queues.setdefault(queue, deque())
 
-    async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None) -> None:
+    async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
+                      confirm: bool = True) -> None:
         if self.fail_publish > 0:
             self.fail_publish -= 1
             raise ConnectionError("injected publish failure")

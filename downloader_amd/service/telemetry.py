@@ -50,7 +50,7 @@ class Telemetry:
             return
         msg = api.TelemetryStatus(mediaId=media_id, status=int(status))
         try:
-            await self.broker.publish(self.status_queue, api.encode(msg))
+            await self.broker.publish(self.status_queue, api.encode(msg), confirm=False)
         except Exception as e:  # telemetry must never fail a job
             self.log.warn("failed to emit status", err=str(e))
 
@@ -61,7 +61,7 @@ class Telemetry:
             return
         msg = api.TelemetryProgress(mediaId=media_id, status=int(status), progress=int(progress))
         try:
-            await self.broker.publish(self.progress_queue, api.encode(msg))
+            await self.broker.publish(self.progress_queue, api.encode(msg), confirm=False)
         except Exception as e:
             self.log.warn("failed to emit progress", err=str(e))
 

@@ -289,3 +289,22 @@ def test_settling_on_a_dead_connection_is_a_noop():
     assert ch.basic_ack(7) is False and ch.basic_nack(7) is False
     ch.closed = True
     assert ch.basic_ack(8) is False
+
+
+def test_fire_and_forget_publishes_keep_confirms_aligned(run):
+    """Telemetry publishes skip the publisher-confirm wait; the broker still numbers them,
+    so a later confirmed publish (the convert message) resolves on ITS confirm."""
+    async def go():
+        srv = await BrokerServer().start()
+        b = AmqpBroker(srv.url)
+        await b.connect()
+        await b.declare("t")
+        await b.declare("c")
+        for i in range(5):
+            await b.publish("t", b"tele%d" % i, confirm=False)
+        await asyncio.wait_for(b.publish("c", b"convert"), 5)
+        assert not b._pub_ch._confirms          # nothing left pending
+        assert srv.depth("t") == 5 and srv.depth("c") == 1
+        await b.close()
+        await srv.stop()
+    run(go())
