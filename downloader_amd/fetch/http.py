@@ -62,15 +62,26 @@ async def _watch(progress: Progress, min_rate: float, window: float, task: async
 async def probe(t: TransportSet, url: str, proxy: Optional[ProxyConfig] = None
                 ) -> Tuple[int, bool, str]:
     """HEAD (redirects followed) -> (content_length or -1, accepts byte ranges, final URL)."""
+    size, ranges, final, _ = await probe_validated(t, url, proxy)
+    return size, ranges, final
+
+
+async def probe_validated(t: TransportSet, url: str, proxy: Optional[ProxyConfig] = None
+                          ) -> Tuple[int, bool, str, str]:
+    """``probe`` plus the response's validator: a strong ``ETag``, else ``Last-Modified``
+    ("" when the origin gives neither). Partial data is only resumed under the same one."""
     try:
         r = await t.request("HEAD", url, expect_body=False, proxy=proxy)
     except Exception:
-        return -1, False, url
+        return -1, False, url, ""
     if not r.ok:
-        return -1, False, url
+        return -1, False, url, ""
     cl = r.header("content-length")
+    etag = (r.header("etag") or "").strip()
+    validator = etag if etag and not etag.startswith("W/") else \
+        ("lm:" + r.header("last-modified") if r.header("last-modified") else "")
     return (int(cl) if cl and cl.isdigit() else -1,
-            (r.header("accept-ranges") or "").lower() == "bytes", r.url or url)
+            (r.header("accept-ranges") or "").lower() == "bytes", r.url or url, validator)
 
 
 async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
@@ -80,18 +91,27 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                       proxy: Optional[ProxyConfig] = None) -> int:
     """Download ``url`` to ``path`` through ``path + '.part'`` (renamed when complete).
 
-    Resume (the reference restarts from byte 0): completed byte ranges are
-    recorded in ``path + '.part.ranges'``; a later attempt with the same job directory skips
-    them, and a single-stream transfer continues from the ``.part`` length when the origin
-    supports ``Range``. A complete ``path`` of the advertised size is reused as is."""
+    Resume (the reference restarts from byte 0): the journal
+    ``path + '.part.ranges'`` records the origin's validator (strong ETag / Last-Modified),
+    its size and the completed byte ranges; a later attempt with the same job directory skips
+    those ranges, or continues a single-stream transfer from the ``.part`` length - but only
+    when the origin still reports the same validator and size (otherwise the partial data
+    belongs to another version of the file and is discarded). A complete ``path`` of the
+    advertised size is reused as is."""
     log = logger or NullLogger()
     progress = progress or Progress()
-    size, ranges, url = await probe(t, url, proxy)    # later GETs go to the final URL
+    size, ranges, url, validator = await probe_validated(t, url, proxy)   # later GETs: final URL
     if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
         log.info("resume: file already complete", path=path)
         return 0
     part_path, state_path = path + ".part", path + ".part.ranges"
-    done = _load_ranges(state_path) if os.path.exists(part_path) else []
+    journal = _load_journal(state_path) if os.path.exists(part_path) else None
+    resumable = bool(journal and validator and journal["validator"] == validator
+                     and journal["size"] == size)
+    if journal and not resumable:
+        log.info("resume: origin changed or unvalidated, restarting", path=path)
+    done = list(journal["ranges"]) if resumable else []
+    _save_journal(state_path, validator, size, done)
     fd = os.open(part_path, os.O_WRONLY | os.O_CREAT | getattr(os, "O_CLOEXEC", 0), 0o644)
     written = 0
     try:
@@ -113,13 +133,14 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                 if r.written != ln:
                     raise HttpDownloadError(f"short range body {r.written} != {ln}")
                 done.append([off, ln])
-                _save_ranges(state_path, done)
+                _save_journal(state_path, validator, size, done)
                 return r.written
 
             task = asyncio.ensure_future(asyncio.gather(*(part(o, ln) for o, ln in todo)))
             written = sum(await _guard(task, progress, min_rate, stall_window))
         else:
-            have = os.fstat(fd).st_size if (ranges and size > 0 and not done) else 0
+            have = os.fstat(fd).st_size if (resumable and ranges and size > 0 and not done) \
+                else 0
             if not (0 < have < size):
                 have = 0
                 os.ftruncate(fd, 0)
@@ -145,19 +166,25 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     return written
 
 
-def _load_ranges(p: str) -> list:
+def _load_journal(p: str) -> Optional[dict]:
+    """{"validator", "size", "ranges"} or None (missing, unreadable, or a journal without a
+    validator - nothing to check partial data against)."""
     try:
         with open(p, "r", encoding="utf-8") as f:
             v = json.load(f)
-        return [list(x) for x in v] if isinstance(v, list) else []
     except (OSError, ValueError):
-        return []
+        return None
+    if not isinstance(v, dict) or not v.get("validator"):
+        return None
+    rng = v.get("ranges")
+    return {"validator": str(v["validator"]), "size": v.get("size"),
+            "ranges": [list(x) for x in rng] if isinstance(rng, list) else []}
 
 
-def _save_ranges(p: str, done: list) -> None:
+def _save_journal(p: str, validator: str, size: int, done: list) -> None:
     tmp = p + ".tmp"
     with open(tmp, "w", encoding="utf-8") as f:
-        json.dump(done, f)
+        json.dump({"validator": validator, "size": size, "ranges": done}, f)
     os.replace(tmp, p)
 
 

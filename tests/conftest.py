@@ -43,6 +43,9 @@ class Origin:
         self.chunked = set()
         self.corrupt = {}       # path -> [file offset, responses left]: flip that byte
         self.redirect = {}      # path -> (status, Location): answered before anything else
+        self.no_validators = False   # True: no ETag (resume cannot be validated)
+        self.hooks = []              # callables(method, path) run before each request
+        self._etags = {}
 
     def _body(self, path: str, data: bytes, s: int, e: int) -> bytes:
         """data[s:e+1], with the byte of an armed ``corrupt`` fault flipped if covered."""
@@ -53,6 +56,14 @@ class Origin:
             i = c[0] - s
             body = body[:i] + bytes([body[i] ^ 0xFF]) + body[i + 1:]
         return body
+
+    def _etag(self, path, data):
+        import hashlib
+        hit = self._etags.get(path)
+        if hit is None or hit[0] is not data:
+            hit = (data, '"%s"' % hashlib.md5(data).hexdigest())
+            self._etags[path] = hit
+        return hit[1]
 
     async def _trickle(self, req, status, body, hdrs):
         from aiohttp import web
@@ -71,6 +82,8 @@ class Origin:
 
         async def handler(req: web.Request):
             self.requests.append((req.method, req.path_qs, req.headers.get("Range")))
+            for h in self.hooks:
+                h(req.method, req.path)
             if req.path in self.redirect:
                 st, loc = self.redirect[req.path]
                 return web.Response(status=st, headers={"Location": loc}, text="moved")
@@ -80,6 +93,8 @@ class Origin:
             if data is None:
                 return web.Response(status=404, text="not found")
             hdrs = {} if self.no_ranges else {"Accept-Ranges": "bytes"}
+            if not self.no_validators:
+                hdrs["ETag"] = self._etag(req.path, data)
             rng = req.headers.get("Range")
             if rng and self.fail_ranges.get(rng, 0) > 0:
                 self.fail_ranges[rng] -= 1

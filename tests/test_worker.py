@@ -687,3 +687,37 @@ def test_complete_multipart_with_lost_reply(run, make_cfg, origin_cls):
         assert o.data == blob and o.etag.endswith("-3")
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+@pytest.mark.parametrize("validators", [True, False])
+def test_http_resume_discards_partial_data_of_a_changed_origin(run, make_cfg, origin_cls,
+                                                               validators):
+    """Attempt 1 is cut mid-body; before the retry the origin serves ANOTHER file of the same
+    size (new ETag). The partial data must not be spliced with the new bytes: the retry
+    starts from 0. Without validators nothing is resumed at all."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls,
+                                        download={"stream_http": False, "http_streams": 1})
+        origin.no_validators = not validators
+        old = os.urandom(3 * 1024 * 1024 + 5)
+        new = os.urandom(len(old))
+        origin.blobs["/v.mkv"] = old
+        origin.truncate.add("/v.mkv")
+        heads = []
+
+        def swap(method, path):     # the retry's first request sees the new file
+            if method == "HEAD" and path == "/v.mkv":
+                heads.append(1)
+                if len(heads) == 2:
+                    origin.blobs["/v.mkv"] = new
+                    origin.truncate.discard("/v.mkv")
+        origin.hooks.append(swap)
+        await w.submit(api.make_download("rv1", "http", origin.url("/v.mkv")))
+        await _wait(w, 2)
+        assert w.results[0].outcome == "retried"
+        assert w.results[1].outcome == "staged", w.results[1]
+        gets = [r for r in origin.requests if r[0] == "GET"]
+        assert not gets[-1][2]                      # a full GET, no Range
+        assert s3.get("triton-staging", keys.object_key("rv1", "v.mkv")) == new
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
