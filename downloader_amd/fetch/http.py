@@ -101,10 +101,13 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     log = logger or NullLogger()
     progress = progress or Progress()
     size, ranges, url, validator = await probe_validated(t, url, proxy)   # later GETs: final URL
-    if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
-        log.info("resume: file already complete", path=path)
-        return 0
     part_path, state_path = path + ".part", path + ".part.ranges"
+    if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
+        j = _load_journal(state_path)
+        if j and validator and j["validator"] == validator and j["size"] == size:
+            log.info("resume: file already complete", path=path)
+            return 0
+        os.unlink(path)                      # another version of the file: fetch again
     journal = _load_journal(state_path) if os.path.exists(part_path) else None
     resumable = bool(journal and validator and journal["validator"] == validator
                      and journal["size"] == size)
@@ -161,8 +164,9 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     finally:
         os.close(fd)
     os.replace(part_path, path)
-    if os.path.exists(state_path):
-        os.unlink(state_path)
+    # the journal stays (ranges = the whole file): a retry whose upload failed reuses the
+    # complete file only if the origin still reports this version
+    _save_journal(state_path, validator, size, [[0, size]])
     return written
 
 

@@ -721,3 +721,31 @@ def test_http_resume_discards_partial_data_of_a_changed_origin(run, make_cfg, or
         assert s3.get("triton-staging", keys.object_key("rv1", "v.mkv")) == new
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_complete_download_reused_only_for_the_same_origin_version(run, make_cfg, origin_cls):
+    """Attempt 1 downloads the whole file but its upload fails; the retry reuses the file on
+    disk only if the origin still reports the same ETag - here it changed, so it refetches."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls,
+                                        download={"stream_http": False, "http_streams": 1})
+        old = os.urandom(2 * 1024 * 1024 + 1)
+        new = os.urandom(len(old))
+        origin.blobs["/c.mkv"] = old
+        s3.faults.add(FaultRule(method="PUT", path_contains="/rc1/original/Yy5ta3Y=",
+                                times=1, status=403, code="AccessDenied"))
+        heads = []
+
+        def swap(method, path):
+            if method == "HEAD" and path == "/c.mkv":
+                heads.append(1)
+                if len(heads) == 2:
+                    origin.blobs["/c.mkv"] = new
+        origin.hooks.append(swap)
+        await w.submit(api.make_download("rc1", "http", origin.url("/c.mkv")))
+        await _wait(w, 2)
+        assert [r.outcome for r in w.results] == ["retried", "staged"], w.results
+        assert s3.get("triton-staging", keys.object_key("rc1", "c.mkv")) == new
+        assert len([r for r in origin.requests if r[0] == "GET"]) == 2
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
