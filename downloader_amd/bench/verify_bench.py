@@ -37,6 +37,13 @@ def kernel_section(gv, sizes, counts, iters) -> None:
                   "GBps_bitop3": round(gb / (ms_b3 / 1e3), 1),
                   "GBps_plain": round(gb / (ms_plain / 1e3), 1),
                   "speedup": round(ms_plain / ms_b3, 3)})
+            if hasattr(gv, "kernel_bench_prefetch"):
+                ms_pf, ms_nopf = gv.kernel_bench_prefetch(plen, n, iters)
+                emit({"section": "kernel_prefetch", "piece_len": plen, "pieces": n,
+                      "ms_prefetch": round(ms_pf, 3), "ms_no_prefetch": round(ms_nopf, 3),
+                      "GBps_prefetch": round(gb / (ms_pf / 1e3), 1),
+                      "GBps_no_prefetch": round(gb / (ms_nopf / 1e3), 1),
+                      "speedup": round(ms_nopf / ms_pf, 3)})
 
 
 def make_files(root: str, total: int, nfiles: int):

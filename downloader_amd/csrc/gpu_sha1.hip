@@ -7,9 +7,13 @@
 //   * SHA-1 is a serial chain over 64-byte blocks inside one piece, so the unit of
 //     parallelism is the piece: ONE LANE PER PIECE, 64 pieces per wavefront. Per-lane work is
 //     ~616 VALU ops per 64-byte block (80 rounds with v_alignbit rotates, v_bfi for Ch and
-//     v_bitop3 for parity/majority, plus the message schedule). Measured (profiles/verify,
-//     profiles/r2_validate): ~41 MB/s per lane - one wave per SIMD leaves dependent-issue
-//     gaps - so throughput is pieces-in-flight x 41 MB/s: ~680 GB/s at 16k pieces, ~170 GB/s
+//     v_bitop3 for parity/majority, plus the message schedule). Each lane loads block k+1
+//     into registers while it hashes block k (sha1_run16): without that every block waited
+//     for its own global loads and one wave per SIMD had nothing to hide the wait with.
+//     Measured (profiles/r2_kpf, kernel A/B in one process): ~58 MB/s per lane with the
+//     prefetch vs ~43 MB/s without (1.37x; ~2,600 cycles per block, 95 % of the 4-cycle
+//     VALU issue bound), so throughput is pieces-in-flight x 58 MB/s: ~930 GB/s at 16k
+//     pieces (one wave per CU - a quarter of the SIMDs), ~234 GB/s
 //     at 4k. Real torrents have 1k-20k pieces, and the host path that feeds the kernel
 //     (pread into pinned slots + PCIe Gen5 x16, ~57 GB/s DMA measured) is the bound.
 //   * Each lane streams its own piece with 16-byte global loads (4 x dwordx4 per block). The
@@ -143,10 +147,65 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t w[16]) {
   }
 }
 
+// Raw 64-byte block as four dwordx4 loads, and its conversion to big-endian words: split so
+// the loads of block k+1 can be issued before block k is hashed (see sha1_run16).
+__device__ __forceinline__ void load_raw16(const uint8_t* p, uint4 v[4]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = q[i];
+}
+__device__ __forceinline__ void to_words(const uint4 v[4], uint32_t w[16]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w[4 * i + 0] = bswap(v[i].x);
+    w[4 * i + 1] = bswap(v[i].y);
+    w[4 * i + 2] = bswap(v[i].z);
+    w[4 * i + 3] = bswap(v[i].w);
+  }
+}
+
+// `nblk` whole blocks at p (16-byte aligned) into s. PF: software-prefetch block k+1 into
+// registers while block k is hashed. Without it every block waited for its own loads right
+// before its first round (s_waitcnt vmcnt(0) at the loop head: ~550 - 900 cycles of an L2 /
+// HBM miss on top of ~2,500 cycles of VALU issue), and with one wave per SIMD nothing else
+// hides that wait.
+template <bool B3, bool PF>
+__device__ __forceinline__ void sha1_run16(Sha1State& s, const uint8_t* p, int64_t nblk) {
+  uint32_t w[16];
+  if constexpr (!PF) {
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+      load_block<16>(p + (blk << 6), w);
+      sha1_block<B3>(s, w);
+    }
+  } else {
+    // Two register buffers with fixed roles (no cur = nxt copy: a move out of a register
+    // with a load in flight waits for that load, which is what the prefetch is to avoid).
+    // The second load of a pair is clamped to the last block, so it is always in bounds
+    // and needs no branch; the duplicate 64 bytes per piece are never hashed.
+    if (nblk <= 0) return;
+    uint4 a[4], b[4];
+    load_raw16(p, a);
+    int64_t blk = 0;
+    for (; blk + 2 <= nblk; blk += 2) {
+      load_raw16(p + ((blk + 1) << 6), b);
+      to_words(a, w);
+      sha1_block<B3>(s, w);
+      const int64_t n2 = blk + 2 < nblk ? blk + 2 : nblk - 1;
+      load_raw16(p + (n2 << 6), a);
+      to_words(b, w);
+      sha1_block<B3>(s, w);
+    }
+    if (blk < nblk) {
+      to_words(a, w);
+      sha1_block<B3>(s, w);
+    }
+  }
+}
+
 // One lane hashes one piece. data holds n_pieces consecutive pieces of piece_len bytes,
 // the last one possibly `last_len` bytes. If `expected` is non-null, ok[i] = digest matches,
 // otherwise digests are written to `out` (5 words, big-endian byte order as bytes).
-template <int ALIGN, bool B3 = true>
+template <int ALIGN, bool B3 = true, bool PF = true>
 __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ data,
                                                    int64_t piece_len, int64_t last_len,
                                                    int n_pieces,
@@ -160,9 +219,13 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
   Sha1State s{0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
   uint32_t w[16];
   const int64_t nfull = len >> 6;
-  for (int64_t blk = 0; blk < nfull; ++blk) {
-    load_block<ALIGN>(p + (blk << 6), w);
-    sha1_block<B3>(s, w);
+  if constexpr (ALIGN == 16) {
+    sha1_run16<B3, PF>(s, p, nfull);
+  } else {
+    for (int64_t blk = 0; blk < nfull; ++blk) {
+      load_block<ALIGN>(p + (blk << 6), w);
+      sha1_block<B3>(s, w);
+    }
   }
   // Tail + padding (one or two blocks), built word by word straight into w[] - no byte
   // array, so the padding logic costs no extra registers or scratch.
@@ -243,10 +306,7 @@ __global__ __launch_bounds__(256) void sha1_chunk(uint32_t* __restrict__ state,
   const int64_t here = last_chunk ? valid : CH;
   uint32_t w[16];
   const int64_t nfull = here >> 6;
-  for (int64_t blk = 0; blk < nfull; ++blk) {
-    load_block<16>(p + (blk << 6), w);
-    sha1_block<B3>(s, w);
-  }
+  sha1_run16<B3, true>(s, p, nfull);
   if (!last_chunk) {
     st[0] = s.h0; st[1] = s.h1; st[2] = s.h2; st[3] = s.h3; st[4] = s.h4;
     return;
@@ -537,6 +597,46 @@ class GpuVerifier {
     return sub;
   }
 
+  // Kernel-only A/B of the block-prefetch (both with v_bitop3): ms per launch with and
+  // without loading block k+1 while block k is hashed, interleaved in one process.
+  std::vector<double> kernel_bench_prefetch(int64_t piece_len, int n_pieces, int iters) {
+    HIP_CHECK(hipSetDevice(device_));
+    size_t bytes = (size_t)piece_len * (size_t)n_pieces;
+    uint8_t *d = nullptr, *dout = nullptr;
+    HIP_CHECK(hipMalloc((void**)&d, bytes));
+    HIP_CHECK(hipMalloc((void**)&dout, (size_t)n_pieces * 20));
+    HIP_CHECK(hipMemset(d, 0x5a, bytes));
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    const int block = 64, grid = (n_pieces + block - 1) / block;
+    double t[2] = {0, 0};
+    for (int it = 0; it < iters + 1; ++it) {
+      for (int v = 0; v < 2; ++v) {
+        HIP_CHECK(hipEventRecord(e0, stream_[0]));
+        if (v == 0)
+          hipLaunchKernelGGL((sha1_pieces<16, true, true>), dim3(grid), dim3(block), 0,
+                             stream_[0], d, piece_len, piece_len, n_pieces, nullptr, nullptr,
+                             dout);
+        else
+          hipLaunchKernelGGL((sha1_pieces<16, true, false>), dim3(grid), dim3(block), 0,
+                             stream_[0], d, piece_len, piece_len, n_pieces, nullptr, nullptr,
+                             dout);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(e1, stream_[0]));
+        HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (it > 0) t[v] += ms;
+      }
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    hipFree(d);
+    hipFree(dout);
+    return {t[0] / iters, t[1] / iters};
+  }
+
   // Kernel-only timing (device-resident data, hipEvents): ms per launch hashing `n_pieces`
   // pieces of `piece_len` bytes; `bitop3` selects the v_bitop3 or the plain-C round forms
   // so both variants are A/B-timed interleaved in one process.
@@ -743,5 +843,19 @@ PYBIND11_MODULE(_gpuhash, m) {
           },
           py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 5,
           "(ms_bitop3, ms_plain): kernel time per launch, device-resident data")
+      .def(
+          "kernel_bench_prefetch",
+          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters) {
+            if (piece_len <= 0 || piece_len % 16 || n_pieces <= 0 || iters <= 0)
+              throw std::invalid_argument("piece_len must be a positive multiple of 16");
+            std::vector<double> r;
+            {
+              py::gil_scoped_release rel;
+              r = g.kernel_bench_prefetch(piece_len, n_pieces, iters);
+            }
+            return py::make_tuple(r[0], r[1]);
+          },
+          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 5,
+          "(ms_prefetch, ms_no_prefetch): kernel time per launch, device-resident data")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
 }

@@ -31,10 +31,21 @@ def ref(data, piece):
     (1000, 257 * 1000 + 999),       # piece_len % 16 != 0 -> dword path
     (999, 300 * 999),               # odd piece length -> byte path
     (64, 64 * 5000),                # many tiny pieces, > 1 workgroup
+    (192, 192 * 200 + 64 * 3 + 7),  # odd block count (3): prefetch pair loop + odd block
+    (1008, 1008 * 129 + 330),       # 15 whole blocks + tail, last piece 5 blocks
 ])
 def test_hash_buffer_matches_hashlib(gv, piece, n):
     data = os.urandom(n)
     assert gv.hash_buffer(data, piece) == ref(data, piece)
+
+
+def test_kernel_ab_timings(gv):
+    """The prefetch / no-prefetch kernel A/B used by verify_bench runs and times both."""
+    pf, nopf = gv.kernel_bench_prefetch(65536, 256, 1)
+    b3, plain = gv.kernel_bench(65536, 256, 1)
+    assert min(pf, nopf, b3, plain) > 0
+    with pytest.raises(ValueError):
+        gv.kernel_bench_prefetch(1000, 256, 1)
 
 
 def test_multi_batch_pipeline(gv):
