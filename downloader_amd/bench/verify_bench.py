@@ -77,6 +77,8 @@ def main(argv=None) -> int:
     ap.add_argument("--chunk-kb", type=int, default=64, help="streamed path chunk per lane")
     ap.add_argument("--kernel-only", action="store_true")
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--kernel-sizes", default="256,1024,4096", help="kernel section piece KiB")
+    ap.add_argument("--kernel-counts", default="1024,4096,16384", help="kernel section pieces")
     a = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -86,7 +88,8 @@ def main(argv=None) -> int:
         return 2
     gv = gpuhash().GpuVerifier(0, a.batch_mb << 20, a.readers)
     emit({"section": "device", "arch": gpuhash().arch()})
-    kernel_section(gv, [256 << 10, 1 << 20, 4 << 20], [1024, 4096, 16384], 3)
+    kernel_section(gv, [int(k) << 10 for k in a.kernel_sizes.split(",")],
+                   [int(n) for n in a.kernel_counts.split(",")], 3)
     if a.kernel_only:
         return 0
 
