@@ -44,14 +44,16 @@ def local_name(download_dir: str, item_name: str, sub_folder: str) -> str:
 
 async def fetch_bucket(uri: str, download_dir: str, secure: bool = True, concurrency: int = 4,
                        transports=None, logger: Optional[Logger] = None, progress=None,
-                       native: bool = True) -> List[str]:
+                       native: bool = True, ssl_verify: bool = True,
+                       ca_file: str = "") -> List[str]:
     from ..s3.client import S3Client
     log = logger or NullLogger()
     src = parse_bucket_uri(uri)
     log.info("bucket", src.redacted())
     log.info("bucket", f"using s3 endpoint: {src.endpoint}")
     client = S3Client(src.endpoint, src.access_key, src.secret_key, secure=secure,
-                      transports=transports, native=native)
+                      transports=transports, native=native, ssl_verify=ssl_verify,
+                      ca_file=ca_file)
     try:
         prefix = src.sub_folder.rstrip("/") + "/"
         items = await client.list_objects(src.bucket, prefix, recursive=True)

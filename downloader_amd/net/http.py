@@ -452,21 +452,38 @@ class NativeTransport(Transport):
 
 
 class AiohttpTransport(Transport):
+    """https:// (and proxied) requests. TLS peers are verified against the system trust store,
+    plus ``ca_file`` (PEM bundle, e.g. the private CA of an in-cluster MinIO) when given;
+    ``ssl_verify=False`` turns verification off (minio-js ``transport`` with
+    ``rejectUnauthorized: false``)."""
+
     def __init__(self, connect_timeout: float = 10.0, io_timeout: float = 300.0,
-                 limit: int = 64, ssl_verify: bool = True):
+                 limit: int = 64, ssl_verify: bool = True, ca_file: str = ""):
         self._session = None
         self.connect_timeout = connect_timeout
         self.io_timeout = io_timeout
         self.limit = limit
         self.ssl_verify = ssl_verify
+        self.ca_file = ca_file
         self.max_body = 64 << 20
+
+    def ssl_context(self):
+        """Value for aiohttp's ``ssl=``: None = default verified context, False = no checks."""
+        if not self.ssl_verify:
+            return False
+        if not self.ca_file:
+            return None
+        import ssl
+        ctx = ssl.create_default_context()
+        ctx.load_verify_locations(cafile=self.ca_file)     # in addition to the system store
+        return ctx
 
     async def _sess(self):
         import aiohttp
         if self._session is None or self._session.closed:
             timeout = aiohttp.ClientTimeout(total=None, connect=self.connect_timeout,
                                             sock_read=self.io_timeout)
-            conn = aiohttp.TCPConnector(limit=self.limit, ssl=None if self.ssl_verify else False)
+            conn = aiohttp.TCPConnector(limit=self.limit, ssl=self.ssl_context())
             self._session = aiohttp.ClientSession(timeout=timeout, connector=conn,
                                                   auto_decompress=False)
         return self._session
@@ -585,9 +602,11 @@ class TransportSet:
 
 
 def make_transports(native: bool = True, max_workers: int = 32, connect_timeout: float = 10.0,
-                    io_timeout: float = 300.0, ssl_verify: bool = True) -> TransportSet:
+                    io_timeout: float = 300.0, ssl_verify: bool = True,
+                    ca_file: str = "") -> TransportSet:
     nt = NativeTransport(max_workers, connect_timeout, io_timeout) if native else None
-    return TransportSet(nt, AiohttpTransport(connect_timeout, io_timeout, ssl_verify=ssl_verify))
+    return TransportSet(nt, AiohttpTransport(connect_timeout, io_timeout, ssl_verify=ssl_verify,
+                                             ca_file=ca_file))
 
 
 Callback = Callable[[int], None]

@@ -100,7 +100,7 @@ class S3Client:
                  part_size: int = 16 * MiB, multipart_threshold: int = 64 * MiB,
                  max_inflight_parts: int = 8, unsigned_payload: bool = True, retries: int = 3,
                  native: bool = True, connect_timeout: float = 10.0,
-                 request_timeout: float = 300.0):
+                 request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = ""):
         if "://" in endpoint:
             secure = endpoint.startswith("https://")
             endpoint = endpoint.split("://", 1)[1]
@@ -111,7 +111,8 @@ class S3Client:
         self.region = region
         self._own_transports = transports is None
         self.t = transports or make_transports(native=native, connect_timeout=connect_timeout,
-                                               io_timeout=request_timeout)
+                                               io_timeout=request_timeout,
+                                               ssl_verify=ssl_verify, ca_file=ca_file)
         self.part_size = max(MIN_PART, part_size)
         self.multipart_threshold = multipart_threshold
         self.max_inflight_parts = max(1, max_inflight_parts)

@@ -97,7 +97,8 @@ def _err(status: int, code: str, msg: str = "", resource: str = "") -> web.Respo
 
 class FakeS3:
     def __init__(self, access_key: str = "minioadmin", secret_key: str = "minioadmin",
-                 verify_signatures: bool = True, host: str = "127.0.0.1", port: int = 0):
+                 verify_signatures: bool = True, host: str = "127.0.0.1", port: int = 0,
+                 ssl_context=None):
         self.creds = {access_key: secret_key}
         self.verify_signatures = verify_signatures
         self.buckets: Dict[str, Dict[str, StoredObject]] = {}
@@ -110,6 +111,7 @@ class FakeS3:
         self._thread: Optional[threading.Thread] = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self.hooks: List[Callable[[str, str], None]] = []
+        self.ssl_context = ssl_context          # serve https (tests of secure / bucket://)
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -121,7 +123,7 @@ class FakeS3:
         app.router.add_route("*", "/{tail:.*}", self._handle)
         self._runner = web.AppRunner(app, access_log=None)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port)
+        site = web.TCPSite(self._runner, self.host, self.port, ssl_context=self.ssl_context)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
         return self.endpoint

@@ -151,7 +151,9 @@ class DownloadStage(Stage):
         files = await bucket_src.fetch_bucket(url, path, secure=d.bucket_secure,
                                               concurrency=d.bucket_concurrency,
                                               logger=job.logger, progress=prog,
-                                              native=self.cfg.s3.native_transport)
+                                              native=self.cfg.s3.native_transport,
+                                              ssl_verify=self.cfg.tls.verify,
+                                              ca_file=self.cfg.tls.ca_file)
         n = sum(os.path.getsize(f) for f in files)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("bucket", n)

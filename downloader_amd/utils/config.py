@@ -161,6 +161,12 @@ class TraceConfig(BaseModel):
     path: str = ""                              # JSONL span sink ("" -> stderr when enabled)
 
 
+class TlsConfig(BaseModel):
+    """TLS for https:// sources, S3 with ``secure: true`` and bucket:// (always TLS)."""
+    verify: bool = True                         # False: accept any certificate
+    ca_file: str = ""                           # extra PEM trust (private CA), beside the system store
+
+
 class Config(BaseModel):
     name: str = "downloader"
     mode: Literal["tuned", "reference"] = "tuned"
@@ -174,6 +180,7 @@ class Config(BaseModel):
     health: HealthConfig = Field(default_factory=HealthConfig)
     metrics: MetricsConfig = Field(default_factory=MetricsConfig)
     trace: TraceConfig = Field(default_factory=TraceConfig)
+    tls: TlsConfig = Field(default_factory=TlsConfig)
     stages: List[str] = Field(default_factory=lambda: ["download", "process", "upload"])
 
     def apply_mode(self) -> "Config":

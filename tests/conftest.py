@@ -30,7 +30,8 @@ def run():
 class Origin:
     """aiohttp origin serving named blobs (Range + HEAD), optional faults."""
 
-    def __init__(self):
+    def __init__(self, ssl_context=None):
+        self.ssl_context = ssl_context
         self.blobs = {}
         self.runner = None
         self.port = 0
@@ -132,13 +133,14 @@ class Origin:
         app.router.add_route("*", "/{tail:.*}", handler)
         self.runner = web.AppRunner(app, access_log=None)
         await self.runner.setup()
-        site = web.TCPSite(self.runner, "127.0.0.1", 0)
+        site = web.TCPSite(self.runner, "127.0.0.1", 0, ssl_context=self.ssl_context)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]
         return self
 
     def url(self, path: str) -> str:
-        return f"http://127.0.0.1:{self.port}{path}"
+        scheme = "https" if self.ssl_context is not None else "http"
+        return f"{scheme}://127.0.0.1:{self.port}{path}"
 
     async def stop(self):
         if self.runner is not None:
