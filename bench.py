@@ -70,6 +70,9 @@ def parse() -> argparse.Namespace:
                         "share, min(mask, cgroup quota) / visible GPUs; -1: no pinning")
     p.add_argument("--procs-per-rank", type=int, default=0,
                    help="worker processes per rank; 0: one per 8 CPUs of the rank's slice")
+    p.add_argument("--tls", choices=["off", "native", "aiohttp"], default="off",
+                   help="origin and S3 over https (self-signed blobd certificate): TLS in the "
+                        "native transport's threads, or through aiohttp on the event loop")
     p.add_argument("--compare-reference", action="store_true",
                    help="also time reference-equivalent mode and report the ratio")
     return p.parse_args()
@@ -175,6 +178,10 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
         "broker": {"backend": "memory"},
         "health": {"enabled": False},
     }
+    ca = getattr(args, "ca_file", "")
+    if args.tls != "off":
+        over["s3"]["secure"] = True
+        over["tls"] = {"ca_file": ca, "native": args.tls == "native"}
     if mode == "tuned":
         if args.http_streams:
             over["download"]["http_streams"] = args.http_streams
@@ -190,8 +197,10 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
     await worker.start(health=False)
     host, port = endpoint.split(":")
 
+    scheme = "https" if args.tls != "off" else "http"
+
     def url(name, sz, seed):
-        return f"http://{host}:{port}/media/{name}?size={sz}&seed={seed}"
+        return f"{scheme}://{host}:{port}/media/{name}?size={sz}&seed={seed}"
     return worker, url
 
 
@@ -377,16 +386,22 @@ def main() -> int:
     args = parse()
     dist = Dist(args.gpus)
     pinned = pin_rank(dist, args.cpus_per_rank)
-    from downloader_amd.bench.infra import Blobd
+    from downloader_amd.bench.infra import Blobd, self_signed_cert
     blob = None
     endpoint = None
+    cert = None
+    if args.tls != "off":
+        cert = self_signed_cert(tempfile.mkdtemp(prefix=f"stager-bench-tls-r{dist.rank}-"))
+        args.ca_file = cert[0]
     if args.peers == "per-rank" or dist.rank == 0:
         # Native origin + S3 sink. per-rank: every worker gets its own peer (the external world
         # is not the bottleneck being measured); shared: one peer on rank 0 for all workers.
-        blob = Blobd(default_size=int(args.size_mb * 1e6), sink=args.sink).start()
+        blob = Blobd(default_size=int(args.size_mb * 1e6), sink=args.sink, tls=cert).start()
         endpoint = blob.endpoint
     if args.peers == "shared":
-        endpoint = dist.bcast(endpoint)
+        endpoint, ca = dist.bcast((endpoint, cert[0] if cert else ""))
+        if cert:
+            args.ca_file = ca
     nproc = args.procs_per_rank
     if nproc <= 0:   # auto: one worker process per 8 CPUs of the rank's slice, at most 8
         nproc = max(1, min(8, len(pinned or os.sched_getaffinity(0)) // 8))
@@ -423,6 +438,7 @@ def main() -> int:
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
             "staging": args.staging if args.mode == "tuned" else "disk",
+            **({"tls": args.tls} if args.tls != "off" else {}),
             "concurrency_per_worker": args.concurrency if args.mode == "tuned" else 1,
             "procs_per_rank": nproc,
             "config": {

@@ -8,17 +8,29 @@ import tempfile
 import time
 import urllib.request
 from pathlib import Path
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 from ..ops import build
 
 PKG = Path(__file__).resolve().parents[1]
 
 
+def self_signed_cert(directory: str, name: str = "127.0.0.1") -> Tuple[str, str]:
+    """Throwaway certificate + key for the TLS bench (openssl CLI; SAN = the IP / name)."""
+    crt, key = os.path.join(directory, "blobd.crt"), os.path.join(directory, "blobd.key")
+    san = f"IP:{name}" if name.replace(".", "").isdigit() else f"DNS:{name}"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key,
+                    "-out", crt, "-days", "2", "-subj", f"/CN={name}", "-addext",
+                    f"subjectAltName={san}"], check=True, capture_output=True, timeout=120)
+    return crt, key
+
+
 class Blobd:
     def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
-                 host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum"):
+                 host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum",
+                 tls: Optional[Tuple[str, str]] = None):
         self.files_root = files_root
+        self.tls = tls                  # (cert PEM, key PEM): serve https
         self.sink = sink
         self.keep_bytes = keep_bytes
         self.default_size = default_size
@@ -34,7 +46,8 @@ class Blobd:
             [str(exe), "--host", self.host, "--port", "0", "--port-file", pf,
              "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)]
             + (["--files-root", self.files_root] if self.files_root else [])
-            + ["--sink", self.sink],
+            + ["--sink", self.sink]
+            + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else []),
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         t0 = time.time()
         while not os.path.exists(pf):
@@ -51,11 +64,15 @@ class Blobd:
     def endpoint(self) -> str:
         return f"{self.host}:{self.port}"
 
+    @property
+    def scheme(self) -> str:
+        return "https" if self.tls else "http"
+
     def media_url(self, name: str, size: int, seed: int) -> str:
-        return f"http://{self.endpoint}/media/{name}?size={size}&seed={seed}"
+        return f"{self.scheme}://{self.endpoint}/media/{name}?size={size}&seed={seed}"
 
     def files_url(self, rel: str = "") -> str:
-        return f"http://{self.endpoint}/files/{rel}"
+        return f"{self.scheme}://{self.endpoint}/files/{rel}"
 
     def cpu_seconds(self) -> float:
         """user+sys CPU time of the blobd process (from /proc/<pid>/stat)."""
@@ -69,7 +86,12 @@ class Blobd:
             return 0.0
 
     def stats(self) -> Dict[str, int]:
-        with urllib.request.urlopen(f"http://{self.endpoint}/_stats", timeout=10) as r:
+        ctx = None
+        if self.tls:
+            import ssl
+            ctx = ssl.create_default_context(cafile=self.tls[0])
+        with urllib.request.urlopen(f"{self.scheme}://{self.endpoint}/_stats", timeout=10,
+                                    context=ctx) as r:
             return json.loads(r.read())
 
     def stop(self) -> None:

@@ -11,6 +11,9 @@
 //            POST ?uploadId, DELETE ?uploadId)
 //   stats:   GET /_stats  (JSON: bytes received/served, objects, requests)
 //
+// --tls-cert/--tls-key: serve https (OpenSSL, one session per connection thread) for the TLS
+// staging bench; bodies then pass through user space both ways (no sendfile / splice).
+//
 // Uploaded bodies are received into a per-connection buffer and folded into a 64-bit
 // checksum (so every byte crosses memory like a real store); objects <= --keep-bytes are
 // kept in memory (done markers, tests), larger ones keep only size + checksum.
@@ -25,6 +28,9 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+
+#include <openssl/err.h>
+#include <openssl/ssl.h>
 
 #include <atomic>
 #include <cerrno>
@@ -66,6 +72,7 @@ int g_devnull = -1;
 int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
+SSL_CTX* g_tls = nullptr;  // --tls-cert / --tls-key
 
 constexpr size_t kPool = 64ull << 20;
 
@@ -144,6 +151,7 @@ class Conn {
  public:
   explicit Conn(int fd) : fd_(fd), buf_(1 << 20) {}
   ~Conn() {
+    if (ssl_) SSL_free(ssl_);
     ::close(fd_);
     if (pipe_[0] >= 0) {
       ::close(pipe_[0]);
@@ -152,6 +160,15 @@ class Conn {
   }
 
   void serve() {
+    if (g_tls) {
+      ssl_ = SSL_new(g_tls);
+      if (!ssl_) return;
+      SSL_set_fd(ssl_, fd_);
+      if (SSL_accept(ssl_) != 1) {
+        ERR_clear_error();
+        return;
+      }
+    }
     for (;;) {
       Request r;
       if (!read_request(r)) return;
@@ -168,6 +185,15 @@ class Conn {
       memmove(buf_.data(), buf_.data() + pos_, end_ - pos_);
       end_ -= pos_;
       pos_ = 0;
+    }
+    if (ssl_) {
+      int r = SSL_read(ssl_, buf_.data() + end_, (int)(buf_.size() - end_));
+      if (r <= 0) {
+        ERR_clear_error();
+        return false;
+      }
+      end_ += (size_t)r;
+      return true;
     }
     ssize_t r = ::recv(fd_, buf_.data() + end_, buf_.size() - end_, 0);
     if (r <= 0) return false;
@@ -233,7 +259,17 @@ class Conn {
 
   // Consume the request body, folding it into `s`; keep up to `keep` bytes in `out`.
   bool read_body(int64_t n, Summer& s, std::string* out, size_t keep) {
-    if (g_discard && n > (int64_t)keep) return discard_body(n, s);
+    if (g_discard && !ssl_ && n > (int64_t)keep) return discard_body(n, s);
+    if (g_discard && n > (int64_t)keep) {  // TLS: decrypt, skip the checksum pass
+      while (n > 0) {
+        if (pos_ == end_ && !fill()) return false;
+        size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
+        pos_ += k;
+        n -= (int64_t)k;
+        g_rx += k;
+      }
+      return true;
+    }
     while (n > 0) {
       if (pos_ == end_ && !fill()) return false;
       size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
@@ -280,6 +316,18 @@ class Conn {
 
   bool send_all(const void* p, size_t n) {
     const char* c = (const char*)p;
+    if (ssl_) {
+      while (n) {
+        int w = SSL_write(ssl_, c, (int)std::min<size_t>(n, (size_t)1 << 30));
+        if (w <= 0) {
+          ERR_clear_error();
+          return false;
+        }
+        c += w;
+        n -= (size_t)w;
+      }
+      return true;
+    }
     while (n) {
       ssize_t w = ::send(fd_, c, n, MSG_NOSIGNAL);
       if (w < 0) {
@@ -366,7 +414,7 @@ class Conn {
     while (left) {
       uint64_t po = (o + seed * 7919ull) % kPool;
       size_t k = (size_t)std::min<uint64_t>(left, std::min<uint64_t>(kPool - po, 4ull << 20));
-      if (g_pool_fd >= 0) {
+      if (g_pool_fd >= 0 && !ssl_) {
         off_t fo = (off_t)po;
         size_t sent = 0;
         while (sent < k) {
@@ -425,6 +473,18 @@ class Conn {
     if (ok && r.method != "HEAD") {
       off_t o = (off_t)start;
       uint64_t left = len;
+      std::vector<uint8_t> tb(ssl_ ? 256 * 1024 : 0);
+      while (ok && left && ssl_) {
+        ssize_t k = ::pread(fd, tb.data(), (size_t)std::min<uint64_t>(left, tb.size()), o);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0 || !send_all(tb.data(), (size_t)k)) {
+          ok = false;
+        } else {
+          o += k;
+          left -= (uint64_t)k;
+          g_tx += (uint64_t)k;
+        }
+      }
       while (ok && left) {
         ssize_t w = ::sendfile(fd_, fd, &o, (size_t)std::min<uint64_t>(left, 8u << 20));
         if (w < 0 && errno == EINTR) continue;
@@ -588,6 +648,7 @@ class Conn {
   }
 
   int fd_;
+  SSL* ssl_ = nullptr;
   std::vector<uint8_t> buf_;
   size_t pos_ = 0, end_ = 0;
   int pipe_[2] = {-1, -1};
@@ -599,6 +660,7 @@ int main(int argc, char** argv) {
   int port = 0;
   std::string host = "127.0.0.1";
   const char* port_file = nullptr;
+  std::string tls_cert, tls_key;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&] { return i + 1 < argc ? argv[++i] : (char*)""; };
@@ -609,11 +671,27 @@ int main(int argc, char** argv) {
     else if (a == "--default-size") g_default_size = strtoull(next(), nullptr, 10);
     else if (a == "--files-root") g_files_root = next();
     else if (a == "--sink") g_discard = std::string(next()) == "discard";
+    else if (a == "--tls-cert") tls_cert = next();
+    else if (a == "--tls-key") tls_key = next();
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
-                      "[--default-size N] [--files-root DIR] [--sink checksum|discard]\n");
+                      "[--default-size N] [--files-root DIR] [--sink checksum|discard] "
+                      "[--tls-cert PEM --tls-key PEM]\n");
       return 2;
     }
+  }
+  if (!tls_cert.empty()) {
+    g_tls = SSL_CTX_new(TLS_server_method());
+    if (!g_tls || SSL_CTX_use_certificate_chain_file(g_tls, tls_cert.c_str()) != 1 ||
+        SSL_CTX_use_PrivateKey_file(g_tls, (tls_key.empty() ? tls_cert : tls_key).c_str(),
+                                    SSL_FILETYPE_PEM) != 1) {
+      fprintf(stderr, "blobd: cannot load TLS certificate / key\n");
+      return 1;
+    }
+    SSL_CTX_set_min_proto_version(g_tls, TLS1_2_VERSION);
+    SSL_CTX_set_options(g_tls, SSL_OP_IGNORE_UNEXPECTED_EOF | SSL_OP_NO_COMPRESSION);
+    SSL_CTX_set_read_ahead(g_tls, 1);
+    SSL_CTX_set_default_read_buffer_len(g_tls, 256 * 1024);
   }
   signal(SIGPIPE, SIG_IGN);
   g_pool.resize(kPool);

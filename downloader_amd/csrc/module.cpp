@@ -227,13 +227,21 @@ PYBIND11_MODULE(_native, m) {
       .def("cancel", [](Progress& p) { p.cancelled.store(true); })
       .def_property_readonly("cancelled", [](const Progress& p) { return p.cancelled.load(); });
 
+  py::class_<TlsContext, std::shared_ptr<TlsContext>>(m, "TlsContext")
+      .def(py::init<bool, const std::string&>(), py::arg("verify") = true,
+           py::arg("ca_file") = "",
+           "Client TLS settings shared by connections: verify peers against the system store "
+           "plus ca_file (PEM), or not at all")
+      .def_property_readonly("verify", &TlsContext::verify);
+
   py::class_<HttpConn>(m, "HttpConn")
-      .def(py::init([](const std::string& host, int port, double cto, double iot) {
+      .def(py::init([](const std::string& host, int port, double cto, double iot,
+                       std::shared_ptr<TlsContext> tls) {
              py::gil_scoped_release rel;
-             return new HttpConn(host, port, cto, iot);
+             return new HttpConn(host, port, cto, iot, std::move(tls));
            }),
            py::arg("host"), py::arg("port"), py::arg("connect_timeout") = 10.0,
-           py::arg("io_timeout") = 300.0)
+           py::arg("io_timeout") = 300.0, py::arg("tls") = nullptr)
       .def(
           "request",
           [](HttpConn& c, const py::bytes& head, const py::object& body, bool expect_body,
@@ -332,5 +340,6 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("is_open", &HttpConn::is_open)
       .def_property_readonly("reusable", &HttpConn::reusable)
       .def_property_readonly("host", &HttpConn::host)
-      .def_property_readonly("port", &HttpConn::port);
+      .def_property_readonly("port", &HttpConn::port)
+      .def_property_readonly("tls", &HttpConn::is_tls);
 }

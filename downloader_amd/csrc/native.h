@@ -10,6 +10,8 @@
 
 typedef struct evp_md_ctx_st EVP_MD_CTX;
 typedef struct evp_md_st EVP_MD;
+typedef struct ssl_st SSL;
+typedef struct ssl_ctx_st SSL_CTX;
 
 namespace stager {
 
@@ -80,6 +82,27 @@ std::vector<std::string> hash_file_ranges(const std::string& path,
                                           const std::vector<std::pair<int64_t, int64_t>>& ranges,
                                           const std::string& algo, int threads);
 
+// ---- tls.cpp ---------------------------------------------------------------------------
+// One client SSL_CTX per trust setting, shared by every connection (and thread) of a transport.
+class TlsContext {
+ public:
+  TlsContext(bool verify, const std::string& ca_file);
+  ~TlsContext();
+  TlsContext(const TlsContext&) = delete;
+  TlsContext& operator=(const TlsContext&) = delete;
+  SSL_CTX* ctx() const { return ctx_; }
+  bool verify() const { return verify_; }
+
+ private:
+  SSL_CTX* ctx_ = nullptr;
+  bool verify_;
+};
+// Client handshake on a connected blocking socket: SNI for DNS names, host name / IP checked
+// against the certificate when verifying. Throws with the verification error on failure.
+SSL* tls_handshake(TlsContext& ctx, int fd, const std::string& name);
+// Message for a failed SSL_read / SSL_write / SSL_connect (drains the thread's error queue).
+std::string tls_error(SSL* s, int r, const std::string& what);
+
 // ---- transfer.cpp ----------------------------------------------------------------------
 // Parts up to this size are relayed through a pooled buffer and hashed with the multi-buffer
 // SHA-1; larger ones take the chunked (L2-sized, single-chain) path.
@@ -111,7 +134,10 @@ struct ResponseHead {
 
 class HttpConn {
  public:
-  HttpConn(const std::string& host, int port, double connect_timeout_s, double io_timeout_s);
+  // `tls` non-null: TLS over the socket (server name = host). Every body path below then
+  // moves bytes through user space (SSL_read / SSL_write) instead of splice / sendfile.
+  HttpConn(const std::string& host, int port, double connect_timeout_s, double io_timeout_s,
+           std::shared_ptr<TlsContext> tls = nullptr);
   ~HttpConn();
   HttpConn(const HttpConn&) = delete;
   HttpConn& operator=(const HttpConn&) = delete;
@@ -152,6 +178,7 @@ class HttpConn {
   // the owner closes the fd as usual.
   void abort();
   bool is_open() const { return fd_ >= 0; }
+  bool is_tls() const { return ssl_ != nullptr; }
   bool reusable() const { return fd_ >= 0 && reusable_; }
   const std::string& host() const { return host_; }
   int port() const { return port_; }
@@ -161,9 +188,13 @@ class HttpConn {
   void send_all(const uint8_t* p, size_t n);
   std::string read_line();
   int64_t take_buffered(uint8_t* p, int64_t n);
+  // Relay through a user-space buffer (either side is TLS).
+  int64_t relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog);
   std::string host_;
   int port_;
   int fd_ = -1;
+  SSL* ssl_ = nullptr;
+  std::shared_ptr<TlsContext> tls_;  // keeps the SSL_CTX alive as long as ssl_
   int pipe_[2] = {-1, -1};
   size_t pipe_sz_ = 0;
   bool reusable_ = true;

@@ -1,18 +1,27 @@
 // Standalone self-test of the host native code, built under sanitizers (SURVEY.md §5.2:
 // "an ASan/UBSan build of the C++ module in CI; TSan for the threaded hashing pool").
 //
-//   g++ -fsanitize=address,undefined selftest.cpp hashing.cpp transfer.cpp -lcrypto -lpthread
-//   g++ -fsanitize=thread            selftest.cpp hashing.cpp transfer.cpp -lcrypto -lpthread
+//   g++ -fsanitize=address,undefined selftest.cpp hashing.cpp sha1_mb.cpp transfer.cpp tls.cpp
+//       -lssl -lcrypto -lpthread                      (python -m downloader_amd.ops.build does it)
+//   g++ -fsanitize=thread            (same sources)
 //
 // Covers: digests vs known vectors, the threaded piece hasher/verifier (threads race on a
 // shared atomic work counter and per-thread buffers), and the HTTP transport against
 // in-process loopback servers: Content-Length body spliced to a file, chunked body, a
-// sendfile request body, and the socket->socket relay.
+// sendfile request body, the socket->socket relay, the hashed relay, and the same transfers
+// over TLS (throwaway in-memory certificate; handshake, verification failure, TLS relay).
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
+#include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
+
+#include <openssl/err.h>
+#include <openssl/evp.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -126,7 +135,97 @@ static int64_t drain_body(int fd, int64_t n) {
   return got;
 }
 
+// ---- TLS fixtures: self-signed P-256 certificate for 127.0.0.1, made in memory
+struct TestCert {
+  EVP_PKEY* key = nullptr;
+  X509* crt = nullptr;
+  std::string pem_path;
+  TestCert() {
+    key = EVP_EC_gen("P-256");
+    crt = X509_new();
+    X509_set_version(crt, 2);
+    ASN1_INTEGER_set(X509_get_serialNumber(crt), 1);
+    X509_gmtime_adj(X509_getm_notBefore(crt), -60);
+    X509_gmtime_adj(X509_getm_notAfter(crt), 3600);
+    X509_set_pubkey(crt, key);
+    X509_NAME* nm = X509_get_subject_name(crt);
+    X509_NAME_add_entry_by_txt(nm, "CN", MBSTRING_ASC, (const unsigned char*)"127.0.0.1", -1, -1, 0);
+    X509_set_issuer_name(crt, nm);
+    X509V3_CTX v3;
+    X509V3_set_ctx_nodb(&v3);
+    X509V3_set_ctx(&v3, crt, crt, nullptr, nullptr, 0);
+    for (auto [nid, val] : {std::pair<int, const char*>{NID_subject_alt_name, "IP:127.0.0.1"},
+                            {NID_basic_constraints, "critical,CA:TRUE"}}) {
+      X509_EXTENSION* ext = X509V3_EXT_conf_nid(nullptr, &v3, nid, val);
+      X509_add_ext(crt, ext, -1);
+      X509_EXTENSION_free(ext);
+    }
+    X509_sign(crt, key, EVP_sha256());
+    char path[] = "/tmp/stager-selftest-ca-XXXXXX";
+    int fd = mkstemp(path);
+    FILE* f = fdopen(fd, "w");
+    PEM_write_X509(f, crt);
+    fclose(f);
+    pem_path = path;
+  }
+  ~TestCert() {
+    unlink(pem_path.c_str());
+    X509_free(crt);
+    EVP_PKEY_free(key);
+  }
+};
+
+// Server side of a TLS test connection: handshake on fd, then plain byte helpers.
+struct TlsServerConn {
+  SSL_CTX* ctx;
+  SSL* s;
+  TlsServerConn(const TestCert& c, int fd) {
+    ctx = SSL_CTX_new(TLS_server_method());
+    SSL_CTX_use_certificate(ctx, c.crt);
+    SSL_CTX_use_PrivateKey(ctx, c.key);
+    s = SSL_new(ctx);
+    SSL_set_fd(s, fd);
+    if (SSL_accept(s) != 1) {
+      ERR_clear_error();
+      SSL_free(s);
+      s = nullptr;
+    }
+  }
+  ~TlsServerConn() {
+    if (s) SSL_free(s);
+    SSL_CTX_free(ctx);
+  }
+  std::string head() {
+    std::string h;
+    char ch;
+    while (s && h.size() < 65536 && SSL_read(s, &ch, 1) == 1) {
+      h.push_back(ch);
+      if (h.size() >= 4 && h.compare(h.size() - 4, 4, "\r\n\r\n") == 0) break;
+    }
+    return h;
+  }
+  void send(const std::string& d) {
+    size_t off = 0;
+    while (s && off < d.size()) {
+      int w = SSL_write(s, d.data() + off, (int)(d.size() - off));
+      if (w <= 0) return;
+      off += (size_t)w;
+    }
+  }
+  int64_t drain(int64_t n) {
+    std::vector<char> b(1 << 16);
+    int64_t got = 0;
+    while (s && got < n) {
+      int r = SSL_read(s, b.data(), (int)std::min<int64_t>(n - got, (int64_t)b.size()));
+      if (r <= 0) break;
+      got += r;
+    }
+    return got;
+  }
+};
+
 int main() {
+  signal(SIGPIPE, SIG_IGN);  // SSL_write on a reset socket (Python does the same at start)
   // ---- digests
   const uint8_t* abc = (const uint8_t*)"abc";
   CHECK(hex(digest("sha1", abc, 3)) == "a9993e364706816aba3e25717850c26c9cd0d89d");
@@ -273,6 +372,79 @@ int main() {
     }
     for (auto& th : ths) th.join();
     CHECK(good.load() == 4);
+  }
+  // ---- TLS: upload from a file (pread + SSL_write), TLS -> TLS hashed relay on 2 threads
+  // (multi-buffer path through a pooled buffer), and a failed verification
+  {
+    TestCert cert;
+    auto ctx = std::make_shared<TlsContext>(true, cert.pem_path);
+    int64_t got = 0;
+    {
+      Server s([&](int fd) {
+        TlsServerConn t(cert, fd);
+        t.head();
+        got = t.drain((int64_t)a.size());
+        t.send("HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nok");
+      });
+      HttpConn c("127.0.0.1", s.port, 5, 5, ctx);
+      CHECK(c.is_tls());
+      int fd = open(fa.c_str(), O_RDONLY);
+      Progress prog;
+      c.send_request_fd("PUT /p HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(a.size()) +
+                            "\r\n\r\n", fd, 0, (int64_t)a.size(), &prog);
+      ResponseHead h = c.read_head();
+      close(fd);
+      CHECK(h.status == 200 && c.read_body(h, 16) == "ok" && prog.bytes.load() == (int64_t)a.size());
+      CHECK(got == (int64_t)a.size());
+    }
+    const int64_t plen = 1 << 16, skip = 1000, n = (int64_t)body.size();
+    const int64_t full = ((n - skip) / plen) * plen;
+    std::string want = hash_pieces("sha1", body.data() + skip, (size_t)full, (size_t)plen, 1);
+    std::atomic<int> good{0};
+    std::vector<std::thread> ths;
+    for (int t = 0; t < 2; ++t) {
+      ths.emplace_back([&] {
+        Server origin([&](int fd) {
+          TlsServerConn s(cert, fd);
+          s.head();
+          s.send("HTTP/1.1 200 OK\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+          s.send(std::string((const char*)body.data(), body.size()));
+        });
+        int64_t sunk = 0;
+        Server sink([&](int fd) {
+          TlsServerConn s(cert, fd);
+          s.head();
+          sunk = s.drain(n);
+          s.send("HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n");
+        });
+        try {
+          HttpConn src("127.0.0.1", origin.port, 5, 5, ctx), dst("127.0.0.1", sink.port, 5, 5, ctx);
+          src.send_request("GET /h HTTP/1.1\r\nHost: x\r\n\r\n", nullptr, 0);
+          ResponseHead g = src.read_head();
+          dst.send_raw("PUT /h HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+          std::string digests, head, tail;
+          int64_t moved = src.relay_body_hashed(dst, g.content_length, skip, full, plen, nullptr,
+                                                &digests, &head, &tail);
+          ResponseHead p = dst.read_head();
+          dst.read_body(p, 16);
+          if (moved == n && p.status == 200 && digests == want && sunk == n) good.fetch_add(1);
+        } catch (const std::exception& e) {
+          fprintf(stderr, "tls relay: %s\n", e.what());
+        }
+      });
+    }
+    for (auto& th : ths) th.join();
+    CHECK(good.load() == 2);
+    // no trust for the throwaway CA: the handshake fails with the verification reason
+    auto strict = std::make_shared<TlsContext>(true, "");
+    Server s([&](int fd) { TlsServerConn t(cert, fd); });
+    std::string err;
+    try {
+      HttpConn c("127.0.0.1", s.port, 5, 5, strict);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    CHECK(err.find("certificate verify failed") != std::string::npos);
   }
   {
     RelayPoolStats st = relay_pool_stats();

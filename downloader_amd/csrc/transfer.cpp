@@ -26,6 +26,9 @@
 #include <sys/types.h>
 #include <unistd.h>
 
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+
 namespace stager {
 
 namespace {
@@ -60,7 +63,7 @@ std::string trim(const std::string& s) {
 }  // namespace
 
 HttpConn::HttpConn(const std::string& host, int port, double connect_timeout_s,
-                   double io_timeout_s)
+                   double io_timeout_s, std::shared_ptr<TlsContext> tls)
     : host_(host), port_(port), rbuf_(64 * 1024) {
   addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
@@ -104,11 +107,24 @@ HttpConn::HttpConn(const std::string& host, int port, double connect_timeout_s,
   }
   freeaddrinfo(res);
   if (fd_ < 0) throw IoError(last + " (" + host + ":" + ps + ")");
+  if (tls) {
+    try {
+      ssl_ = tls_handshake(*tls, fd_, host);
+    } catch (const std::exception& e) {
+      close();  // the destructor does not run for a throwing constructor
+      throw IoError(e.what());
+    }
+    tls_ = std::move(tls);
+  }
 }
 
 HttpConn::~HttpConn() { close(); }
 
 void HttpConn::close() {
+  if (ssl_) {
+    SSL_free(ssl_);  // no close_notify: the socket may be dead or mid-body
+    ssl_ = nullptr;
+  }
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
   for (int i = 0; i < 2; ++i)
@@ -125,6 +141,21 @@ void HttpConn::abort() {
 }
 
 void HttpConn::send_all(const uint8_t* p, size_t n) {
+  if (ssl_) {
+    while (n) {
+      ERR_clear_error();
+      int w = SSL_write(ssl_, p, (int)std::min<size_t>(n, (size_t)1 << 30));
+      if (w <= 0) {
+        const int e = SSL_get_error(ssl_, w);
+        if ((e == SSL_ERROR_WANT_WRITE || e == SSL_ERROR_WANT_READ) && errno == EINTR) continue;
+        reusable_ = false;
+        throw IoError(tls_error(ssl_, w, "send"));
+      }
+      p += w;
+      n -= (size_t)w;
+    }
+    return;
+  }
   while (n) {
     ssize_t w = ::send(fd_, p, n, MSG_NOSIGNAL);
     if (w < 0) {
@@ -138,6 +169,17 @@ void HttpConn::send_all(const uint8_t* p, size_t n) {
 }
 
 size_t HttpConn::recv_some(uint8_t* p, size_t n) {
+  while (ssl_) {
+    ERR_clear_error();
+    int r = SSL_read(ssl_, p, (int)std::min<size_t>(n, (size_t)1 << 30));
+    if (r > 0) return (size_t)r;
+    const int e = SSL_get_error(ssl_, r);
+    if (e == SSL_ERROR_ZERO_RETURN) return 0;  // close_notify, or EOF (IGNORE_UNEXPECTED_EOF)
+    if ((e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) && errno == EINTR) continue;
+    reusable_ = false;
+    if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) throw IoError("recv timeout");
+    throw IoError(tls_error(ssl_, r, "recv"));
+  }
   for (;;) {
     ssize_t r = ::recv(fd_, p, n, 0);
     if (r < 0) {
@@ -170,6 +212,29 @@ void HttpConn::send_request_fd(const std::string& head, int fd, int64_t off, int
   send_all((const uint8_t*)head.data(), head.size());
   off_t o = (off_t)off;
   int64_t left = len;
+  if (ssl_) {  // no sendfile through TLS: pread L2-sized chunks and encrypt them
+    thread_local std::vector<uint8_t> buf(256 * 1024);
+    while (left > 0) {
+      if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+        reusable_ = false;
+        throw IoError("cancelled");
+      }
+      ssize_t k = ::pread(fd, buf.data(), (size_t)std::min<int64_t>(left, (int64_t)buf.size()), o);
+      if (k < 0) {
+        if (errno == EINTR) continue;
+        reusable_ = false;
+        throw IoError(errstr("pread"));
+      }
+      if (k == 0) {
+        reusable_ = false;
+        throw IoError("pread: source file shorter than declared length");
+      }
+      send_all(buf.data(), (size_t)k);
+      o += k;
+      left -= k;
+      if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
+    }
+  }
   while (left > 0) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
@@ -347,15 +412,15 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
       if (n >= 0) n -= k;
     }
     if (n == 0) return;
-    // 2) zero-copy: socket -> pipe -> file.
-    if (pipe_[0] < 0) {
+    // 2) zero-copy: socket -> pipe -> file (plain sockets only: TLS bytes need decrypting).
+    if (!ssl_ && pipe_[0] < 0) {
       if (pipe2(pipe_, O_CLOEXEC) == 0) {
         int want = 1 << 20;
         int got = fcntl(pipe_[1], F_SETPIPE_SZ, want);
         pipe_sz_ = got > 0 ? (size_t)got : 65536;
       }
     }
-    if (pipe_[0] >= 0) {
+    if (!ssl_ && pipe_[0] >= 0) {
       while (n != 0) {
         check_cancel();
         size_t want = n < 0 ? pipe_sz_ : (size_t)std::min<int64_t>(n, (int64_t)pipe_sz_);
@@ -441,6 +506,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog) {
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
   if (moved == n) return moved;
+  if (ssl_ || dst.ssl_) return relay_copy(dst, n, moved, prog);
   if (pipe_[0] < 0) {
     if (pipe2(pipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
     int got = fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
@@ -480,6 +546,38 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog) {
     }
     moved += in;
     if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
+  }
+  return moved;
+}
+
+int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog) {
+  thread_local std::vector<uint8_t> buf(256 * 1024);
+  while (moved < n) {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("cancelled");
+    }
+    size_t r;
+    try {
+      r = recv_some(buf.data(), (size_t)std::min<int64_t>(n - moved, (int64_t)buf.size()));
+    } catch (...) {
+      dst.reusable_ = false;
+      throw;
+    }
+    if (r == 0) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("source closed mid-body");
+    }
+    try {
+      dst.send_all(buf.data(), r);
+    } catch (...) {
+      reusable_ = false;
+      throw;
+    }
+    moved += (int64_t)r;
+    if (prog) prog->bytes.fetch_add((int64_t)r, std::memory_order_relaxed);
   }
   return moved;
 }

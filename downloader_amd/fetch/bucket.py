@@ -45,7 +45,7 @@ def local_name(download_dir: str, item_name: str, sub_folder: str) -> str:
 async def fetch_bucket(uri: str, download_dir: str, secure: bool = True, concurrency: int = 4,
                        transports=None, logger: Optional[Logger] = None, progress=None,
                        native: bool = True, ssl_verify: bool = True,
-                       ca_file: str = "") -> List[str]:
+                       ca_file: str = "", native_tls: bool = True) -> List[str]:
     from ..s3.client import S3Client
     log = logger or NullLogger()
     src = parse_bucket_uri(uri)
@@ -53,7 +53,7 @@ async def fetch_bucket(uri: str, download_dir: str, secure: bool = True, concurr
     log.info("bucket", f"using s3 endpoint: {src.endpoint}")
     client = S3Client(src.endpoint, src.access_key, src.secret_key, secure=secure,
                       transports=transports, native=native, ssl_verify=ssl_verify,
-                      ca_file=ca_file)
+                      ca_file=ca_file, native_tls=native_tls)
     try:
         prefix = src.sub_folder.rstrip("/") + "/"
         items = await client.list_objects(src.bucket, prefix, recursive=True)

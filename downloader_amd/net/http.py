@@ -2,11 +2,13 @@
 
 Two implementations behind one async interface:
 
-* ``NativeTransport`` - plain ``http://`` over the C++ ``HttpConn`` (keep-alive pool). Bodies
-  are spliced socket->file and sent file->socket with ``sendfile``; each request runs on a
-  dedicated thread pool with the GIL released, so many transfers proceed in parallel inside
-  one worker process.
-* ``AiohttpTransport`` - everything else (TLS for ``https://`` / ``bucket://`` sources).
+* ``NativeTransport`` - ``http://`` and ``https://`` over the C++ ``HttpConn`` (keep-alive
+  pool). Plain bodies are spliced socket->file and sent file->socket with ``sendfile``; TLS
+  bodies go through OpenSSL on the same threads (``csrc/tls.cpp``). Each request runs on a
+  dedicated thread pool with the GIL released, so many transfers (and their encryption)
+  proceed in parallel inside one worker process.
+* ``AiohttpTransport`` - the rest: https through a forward proxy (CONNECT), or everything
+  when the native module is off.
 
 A request body is ``bytes`` or a ``FileRange``; a response body is returned in memory or
 written into a ``FileSink``.
@@ -133,6 +135,12 @@ def _via_proxy(proxy: Proxy, url: str, headers: Headers
     return proxy.host, proxy.port, target, hdrs
 
 
+def _host_hdr(host: str, port: int, tls: bool) -> str:
+    if ":" in host:             # IPv6 literal
+        host = f"[{host}]"
+    return host if port == (443 if tls else 80) else f"{host}:{port}"
+
+
 def split_host(url: str) -> Tuple[str, str, int, str]:
     u = urlsplit(url)
     scheme = u.scheme or "http"
@@ -174,14 +182,17 @@ class Transport:
 class NativeTransport(Transport):
     def __init__(self, max_workers: int = 32, connect_timeout: float = 10.0,
                  io_timeout: float = 300.0, max_idle_per_host: int = 64,
-                 idle_ttl: float = 30.0, max_idle_total: int = 512):
+                 idle_ttl: float = 30.0, max_idle_total: int = 512, tls: bool = True,
+                 ssl_verify: bool = True, ca_file: str = ""):
         from ..ops import native
         self._n = native()
-        # (host, port) -> [(conn, released at)], most recently released last. Idle sockets
+        # one SSL_CTX for every https connection of this transport (None: http only)
+        self._tls = self._n.TlsContext(ssl_verify, ca_file) if tls else None
+        # (host, port, tls) -> [(conn, released at)], most recently released last. Idle sockets
         # expire after idle_ttl (servers drop keep-alive connections anyway) and at most
         # max_idle_total stay open over all hosts: a long-running worker that fetched from
         # many origins must not sit on hosts x 64 idle file descriptors.
-        self._pool: Dict[Tuple[str, int], List[Tuple[object, float]]] = {}
+        self._pool: Dict[Tuple[str, int, bool], List[Tuple[object, float]]] = {}
         self.idle_ttl = idle_ttl
         self.max_idle_total = max_idle_total
         self._idle_total = 0
@@ -195,11 +206,18 @@ class NativeTransport(Transport):
         self.io_timeout = io_timeout
         self.max_idle = max_idle_per_host
 
-    def _acquire(self, host: str, port: int) -> Tuple[object, bool]:
+    def handles(self, url: str, proxied: bool = False) -> bool:
+        """http:// always; https:// when TLS is on and no forward proxy applies (a CONNECT
+        tunnel is left to aiohttp)."""
+        if url.startswith("http://"):
+            return True
+        return url.startswith("https://") and self._tls is not None and not proxied
+
+    def _acquire(self, host: str, port: int, tls: bool = False) -> Tuple[object, bool]:
         stale = []
         try:
             with self._lock:
-                idle = self._pool.get((host, port))
+                idle = self._pool.get((host, port, tls))
                 now = time.monotonic()
                 while idle:
                     conn, t = idle.pop()
@@ -213,8 +231,11 @@ class NativeTransport(Transport):
         finally:
             for c in stale:
                 c.close()
+        if tls and self._tls is None:
+            raise ValueError("NativeTransport built without TLS")
         try:
-            return self._n.HttpConn(host, port, self.connect_timeout, self.io_timeout), False
+            return self._n.HttpConn(host, port, self.connect_timeout, self.io_timeout,
+                                    self._tls if tls else None), False
         except RuntimeError as e:
             raise TransportError(str(e)) from e
 
@@ -224,7 +245,7 @@ class NativeTransport(Transport):
             return
         drop = []
         with self._lock:
-            idle = self._pool.setdefault((conn.host, conn.port), [])
+            idle = self._pool.setdefault((conn.host, conn.port, conn.tls), [])
             if len(idle) < self.max_idle:
                 idle.append((conn, time.monotonic()))
                 self._idle_total += 1
@@ -281,12 +302,12 @@ class NativeTransport(Transport):
 
     def _do(self, method: str, host: str, port: int, host_hdr: str, path: str,
             headers: Headers, body, sink: Optional[FileSink], nprog,
-            expect_body: bool, slot: int = 0) -> Response:
+            expect_body: bool, slot: int = 0, tls: bool = False) -> Response:
         blen = body.length if isinstance(body, FileRange) else (len(body) if body else 0)
         head = _build_head(method, host_hdr, path, headers, blen if body is not None else
                            (0 if method in ("PUT", "POST") else None))
         for attempt in (0, 1):
-            conn, reused = self._acquire(host, port)
+            conn, reused = self._acquire(host, port, tls)
             self._track(slot, conn)
             try:
                 if isinstance(body, FileRange):
@@ -314,9 +335,11 @@ class NativeTransport(Transport):
                       progress: Optional[Progress] = None, expect_body: bool = True,
                       proxy: Optional[Proxy] = None) -> Response:
         scheme, host, port, path = split_host(url)
-        if scheme != "http":
-            raise ValueError("NativeTransport handles plain http:// only")
-        host_hdr = host if port == 80 else f"{host}:{port}"
+        if not self.handles(url, proxy is not None):
+            raise ValueError(f"NativeTransport cannot send {scheme}://"
+                             + (" through a proxy" if proxy is not None else ""))
+        tls = scheme == "https"
+        host_hdr = _host_hdr(host, port, tls)
         if proxy is not None:      # absolute-form request target to the forward proxy
             host, port, path, headers = _via_proxy(proxy, url, headers)
         nprog = None
@@ -327,7 +350,7 @@ class NativeTransport(Transport):
         loop = asyncio.get_running_loop()
         slot = self._new_slot()
         fut = loop.run_in_executor(self._exec, self._do, method, host, port, host_hdr, path,
-                                   headers, body, sink, nprog, expect_body, slot)
+                                   headers, body, sink, nprog, expect_body, slot, tls)
         try:
             return await asyncio.shield(fut)
         except asyncio.CancelledError:
@@ -353,17 +376,22 @@ class NativeTransport(Transport):
                length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None,
                src_proxy: Optional[Proxy] = None
                ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
-        _, sh, sp, spath = split_host(src_url)
-        _, dh, dp, dpath = split_host(dst_url)
-        src_host_hdr = sh if sp == 80 else f"{sh}:{sp}"
+        ss, sh, sp, spath = split_host(src_url)
+        ds, dh, dp, dpath = split_host(dst_url)
+        if not (self.handles(src_url, src_proxy is not None) and self.handles(dst_url)):
+            raise TransportError(f"relay {ss}:// -> {ds}://"
+                                 + (" through a proxy" if src_proxy is not None else "")
+                                 + ": not supported by the native transport")
+        stls, dtls = ss == "https", ds == "https"
+        src_host_hdr = _host_hdr(sh, sp, stls)
         if src_proxy is not None:
             sh, sp, spath, src_headers = _via_proxy(src_proxy, src_url, src_headers)
         get_head = _build_head("GET", src_host_hdr, spath, src_headers, None)
-        put_head = _build_head("PUT", dh if dp == 80 else f"{dh}:{dp}", dpath, dst_headers, length)
-        src, _ = self._acquire(sh, sp)
+        put_head = _build_head("PUT", _host_hdr(dh, dp, dtls), dpath, dst_headers, length)
+        src, _ = self._acquire(sh, sp, stls)
         self._track(slot, src)
         try:
-            dst, _ = self._acquire(dh, dp)
+            dst, _ = self._acquire(dh, dp, dtls)
         except BaseException:
             self._untrack(slot, src)
             self._release(src)
@@ -399,8 +427,9 @@ class NativeTransport(Transport):
                     src_proxy: Optional[ProxyConfig] = None
                     ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         """GET ``src_url`` and stream exactly ``length`` body bytes as the body of a PUT to
-        ``dst_url`` without touching user space (socket -> pipe -> socket splice). The PUT is
-        only sent when the GET answers 2xx with exactly that Content-Length.
+        ``dst_url`` without touching user space (socket -> pipe -> socket splice; through an
+        L2-sized buffer when either end is TLS). The PUT is only sent when the GET answers 2xx
+        with exactly that Content-Length.
 
         ``split=(skip, full_len, piece_len)``: relay through L2-sized user-space chunks and
         SHA-1 body bytes [skip, skip+full_len) as consecutive pieces on the way; the 4th
@@ -430,9 +459,10 @@ class NativeTransport(Transport):
             nxt = redirect_target(src_url, get) if put is None else None
             if nxt is None:
                 return out
-            if not nxt.startswith("http://"):
-                raise TransportError(f"relay source {src_url} redirects to {nxt}: the "
-                                     f"socket relay needs plain http", get.status)
+            if not self.handles(nxt, src_proxy is not None and
+                                src_proxy.for_url(nxt) is not None):
+                raise TransportError(f"relay source {src_url} redirects to {nxt}: not "
+                                     f"supported by the socket relay", get.status)
             src_headers = redirect_headers(src_url, nxt, src_headers)
             src_url = nxt
         raise TransportError(f"relay source: more than {MAX_REDIRECTS} redirects", 310)
@@ -566,8 +596,8 @@ class TransportSet:
     native: Optional[NativeTransport] = None
     fallback: AiohttpTransport = field(default_factory=AiohttpTransport)
 
-    def for_url(self, url: str) -> Transport:
-        if self.native is not None and url.startswith("http://"):
+    def for_url(self, url: str, proxied: bool = False) -> Transport:
+        if self.native is not None and self.native.handles(url, proxied):
             return self.native
         return self.fallback
 
@@ -592,7 +622,7 @@ class TransportSet:
     async def _one(self, method: str, url: str, proxy: Optional[ProxyConfig], kw) -> Response:
         px = proxy.for_url(url) if proxy is not None else None
         if px is not None:
-            return await self.for_url(url).request(method, url, proxy=px, **kw)
+            return await self.for_url(url, True).request(method, url, proxy=px, **kw)
         return await self.for_url(url).request(method, url, **kw)
 
     async def close(self) -> None:
@@ -603,8 +633,9 @@ class TransportSet:
 
 def make_transports(native: bool = True, max_workers: int = 32, connect_timeout: float = 10.0,
                     io_timeout: float = 300.0, ssl_verify: bool = True,
-                    ca_file: str = "") -> TransportSet:
-    nt = NativeTransport(max_workers, connect_timeout, io_timeout) if native else None
+                    ca_file: str = "", native_tls: bool = True) -> TransportSet:
+    nt = NativeTransport(max_workers, connect_timeout, io_timeout, tls=native_tls,
+                         ssl_verify=ssl_verify, ca_file=ca_file) if native else None
     return TransportSet(nt, AiohttpTransport(connect_timeout, io_timeout, ssl_verify=ssl_verify,
                                              ca_file=ca_file))
 

@@ -48,13 +48,14 @@ def _run(cmd: List[str], verbose: bool) -> None:
 
 
 def build_native(force: bool = False, verbose: bool = True) -> Path:
-    srcs = [CSRC / "module.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp"]
+    srcs = [CSRC / "module.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp",
+            CSRC / "tls.cpp"]
     out = OPS / f"_native{EXT}"
     if force or _stale(out, srcs + [CSRC / "native.h"]):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
                "-march=x86-64-v3", "-Wall", "-Wno-unused-result",
-               *_pybind_includes(), *[str(s) for s in srcs], "-lcrypto", "-lpthread",
+               *_pybind_includes(), *[str(s) for s in srcs], "-lssl", "-lcrypto", "-lpthread",
                "-o", str(out)]
         _run(cmd, verbose)
     return out
@@ -78,7 +79,7 @@ def build_blobd(force: bool = False, verbose: bool = True) -> Path:
     if force or _stale(out, srcs):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O3", "-std=c++17", "-march=x86-64-v3", "-Wall", str(srcs[0]),
-               "-lpthread", "-o", str(out)]
+               "-lssl", "-lcrypto", "-lpthread", "-o", str(out)]
         _run(cmd, verbose)
     return out
 
@@ -89,13 +90,14 @@ SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"
 
 def build_selftest(kind: str, force: bool = False, verbose: bool = True) -> Path:
     """Host-only sanitizer build of the native code's self-test."""
-    srcs = [CSRC / "selftest.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp"]
+    srcs = [CSRC / "selftest.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp",
+            CSRC / "tls.cpp"]
     BIN.mkdir(exist_ok=True)
     out = BIN / f"selftest_{kind}"
     if force or _stale(out, srcs + [CSRC / "native.h"]):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O1", "-g", "-std=c++17", *SANITIZERS[kind], *[str(s) for s in srcs],
-               "-lcrypto", "-lpthread", "-o", str(out)]
+               "-lssl", "-lcrypto", "-lpthread", "-o", str(out)]
         _run(cmd, verbose)
     return out
 

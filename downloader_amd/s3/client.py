@@ -100,7 +100,8 @@ class S3Client:
                  part_size: int = 16 * MiB, multipart_threshold: int = 64 * MiB,
                  max_inflight_parts: int = 8, unsigned_payload: bool = True, retries: int = 3,
                  native: bool = True, connect_timeout: float = 10.0,
-                 request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = ""):
+                 request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = "",
+                 native_tls: bool = True):
         if "://" in endpoint:
             secure = endpoint.startswith("https://")
             endpoint = endpoint.split("://", 1)[1]
@@ -112,7 +113,8 @@ class S3Client:
         self._own_transports = transports is None
         self.t = transports or make_transports(native=native, connect_timeout=connect_timeout,
                                                io_timeout=request_timeout,
-                                               ssl_verify=ssl_verify, ca_file=ca_file)
+                                               ssl_verify=ssl_verify, ca_file=ca_file,
+                                               native_tls=native_tls)
         self.part_size = max(MIN_PART, part_size)
         self.multipart_threshold = multipart_threshold
         self.max_inflight_parts = max(1, max_inflight_parts)
@@ -322,9 +324,12 @@ class S3Client:
         return {n: remote[n][0] for (n, _, _), d in zip(cand, md5s) if d.hex() == remote[n][0]}
 
     # ------------------------------------------------------------------ streaming relay
-    def can_relay(self, src_url: str) -> bool:
+    def can_relay(self, src_url: str, src_proxy=None) -> bool:
+        """Socket relay source -> this endpoint possible (both http, or https with native TLS;
+        an https source behind a forward proxy is not)."""
         nt = getattr(self.t, "native", None)
-        return nt is not None and src_url.startswith("http://") and self.base.startswith("http://")
+        proxied = src_proxy is not None and src_proxy.for_url(src_url) is not None
+        return nt is not None and nt.handles(src_url, proxied) and nt.handles(self.base)
 
     def _signed(self, method: str, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                 headers: Optional[Dict[str, str]] = None) -> Tuple[str, List[Tuple[str, str]]]:

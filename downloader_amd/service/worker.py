@@ -84,7 +84,7 @@ class Worker:
             max_workers=max(16, cfg.concurrency * 2 *
                             (cfg.s3.max_inflight_parts + cfg.download.http_streams)),
             connect_timeout=cfg.s3.connect_timeout_s, io_timeout=cfg.s3.request_timeout_s,
-            ssl_verify=cfg.tls.verify, ca_file=cfg.tls.ca_file)
+            ssl_verify=cfg.tls.verify, ca_file=cfg.tls.ca_file, native_tls=cfg.tls.native)
         self.s3 = s3 or S3Client.from_config(cfg.s3, self.transports)
         self.telemetry = telemetry or Telemetry.from_config(cfg, self.broker, self.log)
         self.tracer = tracer or init_tracer("downloader", cfg.trace.enabled, cfg.trace.path)

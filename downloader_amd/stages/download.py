@@ -119,10 +119,12 @@ class DownloadStage(Stage):
         supports Range for multipart sizes). The object lands under the same key, the
         progress curve and done marker are unchanged; otherwise the disk path runs."""
         s3 = self.sv.s3
-        if not s3.can_relay(url) or not select_from_config(self.cfg).accepts_single_file(name):
+        if not s3.can_relay(url, self.proxy) or \
+                not select_from_config(self.cfg).accepts_single_file(name):
             return False
         size, ranges, final = await http_src.probe(self.sv.transports, url, self.proxy)
-        if size <= 0 or (size > s3.multipart_threshold and not ranges) or not s3.can_relay(final):
+        if size <= 0 or (size > s3.multipart_threshold and not ranges) or \
+                not s3.can_relay(final, self.proxy):
             return False
         await ensure_staging_bucket(self.sv)
         key = keys.object_key(job.id, name)
@@ -153,7 +155,8 @@ class DownloadStage(Stage):
                                               logger=job.logger, progress=prog,
                                               native=self.cfg.s3.native_transport,
                                               ssl_verify=self.cfg.tls.verify,
-                                              ca_file=self.cfg.tls.ca_file)
+                                              ca_file=self.cfg.tls.ca_file,
+                                              native_tls=self.cfg.tls.native)
         n = sum(os.path.getsize(f) for f in files)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("bucket", n)

@@ -165,6 +165,9 @@ class TlsConfig(BaseModel):
     """TLS for https:// sources, S3 with ``secure: true`` and bucket:// (always TLS)."""
     verify: bool = True                         # False: accept any certificate
     ca_file: str = ""                           # extra PEM trust (private CA), beside the system store
+    # TLS in the native transport (OpenSSL on the transfer threads, csrc/tls.cpp); False
+    # sends https through aiohttp on the event loop (one core per process for all streams)
+    native: bool = True
 
 
 class Config(BaseModel):

@@ -47,13 +47,18 @@ async def _wait(w, n=1, timeout=30.0):
     assert len(w.results) >= n, w.results
 
 
-def test_s3_client_over_tls(run, cert, tmp_path):
+@pytest.mark.parametrize("native_tls", [True, False])
+def test_s3_client_over_tls(run, cert, tmp_path, native_tls):
+    """Same S3 traffic through the native OpenSSL transport (pread + SSL_write for file
+    bodies, SSL_read + pwrite into sinks) and through aiohttp."""
     async def go():
         s3 = FakeS3(ssl_context=_server_ctx(cert))
         ep = await s3.start()
         c = S3Client(ep, *CREDS, secure=True, ca_file=cert[0], part_size=5 << 20,
-                     multipart_threshold=6 << 20)
+                     multipart_threshold=6 << 20, native_tls=native_tls)
         assert c.base.startswith("https://")
+        used = type(c.t.for_url(c.base)).__name__
+        assert used == ("NativeTransport" if native_tls else "AiohttpTransport")
         await c.ensure_bucket("b")
         await c.put_object("b", "small", b"hello")
         assert await c.get_object("b", "small") == b"hello"
@@ -67,11 +72,12 @@ def test_s3_client_over_tls(run, cert, tmp_path):
         assert dst.read_bytes() == blob
         await c.close()
         # the system store alone does not trust the throwaway CA; verify=False does
-        untrusted = S3Client(ep, *CREDS, secure=True, retries=0)
-        with pytest.raises((TransportError, S3Error)):
+        untrusted = S3Client(ep, *CREDS, secure=True, retries=0, native_tls=native_tls)
+        with pytest.raises((TransportError, S3Error)) as ei:
             await untrusted.get_object("b", "small")
+        assert "certificate" in str(ei.value).lower()
         await untrusted.close()
-        lax = S3Client(ep, *CREDS, secure=True, ssl_verify=False)
+        lax = S3Client(ep, *CREDS, secure=True, ssl_verify=False, native_tls=native_tls)
         assert await lax.get_object("b", "small") == b"hello"
         await lax.close()
         await s3.stop()
@@ -97,12 +103,14 @@ def test_worker_https_origin_tls_s3_and_bucket_source(run, make_cfg, origin_cls,
         await _wait(w)
         assert w.results[0].outcome == "staged", w.results[0]
         assert s3.get("triton-staging", keys.object_key("t1", "Movie.mkv")) == blob
-        plain = await origin_cls().start()         # http origin -> TLS S3: no socket relay
+        assert w.results[0].stats.get("streamed")     # https -> https socket relay, no disk
+        plain = await origin_cls().start()         # http origin -> TLS S3
         plain.blobs["/Film.mkv"] = blob[::-1]
         await w.submit(api.make_download("t0", "http", plain.url("/Film.mkv"), "MOVIE"))
         await _wait(w, 2)
         assert w.results[1].outcome == "staged", w.results[1]
         assert s3.get("triton-staging", keys.object_key("t0", "Film.mkv")) == blob[::-1]
+        assert w.results[1].stats.get("streamed")     # http -> https relay
         await plain.stop()
         s3.buckets["src"] = {}
         s3.put("src", "show/S1/ep1.mkv", b"one" * 1000)
@@ -131,6 +139,44 @@ def test_worker_rejects_untrusted_origin(run, make_cfg, origin_cls, cert):
         r = w.results[0]
         assert r.outcome == "dead" and "certificate" in r.error.lower(), r
         assert not s3.buckets.get("triton-staging")
+        await w.stop()
+        await origin.stop()
+        await s3.stop()
+    run(go())
+
+
+def test_stream_torrent_over_tls(run, tmp_path, make_cfg, origin_cls, cert):
+    """Webseed-only torrent on an https webseed, staged into a TLS S3 by the hashed relay
+    (SSL_read -> buffer -> SSL_write, pieces SHA-1'd in flight); a corrupt piece is caught
+    and refetched, nothing touches the disk."""
+    from downloader_amd.torrent.metainfo import make_torrent, parse_torrent
+
+    async def go():
+        s3 = FakeS3(ssl_context=_server_ctx(cert))
+        ep = await s3.start()
+        origin = await origin_cls(ssl_context=_server_ctx(cert)).start()
+        src = tmp_path / "src" / "Show" / "Season 1"
+        src.mkdir(parents=True)
+        data = {"e1.mkv": os.urandom(6_500_001), "e2.mkv": os.urandom(300_007)}
+        for n, d in data.items():
+            (src / n).write_bytes(d)
+            origin.blobs["/ws/Show/Season 1/" + n] = d
+        raw = make_torrent(str(tmp_path / "src" / "Show"), 131072, url_list=[origin.url("/ws/")])
+        origin.blobs["/t/show.torrent"] = raw
+        origin.corrupt["/ws/Show/Season 1/e1.mkv"] = [3_000_000, 1]
+        assert parse_torrent(raw).url_list[0].startswith("https://")
+        w = Worker(make_cfg(ep, s3={"secure": True}, tls={"ca_file": cert[0]},
+                            download={"torrent_enable_dht": False}), broker=MemoryBroker())
+        await w.start(health=False)
+        await w.submit(api.make_download("ts", "http", origin.url("/t/show.torrent"), "TV"))
+        await _wait(w)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        assert r.stats["torrent"]["staging"] == "stream" and r.stats["torrent"]["hash_fails"] >= 1
+        for n, d in data.items():
+            assert s3.get("triton-staging", keys.object_key("ts", n)) == d
+        for dp, _, fns in os.walk(tmp_path / "dl"):
+            assert not [f for f in fns if f.endswith(".mkv")], (dp, fns)
         await w.stop()
         await origin.stop()
         await s3.stop()
