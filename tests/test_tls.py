@@ -181,3 +181,38 @@ def test_stream_torrent_over_tls(run, tmp_path, make_cfg, origin_cls, cert):
         await origin.stop()
         await s3.stop()
     run(go())
+
+
+@pytest.mark.parametrize("native_tls", [True, False])
+def test_tls_host_name_checked(run, tmp_path, native_tls):
+    """DNS names: SNI is sent and the certificate must name the host (SSL_set1_host), like
+    Node's checkServerIdentity; a certificate for another name is refused."""
+    def mk(name):
+        d = tmp_path / name
+        d.mkdir()
+        crt, key = str(d / "c.pem"), str(d / "k.pem")
+        subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout",
+                        key, "-out", crt, "-days", "1", "-subj", f"/CN={name}",
+                        "-addext", f"subjectAltName=DNS:{name}"],
+                       check=True, capture_output=True, timeout=60)
+        return crt, key
+
+    async def go():
+        for name, ok in (("localhost", True), ("other.example", False)):
+            cert = mk(name)
+            s3 = FakeS3(ssl_context=_server_ctx(cert))
+            await s3.start()
+            c = S3Client(f"localhost:{s3.port}", *CREDS, secure=True, ca_file=cert[0],
+                         retries=0, native_tls=native_tls)
+            if ok:
+                await c.ensure_bucket("b")
+                await c.put_object("b", "k", b"v")
+                assert await c.get_object("b", "k") == b"v"
+            else:
+                with pytest.raises((TransportError, S3Error)) as ei:
+                    await c.get_object("b", "k")
+                msg = str(ei.value).lower()
+                assert "certificate" in msg or "hostname" in msg, msg
+            await c.close()
+            await s3.stop()
+    run(go())
