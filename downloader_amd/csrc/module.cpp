@@ -234,7 +234,7 @@ PYBIND11_MODULE(_native, m) {
            "plus ca_file (PEM), or not at all")
       .def_property_readonly("verify", &TlsContext::verify);
 
-  py::class_<HttpConn>(m, "HttpConn")
+  py::class_<HttpConn>(m, "HttpConn", py::dynamic_attr())
       .def(py::init([](const std::string& host, int port, double cto, double iot,
                        std::shared_ptr<TlsContext> tls) {
              py::gil_scoped_release rel;
@@ -335,6 +335,21 @@ PYBIND11_MODULE(_native, m) {
           "relay_to through a user-space chunk that is SHA-1'd on the way: body bytes "
           "[skip, skip+full_len) as consecutive `piece_len` pieces (last may be short). Adds "
           "`digests` (20 B per piece), `head` (bytes before skip) and `tail` (bytes after).")
+      .def(
+          "connect_tunnel",
+          [](HttpConn& c, const std::string& target, const std::string& auth) {
+            py::gil_scoped_release rel;
+            c.connect_tunnel(target, auth);
+          },
+          py::arg("target"), py::arg("auth") = "",
+          "CONNECT tunnel through the forward proxy this socket is connected to")
+      .def(
+          "start_tls",
+          [](HttpConn& c, std::shared_ptr<TlsContext> tls, const std::string& name) {
+            py::gil_scoped_release rel;
+            c.start_tls(std::move(tls), name);
+          },
+          py::arg("tls"), py::arg("server_name"))
       .def("close", &HttpConn::close)
       .def("abort", &HttpConn::abort)
       .def_property_readonly("is_open", &HttpConn::is_open)

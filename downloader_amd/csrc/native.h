@@ -148,6 +148,11 @@ class HttpConn {
   void send_request_fd(const std::string& head, int fd, int64_t off, int64_t len,
                        Progress* prog);
   ResponseHead read_head();
+  // This socket is connected to a forward proxy: open a CONNECT tunnel to "host:port"
+  // (`auth` = Proxy-Authorization value or ""). Throws unless the proxy answers 200.
+  void connect_tunnel(const std::string& target, const std::string& auth);
+  // TLS handshake on the (possibly tunnelled) socket; `name` is the server's host name.
+  void start_tls(std::shared_ptr<TlsContext> tls, const std::string& name);
   // Body into memory (bounded by max_bytes).
   std::string read_body(const ResponseHead& h, int64_t max_bytes);
   // Body into fd at `offset` (splice for Content-Length bodies, read/pwrite for chunked).

@@ -109,13 +109,41 @@ HttpConn::HttpConn(const std::string& host, int port, double connect_timeout_s,
   if (fd_ < 0) throw IoError(last + " (" + host + ":" + ps + ")");
   if (tls) {
     try {
-      ssl_ = tls_handshake(*tls, fd_, host);
-    } catch (const std::exception& e) {
+      start_tls(std::move(tls), host);
+    } catch (...) {
       close();  // the destructor does not run for a throwing constructor
-      throw IoError(e.what());
+      throw;
     }
-    tls_ = std::move(tls);
   }
+}
+
+void HttpConn::start_tls(std::shared_ptr<TlsContext> tls, const std::string& name) {
+  if (fd_ < 0) throw IoError("connection closed");
+  if (ssl_) throw IoError("TLS already started");
+  if (rpos_ != rend_) throw IoError("unread bytes before the TLS handshake");
+  try {
+    ssl_ = tls_handshake(*tls, fd_, name);
+  } catch (const std::exception& e) {
+    reusable_ = false;
+    throw IoError(e.what());
+  }
+  tls_ = std::move(tls);
+}
+
+void HttpConn::connect_tunnel(const std::string& target, const std::string& auth) {
+  std::string req = "CONNECT " + target + " HTTP/1.1\r\nHost: " + target + "\r\n";
+  if (!auth.empty()) req += "Proxy-Authorization: " + auth + "\r\n";
+  req += "\r\n";
+  send_all((const uint8_t*)req.data(), req.size());
+  ResponseHead h = read_head();
+  if (h.status != 200) {
+    reusable_ = false;
+    throw IoError("proxy CONNECT " + target + ": HTTP " + std::to_string(h.status) + " " +
+                  h.reason);
+  }
+  // A 2xx to CONNECT has no body: the socket is the tunnel from here on (read_head judged
+  // it by HTTP framing rules, which do not apply).
+  reusable_ = true;
 }
 
 HttpConn::~HttpConn() { close(); }

@@ -7,8 +7,8 @@ Two implementations behind one async interface:
   bodies go through OpenSSL on the same threads (``csrc/tls.cpp``). Each request runs on a
   dedicated thread pool with the GIL released, so many transfers (and their encryption)
   proceed in parallel inside one worker process.
-* ``AiohttpTransport`` - the rest: https through a forward proxy (CONNECT), or everything
-  when the native module is off.
+  https through a forward proxy tunnels with CONNECT on the same connection.
+* ``AiohttpTransport`` - everything when the native module (or its TLS) is off.
 
 A request body is ``bytes`` or a ``FileRange``; a response body is returned in memory or
 written into a ``FileSink``.
@@ -135,9 +135,12 @@ def _via_proxy(proxy: Proxy, url: str, headers: Headers
     return proxy.host, proxy.port, target, hdrs
 
 
+def _bracket(host: str) -> str:
+    return f"[{host}]" if ":" in host else host      # IPv6 literal
+
+
 def _host_hdr(host: str, port: int, tls: bool) -> str:
-    if ":" in host:             # IPv6 literal
-        host = f"[{host}]"
+    host = _bracket(host)
     return host if port == (443 if tls else 80) else f"{host}:{port}"
 
 
@@ -188,11 +191,12 @@ class NativeTransport(Transport):
         self._n = native()
         # one SSL_CTX for every https connection of this transport (None: http only)
         self._tls = self._n.TlsContext(ssl_verify, ca_file) if tls else None
-        # (host, port, tls) -> [(conn, released at)], most recently released last. Idle sockets
+        # (host, port, tls, via) -> [(conn, released at)], most recently released last (via:
+        # the CONNECT proxy of a tunnelled https connection, else None). Idle sockets
         # expire after idle_ttl (servers drop keep-alive connections anyway) and at most
         # max_idle_total stay open over all hosts: a long-running worker that fetched from
         # many origins must not sit on hosts x 64 idle file descriptors.
-        self._pool: Dict[Tuple[str, int, bool], List[Tuple[object, float]]] = {}
+        self._pool: Dict[tuple, List[Tuple[object, float]]] = {}
         self.idle_ttl = idle_ttl
         self.max_idle_total = max_idle_total
         self._idle_total = 0
@@ -207,17 +211,18 @@ class NativeTransport(Transport):
         self.max_idle = max_idle_per_host
 
     def handles(self, url: str, proxied: bool = False) -> bool:
-        """http:// always; https:// when TLS is on and no forward proxy applies (a CONNECT
-        tunnel is left to aiohttp)."""
+        """http:// always; https:// when TLS is on (behind a proxy: CONNECT tunnel)."""
         if url.startswith("http://"):
             return True
-        return url.startswith("https://") and self._tls is not None and not proxied
+        return url.startswith("https://") and self._tls is not None
 
-    def _acquire(self, host: str, port: int, tls: bool = False) -> Tuple[object, bool]:
+    def _acquire(self, host: str, port: int, tls: bool = False,
+                 tunnel: Optional[Proxy] = None) -> Tuple[object, bool]:
+        key = (host, port, tls, (tunnel.host, tunnel.port, tunnel.auth) if tunnel else None)
         stale = []
         try:
             with self._lock:
-                idle = self._pool.get((host, port, tls))
+                idle = self._pool.get(key)
                 now = time.monotonic()
                 while idle:
                     conn, t = idle.pop()
@@ -233,11 +238,22 @@ class NativeTransport(Transport):
                 c.close()
         if tls and self._tls is None:
             raise ValueError("NativeTransport built without TLS")
+        conn = None
         try:
-            return self._n.HttpConn(host, port, self.connect_timeout, self.io_timeout,
-                                    self._tls if tls else None), False
+            if tunnel is None:
+                conn = self._n.HttpConn(host, port, self.connect_timeout, self.io_timeout,
+                                        self._tls if tls else None)
+            else:                   # https via a forward proxy: CONNECT, then TLS inside
+                conn = self._n.HttpConn(tunnel.host, tunnel.port, self.connect_timeout,
+                                        self.io_timeout)
+                conn.connect_tunnel(f"{_bracket(host)}:{port}", tunnel.auth)
+                conn.start_tls(self._tls, host)
         except RuntimeError as e:
+            if conn is not None:
+                conn.close()
             raise TransportError(str(e)) from e
+        conn.pool_key = key
+        return conn, False
 
     def _release(self, conn) -> None:
         if not conn.reusable:
@@ -245,7 +261,7 @@ class NativeTransport(Transport):
             return
         drop = []
         with self._lock:
-            idle = self._pool.setdefault((conn.host, conn.port, conn.tls), [])
+            idle = self._pool.setdefault(conn.pool_key, [])
             if len(idle) < self.max_idle:
                 idle.append((conn, time.monotonic()))
                 self._idle_total += 1
@@ -302,12 +318,13 @@ class NativeTransport(Transport):
 
     def _do(self, method: str, host: str, port: int, host_hdr: str, path: str,
             headers: Headers, body, sink: Optional[FileSink], nprog,
-            expect_body: bool, slot: int = 0, tls: bool = False) -> Response:
+            expect_body: bool, slot: int = 0, tls: bool = False,
+            tunnel: Optional[Proxy] = None) -> Response:
         blen = body.length if isinstance(body, FileRange) else (len(body) if body else 0)
         head = _build_head(method, host_hdr, path, headers, blen if body is not None else
                            (0 if method in ("PUT", "POST") else None))
         for attempt in (0, 1):
-            conn, reused = self._acquire(host, port, tls)
+            conn, reused = self._acquire(host, port, tls, tunnel)
             self._track(slot, conn)
             try:
                 if isinstance(body, FileRange):
@@ -340,7 +357,8 @@ class NativeTransport(Transport):
                              + (" through a proxy" if proxy is not None else ""))
         tls = scheme == "https"
         host_hdr = _host_hdr(host, port, tls)
-        if proxy is not None:      # absolute-form request target to the forward proxy
+        tunnel = proxy if tls else None
+        if proxy is not None and not tls:   # absolute-form request target to the proxy
             host, port, path, headers = _via_proxy(proxy, url, headers)
         nprog = None
         if progress is not None:
@@ -350,7 +368,7 @@ class NativeTransport(Transport):
         loop = asyncio.get_running_loop()
         slot = self._new_slot()
         fut = loop.run_in_executor(self._exec, self._do, method, host, port, host_hdr, path,
-                                   headers, body, sink, nprog, expect_body, slot, tls)
+                                   headers, body, sink, nprog, expect_body, slot, tls, tunnel)
         try:
             return await asyncio.shield(fut)
         except asyncio.CancelledError:
@@ -384,11 +402,12 @@ class NativeTransport(Transport):
                                  + ": not supported by the native transport")
         stls, dtls = ss == "https", ds == "https"
         src_host_hdr = _host_hdr(sh, sp, stls)
-        if src_proxy is not None:
+        tunnel = src_proxy if stls else None
+        if src_proxy is not None and not stls:
             sh, sp, spath, src_headers = _via_proxy(src_proxy, src_url, src_headers)
         get_head = _build_head("GET", src_host_hdr, spath, src_headers, None)
         put_head = _build_head("PUT", _host_hdr(dh, dp, dtls), dpath, dst_headers, length)
-        src, _ = self._acquire(sh, sp, stls)
+        src, _ = self._acquire(sh, sp, stls, tunnel)
         self._track(slot, src)
         try:
             dst, _ = self._acquire(dh, dp, dtls)
@@ -482,7 +501,8 @@ class NativeTransport(Transport):
 
 
 class AiohttpTransport(Transport):
-    """https:// (and proxied) requests. TLS peers are verified against the system trust store,
+    """Requests when the native transport (or its TLS) is off. TLS peers are verified against
+    the system trust store,
     plus ``ca_file`` (PEM bundle, e.g. the private CA of an in-cluster MinIO) when given;
     ``ssl_verify=False`` turns verification off (minio-js ``transport`` with
     ``rejectUnauthorized: false``)."""

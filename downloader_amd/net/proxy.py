@@ -13,8 +13,8 @@ proxied (request@2 would proxy them unless listed in NO_PROXY).
 ``download.http_proxy`` picks the behaviour: ``env`` (default, as the reference), ``""``
 (never) or an explicit ``http://[user:pass@]host:port`` URL for every source request.
 Plain-http sources go to the proxy in absolute form (``GET http://host/path``) on the native
-transport, so the stream relay still splices origin -> S3; https sources tunnel with CONNECT
-through aiohttp.
+transport, so the stream relay still splices origin -> S3; https sources open a CONNECT
+tunnel on the native transport and run TLS inside it (``HttpConn.connect_tunnel``).
 """
 from __future__ import annotations
 

@@ -216,3 +216,62 @@ def test_tls_host_name_checked(run, tmp_path, native_tls):
             await c.close()
             await s3.stop()
     run(go())
+
+
+def test_https_source_through_connect_proxy(run, make_cfg, origin_cls, cert):
+    """https sources behind download.http_proxy: a CONNECT tunnel on the native transport,
+    TLS inside it (stream relay and disk path); S3 traffic is not proxied."""
+    from test_worker import _ForwardProxy
+
+    async def go():
+        proxy = await _ForwardProxy().start()
+        purl = f"http://user:pw@127.0.0.1:{proxy.port}"
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls(ssl_context=_server_ctx(cert)).start()
+        big = os.urandom((13 << 20) + 1)
+        origin.blobs["/p/big.mkv"] = big
+        for job, stream in (("cp1", True), ("cp2", False)):
+            cfg = make_cfg(ep, tls={"ca_file": cert[0]},
+                           download={"http_proxy": purl, "stream_http": stream})
+            w = Worker(cfg, broker=MemoryBroker())
+            await w.start(health=False)
+            assert type(w.transports.for_url(origin.url("/"), True)).__name__ == "NativeTransport"
+            await w.submit(api.make_download(job, "http", origin.url("/p/big.mkv")))
+            await _wait(w)
+            r = w.results[0]
+            assert r.outcome == "staged", r
+            assert bool(r.stats.get("streamed")) == stream
+            assert s3.get("triton-staging", keys.object_key(job, "big.mkv")) == big
+            await w.stop()
+        lines = [ln for ln, _ in proxy.seen]
+        assert lines and all(ln == f"CONNECT 127.0.0.1:{origin.port} HTTP/1.1" for ln in lines)
+        assert {a for _, a in proxy.seen} == {"Basic dXNlcjpwdw=="}
+        await proxy.stop()
+        await origin.stop()
+        await s3.stop()
+    run(go())
+
+
+def test_connect_refused_by_proxy(run):
+    """A proxy that refuses the tunnel (407) fails the request with the proxy's answer."""
+    from downloader_amd.net.http import NativeTransport
+    from downloader_amd.net.proxy import Proxy
+
+    async def go():
+        async def deny(r, w):
+            await r.readuntil(b"\r\n\r\n")
+            w.write(b"HTTP/1.1 407 Proxy Authentication Required\r\nContent-Length: 0\r\n\r\n")
+            await w.drain()
+            w.close()
+        srv = await asyncio.start_server(deny, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        t = NativeTransport(4)
+        with pytest.raises(TransportError) as ei:
+            await t.request("GET", "https://example.invalid/x",
+                            proxy=Proxy(f"http://127.0.0.1:{port}", "127.0.0.1", port))
+        assert "407" in str(ei.value) and "CONNECT example.invalid:443" in str(ei.value)
+        await t.close()
+        srv.close()
+        await srv.wait_closed()
+    run(go())

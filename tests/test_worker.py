@@ -571,8 +571,8 @@ def test_http_sources_follow_redirects(run, make_cfg, origin_cls):
 
 
 class _ForwardProxy:
-    """Minimal HTTP/1.1 forward proxy for tests: absolute-form requests only, one request
-    per client connection (answers with Connection: close), records what it forwarded."""
+    """Minimal HTTP/1.1 forward proxy for tests: absolute-form requests (one per client
+    connection, answered with Connection: close) and CONNECT tunnels; records what it saw."""
 
     def __init__(self):
         self.seen = []          # (request line, Proxy-Authorization)
@@ -593,6 +593,24 @@ class _ForwardProxy:
             auth = next((ln.split(":", 1)[1].strip() for ln in lines[1:]
                          if ln.lower().startswith("proxy-authorization:")), "")
             self.seen.append((lines[0], auth))
+            if method == "CONNECT":
+                host, _, port = target.rpartition(":")
+                orr, ow = await asyncio.open_connection(host.strip("[]"), int(port))
+                w.write(b"HTTP/1.1 200 Connection established\r\n\r\n")
+                await w.drain()
+
+                async def pump(src, dst):
+                    try:
+                        while True:
+                            chunk = await src.read(1 << 16)
+                            if not chunk:
+                                break
+                            dst.write(chunk)
+                            await dst.drain()
+                    finally:
+                        dst.close()
+                await asyncio.gather(pump(r, ow), pump(orr, w), return_exceptions=True)
+                return
             u = urlsplit(target)
             keep = [ln for ln in lines[1:] if ln and not ln.lower().startswith(
                 ("proxy-authorization:", "connection:"))]
