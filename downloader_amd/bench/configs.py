@@ -68,10 +68,27 @@ def _self_cpu() -> float:
     return ru.ru_utime + ru.ru_stime
 
 
-def _cfg(mode: str, endpoint: str, stage: str, **over) -> object:
+_CERT = None
+
+
+def _tls_cert(a):
+    """--tls: one throwaway certificate per bench process for blobd (origin, webseed, S3)."""
+    global _CERT
+    if not getattr(a, "tls", False):
+        return None
+    if _CERT is None:
+        from .infra import self_signed_cert
+        _CERT = self_signed_cert(tempfile.mkdtemp(prefix="cfg-tls-"))
+    return _CERT
+
+
+def _cfg(mode: str, endpoint: str, stage: str, tls=None, **over) -> object:
     o: Dict = {"mode": mode, "instance": {"download_path": stage}, "s3": {"endpoint": endpoint},
                "broker": {"backend": "memory"}, "health": {"enabled": False},
                "download": {"torrent_enable_dht": False, "progress_interval_s": 5.0}}
+    if tls is not None:
+        o["s3"]["secure"] = True
+        o["tls"] = {"ca_file": tls[0]}
     for k, v in over.items():
         if isinstance(v, dict):
             o.setdefault(k, {}).update(v)
@@ -111,8 +128,9 @@ def _write_random(path: str, n: int, seed: int) -> None:
 # ---------------------------------------------------------------------------- config 1
 async def config1(a) -> Dict:
     stage = tempfile.mkdtemp(prefix="cfg1-")
-    with Blobd(sink="discard") as b:
-        w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1), broker=MemoryBroker())
+    cert = _tls_cert(a)
+    with Blobd(sink="discard", tls=cert) as b:
+        w = Worker(_cfg(a.mode, b.endpoint, stage, cert, concurrency=1), broker=MemoryBroker())
         await w.start(health=False)
         lat = []
         for i in range(a.jobs):
@@ -125,6 +143,7 @@ async def config1(a) -> Dict:
     shutil.rmtree(stage, ignore_errors=True)
     lat = lat[1:] or lat   # first job warms connections
     return {"config": 1, "mode": a.mode, "jobs": len(lat), "object_MB": 10,
+            **({"tls": True} if cert else {}),
             "p50_latency_s": round(statistics.median(lat), 4),
             "p90_latency_s": round(_pct(lat, 0.9), 4),
             "MBps_sequential": round(10 / statistics.mean(lat), 1)}
@@ -154,7 +173,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
     src = tempfile.mkdtemp(prefix=f"cfg{cfg_no}-src-", dir=a.src_dir)
     stage = tempfile.mkdtemp(prefix=f"cfg{cfg_no}-stage-", dir=a.stage_dir or None)
     try:
-        with Blobd(sink="discard", files_root=src) as b:
+        cert = _tls_cert(a)
+        with Blobd(sink="discard", files_root=src, tls=cert) as b:
             t0 = time.perf_counter()
             raw = _make_torrent_tree(src, name, sizes, b.files_url(), a.piece_mb << 20)
             setup_s = time.perf_counter() - t0
@@ -175,7 +195,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["gpu_prewarm"] = False
             part_mb = getattr(a, "part_mb", 0)
             s3o = {"part_size": part_mb << 20} if part_mb else {}
-            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl, s3=s3o),
+            w = Worker(_cfg(a.mode, b.endpoint, stage, cert, concurrency=1, download=dl, s3=s3o),
                        broker=MemoryBroker())
             await w.start(health=False)
             # --reps: the same torrent staged again under a fresh media id (no done marker,
@@ -212,6 +232,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
         shutil.rmtree(src, ignore_errors=True)
         shutil.rmtree(stage, ignore_errors=True)
     return {"config": cfg_no, "mode": a.mode, "bytes": total, "files": len(sizes),
+            **({"tls": True} if cert else {}),
             "piece_len": a.piece_mb << 20, "job_s": round(dt, 3),
             "MBps": round(total / dt / MB, 1), "setup_s": round(setup_s, 2),
             "s3_bytes_received": st["bytes_received"], "uploaded_bytes": r[0].bytes,
@@ -397,6 +418,8 @@ def main(argv=None) -> int:
     ap.add_argument("--seed-inproc", action="store_true",
                     help="config 6: seeders on the measuring process's event loop (round 1)")
     ap.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
+    ap.add_argument("--tls", action="store_true",
+                    help="configs 1/3/4: origin, webseed and S3 over https (blobd certificate)")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")
     ap.add_argument("--piece-mb", type=int, default=4)
