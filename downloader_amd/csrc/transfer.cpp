@@ -128,6 +128,16 @@ void HttpConn::start_tls(std::shared_ptr<TlsContext> tls, const std::string& nam
     throw IoError(e.what());
   }
   tls_ = std::move(tls);
+  // Coalesce outgoing records: SSL_write emits one 16 KiB record per socket write; a buffer
+  // BIO in front of the socket turns them into 256 KiB sends, flushed by send_all.
+  BIO* sock = SSL_get_wbio(ssl_);
+  BIO* buf = BIO_new(BIO_f_buffer());
+  if (buf && BIO_set_write_buffer_size(buf, 256 * 1024) == 1) {
+    BIO_up_ref(sock);  // the chain holds its own reference; SSL drops the old wbio's
+    SSL_set0_wbio(ssl_, BIO_push(buf, sock));
+  } else if (buf) {
+    BIO_free(buf);
+  }
 }
 
 void HttpConn::connect_tunnel(const std::string& target, const std::string& auth) {
@@ -182,6 +192,11 @@ void HttpConn::send_all(const uint8_t* p, size_t n) {
       p += w;
       n -= (size_t)w;
     }
+    while (BIO_flush(SSL_get_wbio(ssl_)) <= 0) {
+      if (BIO_should_retry(SSL_get_wbio(ssl_)) && errno == EINTR) continue;
+      reusable_ = false;
+      throw IoError(errno == EAGAIN ? std::string("send timeout") : errstr("send"));
+    }
     return;
   }
   while (n) {
@@ -200,7 +215,20 @@ size_t HttpConn::recv_some(uint8_t* p, size_t n) {
   while (ssl_) {
     ERR_clear_error();
     int r = SSL_read(ssl_, p, (int)std::min<size_t>(n, (size_t)1 << 30));
-    if (r > 0) return (size_t)r;
+    if (r > 0) {
+      // SSL_read returns one record (<= 16 KiB); take whatever else is already buffered
+      // (read-ahead) so callers move 100s of KiB per call, not one record.
+      size_t got = (size_t)r;
+      while (got < n && SSL_has_pending(ssl_)) {
+        int k = SSL_read(ssl_, p + got, (int)std::min<size_t>(n - got, (size_t)1 << 30));
+        if (k <= 0) {
+          ERR_clear_error();  // reported by the next call, after these bytes are consumed
+          break;
+        }
+        got += (size_t)k;
+      }
+      return got;
+    }
     const int e = SSL_get_error(ssl_, r);
     if (e == SSL_ERROR_ZERO_RETURN) return 0;  // close_notify, or EOF (IGNORE_UNEXPECTED_EOF)
     if ((e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) && errno == EINTR) continue;
