@@ -168,6 +168,14 @@ class Conn {
         ERR_clear_error();
         return;
       }
+      BIO* sock = SSL_get_wbio(ssl_);  // coalesce 16 KiB records into 256 KiB sends
+      BIO* b = BIO_new(BIO_f_buffer());
+      if (b && BIO_set_write_buffer_size(b, 256 * 1024) == 1) {
+        BIO_up_ref(sock);
+        SSL_set0_wbio(ssl_, BIO_push(b, sock));
+      } else if (b) {
+        BIO_free(b);
+      }
     }
     for (;;) {
       Request r;
@@ -193,6 +201,14 @@ class Conn {
         return false;
       }
       end_ += (size_t)r;
+      while (end_ < buf_.size() && SSL_has_pending(ssl_)) {
+        r = SSL_read(ssl_, buf_.data() + end_, (int)(buf_.size() - end_));
+        if (r <= 0) {
+          ERR_clear_error();
+          break;
+        }
+        end_ += (size_t)r;
+      }
       return true;
     }
     ssize_t r = ::recv(fd_, buf_.data() + end_, buf_.size() - end_, 0);
@@ -326,7 +342,7 @@ class Conn {
         c += w;
         n -= (size_t)w;
       }
-      return true;
+      return BIO_flush(SSL_get_wbio(ssl_)) > 0;
     }
     while (n) {
       ssize_t w = ::send(fd_, c, n, MSG_NOSIGNAL);
