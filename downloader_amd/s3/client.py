@@ -18,6 +18,7 @@ from __future__ import annotations
 import asyncio
 import os
 import random
+import re
 import xml.etree.ElementTree as ET
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -28,6 +29,7 @@ from ..net.http import (FileRange, FileSink, Progress, Response, TransportError,
 from . import sigv4
 
 NS = "{http://s3.amazonaws.com/doc/2006-03-01/}"
+_DNS_BUCKET = re.compile(r"^[a-z0-9][a-z0-9.-]{1,61}[a-z0-9]$")
 MiB = 1 << 20
 MAX_PARTS = 10000
 MIN_PART = 5 * MiB
@@ -101,12 +103,16 @@ class S3Client:
                  max_inflight_parts: int = 8, unsigned_payload: bool = True, retries: int = 3,
                  native: bool = True, connect_timeout: float = 10.0,
                  request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = "",
-                 native_tls: bool = True):
+                 native_tls: bool = True, addressing: str = "auto"):
         if "://" in endpoint:
             secure = endpoint.startswith("https://")
             endpoint = endpoint.split("://", 1)[1]
         self.endpoint = endpoint.rstrip("/")
-        self.base = ("https://" if secure else "http://") + self.endpoint
+        self.scheme = "https" if secure else "http"
+        self.base = self.scheme + "://" + self.endpoint
+        if addressing not in ("auto", "path", "virtual"):
+            raise ValueError(f"s3 addressing {addressing!r}: auto, path or virtual")
+        self.addressing = addressing
         self.access_key = access_key
         self.secret_key = secret_key
         self.region = region
@@ -127,7 +133,30 @@ class S3Client:
         return cls(s3cfg.endpoint, s3cfg.access_key, s3cfg.secret_key, s3cfg.region,
                    s3cfg.secure, transports, s3cfg.part_size, s3cfg.multipart_threshold,
                    s3cfg.max_inflight_parts, s3cfg.unsigned_payload, s3cfg.retries,
-                   s3cfg.native_transport, s3cfg.connect_timeout_s, s3cfg.request_timeout_s)
+                   s3cfg.native_transport, s3cfg.connect_timeout_s, s3cfg.request_timeout_s,
+                   addressing=s3cfg.addressing)
+
+    def virtual_host(self, bucket: str) -> bool:
+        """Virtual-hosted-style addressing (``<bucket>.<endpoint>/<key>``) for this bucket?
+        ``auto`` follows minio-js 7: AWS endpoints (``*.amazonaws.com``) with a DNS-compatible
+        bucket name, except names with dots over https (they break the wildcard certificate);
+        everything else (MinIO, the fakes) path-style."""
+        if not bucket or self.addressing == "path":
+            return False
+        if self.addressing == "virtual":
+            return True
+        host = self.endpoint.rsplit(":", 1)[0].lower()
+        if not (host == "amazonaws.com" or host.endswith(".amazonaws.com")):
+            return False
+        if not _DNS_BUCKET.match(bucket) or ".." in bucket:
+            return False
+        return "." not in bucket or self.scheme == "http"
+
+    def _address(self, bucket: str, key: str) -> Tuple[str, str]:
+        """(Host header, canonical URI path) of an object or bucket request."""
+        if self.virtual_host(bucket):
+            return f"{bucket}.{self.endpoint}", "/" + key
+        return self.endpoint, "/" + bucket + ("/" + key if key else "")
 
     async def close(self) -> None:
         if self._own_transports:
@@ -152,13 +181,13 @@ class S3Client:
                        headers: Optional[Dict[str, str]] = None, sink: Optional[FileSink] = None,
                        progress: Optional[Progress] = None, ok: Sequence[int] = (),
                        expect_body: bool = True) -> Response:
-        path = "/" + bucket + ("/" + key if key else "")
+        host, path = self._address(bucket, key)
         qs = sigv4.canonical_query(query)
-        url = self.base + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
+        url = f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
         phash = await self._payload_hash(body)
         attempt = 0
         while True:
-            hdrs = {"host": self.endpoint}
+            hdrs = {"host": host}
             if headers:
                 hdrs.update({k.lower(): v for k, v in headers.items()})
             sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
@@ -333,10 +362,10 @@ class S3Client:
 
     def _signed(self, method: str, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                 headers: Optional[Dict[str, str]] = None) -> Tuple[str, List[Tuple[str, str]]]:
-        path = "/" + bucket + ("/" + key if key else "")
+        host, path = self._address(bucket, key)
         qs = sigv4.canonical_query(query)
-        url = self.base + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
-        hdrs = {"host": self.endpoint}
+        url = f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
+        hdrs = {"host": host}
         if headers:
             hdrs.update({k.lower(): v for k, v in headers.items()})
         sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,

@@ -98,7 +98,7 @@ def _err(status: int, code: str, msg: str = "", resource: str = "") -> web.Respo
 class FakeS3:
     def __init__(self, access_key: str = "minioadmin", secret_key: str = "minioadmin",
                  verify_signatures: bool = True, host: str = "127.0.0.1", port: int = 0,
-                 ssl_context=None):
+                 ssl_context=None, virtual_host_suffix: str = ""):
         self.creds = {access_key: secret_key}
         self.verify_signatures = verify_signatures
         self.buckets: Dict[str, Dict[str, StoredObject]] = {}
@@ -112,6 +112,8 @@ class FakeS3:
         self._loop: Optional[asyncio.AbstractEventLoop] = None
         self.hooks: List[Callable[[str, str], None]] = []
         self.ssl_context = ssl_context          # serve https (tests of secure / bucket://)
+        # virtual-hosted-style requests: Host "<bucket>.<suffix>[:port]", path "/<key>"
+        self.virtual_host_suffix = virtual_host_suffix
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -170,8 +172,11 @@ class FakeS3:
     # ---------------------------------------------------------------- dispatch
     async def _handle(self, req: web.Request) -> web.StreamResponse:
         raw_path, _, raw_query = req.raw_path.partition("?")
-        path = unquote(raw_path)
+        path = sig_path = unquote(raw_path)
         query = parse_qsl(raw_query, keep_blank_values=True)
+        vb = self._virtual_bucket(req.headers.get("Host", ""))
+        if vb:
+            path = "/" + vb + (path if path != "/" else "")
         self.requests.append((req.method, path))
         for h in self.hooks:
             h(req.method, path)
@@ -185,18 +190,26 @@ class FakeS3:
                 raise web.HTTPInternalServerError()
             if rule.status and not rule.drop_after:
                 return _err(rule.status, rule.code, "injected fault", path)
-        resp = await self._dispatch(req, path, query)
+        resp = await self._dispatch(req, path, query, sig_path)
         if rule is not None and rule.drop_after:
             if req.transport is not None:
                 req.transport.close()
             raise web.HTTPInternalServerError()
         return resp
 
-    async def _dispatch(self, req: web.Request, path: str, query) -> web.StreamResponse:
+    def _virtual_bucket(self, host: str) -> str:
+        sfx = self.virtual_host_suffix
+        name = host.rsplit(":", 1)[0] if host.count(":") == 1 else host
+        if sfx and name.endswith("." + sfx):
+            return name[:-len(sfx) - 1]
+        return ""
+
+    async def _dispatch(self, req: web.Request, path: str, query,
+                        sig_path: str = "") -> web.StreamResponse:
         body = await req.read() if req.can_read_body else b""
         if self.verify_signatures:
             hdrs = {k.lower(): v for k, v in req.headers.items()}
-            ok, reason = sigv4.verify(req.method, path, query, hdrs, self.creds)
+            ok, reason = sigv4.verify(req.method, sig_path or path, query, hdrs, self.creds)
             if not ok:
                 return _err(403, reason, "signature check failed", path)
             ph = hdrs.get("x-amz-content-sha256", "")

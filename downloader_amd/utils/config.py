@@ -62,6 +62,9 @@ class S3Config(BaseModel):
     resume_uploads: bool = True
     # Use the native zero-copy HTTP transport for plain-http endpoints.
     native_transport: bool = True
+    # auto: virtual-hosted-style (<bucket>.<endpoint>) for AWS endpoints like minio-js,
+    # path-style elsewhere (MinIO); or force "path" / "virtual"
+    addressing: Literal["auto", "path", "virtual"] = "auto"
     connect_timeout_s: float = 10.0
     request_timeout_s: float = 300.0
     retries: int = 3
