@@ -116,6 +116,10 @@ class S3Client:
         self.access_key = access_key
         self.secret_key = secret_key
         self.region = region
+        # bucket -> region learnt from the server (x-amz-bucket-region / <Region>): an AWS
+        # bucket outside the configured region is signed for its own region after the first
+        # refusal, as minio-js does with its bucket-location cache
+        self._regions: Dict[str, str] = {}
         self._own_transports = transports is None
         self.t = transports or make_transports(native=native, connect_timeout=connect_timeout,
                                                io_timeout=request_timeout,
@@ -152,6 +156,21 @@ class S3Client:
             return False
         return "." not in bucket or self.scheme == "http"
 
+    def region_of(self, bucket: str) -> str:
+        return self._regions.get(bucket, self.region)
+
+    def _region_hint(self, resp: Response, bucket: str) -> Optional[str]:
+        """The bucket's real region when the server refused the signing region, else None."""
+        if not bucket or resp.status not in (301, 400, 403):
+            return None
+        r = resp.header("x-amz-bucket-region") or ""
+        if not r and resp.body:
+            try:
+                r = _text(ET.fromstring(resp.body), "Region")
+            except ET.ParseError:
+                r = ""
+        return r if r and r != self.region_of(bucket) else None
+
     def _address(self, bucket: str, key: str) -> Tuple[str, str]:
         """(Host header, canonical URI path) of an object or bucket request."""
         if self.virtual_host(bucket):
@@ -186,12 +205,13 @@ class S3Client:
         url = f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
         phash = await self._payload_hash(body)
         attempt = 0
+        relocated = False
         while True:
             hdrs = {"host": host}
             if headers:
                 hdrs.update({k.lower(): v for k, v in headers.items()})
             sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
-                       self.region, phash)
+                       self.region_of(bucket), phash)
             try:
                 if sink is not None and attempt > 0:
                     sink.max_bytes = sink.max_bytes  # body rewritten from the same offset
@@ -204,6 +224,11 @@ class S3Client:
             else:
                 if 200 <= resp.status < 300 or resp.status in ok:
                     return resp
+                hint = None if relocated else self._region_hint(resp, bucket)
+                if hint:                # re-sign for the bucket's region, at once
+                    self._regions[bucket] = hint
+                    relocated = True
+                    continue
                 err = parse_error(resp, bucket, key)
                 retry = err.retryable
             if not retry or attempt >= self.retries:
@@ -369,7 +394,7 @@ class S3Client:
         if headers:
             hdrs.update({k.lower(): v for k, v in headers.items()})
         sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
-                   self.region, sigv4.UNSIGNED)
+                   self.region_of(bucket), sigv4.UNSIGNED)
         return url, list(hdrs.items())
 
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
@@ -380,6 +405,7 @@ class S3Client:
         (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``."""
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
         attempt = 0
+        relocated = False
         while True:
             url, hdrs = self._signed("PUT", bucket, key, query,
                                      {"content-type": content_type} if content_type else None)
@@ -398,6 +424,11 @@ class S3Client:
                 if put.ok:
                     etag = (put.header("etag") or "").strip('"')
                     return etag if split is None else (etag, hashed)
+                hint = None if relocated else self._region_hint(put, bucket)
+                if hint:
+                    self._regions[bucket] = hint
+                    relocated = True
+                    continue
                 err = parse_error(put, bucket, key)
                 retry = err.retryable
             if not retry or attempt >= self.retries:

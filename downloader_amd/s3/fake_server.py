@@ -114,6 +114,9 @@ class FakeS3:
         self.ssl_context = ssl_context          # serve https (tests of secure / bucket://)
         # virtual-hosted-style requests: Host "<bucket>.<suffix>[:port]", path "/<key>"
         self.virtual_host_suffix = virtual_host_suffix
+        # bucket -> region: requests signed for another region are refused the way AWS does
+        # (400 AuthorizationHeaderMalformed + x-amz-bucket-region)
+        self.bucket_regions: Dict[str, str] = {}
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -215,6 +218,19 @@ class FakeS3:
             ph = hdrs.get("x-amz-content-sha256", "")
             if ph != sigv4.UNSIGNED and ph != hashlib.sha256(body).hexdigest():
                 return _err(400, "XAmzContentSHA256Mismatch", "", path)
+        want = self.bucket_regions.get(path.lstrip("/").split("/", 1)[0])
+        if want:
+            try:
+                got = sigv4.parse_authorization(req.headers.get("Authorization", ""))[
+                    "Credential"].split("/")[2]
+            except (ValueError, KeyError, IndexError):
+                got = ""
+            if got != want:
+                r = _err(400, "AuthorizationHeaderMalformed",
+                         f"the region '{got}' is wrong; expecting '{want}'", path)
+                r.body = r.body.replace(b"</Error>", f"<Region>{want}</Region></Error>".encode())
+                r.headers["x-amz-bucket-region"] = want
+                return r
         parts = path.lstrip("/").split("/", 1)
         bucket = parts[0]
         key = parts[1] if len(parts) > 1 else ""

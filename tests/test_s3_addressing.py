@@ -76,3 +76,37 @@ def test_virtual_hosted_round_trip(run, tmp_path):
         await fb.close()
         await s3.stop()
     run(go())
+
+
+def test_bucket_region_learnt_from_refusal(run, tmp_path, origin_cls):
+    """A bucket in another region: the first request is refused (400 AuthorizationHeader-
+    Malformed + x-amz-bucket-region), the client re-signs for that region at once and keeps
+    using it - for plain requests, multipart uploads, HEADs and the socket relay."""
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        s3.buckets["eu"] = {}
+        s3.bucket_regions["eu"] = "eu-west-1"
+        origin = await origin_cls().start()
+        blob = os.urandom((11 << 20) + 3)
+        origin.blobs["/m.mkv"] = blob
+        c = S3Client(ep, *CREDS, part_size=5 << 20, multipart_threshold=6 << 20, retries=0)
+        assert await c.bucket_exists("eu")                      # HEAD: header-only hint
+        assert c.region_of("eu") == "eu-west-1" and c.region_of("other") == "us-east-1"
+        c2 = S3Client(ep, *CREDS, part_size=5 << 20, multipart_threshold=6 << 20, retries=0)
+        await c2.put_object("eu", "small", b"x")                # body hint (<Region>)
+        p = tmp_path / "f.bin"
+        p.write_bytes(blob)
+        await c2.fput_object("eu", "big", str(p))
+        assert s3.get("eu", "big") == blob
+        c3 = S3Client(ep, *CREDS, part_size=5 << 20, multipart_threshold=6 << 20, retries=0)
+        assert c3.can_relay(origin.url("/m.mkv"))
+        await c3.relay_object("eu", "relayed", origin.url("/m.mkv"), len(blob))
+        assert s3.get("eu", "relayed") == blob and c3.region_of("eu") == "eu-west-1"
+        s3.bucket_regions["eu"] = "ap-south-1"                  # moved again: learnt again
+        assert await c3.get_object("eu", "small") == b"x"
+        for x in (c, c2, c3):
+            await x.close()
+        await origin.stop()
+        await s3.stop()
+    run(go())
