@@ -124,8 +124,9 @@ def _config(args) -> int:
     from .utils.config import load_config
     d = load_config(path=args.config or None).model_dump(mode="json")
     if not args.show_secrets:
-        if d.get("s3", {}).get("secret_key"):
-            d["s3"]["secret_key"] = "***"
+        for k in ("secret_key", "session_token"):
+            if d.get("s3", {}).get(k):
+                d["s3"][k] = "***"
         url = d.get("broker", {}).get("url") or ""
         u = urlsplit(url)
         if u.password:

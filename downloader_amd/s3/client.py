@@ -103,7 +103,7 @@ class S3Client:
                  max_inflight_parts: int = 8, unsigned_payload: bool = True, retries: int = 3,
                  native: bool = True, connect_timeout: float = 10.0,
                  request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = "",
-                 native_tls: bool = True, addressing: str = "auto"):
+                 native_tls: bool = True, addressing: str = "auto", session_token: str = ""):
         if "://" in endpoint:
             secure = endpoint.startswith("https://")
             endpoint = endpoint.split("://", 1)[1]
@@ -115,6 +115,7 @@ class S3Client:
         self.addressing = addressing
         self.access_key = access_key
         self.secret_key = secret_key
+        self.session_token = session_token
         self.region = region
         # bucket -> region learnt from the server (x-amz-bucket-region / <Region>): an AWS
         # bucket outside the configured region is signed for its own region after the first
@@ -138,7 +139,7 @@ class S3Client:
                    s3cfg.secure, transports, s3cfg.part_size, s3cfg.multipart_threshold,
                    s3cfg.max_inflight_parts, s3cfg.unsigned_payload, s3cfg.retries,
                    s3cfg.native_transport, s3cfg.connect_timeout_s, s3cfg.request_timeout_s,
-                   addressing=s3cfg.addressing)
+                   addressing=s3cfg.addressing, session_token=s3cfg.session_token)
 
     def virtual_host(self, bucket: str) -> bool:
         """Virtual-hosted-style addressing (``<bucket>.<endpoint>/<key>``) for this bucket?
@@ -208,6 +209,8 @@ class S3Client:
         relocated = False
         while True:
             hdrs = {"host": host}
+            if self.session_token:
+                hdrs["x-amz-security-token"] = self.session_token
             if headers:
                 hdrs.update({k.lower(): v for k, v in headers.items()})
             sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
@@ -391,6 +394,8 @@ class S3Client:
         qs = sigv4.canonical_query(query)
         url = f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
         hdrs = {"host": host}
+        if self.session_token:
+            hdrs["x-amz-security-token"] = self.session_token
         if headers:
             hdrs.update({k.lower(): v for k, v in headers.items()})
         sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,

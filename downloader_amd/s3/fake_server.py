@@ -117,6 +117,8 @@ class FakeS3:
         # bucket -> region: requests signed for another region are refused the way AWS does
         # (400 AuthorizationHeaderMalformed + x-amz-bucket-region)
         self.bucket_regions: Dict[str, str] = {}
+        # access key -> session token it must present (signed) as x-amz-security-token
+        self.session_tokens: Dict[str, str] = {}
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -215,6 +217,13 @@ class FakeS3:
             ok, reason = sigv4.verify(req.method, sig_path or path, query, hdrs, self.creds)
             if not ok:
                 return _err(403, reason, "signature check failed", path)
+            if self.session_tokens:
+                auth = sigv4.parse_authorization(hdrs["authorization"])
+                tok = self.session_tokens.get(auth["Credential"].split("/")[0])
+                if tok is not None and (hdrs.get("x-amz-security-token") != tok or
+                                        "x-amz-security-token" not in
+                                        auth["SignedHeaders"].split(";")):
+                    return _err(403, "InvalidToken", "missing or bad session token", path)
             ph = hdrs.get("x-amz-content-sha256", "")
             if ph != sigv4.UNSIGNED and ph != hashlib.sha256(body).hexdigest():
                 return _err(400, "XAmzContentSHA256Mismatch", "", path)

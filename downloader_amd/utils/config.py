@@ -39,6 +39,7 @@ class S3Config(BaseModel):
     endpoint: str = "127.0.0.1:9000"
     access_key: str = "minioadmin"
     secret_key: str = "minioadmin"
+    session_token: str = ""                     # temporary (STS) credentials: x-amz-security-token
     region: str = "us-east-1"
     secure: bool = False
     bucket: str = "triton-staging"

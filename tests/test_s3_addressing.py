@@ -110,3 +110,25 @@ def test_bucket_region_learnt_from_refusal(run, tmp_path, origin_cls):
         await origin.stop()
         await s3.stop()
     run(go())
+
+
+def test_session_token_signed(run, make_cfg):
+    """Temporary credentials: s3.session_token travels as a signed x-amz-security-token."""
+    from downloader_amd.s3.client import S3Error
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        s3.session_tokens["minioadmin"] = "tok/123=="
+        c = S3Client.from_config(make_cfg(ep, s3={"session_token": "tok/123=="}).s3)
+        await c.ensure_bucket("b")
+        await c.put_object("b", "k", b"v")
+        assert await c.get_object("b", "k") == b"v"
+        await c.close()
+        bad = S3Client(ep, *CREDS, retries=0)
+        with pytest.raises(S3Error) as ei:
+            await bad.get_object("b", "k")
+        assert ei.value.code == "InvalidToken"
+        await bad.close()
+        await s3.stop()
+    run(go())
