@@ -412,7 +412,12 @@ async def config_swarm(a) -> Dict:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, action="append", required=True,
-                    help="1, 3, 4, 5 (BASELINE.json) or 6 (peer-wire swarm, extra)")
+                    help="1, 3, 4, 5 (BASELINE.json), 6 (peer-wire swarm, extra) or 7 (chaos "
+                         "soak: worker kills + broker connection drops under load, extra)")
+    ap.add_argument("--chaos-interval", type=float, default=2.0,
+                    help="config 7: seconds between chaos actions (kill / connection drop)")
+    ap.add_argument("--chaos-timeout", type=float, default=900.0,
+                    help="config 7: give up waiting for every job's convert after this long")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
     ap.add_argument("--seed-inproc", action="store_true",
@@ -461,6 +466,9 @@ def main(argv=None) -> int:
             out = asyncio.run(config5(a))
         elif c == 6:
             out = asyncio.run(config_swarm(a))
+        elif c == 7:
+            from .chaos import config_chaos
+            out = asyncio.run(config_chaos(a))
         else:
             raise SystemExit(f"config {c}: use bench.py for config 2")
         print(json.dumps(out), flush=True)

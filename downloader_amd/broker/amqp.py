@@ -404,8 +404,10 @@ class _AmqpDelivery(Delivery):
 
 class AmqpBroker(Broker):
     def __init__(self, url: str, heartbeat: int = 30, reconnect_delay: float = 1.0,
-                 max_reconnect_delay: float = 30.0, metrics=None, connect_retry_s: float = 0.0):
+                 max_reconnect_delay: float = 30.0, metrics=None, connect_retry_s: float = 0.0,
+                 publish_retry_s: float = 120.0):
         self.url = url
+        self.publish_retry_s = publish_retry_s
         self.connect_retry_s = connect_retry_s
         self.heartbeat = heartbeat
         self.reconnect_delay = reconnect_delay
@@ -497,10 +499,28 @@ class AmqpBroker(Broker):
 
     async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
                       confirm: bool = True) -> None:
-        await self._ready()
+        """Publish (with a broker confirm unless ``confirm=False``). A connection lost before
+        the confirm arrives is not an error: the message is sent again once the watchdog has
+        reconnected, as amqp-connection-manager's ChannelWrapper does - at-least-once, so a
+        consumer may see it twice. Channel-level refusals on a live connection still raise,
+        and so does a broker that stays away for ``publish_retry_s``."""
         props = C.Properties(content_type="application/octet-stream", delivery_mode=2,
                              headers=_to_headers(headers))
-        await self._pub_ch.basic_publish("", queue, body, props, wait_confirm=confirm)
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + self.publish_retry_s
+        while True:
+            await self._ready()
+            conn = self.conn
+            try:
+                await self._pub_ch.basic_publish("", queue, body, props, wait_confirm=confirm)
+                break
+            except Exception:   # reset, EOF mid-frame, timeout, channel failure...
+                lost = conn is None or conn.closed.is_set() or conn is not self.conn
+                if not lost or self._closing or loop.time() > deadline:
+                    raise
+                if self.metrics is not None:
+                    self.metrics.messages.labels(queue, "republish").inc()
+                await asyncio.sleep(0.02)   # the watchdog is reconnecting; _ready() waits
         if self.metrics is not None:
             self.metrics.messages.labels(queue, "publish").inc()
 

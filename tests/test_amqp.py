@@ -177,6 +177,42 @@ def test_reconnect_resubscribes(run):
     run(go())
 
 
+def test_publish_survives_connection_drops(run):
+    """Publishing while the broker drops every connection: each publish completes once the
+    watchdog has reconnected (amqp-connection-manager re-sends unconfirmed messages), so
+    nothing is lost; redelivery may duplicate."""
+    async def go():
+        srv = await BrokerServer().start()
+        pub = AmqpBroker(srv.url, reconnect_delay=0.05)
+        sub = AmqpBroker(srv.url, reconnect_delay=0.05)
+        await pub.connect()
+        await sub.connect()
+        got = []
+
+        async def h(d):
+            got.append(d.body)
+            await d.ack()
+        await sub.consume("p", h, 16)
+
+        async def chaos():
+            for _ in range(5):
+                await asyncio.sleep(0.05)
+                srv.drop_connections()
+        task = asyncio.ensure_future(chaos())
+        for i in range(300):
+            await pub.publish("p", str(i).encode())
+        await task
+        want = {str(i).encode() for i in range(300)}
+        for _ in range(300):
+            if want <= set(got):
+                break
+            await asyncio.sleep(0.02)
+        assert want <= set(got), len(want - set(got))
+        assert pub.reconnects >= 1
+        await pub.close(); await sub.close(); await srv.stop()
+    run(go())
+
+
 def test_auth_refused(run):
     async def go():
         srv = await BrokerServer().start()

@@ -164,3 +164,21 @@ def test_supervisor_restarts_crashed_workers_without_blocking():
     assert s0.done and s0.restarts == 2 and s0.exit_codes == [3, 3, 3]
     assert s1.proc is not None and s1.proc.poll() is None and not s1.exit_codes
     assert sup.stop(timeout=10) != []
+
+
+def test_chaos_soak_loses_no_job(tmp_path):
+    """Config 7 in miniature: supervised workers over the bundled AMQP broker while workers are
+    SIGKILLed and every AMQP connection is dropped; every job still reaches v1.convert and
+    nothing is left in the staging directory."""
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="critical")
+    r = subprocess.run([sys.executable, "-m", "downloader_amd.bench.configs", "--config", "7",
+                        "--scale", "0.1", "--workers", "2", "--concurrency", "2", "--qps", "20",
+                        "--chaos-interval", "0.7", "--chaos-timeout", "120", "--cpus", "-1",
+                        "--src-dir", str(tmp_path), "--stage-dir", str(tmp_path)],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["config"] == 7 and out["jobs"] == 60 and not out["timed_out"]
+    assert out["lost_jobs"] == 0, out
+    assert out["kills"] >= 1 and out["connection_drops"] >= 1
+    assert out["stage_leftover_bytes"] == 0
