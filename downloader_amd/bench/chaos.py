@@ -4,11 +4,13 @@ recovery / fault injection, under load).
 The config-5 mix - 10 MB HTTP jobs (5 % with an injected 503) and 50 MB webseed torrents - is
 fed through the bundled AMQP broker to a supervised pool of worker processes while a chaos task
 alternately SIGKILLs a random worker (the supervisor respawns it; the broker requeues its
-unacked deliveries) and drops every AMQP connection (workers reconnect and re-consume). The
-run passes when every published job reaches ``v1.convert`` at least once. Reported: lost jobs
-(must be 0), duplicate converts (at-least-once redeliveries of jobs that were killed between
-their convert publish and their ack), worker restarts, per-process RSS / open-fd high-water
-marks, and what is left in the staging directory after the drain.
+unacked deliveries) and drops every AMQP connection (workers reconnect and re-consume); with
+``--s3-fail-rate`` the S3 peer also answers that share of object/part PUTs with 503 SlowDown
+(the S3 client's retries). The run passes when every published job reaches ``v1.convert``
+at least once. Reported: lost jobs (must be 0), duplicate converts (at-least-once
+redeliveries of jobs that were killed between their convert publish and their ack), worker
+restarts, per-process RSS / open-fd high-water marks, and what is left in the staging
+directory after the drain.
 
 The reference has no equivalent: a crash there drops the in-flight job's local data and relies
 on RabbitMQ redelivery with no resume; stalls ack and lose the job.
@@ -23,7 +25,7 @@ import signal
 import statistics
 import tempfile
 import time
-from typing import Dict, List
+from typing import Dict
 
 from ..models import api
 from .infra import Blobd
@@ -68,7 +70,7 @@ async def config_chaos(a) -> Dict:
     stage = tempfile.mkdtemp(prefix="cfg7-stage-", dir=a.stage_dir or None)
     srv = await BrokerServer(heartbeat=0).start()
     rng = random.Random(7)
-    with Blobd(sink="discard", files_root=src) as b:
+    with Blobd(sink="discard", files_root=src, s3_fail_rate=a.s3_fail_rate) as b:
         torrents = []
         for t in range(4):
             p = os.path.join(src, f"t{t}.mkv")
@@ -167,6 +169,7 @@ async def config_chaos(a) -> Dict:
         # drain: let redelivered duplicates settle, then stop the pool
         await asyncio.sleep(1.0)
         codes = await asyncio.get_running_loop().run_in_executor(None, sup.stop)
+        s3_faults = b.stats().get("s3_faults", 0)
         restarts = sum(s.restarts for s in sup.slots)
         await client.close()
         await srv.stop()
@@ -178,6 +181,7 @@ async def config_chaos(a) -> Dict:
     return {"config": 7, "jobs": n_jobs, "workers": a.workers, "qps_offered": a.qps,
             "chaos_interval_s": a.chaos_interval, "kills": actions["kill"],
             "connection_drops": actions["drop"], "worker_restarts": restarts,
+            "s3_fail_rate": a.s3_fail_rate, "s3_faults_injected": s3_faults,
             "wall_s": round(wall, 2), "timed_out": timed_out,
             "lost_jobs": len(lost), "lost_examples": lost[:5],
             "duplicate_converts": sum(c - 1 for c in converts.values() if c > 1),
@@ -185,7 +189,3 @@ async def config_chaos(a) -> Dict:
             "p99_latency_s": round(sorted(lat)[int(0.99 * (len(lat) - 1))], 4) if lat else None,
             "worker_rss_high_MB": round(hw["rss_MB"], 1), "worker_fds_high": hw["fds"],
             "stage_leftover_bytes": leftover, "worker_exit_codes": codes}
-
-
-def summarise(results: List[Dict]) -> str:
-    return ", ".join(f"{r['lost_jobs']} lost / {r['jobs']}" for r in results)

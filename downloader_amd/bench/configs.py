@@ -416,6 +416,8 @@ def main(argv=None) -> int:
                          "soak: worker kills + broker connection drops under load, extra)")
     ap.add_argument("--chaos-interval", type=float, default=2.0,
                     help="config 7: seconds between chaos actions (kill / connection drop)")
+    ap.add_argument("--s3-fail-rate", type=float, default=0.02,
+                    help="config 7: share of S3 object/part PUTs the peer answers 503 SlowDown")
     ap.add_argument("--chaos-timeout", type=float, default=900.0,
                     help="config 7: give up waiting for every job's convert after this long")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")

@@ -28,9 +28,10 @@ def self_signed_cert(directory: str, name: str = "127.0.0.1") -> Tuple[str, str]
 class Blobd:
     def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
                  host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum",
-                 tls: Optional[Tuple[str, str]] = None):
+                 tls: Optional[Tuple[str, str]] = None, s3_fail_rate: float = 0.0):
         self.files_root = files_root
         self.tls = tls                  # (cert PEM, key PEM): serve https
+        self.s3_fail_rate = s3_fail_rate  # share of object/part PUTs answered 503 SlowDown
         self.sink = sink
         self.keep_bytes = keep_bytes
         self.default_size = default_size
@@ -47,7 +48,8 @@ class Blobd:
              "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)]
             + (["--files-root", self.files_root] if self.files_root else [])
             + ["--sink", self.sink]
-            + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else []),
+            + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else [])
+            + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else []),
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         t0 = time.time()
         while not os.path.exists(pf):

@@ -73,6 +73,8 @@ int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
 SSL_CTX* g_tls = nullptr;  // --tls-cert / --tls-key
+double g_s3_fail_rate = 0;  // --s3-fail-rate: this share of object/part PUTs answer 503 SlowDown
+std::atomic<uint64_t> g_s3_faults{0};
 
 constexpr size_t kPool = 64ull << 20;
 
@@ -549,6 +551,15 @@ class Conn {
       return s3_error(405, "Method Not Allowed", "MethodNotAllowed", bucket);
     }
     // ---- object level
+    if (m == "PUT" && g_s3_fail_rate > 0) {
+      thread_local std::mt19937_64 rng(std::random_device{}());
+      if (std::uniform_real_distribution<double>(0, 1)(rng) < g_s3_fail_rate) {
+        Summer s;
+        if (!read_body(r.content_length, s, nullptr, 0)) return false;
+        g_s3_faults++;
+        return s3_error(503, "Slow Down", "SlowDown", key);
+      }
+    }
     if (m == "PUT") {
       Object o;
       Summer s;
@@ -651,8 +662,8 @@ class Conn {
     }
     snprintf(b, sizeof b,
              "{\"bytes_received\":%" PRIu64 ",\"bytes_served\":%" PRIu64 ",\"requests\":%" PRIu64
-             ",\"objects\":%" PRIu64 ",\"open_uploads\":%zu}",
-             g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup);
+             ",\"objects\":%" PRIu64 ",\"open_uploads\":%zu,\"s3_faults\":%" PRIu64 "}",
+             g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup, g_s3_faults.load());
     return respond(200, "OK", b, "", "application/json");
   }
 
@@ -689,10 +700,11 @@ int main(int argc, char** argv) {
     else if (a == "--sink") g_discard = std::string(next()) == "discard";
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
+    else if (a == "--s3-fail-rate") g_s3_fail_rate = atof(next());
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
                       "[--default-size N] [--files-root DIR] [--sink checksum|discard] "
-                      "[--tls-cert PEM --tls-key PEM]\n");
+                      "[--tls-cert PEM --tls-key PEM] [--s3-fail-rate P]\n");
       return 2;
     }
   }
