@@ -88,7 +88,8 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                       min_split: int = 32 << 20, progress: Optional[Progress] = None,
                       min_rate: float = 0.0, stall_window: float = 30.0,
                       logger: Optional[Logger] = None,
-                      proxy: Optional[ProxyConfig] = None) -> int:
+                      proxy: Optional[ProxyConfig] = None,
+                      space_reserve: Optional[int] = None) -> int:
     """Download ``url`` to ``path`` through ``path + '.part'`` (renamed when complete).
 
     Resume (the reference restarts from byte 0): the journal
@@ -97,7 +98,10 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     those ranges, or continues a single-stream transfer from the ``.part`` length - but only
     when the origin still reports the same validator and size (otherwise the partial data
     belongs to another version of the file and is discarded). A complete ``path`` of the
-    advertised size is reused as is."""
+    advertised size is reused as is.
+
+    ``space_reserve`` (not None): fail with ENOSPC before fetching when the filesystem cannot
+    hold what is still to be written plus that reserve (``stages/space.py``)."""
     log = logger or NullLogger()
     progress = progress or Progress()
     size, ranges, url, validator = await probe_validated(t, url, proxy)   # later GETs: final URL
@@ -114,6 +118,10 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     if journal and not resumable:
         log.info("resume: origin changed or unvalidated, restarting", path=path)
     done = list(journal["ranges"]) if resumable else []
+    if space_reserve is not None and size > 0:
+        from ..stages.space import allocated, ensure_space
+        held = allocated(part_path) if resumable else 0
+        ensure_space(os.path.dirname(path) or ".", size - held, space_reserve)
     _save_journal(state_path, validator, size, done)
     fd = os.open(part_path, os.O_WRONLY | os.O_CREAT | getattr(os, "O_CLOEXEC", 0), 0o644)
     written = 0

@@ -107,7 +107,8 @@ class DownloadStage(Stage):
         prog = Progress()
         n = await http_src.download_to(self.sv.transports, url, out, d.http_streams,
                                        d.http_min_split, prog, d.http_min_rate,
-                                       min(60.0, d.http_timeout_s), job.logger, self.proxy)
+                                       min(60.0, d.http_timeout_s), job.logger, self.proxy,
+                                       space_reserve=d.min_free_bytes)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("http", n)
 

@@ -187,6 +187,9 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
         selected = virtual_selection(meta, job, path, cfg) if seeds else None
         if selected:
             return await _stream_torrent(meta, seeds, selected, job, path, cfg, sv, t0)
+    from ..stages.space import ensure_space, still_to_write
+    if meta is not None:        # .torrent URL: check before any payload is fetched
+        ensure_space(path, still_to_write(meta.local_files(path)), d.min_free_bytes)
     client = client or await get_client(cfg, sv)
     session = await open_session(client, uri, path, sv, meta)
     # Seconds since the backend was entered: open (metainfo fetched, storage ready), metadata,
@@ -209,6 +212,8 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
             job.logger.warn("download failed to progress, killing")
             raise MetadataStalled()
         tl["metadata"] = time.perf_counter() - t0
+        if meta is None:        # magnet: metadata came from peers; little payload so far
+            ensure_space(path, still_to_write(session.meta.local_files(path)), d.min_free_bytes)
         job.logger.debug("hash", session.info_hash.hex())
         job.logger.debug("files", len(session.meta.files))
         eager = await _start_eager(session, job, path, cfg, sv) if d.eager_upload else None

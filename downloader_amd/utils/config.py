@@ -136,6 +136,9 @@ class DownloadConfig(BaseModel):
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on
     webseed_verify_depth_gpu: int = 32          # same when runs are verified by the GPU batcher
+    # Disk paths (HTTP to disk, torrents to disk) check before writing that the staging
+    # filesystem holds what is still to be written plus this reserve (stages/space.py)
+    min_free_bytes: int = 0
     cleanup_on_stall: bool = True               # App. A #6 (reference leaves data behind)
     emit_errored_on_stall: bool = False         # App. A #6 (reference: ack silently)
 

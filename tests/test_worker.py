@@ -767,3 +767,45 @@ def test_complete_download_reused_only_for_the_same_origin_version(run, make_cfg
         assert len([r for r in origin.requests if r[0] == "GET"]) == 2
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_not_enough_space_fails_before_fetching(run, make_cfg, origin_cls, tmp_path, monkeypatch):
+    """Disk paths check free space first (stages/space.py): an HTTP file and a torrent that
+    cannot fit fail with ENOSPC before their payload is fetched; stream staging is unaffected."""
+    import collections
+    import shutil as _shutil
+
+    from downloader_amd.torrent.metainfo import make_torrent
+    real = _shutil.disk_usage
+    Usage = collections.namedtuple("Usage", "total used free")
+    monkeypatch.setattr(_shutil, "disk_usage",
+                        lambda p: Usage(real(p).total, real(p).used, 1_000_000))
+
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, broker={"max_retries": 0},
+                                        download={"stream_http": False,
+                                                  "torrent_stream": "off"})
+        origin.blobs["/big.mkv"] = os.urandom(3_000_000)
+        src = tmp_path / "t.mkv"
+        src.write_bytes(os.urandom(2_000_000))
+        origin.blobs["/ws/t.mkv"] = src.read_bytes()
+        origin.blobs["/t.torrent"] = make_torrent(str(src), 65536,
+                                                  url_list=[origin.url("/ws/t.mkv")])
+        await w.submit(api.make_download("ns1", "http", origin.url("/big.mkv")))
+        await w.submit(api.make_download("ns2", "http", origin.url("/t.torrent")))
+        await _wait(w, 2)
+        for r in w.results:
+            assert r.outcome == "dead" and "not enough space" in r.error, r
+        gets = [(m, p) for m, p, *_ in origin.requests if m == "GET"]
+        assert ("GET", "/big.mkv") not in gets
+        assert not any(p.startswith("/ws/") for _, p in gets)
+        await w.stop()
+        # plenty of room again: the same HTTP job stages normally
+        monkeypatch.setattr(_shutil, "disk_usage", real)
+        w2 = Worker(make_cfg(s3.endpoint, download={"stream_http": False}), broker=MemoryBroker())
+        await w2.start(health=False)
+        await w2.submit(api.make_download("ns3", "http", origin.url("/big.mkv")))
+        await _wait(w2)
+        assert w2.results[0].outcome == "staged", w2.results[0]
+        await w2.stop(); await s3.stop(); await origin.stop()
+    run(go())
