@@ -122,6 +122,10 @@ def _config(args) -> int:
     from urllib.parse import urlsplit, urlunsplit
 
     from .utils.config import load_config
+    if args.reference:
+        from .utils.config_doc import reference_markdown
+        print(reference_markdown())
+        return 0
     d = load_config(path=args.config or None).model_dump(mode="json")
     if not args.show_secrets:
         for k in ("secret_key", "session_token"):
@@ -174,6 +178,8 @@ def main(argv=None) -> int:
     c = sub.add_parser("config")
     c.add_argument("--config", default="")
     c.add_argument("--show-secrets", action="store_true", help="do not mask credentials")
+    c.add_argument("--reference", action="store_true",
+                   help="print the markdown reference of every key (docs/CONFIG.md)")
     args = p.parse_args(argv)
     return {"worker": _worker, "supervisor": _supervisor, "broker": _broker, "submit": _submit,
             "make-torrent": _make_torrent, "verify": _verify, "config": _config}[args.cmd](args)

@@ -27,6 +27,8 @@ MiB = 1024 * 1024
 
 
 class InstanceConfig(BaseModel):
+    # job dirs live in <download_path>/<media.id>; relative = under the project root
+    # (lib/download.js:234-240)
     download_path: str = "downloads"
     # App. A #18: concurrent duplicate deliveries must not share a directory.
     per_attempt_dirs: bool = True
@@ -36,12 +38,14 @@ class InstanceConfig(BaseModel):
 
 
 class S3Config(BaseModel):
-    endpoint: str = "127.0.0.1:9000"
+    endpoint: str = "127.0.0.1:9000"            # host:port, or a URL whose scheme sets `secure`
     access_key: str = "minioadmin"
-    secret_key: str = "minioadmin"
+    secret_key: str = "minioadmin"              # masked in `config` output unless --show-secrets
     session_token: str = ""                     # temporary (STS) credentials: x-amz-security-token
+    # SigV4 signing region; a bucket elsewhere is learnt from the server's refusal
     region: str = "us-east-1"
-    secure: bool = False
+    secure: bool = False                        # https to S3 (minio-js useSSL)
+    # staging bucket, created if missing (lib/upload.js:29-30)
     bucket: str = "triton-staging"
     # minio-js 7 default; per-request Python cost (SigV4, executor hop) makes fewer, larger
     # parts faster even for the socket relay: 100 MB jobs 37 GB/s @16 MiB -> 47.5 GB/s @64 MiB
@@ -50,7 +54,8 @@ class S3Config(BaseModel):
     # requests per job - 100 MB jobs 43 -> 60 GB/s on the build box. rclone's upload cutoff is
     # 200 MiB; minio-js switches at 64 MiB (kept in mode: reference).
     multipart_threshold: int = 128 * MiB
-    max_inflight_parts: int = 8
+    max_inflight_parts: int = 8                 # multipart parts in flight per object (ref: 1)
+    # objects uploaded at once per job (ref: 1, lib/upload.js:34-52)
     concurrent_files: int = 4
     # Sign with UNSIGNED-PAYLOAD (body never re-read for SHA-256); when False the
     # native hasher computes the payload SHA-256 (minio-js over plain HTTP does that).
@@ -67,27 +72,31 @@ class S3Config(BaseModel):
     # path-style elsewhere (MinIO); or force "path" / "virtual"
     addressing: Literal["auto", "path", "virtual"] = "auto"
     connect_timeout_s: float = 10.0
-    request_timeout_s: float = 300.0
+    request_timeout_s: float = 300.0            # socket idle timeout of one request
+    # retries of a retryable S3 error (5xx, SlowDown, resets) with jittered backoff
     retries: int = 3
 
 
 class BrokerConfig(BaseModel):
+    # amqp (RabbitMQ or the bundled broker) or memory (tests, benches)
     backend: Literal["amqp", "memory"] = "amqp"
     url: str = ""  # empty -> dynamics('rabbitmq')
     prefetch: int = 1          # lib/main.js:46 (AMQP arg 1)
     max_retries: int = 2       # lib/main.js:46 (AMQP arg 2, INFERRED as retry budget)
     download_queue: str = "v1.download"   # lib/main.js:172
     convert_queue: str = "v1.convert"     # lib/main.js:164
-    dead_letter_queue: str = "v1.download.dead"
+    dead_letter_queue: str = "v1.download.dead" # jobs that used up max_retries are published here
+    # first re-publish delay of a failed job (doubles per attempt)
     retry_backoff_s: float = 0.5
     retry_backoff_max_s: float = 30.0
-    heartbeat_s: int = 30
+    heartbeat_s: int = 30                       # AMQP heartbeat (0: off)
+    # first reconnect delay after a lost connection (doubles, max 30 s)
     reconnect_delay_s: float = 1.0
     connect_retry_s: float = 60.0               # keep retrying the first connect this long
 
 
 class TelemetryConfig(BaseModel):
-    enabled: bool = True
+    enabled: bool = True                        # status / progress messages (triton-core telemetry)
     status_queue: str = "v1.telemetry.status"
     progress_queue: str = "v1.telemetry.progress"
 
@@ -98,6 +107,7 @@ class DownloadConfig(BaseModel):
     progress_interval_s: float = 30.0           # lib/download.js:88
     allow_file_urls: bool = False               # env ALLOW_FILE_URLS (lib/download.js:178)
     http_streams: int = 4                       # parallel Range GETs per file (ref: 1)
+    # smallest Range slice when a file is split over http_streams
     http_min_split: int = 32 * MiB
     http_timeout_s: float = 300.0
     http_min_rate: float = 0.0                  # bytes/s stall floor, 0 = off
@@ -120,18 +130,19 @@ class DownloadConfig(BaseModel):
     relay_pool_idle_trim_s: float = 5.0
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
+    # torrent piece SHA-1: cpu, gpu (gfx950 kernel) or auto
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
     # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of
     # torrents >= 8 GiB to the GPU instead of paying the cold start inside a job.
     gpu_prewarm: bool = True
-    torrent_listen_port: int = 0
+    torrent_listen_port: int = 0                # incoming peer connections (0: any free port)
     torrent_max_peers: int = 32
-    torrent_enable_dht: bool = True
-    torrent_enable_trackers: bool = True
-    torrent_enable_webseeds: bool = True
-    torrent_request_pipeline: int = 16
+    torrent_enable_dht: bool = True             # BEP-5 mainline DHT
+    torrent_enable_trackers: bool = True        # HTTP / UDP trackers
+    torrent_enable_webseeds: bool = True        # BEP-19 url-list
+    torrent_request_pipeline: int = 16          # 16 KiB block requests in flight per peer
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on
@@ -144,6 +155,7 @@ class DownloadConfig(BaseModel):
 
 
 class ProcessConfig(BaseModel):
+    # kept extensions (lib/process.js:15-20)
     media_exts: List[str] = Field(default_factory=lambda: [".mp4", ".mkv", ".mov", ".webm"])
     case_insensitive_exts: bool = False         # App. A #15 (reference: case-sensitive)
     legacy_full_path_extras: bool = False       # App. A #14
@@ -151,6 +163,7 @@ class ProcessConfig(BaseModel):
 
 
 class HealthConfig(BaseModel):
+    # GET /health (+ /healthz, /readyz, /metrics) on port
     enabled: bool = True
     host: str = "0.0.0.0"
     port: int = 3401                            # lib/main.js:194 (env PORT)
@@ -158,12 +171,13 @@ class HealthConfig(BaseModel):
 
 
 class MetricsConfig(BaseModel):
-    enabled: bool = True
+    enabled: bool = True                        # Prometheus metrics (triton-core prom)
     # /metrics is served on the health port; a dedicated port may be set as well.
     port: int = 0
 
 
 class TraceConfig(BaseModel):
+    # per-job / per-stage spans, traceparent in message headers
     enabled: bool = False
     path: str = ""                              # JSONL span sink ("" -> stderr when enabled)
 
@@ -178,7 +192,9 @@ class TlsConfig(BaseModel):
 
 
 class Config(BaseModel):
+    # config name (the reference loads `converter`, App. A #1; both names are searched)
     name: str = "downloader"
+    # tuned, or reference = the reference's serial structure (BASELINE.md comparison mode)
     mode: Literal["tuned", "reference"] = "tuned"
     concurrency: int = 4                        # jobs in flight per worker process
     instance: InstanceConfig = Field(default_factory=InstanceConfig)
@@ -191,6 +207,7 @@ class Config(BaseModel):
     metrics: MetricsConfig = Field(default_factory=MetricsConfig)
     trace: TraceConfig = Field(default_factory=TraceConfig)
     tls: TlsConfig = Field(default_factory=TlsConfig)
+    # stage modules in order (`module:factory` plugins allowed, lib/main.js:28-32)
     stages: List[str] = Field(default_factory=lambda: ["download", "process", "upload"])
 
     def apply_mode(self) -> "Config":

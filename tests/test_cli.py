@@ -144,3 +144,18 @@ def test_gpu_slots_from_env(monkeypatch):
     assert cpus.gpu_slots() == 1
     monkeypatch.setenv("STAGER_GPU_SLOTS", "4")
     assert cpus.gpu_slots() == 4
+
+
+def test_config_reference_doc_is_current():
+    """docs/CONFIG.md is the generated reference of every key (config --reference)."""
+    from downloader_amd.utils.config import Config
+    from downloader_amd.utils.config_doc import reference_markdown
+    md = reference_markdown()
+    with open(os.path.join(REPO, "docs", "CONFIG.md")) as f:
+        assert f.read().strip() == md.strip(), \
+            "regenerate: python -m downloader_amd config --reference > docs/CONFIG.md"
+    for sec, f in Config.model_fields.items():
+        sub = getattr(f.annotation, "model_fields", None)
+        for k in (sub or {sec: None}):
+            key = f"{sec}.{k}" if sub else sec
+            assert f"| `{key}` |" in md, key
