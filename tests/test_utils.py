@@ -6,6 +6,8 @@ import io
 import json
 import os
 
+import pytest
+
 from downloader_amd.utils.config import load_config
 from downloader_amd.utils.dynamics import dyn
 from downloader_amd.utils.log import Logger, ListSink, Sink
@@ -219,3 +221,40 @@ def test_redact_url_for_logs():
     assert "X-Amz-Algorithm=AWS4-HMAC-SHA256" in r and "partNumber=2" in r
     assert redact_url("http://o/x.mkv?size=1") == "http://o/x.mkv?size=1"
     assert redact_url("magnet:?xt=urn:btih:abc") == "magnet:?xt=urn:btih:abc"
+
+
+def test_native_transport_ipv6_literal(run):
+    """http://[::1]:port/ - bracketed IPv6 literals reach the native transport (getaddrinfo
+    AF_UNSPEC) with a bracketed Host header."""
+    import socket
+
+    from aiohttp import web
+
+    from downloader_amd.net.http import NativeTransport
+    if not socket.has_ipv6:
+        pytest.skip("no IPv6")
+
+    async def go():
+        seen = {}
+
+        async def h(r):
+            seen["host"] = r.headers.get("Host")
+            return web.Response(body=b"v6" * 1000)
+        app = web.Application()
+        app.router.add_get("/x", h)
+        runner = web.AppRunner(app)
+        await runner.setup()
+        try:
+            site = web.TCPSite(runner, "::1", 0)
+            await site.start()
+        except OSError:
+            await runner.cleanup()
+            pytest.skip("no IPv6 loopback")
+        port = site._server.sockets[0].getsockname()[1]
+        t = NativeTransport(2)
+        r = await t.request("GET", f"http://[::1]:{port}/x")
+        assert r.status == 200 and r.body == b"v6" * 1000
+        assert seen["host"] == f"[::1]:{port}"
+        await t.close()
+        await runner.cleanup()
+    run(go())
