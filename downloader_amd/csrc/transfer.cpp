@@ -60,6 +60,19 @@ std::string trim(const std::string& s) {
   return s.substr(a, b - a + 1);
 }
 
+// Size line of a chunked body ("1a2b[;ext]\r\n"): hex digits only, no sign, no overflow.
+int64_t chunk_size(const std::string& line) {
+  int64_t n = 0;
+  size_t i = 0;
+  for (; i < line.size() && isxdigit((unsigned char)line[i]); ++i) {
+    if (n > ((int64_t)1 << 58)) throw IoError("chunk size too large");
+    const char c = (char)tolower((unsigned char)line[i]);
+    n = n * 16 + (c <= '9' ? c - '0' : c - 'a' + 10);
+  }
+  if (i == 0) throw IoError("malformed chunk size line");
+  return n;
+}
+
 }  // namespace
 
 HttpConn::HttpConn(const std::string& host, int port, double connect_timeout_s,
@@ -412,7 +425,7 @@ std::string HttpConn::read_body(const ResponseHead& h, int64_t max_bytes) {
   if (h.chunked) {
     for (;;) {
       std::string line = read_line();
-      int64_t n = strtoll(line.c_str(), nullptr, 16);
+      int64_t n = chunk_size(line);
       if (n == 0) {
         while (true) {
           std::string t = read_line();
@@ -532,7 +545,7 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
   if (h.chunked) {
     for (;;) {
       std::string line = read_line();
-      int64_t n = strtoll(line.c_str(), nullptr, 16);
+      int64_t n = chunk_size(line);
       if (n == 0) {
         while (true) {
           std::string t = read_line();

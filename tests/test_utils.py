@@ -258,3 +258,56 @@ def test_native_transport_ipv6_literal(run):
         await t.close()
         await runner.cleanup()
     run(go())
+
+
+def test_native_http_parser_survives_garbage(run, tmp_path):
+    """Malformed / truncated / hostile responses (bad status lines, negative or non-hex chunk
+    sizes, lying Content-Length, early close) end in an HttpError / TransportError - never a
+    crash of the native parser, never a hang - for bodies read into memory and into files."""
+    import random
+
+    from downloader_amd.net.http import FileSink, HttpError, NativeTransport
+    rng = random.Random(1234)
+    pieces = [b"HTTP/1.1 200 OK\r\n", b"HTTP/1.0 206 Partial\r\n", b"HTTP/1.1 abc\r\n",
+              b"garbage\r\n", b"Content-Length: 10\r\n", b"Content-Length: -4\r\n",
+              b"Content-Length: 99999999999999999999\r\n", b"Transfer-Encoding: chunked\r\n",
+              b"Connection: close\r\n", b"X: " + b"y" * 70000 + b"\r\n", b"\r\n",
+              b"5\r\nhello\r\n", b"-5\r\nhello\r\n", b"zz\r\n", b"0\r\n\r\n",
+              b"fffffffffffffffffffffff\r\n", b"abcdefghij", b"\x00\xff" * 20]
+    cases = [b"".join(rng.choice(pieces) for _ in range(rng.randint(1, 6))) for _ in range(150)]
+    cases += [b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n-5\r\nhello\r\n0\r\n\r\n",
+              b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n",
+              b"HTTP/1.1 200 OK\r\nContent-Length: 100\r\n\r\nshort"]
+
+    async def go():
+        i = {"n": 0}
+
+        async def serve(r, w):
+            payload = cases[i["n"] % len(cases)]
+            try:
+                await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+                w.write(payload)
+                await w.drain()
+            except Exception:
+                pass
+            w.close()
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        t = NativeTransport(4, connect_timeout=2, io_timeout=2)
+        outcomes = {"ok": 0, "err": 0}
+        fd = os.open(str(tmp_path / "sink"), os.O_WRONLY | os.O_CREAT, 0o600)
+        for k in range(len(cases)):
+            i["n"] = k
+            for sink in (None, FileSink(fd, 0, 1 << 20)):
+                try:
+                    await asyncio.wait_for(
+                        t.request("GET", f"http://127.0.0.1:{port}/f", sink=sink), 10)
+                    outcomes["ok"] += 1
+                except (HttpError, ValueError):
+                    outcomes["err"] += 1
+        os.close(fd)
+        assert outcomes["err"] > 50 and sum(outcomes.values()) == 2 * len(cases)
+        await t.close()
+        srv.close()
+        await srv.wait_closed()
+    run(go(), timeout=300)
