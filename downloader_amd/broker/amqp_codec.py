@@ -329,13 +329,22 @@ def method_frame(channel: int, method: Tuple[int, int], *args: Any) -> bytes:
     return struct.pack(">BHI", FRAME_METHOD, channel, len(payload)) + payload + bytes([FRAME_END])
 
 
+_MALFORMED = (struct.error, IndexError, KeyError, ValueError, UnicodeDecodeError,
+              OverflowError, TypeError)
+
+
 def decode_method(payload: bytes) -> Tuple[Tuple[int, int], List[Any]]:
-    cid, mid = struct.unpack(">HH", payload[:4])
-    m = (cid, mid)
-    sig = SIGNATURES.get(m)
-    if sig is None:
-        raise FrameError(f"unsupported method {m}")
-    return m, decode_args(sig, Reader(payload, 4))
+    """Method frame payload -> ((class, method), args). Any malformed payload is a
+    FrameError (the connection's read loop treats it as a broken connection)."""
+    try:
+        cid, mid = struct.unpack(">HH", payload[:4])
+        m = (cid, mid)
+        sig = SIGNATURES.get(m)
+        if sig is None:
+            raise FrameError(f"unsupported method {m}")
+        return m, decode_args(sig, Reader(payload, 4))
+    except _MALFORMED as e:
+        raise FrameError(f"malformed method frame: {type(e).__name__}: {e}") from e
 
 
 # ---------------------------------------------------------------- content
@@ -387,11 +396,14 @@ def header_frame(channel: int, body_size: int, props: Properties, class_id: int 
 
 
 def decode_header(payload: bytes) -> Tuple[int, Properties]:
-    r = Reader(payload)
-    r.short()  # class id
-    r.short()  # weight
-    size = r.longlong()
-    return size, Properties.decode(r)
+    try:
+        r = Reader(payload)
+        r.short()  # class id
+        r.short()  # weight
+        size = r.longlong()
+        return size, Properties.decode(r)
+    except _MALFORMED as e:
+        raise FrameError(f"malformed content header: {type(e).__name__}: {e}") from e
 
 
 def body_frames(channel: int, body: bytes, frame_max: int) -> List[bytes]:
