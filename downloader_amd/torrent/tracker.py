@@ -71,22 +71,33 @@ async def announce_http(url: str, info_hash: bytes, peer_id: bytes, port: int, u
                 status, body = resp.status, await resp.read()
     if status != 200:
         raise TrackerError(f"tracker HTTP {status}")
+    return parse_announce_response(body)
+
+
+def parse_announce_response(body: bytes) -> AnnounceResult:
+    """BEP-3 / BEP-23 / BEP-7 announce response -> AnnounceResult. The body is untrusted:
+    anything malformed (not a dict, wrong value types) is a TrackerError."""
     try:
         d = bdecode(body)
     except ValueError as e:
         raise TrackerError(f"bad tracker response: {e}") from e
-    if b"failure reason" in d:
-        raise TrackerError(d[b"failure reason"].decode("utf-8", "replace"))
-    res = AnnounceResult(int(d.get(b"interval", 1800)), [], int(d.get(b"complete", 0)),
-                         int(d.get(b"incomplete", 0)))
+    if not isinstance(d, dict):
+        raise TrackerError("bad tracker response: not a dictionary")
+    try:
+        if b"failure reason" in d:
+            raise TrackerError(bytes(d[b"failure reason"]).decode("utf-8", "replace"))
+        res = AnnounceResult(int(d.get(b"interval", 1800)), [], int(d.get(b"complete", 0)),
+                             int(d.get(b"incomplete", 0)))
+    except (TypeError, ValueError) as e:
+        raise TrackerError(f"bad tracker response: {e}") from e
     peers = d.get(b"peers", b"")
     if isinstance(peers, bytes):
         res.peers = decode_compact(peers)
-    else:
+    elif isinstance(peers, list):
         for p in peers:
             try:
-                res.peers.append((p[b"ip"].decode(), int(p[b"port"])))
-            except (KeyError, ValueError):
+                res.peers.append((bytes(p[b"ip"]).decode(), int(p[b"port"])))
+            except (KeyError, ValueError, TypeError):
                 continue
     if isinstance(d.get(b"peers6"), bytes):
         res.peers += decode_compact6(d[b"peers6"])

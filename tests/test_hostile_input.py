@@ -122,3 +122,23 @@ def test_broker_survives_garbage_frames(run):
         await b.close()
         await srv.stop()
     run(go())
+
+
+_TRK = st.recursive(
+    st.one_of(st.integers(-5, 10**6), st.binary(max_size=40)),
+    lambda ch: st.one_of(st.lists(ch, max_size=3),
+                         st.dictionaries(st.sampled_from([b"peers", b"ip", b"port", b"interval",
+                                                          b"failure reason", b"peers6",
+                                                          b"complete", b"x"]), ch, max_size=4)),
+    max_leaves=10)
+
+
+@SETTINGS
+@given(_TRK)
+def test_tracker_response_only_raises_tracker_error(v):
+    from downloader_amd.torrent.tracker import TrackerError, parse_announce_response
+    try:
+        r = parse_announce_response(bencode(v))
+    except TrackerError:
+        return
+    assert all(isinstance(h, str) and isinstance(p, int) for h, p in r.peers)
