@@ -159,3 +159,23 @@ def test_config_reference_doc_is_current():
         for k in (sub or {sec: None}):
             key = f"{sec}.{k}" if sub else sec
             assert f"| `{key}` |" in md, key
+
+
+def test_k8s_manifest_matches_the_cli_and_probes():
+    """deploy/k8s/downloader.yaml: valid YAML, its embedded config loads, the command parses,
+    and the probes point at endpoints the health server serves."""
+    import yaml
+
+    from downloader_amd.utils.config import load_config
+    with open(os.path.join(REPO, "deploy", "k8s", "downloader.yaml")) as f:
+        docs = list(yaml.safe_load_all(f))
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")
+    cfg = load_config(overrides=yaml.safe_load(cm["data"]["downloader.yaml"]), env={})
+    assert cfg.concurrency == 8 and cfg.instance.download_path == "/data/downloads"
+    dep = next(d for d in docs if d["kind"] == "Deployment")
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"][:4] == ["python3", "-m", "downloader_amd", "supervisor"]
+    assert c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
+    src = open(os.path.join(REPO, "downloader_amd", "service", "health.py")).read()
+    assert '"/readyz"' in src and '"/healthz"' in src and '"/metrics"' in src
