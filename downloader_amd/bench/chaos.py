@@ -23,6 +23,7 @@ import random
 import shutil
 import signal
 import statistics
+import sys
 import tempfile
 import time
 from typing import Dict
@@ -97,6 +98,9 @@ async def config_chaos(a) -> Dict:
         converts: Dict[str, int] = {}
         done = asyncio.Event()
         hw: Dict[str, float] = {"rss_MB": 0.0, "fds": 0}
+        # pid -> [(t, rss_MB, fds)] every ~5 s: growth of long-lived workers shows leaks
+        series: Dict[int, list] = {}
+        last_sample = [0.0]
         actions = {"kill": 0, "drop": 0}
 
         async def on_convert(d):
@@ -112,11 +116,18 @@ async def config_chaos(a) -> Dict:
         async def supervise():
             while not done.is_set():
                 sup.poll()
+                now = time.perf_counter()
+                sample = now - last_sample[0] >= 5.0
+                if sample:
+                    last_sample[0] = now
                 for s in sup.slots:
                     if s.proc is not None and s.proc.poll() is None:
                         st = _proc_stats(s.proc.pid)
                         hw["rss_MB"] = max(hw["rss_MB"], st["rss_MB"])
                         hw["fds"] = max(hw["fds"], st["fds"])
+                        if sample and st["rss_MB"]:
+                            series.setdefault(s.proc.pid, []).append(
+                                (now, st["rss_MB"], st["fds"]))
                 await asyncio.sleep(0.1)
 
         async def chaos():
@@ -125,7 +136,7 @@ async def config_chaos(a) -> Dict:
                 await asyncio.sleep(a.chaos_interval)
                 if done.is_set():
                     break
-                if k % 2 == 0:
+                if k % 2 == 0 and a.chaos_kill:
                     live = [s for s in sup.slots if s.proc is not None and s.proc.poll() is None]
                     if live:
                         victim = rng.choice(live)
@@ -134,12 +145,21 @@ async def config_chaos(a) -> Dict:
                             actions["kill"] += 1
                         except ProcessLookupError:
                             pass
-                else:
+                elif k % 2 == 1:
                     srv.drop_connections()
                     actions["drop"] += 1
                 k += 1
 
-        tasks = [asyncio.ensure_future(supervise()), asyncio.ensure_future(chaos())]
+        async def report():
+            t_start = time.perf_counter()
+            while not done.is_set():
+                await asyncio.sleep(30)
+                print(f"[chaos] {time.perf_counter() - t_start:.0f}s published {len(published)} "
+                      f"converted {len(first)} kills {actions['kill']} drops {actions['drop']}",
+                      file=sys.stderr, flush=True)
+
+        tasks = [asyncio.ensure_future(supervise()), asyncio.ensure_future(chaos()),
+                 asyncio.ensure_future(report())]
         t0 = time.perf_counter()
         for i in range(n_jobs):
             target = t0 + i / a.qps
@@ -178,6 +198,16 @@ async def config_chaos(a) -> Dict:
         shutil.rmtree(stage, ignore_errors=True)
     lat = list(first.values())
     lost = sorted(set(published) - set(first))
+    # leak check: workers that lived >= 60 s, RSS / fds at their first sample >= 20 s after the
+    # start of the series (warm) vs their last sample
+    growth = []
+    for pid, pts in series.items():
+        if len(pts) < 2 or pts[-1][0] - pts[0][0] < 60:
+            continue
+        warm = next((p for p in pts if p[0] - pts[0][0] >= 20), pts[0])
+        growth.append({"pid": pid, "lived_s": round(pts[-1][0] - pts[0][0], 1),
+                       "rss_warm_MB": round(warm[1], 1), "rss_end_MB": round(pts[-1][1], 1),
+                       "fds_warm": warm[2], "fds_end": pts[-1][2]})
     return {"config": 7, "jobs": n_jobs, "workers": a.workers, "qps_offered": a.qps,
             "chaos_interval_s": a.chaos_interval, "kills": actions["kill"],
             "connection_drops": actions["drop"], "worker_restarts": restarts,
@@ -188,4 +218,5 @@ async def config_chaos(a) -> Dict:
             "p50_latency_s": round(statistics.median(lat), 4) if lat else None,
             "p99_latency_s": round(sorted(lat)[int(0.99 * (len(lat) - 1))], 4) if lat else None,
             "worker_rss_high_MB": round(hw["rss_MB"], 1), "worker_fds_high": hw["fds"],
-            "stage_leftover_bytes": leftover, "worker_exit_codes": codes}
+            "stage_leftover_bytes": leftover, "worker_exit_codes": codes,
+            "long_lived_workers": growth}

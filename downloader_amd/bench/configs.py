@@ -416,6 +416,9 @@ def main(argv=None) -> int:
                          "soak: worker kills + broker connection drops under load, extra)")
     ap.add_argument("--chaos-interval", type=float, default=2.0,
                     help="config 7: seconds between chaos actions (kill / connection drop)")
+    ap.add_argument("--no-chaos-kill", dest="chaos_kill", action="store_false",
+                    help="config 7: no worker kills (connection drops and S3 faults only), so "
+                         "long-lived workers show RSS / fd growth")
     ap.add_argument("--s3-fail-rate", type=float, default=0.02,
                     help="config 7: share of S3 object/part PUTs the peer answers 503 SlowDown")
     ap.add_argument("--chaos-timeout", type=float, default=900.0,
