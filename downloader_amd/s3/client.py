@@ -103,7 +103,8 @@ class S3Client:
                  max_inflight_parts: int = 8, unsigned_payload: bool = True, retries: int = 3,
                  native: bool = True, connect_timeout: float = 10.0,
                  request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = "",
-                 native_tls: bool = True, addressing: str = "auto", session_token: str = ""):
+                 native_tls: bool = True, addressing: str = "auto", session_token: str = "",
+                 split_tls_relays: bool = True):
         if "://" in endpoint:
             secure = endpoint.startswith("https://")
             endpoint = endpoint.split("://", 1)[1]
@@ -116,6 +117,7 @@ class S3Client:
         self.access_key = access_key
         self.secret_key = secret_key
         self.session_token = session_token
+        self.split_tls_relays = split_tls_relays
         self.region = region
         # bucket -> region learnt from the server (x-amz-bucket-region / <Region>): an AWS
         # bucket outside the configured region is signed for its own region after the first
@@ -139,7 +141,8 @@ class S3Client:
                    s3cfg.secure, transports, s3cfg.part_size, s3cfg.multipart_threshold,
                    s3cfg.max_inflight_parts, s3cfg.unsigned_payload, s3cfg.retries,
                    s3cfg.native_transport, s3cfg.connect_timeout_s, s3cfg.request_timeout_s,
-                   addressing=s3cfg.addressing, session_token=s3cfg.session_token)
+                   addressing=s3cfg.addressing, session_token=s3cfg.session_token,
+                   split_tls_relays=s3cfg.split_tls_relays)
 
     def virtual_host(self, bucket: str) -> bool:
         """Virtual-hosted-style addressing (``<bucket>.<endpoint>/<key>``) for this bucket?
@@ -308,8 +311,8 @@ class S3Client:
         finally:
             os.close(fd)
 
-    def plan_parts(self, size: int, align_offset: int = 0,
-                   align: int = 0) -> List[Tuple[int, int, int]]:
+    def plan_parts(self, size: int, align_offset: int = 0, align: int = 0,
+                   part_size: int = 0) -> List[Tuple[int, int, int]]:
         """(part number, offset, length) of a multipart upload of ``size`` bytes.
 
         ``align``/``align_offset``: the object is bytes [align_offset, align_offset + size) of
@@ -317,8 +320,8 @@ class S3Client:
         a multiple of ``align``, the first part is shortened so every interior part boundary
         falls on a unit boundary: a torrent piece then never straddles two parts, so only
         pieces at the file's two ends need assembling from fragments. S3 allows unequal
-        parts (all but the last >= 5 MiB)."""
-        ps = self.part_size
+        parts (all but the last >= 5 MiB). ``part_size``: instead of ``self.part_size``."""
+        ps = max(MIN_PART, part_size) if part_size else self.part_size
         while (size + ps - 1) // ps > MAX_PARTS:
             ps *= 2
         first = ps
@@ -444,14 +447,24 @@ class S3Client:
     async def relay_object(self, bucket: str, key: str, src_url: str, size: int,
                            progress: Optional[Progress] = None,
                            concurrency: Optional[int] = None, src_proxy=None,
-                           content_type: str = "") -> str:
-        """Stage ``src_url`` (``size`` bytes, Range-capable origin) straight into S3: each
-        multipart part is one Range GET relayed socket->socket into one UploadPart.
-        ``src_proxy``: the source-fetch proxy policy (``net/proxy.ProxyConfig``)."""
+                           content_type: str = "", ranges: bool = True) -> str:
+        """Stage ``src_url`` (``size`` bytes) straight into S3: each multipart part is one Range
+        GET relayed socket->socket into one UploadPart; objects up to ``multipart_threshold``
+        go in one relayed PUT. ``src_proxy``: the source-fetch proxy policy
+        (``net/proxy.ProxyConfig``); ``ranges``: the origin serves Range requests.
+
+        Over TLS one relay is bound by one thread decrypting and re-encrypting every byte
+        (~2 - 3 GB/s), so with ``split_tls_relays`` an object of more than 6 MiB that would go
+        in one PUT is cut into up to ``max_inflight_parts`` parts relayed in parallel."""
+        tls = src_url.startswith("https://") or self.scheme == "https"
         if size <= self.multipart_threshold:
-            return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
-                                         src_proxy=src_proxy, content_type=content_type)
-        parts = self.plan_parts(size)
+            if not (tls and self.split_tls_relays and ranges and size > MIN_PART + (1 << 20)):
+                return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
+                                             src_proxy=src_proxy, content_type=content_type)
+            ps = -(-size // max(1, self.max_inflight_parts))
+            parts = self.plan_parts(size, part_size=-(-ps // (1 << 20)) << 20)
+        else:
+            parts = self.plan_parts(size)
         upload_id = await self.create_multipart_upload(bucket, key, content_type)
         sem = asyncio.Semaphore(concurrency or self.max_inflight_parts)
         etags: Dict[int, str] = {}

@@ -131,7 +131,8 @@ class DownloadStage(Stage):
         key = keys.object_key(job.id, name)
         job.logger.info("streaming http source straight to staging", key=key, size=size)
         await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress(),
-                              src_proxy=self.proxy, content_type=media_type(self.cfg, name))
+                              src_proxy=self.proxy, content_type=media_type(self.cfg, name),
+                              ranges=ranges)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
         job.stats.setdefault("streamed", []).append(
             {"file": os.path.join(path, name), "key": key, "size": size, "virtual": True})

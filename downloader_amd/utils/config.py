@@ -71,6 +71,9 @@ class S3Config(BaseModel):
     # auto: virtual-hosted-style (<bucket>.<endpoint>) for AWS endpoints like minio-js,
     # path-style elsewhere (MinIO); or force "path" / "virtual"
     addressing: Literal["auto", "path", "virtual"] = "auto"
+    # Over TLS a relay is bound by one thread's AES-GCM: objects > 6 MiB under the multipart
+    # threshold are relayed as up to max_inflight_parts parallel parts instead of one PUT
+    split_tls_relays: bool = True
     connect_timeout_s: float = 10.0
     request_timeout_s: float = 300.0            # socket idle timeout of one request
     # retries of a retryable S3 error (5xx, SlowDown, resets) with jittered backoff

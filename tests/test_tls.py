@@ -275,3 +275,27 @@ def test_connect_refused_by_proxy(run):
         srv.close()
         await srv.wait_closed()
     run(go())
+
+
+def test_tls_relay_split_into_parallel_parts(run, cert, origin_cls):
+    """Over TLS an object under the multipart threshold but above 6 MiB is relayed as parallel
+    parts (one thread's AES-GCM bounds a single relay); plain http keeps one PUT."""
+    async def go():
+        s3 = FakeS3(ssl_context=_server_ctx(cert))
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(8_000_000)
+        origin.blobs["/o.mkv"] = blob
+        c = S3Client(ep, *CREDS, secure=True, ca_file=cert[0], max_inflight_parts=4)
+        await c.ensure_bucket("b")
+        await c.relay_object("b", "split", origin.url("/o.mkv"), len(blob))
+        assert s3.get("b", "split") == blob
+        assert s3.objects("b")["split"].etag.endswith("-2")        # 5 MiB + the rest
+        c.split_tls_relays = False
+        await c.relay_object("b", "one", origin.url("/o.mkv"), len(blob))
+        assert "-" not in s3.objects("b")["one"].etag
+        await c.relay_object("b", "small", origin.url("/o.mkv"), len(blob), ranges=False)
+        await c.close()
+        await origin.stop()
+        await s3.stop()
+    run(go())
