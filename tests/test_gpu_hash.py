@@ -48,6 +48,15 @@ def test_kernel_ab_timings(gv):
         gv.kernel_bench_prefetch(1000, 256, 1)
 
 
+def test_kernel_prefetch_keeps_its_speedup(gv):
+    """Perf guard for the block prefetch (profiles/r2_kpf: 1.37x per lane, A/B in one
+    process, so box-to-box variance cancels)."""
+    pf, nopf = gv.kernel_bench_prefetch(1 << 20, 4096, 2)
+    assert nopf / pf > 1.15, (pf, nopf)
+    b3, plain = gv.kernel_bench(1 << 20, 4096, 2)
+    assert plain / b3 > 1.05, (b3, plain)
+
+
 def test_multi_batch_pipeline(gv):
     # 64 MiB staging slots, 200 MiB of data -> 4 batches through both streams
     piece = 1 << 20
