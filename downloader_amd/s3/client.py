@@ -160,6 +160,15 @@ class S3Client:
             return False
         return "." not in bucket or self.scheme == "http"
 
+    def presign(self, method: str, bucket: str, key: str, expires: int = 3600) -> str:
+        """Presigned URL (query-string SigV4, minio-js ``presignedUrl``): any HTTP client -
+        the socket relay included - can then GET the object, Range requests too."""
+        host, path = self._address(bucket, key)
+        q = sigv4.presign(method, host, path, [], self.access_key, self.secret_key,
+                          self.region_of(bucket), expires, session_token=self.session_token)
+        return f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + "?" + \
+            sigv4.canonical_query(q)
+
     def region_of(self, bucket: str) -> str:
         return self._regions.get(bucket, self.region)
 

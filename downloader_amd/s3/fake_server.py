@@ -212,7 +212,16 @@ class FakeS3:
     async def _dispatch(self, req: web.Request, path: str, query,
                         sig_path: str = "") -> web.StreamResponse:
         body = await req.read() if req.can_read_body else b""
-        if self.verify_signatures:
+        presigned = any(k == "X-Amz-Signature" for k, _ in query)
+        presigned_cred = dict(query).get("X-Amz-Credential", "")
+        if self.verify_signatures and presigned:
+            hdrs = {k.lower(): v for k, v in req.headers.items()}
+            ok, reason = sigv4.verify_presigned(req.method, sig_path or path, query, hdrs,
+                                                self.creds)
+            if not ok:
+                return _err(403, reason, "presigned URL check failed", path)
+            query = [(k, v) for k, v in query if not k.startswith("X-Amz-")]
+        elif self.verify_signatures:
             hdrs = {k.lower(): v for k, v in req.headers.items()}
             ok, reason = sigv4.verify(req.method, sig_path or path, query, hdrs, self.creds)
             if not ok:
@@ -230,9 +239,10 @@ class FakeS3:
         want = self.bucket_regions.get(path.lstrip("/").split("/", 1)[0])
         if want:
             try:
-                got = sigv4.parse_authorization(req.headers.get("Authorization", ""))[
-                    "Credential"].split("/")[2]
-            except (ValueError, KeyError, IndexError):
+                cred = presigned_cred if presigned else \
+                    sigv4.parse_authorization(req.headers.get("Authorization", ""))["Credential"]
+                got = cred.split("/")[2]
+            except (ValueError, KeyError, IndexError, AttributeError):
                 got = ""
             if got != want:
                 r = _err(400, "AuthorizationHeaderMalformed",

@@ -77,6 +77,62 @@ def sign(method: str, path: str, query: Sequence[Tuple[str, str]], headers: Dict
     return headers
 
 
+def presign(method: str, host: str, path: str, query: Sequence[Tuple[str, str]],
+            access_key: str, secret_key: str, region: str, expires: int = 3600,
+            now: Optional[_dt.datetime] = None, session_token: str = "",
+            service: str = "s3") -> List[Tuple[str, str]]:
+    """Query-string authentication (a presigned URL): returns ``query`` plus the X-Amz-*
+    parameters, X-Amz-Signature last. Only ``host`` is signed and the payload is
+    UNSIGNED-PAYLOAD, so the URL works for Range GETs and through any HTTP client."""
+    amzdate, date = amz_dates(now)
+    scope = f"{date}/{region}/{service}/aws4_request"
+    q = list(query) + [("X-Amz-Algorithm", ALGO),
+                       ("X-Amz-Credential", f"{access_key}/{scope}"),
+                       ("X-Amz-Date", amzdate), ("X-Amz-Expires", str(int(expires))),
+                       ("X-Amz-SignedHeaders", "host")]
+    if session_token:
+        q.append(("X-Amz-Security-Token", session_token))
+    creq = canonical_request(method, path, q, {"host": host}, ["host"], UNSIGNED)
+    sts = "\n".join([ALGO, amzdate, scope, hashlib.sha256(creq.encode()).hexdigest()])
+    sig = hmac.new(signing_key(secret_key, date, region, service), sts.encode(),
+                   hashlib.sha256).hexdigest()
+    return q + [("X-Amz-Signature", sig)]
+
+
+def verify_presigned(method: str, path: str, query: Sequence[Tuple[str, str]],
+                     headers: Mapping[str, str], secrets: Mapping[str, str],
+                     now: Optional[_dt.datetime] = None,
+                     service: str = "s3") -> Tuple[bool, str]:
+    """Server-side check of a presigned request (FakeS3). ``headers`` lower-cased."""
+    q = dict(query)
+    try:
+        given = q["X-Amz-Signature"]
+        access, date, region = q["X-Amz-Credential"].split("/")[:3]
+        amzdate = q["X-Amz-Date"]
+        expires = int(q["X-Amz-Expires"])
+        signed = q["X-Amz-SignedHeaders"].split(";")
+        t0 = _dt.datetime.strptime(amzdate, "%Y%m%dT%H%M%SZ").replace(tzinfo=_dt.timezone.utc)
+    except (KeyError, ValueError):
+        return False, "AuthorizationQueryParametersError"
+    secret = secrets.get(access)
+    if secret is None:
+        return False, "InvalidAccessKeyId"
+    if (now or _dt.datetime.now(_dt.timezone.utc)) > t0 + _dt.timedelta(seconds=expires):
+        return False, "AccessDenied"                     # "Request has expired"
+    rest = [(k, v) for k, v in query if k != "X-Amz-Signature"]
+    try:
+        creq = canonical_request(method, path, rest, headers, signed, UNSIGNED)
+    except KeyError:
+        return False, "AuthorizationQueryParametersError"
+    scope = f"{date}/{region}/{service}/aws4_request"
+    sts = "\n".join([ALGO, amzdate, scope, hashlib.sha256(creq.encode()).hexdigest()])
+    want = hmac.new(signing_key(secret, date, region, service), sts.encode(),
+                    hashlib.sha256).hexdigest()
+    if not hmac.compare_digest(want, given):
+        return False, "SignatureDoesNotMatch"
+    return True, ""
+
+
 def parse_authorization(value: str) -> Dict[str, str]:
     if not value.startswith(ALGO + " "):
         raise ValueError("not a SigV4 authorization header")

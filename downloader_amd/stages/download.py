@@ -151,6 +151,9 @@ class DownloadStage(Stage):
 
     async def bucket(self, url: str, job: Job, path: str) -> None:
         d = self.cfg.download
+        if d.stream_bucket and self.cfg.mode == "tuned" and await self._stream_bucket(url, job,
+                                                                                     path):
+            return
         prog = Progress()
         files = await bucket_src.fetch_bucket(url, path, secure=d.bucket_secure,
                                               concurrency=d.bucket_concurrency,
@@ -162,6 +165,60 @@ class DownloadStage(Stage):
         n = sum(os.path.getsize(f) for f in files)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("bucket", n)
+
+    async def _stream_bucket(self, url: str, job: Job, path: str) -> bool:
+        """bucket:// fast path: the object listing is the file tree the reference would have
+        downloaded (``<dir>/<name minus subFolder>``, lib/download.js:218-226), so the media
+        selector runs on it before any byte moves (``find_virtual``); each selected object is
+        then relayed source S3 -> staging S3 through a presigned GET (Range parts in
+        parallel) with no disk hop, and unselected objects (extras, samples) are never
+        fetched. Falls back to the disk path when nothing is selected (the process stage then
+        fails as in the reference) or the relay cannot reach both endpoints."""
+        from ..s3.client import S3Client
+        d = self.cfg.download
+        src = bucket_src.parse_bucket_uri(url)
+        s3 = self.sv.s3
+        client = S3Client(src.endpoint, src.access_key, src.secret_key, secure=d.bucket_secure,
+                          transports=self.sv.transports)
+        if not s3.can_relay(client.base + "/"):
+            return False
+        prefix = src.sub_folder.rstrip("/") + "/"
+        items = [it for it in await client.list_objects(src.bucket, prefix, recursive=True)
+                 if it.name and not it.name.endswith("/")]
+        by_path: Dict[str, Any] = {}
+        for it in items:
+            dst = bucket_src.local_name(path, it.name, src.sub_folder)
+            if not bucket_src.inside(path, dst):
+                raise ValueError(f"object {it.name!r} escapes the download directory")
+            by_path[os.path.abspath(dst)] = it
+        rel = [os.path.relpath(p, path) for p in by_path]
+        selected = select_from_config(self.cfg).find_virtual(path, rel, job.media.type)
+        if not selected:
+            return False
+        await ensure_staging_bucket(self.sv)
+        owner: Dict[str, str] = {}              # key -> winning file (last in walk order)
+        for f in selected:
+            owner[keys.object_key(job.id, f)] = f
+        job.logger.info("streaming bucket source straight to staging", objects=len(items),
+                        selected=len(selected), staged=len(owner))
+        sem = asyncio.Semaphore(max(1, d.bucket_concurrency))
+        prog = Progress()
+
+        async def one(key: str, f: str) -> None:
+            it = by_path[f]
+            async with sem:
+                await s3.relay_object(self.cfg.s3.bucket, key,
+                                      client.presign("GET", src.bucket, it.name), it.size, prog,
+                                      content_type=media_type(self.cfg, f))
+        await asyncio.gather(*(one(k, f) for k, f in owner.items()))
+        staged = sum(by_path[f].size for f in owner.values())
+        job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + staged
+        job.stats.setdefault("streamed", []).extend(
+            {"file": f, "key": keys.object_key(job.id, f), "size": by_path[f].size,
+             "virtual": True} for f in selected)
+        job.stats["bucket_skipped_bytes"] = sum(it.size for it in items) - staged
+        self._count("bucket", staged)
+        return True
 
     async def torrent(self, uri: str, job: Job, path: str) -> None:
         from ..torrent.backend import download_torrent

@@ -133,6 +133,9 @@ class DownloadConfig(BaseModel):
     relay_pool_idle_trim_s: float = 5.0
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
+    # bucket:// sources: select media from the object listing and relay only the selected
+    # objects source S3 -> staging S3 through presigned GETs (no disk hop, extras never fetched)
+    stream_bucket: bool = True
     # torrent piece SHA-1: cpu, gpu (gfx950 kernel) or auto
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)

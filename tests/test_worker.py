@@ -207,9 +207,12 @@ def test_health_endpoint_semantics(run, make_cfg, origin_cls):
     run(go())
 
 
-def test_multi_file_bucket_source_with_collisions(run, make_cfg, origin_cls):
+@pytest.mark.parametrize("stream", [True, False])
+def test_multi_file_bucket_source_with_collisions(run, make_cfg, origin_cls, stream):
+    """Same outcome on the streamed (presigned relay) and the disk path."""
     async def go():
-        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"bucket_secure": False})
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={
+            "bucket_secure": False, "stream_bucket": stream})
         s3.buckets["src"] = {}
         s3.put("src", "show/S1/KonoSuba S1E1.mkv", b"one")
         s3.put("src", "show/Season 1/KonoSuba S1E1.mkv", b"two")
@@ -222,6 +225,39 @@ def test_multi_file_bucket_source_with_collisions(run, make_cfg, origin_cls):
         assert s3.get("triton-staging", k) == b"two"   # last in walk order wins (App. A #10)
         assert w.metrics.sample("downloader_key_collisions_total") == 1
         assert w.telemetry.progress_of("job9") == [0, 50, 75, 100]
+        assert bool(w.results[0].stats.get("streamed")) == stream
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
+
+
+def test_bucket_source_streams_selected_objects_only(run, make_cfg, origin_cls, tmp_path):
+    """bucket:// fast path: the selector runs on the object listing; selected objects (one
+    above the multipart threshold: Range parts in parallel) are relayed source -> staging
+    through presigned GETs, extras are never fetched and nothing touches the disk."""
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"bucket_secure": False})
+        s3.buckets["src"] = {}
+        big = os.urandom((13 << 20) + 7)
+        s3.put("src", "lib/Show/Season 1/e1.mkv", big)
+        s3.put("src", "lib/Show/Season 1/e2.mkv", b"e2" * 5000)
+        s3.put("src", "lib/Show/Extras/making-of.mkv", os.urandom(3 << 20))
+        s3.put("src", "lib/Show/notes.txt", b"n")
+        uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,lib"
+        await w.submit(api.make_download("bs1", "bucket", uri, "TV"))
+        await _wait(w)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        assert [os.path.basename(x["file"]) for x in r.stats["streamed"]] == ["e1.mkv", "e2.mkv"]
+        assert r.stats["bucket_skipped_bytes"] == (3 << 20) + 1
+        assert s3.get("triton-staging", keys.object_key("bs1", "e1.mkv")) == big
+        assert s3.objects("triton-staging")[keys.object_key("bs1", "e1.mkv")].etag.endswith("-3")
+        assert s3.get("triton-staging", keys.object_key("bs1", "e2.mkv")) == b"e2" * 5000
+        assert s3.get("triton-staging", keys.object_key("bs1", "making-of.mkv")) is None
+        gets = [p for m, p in s3.requests if m == "GET" and p.startswith("/src/")]
+        assert gets and not any("Extras" in p or "notes" in p for p in gets)
+        assert s3.get("triton-staging", keys.done_key("bs1")) is not None
+        for dp, _, fns in os.walk(tmp_path / "dl"):
+            assert not [f for f in fns if f.endswith(".mkv")], (dp, fns)
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
 
