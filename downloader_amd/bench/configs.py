@@ -332,6 +332,43 @@ async def config5(a) -> Dict:
             "torrent_jobs": n_torrent, "worker_exit_codes": codes}
 
 
+# ---------------------------------------------------------------------------- config 8
+async def config_bucket(a) -> Dict:
+    """bucket:// source (extra; the reference fetches every object sequentially with
+    fGetObject, lib/download.js:218-226, then uploads the selected ones): a season of 10
+    episodes plus 2 extras in a synthetic source bucket served by blobd."""
+    ep = int(1e9 * a.scale)
+    objs = {f"lib/Show/Season 1/Show S01E{i + 1:02d}.mkv": ep + i for i in range(10)}
+    objs.update({f"lib/Show/Extras/extra{i}.mkv": ep for i in range(2)})
+    objs["lib/Show/readme.txt"] = 1000
+    stage = tempfile.mkdtemp(prefix="cfg8-stage-", dir=a.stage_dir or None)
+    out: Dict = {"config": 8, "mode": a.mode, "objects": len(objs),
+                 "selected_bytes": sum(n for k, n in objs.items() if "Season" in k),
+                 "listed_bytes": sum(objs.values())}
+    try:
+        with Blobd(sink="discard", synth_bucket="src", synth_objects=objs) as b:
+            dl = {"bucket_secure": False}
+            if a.mode == "tuned":
+                dl["stream_bucket"] = a.torrent_stream != "off"
+            w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl),
+                       broker=MemoryBroker())
+            await w.start(health=False)
+            uri = f"bucket://{b.endpoint},src,minioadmin,minioadmin,lib"
+            cpu0, peer0 = _self_cpu(), b.cpu_seconds()
+            dt, r = await _run_jobs(w, [api.make_download(f"c8-{a.mode}", "bucket", uri, "TV")])
+            cpu, peer = _self_cpu() - cpu0, b.cpu_seconds() - peer0
+            assert r[0].outcome == "staged", r[0]
+            await w.stop()
+            out.update({"streamed": bool(r[0].stats.get("streamed")), "job_s": round(dt, 3),
+                        "MBps_selected": round(out["selected_bytes"] / dt / MB, 1),
+                        "downloaded_bytes": r[0].stats.get("downloaded_bytes"),
+                        "uploaded_bytes": r[0].bytes, "worker_cpu_s": round(cpu, 2),
+                        "peer_cpu_s": round(peer, 2), "stage_s": r[0].stats.get("stage_s")})
+    finally:
+        shutil.rmtree(stage, ignore_errors=True)
+    return out
+
+
 def _seed_proc(conn, raw: bytes, src: str, n: int) -> None:
     """Seeding clients in their own process (remote peers are not on our event loop)."""
     from downloader_amd.torrent.client import TorrentClient
@@ -412,8 +449,9 @@ async def config_swarm(a) -> Dict:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, action="append", required=True,
-                    help="1, 3, 4, 5 (BASELINE.json), 6 (peer-wire swarm, extra) or 7 (chaos "
-                         "soak: worker kills + broker connection drops under load, extra)")
+                    help="1, 3, 4, 5 (BASELINE.json), 6 (peer-wire swarm, extra), 7 (chaos "
+                         "soak: worker kills + broker connection drops under load, extra) or "
+                         "8 (bucket:// season, extra; --torrent-stream off = disk path)")
     ap.add_argument("--chaos-interval", type=float, default=2.0,
                     help="config 7: seconds between chaos actions (kill / connection drop)")
     ap.add_argument("--no-chaos-kill", dest="chaos_kill", action="store_false",
@@ -474,6 +512,8 @@ def main(argv=None) -> int:
         elif c == 7:
             from .chaos import config_chaos
             out = asyncio.run(config_chaos(a))
+        elif c == 8:
+            out = asyncio.run(config_bucket(a))
         else:
             raise SystemExit(f"config {c}: use bench.py for config 2")
         print(json.dumps(out), flush=True)

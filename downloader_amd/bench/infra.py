@@ -28,10 +28,13 @@ def self_signed_cert(directory: str, name: str = "127.0.0.1") -> Tuple[str, str]
 class Blobd:
     def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
                  host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum",
-                 tls: Optional[Tuple[str, str]] = None, s3_fail_rate: float = 0.0):
+                 tls: Optional[Tuple[str, str]] = None, s3_fail_rate: float = 0.0,
+                 synth_bucket: str = "", synth_objects: Optional[Dict[str, int]] = None):
         self.files_root = files_root
         self.tls = tls                  # (cert PEM, key PEM): serve https
         self.s3_fail_rate = s3_fail_rate  # share of object/part PUTs answered 503 SlowDown
+        self.synth_bucket = synth_bucket  # read-only source bucket of synthetic objects
+        self.synth_objects = dict(synth_objects or {})
         self.sink = sink
         self.keep_bytes = keep_bytes
         self.default_size = default_size
@@ -49,7 +52,9 @@ class Blobd:
             + (["--files-root", self.files_root] if self.files_root else [])
             + ["--sink", self.sink]
             + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else [])
-            + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else []),
+            + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else [])
+            + (["--synth-bucket", self.synth_bucket, "--synth-manifest",
+                self._manifest(d)] if self.synth_bucket else []),
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         t0 = time.time()
         while not os.path.exists(pf):
@@ -65,6 +70,13 @@ class Blobd:
     @property
     def endpoint(self) -> str:
         return f"{self.host}:{self.port}"
+
+    def _manifest(self, d: str) -> str:
+        p = os.path.join(d, "synth-manifest")
+        with open(p, "w") as f:
+            for k, n in self.synth_objects.items():
+                f.write(f"{k} {n}\n")
+        return p
 
     @property
     def scheme(self) -> str:

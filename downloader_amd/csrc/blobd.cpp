@@ -10,6 +10,9 @@
 //            PUT|GET|HEAD|DELETE /<bucket>/<key>, multipart (POST ?uploads, PUT ?partNumber,
 //            POST ?uploadId, DELETE ?uploadId)
 //   stats:   GET /_stats  (JSON: bytes received/served, objects, requests)
+//   --synth-bucket NAME --synth-manifest FILE ("<key> <size>" lines): a read-only source
+//            bucket of synthetic objects (List v2, HEAD, GET with Range) for bucket:// jobs;
+//            query-string auth (presigned URLs) is accepted, signatures are not checked
 //
 // --tls-cert/--tls-key: serve https (OpenSSL, one session per connection thread) for the TLS
 // staging bench; bodies then pass through user space both ways (no sendfile / splice).
@@ -73,6 +76,8 @@ int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
 SSL_CTX* g_tls = nullptr;  // --tls-cert / --tls-key
+std::string g_synth_bucket;                       // --synth-bucket
+std::map<std::string, uint64_t> g_synth_objects;  // key -> size (--synth-manifest)
 double g_s3_fail_rate = 0;  // --s3-fail-rate: this share of object/part PUTs answer 503 SlowDown
 std::atomic<uint64_t> g_s3_faults{0};
 
@@ -517,11 +522,37 @@ class Conn {
     return ok;
   }
 
+  // Read-only synthetic source bucket: object bytes are the origin pool at an offset derived
+  // from the key, so any Range of any object is reproducible without storing it.
+  bool synth(const Request& r, const std::string& key) {
+    if (key.empty()) {
+      if (r.method == "HEAD") return respond(200, "OK", "", "", "application/xml", true);
+      std::string prefix = r.q.count("prefix") ? r.q.at("prefix") : "";
+      std::string body = "<?xml version=\"1.0\" encoding=\"UTF-8\"?><ListBucketResult><Name>" +
+                         g_synth_bucket + "</Name><IsTruncated>false</IsTruncated>";
+      for (auto& kv : g_synth_objects)
+        if (kv.first.compare(0, prefix.size(), prefix) == 0)
+          body += "<Contents><Key>" + xml_escape(kv.first) + "</Key><Size>" +
+                  std::to_string(kv.second) + "</Size></Contents>";
+      body += "</ListBucketResult>";
+      return respond(200, "OK", body);
+    }
+    auto it = g_synth_objects.find(key);
+    if (it == g_synth_objects.end()) return s3_error(404, "Not Found", "NoSuchKey", key);
+    Request o = r;
+    o.q["size"] = std::to_string(it->second);
+    o.q["seed"] = std::to_string(std::hash<std::string>{}(key) % 100000);
+    o.q.erase("fail");
+    return origin(o);
+  }
+
   bool s3(const Request& r) {
     std::string p = r.path.substr(1);
     size_t sl = p.find('/');
     std::string bucket = p.substr(0, sl), key = sl == std::string::npos ? "" : p.substr(sl + 1);
     const std::string& m = r.method;
+    if (!g_synth_bucket.empty() && bucket == g_synth_bucket && (m == "GET" || m == "HEAD"))
+      return synth(r, key);
     if (bucket.empty()) return s3_error(400, "Bad Request", "InvalidBucketName", r.path);
     if (key.empty()) {
       if (r.content_length > 0) {
@@ -701,6 +732,18 @@ int main(int argc, char** argv) {
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
     else if (a == "--s3-fail-rate") g_s3_fail_rate = atof(next());
+    else if (a == "--synth-bucket") g_synth_bucket = next();
+    else if (a == "--synth-manifest") {
+      FILE* f = fopen(next(), "r");
+      char line[4096];
+      while (f && fgets(line, sizeof line, f)) {
+        std::string l(line);
+        size_t sp = l.rfind(' ');
+        if (sp == std::string::npos) continue;
+        g_synth_objects[l.substr(0, sp)] = strtoull(l.c_str() + sp + 1, nullptr, 10);
+      }
+      if (f) fclose(f);
+    }
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
                       "[--default-size N] [--files-root DIR] [--sink checksum|discard] "
