@@ -144,6 +144,22 @@ class DownloadStage(Stage):
             raise file_src.FileUrlsNotAllowed()
         src = file_src.file_uri_to_path(url)
         out = file_src.target_path(url, path)
+        d = self.cfg.download
+        if d.stream_file and self.cfg.mode == "tuned" and os.path.isfile(src) and \
+                select_from_config(self.cfg).accepts_single_file(os.path.basename(out)):
+            # the copy's only reader would be the upload: stage straight from the source file
+            # (sendfile), the job directory stays empty (reference: copy, then upload)
+            await ensure_staging_bucket(self.sv)
+            key = keys.object_key(job.id, out)
+            size = os.path.getsize(src)
+            job.logger.info("staging local file without a copy", key=key, size=size)
+            await self.sv.s3.fput_object(self.cfg.s3.bucket, key, src, progress=Progress(),
+                                         content_type=media_type(self.cfg, out))
+            job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
+            job.stats.setdefault("streamed", []).append(
+                {"file": out, "key": key, "size": size, "virtual": True})
+            self._count("file", size)
+            return
         job.logger.debug("file", src, "->", out)
         n = await asyncio.get_running_loop().run_in_executor(None, file_src.copy_file, src, out)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n

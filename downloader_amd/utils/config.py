@@ -136,6 +136,9 @@ class DownloadConfig(BaseModel):
     # bucket:// sources: select media from the object listing and relay only the selected
     # objects source S3 -> staging S3 through presigned GETs (no disk hop, extras never fetched)
     stream_bucket: bool = True
+    # file:// sources: a single selector-approved file is uploaded straight from its path
+    # (sendfile) instead of being copied into the job directory first
+    stream_file: bool = True
     # torrent piece SHA-1: cpu, gpu (gfx950 kernel) or auto
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)

@@ -279,7 +279,18 @@ def test_file_urls_gated(run, make_cfg, origin_cls, tmp_path):
         await _wait(w2)
         assert w2.results[0].outcome == "staged"
         assert s3.get("triton-staging", keys.object_key("j11", "in.mkv")) == b"f" * 12345
-        await w2.stop(); await s3.stop(); await origin.stop()
+        assert w2.results[0].stats.get("streamed")          # uploaded from its own path
+        assert src.read_bytes() == b"f" * 12345               # source untouched
+        await w2.stop()
+        # disk path (stream_file off) and a non-media name: copied, then selected as usual
+        w3 = Worker(make_cfg(s3.endpoint, download={"allow_file_urls": True,
+                                                    "stream_file": False}), broker=b2)
+        await w3.start(health=False)
+        await w3.submit(api.make_download("j12", "file", f"file://{src}"))
+        await _wait(w3)
+        assert w3.results[0].outcome == "staged" and not w3.results[0].stats.get("streamed")
+        assert s3.get("triton-staging", keys.object_key("j12", "in.mkv")) == b"f" * 12345
+        await w3.stop(); await s3.stop(); await origin.stop()
     run(go())
 
 
