@@ -224,7 +224,10 @@ class DownloadStage(Stage):
             it = by_path[f]
             async with sem:
                 await s3.relay_object(self.cfg.s3.bucket, key,
-                                      client.presign("GET", src.bucket, it.name), it.size, prog,
+                                      # every Range part is its own request: the URL must
+                                      # outlive the slowest object's last part
+                                      client.presign("GET", src.bucket, it.name, 12 * 3600),
+                                      it.size, prog,
                                       content_type=media_type(self.cfg, f))
         await asyncio.gather(*(one(k, f) for k, f in owner.items()))
         staged = sum(by_path[f].size for f in owner.values())
