@@ -400,7 +400,7 @@ async def config_swarm(a) -> Dict:
     total = int(2e9 * a.scale)
     src = tempfile.mkdtemp(prefix="swarm-src-", dir=a.src_dir)
     dst = tempfile.mkdtemp(prefix="swarm-dst-", dir=a.stage_dir or None)
-    proc = conn = None
+    procs: List = []
     seeders = []
     try:
         p = os.path.join(src, "swarm.mkv")
@@ -414,11 +414,20 @@ async def config_swarm(a) -> Dict:
                 seeders.append(c)
             ports = [c.listen_port for c in seeders]
         else:
+            # one process per seeder (--seeder-procs 1: all in one, as in the first round-2
+            # runs, where that process's event loop capped the leecher at ~1.4 GB/s)
             ctx = mp.get_context("spawn")
-            conn, child = ctx.Pipe()
-            proc = ctx.Process(target=_seed_proc, args=(child, raw, src, a.seeders), daemon=True)
-            proc.start()
-            ports = await asyncio.get_running_loop().run_in_executor(None, conn.recv)
+            nproc = max(1, min(a.seeders, getattr(a, "seeder_procs", 0) or a.seeders))
+            share = [a.seeders // nproc + (1 if i < a.seeders % nproc else 0)
+                     for i in range(nproc)]
+            for n in share:
+                conn, child = ctx.Pipe()
+                proc = ctx.Process(target=_seed_proc, args=(child, raw, src, n), daemon=True)
+                proc.start()
+                procs.append((proc, conn))
+            ports = []
+            for _, conn in procs:
+                ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline).start()
         cpu0 = _self_cpu()
         t0 = time.perf_counter()
@@ -426,7 +435,8 @@ async def config_swarm(a) -> Dict:
         await asyncio.wait_for(s.wait(), 1800)
         dt = time.perf_counter() - t0
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
-               "seeders_in_process": bool(seeders), "piece_len": a.piece_mb << 20,
+               "seeders_in_process": bool(seeders), "seeder_procs": len(procs),
+               "piece_len": a.piece_mb << 20,
                "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
                "leech_cpu_s": round(_self_cpu() - cpu0, 2), "hash_fails": s.stats["hash_fails"]}
         await leech.close()
@@ -434,11 +444,12 @@ async def config_swarm(a) -> Dict:
     finally:
         for c in seeders:
             await c.close()
-        if proc is not None:
+        for proc, conn in procs:
             try:
                 conn.send("stop")
             except (OSError, ValueError):
                 pass
+        for proc, _ in procs:
             proc.join(timeout=30)
             if proc.is_alive():
                 proc.kill()
@@ -463,6 +474,8 @@ def main(argv=None) -> int:
                     help="config 7: give up waiting for every job's convert after this long")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
+    ap.add_argument("--seeder-procs", type=int, default=0,
+                    help="config 6: processes the seeders run in (0: one per seeder)")
     ap.add_argument("--seed-inproc", action="store_true",
                     help="config 6: seeders on the measuring process's event loop (round 1)")
     ap.add_argument("--mode", choices=["tuned", "reference"], default="tuned")

@@ -579,19 +579,32 @@ class TorrentSession:
         ap.peers.add(id(pc))
         self.downloaded += len(data)
         # endgame: cancel duplicates elsewhere
-        for other_id in ap.req.pop(b, set()):
-            if other_id != id(pc):
-                other = self.peers.get(other_id)
-                if other is not None:
-                    await other.cancel(idx, begin, len(data))
+        dup = ap.req.pop(b, None)
+        if dup:
+            for other_id in dup:
+                if other_id != id(pc):
+                    other = self.peers.get(other_id)
+                    if other is not None:
+                        await other.cancel(idx, begin, len(data))
         if ap.got < ap.nblocks:
             return
         self.picker.complete_blocks(idx)
-        buf = bytes(ap.buf)
+        # The piece's buffer is complete and no longer written (every block is state 2), so it
+        # is hashed and, if good, written to storage in place - one executor hop, no copy.
+        buf = ap.buf
         loop = asyncio.get_running_loop()
-        digest = await loop.run_in_executor(None, hashing.sha1, buf) if len(buf) >= 262144 \
-            else hashing.sha1(buf)
-        if digest != self.meta.piece_hash(idx):
+        off = idx * self.meta.piece_length
+        want = self.meta.piece_hash(idx)
+        try:
+            if len(buf) >= 262144:
+                good = await loop.run_in_executor(None, self._verify_write, buf, off, want)
+            else:
+                good = self._verify_write(buf, off, want)
+        except OSError as e:   # our disk, not the peer: ENOSPC/EIO fail the job (retried)
+            self.picker.requeue(idx)
+            self.fail(TorrentError(f"storage write of piece {idx} failed: {e}"))
+            return
+        if not good:
             self.stats["hash_fails"] += 1
             self.picker.requeue(idx)
             for pid in ap.peers:
@@ -601,14 +614,13 @@ class TorrentSession:
                     if p.hash_fails >= 3:
                         p.close()
             return
-        try:
-            await loop.run_in_executor(None, self.storage.write, idx * self.meta.piece_length,
-                                       buf)
-        except OSError as e:   # our disk, not the peer: ENOSPC/EIO fail the job (retried)
-            self.picker.requeue(idx)
-            self.fail(TorrentError(f"storage write of piece {idx} failed: {e}"))
-            return
         await self._piece_complete(idx)
+
+    def _verify_write(self, buf, off: int, want: bytes) -> bool:
+        if hashing.sha1(buf) != want:
+            return False
+        self.storage.write(off, buf)
+        return True
 
     async def _piece_complete(self, idx: int) -> None:
         if not self.have.set(idx):
