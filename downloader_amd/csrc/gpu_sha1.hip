@@ -20,6 +20,10 @@
 //     64 lanes of a wave touch 64 different lines per load, but each line is fully consumed
 //     by the lane's next load, so the L1/L2 absorb it (no LDS staging needed: the kernel is
 //     ALU-bound per lane, not bandwidth-bound).
+//   * Grid: 64-lane workgroups (one wave each), so 16k pieces spread over 256 workgroups =
+//     every CU; consecutive workgroups land on different XCDs round-robin. No block-to-XCD
+//     remapping: lanes share no data (each reads only its own piece once), so there is no
+//     L2 reuse for an XCD-aware order to keep local.
 //   * The host driver double-buffers pinned staging buffers: reader threads pread() batch
 //     i+1 from the page cache while batch i is copied (hipMemcpyAsync) and hashed on its own
 //     HIP stream; digests are compared on the device and only one byte per piece returns.
