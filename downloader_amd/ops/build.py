@@ -39,12 +39,25 @@ def _stale(out: Path, srcs: Sequence[Path]) -> bool:
 
 
 def _run(cmd: List[str], verbose: bool) -> None:
+    """Run a compile whose last two arguments are ``-o <out>``: the compiler writes a private
+    temporary file that then atomically replaces ``out``, so concurrent builders (the ranks of
+    a multi-GPU bench finding a stale blobd at the same moment) never leave a truncated file
+    and a running binary is never overwritten in place."""
+    assert cmd[-2] == "-o", cmd
+    out = cmd[-1]
+    tmp = f"{out}.tmp.{os.getpid()}"
+    cmd = cmd[:-1] + [tmp]
     if verbose:
-        print("+", " ".join(cmd), flush=True)
+        print("+", " ".join(cmd[:-1] + [out]), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"build failed: {' '.join(cmd[:3])} ... (exit {r.returncode})")
+    os.replace(tmp, out)
 
 
 def build_native(force: bool = False, verbose: bool = True) -> Path:

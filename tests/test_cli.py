@@ -179,3 +179,16 @@ def test_k8s_manifest_matches_the_cli_and_probes():
     assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
     src = open(os.path.join(REPO, "downloader_amd", "service", "health.py")).read()
     assert '"/readyz"' in src and '"/healthz"' in src and '"/metrics"' in src
+
+
+def test_concurrent_builds_never_leave_a_broken_binary(tmp_path):
+    """Ranks of a multi-GPU bench may find a stale blobd together: each builder writes a
+    private temporary file that atomically replaces the binary."""
+    code = ("import sys; sys.path.insert(0, %r); from downloader_amd.ops import build; "
+            "build.build_blobd(force=True, verbose=False)" % REPO)
+    procs = [subprocess.Popen([sys.executable, "-c", code]) for _ in range(3)]
+    assert all(p.wait(timeout=300) == 0 for p in procs)
+    exe = os.path.join(REPO, "downloader_amd", "bin", "blobd")
+    r = subprocess.run([exe, "--bogus"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and "usage: blobd" in r.stderr
+    assert not [f for f in os.listdir(os.path.dirname(exe)) if ".tmp." in f]
