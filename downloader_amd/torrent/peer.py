@@ -287,8 +287,12 @@ class PeerConn:
             idx, begin = struct.unpack(">II", p[:8])
             if self.inflight.pop((idx, begin), None) is not None or s.picker is not None:
                 self.down_bytes += len(p) - 8
-                await s.on_block(self, idx, begin, p[8:])   # copied once, into the piece
-            await s.fill(self)
+                # synchronous fast path (copy into the piece); a coroutine only for endgame
+                # cancels or a completed piece
+                if s.take_block(self, idx, begin, p[8:]):   # copied once, into the piece
+                    await s.block_followup(self, idx, begin, len(p) - 8)
+            if s.refill_due(self):
+                await s.fill(self)
         elif mid == REQUEST:
             idx, begin, ln = struct.unpack(">III", p[:12])
             await s.serve_request(self, idx, begin, ln)

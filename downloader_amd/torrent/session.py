@@ -385,6 +385,9 @@ class TorrentSession:
         self._gpu_verify: Optional[bool] = None
         self.piece_listeners: List = []   # callbacks(piece index) after a piece is verified
         self._piece_cache: "OrderedDict[int, bytes]" = OrderedDict()   # LRU of served pieces
+        # (piece, block) -> (active piece, endgame duplicates) between take_block and
+        # block_followup of the same dispatch
+        self._followup: Dict[Tuple[int, int], tuple] = {}
         self._piece_cache_bytes = 0
         self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0,
                       # summed over webseed streams: time in Range GETs / in piece verification
@@ -550,6 +553,38 @@ class TorrentSession:
         if pc.am_choking and unchoked < self.client.max_uploads and self.have is not None:
             await pc.set_choking(False)
 
+    def refill_due(self, pc: PeerConn) -> bool:
+        """Whether ``fill`` would send anything (checked without a coroutine per block)."""
+        return self.client.pipeline - len(pc.inflight) >= max(1, self.client.pipeline // 4)
+
+    def take_block(self, pc: PeerConn, idx: int, begin: int, data) -> bool:
+        """Synchronous part of ``on_block``: copy a block into its piece. True when
+        ``block_followup`` has work (endgame duplicates to cancel, or the piece is complete)."""
+        if self.picker is None or self.have is None:
+            return False
+        ap = self.picker.active.get(idx)
+        if ap is None or begin % BLOCK or begin >= ap.size:
+            return False
+        b = begin // BLOCK
+        if ap.state[b] == 2 or len(data) != ap.block_len(b):
+            return False
+        ap.buf[begin:begin + len(data)] = data
+        ap.state[b] = 2
+        ap.got += 1
+        ap.peers.add(id(pc))
+        self.downloaded += len(data)
+        rs = ap.req.pop(b, None)
+        others = rs is not None and (len(rs) > 1 or id(pc) not in rs)   # endgame duplicates
+        if others or ap.got >= ap.nblocks:
+            self._followup[(idx, b)] = (ap, rs if others else None)
+            return True
+        return False
+
+    async def block_followup(self, pc: PeerConn, idx: int, begin: int, ln: int) -> None:
+        ent = self._followup.pop((idx, begin // BLOCK), None)
+        if ent is not None:
+            await self._block_done(pc, ent[0], ent[1], idx, begin, ln)
+
     async def fill(self, pc: PeerConn) -> None:
         if self.picker is None or pc.peer_choking or not pc.am_interested or pc.bitfield is None:
             return
@@ -565,27 +600,18 @@ class TorrentSession:
     async def on_block(self, pc: PeerConn, idx: int, begin: int, data) -> None:
         """``data``: the block (bytes or a memoryview of the receive buffer - it is copied
         into the piece before anything awaits)."""
-        if self.picker is None or self.have is None:
-            return
-        ap = self.picker.active.get(idx)
-        if ap is None or begin % BLOCK or begin >= ap.size:
-            return
-        b = begin // BLOCK
-        if ap.state[b] == 2 or len(data) != ap.block_len(b):
-            return
-        ap.buf[begin:begin + len(data)] = data
-        ap.state[b] = 2
-        ap.got += 1
-        ap.peers.add(id(pc))
-        self.downloaded += len(data)
-        # endgame: cancel duplicates elsewhere
-        dup = ap.req.pop(b, None)
+        if self.take_block(pc, idx, begin, data):
+            await self.block_followup(pc, idx, begin, len(data))
+
+    async def _block_done(self, pc: PeerConn, ap: "_Active", dup: Optional[Set[int]], idx: int,
+                          begin: int, ln: int) -> None:
+        # endgame: cancel the duplicates requested from other peers
         if dup:
             for other_id in dup:
                 if other_id != id(pc):
                     other = self.peers.get(other_id)
                     if other is not None:
-                        await other.cancel(idx, begin, len(data))
+                        await other.cancel(idx, begin, ln)
         if ap.got < ap.nblocks:
             return
         self.picker.complete_blocks(idx)
