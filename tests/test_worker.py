@@ -242,12 +242,15 @@ def test_bucket_source_streams_selected_objects_only(run, make_cfg, origin_cls, 
         s3.put("src", "lib/Show/Season 1/e2.mkv", b"e2" * 5000)
         s3.put("src", "lib/Show/Extras/making-of.mkv", os.urandom(3 << 20))
         s3.put("src", "lib/Show/notes.txt", b"n")
+        s3.put("src", "lib/Show/Season 1/e0.mkv", b"")                # empty object
         uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,lib"
         await w.submit(api.make_download("bs1", "bucket", uri, "TV"))
         await _wait(w)
         r = w.results[0]
         assert r.outcome == "staged", r
-        assert [os.path.basename(x["file"]) for x in r.stats["streamed"]] == ["e1.mkv", "e2.mkv"]
+        assert [os.path.basename(x["file"]) for x in r.stats["streamed"]] == \
+            ["e0.mkv", "e1.mkv", "e2.mkv"]
+        assert s3.get("triton-staging", keys.object_key("bs1", "e0.mkv")) == b""
         assert r.stats["bucket_skipped_bytes"] == (3 << 20) + 1
         assert s3.get("triton-staging", keys.object_key("bs1", "e1.mkv")) == big
         assert s3.objects("triton-staging")[keys.object_key("bs1", "e1.mkv")].etag.endswith("-3")
