@@ -142,7 +142,8 @@ void HttpConn::start_tls(std::shared_ptr<TlsContext> tls, const std::string& nam
   }
   tls_ = std::move(tls);
   // Coalesce outgoing records: SSL_write emits one 16 KiB record per socket write; a buffer
-  // BIO in front of the socket turns them into 256 KiB sends, flushed by send_all.
+  // BIO in front of the socket turns them into 256 KiB sends, flushed by send_all. (An A/B on
+  // the build box measured it CPU-neutral for relays: one memcpy traded for 15 sends.)
   BIO* sock = SSL_get_wbio(ssl_);
   BIO* buf = BIO_new(BIO_f_buffer());
   if (buf && BIO_set_write_buffer_size(buf, 256 * 1024) == 1) {
