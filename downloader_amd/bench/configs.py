@@ -347,7 +347,9 @@ async def config_bucket(a) -> Dict:
                  "listed_bytes": sum(objs.values())}
     try:
         with Blobd(sink="discard", synth_bucket="src", synth_objects=objs) as b:
-            dl = {"bucket_secure": False}
+            # blobd is source and staging endpoint but cannot copy server-side: measure the
+            # relay (a same-endpoint deployment would copy without moving any bytes)
+            dl = {"bucket_secure": False, "bucket_server_copy": False}
             if a.mode == "tuned":
                 dl["stream_bucket"] = a.torrent_stream != "off"
             w = Worker(_cfg(a.mode, b.endpoint, stage, concurrency=1, download=dl),

@@ -582,6 +582,11 @@ class Conn {
       return s3_error(405, "Method Not Allowed", "MethodNotAllowed", bucket);
     }
     // ---- object level
+    if (m == "PUT" && r.h.count("x-amz-copy-source")) {  // no server-side copy here: say so
+      Summer s;
+      if (!read_body(r.content_length, s, nullptr, 0)) return false;
+      return s3_error(501, "Not Implemented", "NotImplemented", key);
+    }
     if (m == "PUT" && g_s3_fail_rate > 0) {
       thread_local std::mt19937_64 rng(std::random_device{}());
       if (std::uniform_real_distribution<double>(0, 1)(rng) < g_s3_fail_rate) {

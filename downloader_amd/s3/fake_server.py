@@ -119,6 +119,7 @@ class FakeS3:
         self.bucket_regions: Dict[str, str] = {}
         # access key -> session token it must present (signed) as x-amz-security-token
         self.session_tokens: Dict[str, str] = {}
+        self.server_copies = 0                  # CopyObject / UploadPartCopy served
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -260,6 +261,24 @@ class FakeS3:
             return self._bucket_op(req.method, bucket, q)
         return self._object_op(req, bucket, key, q, body)
 
+    def _copy_source(self, src: str, rng: Optional[str]):
+        """Bytes named by ``x-amz-copy-source: /bucket/key`` (URL-encoded), optionally
+        ``x-amz-copy-source-range: bytes=a-b``; an error response when missing."""
+        sb, _, sk = unquote(src).lstrip("/").partition("/")
+        obj = self.buckets.get(sb, {}).get(sk)
+        if obj is None:
+            return _err(404, "NoSuchKey", "copy source", src)
+        if not rng:
+            return obj.data
+        try:
+            a, b = rng.split("=", 1)[1].split("-")
+            a, b = int(a), int(b)
+        except (IndexError, ValueError):
+            return _err(400, "InvalidArgument", "bad copy source range", src)
+        if not 0 <= a <= b < len(obj.data):
+            return _err(416, "InvalidRange", "", src)
+        return obj.data[a:b + 1]
+
     def _list_buckets(self) -> web.Response:
         b = "".join(f"<Bucket><Name>{escape(n)}</Name></Bucket>" for n in sorted(self.buckets))
         return _xml(f'<ListAllMyBucketsResult xmlns="{XMLNS}"><Buckets>{b}</Buckets>'
@@ -351,6 +370,16 @@ class FakeS3:
                 num = int(q.get("partNumber", "0"))
                 if not 1 <= num <= 10000:
                     return _err(400, "InvalidArgument", "bad part number", key)
+                src = req.headers.get("x-amz-copy-source")
+                if src:                              # UploadPartCopy
+                    data = self._copy_source(src, req.headers.get("x-amz-copy-source-range"))
+                    if isinstance(data, web.Response):
+                        return data
+                    etag = hashlib.md5(data).hexdigest()
+                    up.parts[num] = (data, etag)
+                    self.server_copies += 1
+                    return _xml(f'<CopyPartResult xmlns="{XMLNS}"><ETag>&quot;{etag}&quot;</ETag>'
+                                "</CopyPartResult>")
                 etag = hashlib.md5(body).hexdigest()
                 up.parts[num] = (body, etag)
                 return web.Response(status=200, headers={"ETag": f'"{etag}"'})
@@ -398,6 +427,16 @@ class FakeS3:
                 return _xml(f'<CompleteMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}'
                             f"</Bucket><Key>{escape(key)}</Key><ETag>&quot;{etag}&quot;</ETag>"
                             "</CompleteMultipartUploadResult>")
+        if m == "PUT" and req.headers.get("x-amz-copy-source"):      # CopyObject
+            data = self._copy_source(req.headers["x-amz-copy-source"], None)
+            if isinstance(data, web.Response):
+                return data
+            etag = hashlib.md5(data).hexdigest()
+            objs[key] = StoredObject(data, etag, content_type=req.headers.get(
+                "Content-Type", "application/octet-stream"))
+            self.server_copies += 1
+            return _xml(f'<CopyObjectResult xmlns="{XMLNS}"><ETag>&quot;{etag}&quot;</ETag>'
+                        "</CopyObjectResult>")
         if m == "PUT":
             etag = hashlib.md5(body).hexdigest()
             objs[key] = StoredObject(body, etag, content_type=req.headers.get(

@@ -26,6 +26,11 @@ from .select import select_from_config
 Backend = Callable[[str, Job, str], Awaitable[None]]
 
 
+def _hostport(endpoint: str) -> str:
+    e = endpoint.split("://", 1)[-1].rstrip("/").lower()
+    return e if ":" in e.rsplit("]", 1)[-1] else e + ":default"
+
+
 class DownloadStage(Stage):
     name = "download"
 
@@ -219,10 +224,19 @@ class DownloadStage(Stage):
                         selected=len(selected), staged=len(owner))
         sem = asyncio.Semaphore(max(1, d.bucket_concurrency))
         prog = Progress()
+        # same endpoint and credentials as the staging S3: a server-side copy moves no bytes
+        # through this worker at all
+        same = (_hostport(src.endpoint) == _hostport(s3.endpoint)
+                and src.access_key == s3.access_key and d.bucket_server_copy)
+        job.stats["bucket_server_copy"] = same
 
         async def one(key: str, f: str) -> None:
             it = by_path[f]
             async with sem:
+                if same:
+                    await s3.copy_object(src.bucket, it.name, self.cfg.s3.bucket, key, it.size,
+                                         content_type=media_type(self.cfg, f))
+                    return
                 await s3.relay_object(self.cfg.s3.bucket, key,
                                       # every Range part is its own request: the URL must
                                       # outlive the slowest object's last part

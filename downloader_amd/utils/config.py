@@ -136,6 +136,9 @@ class DownloadConfig(BaseModel):
     # bucket:// sources: select media from the object listing and relay only the selected
     # objects source S3 -> staging S3 through presigned GETs (no disk hop, extras never fetched)
     stream_bucket: bool = True
+    # ... and when the source bucket lives on the staging endpoint with the same credentials,
+    # copy server-side (CopyObject / UploadPartCopy): no bytes through the worker
+    bucket_server_copy: bool = True
     # file:// sources: a single selector-approved file is uploaded straight from its path
     # (sendfile) instead of being copied into the job directory first
     stream_file: bool = True

@@ -230,12 +230,21 @@ def test_multi_file_bucket_source_with_collisions(run, make_cfg, origin_cls, str
     run(go())
 
 
-def test_bucket_source_streams_selected_objects_only(run, make_cfg, origin_cls, tmp_path):
+@pytest.mark.parametrize("server_copy", [False, True])
+def test_bucket_source_streams_selected_objects_only(run, make_cfg, origin_cls, tmp_path,
+                                                     server_copy, monkeypatch):
     """bucket:// fast path: the selector runs on the object listing; selected objects (one
     above the multipart threshold: Range parts in parallel) are relayed source -> staging
-    through presigned GETs, extras are never fetched and nothing touches the disk."""
+    through presigned GETs - or, the source being on the staging endpoint with the same
+    credentials, copied server-side (CopyObject; UploadPartCopy ranges above the copy
+    limit, shrunk here to 5 MiB) - extras are never fetched and nothing touches the disk."""
+    from downloader_amd.s3 import client as s3client
+    monkeypatch.setattr(s3client, "COPY_MAX", 5 << 20)
+    monkeypatch.setattr(s3client, "COPY_PART", 5 << 20)
+
     async def go():
-        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={"bucket_secure": False})
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={
+            "bucket_secure": False, "bucket_server_copy": server_copy})
         s3.buckets["src"] = {}
         big = os.urandom((13 << 20) + 7)
         s3.put("src", "lib/Show/Season 1/e1.mkv", big)
@@ -257,7 +266,12 @@ def test_bucket_source_streams_selected_objects_only(run, make_cfg, origin_cls, 
         assert s3.get("triton-staging", keys.object_key("bs1", "e2.mkv")) == b"e2" * 5000
         assert s3.get("triton-staging", keys.object_key("bs1", "making-of.mkv")) is None
         gets = [p for m, p in s3.requests if m == "GET" and p.startswith("/src/")]
-        assert gets and not any("Extras" in p or "notes" in p for p in gets)
+        assert r.stats["bucket_server_copy"] is server_copy
+        if server_copy:
+            assert not gets and s3.server_copies == 3 + 2      # e0, e2 + e1's 3 ranges
+        else:
+            assert gets and not any("Extras" in p or "notes" in p for p in gets)
+            assert s3.server_copies == 0
         assert s3.get("triton-staging", keys.done_key("bs1")) is not None
         for dp, _, fns in os.walk(tmp_path / "dl"):
             assert not [f for f in fns if f.endswith(".mkv")], (dp, fns)
