@@ -86,6 +86,7 @@ class Worker:
             connect_timeout=cfg.s3.connect_timeout_s, io_timeout=cfg.s3.request_timeout_s,
             ssl_verify=cfg.tls.verify, ca_file=cfg.tls.ca_file, native_tls=cfg.tls.native)
         self.s3 = s3 or S3Client.from_config(cfg.s3, self.transports)
+        self.metrics.watch_runtime(self.transports)
         self.telemetry = telemetry or Telemetry.from_config(cfg, self.broker, self.log)
         self.tracer = tracer or init_tracer("downloader", cfg.trace.enabled, cfg.trace.path)
         self.services = Services(cfg, self.telemetry, self.s3, self.transports, self.metrics,

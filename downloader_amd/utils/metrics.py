@@ -17,6 +17,32 @@ from prometheus_client import CONTENT_TYPE_LATEST  # noqa: F401
 _BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120, 300, 900, 3600)
 
 
+class _RuntimeCollector:
+    def __init__(self, transports, ns: str):
+        self.transports = transports
+        self.ns = ns
+
+    def describe(self):
+        return []
+
+    def collect(self):
+        from prometheus_client.core import GaugeMetricFamily
+        nt = getattr(self.transports, "native", None)
+        if nt is not None:
+            yield GaugeMetricFamily(f"{self.ns}_http_idle_connections",
+                                    "idle keep-alive connections of the native transport",
+                                    value=nt.idle_connections())
+        try:
+            from ..ops import native
+            st = native().relay_pool_stats()
+        except Exception:     # extension not built: nothing to report
+            return
+        yield GaugeMetricFamily(f"{self.ns}_relay_pool_in_use",
+                                "relay part buffers in use", value=st["in_use"])
+        yield GaugeMetricFamily(f"{self.ns}_relay_pool_idle_bytes",
+                                "bytes held by idle relay part buffers", value=st["idle_bytes"])
+
+
 class Metrics:
     def __init__(self, namespace: str = "downloader", registry: Optional[CollectorRegistry] = None):
         self.registry = registry or CollectorRegistry(auto_describe=True)
@@ -43,6 +69,15 @@ class Metrics:
                                       namespace=ns, registry=r)
         self.messages = Counter("broker_messages_total", "broker traffic", ["queue", "op"],
                                 namespace=ns, registry=r)
+
+    def watch_runtime(self, transports=None, namespace: str = "downloader") -> None:
+        """Gauges read at scrape time from the native runtime: idle keep-alive connections
+        of the native transport and the hashed relay's part-buffer pool (in use / idle
+        bytes). Registered once per registry."""
+        if getattr(self, "_runtime", None) is not None:
+            return
+        self._runtime = _RuntimeCollector(transports, namespace)
+        self.registry.register(self._runtime)
 
     @contextmanager
     def time_stage(self, stage: str) -> Iterator[None]:

@@ -200,7 +200,10 @@ def test_health_endpoint_semantics(run, make_cfg, origin_cls):
             async with sess.get(f"http://127.0.0.1:{port}/readyz") as r:
                 assert r.status == 200
             async with sess.get(f"http://127.0.0.1:{port}/metrics") as r:
-                assert "downloader_jobs_total" in await r.text()
+                txt = await r.text()
+                assert "downloader_jobs_total" in txt
+                assert "downloader_http_idle_connections" in txt       # native runtime gauges
+                assert "downloader_relay_pool_idle_bytes" in txt
         w.active.clear()
         await hs.stop()
         await w.stop(); await s3.stop(); await origin.stop()
