@@ -193,6 +193,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["webseed_verify_depth_gpu"] = a.webseed_verify_depth_gpu
             if getattr(a, "no_gpu_prewarm", False):
                 dl["gpu_prewarm"] = False
+            if getattr(a, "relay_trim_s", None) is not None:
+                dl["relay_pool_idle_trim_s"] = a.relay_trim_s
             part_mb = getattr(a, "part_mb", 0)
             s3o = {"part_size": part_mb << 20} if part_mb else {}
             w = Worker(_cfg(a.mode, b.endpoint, stage, cert, concurrency=1, download=dl, s3=s3o),
@@ -500,6 +502,8 @@ def main(argv=None) -> int:
                     help="download.torrent_stream_parallel (parts in flight per job)")
     ap.add_argument("--part-mb", type=int, default=0,
                     help="configs 3/4: override s3.part_size (MiB; one relayed part per unit)")
+    ap.add_argument("--relay-trim-s", type=float, default=None,
+                    help="configs 3/4: download.relay_pool_idle_trim_s (0: trim after every job)")
     ap.add_argument("--no-gpu-prewarm", action="store_true",
                     help="do not init the GPU verifier at worker start (download.gpu_prewarm)")
     ap.add_argument("--workers", type=int, default=4, help="config 5 worker processes")

@@ -269,4 +269,14 @@ class DownloadStage(Stage):
 
 
 async def factory(cfg, services: Services) -> Stage:
+    # The torrent backends are imported lazily (a worker that never sees a torrent does not
+    # pay for them); import them off the event loop at stage creation instead of inside the
+    # first torrent job (~15 ms of module setup on that job's clock).
+    await asyncio.get_running_loop().run_in_executor(None, _warm_imports)
     return DownloadStage(cfg, services)
+
+
+def _warm_imports() -> None:
+    import importlib
+    for mod in ("..torrent.backend", "..torrent.stream", "..torrent.eager", ".space"):
+        importlib.import_module(mod, __package__)
