@@ -73,6 +73,30 @@ int64_t chunk_size(const std::string& line) {
   return n;
 }
 
+// Content-Length value: decimal digits only (a list of identical values is tolerated, as RFC
+// 9110 allows); anything else - sign, hex, overflow, conflicting values - is an error rather
+// than a guess at the body's end.
+int64_t content_length(const std::string& v) {
+  int64_t out = -1;
+  size_t i = 0;
+  while (i <= v.size()) {
+    size_t j = v.find(',', i);
+    if (j == std::string::npos) j = v.size();
+    std::string t = trim(v.substr(i, j - i));
+    if (t.empty() || t.size() > 18 || t.find_first_not_of("0123456789") != std::string::npos)
+      throw IoError("malformed Content-Length: " + v.substr(0, 64));
+    const int64_t n = std::stoll(t);
+    if (out >= 0 && n != out) throw IoError("conflicting Content-Length values");
+    out = n;
+    i = j + 1;
+  }
+  return out;
+}
+
+// A response head (or chunked trailer) larger than this is refused instead of buffered.
+constexpr size_t kMaxHeadBytes = 256 * 1024;
+constexpr size_t kMaxHeadLines = 1024;
+
 }  // namespace
 
 HttpConn::HttpConn(const std::string& host, int port, double connect_timeout_s,
@@ -359,20 +383,47 @@ ResponseHead HttpConn::read_head() {
     reusable_ = false;
     throw IoError("malformed status line: " + trim(status));
   }
-  size_t sp = status.find(' ');
-  h.status = atoi(status.c_str() + sp + 1);
+  // "HTTP/x.y NNN reason": exactly three digits, 100 - 599
+  const size_t sp = status.find(' ');
+  const std::string code = sp == std::string::npos ? "" : status.substr(sp + 1, 3);
+  if (code.size() != 3 || code.find_first_not_of("0123456789") != std::string::npos ||
+      (status.size() > sp + 4 && !isspace((unsigned char)status[sp + 4])) || code < "100" ||
+      code > "599") {
+    reusable_ = false;
+    throw IoError("malformed status line: " + trim(status).substr(0, 128));
+  }
+  h.status = std::stoi(code);
   size_t sp2 = status.find(' ', sp + 1);
   h.reason = sp2 == std::string::npos ? "" : trim(status.substr(sp2 + 1));
   bool http10 = status.compare(0, 8, "HTTP/1.0") == 0;
   h.keep_alive = !http10;
+  size_t head_bytes = status.size();
   for (;;) {
     std::string line = read_line();
     if (line == "\r\n" || line == "\n" || line.empty()) break;
+    head_bytes += line.size();
+    if (head_bytes > kMaxHeadBytes || h.headers.size() >= kMaxHeadLines) {
+      reusable_ = false;
+      throw IoError("response head too large");
+    }
     size_t c = line.find(':');
     if (c == std::string::npos) continue;
     std::string k = lower(trim(line.substr(0, c)));
     std::string v = trim(line.substr(c + 1));
-    if (k == "content-length") h.content_length = atoll(v.c_str());
+    if (k == "content-length") {
+      int64_t n;
+      try {
+        n = content_length(v);
+      } catch (...) {
+        reusable_ = false;
+        throw;
+      }
+      if (h.content_length >= 0 && n != h.content_length) {
+        reusable_ = false;
+        throw IoError("conflicting Content-Length values");
+      }
+      h.content_length = n;
+    }
     if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) h.chunked = true;
     if (k == "connection") {
       std::string lv = lower(v);
@@ -428,9 +479,11 @@ std::string HttpConn::read_body(const ResponseHead& h, int64_t max_bytes) {
       std::string line = read_line();
       int64_t n = chunk_size(line);
       if (n == 0) {
+        size_t trailer = 0;
         while (true) {
           std::string t = read_line();
           if (t == "\r\n" || t.empty()) break;
+          if ((trailer += t.size()) > kMaxHeadBytes) throw IoError("chunked trailer too large");
         }
         break;
       }
@@ -548,9 +601,11 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
       std::string line = read_line();
       int64_t n = chunk_size(line);
       if (n == 0) {
+        size_t trailer = 0;
         while (true) {
           std::string t = read_line();
           if (t == "\r\n" || t.empty()) break;
+          if ((trailer += t.size()) > kMaxHeadBytes) throw IoError("chunked trailer too large");
         }
         break;
       }

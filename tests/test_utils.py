@@ -311,3 +311,56 @@ def test_native_http_parser_survives_garbage(run, tmp_path):
         srv.close()
         await srv.wait_closed()
     run(go(), timeout=300)
+
+
+def test_native_http_head_limits_and_strict_lengths(run):
+    """The native parser refuses what it cannot delimit safely instead of guessing: a
+    Content-Length that is not plain decimal, conflicting Content-Length values, a status code
+    that is not three digits in 100-599, and a head of more than 1,024 lines / 256 KiB (an
+    origin streaming headers forever would otherwise grow memory without bound). Identical
+    repeated lengths (RFC 9110) are accepted."""
+    from downloader_amd.net.http import HttpError, NativeTransport
+    hdrs = b"".join(b"X-%d: v\r\n" % i for i in range(2000))
+    cases = {
+        "bad_len": (b"HTTP/1.1 200 OK\r\nContent-Length: 0x10\r\n\r\n" + b"a" * 16, None),
+        "plus_len": (b"HTTP/1.1 200 OK\r\nContent-Length: +5\r\n\r\nhello", None),
+        "conflict": (b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\nContent-Length: 6\r\n\r\n"
+                     b"hello!", None),
+        "list_conflict": (b"HTTP/1.1 200 OK\r\nContent-Length: 5, 6\r\n\r\nhello!", None),
+        "list_same": (b"HTTP/1.1 200 OK\r\nContent-Length: 5, 5\r\n\r\nhello", b"hello"),
+        "code4": (b"HTTP/1.1 2000 OK\r\nContent-Length: 1\r\n\r\nx", None),
+        "code99": (b"HTTP/1.1 099 Odd\r\nContent-Length: 1\r\n\r\nx", None),
+        "nocode": (b"HTTP/1.1\r\nContent-Length: 1\r\n\r\nx", None),
+        "many_headers": (b"HTTP/1.1 200 OK\r\n" + hdrs + b"Content-Length: 1\r\n\r\nx", None),
+        "big_trailer": (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n1\r\nx\r\n0\r\n"
+                        + (b"T: " + b"t" * 60000 + b"\r\n") * 5 + b"\r\n", None),
+        "ok": (b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\n\r\nhello", b"hello"),
+    }
+
+    async def go():
+        current = {"k": None}
+
+        async def serve(r, w):
+            try:
+                await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+                w.write(cases[current["k"]][0])
+                await w.drain()
+                await asyncio.sleep(0.05)
+            except Exception:
+                pass
+            w.close()
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        t = NativeTransport(2, connect_timeout=2, io_timeout=2)
+        for k, (_, want) in cases.items():
+            current["k"] = k
+            if want is None:
+                with pytest.raises(HttpError):
+                    await asyncio.wait_for(t.request("GET", f"http://127.0.0.1:{port}/{k}"), 10)
+            else:
+                r = await asyncio.wait_for(t.request("GET", f"http://127.0.0.1:{port}/{k}"), 10)
+                assert r.status == 200 and r.body == want, k
+        await t.close()
+        srv.close()
+        await srv.wait_closed()
+    run(go(), timeout=120)
