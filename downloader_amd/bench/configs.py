@@ -135,18 +135,18 @@ async def config1(a) -> Dict:
         lat = []
         for i in range(a.jobs):
             m = api.make_download(f"c1-{a.mode}-{i}", "http",
-                                  b.media_url(f"c1-{i}.mkv", 10 * MB, i))
+                                  b.media_url(f"c1-{i}.mkv", a.object_mb * MB, i))
             _, r = await _run_jobs(w, [m])
             assert r[0].outcome == "staged", r[0]
             lat.append(r[0].seconds)
         await w.stop()
     shutil.rmtree(stage, ignore_errors=True)
     lat = lat[1:] or lat   # first job warms connections
-    return {"config": 1, "mode": a.mode, "jobs": len(lat), "object_MB": 10,
+    return {"config": 1, "mode": a.mode, "jobs": len(lat), "object_MB": a.object_mb,
             **({"tls": True} if cert else {}),
             "p50_latency_s": round(statistics.median(lat), 4),
             "p90_latency_s": round(_pct(lat, 0.9), 4),
-            "MBps_sequential": round(10 / statistics.mean(lat), 1)}
+            "MBps_sequential": round(a.object_mb / statistics.mean(lat), 1)}
 
 
 # ---------------------------------------------------------------------------- configs 3/4
@@ -487,6 +487,8 @@ def main(argv=None) -> int:
                     help="configs 1/3/4: origin, webseed and S3 over https (blobd certificate)")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--jobs", type=int, default=21, help="config 1: sequential jobs")
+    ap.add_argument("--object-mb", type=int, default=10,
+                    help="config 1: object size (BASELINE: 10 MB)")
     ap.add_argument("--piece-mb", type=int, default=4)
     ap.add_argument("--reps", type=int, default=1,
                     help="configs 3/4: stage the torrent this many times, report the median")
