@@ -245,7 +245,13 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"],
             "worker_rss_peak_MB": rss["rss_peak_MB"],
             "relay_pool_after": pool,
-            "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps]}
+            "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps],
+            # per rep (the first is the worker's cold job): job seconds, summed relay seconds
+            # of all parts, worker and peer CPU seconds
+            "reps_detail": [{"job_s": round(x[0], 3),
+                             "relay_s": x[1][0].stats.get("torrent", {}).get("webseed_fetch_s"),
+                             "worker_cpu_s": round(x[2], 2), "peer_cpu_s": round(x[3], 2)}
+                            for x in reps]}
 
 
 # ---------------------------------------------------------------------------- config 5
