@@ -467,12 +467,48 @@ async def config_swarm(a) -> Dict:
         shutil.rmtree(dst, ignore_errors=True)
 
 
+# ---------------------------------------------------------------------------- config 9
+async def config_small(a) -> Dict:
+    """Control-plane ceiling (extra): ``--jobs`` tiny HTTP jobs (``--small-kb``) submitted at
+    once to ONE worker process with ``--concurrency`` jobs in flight. Every job still does the
+    whole protocol - done-marker check, relayed PUT, done marker, convert publish, telemetry -
+    so jobs/s and CPU-ms per job are the per-process cost of a job apart from its bytes."""
+    stage = tempfile.mkdtemp(prefix="cfg9-")
+    n = max(100, a.jobs)
+    with Blobd(sink="discard") as b:
+        w = Worker(_cfg(a.mode, b.endpoint, stage, None, concurrency=a.concurrency),
+                   broker=MemoryBroker())
+        await w.start(health=False)
+        warm = [api.make_download(f"c9-w{i}", "http", b.media_url(f"w{i}.mkv", 1000, i))
+                for i in range(min(100, n))]
+        await _run_jobs(w, warm)
+        msgs = [api.make_download(f"c9-{a.mode}-{i}", "http",
+                                  b.media_url(f"c9-{i}.mkv", a.small_kb * 1000, i))
+                for i in range(n)]
+        c0, p0 = _self_cpu(), b.cpu_seconds()
+        dt, res = await _run_jobs(w, msgs)
+        cpu, peer = _self_cpu() - c0, b.cpu_seconds() - p0
+        await w.stop()
+    shutil.rmtree(stage, ignore_errors=True)
+    staged = sum(1 for r in res if r.outcome == "staged")
+    lat = [r.seconds for r in res]
+    return {"config": 9, "mode": a.mode, "jobs": n, "staged": staged,
+            "object_kB": a.small_kb, "concurrency": a.concurrency,
+            "jobs_per_s": round(n / dt, 1), "worker_cpu_ms_per_job": round(1000 * cpu / n, 3),
+            "peer_cpu_ms_per_job": round(1000 * peer / n, 3),
+            "p50_latency_s": round(statistics.median(lat), 4),
+            "p99_latency_s": round(_pct(lat, 0.99), 4)}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, action="append", required=True,
                     help="1, 3, 4, 5 (BASELINE.json), 6 (peer-wire swarm, extra), 7 (chaos "
                          "soak: worker kills + broker connection drops under load, extra) or "
-                         "8 (bucket:// season, extra; --torrent-stream off = disk path)")
+                         "8 (bucket:// season, extra; --torrent-stream off = disk path) or 9 "
+                         "(control-plane ceiling: tiny jobs through one worker, extra)")
+    ap.add_argument("--small-kb", type=int, default=1,
+                    help="config 9: object size in kB (jobs = --jobs, in flight = --concurrency)")
     ap.add_argument("--chaos-interval", type=float, default=2.0,
                     help="config 7: seconds between chaos actions (kill / connection drop)")
     ap.add_argument("--no-chaos-kill", dest="chaos_kill", action="store_false",
@@ -541,6 +577,8 @@ def main(argv=None) -> int:
             out = asyncio.run(config_chaos(a))
         elif c == 8:
             out = asyncio.run(config_bucket(a))
+        elif c == 9:
+            out = asyncio.run(config_small(a))
         else:
             raise SystemExit(f"config {c}: use bench.py for config 2")
         print(json.dumps(out), flush=True)

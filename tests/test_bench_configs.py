@@ -28,3 +28,12 @@ def test_config4_single_rep_default(run):
     r = run(configs.config_torrent(_ns(), 4), timeout=120)
     assert r["reps"] == 1 and r["files"] == 50
     assert r["uploaded_bytes"] == r["bytes"]
+
+
+def test_config9_control_plane_ceiling(run):
+    """Config 9: tiny jobs through one worker; every job is staged and the per-job CPU cost
+    is reported."""
+    r = run(configs.config_small(_ns(jobs=150, concurrency=16, small_kb=1)), timeout=120)
+    assert r["staged"] == r["jobs"] == 150
+    assert r["jobs_per_s"] > 0 and r["worker_cpu_ms_per_job"] > 0
+    assert r["p99_latency_s"] >= r["p50_latency_s"]
