@@ -54,6 +54,12 @@ class DownloadStage(Stage):
             job.jobdir.acquire()
         return job.jobdir.path
 
+    def _make_dir(self, job: Job) -> str:
+        """Claim and create the job directory (one executor hop per job)."""
+        path = self.job_dir(job)
+        os.makedirs(path, exist_ok=True)
+        return path
+
     def _count(self, proto: str, n: int) -> None:
         if self.sv.metrics is not None and n:
             self.sv.metrics.bytes_downloaded.labels(proto).inc(n)
@@ -62,9 +68,7 @@ class DownloadStage(Stage):
         media = job.media
         protocol = api.enum_to_string("SourceType", media.source)
         try:
-            path = await asyncio.get_running_loop().run_in_executor(None, self.job_dir, job)
-            await asyncio.get_running_loop().run_in_executor(
-                None, lambda: os.makedirs(path, exist_ok=True))
+            path = await asyncio.get_running_loop().run_in_executor(None, self._make_dir, job)
             job.logger.info("created downloadPath", path)
         except OSError as e:
             job.logger.error("Failed to create directory", str(e))
