@@ -30,10 +30,12 @@ def _worker(args) -> int:
     from .utils.config import load_config
     from .utils.log import get_logger
     log = get_logger("index.py")
+    from .utils.limits import raise_nofile
     cfg = load_config(path=args.config or None)
     if args.mode:
         cfg.mode = args.mode
         cfg.apply_mode()
+    raise_nofile()   # one descriptor per torrent file for a session: EMFILE at 1,024 otherwise
 
     async def main() -> int:
         stop = asyncio.Event()

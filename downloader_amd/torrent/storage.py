@@ -7,10 +7,12 @@ uses the native SHA-1 (``ops.hashing``); a full recheck can run on the MI355X.
 """
 from __future__ import annotations
 
+import errno
 import os
 from typing import List, Optional, Sequence, Tuple
 
 from ..ops import hashing
+from ..utils import limits
 from .metainfo import Metainfo
 
 
@@ -62,12 +64,22 @@ class Bitfield:
         return [i for i in range(self.n) if i not in self]
 
 
+FD_MARGIN = 64      # connections, logs, pipes of the job besides the storage's own files
+
+
 class Storage:
     def __init__(self, meta: Metainfo, root: str, preallocate: bool = True):
         self.meta = meta
         self.root = root
         self.paths = meta.local_files(root)
         self.fds: List[int] = []
+        # one descriptor per file for the session, plus the verifier's own opens and the
+        # job's connections: fail with a clear error instead of EMFILE halfway through
+        need = len(self.paths) * 2 + FD_MARGIN
+        if need > limits.fd_headroom():
+            raise OSError(errno.EMFILE, f"torrent has {len(self.paths)} files: needs about "
+                                        f"{need} more open files than RLIMIT_NOFILE leaves "
+                                        f"({limits.fd_headroom()}); raise the limit")
         # Only data that was on disk before we created/preallocated the files can be resumed;
         # a fresh (sparse) layout needs no recheck pass at all.
         self.preexisting = any(os.path.isfile(p) and os.path.getsize(p) > 0 for p, _ in self.paths)

@@ -364,3 +364,34 @@ def test_native_http_head_limits_and_strict_lengths(run):
         srv.close()
         await srv.wait_closed()
     run(go(), timeout=120)
+
+
+def test_nofile_limit_raised_and_storage_headroom_checked(tmp_path):
+    """A torrent with more files than RLIMIT_NOFILE leaves fails up front with EMFILE and a
+    clear message (not halfway through the job); ``raise_nofile`` (worker start) lifts the
+    soft limit to the hard one so the same torrent opens."""
+    import errno
+    import resource
+
+    from downloader_amd.torrent.bencode import bencode
+    from downloader_amd.torrent.metainfo import parse_torrent
+    from downloader_amd.torrent.storage import Storage
+    from downloader_amd.utils import limits
+    files = [{b"length": 10, b"path": [b"f%04d.mkv" % i]} for i in range(600)]
+    info = {b"name": b"many", b"piece length": 16384, b"pieces": b"\0" * 20, b"files": files}
+    meta = parse_torrent(bencode({b"info": info}))
+    soft0, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if hard != resource.RLIM_INFINITY and hard < 1400:
+        pytest.skip(f"hard RLIMIT_NOFILE {hard} too low for this test")
+    try:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (512, hard))
+        with pytest.raises(OSError) as ei:
+            Storage(meta, str(tmp_path / "a"))
+        assert ei.value.errno == errno.EMFILE and "600 files" in str(ei.value)
+        soft, _ = limits.raise_nofile()
+        assert soft >= min(hard, limits.NOFILE_CAP) and soft > 512
+        st = Storage(meta, str(tmp_path / "b"))
+        assert len(st.fds) == 600
+        st.close()
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft0, hard))
