@@ -74,11 +74,15 @@ class Metainfo:
             return [(os.path.join(base, *[_safe(p) for p in f.path]), f.length) for f in self.files]
         return [(os.path.join(root, _safe(self.name)), self.total_length)]
 
-    def file_at(self, offset: int) -> int:
-        """Index of the (non-empty) file holding storage byte ``offset``."""
+    def _file_ends(self) -> List[int]:
         ends = self.__dict__.get("_ends")
         if ends is None:
             ends = self.__dict__["_ends"] = [f.offset + f.length for f in self.files]
+        return ends
+
+    def file_at(self, offset: int) -> int:
+        """Index of the (non-empty) file holding storage byte ``offset``."""
+        ends = self._file_ends()
         i = bisect.bisect_right(ends, offset)
         while i < len(self.files) - 1 and self.files[i].length == 0:
             i += 1
@@ -88,7 +92,10 @@ class Metainfo:
         """Split a storage byte range into (file_index, file_offset, length) segments."""
         out = []
         end = offset + length
-        for idx, f in enumerate(self.files):
+        # first file ending after `offset` (bisect: a torrent may have tens of thousands of
+        # files, and this runs per fetched run / written piece)
+        for idx in range(bisect.bisect_right(self._file_ends(), offset), len(self.files)):
+            f = self.files[idx]
             fs, fe = f.offset, f.offset + f.length
             if fe <= offset or f.length == 0:
                 continue
@@ -99,10 +106,23 @@ class Metainfo:
         return out
 
 
+NAME_MAX = 255      # bytes per path component on Linux filesystems
+
+
 def _safe(component: str) -> str:
     c = component.replace("/", "_").replace("\\", "_").replace("\x00", "")
     if c in ("", ".", ".."):
         c = "_" + c
+    if len(c.encode("utf-8", "surrogateescape")) > NAME_MAX:
+        # too long to create (ENAMETOOLONG): keep the head and the extension, plus a digest
+        # of the whole name so two long names with the same head stay distinct
+        stem, ext = os.path.splitext(c)
+        if len(ext.encode("utf-8", "surrogateescape")) > 32:
+            stem, ext = c, ""
+        tag = "~" + hashlib.sha1(c.encode("utf-8", "surrogateescape")).hexdigest()[:12]
+        room = NAME_MAX - len((tag + ext).encode("utf-8", "surrogateescape"))
+        head = stem.encode("utf-8", "surrogateescape")[:room].decode("utf-8", "ignore")
+        c = head + tag + ext
     return c
 
 

@@ -854,3 +854,50 @@ def test_peer_read_batch_handles_every_split(run):
             await f
             assert got == msgs, cut
     run(go())
+
+
+def test_file_spans_bisect_matches_linear_scan():
+    """file_spans starts at the first file ending after the offset (bisect) and returns what
+    a scan over every file returns, zero-length files included."""
+    import random
+
+    from downloader_amd.torrent.bencode import bencode
+    from downloader_amd.torrent.metainfo import parse_torrent
+    rng = random.Random(7)
+    lengths = [rng.choice([0, 1, 5, 16384, 70000, 1 << 20]) for _ in range(300)]
+    lengths[0] = max(lengths[0], 1)
+    files = [{b"length": n, b"path": [b"f%03d.mkv" % i]} for i, n in enumerate(lengths)]
+    total = sum(lengths)
+    npieces = -(-total // 16384)
+    meta = parse_torrent(bencode({b"info": {b"name": b"t", b"piece length": 16384,
+                                            b"pieces": b"\0" * 20 * npieces, b"files": files}}))
+
+    def linear(offset, length):
+        out, end = [], offset + length
+        for idx, f in enumerate(meta.files):
+            fs, fe = f.offset, f.offset + f.length
+            if fe <= offset or f.length == 0:
+                continue
+            if fs >= end:
+                break
+            out.append((idx, max(fs, offset) - fs, min(fe, end) - max(fs, offset)))
+        return out
+    for _ in range(2000):
+        off = rng.randrange(total)
+        ln = rng.randrange(1, min(total - off, 3 << 20) + 1)
+        assert meta.file_spans(off, ln) == linear(off, ln)
+
+
+def test_overlong_path_components_are_shortened():
+    """A torrent path component longer than NAME_MAX (255 bytes) would fail with
+    ENAMETOOLONG on disk: it is cut to fit, keeping the extension, with a digest of the full
+    name so two long names sharing a prefix stay distinct; multi-byte characters are not
+    split."""
+    from downloader_amd.torrent.metainfo import NAME_MAX, _safe
+    a, b = "é" * 200 + "A.mkv", "é" * 200 + "B.mkv"
+    sa, sb = _safe(a), _safe(b)
+    assert sa != sb and sa.endswith(".mkv") and sb.endswith(".mkv")
+    assert len(sa.encode()) <= NAME_MAX and len(sb.encode()) <= NAME_MAX
+    sa.encode("utf-8")                                   # still valid UTF-8
+    assert _safe("short.mkv") == "short.mkv"
+    assert len(_safe("x" * 300).encode()) <= NAME_MAX
