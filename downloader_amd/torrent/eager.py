@@ -15,6 +15,7 @@ wins a basename collision). The upload stage later skips files listed as ``strea
 from __future__ import annotations
 
 import asyncio
+import bisect
 import os
 import time
 from dataclasses import dataclass, field
@@ -64,6 +65,10 @@ class EagerUploader:
             parts = [(1, 0, size)] if single else \
                 self.s3.plan_parts(size, meta.files[fi].offset, self.plen)
             self.files.append(_File(f, key, meta.files[fi].offset, size, parts, single=single))
+        # by torrent offset, for on_piece's bisect (files never overlap, so the ends are
+        # sorted too): per verified piece only the files it touches are looked at
+        self._by_off = sorted(self.files, key=lambda f: (f.offset, f.size))
+        self._ends = [f.offset + f.size for f in self._by_off]
         self.sem = asyncio.Semaphore(max(1, cfg.s3.max_inflight_parts * 2))
         self.tasks: List[asyncio.Task] = []
         self.error: Optional[BaseException] = None
@@ -86,8 +91,11 @@ class EagerUploader:
 
     def on_piece(self, idx: int) -> None:
         lo, hi = idx * self.plen, idx * self.plen + self.s.meta.piece_size(idx)
-        for f in self.files:
-            if f.offset >= hi or f.offset + f.size <= lo:
+        for k in range(bisect.bisect_right(self._ends, lo), len(self._by_off)):
+            f = self._by_off[k]
+            if f.offset >= hi:
+                break
+            if f.offset + f.size <= lo:
                 continue
             for num, off, ln in f.parts:
                 a = f.offset + off
