@@ -182,6 +182,20 @@ class Transport:
         pass
 
 
+async def _drain(fut: "asyncio.Future", timeout: float = 10.0) -> None:
+    """After cancelling a native call (progress flag set, sockets shut down), wait for its
+    worker thread to return before the caller's cancellation completes. The caller may close
+    the sink's fd right after (a torrent session closing its storage): a transfer still
+    splicing into that descriptor number would write into whatever file reuses it. Bounded:
+    the shut-down socket ends a blocked recv / splice at once. The outcome is discarded."""
+    try:
+        await asyncio.wait_for(asyncio.shield(fut), timeout)
+    except BaseException:
+        pass
+    if fut.done() and not fut.cancelled():
+        fut.exception()        # retrieved: no "Future exception was never retrieved" log
+
+
 class NativeTransport(Transport):
     def __init__(self, max_workers: int = 32, connect_timeout: float = 10.0,
                  io_timeout: float = 300.0, max_idle_per_host: int = 64,
@@ -375,6 +389,7 @@ class NativeTransport(Transport):
             if nprog is not None:
                 nprog.cancel()
             self._abort_slot(slot)
+            await _drain(fut)
             raise
         finally:
             self._end_slot(slot)
@@ -470,6 +485,7 @@ class NativeTransport(Transport):
                 if nprog is not None:
                     nprog.cancel()
                 self._abort_slot(slot)
+                await _drain(fut)
                 raise
             finally:
                 self._end_slot(slot)

@@ -395,3 +395,54 @@ def test_nofile_limit_raised_and_storage_headroom_checked(tmp_path):
         st.close()
     finally:
         resource.setrlimit(resource.RLIMIT_NOFILE, (soft0, hard))
+
+
+def test_cancelled_native_download_never_writes_after_cancel(run, tmp_path):
+    """Cancelling a native download into a file returns only once the transfer thread has
+    let go of the descriptor: a file opened right after (reusing the fd number, as a torrent
+    session's next storage would) receives none of the old transfer's bytes."""
+    from downloader_amd.net.http import FileSink, NativeTransport
+
+    async def go():
+        async def slow(r, w):
+            await r.readuntil(b"\r\n\r\n")
+            w.write(b"HTTP/1.1 200 OK\r\nContent-Length: 100000000\r\n\r\n")
+            try:
+                for _ in range(400):
+                    w.write(b"x" * 65536)
+                    await w.drain()
+                    await asyncio.sleep(0.005)
+            except Exception:
+                pass
+            w.close()
+        srv = await asyncio.start_server(slow, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        t = NativeTransport(2, connect_timeout=2, io_timeout=10)
+        loop = asyncio.get_running_loop()
+        futs = []
+        orig = loop.run_in_executor
+
+        def capture(ex, fn, *a):
+            f = orig(ex, fn, *a)
+            futs.append(f)
+            return f
+        loop.run_in_executor = capture
+        fd = os.open(str(tmp_path / "old"), os.O_WRONLY | os.O_CREAT, 0o600)
+        task = asyncio.ensure_future(t.request("GET", f"http://127.0.0.1:{port}/big",
+                                               sink=FileSink(fd, 0, 100_000_000)))
+        await asyncio.sleep(0.3)
+        task.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await task
+        assert futs and all(f.done() for f in futs)    # the thread has returned
+        loop.run_in_executor = orig
+        os.close(fd)
+        fd2 = os.open(str(tmp_path / "new"), os.O_WRONLY | os.O_CREAT, 0o600)
+        await asyncio.sleep(0.5)
+        os.close(fd2)
+        assert os.path.getsize(tmp_path / "new") == 0
+        assert os.path.getsize(tmp_path / "old") > 0
+        await t.close()
+        srv.close()
+        await srv.wait_closed()
+    run(go(), timeout=60)
