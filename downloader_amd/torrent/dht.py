@@ -2,10 +2,14 @@
 (yarn.lock:367,1912-1936).
 
 KRPC over UDP with bencoded ``ping`` / ``find_node`` / ``get_peers`` / ``announce_peer`` in both
-directions. The routing table keeps up to ``k`` nodes per XOR-distance bucket (160 buckets,
-least-recently-seen replaced when a bucket is full and its oldest node fails a ping is
-simplified to "drop the oldest"). ``get_peers`` runs the iterative alpha=3 lookup, collects
-``values`` and then announces to the closest nodes that returned tokens.
+directions. The routing table keeps up to ``k`` nodes per XOR-distance bucket (160 buckets).
+BEP-5 keeps good nodes over new ones: a full bucket only admits a newcomer by evicting a node
+not heard from for ``STALE_S`` (the "ping the questionable node" step is simplified to "a
+questionable node loses its slot"), so a flood of queries under fresh ids cannot flush the
+nodes a lookup relies on. ``get_peers`` runs the iterative alpha=3 lookup, collects ``values``
+and then announces to the closest nodes that returned tokens. A reply is accepted only from
+the address the query went to (a guessed 16-bit transaction id from elsewhere is dropped), and
+announced peers expire after ``PEER_TTL_S`` as in BEP-5.
 """
 from __future__ import annotations
 
@@ -25,6 +29,8 @@ K = 8
 ALPHA = 3
 STORE_MAX_TORRENTS = 10000      # announce_peer store bounds (any node can announce)
 STORE_MAX_PEERS = 200
+STALE_S = 15 * 60               # BEP-5: a node unheard-from for 15 minutes is questionable
+PEER_TTL_S = 30 * 60            # announced peers are forgotten after 30 minutes
 
 
 def distance(a: bytes, b: bytes) -> int:
@@ -41,6 +47,10 @@ class Node:
     id: bytes
     addr: Addr
     seen: float
+
+
+def _is_id(x) -> bool:
+    return isinstance(x, bytes) and len(x) == 20
 
 
 def pack_nodes(nodes: Sequence[Node]) -> bytes:
@@ -85,8 +95,10 @@ class RoutingTable:
                 b[i] = n
                 return
         if len(b) >= self.k:
-            b.sort(key=lambda x: x.seen)
-            b.pop(0)
+            oldest = min(range(len(b)), key=lambda i: b[i].seen)
+            if n.seen - b[oldest].seen < STALE_S:
+                return                   # every resident node is still good: keep them
+            b.pop(oldest)
         b.append(n)
 
     def remove(self, node_id: bytes) -> None:
@@ -112,7 +124,8 @@ class DHTNode(asyncio.DatagramProtocol):
         self.timeout = timeout
         self.table = RoutingTable(self.id)
         self.store: Dict[bytes, Dict[Addr, float]] = {}
-        self._pending: Dict[bytes, asyncio.Future] = {}
+        self._pending: Dict[bytes, Tuple[asyncio.Future, Addr]] = {}
+        self._tasks: Set[asyncio.Task] = set()
         self._tid = 0
         self._secret = os.urandom(16)
         self._old_secret = self._secret
@@ -147,9 +160,11 @@ class DHTNode(asyncio.DatagramProtocol):
             await self.lookup(self.id, want_peers=False)
 
     async def close(self) -> None:
-        for f in self._pending.values():
+        for f, _a in self._pending.values():
             if not f.done():
                 f.cancel()
+        for task in list(self._tasks):
+            task.cancel()
         if self.transport is not None:
             self.transport.close()
 
@@ -171,7 +186,7 @@ class DHTNode(asyncio.DatagramProtocol):
         self._tid = (self._tid + 1) & 0xFFFF
         t = struct.pack(">H", self._tid)
         fut = asyncio.get_running_loop().create_future()
-        self._pending[t] = fut
+        self._pending[t] = (fut, (addr[0], addr[1]))
         a = dict(args)
         a["id"] = self.id
         self._send({"t": t, "y": "q", "q": q, "a": a}, addr)
@@ -208,8 +223,13 @@ class DHTNode(asyncio.DatagramProtocol):
             return
         addr = (addr[0], addr[1])
         if y == b"r" or y == b"e":
-            f = self._pending.get(t)
-            if f is not None and not f.done():
+            ent = self._pending.get(t)
+            if ent is None or ent[1] != addr:      # unknown tid, or a reply from elsewhere
+                if ent is not None:
+                    self.bad_packets += 1
+                return
+            f = ent[0]
+            if not f.done():
                 if y == b"r" and isinstance(msg.get(b"r"), dict):
                     f.set_result(msg[b"r"])
                 else:
@@ -233,13 +253,17 @@ class DHTNode(asyncio.DatagramProtocol):
         r: Dict[str, object] = {"id": self.id}
         if q == b"ping":
             pass
+        elif q in (b"find_node", b"get_peers") and not _is_id(
+                a.get(b"target" if q == b"find_node" else b"info_hash")):
+            self._send({"t": t, "y": "e", "e": [203, "bad target"]}, addr)
+            return
         elif q == b"find_node":
             target = a.get(b"target", b"")
             r["nodes"] = pack_nodes(self.table.closest(target))
         elif q == b"get_peers":
             ih = a.get(b"info_hash", b"")
             r["token"] = self._token(addr[0])
-            peers = self.store.get(ih)
+            peers = self._live_peers(ih)
             if peers:
                 r["values"] = [pack_peer(p) for p in list(peers)[:50]]
             else:
@@ -267,6 +291,18 @@ class DHTNode(asyncio.DatagramProtocol):
             return
         self._send({"t": t, "y": "r", "r": r}, addr)
 
+    def _live_peers(self, ih: bytes) -> Dict[Addr, float]:
+        """Peers announced for ``ih`` within ``PEER_TTL_S``; expired ones are dropped."""
+        peers = self.store.get(ih)
+        if not peers:
+            return {}
+        cut = time.monotonic() - PEER_TTL_S
+        for p in [p for p, ts in peers.items() if ts < cut]:
+            del peers[p]
+        if not peers:
+            del self.store[ih]
+        return peers
+
     # ---------------------------------------------------------------- client operations
     async def ping(self, addr: Addr) -> bytes:
         r = await self.query(addr, "ping", {})
@@ -278,7 +314,9 @@ class DHTNode(asyncio.DatagramProtocol):
                 await self.ping(addr)
             except Exception:
                 pass
-        asyncio.get_running_loop().create_task(_p())
+        task = asyncio.get_running_loop().create_task(_p())
+        self._tasks.add(task)                  # the loop holds only weak task references
+        task.add_done_callback(self._tasks.discard)
 
     async def _find_node_at(self, addr: Addr, target: bytes) -> List[Node]:
         r = await self.query(addr, "find_node", {"target": target})
@@ -332,7 +370,7 @@ class DHTNode(asyncio.DatagramProtocol):
 
     async def get_peers(self, info_hash: bytes, announce_port: int = 0) -> List[Addr]:
         peers, best = await self.lookup(info_hash, want_peers=True)
-        local = list(self.store.get(info_hash, {}))
+        local = list(self._live_peers(info_hash))
         if announce_port:
             await asyncio.gather(*(self.query(n.addr, "announce_peer", {
                 "info_hash": info_hash, "port": announce_port, "token": tok, "implied_port": 0})

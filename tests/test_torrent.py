@@ -901,3 +901,58 @@ def test_overlong_path_components_are_shortened():
     sa.encode("utf-8")                                   # still valid UTF-8
     assert _safe("short.mkv") == "short.mkv"
     assert len(_safe("x" * 300).encode()) <= NAME_MAX
+
+
+def test_dht_table_store_and_reply_source(run):
+    """DHT hardening (BEP-5): a full bucket keeps its good nodes and only gives up a stale
+    one; announced peers expire after PEER_TTL_S; a reply whose transaction id matches but
+    that comes from another address is dropped (the query still times out / gets the real
+    answer); find_node / get_peers with a malformed target get a KRPC error."""
+    import time as _t
+
+    from downloader_amd.torrent import dht as D
+    from downloader_amd.torrent.bencode import bdecode, bencode
+
+    own = b"\0" * 20
+    rt = D.RoutingTable(own, k=2)
+    now = _t.monotonic()
+    ids = [bytes([0x80]) + bytes([i]) * 19 for i in range(1, 4)]     # all in bucket 159
+    rt.add(D.Node(ids[0], ("10.0.0.1", 1), now))
+    rt.add(D.Node(ids[1], ("10.0.0.2", 1), now))
+    rt.add(D.Node(ids[2], ("10.0.0.3", 1), now + 1))                 # bucket full of good nodes
+    assert {n.id for n in rt.buckets[159]} == {ids[0], ids[1]}
+    rt.buckets[159][0].seen = now - D.STALE_S - 1                     # ids[0] goes questionable
+    rt.add(D.Node(ids[2], ("10.0.0.3", 1), now + 1))
+    assert {n.id for n in rt.buckets[159]} == {ids[1], ids[2]}
+
+    async def go():
+        node = await D.DHTNode(host="127.0.0.1").start()
+        probe = await D.DHTNode(host="127.0.0.1", timeout=0.5).start()
+        spoof = await D.DHTNode(host="127.0.0.1").start()
+        ih = b"h" * 20
+        node.store[ih] = {("1.2.3.4", 5): _t.monotonic() - D.PEER_TTL_S - 1,
+                          ("1.2.3.5", 6): _t.monotonic()}
+        r = await probe.query(("127.0.0.1", node.port), "get_peers", {"info_hash": ih})
+        assert [D.unpack_peer(v) for v in r[b"values"]] == [("1.2.3.5", 6)]
+        assert list(node.store[ih]) == [("1.2.3.5", 6)]
+        # a reply with the next transaction id, sent from a third socket, must not resolve it
+        nxt = (probe._tid + 1) & 0xFFFF
+        silent = ("127.0.0.1", spoof.port)                 # spoof never answers queries...
+        spoof.datagram_received = lambda data, addr: None
+        q = asyncio.ensure_future(probe.query(silent, "ping", {}))
+        await asyncio.sleep(0.05)
+        fake = bencode({"t": struct.pack(">H", nxt), "y": "r", "r": {"id": b"z" * 20}})
+        node.transport.sendto(fake, ("127.0.0.1", probe.port))   # ...so this is a forgery
+        with pytest.raises(asyncio.TimeoutError):
+            await q
+        assert probe.bad_packets >= 1 and all(n.id != b"z" * 20 for b in probe.table.buckets for n in b)
+        # malformed targets answer 203
+        got = asyncio.get_running_loop().create_future()
+        probe.datagram_received = lambda data, addr: got.done() or got.set_result(bdecode(data))
+        probe.transport.sendto(bencode({"t": b"xy", "y": "q", "q": "find_node",
+                                        "a": {"id": b"i" * 20, "target": [1]}}), ("127.0.0.1", node.port))
+        e = await asyncio.wait_for(got, 2)
+        assert e[b"y"] == b"e" and e[b"e"][0] == 203
+        for n in (node, probe, spoof):
+            await n.close()
+    run(go())
