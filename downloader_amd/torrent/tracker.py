@@ -126,7 +126,7 @@ async def announce_udp(url: str, info_hash: bytes, peer_id: bytes, port: int, up
     loop = asyncio.get_running_loop()
     tr, proto = await loop.create_datagram_endpoint(_UdpProto, remote_addr=(u.hostname, u.port or 80))
     try:
-        async def rt(packet: bytes, tid: int, min_len: int) -> bytes:
+        async def rt(packet: bytes, tid: int, want: int, min_len: int) -> bytes:
             for attempt in range(retries + 1):
                 tr.sendto(packet)
                 try:
@@ -138,6 +138,9 @@ async def announce_udp(url: str, info_hash: bytes, peer_id: bytes, port: int, up
                             action = struct.unpack(">I", data[:4])[0]
                             if action == 3:
                                 raise TrackerError(data[8:].decode("utf-8", "replace"))
+                            if action != want:
+                                raise TrackerError(f"UDP tracker replied action {action}, "
+                                                   f"expected {want}")
                             if len(data) < min_len:
                                 raise TrackerError("short UDP tracker reply")
                             return data
@@ -146,15 +149,18 @@ async def announce_udp(url: str, info_hash: bytes, peer_id: bytes, port: int, up
             raise TrackerError("UDP tracker timeout")
 
         tid = random.getrandbits(32)
-        data = await rt(struct.pack(">QII", UDP_MAGIC, 0, tid), tid, 16)
+        data = await rt(struct.pack(">QII", UDP_MAGIC, 0, tid), tid, 0, 16)
         conn_id = struct.unpack(">Q", data[8:16])[0]
         tid = random.getrandbits(32)
         pkt = struct.pack(">QII20s20sQQQIIIiH", conn_id, 1, tid, info_hash, peer_id, downloaded,
                           left, uploaded, EVENTS.get(event, 0), 0, random.getrandbits(32),
                           numwant, port)
-        data = await rt(pkt, tid, 20)
+        data = await rt(pkt, tid, 1, 20)
         interval, leechers, seeders = struct.unpack(">III", data[8:20])
-        return AnnounceResult(interval, decode_compact(data[20:]), seeders, leechers)
+        # BEP-15: the peer list's address family is the one the tracker was reached over
+        v6 = tr.get_extra_info("socket").family == socket.AF_INET6
+        peers = (decode_compact6 if v6 else decode_compact)(data[20:])
+        return AnnounceResult(interval, peers, seeders, leechers)
     finally:
         tr.close()
 

@@ -956,3 +956,27 @@ def test_dht_table_store_and_reply_source(run):
         for n in (node, probe, spoof):
             await n.close()
     run(go())
+
+
+def test_udp_tracker_reply_action_checked(run):
+    """BEP-15: a reply whose transaction id matches but whose action is not the one asked
+    for (here a scrape reply, action 2, to a connect) is a TrackerError, not a connection
+    id read out of the wrong fields."""
+    from downloader_amd.torrent.tracker import TrackerError, announce_udp
+
+    class Bad(asyncio.DatagramProtocol):
+        def connection_made(self, tr):
+            self.tr = tr
+
+        def datagram_received(self, data, addr):
+            self.tr.sendto(struct.pack(">II", 2, struct.unpack(">I", data[12:16])[0]) + b"\0" * 12, addr)
+
+    async def go():
+        tr, _ = await asyncio.get_running_loop().create_datagram_endpoint(
+            Bad, local_addr=("127.0.0.1", 0))
+        port = tr.get_extra_info("sockname")[1]
+        with pytest.raises(TrackerError, match="action 2"):
+            await announce_udp(f"udp://127.0.0.1:{port}/announce", b"h" * 20, b"p" * 20,
+                               1, 0, 0, 0, timeout=1.0, retries=0)
+        tr.close()
+    run(go())
