@@ -329,8 +329,9 @@ class PeerConn:
         elif mid == CANCEL:
             pass  # blocks are sent as soon as they are read; nothing queued to cancel
         elif mid == PORT:
-            if s.client.dht is not None and len(p) >= 2:
-                s.client.dht.add_node_addr((self.addr[0], struct.unpack(">H", p[:2])[0]))
+            port = struct.unpack(">H", p[:2])[0] if len(p) >= 2 else 0
+            if s.client.dht is not None and port:
+                s.client.dht.add_node_addr((self.addr[0], port))
         elif mid == EXTENDED:
             await self._extended(p)
 
@@ -345,8 +346,10 @@ class PeerConn:
             m = d.get(b"m", {})
             if isinstance(m, dict):
                 self.ext = {k: int(v) for k, v in m.items() if isinstance(v, int) and v > 0}
-            self.metadata_size = int(d.get(b"metadata_size", 0) or 0)
-            self.listen_port = int(d.get(b"p", 0) or 0)
+            # untrusted: a negative size or an out-of-range port counts as absent
+            ms, lp = d.get(b"metadata_size", 0), d.get(b"p", 0)
+            self.metadata_size = ms if isinstance(ms, int) and ms > 0 else 0
+            self.listen_port = lp if isinstance(lp, int) and 0 < lp < 65536 else 0
             if self.listen_port and not self.outgoing:
                 self.s.add_peers([(self.addr[0], self.listen_port)], source="incoming")
             await self.s.on_ext_handshake(self)
