@@ -68,7 +68,8 @@ def _supervisor(args) -> int:
 def _broker(args) -> int:
     from .broker.server import run_broker
     try:
-        asyncio.run(run_broker(args.host, args.port))
+        asyncio.run(run_broker(args.host, args.port, args.consumer_timeout, args.certfile,
+                               args.keyfile))
     except KeyboardInterrupt:
         pass
     return 0
@@ -160,6 +161,10 @@ def main(argv=None) -> int:
     b = sub.add_parser("broker")
     b.add_argument("--host", default="0.0.0.0")
     b.add_argument("--port", type=int, default=5672)
+    b.add_argument("--consumer-timeout", type=float, default=0.0,
+                   help="close a channel whose delivery stays unacked this long (s, 0: never)")
+    b.add_argument("--certfile", default="", help="PEM certificate: serve amqps://")
+    b.add_argument("--keyfile", default="")
     su = sub.add_parser("submit")
     su.add_argument("id")
     su.add_argument("source", choices=["http", "torrent", "file", "bucket"])

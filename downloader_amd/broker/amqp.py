@@ -6,12 +6,23 @@ channel for consuming (``basic.qos`` prefetch + ``basic.consume``) and one for p
 with publisher confirms, ``basic.ack``/``basic.nack``, and automatic reconnect that
 re-declares queues and re-subscribes consumers (unacked deliveries of a dead connection are
 requeued by the broker, so they are redelivered with ``redelivered=True``).
+
+Liveness below the connection (amqp-connection-manager re-runs its channel setup whenever a
+channel dies): a broker ``channel.close`` (RabbitMQ's ``consumer_timeout`` on a long job, a
+406 on a bad ack, a 404 on a deleted queue) reopens that channel on the live connection and
+re-runs setup; a broker ``basic.cancel`` (queue deleted, node failover) re-declares the queue
+and re-consumes with backoff. When the setup itself fails the connection is aborted and the
+reconnect watchdog takes over. ``consumer_live()`` is what ``/readyz`` reports.
+
+``amqps://`` (port 5671) runs the same protocol over asyncio TLS (``tls.verify``,
+``tls.ca_file``), as amqplib does for ``dyn('rabbitmq')`` URLs (lib/main.js:46).
 """
 from __future__ import annotations
 
 import asyncio
 import itertools
 import platform
+import ssl
 from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
 from urllib.parse import unquote, urlsplit
 
@@ -20,12 +31,30 @@ from .base import Broker, Delivery, Handler, Headers
 
 
 def parse_url(url: str) -> Tuple[str, int, str, str, str]:
+    """``(host, port, user, password, vhost)`` of an ``amqp://`` / ``amqps://`` URL."""
     u = urlsplit(url)
-    if u.scheme not in ("amqp", ""):
-        raise ValueError("only amqp:// URLs are supported (amqps needs TLS termination)")
+    if u.scheme not in ("amqp", "amqps", ""):
+        raise ValueError(f"not an AMQP URL (amqp:// or amqps://): {u.scheme}://")
     vhost = unquote(u.path[1:]) if u.path and u.path != "/" else "/"
-    return (u.hostname or "127.0.0.1", u.port or 5672, unquote(u.username or "guest"),
+    port = u.port or (5671 if u.scheme == "amqps" else 5672)
+    return (u.hostname or "127.0.0.1", port, unquote(u.username or "guest"),
             unquote(u.password or "guest"), vhost)
+
+
+def is_tls_url(url: str) -> bool:
+    return urlsplit(url).scheme == "amqps"
+
+
+def client_ssl_context(verify: bool = True, ca_file: str = "") -> ssl.SSLContext:
+    """TLS for ``amqps://``: the system trust store plus ``ca_file`` (a private CA, the
+    usual RabbitMQ setup); ``verify=False`` accepts any certificate."""
+    ctx = ssl.create_default_context()
+    if ca_file:
+        ctx.load_verify_locations(cafile=ca_file)
+    if not verify:
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+    return ctx
 
 
 class Message:
@@ -59,6 +88,9 @@ class Channel:
         self._pending_size = 0
         self._pending_body: List[bytes] = []
         self._get_waiter: Optional[asyncio.Future] = None
+        # owner hooks: broker-initiated channel.close / basic.cancel (consumer recovery)
+        self.on_close: Optional[Callable[["Channel", BaseException], None]] = None
+        self.on_cancel: Optional[Callable[["Channel", str], None]] = None
 
     async def rpc(self, method: Tuple[int, int], args: List[Any],
                   expect: Tuple[Tuple[int, int], ...]) -> Tuple[Tuple[int, int], List[Any]]:
@@ -86,12 +118,19 @@ class Channel:
             return
         if m == C.CHANNEL_CLOSE:
             self.closed = True
-            self.conn.send(C.method_frame(self.id, C.CHANNEL_CLOSE_OK))
+            self.conn.channels.pop(self.id, None)
+            try:
+                self.conn.send(C.method_frame(self.id, C.CHANNEL_CLOSE_OK))
+            except ConnectionError:
+                pass
             err = C.AMQPError(f"channel closed by broker: {args[0]} {args[1]}", args[0])
             self._fail(err)
+            if self.on_close is not None:
+                self.on_close(self, err)
             return
-        if m == C.BASIC_CANCEL:  # broker-side cancel (queue deleted)
-            self.consumers.pop(args[0], None)
+        if m == C.BASIC_CANCEL:  # broker-side cancel (queue deleted, HA failover)
+            if self.consumers.pop(args[0], None) is not None and self.on_cancel is not None:
+                self.on_cancel(self, args[0])
             return
         if m == C.BASIC_GET_EMPTY and self._get_waiter is not None:
             if not self._get_waiter.done():
@@ -239,8 +278,12 @@ class Channel:
 
 class Connection:
     def __init__(self, url: str, heartbeat: int = 30, frame_max: int = 131072,
-                 rpc_timeout: float = 30.0, connect_timeout: float = 10.0):
+                 rpc_timeout: float = 30.0, connect_timeout: float = 10.0,
+                 ssl_context: Optional[ssl.SSLContext] = None):
         self.host, self.port, self.user, self.password, self.vhost = parse_url(url)
+        self.ssl_context = ssl_context
+        if self.ssl_context is None and is_tls_url(url):
+            self.ssl_context = client_ssl_context()
         self.heartbeat = heartbeat
         self.frame_max = frame_max
         self.rpc_timeout = rpc_timeout
@@ -271,8 +314,10 @@ class Connection:
             await self.writer.drain()
 
     async def connect(self) -> "Connection":
+        tls = {} if self.ssl_context is None else {"ssl": self.ssl_context,
+                                                   "server_hostname": self.host}
         self.reader, self.writer = await asyncio.wait_for(
-            asyncio.open_connection(self.host, self.port), self.connect_timeout)
+            asyncio.open_connection(self.host, self.port, **tls), self.connect_timeout)
         self.writer.write(C.PROTOCOL_HEADER)
         m, a = await self._expect_method(C.CONNECTION_START)
         self.server_properties = a[2]
@@ -359,11 +404,18 @@ class Connection:
                 self.writer.close()
 
     async def channel(self) -> Channel:
-        cid = next(self._ids)
+        # lowest free id: a connection that outlives many channel recoveries stays far
+        # below channel_max (2047)
+        cid = next(i for i in itertools.count(1) if i not in self.channels)
         ch = Channel(self, cid)
         self.channels[cid] = ch
         await ch.rpc(C.CHANNEL_OPEN, [""], (C.CHANNEL_OPEN_OK,))
         return ch
+
+    def abort(self) -> None:
+        """Drop the socket: the read loop fails every channel and sets ``closed``."""
+        if self.writer is not None:
+            self.writer.transport.abort()
 
     async def close(self) -> None:
         if self.closed.is_set():
@@ -405,27 +457,36 @@ class _AmqpDelivery(Delivery):
 class AmqpBroker(Broker):
     def __init__(self, url: str, heartbeat: int = 30, reconnect_delay: float = 1.0,
                  max_reconnect_delay: float = 30.0, metrics=None, connect_retry_s: float = 0.0,
-                 publish_retry_s: float = 120.0):
+                 publish_retry_s: float = 120.0, ssl_context: Optional[ssl.SSLContext] = None,
+                 recover_delay: Optional[float] = None):
         self.url = url
+        self.ssl_context = ssl_context
         self.publish_retry_s = publish_retry_s
         self.connect_retry_s = connect_retry_s
         self.heartbeat = heartbeat
         self.reconnect_delay = reconnect_delay
         self.max_reconnect_delay = max_reconnect_delay
+        # first wait before reopening a broker-closed channel / re-consuming a cancelled
+        # consumer (doubles on failure, capped at max_reconnect_delay)
+        self.recover_delay = reconnect_delay if recover_delay is None else recover_delay
         self.metrics = metrics
         self.conn: Optional[Connection] = None
         self._cons_ch: Optional[Channel] = None
         self._pub_ch: Optional[Channel] = None
-        self._declared: set = set()
+        self._declared: Dict[str, Dict[str, Any]] = {}     # queue -> x-arguments
         self._consumers: Dict[str, Tuple[str, Handler, int]] = {}
-        self._ctags: Dict[str, str] = {}    # our tag -> broker tag (current connection)
+        self._ctags: Dict[str, str] = {}    # our tag -> broker tag (current consumer channel)
         self._ids = itertools.count(1)
         self._gen = 0
         self._lock = asyncio.Lock()
         self._closing = False
         self._watch: Optional[asyncio.Task] = None
+        self._tasks: set = set()
+        self._recovering = False
         self.connected = False
         self.reconnects = 0
+        self.channel_recoveries = 0
+        self.resubscribes = 0
 
     async def connect(self) -> None:
         deadline = asyncio.get_running_loop().time() + self.connect_retry_s
@@ -445,17 +506,120 @@ class AmqpBroker(Broker):
                 delay = min(self.max_reconnect_delay, delay * 2)
         self._watch = asyncio.get_running_loop().create_task(self._watchdog())
 
+    def _spawn(self, coro) -> None:
+        t = asyncio.get_running_loop().create_task(coro)
+        self._tasks.add(t)
+        t.add_done_callback(self._tasks.discard)
+
     async def _open(self) -> None:
-        self.conn = await Connection(self.url, self.heartbeat).connect()
-        self._cons_ch = await self.conn.channel()
-        self._pub_ch = await self.conn.channel()
-        await self._pub_ch.confirm_select()
+        self.connected = False
+        self.conn = await Connection(self.url, self.heartbeat,
+                                     ssl_context=self.ssl_context).connect()
         self._gen += 1
-        for q in list(self._declared):
-            await self._cons_ch.queue_declare(q)
+        self._ctags.clear()
+        await self._setup_publisher()
+        await self._setup_consumer()
+        self.connected = True
+
+    async def _setup_publisher(self) -> None:
+        ch = await self.conn.channel()
+        ch.on_close = self._on_channel_close
+        await ch.confirm_select()
+        self._pub_ch = ch
+
+    async def _setup_consumer(self) -> None:
+        """Open the consumer channel and re-run the topology: every declared queue, then
+        every registered consumer (amqp-connection-manager's ``setup`` callback)."""
+        self._ctags.clear()
+        ch = await self.conn.channel()
+        ch.on_close = self._on_channel_close
+        ch.on_cancel = self._on_consumer_cancel
+        self._cons_ch = ch
+        for q, args in list(self._declared.items()):
+            await ch.queue_declare(q, arguments=args)
         for tag, (q, handler, prefetch) in list(self._consumers.items()):
             await self._subscribe(tag, q, handler, prefetch)
-        self.connected = True
+
+    # ------------------------------------------------------------ channel-level recovery
+    def _on_channel_close(self, ch: Channel, err: BaseException) -> None:
+        if self._closing or ch.conn is not self.conn or ch.conn.closed.is_set():
+            return                                  # connection loss: the watchdog's job
+        if ch is self._cons_ch:
+            self._ctags.clear()                     # the broker cancelled them with the channel
+        if not self._recovering:
+            self._recovering = True
+            self._spawn(self._recover_channels())
+
+    async def _recover_channels(self) -> None:
+        delay = self.recover_delay
+        try:
+            while not self._closing:
+                await asyncio.sleep(delay)
+                conn = self.conn
+                if conn is None or conn.closed.is_set():
+                    return                          # the watchdog reconnects and re-runs setup
+                try:
+                    async with self._lock:
+                        if conn is not self.conn:
+                            return
+                        if self._pub_ch is None or self._pub_ch.closed:
+                            await self._setup_publisher()
+                        if self._cons_ch is None or self._cons_ch.closed:
+                            await self._setup_consumer()
+                    self.channel_recoveries += 1
+                    if self.metrics is not None:
+                        self.metrics.messages.labels("*", "channel_recover").inc()
+                    return
+                except (C.AMQPError, asyncio.TimeoutError) as e:
+                    # setup refused on a live connection (e.g. a 406 on re-declare): retry a
+                    # few times, then let the watchdog start from a fresh connection
+                    if delay >= self.max_reconnect_delay or isinstance(e, asyncio.TimeoutError):
+                        conn.abort()
+                        return
+                    delay = min(self.max_reconnect_delay, delay * 2)
+                except (OSError, ConnectionError):
+                    return
+        finally:
+            self._recovering = False
+
+    def _on_consumer_cancel(self, ch: Channel, btag: str) -> None:
+        """Broker-side ``basic.cancel``: the queue went away (deleted, failover). Re-declare
+        it and consume again, as amqp-connection-manager's setup re-run does."""
+        for tag, b in list(self._ctags.items()):
+            if b == btag:
+                del self._ctags[tag]
+                if not self._closing and tag in self._consumers:
+                    self._spawn(self._resubscribe(tag, ch))
+
+    async def _resubscribe(self, tag: str, ch: Channel) -> None:
+        delay = self.recover_delay
+        while not self._closing:
+            await asyncio.sleep(delay)
+            try:
+                async with self._lock:
+                    ent = self._consumers.get(tag)
+                    if (ent is None or tag in self._ctags or not self.connected
+                            or self._cons_ch is not ch or ch.closed):
+                        return                  # cancelled, or a channel/connection setup ran
+                    await self._subscribe(tag, *ent)
+                self.resubscribes += 1
+                if self.metrics is not None:
+                    self.metrics.messages.labels(ent[0], "resubscribe").inc()
+                return
+            except (C.AMQPError, asyncio.TimeoutError, OSError, ConnectionError):
+                delay = min(self.max_reconnect_delay, delay * 2)
+
+    def consumer_live(self, consumer_tag: Optional[str] = None) -> bool:
+        """True while the broker holds a subscription for ``consumer_tag`` (every registered
+        consumer when None) on the live consumer channel - what ``/readyz`` reports. A
+        connected client whose consumer was cancelled or whose channel was closed by the
+        broker receives nothing and must not look ready."""
+        if not self.connected or self.conn is None or self.conn.closed.is_set():
+            return False
+        if self._cons_ch is None or self._cons_ch.closed:
+            return False
+        tags = [consumer_tag] if consumer_tag is not None else list(self._consumers)
+        return all(t in self._ctags and self._ctags[t] in self._cons_ch.consumers for t in tags)
 
     async def _watchdog(self) -> None:
         delay = self.reconnect_delay
@@ -473,13 +637,21 @@ class AmqpBroker(Broker):
                     delay = self.reconnect_delay
                     break
                 except (OSError, C.AMQPError, asyncio.TimeoutError, ConnectionError):
+                    if self.conn is not None:
+                        self.conn.abort()
                     delay = min(self.max_reconnect_delay, delay * 2)
 
-    async def _ready(self) -> None:
-        for _ in range(int(max(1.0, self.max_reconnect_delay) * 20)):
-            if self.connected and self.conn is not None and not self.conn.closed.is_set():
+    def _usable(self) -> bool:
+        return (self.connected and self.conn is not None and not self.conn.closed.is_set()
+                and self._pub_ch is not None and not self._pub_ch.closed)
+
+    async def _ready(self, timeout: Optional[float] = None) -> None:
+        loop = asyncio.get_running_loop()
+        end = loop.time() + (max(1.0, self.max_reconnect_delay) if timeout is None else timeout)
+        while True:
+            if self._usable():
                 return
-            if self._closing:
+            if self._closing or loop.time() >= end:
                 break
             await asyncio.sleep(0.05)
         raise ConnectionError("AMQP broker not connected")
@@ -488,41 +660,59 @@ class AmqpBroker(Broker):
         self._closing = True
         if self._watch is not None:
             self._watch.cancel()
+        for t in list(self._tasks):
+            t.cancel()
         if self.conn is not None:
             await self.conn.close()
         self.connected = False
 
-    async def declare(self, queue: str) -> None:
-        self._declared.add(queue)
+    async def declare(self, queue: str, arguments: Optional[Dict[str, Any]] = None) -> None:
+        self._declared[queue] = dict(arguments or {})
         await self._ready()
-        await self._cons_ch.queue_declare(queue)
+        await self._cons_ch.queue_declare(queue, arguments=arguments)
 
     async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
                       confirm: bool = True) -> None:
         """Publish (with a broker confirm unless ``confirm=False``). A connection lost before
         the confirm arrives is not an error: the message is sent again once the watchdog has
         reconnected, as amqp-connection-manager's ChannelWrapper does - at-least-once, so a
-        consumer may see it twice. Channel-level refusals on a live connection still raise,
+        consumer may see it twice. A publisher channel closed by the broker is reopened and
+        the publish retried the same way. Refusals on a live channel (a nack) still raise,
         and so does a broker that stays away for ``publish_retry_s``."""
         props = C.Properties(content_type="application/octet-stream", delivery_mode=2,
                              headers=_to_headers(headers))
         loop = asyncio.get_running_loop()
         deadline = loop.time() + self.publish_retry_s
         while True:
-            await self._ready()
-            conn = self.conn
+            conn, ch = self.conn, self._pub_ch
             try:
-                await self._pub_ch.basic_publish("", queue, body, props, wait_confirm=confirm)
+                await self._ready(max(0.05, deadline - loop.time()))
+                conn, ch = self.conn, self._pub_ch
+                await ch.basic_publish("", queue, body, props, wait_confirm=confirm)
                 break
-            except Exception:   # reset, EOF mid-frame, timeout, channel failure...
-                lost = conn is None or conn.closed.is_set() or conn is not self.conn
+            except Exception:   # reset, EOF mid-frame, timeout, channel failure, not ready...
+                lost = (conn is None or conn.closed.is_set() or conn is not self.conn
+                        or ch is None or ch.closed)
                 if not lost or self._closing or loop.time() > deadline:
                     raise
                 if self.metrics is not None:
                     self.metrics.messages.labels(queue, "republish").inc()
-                await asyncio.sleep(0.02)   # the watchdog is reconnecting; _ready() waits
+                await asyncio.sleep(0.02)   # watchdog / channel recovery in progress
         if self.metrics is not None:
             self.metrics.messages.labels(queue, "publish").inc()
+
+    async def publish_delayed(self, queue: str, body: bytes, headers: Optional[Headers],
+                              delay_s: float) -> None:
+        """Deliver to ``queue`` after ``delay_s`` without holding anything in this process:
+        publish to a per-delay holding queue whose ``x-message-ttl`` dead-letters the
+        message back to ``queue`` through the default exchange (RabbitMQ's delayed-retry
+        idiom; one queue per distinct delay, so no head-of-line blocking)."""
+        ms = max(1, int(delay_s * 1000))
+        hold = f"{queue}.delay.{ms}"
+        if hold not in self._declared:
+            await self.declare(hold, {"x-message-ttl": ms, "x-dead-letter-exchange": "",
+                                      "x-dead-letter-routing-key": queue})
+        await self.publish(hold, body, headers)
 
     async def _subscribe(self, tag: str, queue: str, handler: Handler, prefetch: int) -> None:
         gen = self._gen
@@ -535,22 +725,25 @@ class AmqpBroker(Broker):
                 if not d.settled:
                     await d.nack(requeue=True)
 
-        await self._cons_ch.queue_declare(queue)
-        await self._cons_ch.basic_qos(prefetch)
-        self._ctags[tag] = await self._cons_ch.basic_consume(queue, on_msg)
+        ch = self._cons_ch
+        await ch.queue_declare(queue, arguments=self._declared.get(queue))
+        await ch.basic_qos(prefetch)
+        self._ctags[tag] = await ch.basic_consume(queue, on_msg)
 
     async def consume(self, queue: str, handler: Handler, prefetch: int = 1) -> str:
         await self._ready()
         tag = f"amqp-ctag-{next(self._ids)}"
         self._consumers[tag] = (queue, handler, prefetch)
-        self._declared.add(queue)
-        await self._subscribe(tag, queue, handler, prefetch)
+        self._declared.setdefault(queue, {})
+        async with self._lock:
+            if tag not in self._ctags:          # a reconnect under the lock may have done it
+                await self._subscribe(tag, queue, handler, prefetch)
         return tag
 
     async def cancel(self, consumer_tag: str) -> None:
         self._consumers.pop(consumer_tag, None)
         btag = self._ctags.pop(consumer_tag, None)
-        if btag and self.connected:
+        if btag and self.connected and self._cons_ch is not None and not self._cons_ch.closed:
             try:
                 await self._cons_ch.basic_cancel(btag)
             except Exception:
@@ -565,5 +758,5 @@ class AmqpBroker(Broker):
 
     async def queue_size(self, queue: str) -> int:
         await self._ready()
-        _, n, _ = await self._cons_ch.queue_declare(queue)
+        _, n, _ = await self._cons_ch.queue_declare(queue, arguments=self._declared.get(queue))
         return n

@@ -64,7 +64,9 @@ class Broker(abc.ABC):
     async def close(self) -> None: ...
 
     @abc.abstractmethod
-    async def declare(self, queue: str) -> None: ...
+    async def declare(self, queue: str, arguments: Optional[Dict[str, Any]] = None) -> None:
+        """Declare ``queue`` (idempotent). ``arguments``: RabbitMQ x-arguments, e.g.
+        ``x-message-ttl`` / ``x-dead-letter-exchange`` / ``x-dead-letter-routing-key``."""
 
     @abc.abstractmethod
     async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
@@ -87,6 +89,17 @@ class Broker(abc.ABC):
     async def queue_size(self, queue: str) -> int:
         raise NotImplementedError
 
+    async def publish_delayed(self, queue: str, body: bytes, headers: Optional[Headers],
+                              delay_s: float) -> None:
+        """Publish ``body`` so that it reaches ``queue`` after ``delay_s`` seconds, without
+        the caller holding a delivery (or a prefetch slot) while it waits."""
+        raise NotImplementedError
+
+    def consumer_live(self, consumer_tag: Optional[str] = None) -> bool:
+        """True while ``consumer_tag`` (all consumers when None) is subscribed at the broker
+        and can receive deliveries. ``/readyz`` reports it."""
+        return self.connected
+
     # Reference-style aliases -----------------------------------------------------------
     async def listen(self, queue: str, fn: Handler, prefetch: int = 1) -> str:
         return await self.consume(queue, fn, prefetch)
@@ -97,8 +110,12 @@ def make_broker(cfg, metrics=None) -> Broker:
     if cfg.broker.backend == "memory":
         from .memory import MemoryBroker
         return MemoryBroker.shared()
-    from .amqp import AmqpBroker
+    from .amqp import AmqpBroker, client_ssl_context, is_tls_url
     url = cfg.broker.url or dyn("rabbitmq")
+    ctx = None
+    if is_tls_url(url):     # amqps://: the same trust settings as every other TLS peer
+        ctx = client_ssl_context(cfg.tls.verify, cfg.broker.ca_file or cfg.tls.ca_file)
     return AmqpBroker(url, heartbeat=cfg.broker.heartbeat_s,
                       reconnect_delay=cfg.broker.reconnect_delay_s, metrics=metrics,
-                      connect_retry_s=cfg.broker.connect_retry_s)
+                      connect_retry_s=cfg.broker.connect_retry_s, ssl_context=ctx,
+                      recover_delay=cfg.broker.recover_delay_s)

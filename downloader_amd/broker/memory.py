@@ -57,6 +57,8 @@ class MemoryBroker(Broker):
         self._tasks: set = set()
         self.connected = False
         self.fail_publish: int = 0  # fault injection: fail the next N publishes
+        self.delayed = 0            # publish_delayed messages not yet due
+        self._timers: set = set()
 
     @classmethod
     def shared(cls) -> "MemoryBroker":
@@ -72,10 +74,31 @@ class MemoryBroker(Broker):
             await self.cancel(tag)
         for t in list(self._tasks):
             t.cancel()
+        for h in list(self._timers):
+            h.cancel()
+        self._timers.clear()
         self.connected = False
 
-    async def declare(self, queue: str) -> None:
+    async def declare(self, queue: str, arguments: Optional[Dict] = None) -> None:
         self.queues.setdefault(queue, deque())
+
+    async def publish_delayed(self, queue: str, body: bytes, headers: Optional[Headers],
+                              delay_s: float) -> None:
+        """The delay lives in the event loop (what a TTL holding queue does at a broker)."""
+        loop = asyncio.get_running_loop()
+        self.delayed += 1
+
+        def fire() -> None:
+            self.delayed -= 1
+            t = loop.create_task(self.publish(queue, body, headers))
+            self._tasks.add(t)
+            t.add_done_callback(self._tasks.discard)
+        self._timers.add(loop.call_later(max(0.0, delay_s), fire))
+
+    def consumer_live(self, consumer_tag: Optional[str] = None) -> bool:
+        if not self.connected:
+            return False
+        return consumer_tag is None or consumer_tag in self.consumers
 
     async def publish(self, queue: str, body: bytes, headers: Optional[Headers] = None,
                       confirm: bool = True) -> None:

@@ -7,12 +7,24 @@ with RabbitMQ's delivery semantics: round-robin dispatch bounded by prefetch, un
 messages requeued at the head with ``redelivered`` set when their channel or connection goes
 away. Queues are in memory.
 
+RabbitMQ behaviours the worker has to survive are reproduced too:
+  * ``consumer_timeout`` - a channel holding a delivery unacked for longer is closed with
+    406 PRECONDITION_FAILED (its deliveries requeued), as RabbitMQ >= 3.8.15 does;
+  * ``queue.delete`` sends ``basic.cancel`` to the queue's consumers (consumer_cancel_notify);
+  * ``x-message-ttl`` + ``x-dead-letter-exchange`` / ``x-dead-letter-routing-key`` queue
+    arguments (expired messages are dead-lettered with an ``x-death`` header) - the
+    delayed-retry holding queues;
+  * TLS listeners (``amqps://``) when given an ``ssl.SSLContext``.
+
 Run standalone: ``python -m downloader_amd broker --port 5672``.
 """
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import itertools
+import ssl
+import time
 from collections import deque
 from dataclasses import dataclass, field
 from typing import Deque, Dict, List, Optional, Tuple
@@ -25,6 +37,7 @@ class _Msg:
     body: bytes
     props: C.Properties
     redelivered: bool = False
+    expires: float = 0.0        # monotonic deadline in a TTL queue (0: none)
 
 
 @dataclass
@@ -44,6 +57,9 @@ class _Queue:
     rr: int = 0
     published: int = 0
     delivered: int = 0
+    args: Dict = field(default_factory=dict)
+    expired: int = 0
+    timer: Optional[asyncio.TimerHandle] = None
 
 
 class _Chan:
@@ -52,7 +68,8 @@ class _Chan:
         self.id = cid
         self.prefetch = 0
         self.consumers: Dict[str, _Consumer] = {}
-        self.unacked: Dict[int, Tuple[str, _Msg, Optional[_Consumer]]] = {}
+        # delivery tag -> (queue, message, consumer, monotonic time of delivery)
+        self.unacked: Dict[int, Tuple[str, _Msg, Optional[_Consumer], float]] = {}
         self.dtags = itertools.count(1)
         self.confirming = False
         self.pub_seq = 0
@@ -80,9 +97,16 @@ class _Conn:
 
 class BrokerServer:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, users: Optional[Dict[str, str]] = None,
-                 heartbeat: int = 60, frame_max: int = 131072):
+                 heartbeat: int = 60, frame_max: int = 131072,
+                 consumer_timeout: float = 0.0, ssl_context: Optional[ssl.SSLContext] = None):
         self.host = host
         self.port = port
+        # seconds a delivery may stay unacked before its channel is closed (0: never;
+        # RabbitMQ's default is 30 min)
+        self.consumer_timeout = consumer_timeout
+        self.ssl_context = ssl_context
+        self.timeouts = 0           # channels closed by consumer_timeout
+        self._reaper: Optional[asyncio.Task] = None
         self.users = users if users is not None else {"guest": "guest"}
         self.heartbeat = heartbeat
         self.frame_max = frame_max
@@ -93,15 +117,23 @@ class BrokerServer:
 
     @property
     def url(self) -> str:
-        return f"amqp://guest:guest@{self.host}:{self.port}/"
+        scheme = "amqps" if self.ssl_context is not None else "amqp"
+        return f"{scheme}://guest:guest@{self.host}:{self.port}/"
 
     async def start(self) -> "BrokerServer":
         self._server = await asyncio.start_server(self._handle, self.host, self.port,
-                                                  reuse_address=True)
+                                                  reuse_address=True, ssl=self.ssl_context)
         self.port = self._server.sockets[0].getsockname()[1]
+        if self.consumer_timeout > 0:
+            self._reaper = asyncio.get_running_loop().create_task(self._timeout_loop())
         return self
 
     async def stop(self) -> None:
+        if self._reaper is not None:
+            self._reaper.cancel()
+        for q in self.queues.values():
+            if q.timer is not None:
+                q.timer.cancel()
         if self._server is not None:
             self._server.close()
         for c in list(self.conns):
@@ -123,6 +155,48 @@ class BrokerServer:
     def depth(self, queue: str) -> int:
         q = self.queues.get(queue)
         return len(q.msgs) if q else 0
+
+    def consumers(self, queue: str) -> int:
+        q = self.queues.get(queue)
+        return len(q.consumers) if q else 0
+
+    def delete_queue(self, queue: str) -> int:
+        """Admin-side delete (rabbitmqctl delete_queue): consumers get ``basic.cancel``."""
+        q = self.queues.pop(queue, None)
+        if q is None:
+            return 0
+        if q.timer is not None:
+            q.timer.cancel()
+        for c in q.consumers:
+            c.chan.consumers.pop(c.tag, None)
+            c.chan.conn.send(C.method_frame(c.chan.id, C.BASIC_CANCEL, c.tag, False))
+        return len(q.msgs)
+
+    def close_consumer_channels(self, queue: str, code: int = 320,
+                                text: str = "CONNECTION_FORCED - channel closed by operator") -> int:
+        """Fault injection: the broker closes every channel consuming ``queue``."""
+        q = self.queues.get(queue)
+        chans = {id(c.chan): c.chan for c in (q.consumers if q else [])}
+        for ch in chans.values():
+            self._chan_error(ch, code, text, (0, 0))
+        return len(chans)
+
+    async def _timeout_loop(self) -> None:
+        """RabbitMQ's consumer_timeout: a channel with a delivery unacked for longer than
+        the limit is closed with 406 and its deliveries are requeued."""
+        period = max(0.02, min(1.0, self.consumer_timeout / 4))
+        while True:
+            await asyncio.sleep(period)
+            now = time.monotonic()
+            for conn in list(self.conns):
+                for ch in list(conn.chans.values()):
+                    if any(now - ent[3] > self.consumer_timeout
+                           for ent in ch.unacked.values() if ent[2] is not None):
+                        self.timeouts += 1
+                        ms = int(self.consumer_timeout * 1000)
+                        self._chan_error(ch, 406, "PRECONDITION_FAILED - delivery acknowledgement "
+                                         f"on channel {ch.id} timed out. Timeout value used: "
+                                         f"{ms} ms", (0, 0))
 
     # ---------------------------------------------------------------- connection handling
     async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
@@ -248,7 +322,7 @@ class BrokerServer:
                 if passive:
                     self._chan_error(ch, 404, f"NOT_FOUND - no queue '{name}'", m)
                     return
-                q = self.queues[name] = _Queue(name)
+                q = self.queues[name] = _Queue(name, args=dict(a[7] or {}))
             if not a[6]:
                 conn.send(C.method_frame(cid, C.QUEUE_DECLARE_OK, name, len(q.msgs), len(q.consumers)))
         elif m == C.QUEUE_PURGE:
@@ -258,12 +332,7 @@ class BrokerServer:
                 q.msgs.clear()
             conn.send(C.method_frame(cid, C.QUEUE_PURGE_OK, n))
         elif m == C.QUEUE_DELETE:
-            q = self.queues.pop(a[1], None)
-            n = len(q.msgs) if q else 0
-            if q:
-                for c in q.consumers:
-                    c.chan.consumers.pop(c.tag, None)
-                    c.chan.conn.send(C.method_frame(c.chan.id, C.BASIC_CANCEL, c.tag, False))
+            n = self.delete_queue(a[1])
             conn.send(C.method_frame(cid, C.QUEUE_DELETE_OK, n))
         elif m == C.BASIC_QOS:
             ch.prefetch = a[1]
@@ -300,7 +369,7 @@ class BrokerServer:
             msg = q.msgs.popleft()
             tag = next(ch.dtags)
             if not a[2]:
-                ch.unacked[tag] = (q.name, msg, None)
+                ch.unacked[tag] = (q.name, msg, None, time.monotonic())
             conn.send(C.content_frames(cid, C.method_frame(cid, C.BASIC_GET_OK, tag, msg.redelivered,
                                                            "", q.name, len(q.msgs)),
                                        msg.body, msg.props, conn.frame_max))
@@ -327,14 +396,49 @@ class BrokerServer:
         ch.pending = None
         ch.pending_body = []
         if exchange == "":
-            q = self.queues.get(rkey)
-            if q is not None:
-                q.msgs.append(_Msg(body, props))
-                q.published += 1
-                self._dispatch(q)
+            self._enqueue(rkey, _Msg(body, props))
         if ch.confirming:
             ch.pub_seq += 1
             ch.conn.send(C.method_frame(ch.id, C.BASIC_ACK, ch.pub_seq, False))
+
+    def _enqueue(self, qname: str, msg: _Msg) -> None:
+        q = self.queues.get(qname)
+        if q is None:
+            return                              # unroutable on the default exchange: dropped
+        ttl = q.args.get("x-message-ttl")
+        if isinstance(ttl, int) and ttl >= 0:
+            msg.expires = time.monotonic() + ttl / 1000.0
+        q.msgs.append(msg)
+        q.published += 1
+        self._dispatch(q)
+        self._arm_expiry(q)
+
+    def _arm_expiry(self, q: _Queue) -> None:
+        if q.timer is not None or not q.msgs or not q.msgs[0].expires:
+            return
+        delay = max(0.0, q.msgs[0].expires - time.monotonic())
+        q.timer = asyncio.get_running_loop().call_later(delay, self._expire, q)
+
+    def _expire(self, q: _Queue) -> None:
+        """Dead-letter expired messages from the head (RabbitMQ expires at the head only)."""
+        q.timer = None
+        now = time.monotonic()
+        while q.msgs and q.msgs[0].expires and q.msgs[0].expires <= now:
+            msg = q.msgs.popleft()
+            q.expired += 1
+            if "x-dead-letter-exchange" not in q.args:
+                continue                        # no DLX: expired messages are dropped
+            rkey = q.args.get("x-dead-letter-routing-key") or q.name
+            hdrs = dict(msg.props.headers or {})
+            deaths = list(hdrs.get("x-death") or [])
+            deaths.insert(0, {"queue": q.name, "reason": "expired", "count": 1,
+                              "exchange": "", "routing-keys": [q.name]})
+            hdrs["x-death"] = deaths
+            props = dataclasses.replace(msg.props, headers=hdrs)
+            if q.args.get("x-dead-letter-exchange", "") == "":
+                self._enqueue(rkey, _Msg(msg.body, props))
+        if q.name in self.queues:
+            self._arm_expiry(q)
 
     def _dispatch(self, q: _Queue) -> None:
         while q.msgs and q.consumers:
@@ -351,7 +455,7 @@ class BrokerServer:
             msg = q.msgs.popleft()
             ch = target.chan
             tag = next(ch.dtags)
-            ch.unacked[tag] = (q.name, msg, target)
+            ch.unacked[tag] = (q.name, msg, target, time.monotonic())
             target.unacked += 1
             q.delivered += 1
             ch.conn.send(C.content_frames(
@@ -365,7 +469,7 @@ class BrokerServer:
             ent = ch.unacked.pop(t, None)
             if ent is None:
                 continue
-            qname, msg, cons = ent
+            qname, msg, cons, _ = ent
             if cons is not None:
                 cons.unacked -= 1
             q = self.queues.get(qname)
@@ -394,8 +498,13 @@ class BrokerServer:
         ch.conn.chans.pop(ch.id, None)
 
 
-async def run_broker(host: str = "0.0.0.0", port: int = 5672) -> None:
-    srv = BrokerServer(host, port)
+async def run_broker(host: str = "0.0.0.0", port: int = 5672, consumer_timeout: float = 0.0,
+                     certfile: str = "", keyfile: str = "") -> None:
+    ctx = None
+    if certfile:
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.load_cert_chain(certfile, keyfile or None)
+    srv = BrokerServer(host, port, consumer_timeout=consumer_timeout, ssl_context=ctx)
     await srv.start()
     print(f"broker listening on {host}:{srv.port}", flush=True)
     while True:

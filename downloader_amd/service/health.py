@@ -3,7 +3,7 @@
 ``GET /health`` keeps the reference contract: 500 ``{"message":"Not Running Jobs"}`` when idle
 (App. A #9, switchable with ``health.legacy_idle_500``), otherwise 200 ``{"metadata":
 {"success": true, "host": <hostname>}, "data": {"active": n}}``. Added: ``/healthz`` (liveness),
-``/readyz`` (broker connected and not draining) and ``/metrics`` (Prometheus exposition).
+``/readyz`` (broker connected, download consumer live, not draining) and ``/metrics`` (Prometheus exposition).
 """
 from __future__ import annotations
 
@@ -45,8 +45,16 @@ class HealthServer:
         return web.json_response({"ok": True})
 
     async def _readyz(self, req: web.Request) -> web.Response:
-        ready = getattr(self.worker.broker, "connected", False) and not self.worker._stopping
-        return web.json_response({"ready": bool(ready)}, status=200 if ready else 503)
+        """Ready = the broker connection is up AND the ``v1.download`` consumer is subscribed
+        at the broker (a consumer cancelled by the broker, or whose channel the broker
+        closed, receives nothing while the connection looks healthy) AND not draining."""
+        b = self.worker.broker
+        connected = bool(getattr(b, "connected", False))
+        tag = self.worker._consumer
+        consuming = connected and tag is not None and b.consumer_live(tag)
+        ready = consuming and not self.worker._stopping
+        return web.json_response({"ready": ready, "broker": connected, "consumer": consuming},
+                                 status=200 if ready else 503)
 
     async def _metrics(self, req: web.Request) -> web.Response:
         return web.Response(body=self.worker.metrics.exposition(),

@@ -14,8 +14,10 @@ removes finished jobs (#2), so ``/health`` and shutdown behave.
 
 Retry policy (``broker.max_retries``, reference AMQP arg ``2`` INFERRED): a failed job is
 re-published with ``x-attempt`` + 1 after exponential backoff, then dead-lettered to
-``broker.dead_letter_queue`` when the budget is spent. ``mode: reference`` uses plain
-``nack(requeue)``.
+``broker.dead_letter_queue`` when the budget is spent. The backoff is held by the broker (a
+TTL holding queue dead-lettering back to ``v1.download``), not by this consumer: the failed
+delivery is acked at once, so its prefetch slot goes to the next job. ``mode: reference``
+uses plain ``nack(requeue)``.
 """
 from __future__ import annotations
 
@@ -309,12 +311,17 @@ class Worker:
             await self._dead_letter(d, err)
             return "dead"
         delay = min(b.retry_backoff_max_s, b.retry_backoff_s * (2 ** attempt))
-        await asyncio.sleep(delay)
         hdrs = dict(d.headers)
         hdrs["x-attempt"] = attempt + 1
         hdrs["x-last-error"] = err[:512]
         try:
-            await self.broker.publish(b.download_queue, d.body, hdrs)
+            if b.retry_delay == "queue":
+                # the broker holds the message for `delay`; this delivery (and its prefetch
+                # slot) is released right away, so healthy jobs never queue behind a backoff
+                await self.broker.publish_delayed(b.download_queue, d.body, hdrs, delay)
+            else:
+                await asyncio.sleep(delay)
+                await self.broker.publish(b.download_queue, d.body, hdrs)
         except Exception:
             await d.nack(requeue=True)
             return "failed"

@@ -96,6 +96,15 @@ class BrokerConfig(BaseModel):
     # first reconnect delay after a lost connection (doubles, max 30 s)
     reconnect_delay_s: float = 1.0
     connect_retry_s: float = 60.0               # keep retrying the first connect this long
+    # first wait before reopening a channel the broker closed (consumer_timeout, 406) or
+    # re-consuming after a broker basic.cancel (queue deleted); doubles, max 30 s
+    recover_delay_s: float = 1.0
+    # failed-job backoff: "queue" = ack now and re-publish through a TTL holding queue that
+    # dead-letters back to download_queue (no prefetch slot held while waiting); "sleep" =
+    # wait inside the consumer, holding the delivery (round-2 behaviour, kept for A/B)
+    retry_delay: Literal["queue", "sleep"] = "queue"
+    # PEM CA bundle for amqps:// (default: tls.ca_file)
+    ca_file: str = ""
 
 
 class TelemetryConfig(BaseModel):

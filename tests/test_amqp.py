@@ -344,3 +344,225 @@ def test_fire_and_forget_publishes_keep_confirms_aligned(run):
         await b.close()
         await srv.stop()
     run(go())
+
+
+# ---------------------------------------------------------------- consumer liveness (round 3)
+async def _readyz(port):
+    import aiohttp
+    async with aiohttp.ClientSession() as s:
+        async with s.get(f"http://127.0.0.1:{port}/readyz") as r:
+            return r.status
+
+
+async def _start_worker(make_cfg, srv, s3_ep, **broker):
+    from downloader_amd.service.worker import Worker
+    b = {"backend": "amqp", "url": srv.url, "reconnect_delay_s": 0.05, "recover_delay_s": 0.4}
+    b.update(broker)
+    cfg = make_cfg(s3_ep, broker=b, health={"enabled": True, "port": 0, "host": "127.0.0.1"})
+    w = Worker(cfg)
+    await w.start()
+    return w
+
+
+async def _wait_status(port, want, timeout=10.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        if await _readyz(port) == want:
+            return True
+        await asyncio.sleep(0.01)
+    return False
+
+
+async def _stage_one(w, client, origin, job_id, timeout=15.0):
+    from downloader_amd.models import api
+    origin.blobs[f"/{job_id}.mkv"] = os.urandom(20_000)
+    await client.publish("v1.download", api.encode(api.make_download(
+        job_id, "http", origin.url(f"/{job_id}.mkv"))))
+    for _ in range(int(timeout / 0.02)):
+        if any(r.job_id == job_id and r.outcome == "staged" for r in w.results):
+            return True
+        await asyncio.sleep(0.02)
+    return False
+
+
+def _liveness_case(run, make_cfg, origin_cls, break_it, server_kw=None, slow_first=False):
+    async def go():
+        from downloader_amd.s3.fake_server import FakeS3
+        srv = await BrokerServer(**(server_kw or {})).start()
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        w = await _start_worker(make_cfg, srv, ep)
+        port = w._health.port
+        client = AmqpBroker(srv.url)
+        await client.connect()
+        assert await _wait_status(port, 200)
+        assert await _stage_one(w, client, origin, "before")
+        await break_it(srv, client, origin, w)
+        # the consumer is gone while the connection stays up: /readyz must say so ...
+        assert await _wait_status(port, 503, 5.0), "readyz never reported the dead consumer"
+        assert w.broker.connected
+        # ... until the worker has re-subscribed by itself
+        assert await _wait_status(port, 200, 10.0), "consumer never recovered"
+        assert srv.consumers("v1.download") == 1
+        assert await _stage_one(w, client, origin, "after"), "next message not consumed"
+        await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()
+    run(go(), timeout=90)
+
+
+def test_consumer_recovers_after_queue_delete_and_redeclare(run, make_cfg, origin_cls):
+    """The verdict's repro: the queue is deleted (broker basic.cancel to its consumers) and
+    re-declared by someone else; the worker must consume again and /readyz flip 503->200."""
+    async def break_it(srv, client, origin, w):
+        srv.delete_queue("v1.download")
+        await client.declare("v1.download")
+    _liveness_case(run, make_cfg, origin_cls, break_it)
+
+
+def test_consumer_recovers_after_server_channel_close(run, make_cfg, origin_cls):
+    async def break_it(srv, client, origin, w):
+        assert srv.close_consumer_channels("v1.download") == 1
+    _liveness_case(run, make_cfg, origin_cls, break_it)
+
+
+def test_consumer_recovers_after_consumer_timeout(run, make_cfg, origin_cls):
+    """RabbitMQ closes a channel whose delivery stays unacked past consumer_timeout (a long
+    torrent). The channel is reopened, the requeued job is redelivered and finishes, and
+    the next message is consumed."""
+    async def break_it(srv, client, origin, w):
+        from downloader_amd.models import api
+        origin.blobs["/long.mkv"] = os.urandom(60_000)
+        origin.slow["/long.mkv"] = 30_000          # ~2 s body: longer than the timeout
+        gets = []
+
+        def hook(method, path):
+            if path == "/long.mkv" and method == "GET":
+                gets.append(1)
+                if len(gets) >= 2:                 # the redelivered copy is fast
+                    origin.slow.pop("/long.mkv", None)
+        origin.hooks.append(hook)
+        await client.publish("v1.download", api.encode(api.make_download(
+            "long", "http", origin.url("/long.mkv"))))
+        for _ in range(300):
+            if srv.timeouts:
+                break
+            await asyncio.sleep(0.02)
+        assert srv.timeouts >= 1
+    _liveness_case(run, make_cfg, origin_cls, break_it, server_kw={"consumer_timeout": 0.6})
+
+
+def test_publish_waits_out_a_long_broker_outage(run):
+    """publish() must keep retrying for publish_retry_s even when the reconnect
+    backoff has grown past max_reconnect_delay (the old _ready() raised after ~that)."""
+    async def go():
+        srv = await BrokerServer().start()
+        port = srv.port
+        b = AmqpBroker(srv.url, reconnect_delay=0.05, max_reconnect_delay=0.2,
+                       publish_retry_s=10.0)
+        await b.connect()
+        await b.declare("o")
+        await srv.stop()
+        for c in list(srv.conns):
+            c.writer.transport.abort()
+
+        async def restart():
+            await asyncio.sleep(1.5)                # > 7 x max_reconnect_delay
+            srv2 = BrokerServer(port=port)
+            await srv2.start()
+            return srv2
+        t = asyncio.ensure_future(restart())
+        await asyncio.wait_for(b.publish("o", b"late"), 8)
+        srv2 = await t
+        assert srv2.depth("o") == 1
+        await b.close(); await srv2.stop()
+    run(go())
+
+
+def test_ttl_queue_dead_letters_back_with_x_death(run):
+    async def go():
+        srv = await BrokerServer().start()
+        b = AmqpBroker(srv.url)
+        await b.connect()
+        await b.declare("work")
+        t0 = asyncio.get_running_loop().time()
+        await b.publish_delayed("work", b"again", {"x-attempt": 1}, 0.3)
+        assert srv.depth("work") == 0 and srv.depth("work.delay.300") == 1
+        d = None
+        for _ in range(100):
+            d = await b.get("work")
+            if d is not None:
+                break
+            await asyncio.sleep(0.02)
+        assert d is not None and d.body == b"again"
+        assert asyncio.get_running_loop().time() - t0 >= 0.28
+        assert d.headers["x-attempt"] == 1
+        assert d.headers["x-death"][0]["queue"] == "work.delay.300"
+        await d.ack()
+        await b.close(); await srv.stop()
+    run(go())
+
+
+def test_retry_backoff_does_not_hold_a_prefetch_slot(run, make_cfg, origin_cls):
+    """A failing job backs off in the broker's holding queue, not in the consumer: with one
+    prefetch slot and a 3 s backoff, a healthy job published after it is staged at once."""
+    async def go():
+        from downloader_amd.models import api
+        from downloader_amd.s3.fake_server import FakeS3
+        from downloader_amd.service.worker import Worker
+        srv = await BrokerServer().start()
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        origin.fail_status["/bad.mkv"] = 500
+        origin.blobs["/good.mkv"] = os.urandom(10_000)
+        cfg = make_cfg(ep, concurrency=1, broker={"backend": "amqp", "url": srv.url,
+                                                  "retry_backoff_s": 3.0, "prefetch": 1})
+        w = Worker(cfg)
+        await w.start(health=False)
+        client = AmqpBroker(srv.url)
+        await client.connect()
+        await client.publish("v1.download", api.encode(api.make_download("bad", "http",
+                                                                          origin.url("/bad.mkv"))))
+        await client.publish("v1.download", api.encode(api.make_download("good", "http",
+                                                                          origin.url("/good.mkv"))))
+        t0 = asyncio.get_running_loop().time()
+        for _ in range(200):
+            if any(r.job_id == "good" for r in w.results):
+                break
+            await asyncio.sleep(0.02)
+        took = asyncio.get_running_loop().time() - t0
+        assert [r.outcome for r in w.results if r.job_id == "good"] == ["staged"]
+        assert took < 2.5, took
+        assert [r.outcome for r in w.results if r.job_id == "bad"] == ["retried"]
+        assert srv.depth("v1.download.delay.3000") == 1
+        await client.close(); await w.stop(); await srv.stop(); await s3.stop(); await origin.stop()
+    run(go(), timeout=60)
+
+
+@pytest.mark.skipif(__import__("shutil").which("openssl") is None, reason="needs openssl")
+def test_amqps_round_trip(run, tmp_path):
+    async def go():
+        import ssl as _ssl
+        import subprocess
+        from downloader_amd.broker.amqp import client_ssl_context
+        key, crt = str(tmp_path / "k.pem"), str(tmp_path / "c.pem")
+        subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key,
+                        "-out", crt, "-days", "1", "-subj", "/CN=127.0.0.1",
+                        "-addext", "subjectAltName=IP:127.0.0.1"], check=True, capture_output=True)
+        sctx = _ssl.SSLContext(_ssl.PROTOCOL_TLS_SERVER)
+        sctx.load_cert_chain(crt, key)
+        srv = await BrokerServer(ssl_context=sctx).start()
+        assert srv.url.startswith("amqps://")
+        # untrusted certificate: refused
+        with pytest.raises(_ssl.SSLError):
+            await Connection(srv.url).connect()
+        b = AmqpBroker(srv.url, ssl_context=client_ssl_context(True, crt))
+        await b.connect()
+        await b.declare("s")
+        await b.publish("s", b"secret")
+        d = await b.get("s")
+        assert d.body == b"secret"
+        await d.ack()
+        await b.close(); await srv.stop()
+    run(go())

@@ -6,6 +6,8 @@ from __future__ import annotations
 import asyncio
 import json
 import os
+import shutil
+import ssl
 import subprocess
 import sys
 
@@ -15,14 +17,29 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.slow
-def test_supervisor_two_workers_over_amqp(run, tmp_path, origin_cls):
+@pytest.mark.parametrize("tls", [False, True], ids=["amqp", "amqps"])
+def test_supervisor_two_workers_over_amqp(run, tmp_path, origin_cls, tls):
+    if tls and shutil.which("openssl") is None:
+        pytest.skip("needs the openssl CLI")
+
     async def go():
-        from downloader_amd.broker.amqp import AmqpBroker
+        from downloader_amd.broker.amqp import AmqpBroker, client_ssl_context
         from downloader_amd.broker.server import BrokerServer
         from downloader_amd.models import api, keys
         from downloader_amd.parallel.supervisor import Supervisor, worker_argv
         from downloader_amd.s3.fake_server import FakeS3
-        srv = await BrokerServer().start()
+        sctx, cctx, extra = None, None, {}
+        if tls:     # amqps://: private CA handed to the workers through the config env
+            key, crt = str(tmp_path / "k.pem"), str(tmp_path / "c.pem")
+            subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes",
+                            "-keyout", key, "-out", crt, "-days", "1", "-subj", "/CN=127.0.0.1",
+                            "-addext", "subjectAltName=IP:127.0.0.1"], check=True,
+                           capture_output=True)
+            sctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            sctx.load_cert_chain(crt, key)
+            cctx = client_ssl_context(True, crt)
+            extra = {"STAGER_BROKER__CA_FILE": crt}
+        srv = await BrokerServer(ssl_context=sctx).start()
         s3 = FakeS3()
         ep = await s3.start()
         origin = await origin_cls().start()
@@ -30,10 +47,10 @@ def test_supervisor_two_workers_over_amqp(run, tmp_path, origin_cls):
                    STAGER_BROKER__URL=srv.url, STAGER_BROKER__BACKEND="amqp",
                    STAGER_S3__ENDPOINT=ep, STAGER_INSTANCE__DOWNLOAD_PATH=str(tmp_path / "dl"),
                    STAGER_HEALTH__ENABLED="false", STAGER_DOWNLOAD__TORRENT_ENABLE_DHT="false",
-                   STAGER_CONCURRENCY="1")
+                   STAGER_CONCURRENCY="1", **extra)
         sup = Supervisor(2, worker_argv(), env=env)
         sup.start()
-        client = AmqpBroker(srv.url)
+        client = AmqpBroker(srv.url, ssl_context=cctx)
         await client.connect()
         await client.declare("v1.download")   # unroutable publishes are dropped, like RabbitMQ
         # both worker processes subscribed before the jobs go out (a loaded CI box may start
