@@ -16,8 +16,15 @@ Launch: ``python bench.py`` (N=1) or ``python -m torch.distributed.run --nproc-p
 bench.py --gpus N``. Each rank starts its own native ``blobd`` peer (origin + S3 sink;
 ``--peers shared`` = one on rank 0) and pins itself to its GPU slot's CPU share (the same
 at every N, so the 1/2/4/8 curve is weak scaling of one slot's host resources); ranks
-synchronise over gloo (the workload is host-side: there is no tensor compute). The run fails
-if the S3 peer received fewer bytes than the workers claim to have staged.
+synchronise over gloo (the workload is host-side: there is no tensor compute).
+
+Objects above 64 MiB go as S3 multipart uploads of 64 MiB parts (minio-js' split), so a 100 MB
+job is 2 parts. The run fails unless the S3 peer's own counters, sampled at "go" and after the
+last timed job, show (a) at least as many bytes received as the workers claim to have staged,
+and (b) with ``--sink sample`` (default) / ``verify``, every timed object matched against the
+bytes the origin generated for it (sampled windows / every byte) with zero mismatches. A
+second, same-call run with the round-2 settings (single PUT up to 128 MiB) is reported as
+``single_put_MBps``.
 """
 from __future__ import annotations
 
@@ -63,8 +70,15 @@ def parse() -> argparse.Namespace:
                    help="stream: single-file HTTP jobs relay origin->S3; disk: stage on disk first")
     p.add_argument("--peers", choices=["per-rank", "shared"], default="per-rank",
                    help="one blobd origin+S3 peer per worker, or one shared on rank 0")
-    p.add_argument("--sink", choices=["discard", "checksum"], default="discard",
-                   help="blobd S3 sink: splice bodies to /dev/null, or checksum every byte")
+    p.add_argument("--sink", choices=["sample", "verify", "discard", "checksum"], default="sample",
+                   help="blobd S3 sink: sample = splice bodies to /dev/null but compare a 4 KiB "
+                        "window of every MiB (and each body's tail) with the origin generator's "
+                        "bytes at the object offset; verify = compare every byte (checksum of the "
+                        "body vs checksum of the generated range); discard = no check; checksum "
+                        "= fold every byte, no comparison")
+    p.add_argument("--no-compare-single-put", dest="compare_single_put", action="store_false",
+                   help="skip the same-call comparison run with round-2 settings (objects up to "
+                        "128 MiB in one PUT)")
     p.add_argument("--cpus-per-rank", type=int, default=0,
                    help="pin each rank (worker + its peer) to this many CPUs; 0: its GPU slot's "
                         "share, min(mask, cgroup quota) / visible GPUs; -1: no pinning")
@@ -183,6 +197,8 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
         over["s3"]["secure"] = True
         over["tls"] = {"ca_file": ca, "native": args.tls == "native"}
     if mode == "tuned":
+        if getattr(args, "single_put", False):   # round-2 headline settings, for comparison
+            over["s3"]["multipart_threshold"] = 128 << 20
         if args.http_streams:
             over["download"]["http_streams"] = args.http_streams
         if args.part_mb:
@@ -204,9 +220,14 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
     return worker, url
 
 
+def _tag(args, mode: str) -> str:
+    """Job-id tag of a measurement: each one stages fresh ids (no done-marker skips)."""
+    return mode + ("-1put" if getattr(args, "single_put", False) else "")
+
+
 async def _warmup(args, worker, url, wid: int, mode: str) -> None:
     _, wres = await run_phase(worker, url, wid, 0, args.warmup * args.jobs_per_step,
-                              int(args.size_mb * 1e6), mode)
+                              int(args.size_mb * 1e6), _tag(args, mode))
     bad = [r for r in wres if r.outcome != "staged"]
     if bad:
         raise RuntimeError(f"warmup job failed: {bad[0]}")
@@ -218,7 +239,7 @@ async def _timed(args, worker, url, wid: int, mode: str, count: int) -> dict:
     t0 = time.perf_counter()
     loop_cpu0 = time.thread_time()
     dt, res = await run_phase(worker, url, wid, args.warmup * B, count,
-                              int(args.size_mb * 1e6), mode)
+                              int(args.size_mb * 1e6), _tag(args, mode))
     loop_cpu = time.thread_time() - loop_cpu0
     t1 = time.perf_counter()
     bad = [r for r in res if r.outcome != "staged"]
@@ -228,10 +249,12 @@ async def _timed(args, worker, url, wid: int, mode: str, count: int) -> dict:
             "err": bad[0].error if bad else "", "loop_busy": loop_cpu / max(1e-9, t1 - t0)}
 
 
-async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str):
+async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str, on_go=None):
     worker, url = await _start_worker(args, endpoint, mode, stage_root)
     await _warmup(args, worker, url, dist.rank, mode)
     dist.barrier()
+    if on_go is not None:
+        on_go()                     # sink counters at "go": warmup bytes are not timed bytes
     cuda_sync()
     t0 = time.perf_counter()
     out = await _timed(args, worker, url, dist.rank, mode, args.steps * args.jobs_per_step)
@@ -269,7 +292,7 @@ def _proc_main(conn, args, endpoint: str, mode: str, stage_root: str, wid: int, 
 
 
 def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, nproc: int,
-               cpus: list) -> dict:
+               cpus: list, on_go=None) -> dict:
     """Run a rank as ``nproc`` worker processes (like ``downloader_amd supervisor -n`` does for
     a GPU slot): one asyncio worker saturates its event loop + GIL long before the rank's CPU
     share (two single-process ranks on one 16-CPU box: 82 GB/s vs 55 GB/s for one). Each
@@ -300,6 +323,8 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
         for c in conns:
             recv(c)                           # all warmed up
         dist.barrier()
+        if on_go is not None:
+            on_go()
         cuda_sync()
         t0 = time.perf_counter()
         for c in conns:
@@ -319,18 +344,26 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
             "child_cpu_s": sum(o["worker_cpu_s"] for o in outs)}
 
 
+SINK_KEYS = ("bytes_received", "verify_objects", "verify_bytes", "verify_mismatches",
+             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests")
+
+
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 1,
             cpus: Optional[list] = None):
     stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
-    rx0 = blob.stats()["bytes_received"] if blob is not None else 0
+    at_go: dict = {}
+
+    def on_go() -> None:
+        if blob is not None:
+            at_go.update(blob.stats())
     peer_cpu0 = blob.cpu_seconds() if blob is not None else 0.0
     t = os.times()
     cpu0 = t.user + t.system
     try:
         if nproc > 1:
-            out = rank_procs(args, dist, endpoint, mode, stage_root, nproc, cpus or [])
+            out = rank_procs(args, dist, endpoint, mode, stage_root, nproc, cpus or [], on_go)
         else:
-            out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root))
+            out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root, on_go))
     finally:
         if not args.stage_dir:
             shutil.rmtree(stage_root, ignore_errors=True)
@@ -338,23 +371,38 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
     out["worker_cpu_s"] = t.user + t.system - cpu0 + out.pop("child_cpu_s", 0.0)
     out["peer_cpu_s"] = (blob.cpu_seconds() - peer_cpu0) if blob is not None else 0.0
     dist.barrier()
-    # The S3 peer's own byte counter must cover every byte the workers claim to have staged.
-    out["sink_bytes"] = (blob.stats()["bytes_received"] - rx0) if blob is not None else 0
+    # The S3 peer's own counters, between "go" and the end of the timed jobs (every rank is
+    # past the barrier): bytes it received, objects it matched against the origin generator.
+    end = blob.stats() if blob is not None else {}
+    out["sink"] = {k: int(end.get(k, 0)) - int(at_go.get(k, 0)) for k in SINK_KEYS}
+    out["sink"]["mismatches_total"] = int(end.get("verify_mismatches", 0))
+    out["sink"]["unknown_total"] = int(end.get("verify_unknown", 0))
     allr = dist.gather(out)
     elapsed = max(r["elapsed"] for r in allr)
     total_bytes = sum(r["bytes"] for r in allr)
-    sink = sum(r["sink_bytes"] for r in allr)
+    sink = {k: sum(r["sink"][k] for r in allr) for k in allr[0]["sink"]}
     lats = [x for r in allr for x in r["latencies"]]
     failed = sum(r["failed"] for r in allr)
+    jobs = args.steps * args.jobs_per_step * dist.world
     if failed:
         raise RuntimeError(f"{failed} timed jobs failed: {[r['err'] for r in allr if r['err']][:1]}")
-    if sink < total_bytes:
-        raise RuntimeError(f"S3 peer received {sink} bytes < {total_bytes} claimed staged")
-    gb_all = max(1e-9, sink / 1e9)
+    if sink["bytes_received"] < total_bytes:
+        raise RuntimeError(f"S3 peer received {sink['bytes_received']} bytes in the timed region "
+                           f"< {total_bytes} claimed staged")
+    if args.sink in ("sample", "verify"):
+        if sink["mismatches_total"] or sink["unknown_total"]:
+            raise RuntimeError(f"S3 peer: {sink['mismatches_total']} staged objects differ from "
+                               f"the origin's bytes, {sink['unknown_total']} unmatched")
+        if sink["verify_objects"] < jobs:
+            raise RuntimeError(f"S3 peer checked {sink['verify_objects']} objects in the timed "
+                               f"region < {jobs} timed jobs")
+    gb_all = max(1e-9, sink["bytes_received"] / 1e9)
+    mp = sink["multipart_objects"]
     return {"mbps": total_bytes / elapsed / 1e6, "elapsed": elapsed,
             "p50": statistics.median(lats) if lats else 0.0,
             "p90": sorted(lats)[int(0.9 * (len(lats) - 1))] if lats else 0.0,
-            "bytes": total_bytes, "sink_bytes": sink,
+            "bytes": total_bytes, "sink": sink,
+            "parts_per_object": round(sink["multipart_parts"] / mp, 3) if mp else 1.0,
             "worker_cpu_s_per_GB": sum(r["worker_cpu_s"] for r in allr) / gb_all,
             "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all,
             "loop_busy": max(r["loop_busy"] for r in allr)}
@@ -409,6 +457,11 @@ def main() -> int:
         nproc = 1    # the reference is one serial consumer per container (explicit N: N of them)
     try:
         tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
+        single = None
+        if args.compare_single_put and args.mode == "tuned":
+            args.single_put = True
+            single = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
+            args.single_put = False
         ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
     finally:
         if blob is not None:
@@ -429,7 +482,13 @@ def main() -> int:
             "dtype": "bytes",
             "data": "synthetic random-byte media blobs served by the native blobd origin",
             "p50_job_latency_s": round(tuned["p50"], 4),
-            "s3_peer_bytes_received": tuned["sink_bytes"],
+            # S3 side, counted by the sink itself between "go" and the end of the timed jobs
+            "timed_sink_bytes": tuned["sink"]["bytes_received"],
+            "parts_per_object": tuned["parts_per_object"],
+            "sink": args.sink,
+            "sink_verified_objects": tuned["sink"]["verify_objects"],
+            "sink_verified_bytes": tuned["sink"]["verify_bytes"],
+            "sink_mismatches": tuned["sink"]["mismatches_total"],
             "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
             "event_loop_busy": round(tuned["loop_busy"], 3),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
@@ -451,6 +510,10 @@ def main() -> int:
                 "jobs_timed": n * args.steps * args.jobs_per_step,
             },
         }
+        if single is not None:   # same call, round-2 settings: 100 MB objects in one PUT
+            line["single_put_MBps"] = round(single["mbps"], 2)
+            line["single_put_p50_s"] = round(single["p50"], 4)
+            line["single_put_parts_per_object"] = single["parts_per_object"]
         if ref is not None:
             line["reference_mode_MBps"] = round(ref["mbps"], 2)
             line["reference_mode_p50_s"] = round(ref["p50"], 4)

@@ -29,10 +29,13 @@ class Blobd:
     def __init__(self, keep_bytes: int = 1 << 20, default_size: int = 100_000_000,
                  host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum",
                  tls: Optional[Tuple[str, str]] = None, s3_fail_rate: float = 0.0,
-                 synth_bucket: str = "", synth_objects: Optional[Dict[str, int]] = None):
+                 synth_bucket: str = "", synth_objects: Optional[Dict[str, int]] = None,
+                 s3_corrupt_rate: float = 0.0):
         self.files_root = files_root
         self.tls = tls                  # (cert PEM, key PEM): serve https
         self.s3_fail_rate = s3_fail_rate  # share of object/part PUTs answered 503 SlowDown
+        # share of checksummed PUT bodies with one byte flipped on arrival (-> 400 BadDigest)
+        self.s3_corrupt_rate = s3_corrupt_rate
         self.synth_bucket = synth_bucket  # read-only source bucket of synthetic objects
         self.synth_objects = dict(synth_objects or {})
         self.sink = sink
@@ -53,6 +56,7 @@ class Blobd:
             + ["--sink", self.sink]
             + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else [])
             + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else [])
+            + (["--s3-corrupt-rate", str(self.s3_corrupt_rate)] if self.s3_corrupt_rate else [])
             + (["--synth-bucket", self.synth_bucket, "--synth-manifest",
                 self._manifest(d)] if self.synth_bucket else []),
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)

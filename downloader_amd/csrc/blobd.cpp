@@ -21,6 +21,24 @@
 // checksum (so every byte crosses memory like a real store); objects <= --keep-bytes are
 // kept in memory (done markers, tests), larger ones keep only size + checksum.
 // SigV4 is NOT verified here (the Python FakeS3 does that in the test-suite).
+//
+// --sink picks what happens to large S3 bodies:
+//   checksum  every byte folded into the checksum (default)
+//   discard   spliced socket -> /dev/null, no user-space copy
+//   sample    spliced like discard, but a window of --sample-len bytes every --sample-stride
+//             bytes (plus the body's last window) is read and kept, then compared with the
+//             bytes the origin generator produced for that object once its offset is known
+//   verify    every byte folded into the checksum, compared at completion with the checksum
+//             of the generator's bytes for the same range
+// An S3 object is matched to its origin object through the key the staging service writes,
+// `<id>/original/<base64(basename)>`, and the /media/<basename> requests this process served
+// (size, seed). Multipart parts are checked at CompleteMultipartUpload, when their offsets are
+// known. Counters: verify_objects / verify_bytes / verify_mismatches / verify_unknown.
+//
+// Payload checksums are verified whatever the sink: `x-amz-checksum-crc32c` as a header or as
+// an aws-chunked trailer (`x-amz-trailer`, `Content-Encoding: aws-chunked`), and `Content-MD5`;
+// a mismatch is answered 400 BadDigest and nothing is stored. --s3-corrupt-rate P flips one
+// byte of that share of checksummed bodies on arrival (transit corruption, fault injection).
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -33,8 +51,12 @@
 #include <unistd.h>
 
 #include <openssl/err.h>
+#include <openssl/evp.h>
 #include <openssl/ssl.h>
 
+#include "crc32c.h"
+
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <cinttypes>
@@ -58,9 +80,23 @@ struct Object {
   std::string etag;
 };
 
+// Sampled window of a body: bytes [pos, pos + bytes.size()) of the PUT payload.
+struct Sample {
+  uint64_t pos;
+  std::string bytes;
+};
+
+// What the sample / verify sinks keep of one PUT body until its object offset is known.
+struct BodyCheck {
+  uint64_t len = 0;
+  uint64_t sum = 0;              // verify: checksum of every byte
+  std::vector<Sample> windows;   // sample
+};
+
 struct Upload {
   std::string bucket, key;
   std::map<int, Object> parts;
+  std::map<int, BodyCheck> checks;
 };
 
 std::mutex g_mu;
@@ -70,7 +106,16 @@ std::unordered_map<std::string, int> g_fail_counts;
 std::atomic<uint64_t> g_rx{0}, g_tx{0}, g_reqs{0}, g_objects{0}, g_upload_seq{1};
 std::vector<uint8_t> g_pool;  // random pool the origin serves from
 size_t g_keep_bytes = 1 << 20;
-bool g_discard = false;     // --sink discard
+enum SinkMode { kSinkChecksum, kSinkDiscard, kSinkSample, kSinkVerify };
+SinkMode g_sink = kSinkChecksum;
+bool g_discard = false;     // large bodies spliced to /dev/null (--sink discard | sample)
+uint64_t g_sample_stride = 1 << 20, g_sample_len = 4096;
+double g_s3_corrupt_rate = 0;
+std::mutex g_media_mu;
+std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> g_media;  // basename -> size, seed
+std::atomic<uint64_t> g_verify_objects{0}, g_verify_bytes{0}, g_verify_mismatch{0},
+    g_verify_unknown{0}, g_bad_digest{0}, g_checksummed{0}, g_corrupted{0}, g_parts{0},
+    g_mp_objects{0}, g_mp_parts{0};
 int g_devnull = -1;
 int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
@@ -144,6 +189,178 @@ std::string xml_escape(const std::string& s) {
     else o.push_back(c);
   }
   return o;
+}
+
+bool b64_decode(const std::string& in, std::string& out) {
+  static int8_t T[256];
+  static bool init = [] {
+    memset(T, -1, sizeof T);
+    const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    for (int i = 0; i < 64; ++i) T[(uint8_t)A[i]] = (int8_t)i;
+    return true;
+  }();
+  (void)init;
+  out.clear();
+  uint32_t acc = 0;
+  int bits = 0;
+  for (char ch : in) {
+    if (ch == '=') break;
+    int v = T[(uint8_t)ch];
+    if (v < 0) return false;
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      out.push_back((char)((acc >> bits) & 0xff));
+    }
+  }
+  return true;
+}
+
+// Origin object behind a staged key `<id>/original/<base64(basename)>` (the key layout of
+// lib/upload.js:43-45): false for keys of another shape and for the done marker.
+bool media_of_key(const std::string& key, uint64_t& size, uint64_t& seed, bool& media_like) {
+  media_like = false;
+  size_t p = key.find("/original/");
+  if (p == std::string::npos) return false;
+  std::string enc = key.substr(p + 10), name;
+  if (enc == "done" || enc.empty()) return false;
+  media_like = true;
+  if (!b64_decode(enc, name)) return false;
+  std::lock_guard<std::mutex> lk(g_media_mu);
+  auto it = g_media.find(name);
+  if (it == g_media.end()) return false;
+  size = it->second.first;
+  seed = it->second.second;
+  return true;
+}
+
+inline const uint8_t* pool_at(uint64_t o, uint64_t seed, uint64_t& avail) {
+  uint64_t po = (o + seed * 7919ull) % kPool;
+  avail = kPool - po;
+  return g_pool.data() + po;
+}
+
+// Does `chk` (a body received for bytes [off, off + chk.len) of the object with `seed`) match
+// what the origin generated for that range?
+bool check_range(const BodyCheck& chk, uint64_t off, uint64_t seed) {
+  if (g_sink == kSinkVerify) {
+    Summer s;
+    uint64_t o = off, left = chk.len;
+    while (left) {
+      uint64_t avail;
+      const uint8_t* p = pool_at(o, seed, avail);
+      uint64_t k = std::min(left, avail);
+      s.feed(p, (size_t)k);
+      o += k;
+      left -= k;
+    }
+    g_verify_bytes += chk.len;
+    return s.final() == chk.sum;
+  }
+  for (const Sample& w : chk.windows) {
+    uint64_t o = off + w.pos, i = 0;
+    while (i < w.bytes.size()) {
+      uint64_t avail;
+      const uint8_t* p = pool_at(o + i, seed, avail);
+      uint64_t k = std::min<uint64_t>(w.bytes.size() - i, avail);
+      if (memcmp(p, w.bytes.data() + i, (size_t)k) != 0) return false;
+      i += k;
+    }
+    g_verify_bytes += w.bytes.size();
+  }
+  return true;
+}
+
+// Consumer of one request body's payload bytes (after any aws-chunked framing is removed):
+// checksum fold, small-body capture, CRC32C / MD5 of payload checksums, sampled windows.
+struct Consumer {
+  Summer sum;
+  bool fold = false;
+  std::string* out = nullptr;
+  size_t keep = 0;
+  bool crc_on = false;
+  uint32_t crc = 0;
+  EVP_MD_CTX* md5 = nullptr;
+  std::vector<Sample>* windows = nullptr;   // sample sink
+  uint64_t total = 0;                       // payload length (window layout)
+  int64_t corrupt_at = -1;                  // fault injection: flip this payload byte
+  ~Consumer() {
+    if (md5) EVP_MD_CTX_free(md5);
+  }
+  bool needs_all() const { return fold || crc_on || md5 != nullptr || out != nullptr; }
+  uint64_t tail_start() const { return total > g_sample_len ? total - g_sample_len : 0; }
+  bool in_window(uint64_t pos) const {
+    return pos % g_sample_stride < g_sample_len || pos >= tail_start();
+  }
+  uint64_t window_end(uint64_t pos) const {      // pos in a window
+    if (pos >= tail_start()) return total;
+    uint64_t e = pos - pos % g_sample_stride + g_sample_len;
+    return e >= tail_start() ? total : std::min(e, total);
+  }
+  uint64_t next_window(uint64_t pos) const {     // pos outside every window
+    return std::min({(pos / g_sample_stride + 1) * g_sample_stride, tail_start(), total});
+  }
+  void sample(uint64_t pos, const uint8_t* p, size_t k) {
+    while (k) {
+      if (in_window(pos)) {
+        size_t t = (size_t)std::min<uint64_t>(k, window_end(pos) - pos);
+        if (!windows->empty() && windows->back().pos + windows->back().bytes.size() == pos)
+          windows->back().bytes.append((const char*)p, t);
+        else
+          windows->push_back(Sample{pos, std::string((const char*)p, t)});
+        pos += t;
+        p += t;
+        k -= t;
+      } else {
+        size_t t = (size_t)std::min<uint64_t>(k, next_window(pos) - pos);
+        pos += t;
+        p += t;
+        k -= t;
+      }
+    }
+  }
+  void feed_raw(uint64_t pos, const uint8_t* p, size_t k) {
+    if (fold) sum.feed(p, k);
+    if (out && out->size() < keep) out->append((const char*)p, std::min(k, keep - out->size()));
+    if (crc_on) crc = crc32c_update(crc, p, k);
+    if (md5) EVP_DigestUpdate(md5, p, k);
+    if (windows) sample(pos, p, k);
+  }
+  void feed(uint64_t pos, const uint8_t* p, size_t k) {
+    if (corrupt_at >= 0 && (uint64_t)corrupt_at >= pos && (uint64_t)corrupt_at < pos + k) {
+      size_t i = (size_t)((uint64_t)corrupt_at - pos);
+      uint8_t flipped = p[i] ^ 0x01;
+      feed_raw(pos, p, i);
+      feed_raw(pos + i, &flipped, 1);
+      feed_raw(pos + i + 1, p + i + 1, k - i - 1);
+      corrupt_at = -1;
+      g_corrupted++;
+      return;
+    }
+    feed_raw(pos, p, k);
+  }
+};
+
+// Parts (in part-number order) of one staged object against its origin object.
+void verify_object(const std::vector<BodyCheck>& parts, bool known, uint64_t size, uint64_t seed) {
+  if (!known) {
+    g_verify_unknown++;
+    return;
+  }
+  uint64_t off = 0;
+  bool ok = true;
+  for (const BodyCheck& c : parts) {
+    if (g_sink == kSinkVerify || !c.windows.empty() || c.len == 0) {
+      if (!check_range(c, off, seed)) ok = false;
+    } else {
+      ok = false;   // a part that arrived before the check was set up: unplaceable
+    }
+    off += c.len;
+  }
+  if (off != size) ok = false;
+  g_verify_objects++;
+  if (!ok) g_verify_mismatch++;
 }
 
 struct Request {
@@ -280,61 +497,159 @@ class Conn {
     return true;
   }
 
-  // Consume the request body, folding it into `s`; keep up to `keep` bytes in `out`.
-  bool read_body(int64_t n, Summer& s, std::string* out, size_t keep) {
-    if (g_discard && !ssl_ && n > (int64_t)keep) return discard_body(n, s);
-    if (g_discard && n > (int64_t)keep) {  // TLS: decrypt, skip the checksum pass
-      while (n > 0) {
-        if (pos_ == end_ && !fill()) return false;
-        size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
-        pos_ += k;
-        n -= (int64_t)k;
-        g_rx += k;
-      }
-      return true;
+  // Read `n` plain payload bytes into `c` (payload offset `pos` onwards). Spliced socket ->
+  // /dev/null when no consumer needs every byte (discard / sample sinks), reading only the
+  // sampled windows into user space.
+  bool read_plain(int64_t n, Consumer& c, uint64_t pos = 0) {
+    if (pos_ < end_ && n > 0) {
+      size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
+      c.feed(pos, buf_.data() + pos_, k);
+      pos_ += k;
+      pos += k;
+      n -= (int64_t)k;
+      g_rx += k;
     }
+    if (n == 0) return true;
+    if (!c.needs_all() && !ssl_) return splice_plain(n, c, pos);
     while (n > 0) {
       if (pos_ == end_ && !fill()) return false;
       size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
-      s.feed(buf_.data() + pos_, k);
-      if (out && out->size() < keep) out->append((const char*)buf_.data() + pos_, std::min(k, keep - out->size()));
+      c.feed(pos, buf_.data() + pos_, k);
       pos_ += k;
+      pos += k;
       n -= (int64_t)k;
       g_rx += k;
     }
     return true;
   }
 
-  // --sink discard: large bodies go socket -> pipe -> /dev/null (no user-space copy); the
-  // checksum then covers only the bytes that were already buffered with the header.
-  bool discard_body(int64_t n, Summer& s) {
-    if (pos_ < end_) {
-      size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
-      s.feed(buf_.data() + pos_, k);
-      pos_ += k;
-      n -= (int64_t)k;
-      g_rx += k;
-    }
+  bool splice_plain(int64_t n, Consumer& c, uint64_t pos) {
     if (pipe_[0] < 0) {
       if (pipe2(pipe_, O_CLOEXEC) != 0) return false;
       fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
     }
+    uint8_t win[16384];
     while (n > 0) {
-      ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, (size_t)std::min<int64_t>(n, 1 << 20),
-                            SPLICE_F_MOVE | SPLICE_F_MORE);
-      if (in < 0 && errno == EINTR) continue;
-      if (in <= 0) return false;
-      ssize_t left = in;
-      while (left > 0) {
-        ssize_t out = ::splice(pipe_[0], nullptr, g_devnull, nullptr, (size_t)left, SPLICE_F_MOVE);
-        if (out < 0 && errno == EINTR) continue;
-        if (out <= 0) return false;
-        left -= out;
+      if (c.windows && c.in_window(pos)) {   // a sampled window: recv exactly its bytes
+        size_t want = (size_t)std::min<uint64_t>((uint64_t)n, c.window_end(pos) - pos);
+        want = std::min(want, sizeof win);
+        ssize_t r = ::recv(fd_, win, want, 0);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return false;
+        c.feed(pos, win, (size_t)r);
+        pos += (uint64_t)r;
+        n -= r;
+        g_rx += (uint64_t)r;
+        continue;
       }
-      n -= in;
-      g_rx += (uint64_t)in;
+      uint64_t stop = c.windows ? std::min<uint64_t>(c.next_window(pos), pos + (uint64_t)n)
+                                : pos + (uint64_t)n;
+      int64_t run = (int64_t)(stop - pos);
+      while (run > 0) {
+        ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, (size_t)std::min<int64_t>(run, 1 << 20),
+                              SPLICE_F_MOVE | SPLICE_F_MORE);
+        if (in < 0 && errno == EINTR) continue;
+        if (in <= 0) return false;
+        ssize_t left = in;
+        while (left > 0) {
+          ssize_t out = ::splice(pipe_[0], nullptr, g_devnull, nullptr, (size_t)left, SPLICE_F_MOVE);
+          if (out < 0 && errno == EINTR) continue;
+          if (out <= 0) return false;
+          left -= out;
+        }
+        run -= in;
+        n -= in;
+        pos += (uint64_t)in;
+        g_rx += (uint64_t)in;
+      }
     }
     return true;
+  }
+
+  // Control bodies (bucket ops, complete XML, refused PUTs): into user space unless large
+  // and the sink discards.
+  bool read_body(int64_t n, Summer& s, std::string* out, size_t keep) {
+    Consumer c;
+    const bool big = g_discard && n > (int64_t)keep;
+    c.fold = !big;
+    c.out = big ? nullptr : out;
+    c.keep = keep;
+    if (!read_plain(n, c, 0)) return false;
+    s = c.sum;
+    return true;
+  }
+
+  bool get_line(std::string& line, size_t max = 8192) {
+    for (;;) {
+      const char* b = (const char*)buf_.data() + pos_;
+      size_t n = end_ - pos_;
+      const char* e = (const char*)memmem(b, n, "\r\n", 2);
+      if (e) {
+        line.assign(b, (size_t)(e - b));
+        pos_ += (size_t)(e - b) + 2;
+        return true;
+      }
+      if (n > max) return false;
+      if (!fill()) return false;
+    }
+  }
+
+  // aws-chunked payload: `<hex>[;ext]\r\n<data>\r\n` ... `0\r\n<trailer lines>\r\n\r\n`.
+  bool read_aws_chunked(Consumer& c, uint64_t& data_len, std::map<std::string, std::string>& trailers) {
+    data_len = 0;
+    std::string line;
+    for (;;) {
+      if (!get_line(line)) return false;
+      std::string hx = line.substr(0, line.find(';'));
+      char* endp = nullptr;
+      uint64_t k = strtoull(hx.c_str(), &endp, 16);
+      if (hx.empty() || (endp && *endp)) return false;
+      if (k == 0) {
+        for (;;) {
+          if (!get_line(line)) return false;
+          if (line.empty()) return true;
+          size_t colon = line.find(':');
+          if (colon == std::string::npos) continue;
+          std::string name = line.substr(0, colon);
+          for (auto& ch : name) ch = (char)tolower((unsigned char)ch);
+          size_t vs = line.find_first_not_of(' ', colon + 1);
+          trailers[name] = vs == std::string::npos ? "" : line.substr(vs);
+        }
+      }
+      uint64_t left = k;
+      while (left > 0) {
+        if (pos_ == end_ && !fill()) return false;
+        size_t t = (size_t)std::min<uint64_t>(left, end_ - pos_);
+        c.feed(data_len, buf_.data() + pos_, t);
+        pos_ += t;
+        left -= t;
+        data_len += t;
+        g_rx += t;
+      }
+      if (!get_line(line) || !line.empty()) return false;
+    }
+  }
+
+  static bool aws_chunked(const Request& r) {
+    auto it = r.h.find("content-encoding");
+    return it != r.h.end() && strcasestr(it->second.c_str(), "aws-chunked") != nullptr;
+  }
+
+  static uint64_t payload_len(const Request& r) {
+    if (!aws_chunked(r)) return (uint64_t)std::max<int64_t>(0, r.content_length);
+    auto it = r.h.find("x-amz-decoded-content-length");
+    return it == r.h.end() ? 0 : strtoull(it->second.c_str(), nullptr, 10);
+  }
+
+  // Consume a refused PUT's payload, whatever its encoding.
+  bool skip_payload(const Request& r) {
+    Consumer c;
+    if (aws_chunked(r)) {
+      uint64_t got;
+      std::map<std::string, std::string> tr;
+      return read_aws_chunked(c, got, tr);
+    }
+    return read_plain(r.content_length, c, 0);
   }
 
   bool send_all(const void* p, size_t n) {
@@ -400,6 +715,10 @@ class Conn {
     if (it != r.q.end()) size = strtoull(it->second.c_str(), nullptr, 10);
     it = r.q.find("seed");
     if (it != r.q.end()) seed = strtoull(it->second.c_str(), nullptr, 10);
+    if ((g_sink == kSinkSample || g_sink == kSinkVerify) && r.path.rfind("/media/", 0) == 0) {
+      std::lock_guard<std::mutex> lk(g_media_mu);  // what a staged copy of it must contain
+      g_media[r.path.substr(7)] = {size, seed};
+    }
     uint64_t start = 0, end = size ? size - 1 : 0;
     bool ranged = false;
     it = r.h.find("range");
@@ -583,58 +902,134 @@ class Conn {
     }
     // ---- object level
     if (m == "PUT" && r.h.count("x-amz-copy-source")) {  // no server-side copy here: say so
-      Summer s;
-      if (!read_body(r.content_length, s, nullptr, 0)) return false;
+      if (!skip_payload(r)) return false;
       return s3_error(501, "Not Implemented", "NotImplemented", key);
     }
+    thread_local std::mt19937_64 rng(std::random_device{}());
     if (m == "PUT" && g_s3_fail_rate > 0) {
-      thread_local std::mt19937_64 rng(std::random_device{}());
       if (std::uniform_real_distribution<double>(0, 1)(rng) < g_s3_fail_rate) {
-        Summer s;
-        if (!read_body(r.content_length, s, nullptr, 0)) return false;
+        if (!skip_payload(r)) return false;
         g_s3_faults++;
         return s3_error(503, "Slow Down", "SlowDown", key);
       }
     }
     if (m == "PUT") {
+      const bool part = r.q.count("uploadId") > 0;
+      const uint64_t dlen = payload_len(r);
+      const bool chunked = aws_chunked(r);
       Object o;
-      Summer s;
-      if (!read_body(r.content_length, s, &o.data, g_keep_bytes)) return false;
-      if ((uint64_t)r.content_length > g_keep_bytes) o.data.clear();
-      o.size = (uint64_t)r.content_length;
-      o.sum = s.final();
+      BodyCheck chk;
+      Consumer c;
+      auto hc = r.h.find("x-amz-checksum-crc32c");
+      auto tr = r.h.find("x-amz-trailer");
+      const bool trailer_crc =
+          tr != r.h.end() && strcasestr(tr->second.c_str(), "x-amz-checksum-crc32c") != nullptr;
+      auto hm = r.h.find("content-md5");
+      c.crc_on = hc != r.h.end() || trailer_crc;
+      if (hm != r.h.end()) {
+        c.md5 = EVP_MD_CTX_new();
+        EVP_DigestInit_ex(c.md5, EVP_md5(), nullptr);
+      }
+      const bool small = dlen <= g_keep_bytes;
+      c.fold = small || !g_discard;
+      if (small) {
+        c.out = &o.data;
+        c.keep = g_keep_bytes;
+      }
+      const bool checking = g_sink == kSinkSample || g_sink == kSinkVerify;
+      bool media_like = false, known = false;
+      uint64_t msize = 0, mseed = 0;
+      if (checking) {
+        known = !part && media_of_key(key, msize, mseed, media_like);
+        if (part) media_like = key.find("/original/") != std::string::npos;
+        if (g_sink == kSinkSample && media_like) {
+          c.windows = &chk.windows;
+          c.total = dlen;
+        }
+      }
+      if ((c.crc_on || c.md5) && g_s3_corrupt_rate > 0 && dlen > 0 &&
+          std::uniform_real_distribution<double>(0, 1)(rng) < g_s3_corrupt_rate)
+        c.corrupt_at = (int64_t)(dlen / 2);
+      uint64_t got = 0;
+      std::map<std::string, std::string> trailers;
+      if (chunked) {
+        if (!read_aws_chunked(c, got, trailers)) return false;
+      } else {
+        if (!read_plain(r.content_length, c, 0)) return false;
+        got = (uint64_t)std::max<int64_t>(0, r.content_length);
+      }
+      std::string extra;
+      if (c.crc_on || c.md5) g_checksummed++;
+      if (chunked && got != dlen) return s3_error(400, "Bad Request", "IncompleteBody", key);
+      if (c.crc_on) {
+        char b[9];
+        crc32c_b64(c.crc, b);
+        const std::string want = hc != r.h.end() ? hc->second : trailers["x-amz-checksum-crc32c"];
+        if (want != b) {
+          g_bad_digest++;
+          return s3_error(400, "Bad Request", "BadDigest", key);
+        }
+        extra += std::string("x-amz-checksum-crc32c: ") + b + "\r\n";
+      }
+      if (c.md5) {
+        unsigned char d[EVP_MAX_MD_SIZE];
+        unsigned int dl = 0;
+        EVP_DigestFinal_ex(c.md5, d, &dl);
+        unsigned char enc[64];
+        int el = EVP_EncodeBlock(enc, d, (int)dl);
+        if (hm->second != std::string((const char*)enc, (size_t)el)) {
+          g_bad_digest++;
+          return s3_error(400, "Bad Request", "BadDigest", key);
+        }
+      }
+      if (!small) o.data.clear();
+      o.size = got;
+      o.sum = c.sum.final();
       o.etag = hex64(o.sum, o.size);
-      auto up = r.q.find("uploadId");
-      std::lock_guard<std::mutex> lk(g_mu);
-      if (up != r.q.end()) {
-        auto it = g_uploads.find(up->second);
+      chk.len = got;
+      chk.sum = o.sum;
+      extra = "ETag: \"" + o.etag + "\"\r\n" + extra;
+      if (part) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_uploads.find(r.q.at("uploadId"));
         if (it == g_uploads.end()) return s3_error(404, "Not Found", "NoSuchUpload", key);
         int num = atoi(r.q.count("partNumber") ? r.q.at("partNumber").c_str() : "0");
-        std::string et = o.etag;
         it->second.parts[num] = std::move(o);
-        return respond(200, "OK", "", "ETag: \"" + et + "\"\r\n");
+        if (checking && media_like) it->second.checks[num] = std::move(chk);
+        g_parts++;
+        return respond(200, "OK", "", extra);
       }
-      if (!g_buckets.count(bucket)) return s3_error(404, "Not Found", "NoSuchBucket", bucket);
-      std::string et = o.etag;
-      g_buckets[bucket][key] = std::move(o);
-      g_objects++;
-      return respond(200, "OK", "", "ETag: \"" + et + "\"\r\n");
+      {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_buckets.count(bucket)) return s3_error(404, "Not Found", "NoSuchBucket", bucket);
+        g_buckets[bucket][key] = std::move(o);
+        g_objects++;
+      }
+      if (checking && media_like) {
+        std::vector<BodyCheck> one;
+        one.push_back(std::move(chk));
+        verify_object(one, known, msize, mseed);
+      }
+      return respond(200, "OK", "", extra);
     }
     if (m == "POST") {
       Summer s;
       std::string body;
       if (!read_body(r.content_length, s, &body, 1 << 20)) return false;
-      std::lock_guard<std::mutex> lk(g_mu);
-      if (r.q.count("uploads")) {
-        std::string id = "up" + std::to_string(g_upload_seq++);
-        g_uploads[id] = Upload{bucket, key, {}};
-        return respond(200, "OK",
-                       "<?xml version=\"1.0\" encoding=\"UTF-8\"?><InitiateMultipartUploadResult><Bucket>" +
-                           bucket + "</Bucket><Key>" + xml_escape(key) + "</Key><UploadId>" + id +
-                           "</UploadId></InitiateMultipartUploadResult>");
-      }
-      auto up = r.q.find("uploadId");
-      if (up != r.q.end()) {
+      std::string reply;
+      std::vector<BodyCheck> checks;
+      {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (r.q.count("uploads")) {
+          std::string id = "up" + std::to_string(g_upload_seq++);
+          g_uploads[id] = Upload{bucket, key, {}, {}};
+          return respond(200, "OK",
+                         "<?xml version=\"1.0\" encoding=\"UTF-8\"?><InitiateMultipartUploadResult><Bucket>" +
+                             bucket + "</Bucket><Key>" + xml_escape(key) + "</Key><UploadId>" + id +
+                             "</UploadId></InitiateMultipartUploadResult>");
+        }
+        auto up = r.q.find("uploadId");
+        if (up == r.q.end()) return s3_error(400, "Bad Request", "InvalidRequest", key);
         auto it = g_uploads.find(up->second);
         if (it == g_uploads.end()) return s3_error(404, "Not Found", "NoSuchUpload", key);
         Object o;
@@ -647,16 +1042,28 @@ class Conn {
         if (o.size > g_keep_bytes) o.data.clear();
         o.sum = h;
         o.etag = hex64(h, o.size) + "-" + std::to_string(it->second.parts.size());
+        g_mp_objects++;
+        g_mp_parts += it->second.parts.size();
+        for (auto& kv : it->second.parts) {   // a part without a check cannot be placed
+          auto ck = it->second.checks.find(kv.first);
+          checks.push_back(ck == it->second.checks.end() ? BodyCheck{kv.second.size, 0, {}}
+                                                         : std::move(ck->second));
+        }
         std::string et = o.etag;
         g_buckets[bucket][key] = std::move(o);
         g_uploads.erase(it);
         g_objects++;
-        return respond(200, "OK",
-                       "<?xml version=\"1.0\" encoding=\"UTF-8\"?><CompleteMultipartUploadResult><Bucket>" +
-                           bucket + "</Bucket><Key>" + xml_escape(key) + "</Key><ETag>&quot;" + et +
-                           "&quot;</ETag></CompleteMultipartUploadResult>");
+        reply = "<?xml version=\"1.0\" encoding=\"UTF-8\"?><CompleteMultipartUploadResult><Bucket>" +
+                bucket + "</Bucket><Key>" + xml_escape(key) + "</Key><ETag>&quot;" + et +
+                "&quot;</ETag></CompleteMultipartUploadResult>";
       }
-      return s3_error(400, "Bad Request", "InvalidRequest", key);
+      if (g_sink == kSinkSample || g_sink == kSinkVerify) {   // offsets are known now
+        bool media_like = false;
+        uint64_t msize = 0, mseed = 0;
+        bool known = media_of_key(key, msize, mseed, media_like);
+        if (media_like) verify_object(checks, known, msize, mseed);
+      }
+      return respond(200, "OK", reply);
     }
     if (r.content_length > 0) {
       Summer s;
@@ -690,16 +1097,25 @@ class Conn {
   }
 
   bool stats() {
-    char b[512];
+    char b[1536];
     size_t nup;
     {
       std::lock_guard<std::mutex> lk(g_mu);
       nup = g_uploads.size();
     }
+    const char* sink = g_sink == kSinkDiscard ? "discard" : g_sink == kSinkSample ? "sample"
+                       : g_sink == kSinkVerify ? "verify" : "checksum";
     snprintf(b, sizeof b,
              "{\"bytes_received\":%" PRIu64 ",\"bytes_served\":%" PRIu64 ",\"requests\":%" PRIu64
-             ",\"objects\":%" PRIu64 ",\"open_uploads\":%zu,\"s3_faults\":%" PRIu64 "}",
-             g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup, g_s3_faults.load());
+             ",\"objects\":%" PRIu64 ",\"open_uploads\":%zu,\"s3_faults\":%" PRIu64
+             ",\"sink\":\"%s\",\"verify_objects\":%" PRIu64 ",\"verify_bytes\":%" PRIu64
+             ",\"verify_mismatches\":%" PRIu64 ",\"verify_unknown\":%" PRIu64
+             ",\"checksummed_puts\":%" PRIu64 ",\"bad_digests\":%" PRIu64 ",\"corrupted\":%" PRIu64
+             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64 "}",
+             g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup, g_s3_faults.load(), sink,
+             g_verify_objects.load(), g_verify_bytes.load(), g_verify_mismatch.load(),
+             g_verify_unknown.load(), g_checksummed.load(), g_bad_digest.load(), g_corrupted.load(),
+             g_parts.load(), g_mp_objects.load(), g_mp_parts.load());
     return respond(200, "OK", b, "", "application/json");
   }
 
@@ -733,7 +1149,15 @@ int main(int argc, char** argv) {
     else if (a == "--keep-bytes") g_keep_bytes = strtoull(next(), nullptr, 10);
     else if (a == "--default-size") g_default_size = strtoull(next(), nullptr, 10);
     else if (a == "--files-root") g_files_root = next();
-    else if (a == "--sink") g_discard = std::string(next()) == "discard";
+    else if (a == "--sink") {
+      std::string v = next();
+      g_sink = v == "discard" ? kSinkDiscard : v == "sample" ? kSinkSample
+             : v == "verify" ? kSinkVerify : kSinkChecksum;
+      g_discard = g_sink == kSinkDiscard || g_sink == kSinkSample;
+    }
+    else if (a == "--sample-stride") g_sample_stride = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
+    else if (a == "--sample-len") g_sample_len = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
+    else if (a == "--s3-corrupt-rate") g_s3_corrupt_rate = atof(next());
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
     else if (a == "--s3-fail-rate") g_s3_fail_rate = atof(next());
@@ -751,7 +1175,8 @@ int main(int argc, char** argv) {
     }
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
-                      "[--default-size N] [--files-root DIR] [--sink checksum|discard] "
+                      "[--default-size N] [--files-root DIR] [--sink checksum|discard|sample|verify] "
+                      "[--sample-stride N] [--sample-len N] [--s3-corrupt-rate P] "
                       "[--tls-cert PEM --tls-key PEM] [--s3-fail-rate P]\n");
       return 2;
     }

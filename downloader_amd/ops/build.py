@@ -89,7 +89,7 @@ def build_blobd(force: bool = False, verbose: bool = True) -> Path:
     srcs = [CSRC / "blobd.cpp"]
     BIN.mkdir(exist_ok=True)
     out = BIN / "blobd"
-    if force or _stale(out, srcs):
+    if force or _stale(out, srcs + [CSRC / "crc32c.h"]):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O3", "-std=c++17", "-march=x86-64-v3", "-Wall", str(srcs[0]),
                "-lssl", "-lcrypto", "-lpthread", "-o", str(out)]

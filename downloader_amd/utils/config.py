@@ -50,10 +50,11 @@ class S3Config(BaseModel):
     # minio-js 7 default; per-request Python cost (SigV4, executor hop) makes fewer, larger
     # parts faster even for the socket relay: 100 MB jobs 37 GB/s @16 MiB -> 47.5 GB/s @64 MiB
     part_size: int = 64 * MiB
-    # Objects up to this size go in ONE PUT (socket relay or sendfile): fewer connections and
-    # requests per job - 100 MB jobs 43 -> 60 GB/s on the build box. rclone's upload cutoff is
-    # 200 MiB; minio-js switches at 64 MiB (kept in mode: reference).
-    multipart_threshold: int = 128 * MiB
+    # Objects up to this size go in ONE PUT (socket relay or sendfile), larger ones as
+    # multipart uploads of part_size parts - minio-js' split (lib/upload.js:45 fPutObject), so a
+    # 100 MB object is 2 parts relayed in parallel. Round 2 used 128 MiB (one PUT per 100 MB
+    # job); bench.py reports that setting in the same call as `single_put_MBps`.
+    multipart_threshold: int = 64 * MiB
     max_inflight_parts: int = 8                 # multipart parts in flight per object (ref: 1)
     # objects uploaded at once per job (ref: 1, lib/upload.js:34-52)
     concurrent_files: int = 4

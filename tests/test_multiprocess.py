@@ -140,7 +140,35 @@ def test_bench_rank_with_two_worker_processes(tmp_path):
     assert len(lines) == 1, r.stdout
     j = json.loads(lines[0])
     assert j["procs_per_rank"] == 2 and j["config"]["jobs_timed"] == 6
-    assert j["s3_peer_bytes_received"] >= 6 * 4_000_000 and j["value"] > 0
+    assert j["timed_sink_bytes"] >= 6 * 4_000_000 and j["value"] > 0
+    assert j["sink"] == "sample" and j["sink_mismatches"] == 0
+    assert j["sink_verified_objects"] >= 6
+    assert "single_put_MBps" in j
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("sink", ["sample", "verify"])
+def test_bench_multipart_objects_checked_against_the_origin(tmp_path, sink):
+    """The headline shape in miniature: objects above the threshold go as multipart uploads
+    (here 12 MB in 5 MiB parts = 3 parts), and the S3 peer matches every timed object, part by
+    part at its offset, against the bytes its origin generated (sampled windows / every byte);
+    the sink counters are taken inside the timed bracket."""
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
+                        "--warmup", "1", "--jobs-per-step", "2", "--size-mb", "12",
+                        "--part-mb", "5", "--threshold-mb", "5", "--sink", sink,
+                        "--no-compare-single-put"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["parts_per_object"] == 3.0
+    assert j["sink_verified_objects"] == 4 and j["sink_mismatches"] == 0
+    assert 4 * 12_000_000 <= j["timed_sink_bytes"] < 2 * 4 * 12_000_000   # no warmup bytes
+    if sink == "verify":
+        assert j["sink_verified_bytes"] == 4 * 12_000_000
+    else:
+        assert 0 < j["sink_verified_bytes"] < 4 * 12_000_000
+    assert "single_put_MBps" not in j
 
 
 @pytest.mark.slow
