@@ -6,10 +6,13 @@
 // with the GIL released on a pool of std::threads; digests come from OpenSSL EVP, which uses
 // SHA-NI / AVX2 on the host CPU.
 #include "native.h"
+#include "crc32c.h"
 
 #include <openssl/evp.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -419,6 +422,30 @@ std::vector<std::string> hash_file_ranges(const std::string& path,
   }
   ::close(fd);
   return out;
+}
+
+// ---- CRC32C (S3 flexible payload checksums, csrc/crc32c.h) ------------------------------
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) { return crc32c_update(crc, p, n); }
+
+uint32_t crc32c_fd(int fd, int64_t off, int64_t len) {
+  // 256 KiB reads stay in L2 between the page-cache copy and the CRC pass.
+  thread_local std::vector<uint8_t> buf(256 * 1024);
+  uint32_t c = 0;
+  while (len > 0) {
+    ssize_t r = ::pread(fd, buf.data(), (size_t)std::min<int64_t>(len, (int64_t)buf.size()), off);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) throw std::runtime_error("crc32c_fd: short read");
+    c = crc32c_update(c, buf.data(), (size_t)r);
+    off += r;
+    len -= r;
+  }
+  return c;
+}
+
+std::string crc32c_base64(uint32_t crc) {
+  char b[9];
+  crc32c_b64(crc, b);
+  return std::string(b, 8);
 }
 
 }  // namespace stager

@@ -60,11 +60,14 @@ struct PieceSplit {
 // GET on `src`, then (only on 200/206 with exactly `length` bytes) the PUT head on `dst`
 // followed by the body: spliced socket->pipe->socket, or - with `split` - through a hashed
 // user-space chunk (HttpConn::relay_body_hashed).
+// `crc`: the PUT is aws-chunked (the head carries the encoded Content-Length): one data chunk,
+// then a zero chunk whose trailer is the CRC32C of the bytes moved (x-amz-checksum-crc32c).
 py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
-               int64_t length, Progress* prog, int64_t max_body, const PieceSplit* split) {
+               int64_t length, Progress* prog, int64_t max_body, const PieceSplit* split,
+               bool crc) {
   std::string gh = get_head, ph = put_head;
   ResponseHead g, p;
-  std::string gerr, pbody, digests, head, tail;
+  std::string gerr, pbody, digests, head, tail, crc_b64;
   int64_t moved = 0;
   {
     py::gil_scoped_release rel;
@@ -77,9 +80,21 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
       int cork = 1;
       setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
       dst.send_raw(ph);
+      uint32_t c = 0;
+      if (crc && length > 0) {
+        char hx[32];
+        snprintf(hx, sizeof hx, "%llx\r\n", (unsigned long long)length);
+        dst.send_raw(hx);
+      }
       moved = split ? src.relay_body_hashed(dst, length, split->skip, split->full_len,
-                                            split->piece_len, prog, &digests, &head, &tail)
-                    : src.relay_body_to(dst, length, prog);
+                                            split->piece_len, prog, &digests, &head, &tail,
+                                            crc ? &c : nullptr)
+                    : src.relay_body_to(dst, length, prog, crc ? &c : nullptr);
+      if (crc) {
+        crc_b64 = crc32c_base64(c);
+        dst.send_raw(std::string(length > 0 ? "\r\n" : "") + "0\r\nx-amz-checksum-crc32c:" +
+                     crc_b64 + "\r\n\r\n");
+      }
       cork = 0;
       setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
       p = dst.read_head();
@@ -92,6 +107,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
   d["put"] = p.status ? (py::object)head_to_dict(p) : py::none();
   d["put_body"] = py::bytes(pbody);
   d["moved"] = moved;
+  d["crc32c"] = crc_b64;
   if (split) {
     d["digests"] = py::bytes(digests);
     d["head"] = py::bytes(head);
@@ -133,6 +149,25 @@ PYBIND11_MODULE(_native, m) {
         return py::bytes(out);
       },
       py::arg("algo"), py::arg("data"));
+  m.def(
+      "crc32c",
+      [](const py::buffer& data, uint32_t crc) {
+        BufView v = view(data);
+        if (v.n < 65536) return crc32c(v.p, v.n, crc);
+        py::gil_scoped_release rel;
+        return crc32c(v.p, v.n, crc);
+      },
+      py::arg("data"), py::arg("crc") = 0,
+      "CRC32C (Castagnoli) of data, continuing from `crc` (SSE4.2, three interleaved chains).");
+  m.def(
+      "crc32c_fd",
+      [](int fd, int64_t off, int64_t len) {
+        py::gil_scoped_release rel;
+        return crc32c_fd(fd, off, len);
+      },
+      py::arg("fd"), py::arg("offset"), py::arg("length"), "CRC32C of a file range.");
+  m.def("crc32c_base64", &crc32c_base64, py::arg("crc"),
+        "x-amz-checksum-crc32c value: base64 of the big-endian CRC.");
   m.def(
       "hash_pieces",
       [](const std::string& algo, const py::buffer& data, size_t piece_len, int threads) {
@@ -313,25 +348,29 @@ PYBIND11_MODULE(_native, m) {
       .def(
           "relay_to",
           [](HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
-             int64_t length, Progress* prog, int64_t max_body) {
-            return relay(src, get_head, dst, put_head, length, prog, max_body, nullptr);
+             int64_t length, Progress* prog, int64_t max_body, bool crc) {
+            return relay(src, get_head, dst, put_head, length, prog, max_body, nullptr, crc);
           },
           py::arg("get_head"), py::arg("dst"), py::arg("put_head"), py::arg("length"),
           py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)1 << 20,
+          py::arg("crc") = false,
           "GET on this connection and stream exactly `length` body bytes as the body of the "
           "PUT sent on `dst` (socket->pipe->socket splice). The GET must answer 200/206 with "
-          "that Content-Length, otherwise nothing is sent on `dst`.")
+          "that Content-Length, otherwise nothing is sent on `dst`. crc=True: aws-chunked body "
+          "with a trailing x-amz-checksum-crc32c (bytes through user space), returned as "
+          "`crc32c` (base64).")
       .def(
           "relay_hashed_to",
           [](HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
              int64_t length, int64_t skip, int64_t full_len, int64_t piece_len, Progress* prog,
-             int64_t max_body) {
+             int64_t max_body, bool crc) {
             PieceSplit ps{skip, full_len, piece_len};
-            return relay(src, get_head, dst, put_head, length, prog, max_body, &ps);
+            return relay(src, get_head, dst, put_head, length, prog, max_body, &ps, crc);
           },
           py::arg("get_head"), py::arg("dst"), py::arg("put_head"), py::arg("length"),
           py::arg("skip"), py::arg("full_len"), py::arg("piece_len"),
           py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)1 << 20,
+          py::arg("crc") = false,
           "relay_to through a user-space chunk that is SHA-1'd on the way: body bytes "
           "[skip, skip+full_len) as consecutive `piece_len` pieces (last may be short). Adds "
           "`digests` (20 B per piece), `head` (bytes before skip) and `tail` (bytes after).")

@@ -41,6 +41,11 @@ class Hasher {
 };
 
 std::string digest(const std::string& algo, const uint8_t* p, size_t n);
+// CRC32C of S3 flexible checksums (x-amz-checksum-crc32c): continue `crc` over p[0, n).
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
+// CRC32C of a file range (pread through an L2-sized buffer).
+uint32_t crc32c_fd(int fd, int64_t off, int64_t len);
+std::string crc32c_base64(uint32_t crc);
 std::string hash_pieces(const std::string& algo, const uint8_t* p, size_t n, size_t piece_len,
                         int threads);
 
@@ -162,18 +167,20 @@ class HttpConn {
   void discard_body(const ResponseHead& h);
   // Move exactly `n` body bytes of the response being read on *this to `dst`'s socket
   // (bytes already buffered first, then socket -> pipe -> socket with splice).
-  int64_t relay_body_to(HttpConn& dst, int64_t n, Progress* prog);
+  // `crc` non-null: the bytes go through user space (relay_copy) and are CRC32C'd on the way
+  // (S3 trailing checksum of an aws-chunked PUT).
+  int64_t relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32_t* crc = nullptr);
   // Same relay, but through a user-space chunk that is also hashed: body bytes [skip,
   // skip + full_len) are SHA-1'd as consecutive pieces of `piece_len` (the last may be
   // short) into `digests`; bytes before `skip` go to `head`, bytes after to `tail` (the
   // fragments of pieces that straddle the body's ends). One pass, L2-resident chunks.
   int64_t relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                             int64_t piece_len, Progress* prog, std::string* digests,
-                            std::string* head, std::string* tail);
+                            std::string* head, std::string* tail, uint32_t* crc = nullptr);
   // relay_body_hashed for parts of >= 8 pieces: buffer the part, then multi-buffer SHA-1.
   int64_t relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                                int64_t piece_len, Progress* prog, std::string* digests,
-                               std::string* head, std::string* tail);
+                               std::string* head, std::string* tail, uint32_t* crc = nullptr);
   void send_raw(const std::string& s) { send_all((const uint8_t*)s.data(), s.size()); }
   int fd() const { return fd_; }
   void mark_unusable() { reusable_ = false; }
@@ -194,7 +201,8 @@ class HttpConn {
   std::string read_line();
   int64_t take_buffered(uint8_t* p, int64_t n);
   // Relay through a user-space buffer (either side is TLS).
-  int64_t relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog);
+  int64_t relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
+                     uint32_t* crc = nullptr);
   std::string host_;
   int port_;
   int fd_ = -1;

@@ -621,17 +621,18 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
   return written;
 }
 
-int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog) {
+int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32_t* crc) {
   int64_t moved = 0;
   if (rpos_ < rend_) {
     int64_t k = std::min<int64_t>(n, (int64_t)(rend_ - rpos_));
+    if (crc) *crc = stager::crc32c(rbuf_.data() + rpos_, (size_t)k, *crc);
     dst.send_all(rbuf_.data() + rpos_, (size_t)k);
     rpos_ += (size_t)k;
     moved += k;
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
   if (moved == n) return moved;
-  if (ssl_ || dst.ssl_) return relay_copy(dst, n, moved, prog);
+  if (ssl_ || dst.ssl_ || crc) return relay_copy(dst, n, moved, prog, crc);
   if (pipe_[0] < 0) {
     if (pipe2(pipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
     int got = fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
@@ -675,7 +676,8 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog) {
   return moved;
 }
 
-int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog) {
+int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
+                             uint32_t* crc) {
   thread_local std::vector<uint8_t> buf(256 * 1024);
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
@@ -695,6 +697,7 @@ int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* 
       dst.reusable_ = false;
       throw IoError("source closed mid-body");
     }
+    if (crc) *crc = stager::crc32c(buf.data(), r, *crc);
     try {
       dst.send_all(buf.data(), r);
     } catch (...) {
@@ -709,12 +712,12 @@ int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* 
 
 int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                                     int64_t piece_len, Progress* prog, std::string* digests,
-                                    std::string* head, std::string* tail) {
+                                    std::string* head, std::string* tail, uint32_t* crc) {
   if (skip < 0 || full_len < 0 || skip + full_len > n || piece_len <= 0)
     throw IoError("relay_body_hashed: bad piece split");
   const int64_t npieces = (full_len + piece_len - 1) / piece_len;
   if (npieces >= 8 && n <= kMaxBufferedPart && sha1_mb_supported())
-    return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail);
+    return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail, crc);
   // Chunk size: 512 KiB stays in a Zen 5 core's 1 MiB L2 between the recv copy, the send
   // copy and the SHA-1 pass, so the payload is read from DRAM once.
   thread_local std::vector<uint8_t> buf(512 * 1024);
@@ -768,6 +771,7 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
       }
       k = (int64_t)r;
     }
+    if (crc) *crc = stager::crc32c(buf.data(), (size_t)k, *crc);
     try {
       dst.send_all(buf.data(), (size_t)k);
     } catch (...) {
@@ -895,7 +899,7 @@ RelayPoolStats relay_pool_stats() { return part_pool().stats(); }
 int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
                                        int64_t full_len, int64_t piece_len, Progress* prog,
                                        std::string* digests, std::string* head,
-                                       std::string* tail) {
+                                       std::string* tail, uint32_t* crc) {
   // The whole part lands in a per-thread buffer on its way to `dst` (recv into it, send from
   // it: the same two copies as the chunked path), then its pieces are hashed 16 at a time in
   // the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the per-core rate of a single SHA-NI
@@ -926,6 +930,7 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
       }
       k = (int64_t)r;
     }
+    if (crc) *crc = stager::crc32c(b + pos, (size_t)k, *crc);
     try {
       dst.send_all(b + pos, (size_t)k);
     } catch (...) {

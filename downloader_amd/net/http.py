@@ -70,6 +70,7 @@ class Response:
     written: int = 0
     reason: str = ""
     url: str = ""                # the URL that produced this response (after redirects)
+    sent_crc32c: str = ""        # relayed aws-chunked PUT: the trailing CRC32C we sent
 
     def header(self, name: str, default: Optional[str] = None) -> Optional[str]:
         name = name.lower()
@@ -169,6 +170,18 @@ def _build_head(method: str, host_hdr: str, path: str, headers: Headers,
         lines.append(f"Content-Length: {body_len}")
     lines.append("User-Agent: downloader-amd/0.1")
     return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
+
+
+# aws-chunked framing of a relayed PUT that carries a trailing CRC32C (S3 flexible checksums):
+# "<hex n>\r\n" <n bytes> "\r\n" "0\r\n" "x-amz-checksum-crc32c:<8 b64>\r\n" "\r\n"
+CRC_TRAILER = "x-amz-checksum-crc32c"
+
+
+def aws_chunked_length(n: int) -> int:
+    """Encoded Content-Length of an ``n``-byte payload sent as one aws-chunked data chunk
+    plus the zero chunk with the CRC32C trailer (csrc/module.cpp ``relay``)."""
+    data = len(f"{n:x}") + 2 + n + 2 if n > 0 else 0
+    return data + 3 + len(CRC_TRAILER) + 1 + 8 + 2 + 2
 
 
 class Transport:
@@ -407,7 +420,7 @@ class NativeTransport(Transport):
 
     def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
                length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None,
-               src_proxy: Optional[Proxy] = None
+               src_proxy: Optional[Proxy] = None, checksum: bool = False
                ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         ss, sh, sp, spath = split_host(src_url)
         ds, dh, dp, dpath = split_host(dst_url)
@@ -421,7 +434,8 @@ class NativeTransport(Transport):
         if src_proxy is not None and not stls:
             sh, sp, spath, src_headers = _via_proxy(src_proxy, src_url, src_headers)
         get_head = _build_head("GET", src_host_hdr, spath, src_headers, None)
-        put_head = _build_head("PUT", _host_hdr(dh, dp, dtls), dpath, dst_headers, length)
+        put_head = _build_head("PUT", _host_hdr(dh, dp, dtls), dpath, dst_headers,
+                               aws_chunked_length(length) if checksum else length)
         src, _ = self._acquire(sh, sp, stls, tunnel)
         self._track(slot, src)
         try:
@@ -433,9 +447,10 @@ class NativeTransport(Transport):
         self._track(slot, dst)
         try:
             if split is None:
-                d = src.relay_to(get_head, dst, put_head, length, nprog)
+                d = src.relay_to(get_head, dst, put_head, length, nprog, crc=checksum)
             else:
-                d = src.relay_hashed_to(get_head, dst, put_head, length, *split, nprog)
+                d = src.relay_hashed_to(get_head, dst, put_head, length, *split, nprog,
+                                        crc=checksum)
         except RuntimeError as e:
             self._untrack(slot, src)
             self._untrack(slot, dst)
@@ -452,13 +467,14 @@ class NativeTransport(Transport):
         if d["put"] is not None:
             p = d["put"]
             put = Response(p["status"], list(p["headers"]), d["put_body"], 0, p.get("reason", ""))
+            put.sent_crc32c = d.get("crc32c", "")
         hashed = {k: d[k] for k in ("digests", "head", "tail")} if split is not None else None
         return get, put, d["moved"], hashed
 
     async def relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
                     length: int, progress: Optional[Progress] = None,
                     split: Optional[Tuple[int, int, int]] = None,
-                    src_proxy: Optional[ProxyConfig] = None
+                    src_proxy: Optional[ProxyConfig] = None, checksum: bool = False
                     ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         """GET ``src_url`` and stream exactly ``length`` body bytes as the body of a PUT to
         ``dst_url`` without touching user space (socket -> pipe -> socket splice; through an
@@ -467,7 +483,11 @@ class NativeTransport(Transport):
 
         ``split=(skip, full_len, piece_len)``: relay through L2-sized user-space chunks and
         SHA-1 body bytes [skip, skip+full_len) as consecutive pieces on the way; the 4th
-        result is then ``{"digests", "head", "tail"}`` (``HttpConn.relay_hashed_to``)."""
+        result is then ``{"digests", "head", "tail"}`` (``HttpConn.relay_hashed_to``).
+
+        ``checksum``: the PUT body is aws-chunked with a trailing ``x-amz-checksum-crc32c``
+        computed on the way (bytes through user space); ``dst_headers`` must carry the
+        aws-chunked headers (``S3Client._relay_put`` does)."""
         nprog = None
         if progress is not None:
             if progress.native is None:
@@ -478,7 +498,7 @@ class NativeTransport(Transport):
             slot = self._new_slot()
             px = src_proxy.for_url(src_url) if src_proxy is not None else None
             fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
-                                       dst_headers, length, nprog, slot, split, px)
+                                       dst_headers, length, nprog, slot, split, px, checksum)
             try:
                 out = await asyncio.shield(fut)
             except asyncio.CancelledError:

@@ -64,7 +64,7 @@ def build_native(force: bool = False, verbose: bool = True) -> Path:
     srcs = [CSRC / "module.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp",
             CSRC / "tls.cpp"]
     out = OPS / f"_native{EXT}"
-    if force or _stale(out, srcs + [CSRC / "native.h"]):
+    if force or _stale(out, srcs + [CSRC / "native.h", CSRC / "crc32c.h"]):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
                "-march=x86-64-v3", "-Wall", "-Wno-unused-result",
@@ -107,9 +107,10 @@ def build_selftest(kind: str, force: bool = False, verbose: bool = True) -> Path
             CSRC / "tls.cpp"]
     BIN.mkdir(exist_ok=True)
     out = BIN / f"selftest_{kind}"
-    if force or _stale(out, srcs + [CSRC / "native.h"]):
+    if force or _stale(out, srcs + [CSRC / "native.h", CSRC / "crc32c.h"]):
         cxx = os.environ.get("CXX", "g++")
-        cmd = [cxx, "-O1", "-g", "-std=c++17", *SANITIZERS[kind], *[str(s) for s in srcs],
+        cmd = [cxx, "-O1", "-g", "-std=c++17", "-msse4.2", *SANITIZERS[kind],
+               *[str(s) for s in srcs],
                "-lssl", "-lcrypto", "-lpthread", "-o", str(out)]
         _run(cmd, verbose)
     return out

@@ -42,6 +42,22 @@ def md5(data) -> bytes:
     return native().digest("md5", data)
 
 
+def crc32c(data, crc: int = 0) -> int:
+    """CRC32C (Castagnoli), continuing from ``crc``: S3's x-amz-checksum-crc32c."""
+    return native().crc32c(data, crc)
+
+
+def crc32c_b64(data) -> str:
+    """``x-amz-checksum-crc32c`` header value of ``data`` (base64 of the big-endian CRC)."""
+    n = native()
+    return n.crc32c_base64(n.crc32c(data))
+
+
+def crc32c_fd_b64(fd: int, offset: int, length: int) -> str:
+    n = native()
+    return n.crc32c_base64(n.crc32c_fd(fd, offset, length))
+
+
 def new(algo: str):
     return native().Hasher(algo)
 

@@ -12,6 +12,13 @@ Differences by design:
   * transient failures (connection errors, 5xx, SlowDown) are retried with backoff.
   * an interrupted multipart upload can be resumed: parts whose ETag equals the local MD5
     of the same range are skipped.
+  * payload integrity per PUT / part with S3 flexible checksums (CRC32C) instead of minio-js'
+    Content-MD5 / signed SHA-256: ``x-amz-checksum-crc32c`` as a header for
+    in-memory and on-disk bodies, as the trailer of an aws-chunked body for socket relays
+    (computed while the bytes pass). The server recomputes it and refuses a mismatch with
+    400 BadDigest, which is retried. ``checksum``: ``auto`` = wherever the bytes cross user
+    space anyway (memory, disk, TLS relays, piece-hashed torrent relays), not the plain
+    splice relay; ``always`` = that too (relays then copy through user space); ``off``.
 """
 from __future__ import annotations
 
@@ -53,8 +60,11 @@ class S3Error(Exception):
 
     @property
     def retryable(self) -> bool:
+        # BadDigest / checksum mismatch: bytes corrupted on the way; sending them again (from
+        # the file, or a fresh source range) is the remedy
         return self.status >= 500 or self.code in ("SlowDown", "RequestTimeout",
-                                                   "InternalError", "ServiceUnavailable")
+                                                   "InternalError", "ServiceUnavailable",
+                                                   "BadDigest", "XAmzContentChecksumMismatch")
 
 
 @dataclass
@@ -106,7 +116,7 @@ class S3Client:
                  native: bool = True, connect_timeout: float = 10.0,
                  request_timeout: float = 300.0, ssl_verify: bool = True, ca_file: str = "",
                  native_tls: bool = True, addressing: str = "auto", session_token: str = "",
-                 split_tls_relays: bool = True):
+                 split_tls_relays: bool = True, checksum: str = "auto"):
         if "://" in endpoint:
             secure = endpoint.startswith("https://")
             endpoint = endpoint.split("://", 1)[1]
@@ -120,6 +130,9 @@ class S3Client:
         self.secret_key = secret_key
         self.session_token = session_token
         self.split_tls_relays = split_tls_relays
+        if checksum not in ("auto", "always", "off"):
+            raise ValueError(f"s3 checksum {checksum!r}: auto, always or off")
+        self.checksum = checksum
         self.region = region
         # bucket -> region learnt from the server (x-amz-bucket-region / <Region>): an AWS
         # bucket outside the configured region is signed for its own region after the first
@@ -144,7 +157,7 @@ class S3Client:
                    s3cfg.max_inflight_parts, s3cfg.unsigned_payload, s3cfg.retries,
                    s3cfg.native_transport, s3cfg.connect_timeout_s, s3cfg.request_timeout_s,
                    addressing=s3cfg.addressing, session_token=s3cfg.session_token,
-                   split_tls_relays=s3cfg.split_tls_relays)
+                   split_tls_relays=s3cfg.split_tls_relays, checksum=s3cfg.checksum)
 
     def virtual_host(self, bucket: str) -> bool:
         """Virtual-hosted-style addressing (``<bucket>.<endpoint>/<key>``) for this bucket?
@@ -210,15 +223,33 @@ class S3Client:
             return h.hexdigest()
         return native().digest("sha256", body).hex()
 
+    def want_checksum(self, relay: bool = False, tls: bool = False, hashed: bool = False) -> bool:
+        """Send a CRC32C with this upload? (``checksum`` policy, see the module docstring)."""
+        if self.checksum == "off":
+            return False
+        if self.checksum == "always" or not relay:
+            return True
+        return tls or hashed
+
+    async def _checksum_header(self, body) -> str:
+        from ..ops import hashing
+        if isinstance(body, FileRange):
+            return await asyncio.get_running_loop().run_in_executor(
+                None, hashing.crc32c_fd_b64, body.fd, body.offset, body.length)
+        return hashing.crc32c_b64(body)
+
     async def _request(self, method: str, bucket: str, key: str = "",
                        query: Sequence[Tuple[str, str]] = (), body=None,
                        headers: Optional[Dict[str, str]] = None, sink: Optional[FileSink] = None,
                        progress: Optional[Progress] = None, ok: Sequence[int] = (),
-                       expect_body: bool = True) -> Response:
+                       expect_body: bool = True, checksum: bool = False) -> Response:
         host, path = self._address(bucket, key)
         qs = sigv4.canonical_query(query)
         url = f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
         phash = await self._payload_hash(body)
+        if checksum and body is not None:
+            headers = dict(headers or {})
+            headers["x-amz-checksum-crc32c"] = await self._checksum_header(body)
         attempt = 0
         relocated = False
         while True:
@@ -298,7 +329,8 @@ class S3Client:
         if isinstance(data, str):
             data = data.encode("utf-8")
         hdrs = {"content-type": content_type} if content_type else None
-        r = await self._request("PUT", bucket, key, body=bytes(data), headers=hdrs)
+        r = await self._request("PUT", bucket, key, body=bytes(data), headers=hdrs,
+                                checksum=self.want_checksum())
         return (r.header("etag") or "").strip('"')
 
     async def delete_object(self, bucket: str, key: str) -> None:
@@ -315,7 +347,8 @@ class S3Client:
         try:
             if size <= self.multipart_threshold:
                 r = await self._request("PUT", bucket, key, body=FileRange(fd, 0, size),
-                                        progress=progress, headers=hdrs)
+                                        progress=progress, headers=hdrs,
+                                        checksum=self.want_checksum())
                 return (r.header("etag") or "").strip('"')
             return await self._multipart(bucket, key, fd, size, path, progress, resume,
                                          concurrency or self.max_inflight_parts, content_type)
@@ -403,7 +436,8 @@ class S3Client:
         return nt is not None and nt.handles(src_url, proxied) and nt.handles(self.base)
 
     def _signed(self, method: str, bucket: str, key: str, query: Sequence[Tuple[str, str]],
-                headers: Optional[Dict[str, str]] = None) -> Tuple[str, List[Tuple[str, str]]]:
+                headers: Optional[Dict[str, str]] = None,
+                phash: str = sigv4.UNSIGNED) -> Tuple[str, List[Tuple[str, str]]]:
         host, path = self._address(bucket, key)
         qs = sigv4.canonical_query(query)
         url = f"{self.scheme}://{host}" + sigv4.uri_encode(path, True) + ("?" + qs if qs else "")
@@ -413,25 +447,33 @@ class S3Client:
         if headers:
             hdrs.update({k.lower(): v for k, v in headers.items()})
         sigv4.sign(method, path, list(query), hdrs, self.access_key, self.secret_key,
-                   self.region_of(bucket), sigv4.UNSIGNED)
+                   self.region_of(bucket), phash)
         return url, list(hdrs.items())
 
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                          src_url: str, offset: int, length: int, whole: bool,
                          progress: Optional[Progress], split=None, src_proxy=None,
-                         content_type: str = ""):
+                         content_type: str = "", checksum: bool = False):
         """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
-        (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``."""
+        (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``.
+        ``checksum``: aws-chunked body with a trailing CRC32C of the relayed bytes."""
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
+        put_hdrs: Dict[str, str] = {"content-type": content_type} if content_type else {}
+        phash = sigv4.UNSIGNED
+        if checksum:
+            put_hdrs.update({"content-encoding": "aws-chunked",
+                             "x-amz-decoded-content-length": str(length),
+                             "x-amz-trailer": "x-amz-checksum-crc32c"})
+            phash = sigv4.STREAMING_TRAILER
         attempt = 0
         relocated = False
         while True:
-            url, hdrs = self._signed("PUT", bucket, key, query,
-                                     {"content-type": content_type} if content_type else None)
+            url, hdrs = self._signed("PUT", bucket, key, query, put_hdrs or None, phash)
             try:
                 get, put, _, hashed = await self.t.native.relay(src_url, src_hdrs, url, hdrs,
                                                                 length, progress, split,
-                                                                src_proxy=src_proxy)
+                                                                src_proxy=src_proxy,
+                                                                checksum=checksum)
             except TransportError as e:
                 err: Exception = e
                 retry = True
@@ -468,10 +510,12 @@ class S3Client:
         (~2 - 3 GB/s), so with ``split_tls_relays`` an object of more than 6 MiB that would go
         in one PUT is cut into up to ``max_inflight_parts`` parts relayed in parallel."""
         tls = src_url.startswith("https://") or self.scheme == "https"
+        crc = self.want_checksum(relay=True, tls=tls)
         if size <= self.multipart_threshold:
             if not (tls and self.split_tls_relays and ranges and size > MIN_PART + (1 << 20)):
                 return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
-                                             src_proxy=src_proxy, content_type=content_type)
+                                             src_proxy=src_proxy, content_type=content_type,
+                                             checksum=crc)
             ps = -(-size // max(1, self.max_inflight_parts))
             parts = self.plan_parts(size, part_size=-(-ps // (1 << 20)) << 20)
         else:
@@ -484,7 +528,7 @@ class S3Client:
             async with sem:
                 etags[num] = await self._relay_put(
                     bucket, key, [("partNumber", str(num)), ("uploadId", upload_id)], src_url,
-                    off, ln, False, progress, src_proxy=src_proxy)
+                    off, ln, False, progress, src_proxy=src_proxy, checksum=crc)
         try:
             await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts))
             return await self.complete_multipart_upload(bucket, key, upload_id,
@@ -551,9 +595,12 @@ class S3Client:
         multipart ``part=(number, upload_id)``) while SHA-1-ing the torrent pieces inside it
         (``split``); returns ``(etag, {"digests", "head", "tail"})``."""
         query = [] if part is None else [("partNumber", str(part[0])), ("uploadId", part[1])]
+        tls = src_url.startswith("https://") or self.scheme == "https"
         return await self._relay_put(bucket, key, query, src_url, offset, length, whole,
                                      progress, split,
-                                     content_type=content_type if part is None else "")
+                                     content_type=content_type if part is None else "",
+                                     checksum=self.want_checksum(relay=True, tls=tls,
+                                                                 hashed=True))
 
     async def create_multipart_upload(self, bucket: str, key: str, content_type: str = "") -> str:
         r = await self._request("POST", bucket, key, query=[("uploads", "")],
@@ -564,7 +611,7 @@ class S3Client:
                           progress: Optional[Progress] = None) -> str:
         r = await self._request("PUT", bucket, key,
                                 query=[("partNumber", str(num)), ("uploadId", upload_id)],
-                                body=body, progress=progress)
+                                body=body, progress=progress, checksum=self.want_checksum())
         return (r.header("etag") or "").strip('"')
 
     async def complete_multipart_upload(self, bucket: str, key: str, upload_id: str,

@@ -8,10 +8,17 @@ verified (``x-amz-content-sha256`` too unless UNSIGNED-PAYLOAD). ETags are MD5 /
 
 Fault injection: ``faults.add(FaultRule(...))`` makes matching requests fail
 with a status/code, stall, or drop the connection mid-response.
+
+Payload integrity like S3: ``x-amz-checksum-crc32c`` (header, or trailer of an aws-chunked
+body with ``x-amz-content-sha256: STREAMING-UNSIGNED-PAYLOAD-TRAILER``) and ``Content-MD5`` are
+recomputed over the received bytes; a mismatch is 400 BadDigest and nothing is stored.
+``corrupt_next = n`` flips one byte of the next n checksummed PUT bodies on arrival (transit
+corruption the checksum must catch).
 """
 from __future__ import annotations
 
 import asyncio
+import base64
 import hashlib
 import secrets
 import threading
@@ -83,6 +90,36 @@ class Faults:
         return None
 
 
+def decode_aws_chunked(body: bytes) -> Optional[Tuple[bytes, Dict[str, str]]]:
+    """``(payload, trailers)`` of an aws-chunked body (``<hex>[;ext]\r\n<data>\r\n`` ...
+    ``0\r\n<trailer lines>\r\n``), or None when malformed."""
+    out, pos, trailers = [], 0, {}
+    while True:
+        e = body.find(b"\r\n", pos)
+        if e < 0:
+            return None
+        try:
+            n = int(body[pos:e].split(b";", 1)[0], 16)
+        except ValueError:
+            return None
+        pos = e + 2
+        if n == 0:
+            while True:
+                e = body.find(b"\r\n", pos)
+                if e < 0:
+                    return None
+                line = body[pos:e].decode("latin-1")
+                pos = e + 2
+                if not line:
+                    return b"".join(out), trailers
+                k, _, v = line.partition(":")
+                trailers[k.strip().lower()] = v.strip()
+        if pos + n + 2 > len(body) or body[pos + n:pos + n + 2] != b"\r\n":
+            return None
+        out.append(body[pos:pos + n])
+        pos += n + 2
+
+
 def _xml(body: str) -> web.Response:
     return web.Response(body=('<?xml version="1.0" encoding="UTF-8"?>' + body).encode(),
                         content_type="application/xml")
@@ -120,6 +157,10 @@ class FakeS3:
         # access key -> session token it must present (signed) as x-amz-security-token
         self.session_tokens: Dict[str, str] = {}
         self.server_copies = 0                  # CopyObject / UploadPartCopy served
+        self.corrupt_next = 0                   # flip a byte of the next n checksummed PUTs
+        self.corrupted = 0
+        self.bad_digests = 0                    # PUTs refused: payload checksum mismatch
+        self.checksummed = 0                    # PUTs that carried a payload checksum
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -210,9 +251,45 @@ class FakeS3:
             return name[:-len(sfx) - 1]
         return ""
 
+    def _check_payload(self, req: web.Request, body: bytes, trailers: Dict[str, str],
+                       path: str):
+        """S3 payload checksums of a PUT; returns (possibly corrupted) body, the CRC header to
+        echo, and an error response or None."""
+        from ..ops import hashing
+        want_crc = req.headers.get("x-amz-checksum-crc32c") or trailers.get("x-amz-checksum-crc32c")
+        want_md5 = req.headers.get("Content-MD5")
+        if "x-amz-checksum-crc32c" in req.headers.get("x-amz-trailer", "") and \
+                "x-amz-checksum-crc32c" not in trailers:
+            return body, "", _err(400, "MalformedTrailerError", "declared trailer missing", path)
+        if want_crc is None and want_md5 is None:
+            return body, "", None
+        self.checksummed += 1
+        if self.corrupt_next > 0 and body:
+            self.corrupt_next -= 1
+            self.corrupted += 1
+            i = len(body) // 2
+            body = body[:i] + bytes([body[i] ^ 0x01]) + body[i + 1:]
+        if want_crc is not None and hashing.crc32c_b64(body) != want_crc:
+            self.bad_digests += 1
+            return body, "", _err(400, "BadDigest", "The CRC32C you specified did not match "
+                                  "the calculated checksum.", path)
+        if want_md5 is not None and \
+                base64.b64encode(hashlib.md5(body).digest()).decode() != want_md5:
+            self.bad_digests += 1
+            return body, "", _err(400, "BadDigest", "The Content-MD5 you specified did not "
+                                  "match what was received.", path)
+        return body, want_crc or "", None
+
     async def _dispatch(self, req: web.Request, path: str, query,
                         sig_path: str = "") -> web.StreamResponse:
         body = await req.read() if req.can_read_body else b""
+        trailers: Dict[str, str] = {}
+        if "aws-chunked" in req.headers.get("Content-Encoding", ""):
+            dec = decode_aws_chunked(body)
+            want_len = req.headers.get("x-amz-decoded-content-length", "")
+            if dec is None or not want_len.isdigit() or int(want_len) != len(dec[0]):
+                return _err(400, "IncompleteBody", "bad aws-chunked body", path)
+            body, trailers = dec
         presigned = any(k == "X-Amz-Signature" for k, _ in query)
         presigned_cred = dict(query).get("X-Amz-Credential", "")
         if self.verify_signatures and presigned:
@@ -235,8 +312,16 @@ class FakeS3:
                                         auth["SignedHeaders"].split(";")):
                     return _err(403, "InvalidToken", "missing or bad session token", path)
             ph = hdrs.get("x-amz-content-sha256", "")
-            if ph != sigv4.UNSIGNED and ph != hashlib.sha256(body).hexdigest():
+            if ph not in (sigv4.UNSIGNED, sigv4.STREAMING_TRAILER) and \
+                    ph != hashlib.sha256(body).hexdigest():
                 return _err(400, "XAmzContentSHA256Mismatch", "", path)
+            if ph == sigv4.STREAMING_TRAILER and not trailers:
+                return _err(400, "IncompleteBody", "streaming payload without trailer", path)
+        echo = ""
+        if req.method == "PUT":
+            body, echo, bad = self._check_payload(req, body, trailers, path)
+            if bad is not None:
+                return bad
         want = self.bucket_regions.get(path.lstrip("/").split("/", 1)[0])
         if want:
             try:
@@ -259,7 +344,10 @@ class FakeS3:
             return self._list_buckets()
         if not key:
             return self._bucket_op(req.method, bucket, q)
-        return self._object_op(req, bucket, key, q, body)
+        resp = self._object_op(req, bucket, key, q, body)
+        if echo and resp.status == 200:
+            resp.headers["x-amz-checksum-crc32c"] = echo
+        return resp
 
     def _copy_source(self, src: str, rng: Optional[str]):
         """Bytes named by ``x-amz-copy-source: /bucket/key`` (URL-encoded), optionally

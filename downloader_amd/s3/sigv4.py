@@ -15,6 +15,8 @@ from urllib.parse import quote
 
 EMPTY_SHA256 = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 UNSIGNED = "UNSIGNED-PAYLOAD"
+# aws-chunked body without chunk signatures, followed by trailing headers (the CRC32C)
+STREAMING_TRAILER = "STREAMING-UNSIGNED-PAYLOAD-TRAILER"
 ALGO = "AWS4-HMAC-SHA256"
 
 

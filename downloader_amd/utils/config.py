@@ -75,6 +75,11 @@ class S3Config(BaseModel):
     # Over TLS a relay is bound by one thread's AES-GCM: objects > 6 MiB under the multipart
     # threshold are relayed as up to max_inflight_parts parallel parts instead of one PUT
     split_tls_relays: bool = True
+    # payload integrity per PUT / part: CRC32C (x-amz-checksum-crc32c) the server verifies.
+    # auto = wherever bytes cross user space anyway (memory, disk uploads, TLS relays,
+    # piece-hashed torrent relays); always = also the plain splice relay (copies through user
+    # space); off. minio-js sends Content-MD5 over https / a signed SHA-256 over http.
+    checksum: Literal["auto", "always", "off"] = "auto"
     connect_timeout_s: float = 10.0
     request_timeout_s: float = 300.0            # socket idle timeout of one request
     # retries of a retryable S3 error (5xx, SlowDown, resets) with jittered backoff
@@ -245,6 +250,7 @@ class Config(BaseModel):
             # minio-js over plain HTTP signs every PUT/part with its payload SHA-256
             # (SURVEY §2.5); over TLS it would send UNSIGNED-PAYLOAD + Content-MD5 instead.
             self.s3.unsigned_payload = self.s3.secure
+            self.s3.checksum = "off"                 # (SHA-256 payload signing checks bytes)
             self.download.http_streams = 1
             self.download.bucket_concurrency = 1
             self.download.webseed_streams = 1
