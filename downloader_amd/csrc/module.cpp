@@ -75,7 +75,12 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
     g = src.read_head();
     bool ok = (g.status == 200 || g.status == 206) && !g.chunked && g.content_length == length;
     if (!ok) {
-      gerr = src.read_body(g, 1 << 20);
+      // an error page is read for the message; a big unwanted body (a whole 200 where a 206
+      // slice was asked - If-Range on a changed source) is not: the connection is dropped
+      if (!g.chunked && g.content_length >= 0 && g.content_length <= (1 << 20))
+        gerr = src.read_body(g, 1 << 20);
+      else
+        src.mark_unusable();
     } else {
       int cork = 1;
       setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
@@ -331,7 +336,9 @@ PYBIND11_MODULE(_native, m) {
               py::gil_scoped_release rel;
               c.send_request(hs, nullptr, 0);
               h = c.read_head();
-              if (h.status >= 200 && h.status < 300)
+              if (h.status >= 200 && h.status < 300 && !h.chunked && h.content_length > max_bytes)
+                c.mark_unusable();   // more than asked (a 200 for a Range GET): not written
+              else if (h.status >= 200 && h.status < 300)
                 n = c.read_body_to_fd(h, fd, off, max_bytes, prog);
               else
                 err = c.read_body(h, max_err_body);

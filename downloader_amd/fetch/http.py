@@ -21,7 +21,7 @@ import time
 from typing import Optional, Tuple
 from urllib.parse import urlsplit
 
-from ..net.http import FileSink, HttpError, Progress, TransportSet
+from ..net.http import FileSink, HttpError, Progress, SourceChanged, TransportSet, pin_headers
 from ..net.proxy import ProxyConfig
 from ..stages.select import node_extname
 from ..utils.log import Logger, NullLogger
@@ -84,6 +84,9 @@ async def probe_validated(t: TransportSet, url: str, proxy: Optional[ProxyConfig
             (r.header("accept-ranges") or "").lower() == "bytes", r.url or url, validator)
 
 
+SOURCE_RESTARTS = 2
+
+
 async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                       min_split: int = 32 << 20, progress: Optional[Progress] = None,
                       min_rate: float = 0.0, stall_window: float = 30.0,
@@ -91,6 +94,12 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                       proxy: Optional[ProxyConfig] = None,
                       space_reserve: Optional[int] = None) -> int:
     """Download ``url`` to ``path`` through ``path + '.part'`` (renamed when complete).
+
+    Every GET is pinned to the version the probe saw (``pin_headers``: If-Match /
+    If-Unmodified-Since, plus If-Range on Range requests): parallel ranges, a resumed tail
+    and the whole-file GET are all of one version. When the origin changes mid-transfer the
+    partial data is dropped and the file is fetched again from the new version (at most
+    ``SOURCE_RESTARTS`` times), never stitched from two.
 
     Resume (the reference restarts from byte 0): the journal
     ``path + '.part.ranges'`` records the origin's validator (strong ETag / Last-Modified),
@@ -104,6 +113,25 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
     hold what is still to be written plus that reserve (``stages/space.py``)."""
     log = logger or NullLogger()
     progress = progress or Progress()
+    for attempt in range(SOURCE_RESTARTS + 1):
+        try:
+            return await _download_once(t, url, path, streams, min_split, progress, min_rate,
+                                        stall_window, log, proxy, space_reserve)
+        except SourceChanged as e:
+            if attempt == SOURCE_RESTARTS:
+                raise HttpDownloadError(f"origin kept changing during the download: {e}") from e
+            log.warn("origin changed mid-download, restarting from the new version", err=str(e))
+            for stale in (path + ".part", path + ".part.ranges"):
+                try:
+                    os.unlink(stale)
+                except FileNotFoundError:
+                    pass
+    raise AssertionError("unreachable")
+
+
+async def _download_once(t: TransportSet, url: str, path: str, streams: int, min_split: int,
+                         progress: Progress, min_rate: float, stall_window: float, log: Logger,
+                         proxy: Optional[ProxyConfig], space_reserve: Optional[int]) -> int:
     size, ranges, url, validator = await probe_validated(t, url, proxy)   # later GETs: final URL
     part_path, state_path = path + ".part", path + ".part.ranges"
     if size >= 0 and os.path.isfile(path) and os.path.getsize(path) == size:
@@ -137,8 +165,11 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
             log.debug("parallel range download", streams=n, size=size)
 
             async def part(off: int, ln: int) -> int:
-                r = await t.request("GET", url, headers=[("Range", f"bytes={off}-{off + ln - 1}")],
-                                    sink=FileSink(fd, off, ln), progress=progress, proxy=proxy)
+                hdrs = [("Range", f"bytes={off}-{off + ln - 1}")] + pin_headers(validator, True)
+                r = await t.request("GET", url, headers=hdrs, sink=FileSink(fd, off, ln),
+                                    progress=progress, proxy=proxy)
+                if r.status == 412 or (validator and r.status == 200):
+                    raise SourceChanged(f"range {off}+{ln}: HTTP {r.status}", r.status)
                 if r.status != 206:
                     raise HttpDownloadError(f"range request got HTTP {r.status}")
                 if r.written != ln:
@@ -156,11 +187,14 @@ async def download_to(t: TransportSet, url: str, path: str, streams: int = 1,
                 have = 0
                 os.ftruncate(fd, 0)
             hdrs = [("Range", f"bytes={have}-")] if have else []
+            hdrs += pin_headers(validator, bool(have))
             if have:
                 log.info("resume: continuing partial download", offset=have, size=size)
             task = asyncio.ensure_future(t.request("GET", url, headers=hdrs, proxy=proxy,
                                                    sink=FileSink(fd, have), progress=progress))
             r = await _guard(task, progress, min_rate, stall_window)
+            if r.status == 412 or (have and validator and r.status == 200):
+                raise SourceChanged(f"GET from {have}: HTTP {r.status}", r.status)
             if not r.ok or (have and r.status != 206):
                 raise HttpDownloadError(f"GET {url} -> HTTP {r.status} {r.reason}")
             cl = r.header("content-length")

@@ -172,6 +172,25 @@ def _build_head(method: str, host_hdr: str, path: str, headers: Headers,
     return ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
 
 
+class SourceChanged(TransportError):
+    """The origin answered a pinned request (If-Match / If-Unmodified-Since / If-Range) with
+    412, or with a whole 200 body where a 206 range was asked: the object is no longer the
+    version the transfer started on, so the bytes already moved belong to another version."""
+
+
+def pin_headers(validator: str, ranged: bool) -> List[Tuple[str, str]]:
+    """Request headers that pin a GET to the version ``validator`` (``probe_validated``: a
+    strong ETag, or ``lm:<Last-Modified>``): a changed object answers 412 (``If-Match`` /
+    ``If-Unmodified-Since``), and - for servers that only honour ``If-Range`` - a ranged GET
+    answers 200 with the whole new body instead of the 206 slice."""
+    if not validator:
+        return []
+    if validator.startswith("lm:"):
+        date = validator[3:]
+        return [("If-Unmodified-Since", date)] + ([("If-Range", date)] if ranged else [])
+    return [("If-Match", validator)] + ([("If-Range", validator)] if ranged else [])
+
+
 # aws-chunked framing of a relayed PUT that carries a trailing CRC32C (S3 flexible checksums):
 # "<hex n>\r\n" <n bytes> "\r\n" "0\r\n" "x-amz-checksum-crc32c:<8 b64>\r\n" "\r\n"
 CRC_TRAILER = "x-amz-checksum-crc32c"
@@ -592,6 +611,10 @@ class AiohttpTransport(Transport):
                                     proxy=proxy.url if proxy is not None else None) as resp:
                 rh = [(k.lower(), v) for k, v in resp.headers.items()]
                 final = str(resp.url)
+                if sink is not None and 200 <= resp.status < 300 and \
+                        (resp.content_length or 0) > sink.max_bytes:
+                    # more than asked (a 200 for a Range GET): not written, like the native path
+                    return Response(resp.status, rh, b"", 0, resp.reason or "", final)
                 if sink is not None and 200 <= resp.status < 300:
                     written = 0
                     async for chunk in resp.content.iter_chunked(1 << 20):

@@ -31,8 +31,8 @@ from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import quote
 
-from ..net.http import (FileRange, FileSink, Progress, Response, TransportError,
-                        TransportSet, make_transports)
+from ..net.http import (FileRange, FileSink, Progress, Response, SourceChanged,
+                        TransportError, TransportSet, make_transports, pin_headers)
 from . import sigv4
 
 NS = "{http://s3.amazonaws.com/doc/2006-03-01/}"
@@ -453,11 +453,14 @@ class S3Client:
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                          src_url: str, offset: int, length: int, whole: bool,
                          progress: Optional[Progress], split=None, src_proxy=None,
-                         content_type: str = "", checksum: bool = False):
+                         content_type: str = "", checksum: bool = False, validator: str = ""):
         """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
         (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``.
-        ``checksum``: aws-chunked body with a trailing CRC32C of the relayed bytes."""
+        ``checksum``: aws-chunked body with a trailing CRC32C of the relayed bytes.
+        ``validator``: pin the source GET to that version; a changed source raises
+        ``SourceChanged`` (nothing is sent to S3 for that GET)."""
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
+        src_hdrs += pin_headers(validator, not whole)
         put_hdrs: Dict[str, str] = {"content-type": content_type} if content_type else {}
         phash = sigv4.UNSIGNED
         if checksum:
@@ -479,6 +482,10 @@ class S3Client:
                 retry = True
             else:
                 if put is None:
+                    if get.status == 412 or (validator and not whole and get.status == 200):
+                        raise SourceChanged(f"source changed since {validator} (HTTP "
+                                            f"{get.status} for {length} bytes at {offset})",
+                                            get.status)
                     raise TransportError(f"source {src_url} answered HTTP {get.status} "
                                          f"(Content-Length {get.header('content-length')}) "
                                          f"for {length} bytes at {offset}", get.status)
@@ -500,11 +507,18 @@ class S3Client:
     async def relay_object(self, bucket: str, key: str, src_url: str, size: int,
                            progress: Optional[Progress] = None,
                            concurrency: Optional[int] = None, src_proxy=None,
-                           content_type: str = "", ranges: bool = True) -> str:
+                           content_type: str = "", ranges: bool = True,
+                           validator: str = "") -> str:
         """Stage ``src_url`` (``size`` bytes) straight into S3: each multipart part is one Range
         GET relayed socket->socket into one UploadPart; objects up to ``multipart_threshold``
         go in one relayed PUT. ``src_proxy``: the source-fetch proxy policy
         (``net/proxy.ProxyConfig``); ``ranges``: the origin serves Range requests.
+
+        ``validator`` (strong ETag or ``lm:<Last-Modified>``): every part's GET is pinned to
+        that version, so parts of two versions of a changing origin are never combined into
+        one object (the reference's single GET per file cannot mix versions either,
+        lib/download.js:159-160). A change aborts the upload with ``SourceChanged``; the
+        caller restarts from the new version.
 
         Over TLS one relay is bound by one thread decrypting and re-encrypting every byte
         (~2 - 3 GB/s), so with ``split_tls_relays`` an object of more than 6 MiB that would go
@@ -515,7 +529,7 @@ class S3Client:
             if not (tls and self.split_tls_relays and ranges and size > MIN_PART + (1 << 20)):
                 return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
                                              src_proxy=src_proxy, content_type=content_type,
-                                             checksum=crc)
+                                             checksum=crc, validator=validator)
             ps = -(-size // max(1, self.max_inflight_parts))
             parts = self.plan_parts(size, part_size=-(-ps // (1 << 20)) << 20)
         else:
@@ -528,7 +542,8 @@ class S3Client:
             async with sem:
                 etags[num] = await self._relay_put(
                     bucket, key, [("partNumber", str(num)), ("uploadId", upload_id)], src_url,
-                    off, ln, False, progress, src_proxy=src_proxy, checksum=crc)
+                    off, ln, False, progress, src_proxy=src_proxy, checksum=crc,
+                    validator=validator)
         try:
             await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts))
             return await self.complete_multipart_upload(bucket, key, upload_id,

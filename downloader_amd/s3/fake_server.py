@@ -540,6 +540,10 @@ class FakeS3:
             return _err(404, "NoSuchKey", "The specified key does not exist.", key)
         hdrs = {"ETag": f'"{o.etag}"', "Last-Modified": time.strftime(
             "%a, %d %b %Y %H:%M:%S GMT", time.gmtime(o.mtime)), "Accept-Ranges": "bytes"}
+        im = req.headers.get("If-Match")
+        if im and im != "*" and im.strip('"') != o.etag:        # S3 conditional GET / HEAD
+            return _err(412, "PreconditionFailed", "At least one of the pre-conditions you "
+                        "specified did not hold", key)
         if m == "HEAD":
             hdrs["Content-Length"] = str(len(o.data))
             return web.Response(status=200, headers=hdrs)

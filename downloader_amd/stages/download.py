@@ -15,13 +15,17 @@ from ..fetch import bucket as bucket_src
 from ..fetch import http as http_src
 from ..fetch import local as file_src
 from ..models import api, keys
-from ..net.http import Progress
+from ..net.http import Progress, SourceChanged
 from ..net.proxy import ProxyConfig
 from ..utils.log import redact_url
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket, media_type)
 from .jobdir import JobDir, dir_name
 from .select import select_from_config
+
+# a source that changes version mid-transfer is restarted from its new version this often
+# before the job fails (and goes through the broker retry)
+SOURCE_RESTARTS = 2
 
 Backend = Callable[[str, Job, str], Awaitable[None]]
 
@@ -132,16 +136,33 @@ class DownloadStage(Stage):
         if not s3.can_relay(url, self.proxy) or \
                 not select_from_config(self.cfg).accepts_single_file(name):
             return False
-        size, ranges, final = await http_src.probe(self.sv.transports, url, self.proxy)
+        size, ranges, final, validator = await http_src.probe_validated(
+            self.sv.transports, url, self.proxy)
         if size <= 0 or (size > s3.multipart_threshold and not ranges) or \
                 not s3.can_relay(final, self.proxy):
             return False
         await ensure_staging_bucket(self.sv)
         key = keys.object_key(job.id, name)
         job.logger.info("streaming http source straight to staging", key=key, size=size)
-        await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress(),
-                              src_proxy=self.proxy, content_type=media_type(self.cfg, name),
-                              ranges=ranges)
+        for attempt in range(SOURCE_RESTARTS + 1):
+            try:
+                # every part GET pinned to the probed version: a mid-job change aborts the
+                # upload instead of completing a torn object
+                await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress(),
+                                      src_proxy=self.proxy,
+                                      content_type=media_type(self.cfg, name), ranges=ranges,
+                                      validator=validator)
+                break
+            except SourceChanged as e:
+                if attempt == SOURCE_RESTARTS:
+                    raise
+                job.logger.warn("origin changed mid-transfer, restarting from the new version",
+                                err=str(e))
+                job.stats["source_restarts"] = job.stats.get("source_restarts", 0) + 1
+                size, ranges, final, validator = await http_src.probe_validated(
+                    self.sv.transports, url, self.proxy)
+                if size <= 0 or (size > s3.multipart_threshold and not ranges):
+                    raise
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + size
         job.stats.setdefault("streamed", []).append(
             {"file": os.path.join(path, name), "key": key, "size": size, "virtual": True})
@@ -246,7 +267,9 @@ class DownloadStage(Stage):
                                       # outlive the slowest object's last part
                                       client.presign("GET", src.bucket, it.name, 12 * 3600),
                                       it.size, prog,
-                                      content_type=media_type(self.cfg, f))
+                                      content_type=media_type(self.cfg, f),
+                                      # parts pinned to the listed version (If-Match)
+                                      validator=f'"{it.etag}"' if it.etag else "")
         await asyncio.gather(*(one(k, f) for k, f in owner.items()))
         staged = sum(by_path[f].size for f in owner.values())
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + staged

@@ -46,6 +46,7 @@ class Origin:
         self.redirect = {}      # path -> (status, Location): answered before anything else
         self.no_validators = False   # True: no ETag (resume cannot be validated)
         self.hooks = []              # callables(method, path) run before each request
+        self.ignore_if_match = False  # True: like servers that only honour If-Range
         self._etags = {}
 
     def _body(self, path: str, data: bytes, s: int, e: int) -> bytes:
@@ -94,9 +95,15 @@ class Origin:
             if data is None:
                 return web.Response(status=404, text="not found")
             hdrs = {} if self.no_ranges else {"Accept-Ranges": "bytes"}
-            if not self.no_validators:
-                hdrs["ETag"] = self._etag(req.path, data)
             rng = req.headers.get("Range")
+            if not self.no_validators:
+                etag = hdrs["ETag"] = self._etag(req.path, data)
+                im = req.headers.get("If-Match")
+                if im and not self.ignore_if_match and im not in ("*", etag):
+                    return web.Response(status=412, text="precondition failed")
+                ir = req.headers.get("If-Range")
+                if rng and ir and ir != etag:
+                    rng = None                   # RFC 9110: changed -> the whole new body
             if rng and self.fail_ranges.get(rng, 0) > 0:
                 self.fail_ranges[rng] -= 1
                 return web.Response(status=503, text="injected range failure")
