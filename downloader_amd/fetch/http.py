@@ -24,7 +24,7 @@ from urllib.parse import urlsplit
 from ..net.http import FileSink, HttpError, Progress, SourceChanged, TransportSet, pin_headers
 from ..net.proxy import ProxyConfig
 from ..stages.select import node_extname
-from ..utils.log import Logger, NullLogger
+from ..utils.log import Logger, NullLogger, redact_url
 
 
 class HttpDownloadError(Exception):
@@ -196,7 +196,7 @@ async def _download_once(t: TransportSet, url: str, path: str, streams: int, min
             if r.status == 412 or (have and validator and r.status == 200):
                 raise SourceChanged(f"GET from {have}: HTTP {r.status}", r.status)
             if not r.ok or (have and r.status != 206):
-                raise HttpDownloadError(f"GET {url} -> HTTP {r.status} {r.reason}")
+                raise HttpDownloadError(f"GET {redact_url(url)} -> HTTP {r.status} {r.reason}")
             cl = r.header("content-length")
             if cl and cl.isdigit() and int(cl) != r.written:
                 raise HttpDownloadError(f"truncated body: {r.written} of {cl} bytes")
@@ -251,7 +251,7 @@ async def _guard(task: asyncio.Future, progress: Progress, min_rate: float, wind
 async def fetch_bytes(t: TransportSet, url: str, limit: int = 64 << 20) -> bytes:
     r = await t.request("GET", url)
     if not r.ok:
-        raise HttpError(f"GET {url} -> HTTP {r.status}", r.status, r.body)
+        raise HttpError(f"GET {redact_url(url)} -> HTTP {r.status}", r.status, r.body)
     if len(r.body) > limit:
         raise HttpError("body too large", r.status)
     return r.body

@@ -30,6 +30,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
 from urllib.parse import quote, urljoin, urlsplit
 
 from .proxy import Proxy, ProxyConfig
+from ..utils.log import redact_text, redact_url
 
 Headers = Sequence[Tuple[str, str]]
 
@@ -535,7 +536,8 @@ class NativeTransport(Transport):
                 return out
             if not self.handles(nxt, src_proxy is not None and
                                 src_proxy.for_url(nxt) is not None):
-                raise TransportError(f"relay source {src_url} redirects to {nxt}: not "
+                raise TransportError(f"relay source {redact_url(src_url)} redirects to "
+                                     f"{redact_url(nxt)}: not "
                                      f"supported by the socket relay", get.status)
             src_headers = redirect_headers(src_url, nxt, src_headers)
             src_url = nxt
@@ -639,7 +641,8 @@ class AiohttpTransport(Transport):
                 return Response(resp.status, rh, payload, 0, resp.reason or "", final)
         except (aiohttp.ClientConnectionError, aiohttp.ClientPayloadError,
                 asyncio.TimeoutError) as e:
-            raise TransportError(f"{method} {url}: {type(e).__name__}: {e}") from e
+            raise TransportError(f"{method} {redact_url(url)}: {type(e).__name__}: "
+                                 f"{redact_text(str(e))}") from e
 
     async def close(self) -> None:
         if self._session is not None:
@@ -696,7 +699,8 @@ class TransportSet:
                 return r
             kw["headers"] = redirect_headers(r.url, nxt, kw.get("headers") or ())
             url = nxt
-        raise TransportError(f"{method} {url}: more than {MAX_REDIRECTS} redirects", 310)
+        raise TransportError(f"{method} {redact_url(url)}: more than {MAX_REDIRECTS} redirects",
+                             310)
 
     async def _one(self, method: str, url: str, proxy: Optional[ProxyConfig], kw) -> Response:
         px = proxy.for_url(url) if proxy is not None else None

@@ -33,6 +33,7 @@ from urllib.parse import quote
 
 from ..net.http import (FileRange, FileSink, Progress, Response, SourceChanged,
                         TransportError, TransportSet, make_transports, pin_headers)
+from ..utils.log import redact_url
 from . import sigv4
 
 NS = "{http://s3.amazonaws.com/doc/2006-03-01/}"
@@ -486,7 +487,7 @@ class S3Client:
                         raise SourceChanged(f"source changed since {validator} (HTTP "
                                             f"{get.status} for {length} bytes at {offset})",
                                             get.status)
-                    raise TransportError(f"source {src_url} answered HTTP {get.status} "
+                    raise TransportError(f"source {redact_url(src_url)} answered HTTP {get.status} "
                                          f"(Content-Length {get.header('content-length')}) "
                                          f"for {length} bytes at {offset}", get.status)
                 if put.ok:
@@ -648,7 +649,11 @@ class S3Client:
                 info = await self.head_object(bucket, key)
             except S3Error:
                 raise e from None
-            if info.etag != multipart_etag([t for _, t in parts]):
+            try:
+                want = multipart_etag([t for _, t in parts])
+            except ValueError:      # part ETags that are not MD5 hex (SSE-KMS / SSE-C, ...)
+                raise e from None
+            if info.etag != want:
                 raise
             return info.etag
         root = ET.fromstring(r.body)

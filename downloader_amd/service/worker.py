@@ -35,7 +35,7 @@ from ..stages import build_stages
 from ..stages.base import EventEmitter, Job, Services, Stage
 from ..stages.jobdir import get_reaper
 from ..utils.config import Config
-from ..utils.log import Logger, get_logger
+from ..utils.log import Logger, get_logger, redact_text
 from ..utils.metrics import Metrics
 from ..utils.trace import Tracer, init_tracer
 from .telemetry import Telemetry
@@ -313,7 +313,7 @@ class Worker:
         delay = min(b.retry_backoff_max_s, b.retry_backoff_s * (2 ** attempt))
         hdrs = dict(d.headers)
         hdrs["x-attempt"] = attempt + 1
-        hdrs["x-last-error"] = err[:512]
+        hdrs["x-last-error"] = redact_text(err)[:512]
         try:
             if b.retry_delay == "queue":
                 # the broker holds the message for `delay`; this delivery (and its prefetch
@@ -331,7 +331,7 @@ class Worker:
 
     async def _dead_letter(self, d: Delivery, err: str) -> None:
         hdrs = dict(d.headers)
-        hdrs["x-last-error"] = err[:512]
+        hdrs["x-last-error"] = redact_text(err)[:512]
         try:
             await self.broker.publish(self.cfg.broker.dead_letter_queue, d.body, hdrs)
             await d.ack()

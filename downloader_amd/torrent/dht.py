@@ -64,9 +64,11 @@ def pack_nodes(nodes: Sequence[Node]) -> bytes:
 
 
 def unpack_nodes(b: bytes) -> List[Node]:
-    now = time.monotonic()
+    """Compact node info from a reply. These nodes are second-hand (a third party vouches
+    for them), so they carry ``seen=0`` - questionable - and are lookup candidates only: a
+    node enters the routing table when it answers us itself (``query``) or queries us."""
     return [Node(b[i:i + 20], (socket.inet_ntoa(b[i + 20:i + 24]),
-                               struct.unpack(">H", b[i + 24:i + 26])[0]), now)
+                               struct.unpack(">H", b[i + 24:i + 26])[0]), 0.0)
             for i in range(0, len(b) - len(b) % 26, 26)]
 
 
@@ -87,11 +89,16 @@ class RoutingTable:
         self.buckets: List[List[Node]] = [[] for _ in range(160)]
 
     def add(self, n: Node) -> None:
-        if n.id == self.own or len(n.id) != 20 or n.addr[1] == 0:
+        """Insert / refresh ``n``, which must have been heard from directly (it answered or
+        queried us from ``n.addr``). A known id keeps its address while that entry is good:
+        another host claiming the id cannot re-point it (BEP-5 node-id hijack)."""
+        if n.id == self.own or len(n.id) != 20 or n.addr[1] == 0 or n.seen <= 0:
             return
         b = self.buckets[bucket_index(self.own, n.id)]
         for i, x in enumerate(b):
             if x.id == n.id:
+                if x.addr != n.addr and n.seen - x.seen < STALE_S:
+                    return
                 b[i] = n
                 return
         if len(b) >= self.k:
@@ -319,10 +326,13 @@ class DHTNode(asyncio.DatagramProtocol):
         task.add_done_callback(self._tasks.discard)
 
     async def _find_node_at(self, addr: Addr, target: bytes) -> List[Node]:
+        """find_node at ``addr``; the responder itself enters the table (``query``), the
+        nodes it names do not - they are pinged so the ones that answer get in."""
         r = await self.query(addr, "find_node", {"target": target})
         nodes = unpack_nodes(r.get(b"nodes", b""))
-        for n in nodes:
-            self.table.add(n)
+        for n in nodes[:K]:
+            if n.id != self.id:
+                self.add_node_addr(n.addr)
         return nodes
 
     async def lookup(self, target: bytes, want_peers: bool = True

@@ -26,6 +26,7 @@ from urllib.parse import quote
 
 from ..net.http import FileSink, TransportError
 from ..ops import hashing
+from ..utils.log import redact_url
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
 from .peer import BLOCK, METADATA_PIECE, PeerConn
@@ -247,11 +248,15 @@ class PiecePicker:
                         out.append((ap.idx, b * BLOCK, ap.block_len(b)))
         return out
 
-    def complete_blocks(self, idx: int) -> None:
+    def complete_blocks(self, idx: int) -> bool:
         """All blocks of active piece ``idx`` arrived: it leaves ``active`` for ``verifying``
-        (not a candidate again unless its hash check fails -> ``requeue``)."""
+        (not a candidate again unless its hash check fails -> ``requeue``). False when it was
+        not active any more: another follow-up (an endgame duplicate finishing the same
+        piece) got there first and owns the verification."""
+        if self.active.pop(idx, None) is None:
+            return False
         self.verifying.add(idx)
-        self.active.pop(idx, None)
+        return True
 
     def release(self, peer_id: int, piece: int, begin: int) -> None:
         ap = self.active.get(piece)
@@ -275,12 +280,12 @@ class PiecePicker:
         fallback = None
         i = 0
         while i < self.n:
-            if i in self.have or i in self.active or i in self.claimed:
+            if i in self.have or i in self.active or i in self.claimed or i in self.verifying:
                 i += 1
                 continue
             j = i
             while j < self.n and j - i < maxp and j not in self.have and j not in self.active \
-                    and j not in self.claimed:
+                    and j not in self.claimed and j not in self.verifying:
                 j += 1
             if not busy_files or not busy_files.get(self.meta.file_at(i * plen), 0):
                 fallback = (i, j)
@@ -612,9 +617,8 @@ class TorrentSession:
                     other = self.peers.get(other_id)
                     if other is not None:
                         await other.cancel(idx, begin, ln)
-        if ap.got < ap.nblocks:
-            return
-        self.picker.complete_blocks(idx)
+        if ap.got < ap.nblocks or not self.picker.complete_blocks(idx):
+            return                  # not complete, or the other follow-up verifies it
         # The piece's buffer is complete and no longer written (every block is state 2), so it
         # is hashed and, if good, written to storage in place - one executor hop, no copy.
         buf = ap.buf
@@ -888,7 +892,8 @@ class TorrentSession:
             r = await self.client.transports.request("GET", url, headers=hdrs,
                                                      sink=FileSink(fd, foff, ln))
             if r.status not in (200, 206) or (r.status == 200 and hdrs) or r.written != ln:
-                raise TransportError(f"webseed {url}: HTTP {r.status}, {r.written}/{ln} B",
+                raise TransportError(f"webseed {redact_url(url)}: HTTP {r.status}, "
+                                     f"{r.written}/{ln} B",
                                      r.status)
             self.webseed_bytes += ln
             self.downloaded += ln

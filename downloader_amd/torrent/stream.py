@@ -33,6 +33,7 @@ from typing import Dict, List, Optional, Set, Tuple
 from ..models import keys
 from ..stages.base import media_type
 from ..net.http import TransportError
+from ..utils.log import redact_url
 from .metainfo import Metainfo
 from .session import TorrentError, webseed_url
 
@@ -386,7 +387,8 @@ class StreamStager:
             r = await self.sv.transports.request(
                 "GET", url, headers=[("Range", f"bytes={foff}-{foff + ln - 1}")])
             if r.status != 206 or len(r.body) != ln:
-                raise TransportError(f"webseed {url}: HTTP {r.status}, {len(r.body)}/{ln} B",
+                raise TransportError(f"webseed {redact_url(url)}: HTTP {r.status}, "
+                                     f"{len(r.body)}/{ln} B",
                                      r.status)
             buf += r.body
         self.fetched_bytes += u.length

@@ -91,11 +91,12 @@ class Logger:
         elif args:
             msg = " ".join([str(msg)] + [str(a) for a in args])
         if isinstance(msg, BaseException):
-            rec["err"] = {"type": type(msg).__name__, "message": str(msg)}
+            rec["err"] = {"type": type(msg).__name__, "message": redact_text(str(msg))}
             msg = str(msg)
         if msg is not None:
-            rec["msg"] = msg
-        rec.update(fields)
+            rec["msg"] = redact_text(msg) if isinstance(msg, str) else msg
+        for k, v in fields.items():
+            rec[k] = redact_text(v) if isinstance(v, str) else v
         self.sink.write(rec)
 
     def trace(self, msg: Any, *a: Any, **kw: Any) -> None:
@@ -168,3 +169,15 @@ def redact_url(url: str) -> str:
             parts.append(f"{k}=***" if eq and _SECRET_PARAM.search(k) else kv)
         query = "&".join(parts)
     return urlunsplit((u.scheme, netloc, u.path, query, u.fragment))
+
+
+_URL_IN_TEXT = re.compile(r"https?://[^\s\"'<>]+")
+
+
+def redact_text(text: str) -> str:
+    """``text`` with every http(s) URL in it passed through ``redact_url``: error messages
+    quote request URLs (a presigned bucket:// relay source, an origin with a token in its
+    query) and must not carry the signature or credential into logs or message headers."""
+    if "://" not in text:
+        return text
+    return _URL_IN_TEXT.sub(lambda m: redact_url(m.group(0)), text)

@@ -980,3 +980,59 @@ def test_udp_tracker_reply_action_checked(run):
                                1, 0, 0, 0, timeout=1.0, retries=0)
         tr.close()
     run(go())
+
+
+def test_dht_second_hand_nodes_and_id_hijack(run):
+    """nodes named in someone else's reply carry seen=0 and never enter the
+    routing table by themselves (only after answering us); a known id's address is not
+    re-pointed by another host while the entry is good."""
+    import time as _t
+
+    from downloader_amd.torrent import dht as D
+
+    own = b"\0" * 20
+    rt = D.RoutingTable(own, k=2)
+    nid = bytes([0x80]) + b"\1" * 19
+    second = D.unpack_nodes(nid + bytes([10, 0, 0, 9]) + struct.pack(">H", 7))
+    assert second[0].seen == 0
+    rt.add(second[0])
+    assert len(rt) == 0                                     # hearsay is not a table entry
+    now = _t.monotonic()
+    rt.add(D.Node(nid, ("10.0.0.1", 1), now))
+    rt.add(D.Node(nid, ("6.6.6.6", 1), now + 1))           # same id, other host: refused
+    assert rt.buckets[159][0].addr == ("10.0.0.1", 1)
+    rt.add(D.Node(nid, ("6.6.6.6", 1), now + D.STALE_S + 1))   # the old entry went stale
+    assert rt.buckets[159][0].addr == ("6.6.6.6", 1)
+
+    async def go():
+        a = await D.DHTNode(host="127.0.0.1").start()
+        b = await D.DHTNode(host="127.0.0.1").start()
+        fake = bytes([0x40]) + b"\2" * 19              # a node b claims exists, that is nobody
+        b.table.add(D.Node(fake, ("127.0.0.1", 9), _t.monotonic()))
+        await a._find_node_at(("127.0.0.1", b.port), fake)
+        await asyncio.sleep(a.timeout + 0.3)            # the ping of the named node times out
+        ids = {n.id for bk in a.table.buckets for n in bk}
+        assert b.id in ids and fake not in ids
+        await a.close()
+        await b.close()
+    run(go(), timeout=30)
+
+
+def test_picker_verifying_pieces_are_not_reclaimed_or_verified_twice():
+    """a piece whose blocks are all in (being hashed / written) is not handed to
+    a webseed run, and the second of two racing follow-ups does not verify it again."""
+    from downloader_amd.torrent.metainfo import FileEntry, Metainfo
+    from downloader_amd.torrent.session import PiecePicker
+    from downloader_amd.torrent.storage import Bitfield
+    n = 8
+    m = Metainfo(b"x" * 20, "t", 16384, b"\0" * 20 * n, [FileEntry(["t"], n * 16384, 0)],
+                 n * 16384)
+    pk = PiecePicker(m, Bitfield(n))
+    pk.active[3] = object()
+    assert pk.complete_blocks(3) is True and 3 in pk.verifying
+    assert pk.complete_blocks(3) is False           # the racing follow-up backs off
+    start, count = pk.claim_run(8 * 16384)
+    claimed = set(range(start, start + count))
+    assert 3 not in claimed and claimed == {0, 1, 2}
+    start, count = pk.claim_run(8 * 16384)
+    assert set(range(start, start + count)) == {4, 5, 6, 7}

@@ -876,3 +876,70 @@ def test_not_enough_space_fails_before_fetching(run, make_cfg, origin_cls, tmp_p
         assert w2.results[0].outcome == "staged", w2.results[0]
         await w2.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+def test_failed_bucket_relay_does_not_log_presigned_signature(run, make_cfg, origin_cls):
+    """ADVICE r2: a bucket:// relay whose presigned source GET fails must not put the
+    X-Amz-Signature / X-Amz-Credential of that URL into logs or the retry headers."""
+    from downloader_amd.s3.fake_server import FaultRule
+    from downloader_amd.utils.log import ListSink, set_default_sink, _default_sink
+
+    async def go():
+        s3, origin, b, w = await _setup(make_cfg, origin_cls, download={
+            "bucket_secure": False, "bucket_server_copy": False}, broker={"max_retries": 0})
+        s3.buckets["src"] = {}
+        s3.put("src", "lib/Movie/m.mkv", os.urandom(100_000))
+        s3.faults.add(FaultRule(method="GET", path_contains="/src/lib/Movie/m.mkv", times=10,
+                                status=403, code="AccessDenied"))
+        uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,lib"
+        await w.submit(api.make_download("leak", "bucket", uri, "MOVIE"))
+        await _wait(w)
+        assert w.results[0].outcome in ("dead", "failed"), w.results[0]
+        dead = b.queues.get("v1.download.dead") or []
+        await w.stop(); await s3.stop(); await origin.stop()
+        return dead
+    saved = _default_sink
+    sink = ListSink()
+    set_default_sink(sink)
+    try:
+        import os as _os
+        old = _os.environ.get("LOG_LEVEL")
+        _os.environ["LOG_LEVEL"] = "info"
+        try:
+            dead = run(go())
+        finally:
+            if old is None:
+                _os.environ.pop("LOG_LEVEL", None)
+            else:
+                _os.environ["LOG_LEVEL"] = old
+    finally:
+        set_default_sink(saved)
+    text = "\n".join(str(r) for r in sink.records)
+    assert "answered HTTP 403" in text                       # the failure is logged ...
+    assert "X-Amz-Signature=***" in text
+    import re
+    for m in re.finditer(r"X-Amz-(Signature|Credential)=([^&\s'\"]*)", text):
+        assert m.group(2) == "***", text[m.start():m.start() + 80]
+    for m in dead:
+        err = m.headers.get("x-last-error", "")
+        assert "X-Amz-Signature=" not in err or "X-Amz-Signature=***" in err
+
+
+def test_lost_complete_reply_with_non_md5_part_etags_keeps_the_s3_error(run):
+    """SSE-KMS / SSE-C part ETags are not MD5 hex; the NoSuchUpload recovery must
+    re-raise the S3 error instead of a ValueError from computing the multipart ETag."""
+    from downloader_amd.s3.client import ObjectInfo, S3Client, S3Error
+
+    class Stub(S3Client):
+        async def _request(self, *a, **kw):
+            raise S3Error("NoSuchUpload", "gone", 404, "k", "b")
+
+        async def head_object(self, bucket, key):
+            return ObjectInfo(key, 10, "whatever-2")
+
+    async def go():
+        c = Stub("127.0.0.1:9", "a", "b")
+        with pytest.raises(S3Error) as ei:
+            await c.complete_multipart_upload("b", "k", "u", [(1, "kms-opaque-1"), (2, "x")])
+        assert ei.value.code == "NoSuchUpload"
+    run(go())
