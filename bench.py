@@ -450,6 +450,9 @@ def main() -> int:
         endpoint, ca = dist.bcast((endpoint, cert[0] if cert else ""))
         if cert:
             args.ca_file = ca
+    # every rank's CPU slice and S3/origin peer, reported by rank 0 (placement evidence for
+    # the driver's 1/2/4/8 runs: disjoint slices, one peer per rank)
+    topo = dist.gather({"cpus": pinned, "peer": endpoint if blob is not None else None})
     nproc = args.procs_per_rank
     if nproc <= 0:   # auto: one worker process per 8 CPUs of the rank's slice, at most 8
         nproc = max(1, min(8, len(pinned or os.sched_getaffinity(0)) // 8))
@@ -494,6 +497,8 @@ def main() -> int:
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
             "peers": args.peers,
             "cpus_per_rank": len(pinned) if pinned else len(os.sched_getaffinity(0)),
+            "rank_cpus": [t["cpus"] for t in topo],
+            "rank_peers": [t["peer"] for t in topo],
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
             "staging": args.staging if args.mode == "tuned" else "disk",

@@ -166,6 +166,7 @@ class Worker:
             pass
         await self.s3.close()
         await self.transports.close()
+        self.tracer.close()             # drains the span exporter thread
         return 1 if had_active and self.active else 0
 
     # ------------------------------------------------------------------ message path

@@ -34,7 +34,8 @@ class ProcessStage(Stage):
         job.logger.info({"files": files})
         out = {"files": files, "downloadPath": root}
         if last.get("streamed"):   # eagerly staged torrent files: the upload stage skips them
-            out["streamed"] = [s for s in last["streamed"] if s["file"] in set(files)]
+            keep = set(files)      # once: a 10k-file torrent streams 10k entries
+            out["streamed"] = [s for s in last["streamed"] if s["file"] in keep]
         return out
 
 

@@ -7,6 +7,7 @@ in message headers so a convert job can be correlated with the download that pro
 """
 from __future__ import annotations
 
+import atexit
 import contextvars
 import json
 import os
@@ -14,8 +15,9 @@ import secrets
 import sys
 import threading
 import time
+from collections import deque
 from contextlib import contextmanager
-from typing import Any, Dict, Iterator, List, Optional, TextIO
+from typing import Any, Deque, Dict, Iterator, List, Optional, TextIO
 
 _current: contextvars.ContextVar[Optional["Span"]] = contextvars.ContextVar("span", default=None)
 
@@ -57,14 +59,87 @@ def parse_traceparent(tp: Optional[str]) -> Optional[tuple]:
     return parts[1], parts[2]
 
 
+class SpanExporter:
+    """JSON-lines span sink on its own thread. Finished spans are queued by the event loop
+    (no serialisation, no file I/O there - round 2 opened and wrote the trace file on the
+    loop thread for every span, ~4 per job at ~1k jobs/s) and written in batches through one
+    open file. The queue is bounded: past ``max_queue`` spans are dropped and counted."""
+
+    def __init__(self, path: str = "", stream: Optional[TextIO] = None, max_queue: int = 100_000):
+        self.path = path
+        self.stream = stream
+        self.max_queue = max_queue
+        self.dropped = 0
+        self.written = 0
+        self._q: Deque[Span] = deque()
+        self._cv = threading.Condition()
+        self._closed = False
+        self._busy = False
+        self._thread = threading.Thread(target=self._run, name="span-export", daemon=True)
+        self._thread.start()
+        atexit.register(self.close)
+
+    def submit(self, span: Span) -> None:
+        with self._cv:
+            if self._closed or len(self._q) >= self.max_queue:
+                self.dropped += 1
+                return
+            self._q.append(span)
+            if len(self._q) == 1:
+                self._cv.notify()
+
+    def _run(self) -> None:
+        f = open(self.path, "a", encoding="utf-8") if self.path else None
+        try:
+            while True:
+                with self._cv:
+                    while not self._q and not self._closed:
+                        self._cv.wait()
+                    if not self._q and self._closed:
+                        return
+                    batch = list(self._q)
+                    self._q.clear()
+                    self._busy = True
+                out = f or self.stream or sys.stderr
+                out.write("".join(json.dumps(s.to_dict(), default=str) + "\n" for s in batch))
+                out.flush()
+                with self._cv:
+                    self.written += len(batch)
+                    self._busy = False
+                    self._cv.notify_all()
+        finally:
+            if f is not None:
+                f.close()
+
+    def flush(self, timeout: float = 5.0) -> bool:
+        """Wait until every queued span is written."""
+        end = time.monotonic() + timeout
+        with self._cv:
+            while self._q or self._busy:
+                left = end - time.monotonic()
+                if left <= 0 or not self._thread.is_alive():
+                    return False
+                self._cv.wait(left)
+        return True
+
+    def close(self, timeout: float = 5.0) -> None:
+        with self._cv:
+            if self._closed:
+                return
+            self._closed = True
+            self._cv.notify_all()
+        self._thread.join(timeout)
+
+
 class Tracer:
     def __init__(self, service: str = "downloader", enabled: bool = True,
                  stream: Optional[TextIO] = None, path: str = ""):
         self.service = service
         self.enabled = enabled
-        self._lock = threading.Lock()
         self._stream = stream
         self._path = path
+        self._exporter: Optional[SpanExporter] = None
+        self._lock = threading.Lock()
         self.finished: List[Span] = []
         self.keep = False
 
@@ -73,13 +148,18 @@ class Tracer:
             self.finished.append(span)
         if not self.enabled:
             return
-        line = json.dumps(span.to_dict(), default=str)
-        with self._lock:
-            if self._path:
-                with open(self._path, "a", encoding="utf-8") as f:
-                    f.write(line + "\n")
-            else:
-                (self._stream or sys.stderr).write(line + "\n")
+        if self._exporter is None:
+            with self._lock:
+                if self._exporter is None:
+                    self._exporter = SpanExporter(self._path, self._stream)
+        self._exporter.submit(span)
+
+    def flush(self, timeout: float = 5.0) -> bool:
+        return self._exporter.flush(timeout) if self._exporter is not None else True
+
+    def close(self) -> None:
+        if self._exporter is not None:
+            self._exporter.close()
 
     @contextmanager
     def span(self, name: str, traceparent: Optional[str] = None, **attrs: Any) -> Iterator[Span]:

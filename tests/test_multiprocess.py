@@ -127,6 +127,29 @@ def test_supervisor_auto_pinning_quota_share():
 
 
 @pytest.mark.slow
+def test_bench_four_ranks_disjoint_cpus_and_own_peers(tmp_path):
+    """The driver's N=4 launch rehearsed on CPU: 4 ranks over gloo, each pinned to its own
+    GPU-slot CPU slice (disjoint, same size) with its own blobd peer, one JSON line whose
+    totals cover all four ranks."""
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error", STAGER_GPU_SLOTS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
+           "--gpus", "4", "--steps", "2", "--warmup", "1", "--size-mb", "2", "--jobs-per-step", "2",
+           "--no-compare-single-put"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["n_gpus"] == 4 and j["config"]["jobs_timed"] == 4 * 2 * 2
+    cpus = [set(c) for c in j["rank_cpus"]]
+    if len(os.sched_getaffinity(0)) >= 4:
+        assert all(cpus) and len({len(c) for c in cpus}) == 1
+        assert sum(len(c) for c in cpus) == len(set().union(*cpus))      # pairwise disjoint
+    peers = j["rank_peers"]
+    assert len(peers) == 4 and all(peers) and len(set(peers)) == 4
+    assert j["timed_sink_bytes"] >= 4 * 2 * 2 * 2_000_000 and j["sink_mismatches"] == 0
+
+
+@pytest.mark.slow
 def test_bench_rank_with_two_worker_processes(tmp_path):
     """--procs-per-rank 2: the rank spawns two worker processes, splits the timed jobs, and
     still prints exactly one JSON line whose byte count the S3 peer confirmed."""

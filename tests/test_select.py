@@ -180,3 +180,29 @@ def test_use_real_logger_switch(monkeypatch):
     assert isinstance(make_test_logger(), NullLogger)
     monkeypatch.setenv("USE_REAL_LOGGER", "1")
     assert not isinstance(make_test_logger(), NullLogger)
+
+
+def test_process_stage_many_file_torrent_is_linear(run, tmp_path):
+    """A 10k-file torrent whose files were all eagerly staged: the process stage filters the
+    streamed entries against the selection in linear time (it rebuilt set(files) once per
+    entry - 10^8 inserts - in round 2)."""
+    import time
+
+    from downloader_amd.stages.base import Job
+    from downloader_amd.stages.process import ProcessStage
+    from downloader_amd.utils.config import load_config
+    root = tmp_path / "job" / "Movie"
+    root.mkdir(parents=True)
+    n = 10_000
+    for i in range(n):
+        (root / f"f{i:05d}.mkv").touch()
+    files = [str(root / f"f{i:05d}.mkv") for i in range(n)]
+    streamed = [{"file": f, "key": f"k{i}", "size": 0} for i, f in enumerate(files)]
+    msg = api.make_download("big", "torrent", "magnet:?xt=urn:btih:" + "0" * 40, "MOVIE")
+    job = Job(msg=msg, media=msg.media, last_stage={"path": str(tmp_path / "job"),
+                                                  "streamed": streamed})
+    st = ProcessStage(load_config(env={}), None)
+    t0 = time.perf_counter()
+    out = run(st.run(job))
+    assert time.perf_counter() - t0 < 5.0
+    assert len(out["files"]) == n and len(out["streamed"]) == n

@@ -100,6 +100,41 @@ def test_trace_spans_nest_and_propagate():
     assert parse_traceparent("garbage") is None
 
 
+def test_trace_export_off_the_calling_thread(tmp_path, monkeypatch):
+    """Spans are serialised and written by the exporter thread through one open file: the
+    thread that finishes a span (the event loop) neither opens the trace file nor
+    json-encodes; flush() waits for the queue, close() drains it."""
+    import builtins
+    import threading
+
+    import downloader_amd.utils.trace as T
+    path = str(tmp_path / "spans.jsonl")
+    caller = threading.current_thread()
+    opens, dumps = [], []
+    real_open, real_dumps = builtins.open, T.json.dumps
+
+    def spy_open(*a, **kw):
+        opens.append(threading.current_thread() is caller)
+        return real_open(*a, **kw)
+
+    def spy_dumps(*a, **kw):
+        dumps.append(threading.current_thread() is caller)
+        return real_dumps(*a, **kw)
+    monkeypatch.setattr(builtins, "open", spy_open)
+    monkeypatch.setattr(T.json, "dumps", spy_dumps)
+    t = Tracer("downloader", enabled=True, path=path)
+    for i in range(500):
+        with t.span("job", n=i):
+            with t.span("stage.upload"):
+                pass
+    assert t.flush(10)
+    t.close()
+    monkeypatch.setattr(builtins, "open", real_open)
+    lines = real_open(path).read().splitlines()
+    assert len(lines) == 1000 and not any(opens) and not any(dumps) and opens
+    assert [json.loads(x)["name"] for x in lines[:2]] == ["stage.upload", "job"]
+
+
 def test_metrics_registry_exposition():
     m = Metrics()
     m.bytes_downloaded.labels("http").inc(10)
