@@ -28,8 +28,8 @@
 //   sample    spliced like discard, but a window of --sample-len bytes every --sample-stride
 //             bytes (plus the body's last window) is read and kept, then compared with the
 //             bytes the origin generator produced for that object once its offset is known
-//   verify    every byte folded into the checksum, compared at completion with the checksum
-//             of the generator's bytes for the same range
+//   verify    every byte CRC32C'd on arrival, compared at completion with the CRC32C of the
+//             generator's bytes for the same range
 // An S3 object is matched to its origin object through the key the staging service writes,
 // `<id>/original/<base64(basename)>`, and the /media/<basename> requests this process served
 // (size, seed). Multipart parts are checked at CompleteMultipartUpload, when their offsets are
@@ -89,7 +89,7 @@ struct Sample {
 // What the sample / verify sinks keep of one PUT body until its object offset is known.
 struct BodyCheck {
   uint64_t len = 0;
-  uint64_t sum = 0;              // verify: checksum of every byte
+  uint64_t sum = 0;              // verify: CRC32C of every byte
   std::vector<Sample> windows;   // sample
 };
 
@@ -244,19 +244,19 @@ inline const uint8_t* pool_at(uint64_t o, uint64_t seed, uint64_t& avail) {
 // Does `chk` (a body received for bytes [off, off + chk.len) of the object with `seed`) match
 // what the origin generated for that range?
 bool check_range(const BodyCheck& chk, uint64_t off, uint64_t seed) {
-  if (g_sink == kSinkVerify) {
-    Summer s;
+  if (g_sink == kSinkVerify) {    // CRC32C of the generated range vs of the received body
+    uint32_t c = 0;
     uint64_t o = off, left = chk.len;
     while (left) {
       uint64_t avail;
       const uint8_t* p = pool_at(o, seed, avail);
       uint64_t k = std::min(left, avail);
-      s.feed(p, (size_t)k);
+      c = crc32c_update(c, p, (size_t)k);
       o += k;
       left -= k;
     }
     g_verify_bytes += chk.len;
-    return s.final() == chk.sum;
+    return c == (uint32_t)chk.sum;
   }
   for (const Sample& w : chk.windows) {
     uint64_t o = off + w.pos, i = 0;
@@ -283,12 +283,14 @@ struct Consumer {
   uint32_t crc = 0;
   EVP_MD_CTX* md5 = nullptr;
   std::vector<Sample>* windows = nullptr;   // sample sink
+  bool vcrc_on = false;                     // verify sink: CRC32C of every byte
+  uint32_t vcrc = 0;
   uint64_t total = 0;                       // payload length (window layout)
   int64_t corrupt_at = -1;                  // fault injection: flip this payload byte
   ~Consumer() {
     if (md5) EVP_MD_CTX_free(md5);
   }
-  bool needs_all() const { return fold || crc_on || md5 != nullptr || out != nullptr; }
+  bool needs_all() const { return fold || crc_on || vcrc_on || md5 != nullptr || out != nullptr; }
   uint64_t tail_start() const { return total > g_sample_len ? total - g_sample_len : 0; }
   bool in_window(uint64_t pos) const {
     return pos % g_sample_stride < g_sample_len || pos >= tail_start();
@@ -324,6 +326,7 @@ struct Consumer {
     if (fold) sum.feed(p, k);
     if (out && out->size() < keep) out->append((const char*)p, std::min(k, keep - out->size()));
     if (crc_on) crc = crc32c_update(crc, p, k);
+    if (vcrc_on) vcrc = crc32c_update(vcrc, p, k);
     if (md5) EVP_DigestUpdate(md5, p, k);
     if (windows) sample(pos, p, k);
   }
@@ -931,7 +934,7 @@ class Conn {
         EVP_DigestInit_ex(c.md5, EVP_md5(), nullptr);
       }
       const bool small = dlen <= g_keep_bytes;
-      c.fold = small || !g_discard;
+      c.fold = small || g_sink == kSinkChecksum;
       if (small) {
         c.out = &o.data;
         c.keep = g_keep_bytes;
@@ -946,6 +949,7 @@ class Conn {
           c.windows = &chk.windows;
           c.total = dlen;
         }
+        if (g_sink == kSinkVerify && media_like) c.vcrc_on = true;
       }
       if ((c.crc_on || c.md5) && g_s3_corrupt_rate > 0 && dlen > 0 &&
           std::uniform_real_distribution<double>(0, 1)(rng) < g_s3_corrupt_rate)
@@ -984,10 +988,10 @@ class Conn {
       }
       if (!small) o.data.clear();
       o.size = got;
-      o.sum = c.sum.final();
+      o.sum = c.vcrc_on && !c.fold ? c.vcrc : c.sum.final();
       o.etag = hex64(o.sum, o.size);
       chk.len = got;
-      chk.sum = o.sum;
+      chk.sum = c.vcrc;
       extra = "ETag: \"" + o.etag + "\"\r\n" + extra;
       if (part) {
         std::lock_guard<std::mutex> lk(g_mu);

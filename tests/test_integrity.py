@@ -353,3 +353,49 @@ def test_bucket_relay_parts_pinned_to_listed_etag(run, origin_cls):
         await c.close()
         await s3.stop()
     run(go())
+
+
+@pytest.mark.parametrize("sink", ["sample", "verify"])
+def test_blobd_sink_detects_wrong_torn_and_reordered_objects(sink):
+    """The bench's S3 sink compares each staged object with what its origin generated: an
+    exact copy passes; other bytes, a truncated object and swapped multipart parts are all
+    counted as mismatches (so the headline cannot pass while staging wrong bytes)."""
+    from downloader_amd.bench.infra import Blobd
+    n = 3 * 1_048_576 + 5
+    key = "/bk/job/original/" + base64.b64encode(b"x.mkv").decode()
+    with Blobd(sink=sink) as b:
+        port = b.port
+        assert _put(port, "/bk", b"", {})[0] == 200
+        with urllib.request.urlopen(b.media_url("x.mkv", n, 7)) as r:
+            good = r.read()
+
+        def mp(parts):
+            s = socket.create_connection(("127.0.0.1", port))
+            s.sendall(f"POST {key}?uploads HTTP/1.1\r\nHost: x\r\nContent-Length: 0\r\n"
+                      "Connection: close\r\n\r\n".encode())
+            resp = b""
+            while True:
+                d = s.recv(65536)
+                if not d:
+                    break
+                resp += d
+            uid = resp.split(b"<UploadId>")[1].split(b"</UploadId>")[0].decode()
+            for num, body in parts:
+                assert _put(port, f"{key}?partNumber={num}&uploadId={uid}", body, {})[0] == 200
+            s = socket.create_connection(("127.0.0.1", port))
+            s.sendall(f"POST {key}?uploadId={uid} HTTP/1.1\r\nHost: x\r\nContent-Length: 0\r\n"
+                      "Connection: close\r\n\r\n".encode())
+            while s.recv(65536):
+                pass
+        assert _put(port, key, good, {})[0] == 200
+        assert b.stats()["verify_mismatches"] == 0
+        bad = bytearray(good)
+        bad[2_000_000] ^= 0xFF          # a byte outside every sampled window still differs in
+        bad[0] ^= 0xFF                  # ... and one inside the first window
+        assert _put(port, key, bytes(bad), {})[0] == 200
+        assert _put(port, key, good[:-1], {})[0] == 200                    # truncated
+        h = 1 << 21
+        mp([(1, good[:h]), (2, good[h:])])                                   # coherent
+        mp([(1, good[h:2 * h]), (2, good[:h] + good[2 * h:])])              # parts swapped
+        st = b.stats()
+        assert st["verify_objects"] == 5 and st["verify_mismatches"] == 3, st
