@@ -50,13 +50,14 @@ METRIC = "MB/s staged end-to-end (download->S3) + p50 job latency"
 def parse() -> argparse.Namespace:
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1, help="worker processes (one per GPU slot)")
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--size-mb", type=float, default=100.0, help="object size in MB (1e6 B)")
     p.add_argument("--mode", choices=["tuned", "reference"], default="tuned")
-    p.add_argument("--concurrency", type=int, default=8,
-                   help="jobs in flight per worker (8: best MB/s on the build box, p50 +4 ms vs 4: "
-                        "profiles/bench_defaults_r1.jsonl)")
+    p.add_argument("--concurrency", type=int, default=4,
+                   help="jobs in flight per worker process (4: with 2-part multipart jobs this "
+                        "keeps 16 relays in flight per rank - 70.3 GB/s, p50 11 ms vs 49.3 GB/s, "
+                        "27 ms at 8: profiles/r3_mp_sweep)")
     p.add_argument("--jobs-per-step", type=int, default=64,
                    help="jobs per worker per step (64: ~1 s timed at N=1 for 10 steps; 16/32/64 "
                         "give the same MB/s, profiles/s2_r1/jobs_ab.jsonl)")

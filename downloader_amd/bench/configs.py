@@ -193,6 +193,10 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["webseed_verify_depth_gpu"] = a.webseed_verify_depth_gpu
             if getattr(a, "no_gpu_prewarm", False):
                 dl["gpu_prewarm"] = False
+            if getattr(a, "stream_verify", ""):
+                dl["stream_verify_backend"] = a.stream_verify
+            if getattr(a, "stream_gpu_pending", 0):
+                dl["stream_gpu_pending"] = a.stream_gpu_pending
             if getattr(a, "relay_trim_s", None) is not None:
                 dl["relay_pool_idle_trim_s"] = a.relay_trim_s
             part_mb = getattr(a, "part_mb", 0)
@@ -225,6 +229,10 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 pool = native().relay_pool_stats()
             except Exception:
                 pool = {}
+            gpu_relay = {}
+            if getattr(a, "stream_verify", "") == "gpu":
+                from downloader_amd.ops import hashing
+                gpu_relay = hashing.gpu_relay_stats()
             await w.stop()
             # the median rep is the one reported in full
             reps_sorted = sorted(reps, key=lambda x: x[0])
@@ -245,6 +253,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"],
             "worker_rss_peak_MB": rss["rss_peak_MB"],
             "relay_pool_after": pool,
+            **({"stream_verify": a.stream_verify, "gpu_relay": gpu_relay}
+               if getattr(a, "stream_verify", "") else {}),
             "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps],
             # per rep (the first is the worker's cold job): job seconds, summed relay seconds
             # of all parts, worker and peer CPU seconds
@@ -542,6 +552,11 @@ def main(argv=None) -> int:
                     help="fetched runs queued per stream when the GPU batcher verifies them")
     ap.add_argument("--torrent-stream", choices=["auto", "always", "off"], default="auto",
                     help="download.torrent_stream: webseed->S3 relay (auto) or disk staging (off)")
+    ap.add_argument("--stream-verify", choices=["cpu", "gpu"], default="",
+                    help="download.stream_verify_backend: relayed parts' pieces hashed by the "
+                         "host multi-buffer SHA-1 or the gfx950 PartHasher")
+    ap.add_argument("--stream-gpu-pending", type=int, default=0,
+                    help="download.stream_gpu_pending (parts per job awaiting GPU digests)")
     ap.add_argument("--stream-parallel", type=int, default=0,
                     help="download.torrent_stream_parallel (parts in flight per job)")
     ap.add_argument("--part-mb", type=int, default=0,

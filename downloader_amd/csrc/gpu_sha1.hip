@@ -35,13 +35,19 @@
 #include <atomic>
 #include <chrono>
 #include <cerrno>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <fcntl.h>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <unistd.h>
+#include <unordered_map>
 #include <vector>
+
+#include "gpu_part_api.h"
 
 namespace py = pybind11;
 
@@ -206,20 +212,9 @@ __device__ __forceinline__ void sha1_run16(Sha1State& s, const uint8_t* p, int64
   }
 }
 
-// One lane hashes one piece. data holds n_pieces consecutive pieces of piece_len bytes,
-// the last one possibly `last_len` bytes. If `expected` is non-null, ok[i] = digest matches,
-// otherwise digests are written to `out` (5 words, big-endian byte order as bytes).
-template <int ALIGN, bool B3 = true, bool PF = true>
-__global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ data,
-                                                   int64_t piece_len, int64_t last_len,
-                                                   int n_pieces,
-                                                   const uint8_t* __restrict__ expected,
-                                                   uint8_t* __restrict__ ok,
-                                                   uint8_t* __restrict__ out) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_pieces) return;
-  const int64_t len = (i == n_pieces - 1) ? last_len : piece_len;
-  const uint8_t* p = data + (int64_t)i * piece_len;
+// SHA-1 of `len` bytes at p (one lane, one piece): whole blocks, then tail + padding.
+template <int ALIGN, bool B3, bool PF>
+__device__ __forceinline__ void sha1_piece(const uint8_t* p, int64_t len, uint32_t hv[5]) {
   Sha1State s{0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
   uint32_t w[16];
   const int64_t nfull = len >> 6;
@@ -255,7 +250,38 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
     }
     sha1_block<B3>(s, w);
   }
-  uint32_t hv[5] = {s.h0, s.h1, s.h2, s.h3, s.h4};
+  hv[0] = s.h0;
+  hv[1] = s.h1;
+  hv[2] = s.h2;
+  hv[3] = s.h3;
+  hv[4] = s.h4;
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* o, const uint32_t hv[5]) {
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    o[4 * k] = (uint8_t)(hv[k] >> 24);
+    o[4 * k + 1] = (uint8_t)(hv[k] >> 16);
+    o[4 * k + 2] = (uint8_t)(hv[k] >> 8);
+    o[4 * k + 3] = (uint8_t)hv[k];
+  }
+}
+
+// One lane hashes one piece. data holds n_pieces consecutive pieces of piece_len bytes,
+// the last one possibly `last_len` bytes. If `expected` is non-null, ok[i] = digest matches,
+// otherwise digests are written to `out` (5 words, big-endian byte order as bytes).
+template <int ALIGN, bool B3 = true, bool PF = true>
+__global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ data,
+                                                   int64_t piece_len, int64_t last_len,
+                                                   int n_pieces,
+                                                   const uint8_t* __restrict__ expected,
+                                                   uint8_t* __restrict__ ok,
+                                                   uint8_t* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pieces) return;
+  const int64_t len = (i == n_pieces - 1) ? last_len : piece_len;
+  uint32_t hv[5];
+  sha1_piece<ALIGN, B3, PF>(data + (int64_t)i * piece_len, len, hv);
   if (expected) {
     const uint8_t* ex = expected + (int64_t)i * 20;
     bool good = true;
@@ -267,15 +293,22 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
     }
     ok[i] = good ? 1 : 0;
   } else {
-    uint8_t* o = out + (int64_t)i * 20;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      o[4 * k] = (uint8_t)(hv[k] >> 24);
-      o[4 * k + 1] = (uint8_t)(hv[k] >> 16);
-      o[4 * k + 2] = (uint8_t)(hv[k] >> 8);
-      o[4 * k + 3] = (uint8_t)hv[k];
-    }
+    store_digest(out + (int64_t)i * 20, hv);
   }
+}
+
+// Batch of relayed parts (PartHasher): lane i hashes lane_len[i] bytes at data + lane_off[i]
+// (pieces of many parts packed back to back in one device slot) into out + 20 * i.
+template <int ALIGN>
+__global__ __launch_bounds__(256) void sha1_lanes(const uint8_t* __restrict__ data,
+                                                  const int64_t* __restrict__ lane_off,
+                                                  const int64_t* __restrict__ lane_len, int n,
+                                                  uint8_t* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t hv[5];
+  sha1_piece<ALIGN, true, ALIGN == 16>(data + lane_off[i], lane_len[i], hv);
+  store_digest(out + (int64_t)i * 20, hv);
 }
 
 // Chunk-streamed variant: lane k owns piece (first + k) of a window - or, with a piece list,
@@ -762,6 +795,402 @@ class GpuVerifier {
   size_t meta_stride_ = 0;
 };
 
+// ---------------------------------------------------------------------------------------
+// PartHasher: piece SHA-1 of parts the hashed relay (csrc/transfer.cpp) has just moved
+// webseed -> S3, so the host no longer spends ~40 % of a torrent job's worker CPU on the
+// multi-buffer SHA-1 (docs/PERFORMANCE.md). SHA-1 is serial inside a piece, so a piece costs
+// piece_len / ~58 MB/s on one lane (72 ms for 4 MiB) whatever else runs: throughput comes
+// from many pieces per launch, and the latency is hidden by the stager keeping parts in
+// flight. Hence:
+//   * the relay submits the finished part (page-locked pooled buffer) and moves on; the
+//     dispatcher thread DMAs it into the open device slot at once on a copy stream, and the
+//     relay's lease on the buffer ends when that copy completes - not when the hash does;
+//   * a slot (up to slot_bytes / max_lanes pieces of any number of parts) is launched as ONE
+//     sha1_lanes kernel as soon as a compute stream is idle; while all are busy the open
+//     slot keeps filling, so batches grow with the arrival rate (self-balancing: at R bytes/s
+//     and T = per-piece kernel time over Q streams, a batch holds ~R*T/Q bytes);
+//   * digests return with one D2H per slot; waiters are woken per ticket.
+// Compute streams are capped at 4 = GPU_MAX_HW_QUEUES (more would share hardware queues and
+// serialise). A HIP error marks the hasher broken: queued and later parts are refused or
+// failed, and the relay falls back to the host multi-buffer SHA-1.
+class PartHasher {
+ public:
+  PartHasher(int device, int64_t slot_bytes, int slots, int streams, int max_lanes)
+      : device_(device), slot_bytes_(slot_bytes), max_lanes_(max_lanes) {
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) throw std::runtime_error("no such HIP device");
+    if (slots < 2 || streams < 1 || slot_bytes < (1 << 20) || max_lanes < 64)
+      throw std::invalid_argument("PartHasher: bad geometry");
+    HIP_CHECK(hipSetDevice(device_));
+    HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+    streams_.resize((size_t)std::min(streams, 4));
+    for (auto& st : streams_) {
+      HIP_CHECK(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
+      st.slot = -1;
+    }
+    slots_.resize((size_t)slots);
+    for (auto& sl : slots_) {
+      HIP_CHECK(hipMalloc((void**)&sl.d_data, (size_t)slot_bytes_));
+      HIP_CHECK(hipMalloc((void**)&sl.d_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t)));
+      HIP_CHECK(hipMalloc((void**)&sl.d_dig, (size_t)max_lanes_ * 20));
+      HIP_CHECK(hipHostMalloc((void**)&sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
+                              hipHostMallocDefault));
+      HIP_CHECK(hipHostMalloc((void**)&sl.h_dig, (size_t)max_lanes_ * 20, hipHostMallocDefault));
+      HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    api_.abi = GPU_PART_API_ABI;
+    api_.ctx = this;
+    api_.reg = [](void* c, void* p, size_t n) { return ((PartHasher*)c)->reg(p, n); };
+    api_.unreg = [](void* c, void* p) { ((PartHasher*)c)->unreg(p); };
+    api_.submit = [](void* c, const uint8_t* d, int64_t len, int64_t pl) {
+      return ((PartHasher*)c)->submit(d, len, pl);
+    };
+    api_.wait = [](void* c, uint64_t t, int ph, uint8_t* out, size_t ol, char* err, size_t el) {
+      return ((PartHasher*)c)->wait(t, ph, out, ol, err, el);
+    };
+    thread_ = std::thread([this] { run(); });
+  }
+
+  ~PartHasher() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (thread_.joinable()) thread_.join();
+    hipSetDevice(device_);
+    hipStreamSynchronize(copy_);
+    for (auto& st : streams_) {
+      hipStreamSynchronize(st.s);
+      hipStreamDestroy(st.s);
+    }
+    hipStreamDestroy(copy_);
+    for (auto& sl : slots_) {
+      hipFree(sl.d_data);
+      hipFree(sl.d_lane);
+      hipFree(sl.d_dig);
+      hipHostFree(sl.h_lane);
+      hipHostFree(sl.h_dig);
+      hipEventDestroy(sl.copied);
+      hipEventDestroy(sl.done);
+    }
+    for (hipEvent_t e : free_events_) hipEventDestroy(e);
+  }
+
+  const GpuPartHashApi* api() const { return &api_; }
+
+  int reg(void* p, size_t n) {
+    if (hipSetDevice(device_) != hipSuccess) return -1;
+    return hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess ? 0 : -1;
+  }
+  void unreg(void* p) {
+    hipSetDevice(device_);
+    hipHostUnregister(p);
+  }
+
+  uint64_t submit(const uint8_t* data, int64_t len, int64_t piece_len) {
+    if (len <= 0 || piece_len <= 0) return 0;
+    const int64_t np = (len + piece_len - 1) / piece_len;
+    if (np > max_lanes_ || len > slot_bytes_) return 0;
+    std::lock_guard<std::mutex> g(mu_);
+    if (broken_ || stop_) return 0;
+    uint64_t t = ++seq_;
+    Job& j = jobs_[t];
+    j.host = data;
+    j.len = len;
+    j.piece_len = piece_len;
+    j.np = (int)np;
+    queue_.push_back(t);
+    submitted_++;
+    cv_.notify_all();
+    return t;
+  }
+
+  int wait(uint64_t t, int phase, uint8_t* out, size_t out_len, char* err, size_t errlen) {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = jobs_.find(t);
+    if (it == jobs_.end()) return fail(err, errlen, "unknown ticket");
+    Job* j = &it->second;
+    wcv_.wait(lk, [&] { return !j->err.empty() || (phase == GPU_PART_COPIED ? j->copied : j->done); });
+    if (!j->err.empty()) {
+      std::string e = j->err;
+      if (phase == GPU_PART_DONE || j->done) jobs_.erase(it);
+      return fail(err, errlen, e.c_str());
+    }
+    if (phase == GPU_PART_DONE) {
+      if (out_len < j->digests.size()) return fail(err, errlen, "digest buffer too small");
+      memcpy(out, j->digests.data(), j->digests.size());
+      jobs_.erase(it);
+    }
+    return 0;
+  }
+
+  py::dict stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    py::dict d;
+    d["submitted"] = submitted_;
+    d["launches"] = launches_;
+    d["lanes"] = lanes_total_;
+    d["max_batch_lanes"] = max_batch_lanes_;
+    d["broken"] = broken_;
+    d["pending"] = jobs_.size();
+    return d;
+  }
+
+ private:
+  struct Job {
+    const uint8_t* host = nullptr;
+    int64_t len = 0, piece_len = 0;
+    int np = 0;
+    int slot = -1, lane0 = 0;
+    hipEvent_t copy_ev = nullptr;
+    bool copied = false, done = false;
+    std::string err, digests;
+  };
+  struct Slot {
+    uint8_t* d_data = nullptr;
+    int64_t* d_lane = nullptr;
+    uint8_t* d_dig = nullptr;
+    int64_t* h_lane = nullptr;   // [off x max_lanes][len x max_lanes]
+    uint8_t* h_dig = nullptr;
+    hipEvent_t copied = nullptr, done = nullptr;
+    int64_t used = 0;
+    int lanes = 0;
+    bool align16 = true;
+    std::vector<uint64_t> jobs;
+    int state = 0;               // 0 free, 1 filling, 2 closed (waiting for a stream), 3 running
+    std::chrono::steady_clock::time_point opened;
+  };
+  struct Stream {
+    hipStream_t s = nullptr;
+    int slot = -1;
+  };
+
+  static int fail(char* err, size_t errlen, const char* msg) {
+    if (err && errlen) {
+      strncpy(err, msg, errlen - 1);
+      err[errlen - 1] = 0;
+    }
+    return -1;
+  }
+
+  hipEvent_t take_event() {
+    if (!free_events_.empty()) {
+      hipEvent_t e = free_events_.back();
+      free_events_.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
+
+  // Everything below runs on the dispatcher thread; mu_ guards jobs_/queue_ and flags.
+  void run() {
+    try {
+      HIP_CHECK(hipSetDevice(device_));
+      int filling = -1;
+      std::deque<uint64_t> copying;            // tickets whose H2D is in flight, in order
+      for (;;) {
+        std::deque<uint64_t> fresh;
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          if (queue_.empty() && copying.empty() && !any_running() && !any_closed() &&
+              !(filling >= 0 && slots_[(size_t)filling].lanes > 0)) {
+            cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+          }
+          if (stop_ && queue_.empty() && copying.empty() && !any_running() && !any_closed() &&
+              !(filling >= 0 && slots_[(size_t)filling].lanes > 0))
+            return;
+          fresh.swap(queue_);
+        }
+        bool progressed = !fresh.empty();
+        // 1. DMA new parts into the open slot (a new one when it is full)
+        while (!fresh.empty()) {
+          const uint64_t t = fresh.front();
+          Job* j;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            j = &jobs_.at(t);
+          }
+          if (filling >= 0) {
+            Slot& f = slots_[(size_t)filling];
+            const int64_t off = (f.used + 255) & ~(int64_t)255;
+            if (off + j->len > slot_bytes_ || f.lanes + j->np > max_lanes_) {
+              f.state = 2;                    // full: closed, launched when a stream frees
+              HIP_CHECK(hipEventRecord(f.copied, copy_));
+              filling = -1;
+            }
+          }
+          if (filling < 0) {
+            filling = free_slot();
+            if (filling < 0) break;            // every slot busy: the part waits queued
+            Slot& f = slots_[(size_t)filling];
+            f.state = 1;
+            f.used = 0;
+            f.lanes = 0;
+            f.align16 = true;
+            f.jobs.clear();
+            f.opened = std::chrono::steady_clock::now();
+          }
+          Slot& f = slots_[(size_t)filling];
+          const int64_t off = (f.used + 255) & ~(int64_t)255;
+          HIP_CHECK(hipMemcpyAsync(f.d_data + off, j->host, (size_t)j->len, hipMemcpyHostToDevice,
+                                   copy_));
+          j->copy_ev = take_event();
+          HIP_CHECK(hipEventRecord(j->copy_ev, copy_));
+          j->slot = filling;
+          j->lane0 = f.lanes;
+          for (int k = 0; k < j->np; ++k) {
+            const int64_t po = (int64_t)k * j->piece_len;
+            f.h_lane[f.lanes + k] = off + po;
+            f.h_lane[max_lanes_ + f.lanes + k] = std::min(j->piece_len, j->len - po);
+          }
+          if (j->piece_len % 16) f.align16 = false;
+          f.lanes += j->np;
+          f.used = off + j->len;
+          f.jobs.push_back(t);
+          copying.push_back(t);
+          fresh.pop_front();
+        }
+        if (!fresh.empty()) {                   // no free slot: back to the head of the queue
+          std::lock_guard<std::mutex> g(mu_);
+          for (auto it = fresh.rbegin(); it != fresh.rend(); ++it) queue_.push_front(*it);
+        }
+        // 2. completed copies: the relay may reuse those buffers
+        while (!copying.empty()) {
+          Job* j;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            j = &jobs_.at(copying.front());
+          }
+          hipError_t q = hipEventQuery(j->copy_ev);
+          if (q == hipErrorNotReady) break;
+          HIP_CHECK(q);
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            j->copied = true;
+            free_events_.push_back(j->copy_ev);
+            j->copy_ev = nullptr;
+          }
+          wcv_.notify_all();
+          copying.pop_front();
+          progressed = true;
+        }
+        // 3. finished kernels: publish digests, free slot and stream
+        for (auto& st : streams_) {
+          if (st.slot < 0) continue;
+          Slot& sl = slots_[(size_t)st.slot];
+          hipError_t q = hipEventQuery(sl.done);
+          if (q == hipErrorNotReady) continue;
+          HIP_CHECK(q);
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            for (uint64_t t : sl.jobs) {
+              Job& j = jobs_.at(t);
+              j.digests.assign((const char*)sl.h_dig + (size_t)j.lane0 * 20, (size_t)j.np * 20);
+              j.done = true;
+            }
+          }
+          wcv_.notify_all();
+          sl.state = 0;
+          sl.jobs.clear();
+          st.slot = -1;
+          progressed = true;
+        }
+        // 4. launch: closed slots first (oldest first), then the open one, on idle streams
+        for (auto& st : streams_) {
+          if (st.slot >= 0) continue;
+          int pick = oldest(2);
+          if (pick < 0 && filling >= 0 && slots_[(size_t)filling].lanes > 0) {
+            pick = filling;
+            HIP_CHECK(hipEventRecord(slots_[(size_t)pick].copied, copy_));
+            filling = -1;
+          }
+          if (pick < 0) break;
+          launch(pick, st);
+          progressed = true;
+        }
+        if (!progressed) {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait_for(lk, std::chrono::microseconds(200), [&] { return stop_ || !queue_.empty(); });
+        }
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(mu_);
+      broken_ = true;
+      for (auto& kv : jobs_)
+        if (!kv.second.done) kv.second.err = std::string("GPU part hasher: ") + e.what();
+      queue_.clear();
+      wcv_.notify_all();
+    }
+  }
+
+  bool any_running() const {
+    for (auto& st : streams_)
+      if (st.slot >= 0) return true;
+    return false;
+  }
+  bool any_closed() const {
+    for (auto& sl : slots_)
+      if (sl.state == 2) return true;
+    return false;
+  }
+  int free_slot() const {
+    for (size_t i = 0; i < slots_.size(); ++i)
+      if (slots_[i].state == 0) return (int)i;
+    return -1;
+  }
+  int oldest(int state) const {
+    int best = -1;
+    for (size_t i = 0; i < slots_.size(); ++i)
+      if (slots_[i].state == state && (best < 0 || slots_[i].opened < slots_[(size_t)best].opened))
+        best = (int)i;
+    return best;
+  }
+
+  void launch(int si, Stream& st) {
+    Slot& sl = slots_[(size_t)si];
+    HIP_CHECK(hipStreamWaitEvent(st.s, sl.copied, 0));
+    HIP_CHECK(hipMemcpyAsync(sl.d_lane, sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
+                             hipMemcpyHostToDevice, st.s));
+    const int block = 64, grid = (sl.lanes + block - 1) / block;
+    if (sl.align16)
+      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st.s, sl.d_data, sl.d_lane,
+                         sl.d_lane + max_lanes_, sl.lanes, sl.d_dig);
+    else
+      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st.s, sl.d_data, sl.d_lane,
+                         sl.d_lane + max_lanes_, sl.lanes, sl.d_dig);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(sl.h_dig, sl.d_dig, (size_t)sl.lanes * 20, hipMemcpyDeviceToHost, st.s));
+    HIP_CHECK(hipEventRecord(sl.done, st.s));
+    sl.state = 3;
+    st.slot = si;
+    std::lock_guard<std::mutex> g(mu_);
+    launches_++;
+    lanes_total_ += (uint64_t)sl.lanes;
+    max_batch_lanes_ = std::max<uint64_t>(max_batch_lanes_, (uint64_t)sl.lanes);
+  }
+
+  int device_;
+  int64_t slot_bytes_;
+  int max_lanes_;
+  hipStream_t copy_ = nullptr;
+  std::vector<Stream> streams_;
+  std::vector<Slot> slots_;
+  std::vector<hipEvent_t> free_events_;
+  std::mutex mu_;
+  std::condition_variable cv_, wcv_;
+  std::deque<uint64_t> queue_;
+  std::unordered_map<uint64_t, Job> jobs_;
+  uint64_t seq_ = 0, submitted_ = 0, launches_ = 0, lanes_total_ = 0, max_batch_lanes_ = 0;
+  bool stop_ = false, broken_ = false;
+  GpuPartHashApi api_{};
+  std::thread thread_;
+};
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -862,4 +1291,42 @@ PYBIND11_MODULE(_gpuhash, m) {
           py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 5,
           "(ms_prefetch, ms_no_prefetch): kernel time per launch, device-resident data")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
+  py::class_<PartHasher>(m, "PartHasher")
+      .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes) {
+             py::gil_scoped_release rel;
+             return new PartHasher(device, slot_bytes, slots, streams, max_lanes);
+           }),
+           py::arg("device") = 0, py::arg("slot_bytes") = (int64_t)1 << 30, py::arg("slots") = 8,
+           py::arg("streams") = 4, py::arg("max_lanes") = 16384)
+      .def(
+          "api",
+          [](PartHasher& h) {
+            return py::capsule((void*)h.api(), "downloader_amd.gpu_part_api");
+          },
+          py::keep_alive<0, 1>(),
+          "PyCapsule of the C ABI (gpu_part_api.h) for _native.set_gpu_part_hasher")
+      .def(
+          "hash",
+          [](PartHasher& h, const py::buffer& b, int64_t piece_len) {
+            // test / bench entry: the buffer is registered, submitted and waited for here
+            py::buffer_info info = b.request();
+            const int64_t n = (int64_t)info.size * (int64_t)info.itemsize;
+            const int64_t np = piece_len > 0 ? (n + piece_len - 1) / piece_len : 0;
+            std::string out((size_t)np * 20, '\0');
+            char err[256] = {0};
+            int rc;
+            {
+              py::gil_scoped_release rel;
+              void* p = info.ptr;
+              bool r = h.reg(p, (size_t)n) == 0;
+              uint64_t t = h.submit((const uint8_t*)p, n, piece_len);
+              rc = t ? h.wait(t, GPU_PART_DONE, (uint8_t*)out.data(), out.size(), err, sizeof err)
+                     : -1;
+              if (r) h.unreg(p);
+            }
+            if (rc != 0) throw std::runtime_error(err[0] ? err : "PartHasher refused the part");
+            return py::bytes(out);
+          },
+          py::arg("data"), py::arg("piece_len"))
+      .def("stats", &PartHasher::stats);
 }

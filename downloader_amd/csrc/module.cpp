@@ -69,6 +69,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
   ResponseHead g, p;
   std::string gerr, pbody, digests, head, tail, crc_b64;
   int64_t moved = 0;
+  uint64_t ticket = 0;
   {
     py::gil_scoped_release rel;
     src.send_request(gh, nullptr, 0);
@@ -93,7 +94,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
       }
       moved = split ? src.relay_body_hashed(dst, length, split->skip, split->full_len,
                                             split->piece_len, prog, &digests, &head, &tail,
-                                            crc ? &c : nullptr)
+                                            crc ? &c : nullptr, &ticket)
                     : src.relay_body_to(dst, length, prog, crc ? &c : nullptr);
       if (crc) {
         crc_b64 = crc32c_base64(c);
@@ -114,6 +115,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
   d["moved"] = moved;
   d["crc32c"] = crc_b64;
   if (split) {
+    d["gpu_ticket"] = ticket;      // != 0: digests come from gpu_part_wait(ticket)
     d["digests"] = py::bytes(digests);
     d["head"] = py::bytes(head);
     d["tail"] = py::bytes(tail);
@@ -129,6 +131,39 @@ PYBIND11_MODULE(_native, m) {
         "True when the host runs the AVX-512 16-lane multi-buffer SHA-1 (csrc/sha1_mb.cpp)");
   m.def("effective_cpus", &effective_cpus,
         "CPUs usable by this process: affinity mask capped by the cgroup v2 cpu.max quota");
+  m.def(
+      "set_gpu_part_hasher",
+      [](const py::object& capsule, int min_pieces) {
+        if (capsule.is_none()) {
+          set_gpu_part_hasher(nullptr, min_pieces);
+          return;
+        }
+        void* p = PyCapsule_GetPointer(capsule.ptr(), "downloader_amd.gpu_part_api");
+        if (!p) throw py::error_already_set();
+        set_gpu_part_hasher(p, min_pieces);
+      },
+      py::arg("api"), py::arg("min_pieces") = 8,
+      "Route the hashed relay's parts (>= min_pieces whole pieces) to the GPU hasher whose C "
+      "ABI capsule is `api` (_gpuhash.PartHasher.api()); None: host multi-buffer SHA-1");
+  m.def(
+      "gpu_part_wait",
+      [](uint64_t ticket) {
+        std::string d;
+        {
+          py::gil_scoped_release rel;
+          d = gpu_part_wait(ticket);
+        }
+        return py::bytes(d);
+      },
+      py::arg("ticket"), "Digests (20 B per piece) of a part the relay handed to the GPU");
+  m.def("gpu_part_stats", []() {
+    GpuPartStats s = gpu_part_stats();
+    py::dict d;
+    d["submitted"] = s.submitted;
+    d["host_fallbacks"] = s.host_fallbacks;
+    d["refused"] = s.refused;
+    return d;
+  });
   m.def("relay_pool_trim", &relay_pool_trim,
         "Unmap every idle hashed-relay part buffer; returns the bytes freed");
   m.def("relay_pool_set_max_idle", &relay_pool_set_max_idle, py::arg("n"),

@@ -116,6 +116,16 @@ constexpr int64_t kMaxBufferedPart = (int64_t)64 << 20;
 struct RelayPoolStats {
   size_t idle_buffers, idle_bytes, in_use, max_idle;
 };
+// GPU piece hashing of relayed parts (gpu_part_api.h, implemented by _gpuhash): when set,
+// relay_body_hashed_mb hands parts of >= min_pieces whole pieces to the GPU instead of the
+// host multi-buffer SHA-1 and returns a ticket; gpu_part_wait(ticket) gives the digests
+// (the part buffer goes back to the pool once its DMA has completed).
+void set_gpu_part_hasher(const void* api, int min_pieces);
+struct GpuPartStats {
+  uint64_t submitted, host_fallbacks, refused;
+};
+GpuPartStats gpu_part_stats();
+std::string gpu_part_wait(uint64_t ticket);
 // Idle part buffers are unmapped (returns the bytes freed); max_idle bounds the idle list.
 size_t relay_pool_trim();
 void relay_pool_set_max_idle(size_t n);
@@ -174,13 +184,17 @@ class HttpConn {
   // skip + full_len) are SHA-1'd as consecutive pieces of `piece_len` (the last may be
   // short) into `digests`; bytes before `skip` go to `head`, bytes after to `tail` (the
   // fragments of pieces that straddle the body's ends). One pass, L2-resident chunks.
+  // `gpu_ticket` non-null: the part may go to the GPU hasher; then *gpu_ticket != 0 and
+  // `digests` stays empty (gpu_part_wait).
   int64_t relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                             int64_t piece_len, Progress* prog, std::string* digests,
-                            std::string* head, std::string* tail, uint32_t* crc = nullptr);
+                            std::string* head, std::string* tail, uint32_t* crc = nullptr,
+                            uint64_t* gpu_ticket = nullptr);
   // relay_body_hashed for parts of >= 8 pieces: buffer the part, then multi-buffer SHA-1.
   int64_t relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                                int64_t piece_len, Progress* prog, std::string* digests,
-                               std::string* head, std::string* tail, uint32_t* crc = nullptr);
+                               std::string* head, std::string* tail, uint32_t* crc = nullptr,
+                               uint64_t* gpu_ticket = nullptr);
   void send_raw(const std::string& s) { send_all((const uint8_t*)s.data(), s.size()); }
   int fd() const { return fd_; }
   void mark_unusable() { reusable_ = false; }

@@ -7,8 +7,10 @@
 // The Python side owns protocol logic (URLs, SigV4, retries); this layer owns bytes. Every
 // call blocks its calling thread and is invoked with the GIL released.
 #include "native.h"
+#include "gpu_part_api.h"
 
 #include <algorithm>
+#include <atomic>
 #include <arpa/inet.h>
 #include <cerrno>
 #include <cstring>
@@ -25,6 +27,7 @@
 #include <sys/socket.h>
 #include <sys/types.h>
 #include <unistd.h>
+#include <unordered_map>
 
 #include <openssl/err.h>
 #include <openssl/ssl.h>
@@ -712,12 +715,14 @@ int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* 
 
 int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int64_t full_len,
                                     int64_t piece_len, Progress* prog, std::string* digests,
-                                    std::string* head, std::string* tail, uint32_t* crc) {
+                                    std::string* head, std::string* tail, uint32_t* crc,
+                                    uint64_t* gpu_ticket) {
   if (skip < 0 || full_len < 0 || skip + full_len > n || piece_len <= 0)
     throw IoError("relay_body_hashed: bad piece split");
   const int64_t npieces = (full_len + piece_len - 1) / piece_len;
   if (npieces >= 8 && n <= kMaxBufferedPart && sha1_mb_supported())
-    return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail, crc);
+    return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail, crc,
+                                gpu_ticket);
   // Chunk size: 512 KiB stays in a Zen 5 core's 1 MiB L2 between the recv copy, the send
   // copy and the SHA-1 pass, so the payload is read from DRAM once.
   thread_local std::vector<uint8_t> buf(512 * 1024);
@@ -794,6 +799,7 @@ struct PartBuffer {
   uint8_t* base = nullptr;
   size_t mapped = 0, cap = 0;
   uint8_t* data = nullptr;
+  const GpuPartHashApi* reg_api = nullptr;   // page-locked for the GPU hasher's DMA
   explicit PartBuffer(size_t n) {
     const size_t c = (n + kHuge - 1) & ~(kHuge - 1);
     void* m = mmap(nullptr, c + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
@@ -804,7 +810,10 @@ struct PartBuffer {
     madvise(data, c, MADV_HUGEPAGE);  // best effort: THP "never" just keeps 4 KiB pages
     cap = c;
   }
-  ~PartBuffer() { munmap(base, mapped); }
+  ~PartBuffer() {
+    if (reg_api) reg_api->unreg(reg_api->ctx, data);
+    munmap(base, mapped);
+  }
   PartBuffer(const PartBuffer&) = delete;
   PartBuffer& operator=(const PartBuffer&) = delete;
 };
@@ -888,9 +897,75 @@ PartPool& part_pool() {
 struct PartLease {
   std::unique_ptr<PartBuffer> b;
   explicit PartLease(size_t n) : b(part_pool().acquire(n)) {}
-  ~PartLease() { part_pool().release(std::move(b)); }
+  ~PartLease() {
+    if (b) part_pool().release(std::move(b));
+  }
 };
+
+// ---- GPU part hashing (gpu_part_api.h) -------------------------------------------------
+std::atomic<const GpuPartHashApi*> g_gpu_api{nullptr};
+std::atomic<int> g_gpu_min_pieces{8};
+std::atomic<uint64_t> g_gpu_submitted{0}, g_gpu_fallbacks{0}, g_gpu_refused{0};
+
+// A part handed to the GPU: its buffer stays leased until the DMA out of it has completed.
+struct GpuPending {
+  std::unique_ptr<PartBuffer> buf;
+  const GpuPartHashApi* api = nullptr;
+  int64_t skip = 0, full_len = 0, piece_len = 0;
+};
+std::mutex g_gpu_mu;
+std::unordered_map<uint64_t, GpuPending> g_gpu_pending;
+
+void host_digests(const uint8_t* p, int64_t full_len, int64_t piece_len, std::string* out) {
+  const int64_t np = (full_len + piece_len - 1) / piece_len;
+  std::vector<const uint8_t*> ptrs((size_t)np);
+  std::vector<size_t> lens((size_t)np);
+  for (int64_t i = 0; i < np; ++i) {
+    ptrs[(size_t)i] = p + i * piece_len;
+    lens[(size_t)i] = (size_t)std::min<int64_t>(piece_len, full_len - i * piece_len);
+  }
+  out->resize((size_t)np * 20);
+  sha1_mb(ptrs.data(), lens.data(), (size_t)np, (uint8_t*)&(*out)[0]);
+}
 }  // namespace
+
+void set_gpu_part_hasher(const void* api, int min_pieces) {
+  const GpuPartHashApi* a = (const GpuPartHashApi*)api;
+  if (a && a->abi != GPU_PART_API_ABI) throw std::invalid_argument("gpu_part_api ABI mismatch");
+  g_gpu_min_pieces.store(std::max(1, min_pieces));
+  g_gpu_api.store(a);
+}
+
+GpuPartStats gpu_part_stats() {
+  return GpuPartStats{g_gpu_submitted.load(), g_gpu_fallbacks.load(), g_gpu_refused.load()};
+}
+
+std::string gpu_part_wait(uint64_t ticket) {
+  GpuPending pend;
+  {
+    std::lock_guard<std::mutex> g(g_gpu_mu);
+    auto it = g_gpu_pending.find(ticket);
+    if (it == g_gpu_pending.end()) throw IoError("gpu_part_wait: unknown ticket");
+    pend = std::move(it->second);
+    g_gpu_pending.erase(it);
+  }
+  char err[256] = {0};
+  std::string out;
+  const GpuPartHashApi* a = pend.api;
+  if (a->wait(a->ctx, ticket, GPU_PART_COPIED, nullptr, 0, err, sizeof err) != 0) {
+    // the device failed before the DMA finished: the bytes are still ours, hash them here
+    host_digests(pend.buf->data + pend.skip, pend.full_len, pend.piece_len, &out);
+    part_pool().release(std::move(pend.buf));
+    g_gpu_fallbacks++;
+    return out;
+  }
+  part_pool().release(std::move(pend.buf));     // DMA done: the buffer serves the next part
+  const int64_t np = (pend.full_len + pend.piece_len - 1) / pend.piece_len;
+  out.resize((size_t)np * 20);
+  if (a->wait(a->ctx, ticket, GPU_PART_DONE, (uint8_t*)&out[0], out.size(), err, sizeof err) != 0)
+    throw IoError(std::string("GPU piece hashing failed: ") + err);
+  return out;
+}
 
 size_t relay_pool_trim() { return part_pool().trim(); }
 void relay_pool_set_max_idle(size_t n) { part_pool().set_max_idle(n); }
@@ -899,7 +974,8 @@ RelayPoolStats relay_pool_stats() { return part_pool().stats(); }
 int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
                                        int64_t full_len, int64_t piece_len, Progress* prog,
                                        std::string* digests, std::string* head,
-                                       std::string* tail, uint32_t* crc) {
+                                       std::string* tail, uint32_t* crc,
+                                       uint64_t* gpu_ticket) {
   // The whole part lands in a per-thread buffer on its way to `dst` (recv into it, send from
   // it: the same two copies as the chunked path), then its pieces are hashed 16 at a time in
   // the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the per-core rate of a single SHA-NI
@@ -940,17 +1016,32 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
     pos += k;
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
-  const int64_t np = (full_len + piece_len - 1) / piece_len;
-  std::vector<const uint8_t*> ptrs((size_t)np);
-  std::vector<size_t> lens((size_t)np);
-  for (int64_t i = 0; i < np; ++i) {
-    ptrs[(size_t)i] = b + skip + i * piece_len;
-    lens[(size_t)i] = (size_t)std::min<int64_t>(piece_len, full_len - i * piece_len);
-  }
-  digests->resize((size_t)np * 20);
-  sha1_mb(ptrs.data(), lens.data(), (size_t)np, (uint8_t*)&(*digests)[0]);
   head->assign((const char*)b, (size_t)skip);
   tail->assign((const char*)b + skip + full_len, (size_t)(n - skip - full_len));
+  const int64_t np = (full_len + piece_len - 1) / piece_len;
+  const GpuPartHashApi* api = gpu_ticket ? g_gpu_api.load() : nullptr;
+  if (api && np >= g_gpu_min_pieces.load()) {
+    PartBuffer* pb = lease.b.get();
+    if (!pb->reg_api && api->reg(api->ctx, pb->data, pb->cap) == 0)
+      pb->reg_api = api;
+    uint64_t t = pb->reg_api == api ? api->submit(api->ctx, b + skip, full_len, piece_len) : 0;
+    if (t) {
+      GpuPending pend;
+      pend.buf = std::move(lease.b);            // leased until the DMA is done
+      pend.api = api;
+      pend.skip = skip;
+      pend.full_len = full_len;
+      pend.piece_len = piece_len;
+      std::lock_guard<std::mutex> g(g_gpu_mu);
+      g_gpu_pending.emplace(t, std::move(pend));
+      g_gpu_submitted++;
+      digests->clear();
+      *gpu_ticket = t;
+      return pos;
+    }
+    g_gpu_refused++;
+  }
+  host_digests(b + skip, full_len, piece_len, digests);
   return pos;
 }
 

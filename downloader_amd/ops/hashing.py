@@ -117,6 +117,49 @@ def prewarm_gpu() -> bool:
     return True
 
 
+_part_hasher = None
+_part_wait_pool = None
+_part_hasher_failed = False
+
+
+def gpu_relay_hashing(min_pieces: int = 8) -> bool:
+    """Route the hashed relay's parts to the gfx950 ``PartHasher`` (batched, one lane per
+    piece; csrc/gpu_sha1.hip) instead of the host multi-buffer SHA-1. Created once per
+    process on the worker's GPU; False (host hashing) when no HIP device is usable."""
+    global _part_hasher, _part_wait_pool, _part_hasher_failed
+    with _gpu_lock:
+        if _part_hasher is not None:
+            return True
+        if _part_hasher_failed or not gpu_available():
+            return False
+        try:
+            from concurrent.futures import ThreadPoolExecutor
+            ph = gpuhash().PartHasher(gpu_device(), 1 << 30, 8, 4, 16384)
+            native().set_gpu_part_hasher(ph.api(), min_pieces)
+        except Exception:
+            _part_hasher_failed = True
+            raise
+        _part_hasher = ph
+        # digest waits block a thread each (no CPU while the device hashes)
+        _part_wait_pool = ThreadPoolExecutor(max_workers=128, thread_name_prefix="gpu-part")
+        return True
+
+
+async def gpu_part_digests(ticket: int) -> bytes:
+    """Digests of a part the relay queued to the GPU (``gpu_ticket``). Always call it once
+    per ticket: it also returns the part's buffer to the relay pool."""
+    import asyncio
+    loop = asyncio.get_running_loop()
+    return await loop.run_in_executor(_part_wait_pool, native().gpu_part_wait, ticket)
+
+
+def gpu_relay_stats() -> dict:
+    d = dict(native().gpu_part_stats())
+    if _part_hasher is not None:
+        d.update({f"device_{k}": v for k, v in _part_hasher.stats().items()})
+    return d
+
+
 def host_multibuffer() -> bool:
     """The host runs the AVX-512 16-lane SHA-1 (``csrc/sha1_mb.cpp``)."""
     return bool(native().sha1_mb_supported())

@@ -171,9 +171,12 @@ async def _stream_torrent(meta: Metainfo, seeds: List[str], selected: List[str],
                             "webseed_fetch_s": round(st.stats["relay_s"], 4),
                             "webseed_verify_s": 0.0, "gap_bytes": st.stats["gap_bytes"],
                             "skipped_bytes": st.skipped_bytes(),
+                            "verify": st.stats.get("verify", "host"),
+                            "gpu_parts": st.stats.get("gpu_parts", 0),
                             "timeline_s": {"complete": round(time.perf_counter() - t0, 4)}}
     if sv.metrics is not None:
-        sv.metrics.bytes_verified.labels("host").inc(st.fetched_bytes)
+        sv.metrics.bytes_verified.labels("gpu" if st.stats.get("verify") == "gpu" else "host"
+                                         ).inc(st.fetched_bytes)
     return st.fetched_bytes
 
 

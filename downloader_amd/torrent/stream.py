@@ -184,6 +184,13 @@ class StreamStager:
         self._outstanding = 0
         self._finished = asyncio.Event()
         self.stats = {"relay_s": 0.0, "gap_bytes": 0, "units": 0}
+        # GPU piece hashing of relayed parts: at most this many parts awaiting digests
+        self._gpu_slots: Optional[asyncio.Semaphore] = None
+        self._continuations: Set[asyncio.Task] = set()
+        gpu_pending = int(getattr(getattr(cfg, "download", None), "stream_gpu_pending", 0) or 0)
+        if gpu_pending > 0 and _gpu_relay_on(cfg):
+            self._gpu_slots = asyncio.Semaphore(gpu_pending)
+            self.stats["verify"] = "gpu"
 
     # ---------------------------------------------------------------- planning
     def _piece_range(self, p: int) -> Tuple[int, int]:
@@ -243,9 +250,9 @@ class StreamStager:
             try:
                 await self._finished.wait()
             finally:
-                for w in workers:
+                for w in workers + list(self._continuations):
                     w.cancel()
-                await asyncio.gather(*workers, return_exceptions=True)
+                await asyncio.gather(*workers, *self._continuations, return_exceptions=True)
             if self.error is not None:
                 raise self.error
             unverified = [p for p in self.frags if p not in self.verified]
@@ -267,20 +274,74 @@ class StreamStager:
         while True:
             u = await queue.get()
             u.state = "running"
-            try:
-                requeue = await self._process(u)
-            except (TransportError, OSError) as e:
-                u.attempts += 1
-                if u.attempts >= self.max_failures:
-                    self._fail(TorrentError(f"webseed failed: {e}"))
-                    return
-                await asyncio.sleep(min(5.0, 0.1 * (2 ** u.attempts)))
-                requeue = [u]
-            except BaseException as e:
-                self._fail(e)
-                return
+            if self._gpu_slots is not None and u.target is not None:
+                # GPU piece hashing: this worker only moves the part's bytes; waiting for the
+                # digests (~piece_len / 58 MB/s on the device) and the checks run in a
+                # continuation, so the relay slots stay busy relaying meanwhile
+                await self._gpu_slots.acquire()
+                try:
+                    res = await self._relay_part(u)
+                except BaseException as e:
+                    self._gpu_slots.release()
+                    if not await self._unit_failed(u, e, queue):
+                        return
+                    continue
+                if res[1].get("gpu_ticket"):
+                    t = asyncio.ensure_future(self._complete(u, res, queue))
+                    self._continuations.add(t)
+                    t.add_done_callback(self._continuations.discard)
+                    continue
+                self._gpu_slots.release()         # hashed on the host after all (refused)
+                try:
+                    requeue = await self._after_fetch(u, self._accept(u, *res,
+                                                                       res[1]["digests"]))
+                except BaseException as e:
+                    if not await self._unit_failed(u, e, queue):
+                        return
+                    continue
+            else:
+                try:
+                    requeue = await self._process(u)
+                except BaseException as e:
+                    if not await self._unit_failed(u, e, queue):
+                        return
+                    continue
             if self.error is not None:
                 return
+            self._settle(u, requeue, queue)
+
+    async def _unit_failed(self, u: _Unit, e: BaseException,
+                           queue: "asyncio.Queue[_Unit]") -> bool:
+        """A unit's fetch raised: transport errors are retried (backoff, then the unit goes
+        back to the queue), anything else - or too many attempts - fails the stager.
+        False = the caller's loop must stop."""
+        if not isinstance(e, (TransportError, OSError)):
+            self._fail(e)
+            return False
+        u.attempts += 1
+        if u.attempts >= self.max_failures:
+            self._fail(TorrentError(f"webseed failed: {e}"))
+            return False
+        await asyncio.sleep(min(5.0, 0.1 * (2 ** u.attempts)))
+        if self.error is not None:
+            return False
+        self._settle(u, [u], queue)
+        return True
+
+    async def _complete(self, u: _Unit, res, queue: "asyncio.Queue[_Unit]") -> None:
+        """Continuation of a part whose pieces the GPU hashes: digests, checks, settle."""
+        from ..ops import hashing
+        etag, h = res
+        try:
+            digests = await hashing.gpu_part_digests(h["gpu_ticket"])
+            self.stats["gpu_parts"] = self.stats.get("gpu_parts", 0) + 1
+            requeue = await self._after_fetch(u, self._accept(u, etag, h, digests))
+        except BaseException as e:
+            self._gpu_slots.release()
+            await self._unit_failed(u, e, queue)
+            return
+        self._gpu_slots.release()
+        if self.error is None:
             self._settle(u, requeue, queue)
 
     def _settle(self, u: _Unit, requeue: List[_Unit], queue: "asyncio.Queue[_Unit]") -> None:
@@ -333,15 +394,19 @@ class StreamStager:
     async def _process(self, u: _Unit) -> List[_Unit]:
         """Fetch one unit; return the units that must be fetched again (bad pieces)."""
         if u.target is None:
-            pieces = [(u.start, await self._fetch_gap(u))]
-        else:
-            got = await self._relay(u)
-            if got is None:                          # a whole piece inside failed its hash
-                u.attempts += 1
-                if u.attempts >= self.max_failures:
-                    raise TorrentError("webseed served corrupt pieces")
-                return [u]
-            pieces = got
+            return await self._after_fetch(u, [(u.start, await self._fetch_gap(u))])
+        etag, h = await self._relay_part(u)
+        return await self._after_fetch(u, self._accept(u, etag, h, h["digests"]))
+
+    async def _after_fetch(self, u: _Unit, got: Optional[List[Tuple[int, bytes]]]) -> List[_Unit]:
+        """Fragments of a fetched unit into the boundary pieces (checked once complete);
+        ``got`` None = a whole piece inside the part failed its hash."""
+        if got is None:
+            u.attempts += 1
+            if u.attempts >= self.max_failures:
+                raise TorrentError("webseed served corrupt pieces")
+            return [u]
+        pieces = got
         self.stats["units"] += 1
         requeue: List[_Unit] = []
         for a, data in pieces:
@@ -352,7 +417,9 @@ class StreamStager:
                 requeue += [self.units[i] for i in sorted(self.suppliers[p])]
         return requeue
 
-    async def _relay(self, u: _Unit) -> Optional[List[Tuple[int, bytes]]]:
+    async def _relay_part(self, u: _Unit):
+        """Relay one part webseed -> S3 (its whole pieces hashed on the way - by the host
+        multi-buffer SHA-1, or queued to the GPU: then ``h["gpu_ticket"]``)."""
         t = u.target
         url = webseed_url(self.meta, self._base(u), t.index)
         whole = u.file_off == 0 and u.length == t.size
@@ -362,7 +429,12 @@ class StreamStager:
             part=None if t.single else (u.num, t.upload_id), content_type=self._ctype(t))
         self.stats["relay_s"] += time.perf_counter() - t0
         self.fetched_bytes += u.length
-        digests = h["digests"]
+        return etag, h
+
+    def _accept(self, u: _Unit, etag: str, h: dict,
+                digests: bytes) -> Optional[List[Tuple[int, bytes]]]:
+        """Check a relayed part's whole pieces; None = one failed (refetch the part)."""
+        t = u.target
         first = (u.start + u.skip) // self.plen
         for k in range(len(digests) // 20):
             if digests[20 * k:20 * k + 20] != self.meta.piece_hash(first + k):
@@ -442,3 +514,16 @@ class StreamStager:
 
 def _sha1(b: bytes) -> bytes:
     return hashlib.sha1(b).digest()
+
+
+def _gpu_relay_on(cfg) -> bool:
+    """``download.stream_verify_backend``: gpu = the relayed parts' pieces are hashed by the
+    gfx950 PartHasher (set up on first use; a worker without a HIP device stays on the host)."""
+    d = getattr(cfg, "download", None)
+    if getattr(d, "stream_verify_backend", "cpu") != "gpu":
+        return False
+    from ..ops import hashing
+    try:
+        return hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8))
+    except Exception:       # no usable device / HIP failure: the host hashes (logged once)
+        return False

@@ -160,6 +160,13 @@ class DownloadConfig(BaseModel):
     stream_file: bool = True
     # torrent piece SHA-1: cpu, gpu (gfx950 kernel) or auto
     verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
+    # streamed torrents (torrent_stream): pieces of each relayed part hashed by the host
+    # multi-buffer SHA-1 (cpu) or by the gfx950 PartHasher (gpu: batched one-lane-per-piece
+    # launches; the relay slot is freed when the part's bytes are moved, digests arrive in a
+    # continuation)
+    stream_verify_backend: Literal["cpu", "gpu"] = "cpu"
+    stream_gpu_pending: int = 64                # parts per job awaiting GPU digests
+    stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
     # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of
