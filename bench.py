@@ -80,6 +80,10 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-compare-single-put", dest="compare_single_put", action="store_false",
                    help="skip the same-call comparison run with round-2 settings (objects up to "
                         "128 MiB in one PUT)")
+    p.add_argument("--checksum", choices=["auto", "always", "off"], default="",
+                   help="s3.checksum: CRC32C per PUT/part (auto = where bytes cross user space "
+                        "anyway, i.e. not this plain-http splice relay; always = the relay copies "
+                        "through user space to compute it)")
     p.add_argument("--cpus-per-rank", type=int, default=0,
                    help="pin each rank (worker + its peer) to this many CPUs; 0: its GPU slot's "
                         "share, min(mask, cgroup quota) / visible GPUs; -1: no pinning")
@@ -197,6 +201,8 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
     if args.tls != "off":
         over["s3"]["secure"] = True
         over["tls"] = {"ca_file": ca, "native": args.tls == "native"}
+    if args.checksum:
+        over["s3"]["checksum"] = args.checksum
     if mode == "tuned":
         if getattr(args, "single_put", False):   # round-2 headline settings, for comparison
             over["s3"]["multipart_threshold"] = 128 << 20
@@ -502,6 +508,7 @@ def main() -> int:
             "rank_peers": [t["peer"] for t in topo],
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
+            **({"checksum": args.checksum} if args.checksum else {}),
             "staging": args.staging if args.mode == "tuned" else "disk",
             **({"tls": args.tls} if args.tls != "off" else {}),
             "concurrency_per_worker": args.concurrency if args.mode == "tuned" else 1,
