@@ -172,6 +172,8 @@ async def _stream_torrent(meta: Metainfo, seeds: List[str], selected: List[str],
                             "webseed_verify_s": 0.0, "gap_bytes": st.stats["gap_bytes"],
                             "skipped_bytes": st.skipped_bytes(),
                             "verify": st.stats.get("verify", "host"),
+                            **({"verify_fallback": st.stats["verify_fallback"]}
+                               if "verify_fallback" in st.stats else {}),
                             "gpu_parts": st.stats.get("gpu_parts", 0),
                             "timeline_s": {"complete": round(time.perf_counter() - t0, 4)}}
     if sv.metrics is not None:

@@ -188,9 +188,15 @@ class StreamStager:
         self._gpu_slots: Optional[asyncio.Semaphore] = None
         self._continuations: Set[asyncio.Task] = set()
         gpu_pending = int(getattr(getattr(cfg, "download", None), "stream_gpu_pending", 0) or 0)
-        if gpu_pending > 0 and _gpu_relay_on(cfg):
-            self._gpu_slots = asyncio.Semaphore(gpu_pending)
-            self.stats["verify"] = "gpu"
+        if gpu_pending > 0 and getattr(getattr(cfg, "download", None),
+                                       "stream_verify_backend", "cpu") == "gpu":
+            why = _gpu_relay_on(cfg)
+            if why is None:
+                self._gpu_slots = asyncio.Semaphore(gpu_pending)
+                self.stats["verify"] = "gpu"
+            else:
+                self.stats["verify_fallback"] = why
+                job.logger.warn("GPU piece hashing unavailable, hashing on the host", err=why)
 
     # ---------------------------------------------------------------- planning
     def _piece_range(self, p: int) -> Tuple[int, int]:
@@ -516,14 +522,15 @@ def _sha1(b: bytes) -> bytes:
     return hashlib.sha1(b).digest()
 
 
-def _gpu_relay_on(cfg) -> bool:
-    """``download.stream_verify_backend``: gpu = the relayed parts' pieces are hashed by the
-    gfx950 PartHasher (set up on first use; a worker without a HIP device stays on the host)."""
-    d = getattr(cfg, "download", None)
-    if getattr(d, "stream_verify_backend", "cpu") != "gpu":
-        return False
+def _gpu_relay_on(cfg) -> Optional[str]:
+    """``download.stream_verify_backend: gpu``: set up the gfx950 PartHasher (once per
+    process). None when the relayed parts' pieces will be hashed on the device, else why not
+    (no HIP device, init failure) - the host multi-buffer SHA-1 then hashes them."""
     from ..ops import hashing
+    d = getattr(cfg, "download", None)
     try:
-        return hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8))
-    except Exception:       # no usable device / HIP failure: the host hashes (logged once)
-        return False
+        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8)):
+            return None
+        return "no usable HIP device"
+    except Exception as e:
+        return f"{type(e).__name__}: {e}"
