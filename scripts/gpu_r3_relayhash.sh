@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 F=${OUT:-gpurun_out/r3_relayhash}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
+timeout -k 10 120 python -c "from downloader_amd.ops import hashing; print('gpu relay hashing:', hashing.gpu_relay_hashing(8), hashing.gpu_relay_stats())" || exit 1
 timeout -k 10 300 python -u -m pytest tests/test_gpu_hash.py -x -v --timeout 120 --timeout-method thread \
   -k "part_hasher or gpu_relay" > $F/pytest_parthasher.txt 2>&1 || { tail -30 $F/pytest_parthasher.txt; exit 1; }
 tail -3 $F/pytest_parthasher.txt
