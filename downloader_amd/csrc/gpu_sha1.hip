@@ -1303,8 +1303,8 @@ PYBIND11_MODULE(_gpuhash, m) {
           [](PartHasher& h) {
             return py::capsule((void*)h.api(), "downloader_amd.gpu_part_api");
           },
-          py::keep_alive<0, 1>(),
-          "PyCapsule of the C ABI (gpu_part_api.h) for _native.set_gpu_part_hasher")
+          "PyCapsule of the C ABI (gpu_part_api.h) for _native.set_gpu_part_hasher; the "
+          "PartHasher must outlive every user of the capsule (ops.hashing keeps it for good)")
       .def(
           "hash",
           [](PartHasher& h, const py::buffer& b, int64_t piece_len) {
