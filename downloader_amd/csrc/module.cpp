@@ -156,6 +156,13 @@ PYBIND11_MODULE(_native, m) {
         return py::bytes(d);
       },
       py::arg("ticket"), "Digests (20 B per piece) of a part the relay handed to the GPU");
+  py::class_<CpuPartHasher>(m, "CpuPartHasher")
+      .def(py::init<double>(), py::arg("delay_s") = 0.005,
+           "gpu_part_api.h on a host thread (tests of the asynchronous relay-hashing path)")
+      .def("api", [](CpuPartHasher& h) {
+        return py::capsule((void*)h.api(), "downloader_amd.gpu_part_api");
+      })
+      .def_property_readonly("registered", &CpuPartHasher::registered);
   m.def("gpu_part_stats", []() {
     GpuPartStats s = gpu_part_stats();
     py::dict d;

@@ -126,6 +126,19 @@ struct GpuPartStats {
 };
 GpuPartStats gpu_part_stats();
 std::string gpu_part_wait(uint64_t ticket);
+// gpu_part_api.h served by a host thread (copy, then multi-buffer SHA-1, each after
+// `delay_s`): the asynchronous relay-hashing path without a HIP device (tests).
+class CpuPartHasher {
+ public:
+  explicit CpuPartHasher(double delay_s);
+  ~CpuPartHasher();
+  const void* api() const;
+  uint64_t registered() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
 // Idle part buffers are unmapped (returns the bytes freed); max_idle bounds the idle list.
 size_t relay_pool_trim();
 void relay_pool_set_max_idle(size_t n);

@@ -11,6 +11,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <thread>
 #include <arpa/inet.h>
 #include <cerrno>
 #include <cstring>
@@ -934,6 +938,124 @@ void set_gpu_part_hasher(const void* api, int min_pieces) {
   if (a && a->abi != GPU_PART_API_ABI) throw std::invalid_argument("gpu_part_api ABI mismatch");
   g_gpu_min_pieces.store(std::max(1, min_pieces));
   g_gpu_api.store(a);
+}
+
+// ---- CpuPartHasher: the gpu_part_api.h contract served by a host thread ------------------
+// A test double with the device's timing shape: the "DMA" (a copy into its own buffer) and
+// the "kernel" (multi-buffer SHA-1) each complete after a delay on a worker thread, so the
+// stream stager's asynchronous GPU path (tickets, lease release at copy completion,
+// continuations) runs and is tested on hosts without a HIP device.
+namespace {
+struct CpuJob {
+  const uint8_t* host;
+  int64_t len, piece_len;
+  std::string copy, digests;
+  bool copied = false, done = false;
+};
+}  // namespace
+
+struct CpuPartHasher::Impl {
+  std::mutex mu;
+  std::condition_variable cv, wcv;
+  std::unordered_map<uint64_t, CpuJob> jobs;
+  std::deque<uint64_t> queue;
+  uint64_t seq = 0;
+  bool stop = false;
+  double delay_s;
+  std::thread th;
+  GpuPartHashApi api{};
+  uint64_t registered = 0;
+
+  void run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || !queue.empty(); });
+      if (stop && queue.empty()) return;
+      uint64_t t = queue.front();
+      queue.pop_front();
+      CpuJob* j = &jobs.at(t);
+      lk.unlock();
+      std::this_thread::sleep_for(std::chrono::duration<double>(delay_s));
+      std::string c((const char*)j->host, (size_t)j->len);
+      lk.lock();
+      j->copy.swap(c);
+      j->copied = true;
+      wcv.notify_all();
+      lk.unlock();
+      std::this_thread::sleep_for(std::chrono::duration<double>(delay_s));
+      std::string d;
+      host_digests((const uint8_t*)j->copy.data(), j->len, j->piece_len, &d);
+      lk.lock();
+      j->digests.swap(d);
+      j->done = true;
+      wcv.notify_all();
+    }
+  }
+};
+
+CpuPartHasher::CpuPartHasher(double delay_s) : impl_(new Impl) {
+  Impl* m = impl_.get();
+  m->delay_s = delay_s;
+  m->api.abi = GPU_PART_API_ABI;
+  m->api.ctx = m;
+  m->api.reg = [](void* c, void*, size_t) {
+    Impl* i = (Impl*)c;
+    std::lock_guard<std::mutex> g(i->mu);
+    i->registered++;
+    return 0;
+  };
+  m->api.unreg = [](void*, void*) {};
+  m->api.submit = [](void* c, const uint8_t* d, int64_t len, int64_t pl) -> uint64_t {
+    Impl* i = (Impl*)c;
+    std::lock_guard<std::mutex> g(i->mu);
+    if (i->stop || len <= 0 || pl <= 0) return 0;
+    uint64_t t = ++i->seq;
+    CpuJob& j = i->jobs[t];
+    j.host = d;
+    j.len = len;
+    j.piece_len = pl;
+    i->queue.push_back(t);
+    i->cv.notify_all();
+    return t;
+  };
+  m->api.wait = [](void* c, uint64_t t, int phase, uint8_t* out, size_t ol, char* err,
+                   size_t el) -> int {
+    Impl* i = (Impl*)c;
+    std::unique_lock<std::mutex> lk(i->mu);
+    auto it = i->jobs.find(t);
+    if (it == i->jobs.end()) {
+      snprintf(err, el, "unknown ticket");
+      return -1;
+    }
+    CpuJob* j = &it->second;
+    i->wcv.wait(lk, [&] { return phase == GPU_PART_COPIED ? j->copied : j->done; });
+    if (phase == GPU_PART_DONE) {
+      if (ol < j->digests.size()) {
+        snprintf(err, el, "digest buffer too small");
+        return -1;
+      }
+      memcpy(out, j->digests.data(), j->digests.size());
+      i->jobs.erase(it);
+    }
+    return 0;
+  };
+  m->th = std::thread([m] { m->run(); });
+}
+
+CpuPartHasher::~CpuPartHasher() {
+  {
+    std::lock_guard<std::mutex> g(impl_->mu);
+    impl_->stop = true;
+  }
+  impl_->cv.notify_all();
+  impl_->th.join();
+}
+
+const void* CpuPartHasher::api() const { return &impl_->api; }
+
+uint64_t CpuPartHasher::registered() const {
+  std::lock_guard<std::mutex> g(impl_->mu);
+  return impl_->registered;
 }
 
 GpuPartStats gpu_part_stats() {

@@ -488,7 +488,8 @@ class NativeTransport(Transport):
             p = d["put"]
             put = Response(p["status"], list(p["headers"]), d["put_body"], 0, p.get("reason", ""))
             put.sent_crc32c = d.get("crc32c", "")
-        hashed = {k: d[k] for k in ("digests", "head", "tail")} if split is not None else None
+        hashed = {k: d[k] for k in ("digests", "head", "tail", "gpu_ticket")} \
+            if split is not None else None
         return get, put, d["moved"], hashed
 
     async def relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,

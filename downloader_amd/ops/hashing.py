@@ -145,6 +145,19 @@ def gpu_relay_hashing(min_pieces: int = 8) -> bool:
         return True
 
 
+def use_part_hasher(hasher, min_pieces: int = 8) -> None:
+    """Install ``hasher`` (anything with ``api()`` returning the gpu_part_api.h capsule, e.g.
+    ``_native.CpuPartHasher`` in tests) as the relay's part hasher; None restores host
+    hashing. The object is kept alive here."""
+    global _part_hasher, _part_wait_pool
+    from concurrent.futures import ThreadPoolExecutor
+    with _gpu_lock:
+        native().set_gpu_part_hasher(hasher.api() if hasher is not None else None, min_pieces)
+        _part_hasher = hasher
+        if _part_wait_pool is None:
+            _part_wait_pool = ThreadPoolExecutor(max_workers=128, thread_name_prefix="gpu-part")
+
+
 async def gpu_part_digests(ticket: int) -> bytes:
     """Digests of a part the relay queued to the GPU (``gpu_ticket``). Always call it once
     per ticket: it also returns the part's buffer to the relay pool."""
@@ -155,7 +168,7 @@ async def gpu_part_digests(ticket: int) -> bytes:
 
 def gpu_relay_stats() -> dict:
     d = dict(native().gpu_part_stats())
-    if _part_hasher is not None:
+    if _part_hasher is not None and hasattr(_part_hasher, "stats"):
         d.update({f"device_{k}": v for k, v in _part_hasher.stats().items()})
     return d
 

@@ -442,6 +442,10 @@ class StreamStager:
         """Check a relayed part's whole pieces; None = one failed (refetch the part)."""
         t = u.target
         first = (u.start + u.skip) // self.plen
+        if len(digests) != 20 * (-(-u.full // self.plen)):
+            # never accept a part whose pieces were not all hashed
+            raise TorrentError(f"part {u.num}: {len(digests) // 20} digests for "
+                               f"{-(-u.full // self.plen)} pieces")
         for k in range(len(digests) // 20):
             if digests[20 * k:20 * k + 20] != self.meta.piece_hash(first + k):
                 self.hash_fails += 1
@@ -528,6 +532,8 @@ def _gpu_relay_on(cfg) -> Optional[str]:
     (no HIP device, init failure) - the host multi-buffer SHA-1 then hashes them."""
     from ..ops import hashing
     d = getattr(cfg, "download", None)
+    if hashing._part_hasher is not None:         # already set up (or a test double)
+        return None
     try:
         if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8)):
             return None

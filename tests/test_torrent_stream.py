@@ -376,3 +376,50 @@ def test_staged_objects_carry_media_content_types(run, tmp_path, make_cfg, origi
             "application/octet-stream"
         await s3.stop(); await origin.stop()
     run(go())
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_stream_async_part_hashing_with_host_double(run, tmp_path, make_cfg, origin_cls, corrupt):
+    """The GPU relay-hashing path (stream_verify_backend: gpu) on a host: the native
+    CpuPartHasher serves the same C ABI as the gfx950 PartHasher (copy and hash each finish
+    later on its own thread). Relay slots are freed after the bytes move, parts are finished in
+    continuations, a corrupt piece is caught from the late digests and the part refetched,
+    and every buffer lease returns to the pool."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Movie"
+        src.mkdir(parents=True)
+        data = os.urandom(23 * (1 << 20) + 12345)
+        (src / "m.mkv").write_bytes(data)
+        origin.blobs["/ws/Movie/m.mkv"] = data
+        if corrupt:
+            origin.corrupt["/ws/Movie/m.mkv"] = [9 * (1 << 20) + 5, 1]
+        origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
+                                                    url_list=[origin.url("/ws/")])
+        w = _worker(make_cfg, ep, download={"stream_verify_backend": "gpu",
+                                            "stream_gpu_min_pieces": 4})
+        await w.start(health=False)
+        before = native().gpu_part_stats()
+        await w.submit(api.make_download("ah", "http", origin.url("/t/m.torrent")))
+        await _wait(w, timeout=60)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        t = r.stats["torrent"]
+        assert t["verify"] == "gpu" and t["gpu_parts"] >= 4
+        assert s3.get("triton-staging", keys.object_key("ah", "m.mkv")) == data
+        assert (t["hash_fails"] >= 1) == corrupt
+        after = native().gpu_part_stats()
+        assert after["submitted"] - before["submitted"] >= 4 + corrupt
+        assert after["host_fallbacks"] == before["host_fallbacks"]
+        assert native().relay_pool_stats()["in_use"] == 0        # every lease came back
+        await w.stop(); await s3.stop(); await origin.stop()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.01), 4)
+    try:
+        run(go())
+    finally:
+        hashing.use_part_hasher(None)
