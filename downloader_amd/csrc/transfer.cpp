@@ -798,6 +798,9 @@ namespace {
 // MADV_HUGEPAGE and no value-initialisation. A std::vector resize zero-filled every 4 KiB page
 // of a 64 MiB part and faulted them one by one: ~280k minor faults (0.7 CPU-s) the first time
 // 16 relay threads ran, i.e. the first torrent a worker staged ran at half speed.
+// The part hasher the hashed relay hands parts to (set_gpu_part_hasher), or null.
+std::atomic<const GpuPartHashApi*> g_gpu_api{nullptr};
+
 struct PartBuffer {
   static constexpr size_t kHuge = size_t(2) << 20;
   uint8_t* base = nullptr;
@@ -859,7 +862,9 @@ class PartPool {
     {
       std::lock_guard<std::mutex> g(mu_);
       in_use_ -= 1;
-      if (idle_.size() < max_idle_) {
+      if (b->reg_api && b->reg_api != g_gpu_api.load()) {
+        drop = std::move(b);         // registered with a hasher no longer in use: unlock
+      } else if (idle_.size() < max_idle_) {
         idle_bytes_ += b->cap;
         idle_.push_back(std::move(b));
       } else {
@@ -867,6 +872,23 @@ class PartPool {
       }
     }
   }  // `drop` unmapped outside the lock
+  // Idle buffers page-locked for another hasher than `keep` are unregistered and unmapped
+  // (set_gpu_part_hasher: the previous hasher is still alive when this runs).
+  void drop_foreign(const GpuPartHashApi* keep) {
+    std::vector<std::unique_ptr<PartBuffer>> drop;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i = 0; i < idle_.size();) {
+        if (idle_[i]->reg_api && idle_[i]->reg_api != keep) {
+          idle_bytes_ -= idle_[i]->cap;
+          drop.push_back(std::move(idle_[i]));
+          idle_.erase(idle_.begin() + (ptrdiff_t)i);
+        } else {
+          ++i;
+        }
+      }
+    }
+  }
   size_t trim() {
     std::vector<std::unique_ptr<PartBuffer>> drop;
     size_t freed;
@@ -907,7 +929,6 @@ struct PartLease {
 };
 
 // ---- GPU part hashing (gpu_part_api.h) -------------------------------------------------
-std::atomic<const GpuPartHashApi*> g_gpu_api{nullptr};
 std::atomic<int> g_gpu_min_pieces{8};
 std::atomic<uint64_t> g_gpu_submitted{0}, g_gpu_fallbacks{0}, g_gpu_refused{0};
 
@@ -938,6 +959,7 @@ void set_gpu_part_hasher(const void* api, int min_pieces) {
   if (a && a->abi != GPU_PART_API_ABI) throw std::invalid_argument("gpu_part_api ABI mismatch");
   g_gpu_min_pieces.store(std::max(1, min_pieces));
   g_gpu_api.store(a);
+  part_pool().drop_foreign(a);
 }
 
 // ---- CpuPartHasher: the gpu_part_api.h contract served by a host thread ------------------
