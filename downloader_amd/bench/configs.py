@@ -197,6 +197,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["stream_verify_backend"] = a.stream_verify
             if getattr(a, "stream_gpu_pending", 0):
                 dl["stream_gpu_pending"] = a.stream_gpu_pending
+            if getattr(a, "stream_gpu_tail", None) is not None:
+                dl["stream_gpu_tail"] = a.stream_gpu_tail
             if getattr(a, "relay_trim_s", None) is not None:
                 dl["relay_pool_idle_trim_s"] = a.relay_trim_s
             part_mb = getattr(a, "part_mb", 0)
@@ -567,6 +569,8 @@ def main(argv=None) -> int:
                          "host multi-buffer SHA-1 or the gfx950 PartHasher")
     ap.add_argument("--stream-gpu-pending", type=int, default=0,
                     help="download.stream_gpu_pending (parts per job awaiting GPU digests)")
+    ap.add_argument("--stream-gpu-tail", type=int, default=None,
+                    help="download.stream_gpu_tail (queued parts below which the host hashes)")
     ap.add_argument("--stream-parallel", type=int, default=0,
                     help="download.torrent_stream_parallel (parts in flight per job)")
     ap.add_argument("--part-mb", type=int, default=0,

@@ -64,7 +64,7 @@ struct PieceSplit {
 // then a zero chunk whose trailer is the CRC32C of the bytes moved (x-amz-checksum-crc32c).
 py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
                int64_t length, Progress* prog, int64_t max_body, const PieceSplit* split,
-               bool crc) {
+               bool crc, bool gpu = false) {
   std::string gh = get_head, ph = put_head;
   ResponseHead g, p;
   std::string gerr, pbody, digests, head, tail, crc_b64;
@@ -94,7 +94,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
       }
       moved = split ? src.relay_body_hashed(dst, length, split->skip, split->full_len,
                                             split->piece_len, prog, &digests, &head, &tail,
-                                            crc ? &c : nullptr, &ticket)
+                                            crc ? &c : nullptr, gpu ? &ticket : nullptr)
                     : src.relay_body_to(dst, length, prog, crc ? &c : nullptr);
       if (crc) {
         crc_b64 = crc32c_base64(c);
@@ -412,14 +412,14 @@ PYBIND11_MODULE(_native, m) {
           "relay_hashed_to",
           [](HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py::bytes& put_head,
              int64_t length, int64_t skip, int64_t full_len, int64_t piece_len, Progress* prog,
-             int64_t max_body, bool crc) {
+             int64_t max_body, bool crc, bool gpu) {
             PieceSplit ps{skip, full_len, piece_len};
-            return relay(src, get_head, dst, put_head, length, prog, max_body, &ps, crc);
+            return relay(src, get_head, dst, put_head, length, prog, max_body, &ps, crc, gpu);
           },
           py::arg("get_head"), py::arg("dst"), py::arg("put_head"), py::arg("length"),
           py::arg("skip"), py::arg("full_len"), py::arg("piece_len"),
           py::arg("progress") = nullptr, py::arg("max_body") = (int64_t)1 << 20,
-          py::arg("crc") = false,
+          py::arg("crc") = false, py::arg("gpu") = false,
           "relay_to through a user-space chunk that is SHA-1'd on the way: body bytes "
           "[skip, skip+full_len) as consecutive `piece_len` pieces (last may be short). Adds "
           "`digests` (20 B per piece), `head` (bytes before skip) and `tail` (bytes after).")

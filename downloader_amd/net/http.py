@@ -440,7 +440,7 @@ class NativeTransport(Transport):
 
     def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
                length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None,
-               src_proxy: Optional[Proxy] = None, checksum: bool = False
+               src_proxy: Optional[Proxy] = None, checksum: bool = False, gpu: bool = False
                ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         ss, sh, sp, spath = split_host(src_url)
         ds, dh, dp, dpath = split_host(dst_url)
@@ -470,7 +470,7 @@ class NativeTransport(Transport):
                 d = src.relay_to(get_head, dst, put_head, length, nprog, crc=checksum)
             else:
                 d = src.relay_hashed_to(get_head, dst, put_head, length, *split, nprog,
-                                        crc=checksum)
+                                        crc=checksum, gpu=gpu)
         except RuntimeError as e:
             self._untrack(slot, src)
             self._untrack(slot, dst)
@@ -495,7 +495,8 @@ class NativeTransport(Transport):
     async def relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
                     length: int, progress: Optional[Progress] = None,
                     split: Optional[Tuple[int, int, int]] = None,
-                    src_proxy: Optional[ProxyConfig] = None, checksum: bool = False
+                    src_proxy: Optional[ProxyConfig] = None, checksum: bool = False,
+                    gpu: bool = False
                     ) -> Tuple[Response, Optional[Response], int, Optional[dict]]:
         """GET ``src_url`` and stream exactly ``length`` body bytes as the body of a PUT to
         ``dst_url`` without touching user space (socket -> pipe -> socket splice; through an
@@ -508,7 +509,8 @@ class NativeTransport(Transport):
 
         ``checksum``: the PUT body is aws-chunked with a trailing ``x-amz-checksum-crc32c``
         computed on the way (bytes through user space); ``dst_headers`` must carry the
-        aws-chunked headers (``S3Client._relay_put`` does)."""
+        aws-chunked headers (``S3Client._relay_put`` does). ``gpu`` (with ``split``): the
+        part's pieces may go to the installed part hasher (``hashed["gpu_ticket"]``)."""
         nprog = None
         if progress is not None:
             if progress.native is None:
@@ -519,7 +521,8 @@ class NativeTransport(Transport):
             slot = self._new_slot()
             px = src_proxy.for_url(src_url) if src_proxy is not None else None
             fut = loop.run_in_executor(self._exec, self._relay, src_url, src_headers, dst_url,
-                                       dst_headers, length, nprog, slot, split, px, checksum)
+                                       dst_headers, length, nprog, slot, split, px, checksum,
+                                       gpu)
             try:
                 out = await asyncio.shield(fut)
             except asyncio.CancelledError:

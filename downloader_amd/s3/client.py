@@ -454,7 +454,8 @@ class S3Client:
     async def _relay_put(self, bucket: str, key: str, query: Sequence[Tuple[str, str]],
                          src_url: str, offset: int, length: int, whole: bool,
                          progress: Optional[Progress], split=None, src_proxy=None,
-                         content_type: str = "", checksum: bool = False, validator: str = ""):
+                         content_type: str = "", checksum: bool = False, validator: str = "",
+                         gpu: bool = False):
         """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
         (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``.
         ``checksum``: aws-chunked body with a trailing CRC32C of the relayed bytes.
@@ -477,7 +478,7 @@ class S3Client:
                 get, put, _, hashed = await self.t.native.relay(src_url, src_hdrs, url, hdrs,
                                                                 length, progress, split,
                                                                 src_proxy=src_proxy,
-                                                                checksum=checksum)
+                                                                checksum=checksum, gpu=gpu)
             except TransportError as e:
                 err: Exception = e
                 retry = True
@@ -606,17 +607,19 @@ class S3Client:
     async def relay_hashed(self, bucket: str, key: str, src_url: str, offset: int, length: int,
                            whole: bool, split: Tuple[int, int, int],
                            part: Optional[Tuple[int, str]] = None,
-                           progress: Optional[Progress] = None, content_type: str = ""):
+                           progress: Optional[Progress] = None, content_type: str = "",
+                           gpu: bool = False):
         """Relay ``length`` bytes of ``src_url`` at ``offset`` into the object ``key`` (or its
         multipart ``part=(number, upload_id)``) while SHA-1-ing the torrent pieces inside it
-        (``split``); returns ``(etag, {"digests", "head", "tail"})``."""
+        (``split``); returns ``(etag, {"digests", "head", "tail", "gpu_ticket"})`` - with
+        ``gpu`` the pieces may be queued to the part hasher instead (``gpu_ticket`` != 0)."""
         query = [] if part is None else [("partNumber", str(part[0])), ("uploadId", part[1])]
         tls = src_url.startswith("https://") or self.scheme == "https"
         return await self._relay_put(bucket, key, query, src_url, offset, length, whole,
                                      progress, split,
                                      content_type=content_type if part is None else "",
                                      checksum=self.want_checksum(relay=True, tls=tls,
-                                                                 hashed=True))
+                                                                 hashed=True), gpu=gpu)
 
     async def create_multipart_upload(self, bucket: str, key: str, content_type: str = "") -> str:
         r = await self._request("POST", bucket, key, query=[("uploads", "")],

@@ -194,6 +194,8 @@ class StreamStager:
             if why is None:
                 self._gpu_slots = asyncio.Semaphore(gpu_pending)
                 self.stats["verify"] = "gpu"
+                # parts still queued below which the rest hash on the host
+                self.gpu_tail = int(getattr(cfg.download, "stream_gpu_tail", 0) or 0)
             else:
                 self.stats["verify_fallback"] = why
                 job.logger.warn("GPU piece hashing unavailable, hashing on the host", err=why)
@@ -285,8 +287,11 @@ class StreamStager:
                 # digests (~piece_len / 58 MB/s on the device) and the checks run in a
                 # continuation, so the relay slots stay busy relaying meanwhile
                 await self._gpu_slots.acquire()
+                # the job's last parts hash on the host: their GPU latency (~piece_len / 58
+                # MB/s) would land on the end of the job with nothing left to overlap it
+                gpu = queue.qsize() >= self.gpu_tail
                 try:
-                    res = await self._relay_part(u)
+                    res = await self._relay_part(u, gpu)
                 except BaseException as e:
                     self._gpu_slots.release()
                     if not await self._unit_failed(u, e, queue):
@@ -423,7 +428,7 @@ class StreamStager:
                 requeue += [self.units[i] for i in sorted(self.suppliers[p])]
         return requeue
 
-    async def _relay_part(self, u: _Unit):
+    async def _relay_part(self, u: _Unit, gpu: bool = False):
         """Relay one part webseed -> S3 (its whole pieces hashed on the way - by the host
         multi-buffer SHA-1, or queued to the GPU: then ``h["gpu_ticket"]``)."""
         t = u.target
@@ -432,7 +437,8 @@ class StreamStager:
         t0 = time.perf_counter()
         etag, h = await self.s3.relay_hashed(
             self.bucket, t.key, url, u.file_off, u.length, whole, (u.skip, u.full, self.plen),
-            part=None if t.single else (u.num, t.upload_id), content_type=self._ctype(t))
+            part=None if t.single else (u.num, t.upload_id), content_type=self._ctype(t),
+            gpu=gpu)
         self.stats["relay_s"] += time.perf_counter() - t0
         self.fetched_bytes += u.length
         return etag, h

@@ -167,6 +167,9 @@ class DownloadConfig(BaseModel):
     stream_verify_backend: Literal["cpu", "gpu"] = "cpu"
     stream_gpu_pending: int = 64                # parts per job awaiting GPU digests
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
+    # once fewer parts than this are queued, the job's remaining parts hash on the host (the
+    # GPU's per-piece latency would otherwise land on the end of the job)
+    stream_gpu_tail: int = 16
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
     # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of

@@ -270,7 +270,7 @@ def test_stream_torrent_with_gpu_relay_hashing(run, tmp_path, make_cfg, origin_c
         origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
                                                     url_list=[origin.url("/ws/")])
         cfg = make_cfg(ep, download={"torrent_enable_dht": False, "stream_verify_backend": "gpu",
-                                     "stream_gpu_min_pieces": 4})
+                                     "stream_gpu_min_pieces": 4, "stream_gpu_tail": 0})
         w = Worker(cfg, broker=MemoryBroker())
         await w.start(health=False)
         before = native().gpu_part_stats()["submitted"]

@@ -401,7 +401,7 @@ def test_stream_async_part_hashing_with_host_double(run, tmp_path, make_cfg, ori
         origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
                                                     url_list=[origin.url("/ws/")])
         w = _worker(make_cfg, ep, download={"stream_verify_backend": "gpu",
-                                            "stream_gpu_min_pieces": 4})
+                                            "stream_gpu_min_pieces": 4, "stream_gpu_tail": 0})
         await w.start(health=False)
         before = native().gpu_part_stats()
         await w.submit(api.make_download("ah", "http", origin.url("/t/m.torrent")))
