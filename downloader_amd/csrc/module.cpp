@@ -42,15 +42,6 @@ py::dict head_to_dict(const ResponseHead& h) {
   return d;
 }
 
-ResponseHead dict_to_head(const py::dict& d) {
-  ResponseHead h;
-  h.status = d["status"].cast<int>();
-  h.content_length = d["content_length"].cast<int64_t>();
-  h.chunked = d["chunked"].cast<bool>();
-  h.keep_alive = d["keep_alive"].cast<bool>();
-  return h;
-}
-
 }  // namespace
 
 struct PieceSplit {

@@ -36,11 +36,15 @@ def test_crc32c_matches_reference_and_streams():
     n = native()
     assert n.crc32c(b"123456789") == 0xE3069283                  # the CRC-32C check value
     assert n.crc32c_base64(0xE3069283) == base64.b64encode(bytes.fromhex("e3069283")).decode()
-    for size in (0, 1, 7, 9, 255, 256, 769, 8191, 24577, 50_001):
-        b = os.urandom(size)
-        assert n.crc32c(b) == _crc_ref(b), size
-        k = size // 3
-        assert n.crc32c(b[k:], n.crc32c(b[:k])) == _crc_ref(b), size
+    # short inputs (crc32 chains), and >= 1 KiB with odd lengths and misaligned starts (the
+    # AVX-512 VPCLMULQDQ folding path where the CPU has it: 256-byte blocks, 16-byte tail)
+    for size in (0, 1, 7, 9, 255, 256, 769, 1023, 1024, 1025, 1279, 1281, 4103, 8191, 24577,
+                 50_001):
+        for off in (0, 3):
+            b = os.urandom(size + off)[off:]
+            assert n.crc32c(b) == _crc_ref(b), (size, off)
+            k = size // 3
+            assert n.crc32c(b[k:], n.crc32c(b[:k])) == _crc_ref(b), (size, off)
 
 
 def test_decode_aws_chunked():
