@@ -446,6 +446,88 @@ int main() {
     }
     CHECK(err.find("certificate verify failed") != std::string::npos);
   }
+  // ---- CRC32C: check value, the VPCLMULQDQ fold (>= 1 KiB) and the crc32 chains agree with
+  // a bitwise reference at odd lengths / offsets, and a CRC'd relay reports the body's CRC
+  {
+    CHECK(crc32c((const uint8_t*)"123456789", 9) == 0xE3069283u);
+    auto bitwise = [](const uint8_t* p, size_t n) {
+      uint32_t c = ~0u;
+      for (size_t i = 0; i < n; ++i) {
+        c ^= p[i];
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1)));
+      }
+      return ~c;
+    };
+    for (size_t n : {(size_t)1, (size_t)1023, (size_t)1024, (size_t)4099, (size_t)77777, (size_t)300000})
+      for (size_t off : {(size_t)0, (size_t)3}) {
+        const uint8_t* p = body.data() + off;
+        uint32_t split = crc32c(p + n / 3, n - n / 3, crc32c(p, n / 3));
+        CHECK(crc32c(p, n) == bitwise(p, n) && split == bitwise(p, n));
+      }
+    CHECK(crc32c_base64(0xE3069283u) == "4waSgw==");
+    Server origin([&](int fd) {
+      read_head(fd);
+      send_str(fd, "HTTP/1.1 206 Partial Content\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n");
+      send_str(fd, std::string((const char*)body.data(), body.size()));
+    });
+    Server sink([&](int fd) {
+      read_head(fd);
+      drain_body(fd, (int64_t)body.size());
+      send_str(fd, "HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n");
+    });
+    HttpConn src("127.0.0.1", origin.port, 5, 5), dst("127.0.0.1", sink.port, 5, 5);
+    src.send_request("GET /r HTTP/1.1\r\nHost: x\r\n\r\n", nullptr, 0);
+    ResponseHead g = src.read_head();
+    dst.send_raw("PUT /s HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n");
+    uint32_t crc = 0;
+    int64_t moved = src.relay_body_to(dst, g.content_length, nullptr, &crc);
+    ResponseHead p = dst.read_head();
+    dst.read_body(p, 16);
+    CHECK(moved == (int64_t)body.size() && crc == crc32c(body.data(), body.size()));
+  }
+  // ---- asynchronous part hashing (gpu_part_api.h) served by the host double: 4 relays hand
+  // their parts over at once, the waits return the digests and the buffers come back to the
+  // pool; then the hasher is replaced (registered buffers of the old one are dropped)
+  {
+    CpuPartHasher cph(0.002);
+    set_gpu_part_hasher(cph.api(), 8);
+    const int64_t plen = 1 << 16, skip = 1000, n = (int64_t)body.size();
+    const int64_t full = ((n - skip) / plen) * plen;
+    std::string want = hash_pieces("sha1", body.data() + skip, (size_t)full, (size_t)plen, 1);
+    std::atomic<int> good{0};
+    std::vector<std::thread> ths;
+    for (int t = 0; t < 4; ++t) {
+      ths.emplace_back([&] {
+        Server origin([&](int fd) {
+          read_head(fd);
+          send_str(fd, "HTTP/1.1 206 Partial Content\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+          send_str(fd, std::string((const char*)body.data(), body.size()));
+        });
+        Server sink([&](int fd) {
+          read_head(fd);
+          drain_body(fd, n);
+          send_str(fd, "HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n");
+        });
+        HttpConn src("127.0.0.1", origin.port, 5, 5), dst("127.0.0.1", sink.port, 5, 5);
+        src.send_request("GET /g HTTP/1.1\r\nHost: x\r\n\r\n", nullptr, 0);
+        ResponseHead g = src.read_head();
+        dst.send_raw("PUT /g HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+        std::string digests, head, tail;
+        uint64_t ticket = 0;
+        int64_t moved = src.relay_body_hashed(dst, g.content_length, skip, full, plen, nullptr,
+                                              &digests, &head, &tail, nullptr, &ticket);
+        ResponseHead p = dst.read_head();
+        dst.read_body(p, 16);
+        if (ticket) digests = gpu_part_wait(ticket);
+        if (moved == n && p.status == 200 && ticket != 0 && digests == want) good.fetch_add(1);
+      });
+    }
+    for (auto& th : ths) th.join();
+    CHECK(good.load() == 4);
+    GpuPartStats gs = gpu_part_stats();
+    CHECK(gs.submitted >= 4 && cph.registered() >= 1);
+    set_gpu_part_hasher(nullptr, 0);
+  }
   {
     RelayPoolStats st = relay_pool_stats();
     CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);
