@@ -190,8 +190,9 @@ class HttpConn {
   void discard_body(const ResponseHead& h);
   // Move exactly `n` body bytes of the response being read on *this to `dst`'s socket
   // (bytes already buffered first, then socket -> pipe -> socket with splice).
-  // `crc` non-null: the bytes go through user space (relay_copy) and are CRC32C'd on the way
-  // (S3 trailing checksum of an aws-chunked PUT).
+  // `crc` non-null: the bytes are CRC32C'd on the way (S3 trailing checksum of an aws-chunked
+  // PUT): each spliced chunk is tee()d into a second pipe whose copy is read and CRC'd, the
+  // original pages still go to `dst` by splice (one user-space copy instead of recv + send).
   int64_t relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32_t* crc = nullptr);
   // Same relay, but through a user-space chunk that is also hashed: body bytes [skip,
   // skip + full_len) are SHA-1'd as consecutive pieces of `piece_len` (the last may be
@@ -236,6 +237,7 @@ class HttpConn {
   SSL* ssl_ = nullptr;
   std::shared_ptr<TlsContext> tls_;  // keeps the SSL_CTX alive as long as ssl_
   int pipe_[2] = {-1, -1};
+  int tpipe_[2] = {-1, -1};   // tee target of the CRC'd relay
   size_t pipe_sz_ = 0;
   bool reusable_ = true;
   std::vector<uint8_t> rbuf_;

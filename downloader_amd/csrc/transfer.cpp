@@ -210,11 +210,12 @@ void HttpConn::close() {
   }
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
-  for (int i = 0; i < 2; ++i)
-    if (pipe_[i] >= 0) {
-      ::close(pipe_[i]);
-      pipe_[i] = -1;
-    }
+  for (int* fds : {pipe_, tpipe_})
+    for (int i = 0; i < 2; ++i)
+      if (fds[i] >= 0) {
+        ::close(fds[i]);
+        fds[i] = -1;
+      }
 }
 
 void HttpConn::abort() {
@@ -639,12 +640,22 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
   if (moved == n) return moved;
-  if (ssl_ || dst.ssl_ || crc) return relay_copy(dst, n, moved, prog, crc);
+  if (ssl_ || dst.ssl_) return relay_copy(dst, n, moved, prog, crc);
   if (pipe_[0] < 0) {
     if (pipe2(pipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
     int got = fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
     pipe_sz_ = got > 0 ? (size_t)got : 65536;
   }
+  if (crc && tpipe_[0] < 0) {
+    if (pipe2(tpipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
+    fcntl(tpipe_[1], F_SETPIPE_SZ, (int)pipe_sz_);   // smaller: tee duplicates less per call
+  }
+  auto fail = [&](const char* what) {
+    reusable_ = false;
+    dst.reusable_ = false;
+    throw IoError(errstr(what));
+  };
+  thread_local std::vector<uint8_t> cbuf(256 * 1024);   // L2-resident CRC staging
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
@@ -655,10 +666,12 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
     if (in < 0) {
       if (errno == EINTR) continue;
-      reusable_ = false;
-      dst.reusable_ = false;
-      if (errno == EAGAIN) throw IoError("recv timeout");
-      throw IoError(errstr("splice(src)"));
+      if (errno == EAGAIN) {
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError("recv timeout");
+      }
+      fail("splice(src)");
     }
     if (in == 0) {
       reusable_ = false;
@@ -667,15 +680,39 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     }
     ssize_t left = in;
     while (left > 0) {
-      ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)left,
-                             SPLICE_F_MOVE | SPLICE_F_MORE);
-      if (out < 0) {
-        if (errno == EINTR) continue;
-        reusable_ = false;
-        dst.reusable_ = false;
-        throw IoError(errstr("splice(dst)"));
+      ssize_t chunk = left;
+      if (crc) {
+        // duplicate the pipe's pages (no copy), read the duplicate: the CRC sees exactly the
+        // bytes the next splice sends
+        ssize_t t = ::tee(pipe_[0], tpipe_[1], (size_t)left, 0);
+        if (t < 0) {
+          if (errno == EINTR) continue;
+          fail("tee");
+        }
+        if (t == 0) {
+          reusable_ = false;
+          dst.reusable_ = false;
+          throw IoError("tee: no data");
+        }
+        for (ssize_t got = 0; got < t;) {
+          ssize_t r = ::read(tpipe_[0], cbuf.data(), (size_t)std::min<ssize_t>(t - got, (ssize_t)cbuf.size()));
+          if (r < 0 && errno == EINTR) continue;
+          if (r <= 0) fail("read(tee)");
+          *crc = stager::crc32c(cbuf.data(), (size_t)r, *crc);
+          got += r;
+        }
+        chunk = t;
       }
-      left -= out;
+      while (chunk > 0) {
+        ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)chunk,
+                               SPLICE_F_MOVE | SPLICE_F_MORE);
+        if (out < 0) {
+          if (errno == EINTR) continue;
+          fail("splice(dst)");
+        }
+        chunk -= out;
+        left -= out;
+      }
     }
     moved += in;
     if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
