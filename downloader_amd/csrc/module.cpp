@@ -44,6 +44,16 @@ py::dict head_to_dict(const ResponseHead& h) {
 
 }  // namespace
 
+// Wait a GPU part ticket out and drop its digests (the relay failed after queueing the part):
+// returns the part's buffer to the pool and the hasher's slot state.
+void forget_ticket(uint64_t ticket) {
+  if (!ticket) return;
+  try {
+    gpu_part_wait(ticket);
+  } catch (...) {
+  }
+}
+
 struct PieceSplit {
   int64_t skip, full_len, piece_len;
 };
@@ -63,39 +73,49 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
   uint64_t ticket = 0;
   {
     py::gil_scoped_release rel;
-    src.send_request(gh, nullptr, 0);
-    g = src.read_head();
-    bool ok = (g.status == 200 || g.status == 206) && !g.chunked && g.content_length == length;
-    if (!ok) {
-      // an error page is read for the message; a big unwanted body (a whole 200 where a 206
-      // slice was asked - If-Range on a changed source) is not: the connection is dropped
-      if (!g.chunked && g.content_length >= 0 && g.content_length <= (1 << 20))
-        gerr = src.read_body(g, 1 << 20);
-      else
-        src.mark_unusable();
-    } else {
-      int cork = 1;
-      setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
-      dst.send_raw(ph);
-      uint32_t c = 0;
-      if (crc && length > 0) {
-        char hx[32];
-        snprintf(hx, sizeof hx, "%llx\r\n", (unsigned long long)length);
-        dst.send_raw(hx);
+    try {
+      src.send_request(gh, nullptr, 0);
+      g = src.read_head();
+      bool ok = (g.status == 200 || g.status == 206) && !g.chunked && g.content_length == length;
+      if (!ok) {
+        // an error page is read for the message; a big unwanted body (a whole 200 where a 206
+        // slice was asked - If-Range on a changed source) is not: the connection is dropped
+        if (!g.chunked && g.content_length >= 0 && g.content_length <= (1 << 20))
+          gerr = src.read_body(g, 1 << 20);
+        else
+          src.mark_unusable();
+      } else {
+        int cork = 1;
+        setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+        dst.send_raw(ph);
+        uint32_t c = 0;
+        if (crc && length > 0) {
+          char hx[32];
+          snprintf(hx, sizeof hx, "%llx\r\n", (unsigned long long)length);
+          dst.send_raw(hx);
+        }
+        moved = split ? src.relay_body_hashed(dst, length, split->skip, split->full_len,
+                                              split->piece_len, prog, &digests, &head, &tail,
+                                              crc ? &c : nullptr, gpu ? &ticket : nullptr)
+                      : src.relay_body_to(dst, length, prog, crc ? &c : nullptr);
+        if (crc) {
+          crc_b64 = crc32c_base64(c);
+          dst.send_raw(std::string(length > 0 ? "\r\n" : "") + "0\r\nx-amz-checksum-crc32c:" +
+                       crc_b64 + "\r\n\r\n");
+        }
+        cork = 0;
+        setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
+        p = dst.read_head();
+        pbody = dst.read_body(p, max_body);
       }
-      moved = split ? src.relay_body_hashed(dst, length, split->skip, split->full_len,
-                                            split->piece_len, prog, &digests, &head, &tail,
-                                            crc ? &c : nullptr, gpu ? &ticket : nullptr)
-                    : src.relay_body_to(dst, length, prog, crc ? &c : nullptr);
-      if (crc) {
-        crc_b64 = crc32c_base64(c);
-        dst.send_raw(std::string(length > 0 ? "\r\n" : "") + "0\r\nx-amz-checksum-crc32c:" +
-                     crc_b64 + "\r\n\r\n");
-      }
-      cork = 0;
-      setsockopt(dst.fd(), IPPROTO_TCP, TCP_CORK, &cork, sizeof(cork));
-      p = dst.read_head();
-      pbody = dst.read_body(p, max_body);
+    } catch (...) {
+      forget_ticket(ticket);
+      throw;
+    }
+    // a refused PUT is retried from the GET: its queued digests are never asked for
+    if (ticket && !(p.status >= 200 && p.status < 300)) {
+      forget_ticket(ticket);
+      ticket = 0;
     }
   }
   py::dict d;

@@ -530,6 +530,7 @@ class NativeTransport(Transport):
                     nprog.cancel()
                 self._abort_slot(slot)
                 await _drain(fut)
+                self._forget_ticket(fut)
                 raise
             finally:
                 self._end_slot(slot)
@@ -546,6 +547,20 @@ class NativeTransport(Transport):
             src_headers = redirect_headers(src_url, nxt, src_headers)
             src_url = nxt
         raise TransportError(f"relay source: more than {MAX_REDIRECTS} redirects", 310)
+
+    def _forget_ticket(self, fut: "asyncio.Future") -> None:
+        """A cancelled relay that had queued its part to the GPU hasher: nobody will ask for
+        the digests, but the wait must still run to return the part's buffer to the pool."""
+        if not fut.done() or fut.cancelled() or fut.exception() is not None:
+            return
+        hashed = fut.result()[3]
+        if hashed and hashed.get("gpu_ticket"):
+            def wait(n=self._n, t=hashed["gpu_ticket"]) -> None:
+                try:
+                    n.gpu_part_wait(t)
+                except Exception:
+                    pass
+            threading.Thread(target=wait, name="gpu-part-forget", daemon=True).start()
 
     async def close(self) -> None:
         with self._lock:

@@ -163,7 +163,10 @@ async def gpu_part_digests(ticket: int) -> bytes:
     per ticket: it also returns the part's buffer to the relay pool."""
     import asyncio
     loop = asyncio.get_running_loop()
-    return await loop.run_in_executor(_part_wait_pool, native().gpu_part_wait, ticket)
+    # shielded: a cancelled caller (aborted job) must not cancel a wait still queued in the
+    # pool, or the ticket's part buffer would never return to the relay pool
+    return await asyncio.shield(
+        loop.run_in_executor(_part_wait_pool, native().gpu_part_wait, ticket))
 
 
 def gpu_relay_stats() -> dict:

@@ -4,6 +4,7 @@ fetches, refetch of corrupt data, clean abort, and the gate that picks this path
 from __future__ import annotations
 
 import asyncio
+import hashlib
 import os
 import types
 
@@ -417,6 +418,90 @@ def test_stream_async_part_hashing_with_host_double(run, tmp_path, make_cfg, ori
         assert after["host_fallbacks"] == before["host_fallbacks"]
         assert native().relay_pool_stats()["in_use"] == 0        # every lease came back
         await w.stop(); await s3.stop(); await origin.stop()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.01), 4)
+    try:
+        run(go())
+    finally:
+        hashing.use_part_hasher(None)
+
+
+def test_cancelled_digest_wait_still_returns_the_part_buffer(run, origin_cls):
+    """An aborted job cancels its pending ``gpu_part_digests``; a wait still queued behind
+    others in the wait pool must run anyway, or its part buffer never returns to the pool."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from downloader_amd.ops import hashing, native
+    from downloader_amd.s3.client import S3Client
+    from downloader_amd.s3.fake_server import FakeS3
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(4 << 20)
+        origin.blobs["/p.bin"] = blob
+        c = S3Client(ep, "minioadmin", "minioadmin")
+        await c.ensure_bucket("b")
+        tickets = []
+        for i in range(3):
+            _, h = await c.relay_hashed("b", f"k{i}", origin.url("/p.bin"), 0, len(blob), True,
+                                        (0, len(blob), 1 << 18), gpu=True)
+            assert h["gpu_ticket"] and not h["digests"]
+            tickets.append(h["gpu_ticket"])
+        assert native().relay_pool_stats()["in_use"] == 3
+        first = asyncio.ensure_future(hashing.gpu_part_digests(tickets[0]))
+        queued = [asyncio.ensure_future(hashing.gpu_part_digests(t)) for t in tickets[1:]]
+        await asyncio.sleep(0.01)
+        for q in queued:                      # still queued behind the first wait
+            q.cancel()
+        assert len(await first) == 20 * 16
+        for _ in range(300):
+            if native().relay_pool_stats()["in_use"] == 0:
+                break
+            await asyncio.sleep(0.02)
+        assert native().relay_pool_stats()["in_use"] == 0
+        await c.close(); await origin.stop(); await s3.stop()
+
+    saved = hashing._part_wait_pool
+    hashing.use_part_hasher(native().CpuPartHasher(0.2), 4)
+    hashing._part_wait_pool = ThreadPoolExecutor(max_workers=1)
+    try:
+        run(go())
+    finally:
+        hashing._part_wait_pool.shutdown(wait=True)
+        hashing._part_wait_pool = saved
+        hashing.use_part_hasher(None)
+
+
+def test_refused_put_releases_its_queued_part(run, origin_cls):
+    """A relayed part the S3 peer refuses (400 BadDigest after a flipped byte) had already been
+    queued to the part hasher: the relay waits that ticket out itself, the retry queues a new
+    one, and no buffer stays leased."""
+    from downloader_amd.ops import hashing, native
+    from downloader_amd.s3.client import S3Client
+    from downloader_amd.s3.fake_server import FakeS3
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(4 << 20)
+        origin.blobs["/p.bin"] = blob
+        c = S3Client(ep, "minioadmin", "minioadmin")
+        await c.ensure_bucket("b")
+        before = native().gpu_part_stats()["submitted"]
+        s3.corrupt_next = 1
+        _, h = await c.relay_hashed("b", "k", origin.url("/p.bin"), 0, len(blob), True,
+                                    (0, len(blob), 1 << 18), gpu=True)
+        assert s3.bad_digests == 1 and s3.get("b", "k") == blob
+        assert native().gpu_part_stats()["submitted"] - before == 2      # refused + retry
+        assert native().relay_pool_stats()["in_use"] == 1                # the retry's lease
+        digests = await hashing.gpu_part_digests(h["gpu_ticket"])
+        assert digests == b"".join(hashlib.sha1(blob[i:i + (1 << 18)]).digest()
+                                   for i in range(0, len(blob), 1 << 18))
+        assert native().relay_pool_stats()["in_use"] == 0
+        await c.close(); await origin.stop(); await s3.stop()
 
     hashing.use_part_hasher(native().CpuPartHasher(0.01), 4)
     try:
