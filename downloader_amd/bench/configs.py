@@ -497,9 +497,12 @@ async def config_small(a) -> Dict:
     so jobs/s and CPU-ms per job are the per-process cost of a job apart from its bytes."""
     stage = tempfile.mkdtemp(prefix="cfg9-")
     n = max(100, a.jobs)
+    spans = os.path.join(stage, "spans.jsonl")
     with Blobd(sink="discard") as b:
-        w = Worker(_cfg(a.mode, b.endpoint, stage, None, concurrency=a.concurrency),
-                   broker=MemoryBroker())
+        cfg = _cfg(a.mode, b.endpoint, stage, None, concurrency=a.concurrency)
+        if a.trace:                       # spans of every job and stage to a JSONL file
+            cfg.trace.enabled, cfg.trace.path = True, spans
+        w = Worker(cfg, broker=MemoryBroker())
         await w.start(health=False)
         warm = [api.make_download(f"c9-w{i}", "http", b.media_url(f"w{i}.mkv", 1000, i))
                 for i in range(min(100, n))]
@@ -511,6 +514,7 @@ async def config_small(a) -> Dict:
         dt, res = await _run_jobs(w, msgs)
         cpu, peer = _self_cpu() - c0, b.cpu_seconds() - p0
         await w.stop()
+    n_spans = sum(1 for _ in open(spans)) if a.trace and os.path.exists(spans) else 0
     shutil.rmtree(stage, ignore_errors=True)
     staged = sum(1 for r in res if r.outcome == "staged")
     lat = [r.seconds for r in res]
@@ -519,7 +523,8 @@ async def config_small(a) -> Dict:
             "jobs_per_s": round(n / dt, 1), "worker_cpu_ms_per_job": round(1000 * cpu / n, 3),
             "peer_cpu_ms_per_job": round(1000 * peer / n, 3),
             "p50_latency_s": round(statistics.median(lat), 4),
-            "p99_latency_s": round(_pct(lat, 0.99), 4)}
+            "p99_latency_s": round(_pct(lat, 0.99), 4),
+            "trace": bool(a.trace), "spans_written": n_spans}
 
 
 def main(argv=None) -> int:
@@ -531,6 +536,8 @@ def main(argv=None) -> int:
                          "(control-plane ceiling: tiny jobs through one worker, extra)")
     ap.add_argument("--small-kb", type=int, default=1,
                     help="config 9: object size in kB (jobs = --jobs, in flight = --concurrency)")
+    ap.add_argument("--trace", action="store_true",
+                    help="config 9: tracing on (spans to a JSONL file by the exporter thread)")
     ap.add_argument("--chaos-interval", type=float, default=2.0,
                     help="config 7: seconds between chaos actions (kill / connection drop)")
     ap.add_argument("--no-chaos-kill", dest="chaos_kill", action="store_false",
