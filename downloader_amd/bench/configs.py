@@ -500,7 +500,7 @@ async def config_small(a) -> Dict:
     spans = os.path.join(stage, "spans.jsonl")
     with Blobd(sink="discard") as b:
         cfg = _cfg(a.mode, b.endpoint, stage, None, concurrency=a.concurrency)
-        if a.trace:                       # spans of every job and stage to a JSONL file
+        if getattr(a, "trace", False):    # spans of every job and stage to a JSONL file
             cfg.trace.enabled, cfg.trace.path = True, spans
         w = Worker(cfg, broker=MemoryBroker())
         await w.start(health=False)
@@ -514,7 +514,7 @@ async def config_small(a) -> Dict:
         dt, res = await _run_jobs(w, msgs)
         cpu, peer = _self_cpu() - c0, b.cpu_seconds() - p0
         await w.stop()
-    n_spans = sum(1 for _ in open(spans)) if a.trace and os.path.exists(spans) else 0
+    n_spans = sum(1 for _ in open(spans)) if os.path.exists(spans) else 0
     shutil.rmtree(stage, ignore_errors=True)
     staged = sum(1 for r in res if r.outcome == "staged")
     lat = [r.seconds for r in res]
@@ -524,7 +524,7 @@ async def config_small(a) -> Dict:
             "peer_cpu_ms_per_job": round(1000 * peer / n, 3),
             "p50_latency_s": round(statistics.median(lat), 4),
             "p99_latency_s": round(_pct(lat, 0.99), 4),
-            "trace": bool(a.trace), "spans_written": n_spans}
+            "trace": bool(getattr(a, "trace", False)), "spans_written": n_spans}
 
 
 def main(argv=None) -> int:

@@ -231,6 +231,13 @@ class HttpConn {
   // Relay through a user-space buffer (either side is TLS).
   int64_t relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
                      uint32_t* crc = nullptr);
+  // Plain sockets, bytes needed in user space (CRC, piece hashing): splice socket -> pipe ->
+  // socket and read a tee()d duplicate of every chunk into memory the caller names
+  // (room(len) -> where up to len bytes go, may lower len; got(p, k) after each read).
+  template <class Room, class Got>
+  int64_t relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* prog, Room&& room,
+                    Got&& got);
+  void ensure_pipes(bool tee);
   std::string host_;
   int port_;
   int fd_ = -1;

@@ -17,6 +17,7 @@
 #include <thread>
 #include <arpa/inet.h>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <fcntl.h>
 #include <netdb.h>
@@ -629,6 +630,15 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
   return written;
 }
 
+// STAGER_RELAY_TEE=0: user-space relays recv + send instead (A/B of the tee path).
+static bool relay_tee_on() {
+  static const bool on = [] {
+    const char* e = getenv("STAGER_RELAY_TEE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32_t* crc) {
   int64_t moved = 0;
   if (rpos_ < rend_) {
@@ -640,22 +650,98 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
   if (moved == n) return moved;
-  if (ssl_ || dst.ssl_) return relay_copy(dst, n, moved, prog, crc);
+  if (ssl_ || dst.ssl_ || (crc && !relay_tee_on())) return relay_copy(dst, n, moved, prog, crc);
+  if (crc) {
+    thread_local std::vector<uint8_t> cbuf(256 * 1024);   // L2-resident CRC staging
+    return relay_tee(
+        dst, n, moved, prog,
+        [&](size_t& len) {
+          len = std::min(len, cbuf.size());
+          return cbuf.data();
+        },
+        [&](const uint8_t* p, size_t k) { *crc = stager::crc32c(p, k, *crc); });
+  }
+  ensure_pipes(false);
+  while (moved < n) {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("cancelled");
+    }
+    size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)pipe_sz_);
+    ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+    if (in < 0) {
+      if (errno == EINTR) continue;
+      reusable_ = false;
+      dst.reusable_ = false;
+      if (errno == EAGAIN) throw IoError("recv timeout");
+      throw IoError(errstr("splice(src)"));
+    }
+    if (in == 0) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("source closed mid-body");
+    }
+    ssize_t left = in;
+    while (left > 0) {
+      ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)left,
+                             SPLICE_F_MOVE | SPLICE_F_MORE);
+      if (out < 0) {
+        if (errno == EINTR) continue;
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError(errstr("splice(dst)"));
+      }
+      left -= out;
+    }
+    moved += in;
+    if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
+  }
+  return moved;
+}
+
+void HttpConn::ensure_pipes(bool tee) {
   if (pipe_[0] < 0) {
     if (pipe2(pipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
     int got = fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
     pipe_sz_ = got > 0 ? (size_t)got : 65536;
   }
-  if (crc && tpipe_[0] < 0) {
+  if (tee && tpipe_[0] < 0) {
     if (pipe2(tpipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
     fcntl(tpipe_[1], F_SETPIPE_SZ, (int)pipe_sz_);   // smaller: tee duplicates less per call
   }
+}
+
+// The bytes sent and the bytes the caller sees are the same pipe pages: splice moves page
+// references socket -> pipe -> socket, tee() duplicates the references into a second pipe and
+// only that duplicate is copied out (one user-space copy, where recv + send made two and
+// allocated fresh socket-buffer pages for the send).
+template <class Room, class Got>
+int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
+                            Room&& room, Got&& got) {
   auto fail = [&](const char* what) {
     reusable_ = false;
     dst.reusable_ = false;
     throw IoError(errstr(what));
   };
-  thread_local std::vector<uint8_t> cbuf(256 * 1024);   // L2-resident CRC staging
+  // bytes that arrived with the response head
+  while (moved < n && rpos_ < rend_) {
+    size_t len = (size_t)std::min<int64_t>(n - moved, (int64_t)(rend_ - rpos_));
+    uint8_t* p = room(len);
+    memcpy(p, rbuf_.data() + rpos_, len);
+    rpos_ += len;
+    got(p, len);
+    try {
+      dst.send_all(p, len);
+    } catch (...) {
+      reusable_ = false;
+      throw;
+    }
+    moved += (int64_t)len;
+    if (prog) prog->bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
+  }
+  if (moved == n) return moved;
+  ensure_pipes(true);
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
@@ -680,30 +766,26 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     }
     ssize_t left = in;
     while (left > 0) {
-      ssize_t chunk = left;
-      if (crc) {
-        // duplicate the pipe's pages (no copy), read the duplicate: the CRC sees exactly the
-        // bytes the next splice sends
-        ssize_t t = ::tee(pipe_[0], tpipe_[1], (size_t)left, 0);
-        if (t < 0) {
-          if (errno == EINTR) continue;
-          fail("tee");
-        }
-        if (t == 0) {
-          reusable_ = false;
-          dst.reusable_ = false;
-          throw IoError("tee: no data");
-        }
-        for (ssize_t got = 0; got < t;) {
-          ssize_t r = ::read(tpipe_[0], cbuf.data(), (size_t)std::min<ssize_t>(t - got, (ssize_t)cbuf.size()));
-          if (r < 0 && errno == EINTR) continue;
-          if (r <= 0) fail("read(tee)");
-          *crc = stager::crc32c(cbuf.data(), (size_t)r, *crc);
-          got += r;
-        }
-        chunk = t;
+      ssize_t t = ::tee(pipe_[0], tpipe_[1], (size_t)left, 0);
+      if (t < 0) {
+        if (errno == EINTR) continue;
+        fail("tee");
       }
-      while (chunk > 0) {
+      if (t == 0) {
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError("tee: no data");
+      }
+      for (ssize_t seen = 0; seen < t;) {
+        size_t len = (size_t)(t - seen);
+        uint8_t* p = room(len);
+        ssize_t r = ::read(tpipe_[0], p, len);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) fail("read(tee)");
+        got(p, (size_t)r);
+        seen += r;
+      }
+      for (ssize_t chunk = t; chunk > 0;) {
         ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)chunk,
                                SPLICE_F_MOVE | SPLICE_F_MORE);
         if (out < 0) {
@@ -711,8 +793,8 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
           fail("splice(dst)");
         }
         chunk -= out;
-        left -= out;
       }
+      left -= t;
     }
     moved += in;
     if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
@@ -764,8 +846,9 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
   if (npieces >= 8 && n <= kMaxBufferedPart && sha1_mb_supported())
     return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail, crc,
                                 gpu_ticket);
-  // Chunk size: 512 KiB stays in a Zen 5 core's 1 MiB L2 between the recv copy, the send
-  // copy and the SHA-1 pass, so the payload is read from DRAM once.
+  // Chunk size: 512 KiB stays in a Zen 5 core's 1 MiB L2 between the copy in (a tee()d
+  // duplicate on plain sockets, recv on TLS), the send copy (TLS) and the SHA-1 pass, so the
+  // payload is read from DRAM once.
   thread_local std::vector<uint8_t> buf(512 * 1024);
   Hasher h("sha1");
   const int64_t full_end = skip + full_len;
@@ -794,6 +877,19 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
       k -= t;
     }
   };
+  if (!ssl_ && !dst.ssl_ && relay_tee_on()) {
+    relay_tee(
+        dst, n, 0, prog,
+        [&](size_t& len) {
+          len = std::min(len, buf.size());
+          return buf.data();
+        },
+        [&](const uint8_t* p, size_t k) {
+          if (crc) *crc = stager::crc32c(p, k, *crc);
+          consume(p, (int64_t)k);
+        });
+    return pos;
+  }
   while (pos < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
@@ -1157,13 +1253,25 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
                                        std::string* digests, std::string* head,
                                        std::string* tail, uint32_t* crc,
                                        uint64_t* gpu_ticket) {
-  // The whole part lands in a per-thread buffer on its way to `dst` (recv into it, send from
-  // it: the same two copies as the chunked path), then its pieces are hashed 16 at a time in
+  // The whole part lands in a pooled buffer on its way to `dst` (plain sockets: a tee()d copy
+  // of the spliced pages; TLS: recv into it, send from it), then its pieces are hashed 16 at a time in
   // the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the per-core rate of a single SHA-NI
   // chain, which bounds the chunked path once many parts are in flight.
   PartLease lease((size_t)n);
   uint8_t* b = lease.b->data;
   int64_t pos = 0;
+  if (!ssl_ && !dst.ssl_ && relay_tee_on()) {
+    relay_tee(
+        dst, n, 0, prog,
+        [&](size_t& len) {
+          len = std::min<size_t>(len, (size_t)(n - pos));
+          return b + pos;
+        },
+        [&](const uint8_t* p, size_t k) {
+          if (crc) *crc = stager::crc32c(p, k, *crc);
+          pos += (int64_t)k;
+        });
+  }
   while (pos < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
