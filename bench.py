@@ -250,10 +250,22 @@ async def _timed(args, worker, url, wid: int, mode: str, count: int) -> dict:
     loop_cpu = time.thread_time() - loop_cpu0
     t1 = time.perf_counter()
     bad = [r for r in res if r.outcome != "staged"]
+    pipes = _pipe_stats()
     # event-loop thread CPU / wall: ~1.0 means the Python side (one thread) is the limit
     return {"elapsed": t1 - t0, "latencies": [r.seconds for r in res],
             "bytes": sum(r.bytes for r in res), "failed": len(bad),
-            "err": bad[0].error if bad else "", "loop_busy": loop_cpu / max(1e-9, t1 - t0)}
+            "err": bad[0].error if bad else "", "loop_busy": loop_cpu / max(1e-9, t1 - t0),
+            "pipes_created": pipes.get("created", 0), "pipes_short": pipes.get("short", 0)}
+
+
+def _pipe_stats() -> dict:
+    """This process' splice pipes (``short``: created below the asked capacity because the
+    user's pipe page budget, fs.pipe-user-pages-soft, was spent)."""
+    try:
+        from downloader_amd.ops import native
+        return dict(native().pipe_stats())
+    except Exception:
+        return {}
 
 
 async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str, on_go=None):
@@ -348,11 +360,14 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
             "bytes": sum(o["bytes"] for o in outs), "failed": sum(o["failed"] for o in outs),
             "err": next((o["err"] for o in outs if o["err"]), ""),
             "loop_busy": max(o["loop_busy"] for o in outs),
+            "pipes_created": sum(o["pipes_created"] for o in outs),
+            "pipes_short": sum(o["pipes_short"] for o in outs),
             "child_cpu_s": sum(o["worker_cpu_s"] for o in outs)}
 
 
 SINK_KEYS = ("bytes_received", "verify_objects", "verify_bytes", "verify_mismatches",
-             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests")
+             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests",
+             "pipes_short")
 
 
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 1,
@@ -412,7 +427,9 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
             "parts_per_object": round(sink["multipart_parts"] / mp, 3) if mp else 1.0,
             "worker_cpu_s_per_GB": sum(r["worker_cpu_s"] for r in allr) / gb_all,
             "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all,
-            "loop_busy": max(r["loop_busy"] for r in allr)}
+            "loop_busy": max(r["loop_busy"] for r in allr),
+            "pipes_created": sum(r["pipes_created"] for r in allr),
+            "pipes_short": sum(r["pipes_short"] for r in allr)}
 
 
 def pin_rank(dist: Dist, per_rank: int = 0) -> list:
@@ -502,6 +519,9 @@ def main() -> int:
             "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
             "event_loop_busy": round(tuned["loop_busy"], 3),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
+            # splice pipes created below their asked capacity (pipe page budget spent)
+            "pipes_short": {"workers": tuned["pipes_short"], "of": tuned["pipes_created"],
+                            "sink": tuned["sink"]["pipes_short"]},
             "peers": args.peers,
             "cpus_per_rank": len(pinned) if pinned else len(os.sched_getaffinity(0)),
             "rank_cpus": [t["cpus"] for t in topo],

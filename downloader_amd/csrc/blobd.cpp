@@ -117,6 +117,8 @@ std::atomic<uint64_t> g_verify_objects{0}, g_verify_bytes{0}, g_verify_mismatch{
     g_verify_unknown{0}, g_bad_digest{0}, g_checksummed{0}, g_corrupted{0}, g_parts{0},
     g_mp_objects{0}, g_mp_parts{0};
 int g_devnull = -1;
+size_t g_pipe_bytes = size_t(512) << 10;      // sink splice pipe capacity (--pipe-kb)
+std::atomic<uint64_t> g_pipes_short{0};       // pipes created below it (budget spent)
 int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
@@ -380,10 +382,6 @@ class Conn {
   ~Conn() {
     if (ssl_) SSL_free(ssl_);
     ::close(fd_);
-    if (pipe_[0] >= 0) {
-      ::close(pipe_[0]);
-      ::close(pipe_[1]);
-    }
   }
 
   void serve() {
@@ -526,11 +524,22 @@ class Conn {
     return true;
   }
 
+  // The pipe lives for one body only: an unprivileged user's pipes share one page budget
+  // (fs.pipe-user-pages-soft, 64 MiB by default) with the workers' relays on the same box, and
+  // a pipe per kept-alive connection held it even while the connection idled.
   bool splice_plain(int64_t n, Consumer& c, uint64_t pos) {
-    if (pipe_[0] < 0) {
-      if (pipe2(pipe_, O_CLOEXEC) != 0) return false;
-      fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
-    }
+    struct PipeFd {
+      int fd[2] = {-1, -1};
+      ~PipeFd() {
+        if (fd[0] >= 0) ::close(fd[0]);
+        if (fd[1] >= 0) ::close(fd[1]);
+      }
+    } pp;
+    if (pipe2(pp.fd, O_CLOEXEC) != 0) return false;
+    int* pipe_ = pp.fd;
+    fcntl(pipe_[1], F_SETPIPE_SZ, (int)g_pipe_bytes);
+    const int cap = fcntl(pipe_[1], F_GETPIPE_SZ);
+    if (cap < (int)g_pipe_bytes) g_pipes_short++;
     uint8_t win[16384];
     while (n > 0) {
       if (c.windows && c.in_window(pos)) {   // a sampled window: recv exactly its bytes
@@ -549,7 +558,7 @@ class Conn {
                                 : pos + (uint64_t)n;
       int64_t run = (int64_t)(stop - pos);
       while (run > 0) {
-        ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, (size_t)std::min<int64_t>(run, 1 << 20),
+        ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, (size_t)std::min<int64_t>(run, cap > 0 ? cap : 65536),
                               SPLICE_F_MOVE | SPLICE_F_MORE);
         if (in < 0 && errno == EINTR) continue;
         if (in <= 0) return false;
@@ -1115,11 +1124,12 @@ class Conn {
              ",\"sink\":\"%s\",\"verify_objects\":%" PRIu64 ",\"verify_bytes\":%" PRIu64
              ",\"verify_mismatches\":%" PRIu64 ",\"verify_unknown\":%" PRIu64
              ",\"checksummed_puts\":%" PRIu64 ",\"bad_digests\":%" PRIu64 ",\"corrupted\":%" PRIu64
-             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64 "}",
+             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64
+             ",\"pipes_short\":%" PRIu64 "}",
              g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup, g_s3_faults.load(), sink,
              g_verify_objects.load(), g_verify_bytes.load(), g_verify_mismatch.load(),
              g_verify_unknown.load(), g_checksummed.load(), g_bad_digest.load(), g_corrupted.load(),
-             g_parts.load(), g_mp_objects.load(), g_mp_parts.load());
+             g_parts.load(), g_mp_objects.load(), g_mp_parts.load(), g_pipes_short.load());
     return respond(200, "OK", b, "", "application/json");
   }
 
@@ -1134,7 +1144,6 @@ class Conn {
   SSL* ssl_ = nullptr;
   std::vector<uint8_t> buf_;
   size_t pos_ = 0, end_ = 0;
-  int pipe_[2] = {-1, -1};
 };
 
 }  // namespace
@@ -1161,6 +1170,7 @@ int main(int argc, char** argv) {
     }
     else if (a == "--sample-stride") g_sample_stride = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
     else if (a == "--sample-len") g_sample_len = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
+    else if (a == "--pipe-kb") g_pipe_bytes = std::max<size_t>(4, strtoull(next(), nullptr, 10)) << 10;
     else if (a == "--s3-corrupt-rate") g_s3_corrupt_rate = atof(next());
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
@@ -1180,7 +1190,7 @@ int main(int argc, char** argv) {
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
                       "[--default-size N] [--files-root DIR] [--sink checksum|discard|sample|verify] "
-                      "[--sample-stride N] [--sample-len N] [--s3-corrupt-rate P] "
+                      "[--sample-stride N] [--sample-len N] [--pipe-kb N] [--s3-corrupt-rate P] "
                       "[--tls-cert PEM --tls-key PEM] [--s3-fail-rate P]\n");
       return 2;
     }

@@ -186,6 +186,20 @@ PYBIND11_MODULE(_native, m) {
         "Unmap every idle hashed-relay part buffer; returns the bytes freed");
   m.def("relay_pool_set_max_idle", &relay_pool_set_max_idle, py::arg("n"),
         "Keep at most n idle part buffers (the rest are unmapped on release)");
+  m.def("pipe_stats", []() {
+    PipeStats s = pipe_stats();
+    py::dict d;
+    d["created"] = s.created;
+    d["short"] = s.short_pipes;
+    d["in_use"] = s.in_use;
+    d["in_use_bytes"] = s.in_use_bytes;
+    d["idle"] = s.idle;
+    d["idle_bytes"] = s.idle_bytes;
+    return d;
+  }, "splice pipes: created, created below the asked capacity (the user's pipe page budget, "
+     "fs.pipe-user-pages-soft, is spent), leased / idle and their capacity");
+  m.def("set_pipe_sizes", &set_pipe_sizes, py::arg("main"), py::arg("tee") = 0,
+        "capacity asked for new splice pipes and tee() duplicate pipes (0 = keep)");
   m.def("relay_pool_stats", []() {
     RelayPoolStats s = relay_pool_stats();
     py::dict d;

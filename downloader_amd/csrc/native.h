@@ -113,6 +113,16 @@ std::string tls_error(SSL* s, int r, const std::string& what);
 // SHA-1; larger ones take the chunked (L2-sized, single-chain) path.
 constexpr int64_t kMaxBufferedPart = (int64_t)64 << 20;
 
+// Pipes of splice transfers (leased per transfer from a process-wide pool): created, created
+// smaller than asked (the user's pipe page budget is spent), in use / idle and their capacity.
+struct PipeStats {
+  uint64_t created, short_pipes;
+  size_t in_use, in_use_bytes, idle, idle_bytes;
+};
+PipeStats pipe_stats();
+// Capacity asked for new pipes: the splice pipe, and the tee() duplicate pipe (0 = keep).
+void set_pipe_sizes(size_t main, size_t tee);
+
 struct RelayPoolStats {
   size_t idle_buffers, idle_bytes, in_use, max_idle;
 };
@@ -237,15 +247,11 @@ class HttpConn {
   template <class Room, class Got>
   int64_t relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* prog, Room&& room,
                     Got&& got);
-  void ensure_pipes(bool tee);
   std::string host_;
   int port_;
   int fd_ = -1;
   SSL* ssl_ = nullptr;
   std::shared_ptr<TlsContext> tls_;  // keeps the SSL_CTX alive as long as ssl_
-  int pipe_[2] = {-1, -1};
-  int tpipe_[2] = {-1, -1};   // tee target of the CRC'd relay
-  size_t pipe_sz_ = 0;
   bool reusable_ = true;
   std::vector<uint8_t> rbuf_;
   size_t rpos_ = 0, rend_ = 0;

@@ -47,6 +47,94 @@ struct IoError : std::runtime_error {
 
 std::string errstr(const char* what) { return std::string(what) + ": " + strerror(errno); }
 
+// ---- pipes for splice transfers ----------------------------------------------------------
+// Leased per transfer from a process-wide pool instead of living on every connection: an
+// unprivileged user's pipes share one page budget (fs.pipe-user-pages-soft, 16384 pages =
+// 64 MiB by default, counted by capacity, not by bytes held). Past it F_SETPIPE_SZ is refused
+// and new pipes get two pages, and 1 MiB pipes kept on every pooled connection - idle ones
+// included, in the workers and in the S3 peer alike - ran a busy 16-relay worker into it.
+// Now only running transfers hold pipes (plus a few idle ones for reuse).
+std::atomic<size_t> g_pipe_main{size_t(1) << 20}, g_pipe_tee{size_t(256) << 10};
+std::atomic<uint64_t> g_pipes_created{0}, g_pipes_short{0};
+
+struct Pipe {
+  int r = -1, w = -1;
+  size_t cap = 0;
+};
+
+class PipePool {
+ public:
+  Pipe acquire(size_t want) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i = idle_.size(); i-- > 0;)
+        if (idle_[i].cap >= want || idle_[i].cap == short_cap_) {
+          Pipe p = idle_[i];
+          idle_.erase(idle_.begin() + (ptrdiff_t)i);
+          ++in_use_;
+          in_use_bytes_ += p.cap;
+          return p;
+        }
+    }
+    int fds[2];
+    if (pipe2(fds, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
+    Pipe p{fds[0], fds[1], 0};
+    fcntl(p.w, F_SETPIPE_SZ, (int)want);
+    int got = fcntl(p.w, F_GETPIPE_SZ);
+    p.cap = got > 0 ? (size_t)got : 4096;
+    g_pipes_created++;
+    std::lock_guard<std::mutex> g(mu_);
+    if (p.cap < want) {
+      g_pipes_short++;
+      short_cap_ = p.cap;      // the budget is spent: take what an idle pipe has from now on
+    }
+    ++in_use_;
+    in_use_bytes_ += p.cap;
+    return p;
+  }
+  // `clean`: the transfer drained the pipe (an aborted one may leave bytes: closed instead)
+  void release(Pipe p, bool clean) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      --in_use_;
+      in_use_bytes_ -= p.cap;
+      if (clean && idle_.size() < kMaxIdle) {
+        idle_.push_back(p);
+        return;
+      }
+    }
+    ::close(p.r);
+    ::close(p.w);
+  }
+  PipeStats stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t idle_bytes = 0;
+    for (auto& p : idle_) idle_bytes += p.cap;
+    return PipeStats{g_pipes_created.load(), g_pipes_short.load(), in_use_, in_use_bytes_,
+                     idle_.size(), idle_bytes};
+  }
+
+ private:
+  static constexpr size_t kMaxIdle = 8;
+  std::mutex mu_;
+  std::vector<Pipe> idle_;
+  size_t in_use_ = 0, in_use_bytes_ = 0, short_cap_ = 0;
+};
+
+PipePool& pipe_pool() {
+  static PipePool* p = new PipePool();   // never destroyed: transfer threads may outlive exit
+  return *p;
+}
+
+struct PipeLease {
+  Pipe p;
+  bool clean = false;
+  explicit PipeLease(size_t want) : p(pipe_pool().acquire(want)) {}
+  ~PipeLease() { pipe_pool().release(p, clean); }
+  PipeLease(const PipeLease&) = delete;
+  PipeLease& operator=(const PipeLease&) = delete;
+};
+
 void set_timeouts(int fd, double s) {
   if (s <= 0) return;
   timeval tv;
@@ -211,12 +299,6 @@ void HttpConn::close() {
   }
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
-  for (int* fds : {pipe_, tpipe_})
-    for (int i = 0; i < 2; ++i)
-      if (fds[i] >= 0) {
-        ::close(fds[i]);
-        fds[i] = -1;
-      }
 }
 
 void HttpConn::abort() {
@@ -545,18 +627,20 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
     }
     if (n == 0) return;
     // 2) zero-copy: socket -> pipe -> file (plain sockets only: TLS bytes need decrypting).
-    if (!ssl_ && pipe_[0] < 0) {
-      if (pipe2(pipe_, O_CLOEXEC) == 0) {
-        int want = 1 << 20;
-        int got = fcntl(pipe_[1], F_SETPIPE_SZ, want);
-        pipe_sz_ = got > 0 ? (size_t)got : 65536;
+    std::unique_ptr<PipeLease> pl;
+    if (!ssl_) {
+      try {
+        pl.reset(new PipeLease(g_pipe_main.load()));
+      } catch (const IoError&) {
       }
     }
-    if (!ssl_ && pipe_[0] >= 0) {
+    if (pl) {
+      const int pr = pl->p.r, pw = pl->p.w;
+      const size_t psz = pl->p.cap;
       while (n != 0) {
         check_cancel();
-        size_t want = n < 0 ? pipe_sz_ : (size_t)std::min<int64_t>(n, (int64_t)pipe_sz_);
-        ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+        size_t want = n < 0 ? psz : (size_t)std::min<int64_t>(n, (int64_t)psz);
+        ssize_t in = ::splice(fd_, nullptr, pw, nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
         if (in < 0) {
           if (errno == EINTR) continue;
           if (errno == EINVAL) break;  // fs does not support splice: fall back below
@@ -572,7 +656,7 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
         ssize_t left = in;
         while (left > 0) {
           loff_t o = offset + written;
-          ssize_t out = ::splice(pipe_[0], nullptr, fd, &o, (size_t)left, SPLICE_F_MOVE);
+          ssize_t out = ::splice(pr, nullptr, fd, &o, (size_t)left, SPLICE_F_MOVE);
           if (out < 0) {
             if (errno == EINTR) continue;
             reusable_ = false;
@@ -588,6 +672,7 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
           throw IoError("response body exceeds limit");
         }
       }
+      pl->clean = true;        // every spliced byte went on to the file
       if (n == 0) return;
     }
     // 3) fallback: recv + pwrite.
@@ -661,15 +746,16 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
         },
         [&](const uint8_t* p, size_t k) { *crc = stager::crc32c(p, k, *crc); });
   }
-  ensure_pipes(false);
+  PipeLease pl(g_pipe_main.load());
+  const int pr = pl.p.r, pw = pl.p.w;
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
       dst.reusable_ = false;
       throw IoError("cancelled");
     }
-    size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)pipe_sz_);
-    ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+    size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)pl.p.cap);
+    ssize_t in = ::splice(fd_, nullptr, pw, nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
     if (in < 0) {
       if (errno == EINTR) continue;
       reusable_ = false;
@@ -684,7 +770,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     }
     ssize_t left = in;
     while (left > 0) {
-      ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)left,
+      ssize_t out = ::splice(pr, nullptr, dst.fd_, nullptr, (size_t)left,
                              SPLICE_F_MOVE | SPLICE_F_MORE);
       if (out < 0) {
         if (errno == EINTR) continue;
@@ -697,19 +783,8 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     moved += in;
     if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
   }
+  pl.clean = true;
   return moved;
-}
-
-void HttpConn::ensure_pipes(bool tee) {
-  if (pipe_[0] < 0) {
-    if (pipe2(pipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
-    int got = fcntl(pipe_[1], F_SETPIPE_SZ, 1 << 20);
-    pipe_sz_ = got > 0 ? (size_t)got : 65536;
-  }
-  if (tee && tpipe_[0] < 0) {
-    if (pipe2(tpipe_, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
-    fcntl(tpipe_[1], F_SETPIPE_SZ, (int)pipe_sz_);   // smaller: tee duplicates less per call
-  }
 }
 
 // The bytes sent and the bytes the caller sees are the same pipe pages: splice moves page
@@ -741,15 +816,15 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
     if (prog) prog->bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
   }
   if (moved == n) return moved;
-  ensure_pipes(true);
+  PipeLease main(g_pipe_main.load()), dup(g_pipe_tee.load());
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
       dst.reusable_ = false;
       throw IoError("cancelled");
     }
-    size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)pipe_sz_);
-    ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+    size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)main.p.cap);
+    ssize_t in = ::splice(fd_, nullptr, main.p.w, nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
     if (in < 0) {
       if (errno == EINTR) continue;
       if (errno == EAGAIN) {
@@ -766,7 +841,7 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
     }
     ssize_t left = in;
     while (left > 0) {
-      ssize_t t = ::tee(pipe_[0], tpipe_[1], (size_t)left, 0);
+      ssize_t t = ::tee(main.p.r, dup.p.w, (size_t)left, 0);
       if (t < 0) {
         if (errno == EINTR) continue;
         fail("tee");
@@ -779,14 +854,14 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
       for (ssize_t seen = 0; seen < t;) {
         size_t len = (size_t)(t - seen);
         uint8_t* p = room(len);
-        ssize_t r = ::read(tpipe_[0], p, len);
+        ssize_t r = ::read(dup.p.r, p, len);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) fail("read(tee)");
         got(p, (size_t)r);
         seen += r;
       }
       for (ssize_t chunk = t; chunk > 0;) {
-        ssize_t out = ::splice(pipe_[0], nullptr, dst.fd_, nullptr, (size_t)chunk,
+        ssize_t out = ::splice(main.p.r, nullptr, dst.fd_, nullptr, (size_t)chunk,
                                SPLICE_F_MOVE | SPLICE_F_MORE);
         if (out < 0) {
           if (errno == EINTR) continue;
@@ -799,6 +874,7 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
     moved += in;
     if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
   }
+  main.clean = dup.clean = true;
   return moved;
 }
 
@@ -1245,6 +1321,11 @@ std::string gpu_part_wait(uint64_t ticket) {
 }
 
 size_t relay_pool_trim() { return part_pool().trim(); }
+PipeStats pipe_stats() { return pipe_pool().stats(); }
+void set_pipe_sizes(size_t main, size_t tee) {
+  if (main) g_pipe_main.store(main);
+  if (tee) g_pipe_tee.store(tee);
+}
 void relay_pool_set_max_idle(size_t n) { part_pool().set_max_idle(n); }
 RelayPoolStats relay_pool_stats() { return part_pool().stats(); }
 

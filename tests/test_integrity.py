@@ -132,6 +132,9 @@ def test_plain_relay_checksum_policy(run, origin_cls, policy, expect_crc):
         c.multipart_threshold = 64 << 20
         await c.relay_object("b", "one", origin.url("/r.mkv"), len(blob))
         assert s3.get("b", "one") == blob
+        from downloader_amd.ops import native
+        ps = native().pipe_stats()      # pipes are leased per transfer, all returned
+        assert ps["in_use"] == 0 and ps["idle"] <= 8
         await c.close()
         await origin.stop()
         await s3.stop()
