@@ -80,6 +80,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-compare-single-put", dest="compare_single_put", action="store_false",
                    help="skip the same-call comparison run with round-2 settings (objects up to "
                         "128 MiB in one PUT)")
+    p.add_argument("--pipe-kb", type=int, default=0,
+                   help="splice pipe KiB per transfer (0: the uid's pipe budget / workers)")
     p.add_argument("--checksum", choices=["auto", "always", "off"], default="",
                    help="s3.checksum: CRC32C per PUT/part (auto = where bytes cross user space "
                         "anyway, i.e. not this plain-http splice relay; always = the relay copies "
@@ -197,6 +199,8 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
         "broker": {"backend": "memory"},
         "health": {"enabled": False},
     }
+    if getattr(args, "pipe_kb_eff", 0):
+        over["download"]["pipe_kb"] = args.pipe_kb_eff
     ca = getattr(args, "ca_file", "")
     if args.tls != "off":
         over["s3"]["secure"] = True
@@ -366,8 +370,7 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
 
 
 SINK_KEYS = ("bytes_received", "verify_objects", "verify_bytes", "verify_mismatches",
-             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests",
-             "pipes_short")
+             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests")
 
 
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 1,
@@ -482,6 +485,12 @@ def main() -> int:
         nproc = max(1, min(8, len(pinned or os.sched_getaffinity(0)) // 8))
     if args.mode == "reference" and args.procs_per_rank <= 0:
         nproc = 1    # the reference is one serial consumer per container (explicit N: N of them)
+    # Splice pipes: every worker process on the node shares one uid's pipe page budget
+    # (64 MiB for the unprivileged user of the GPU boxes); size them for world x procs workers
+    # with concurrency x 2 parts (+2 spare) relays each, or take --pipe-kb as given.
+    from downloader_amd.utils import limits
+    args.pipe_kb_eff = args.pipe_kb or limits.pipe_size(
+        0, sharers=dist.world * nproc, per_proc=args.concurrency * 2 + 2) >> 10
     try:
         tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
         single = None
@@ -520,8 +529,8 @@ def main() -> int:
             "event_loop_busy": round(tuned["loop_busy"], 3),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
             # splice pipes created below their asked capacity (pipe page budget spent)
-            "pipes_short": {"workers": tuned["pipes_short"], "of": tuned["pipes_created"],
-                            "sink": tuned["sink"]["pipes_short"]},
+            "pipes_short": {"workers": tuned["pipes_short"], "of": tuned["pipes_created"]},
+            "pipe_kb": args.pipe_kb_eff,
             "peers": args.peers,
             "cpus_per_rank": len(pinned) if pinned else len(os.sched_getaffinity(0)),
             "rank_cpus": [t["cpus"] for t in topo],

@@ -24,8 +24,8 @@
 //
 // --sink picks what happens to large S3 bodies:
 //   checksum  every byte folded into the checksum (default)
-//   discard   spliced socket -> /dev/null, no user-space copy
-//   sample    spliced like discard, but a window of --sample-len bytes every --sample-stride
+//   discard   dropped in the kernel (recv MSG_TRUNC), no user-space copy
+//   sample    dropped like discard, but a window of --sample-len bytes every --sample-stride
 //             bytes (plus the body's last window) is read and kept, then compared with the
 //             bytes the origin generator produced for that object once its offset is known
 //   verify    every byte CRC32C'd on arrival, compared at completion with the CRC32C of the
@@ -108,7 +108,7 @@ std::vector<uint8_t> g_pool;  // random pool the origin serves from
 size_t g_keep_bytes = 1 << 20;
 enum SinkMode { kSinkChecksum, kSinkDiscard, kSinkSample, kSinkVerify };
 SinkMode g_sink = kSinkChecksum;
-bool g_discard = false;     // large bodies spliced to /dev/null (--sink discard | sample)
+bool g_discard = false;     // large bodies dropped in the kernel (--sink discard | sample)
 uint64_t g_sample_stride = 1 << 20, g_sample_len = 4096;
 double g_s3_corrupt_rate = 0;
 std::mutex g_media_mu;
@@ -116,9 +116,6 @@ std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> g_media;  // base
 std::atomic<uint64_t> g_verify_objects{0}, g_verify_bytes{0}, g_verify_mismatch{0},
     g_verify_unknown{0}, g_bad_digest{0}, g_checksummed{0}, g_corrupted{0}, g_parts{0},
     g_mp_objects{0}, g_mp_parts{0};
-int g_devnull = -1;
-size_t g_pipe_bytes = size_t(512) << 10;      // sink splice pipe capacity (--pipe-kb)
-std::atomic<uint64_t> g_pipes_short{0};       // pipes created below it (budget spent)
 int g_pool_fd = -1;         // memfd holding the origin pool (sendfile source)
 std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with sendfile (webseeds)
 uint64_t g_default_size = 100ull << 20;
@@ -511,7 +508,7 @@ class Conn {
       g_rx += k;
     }
     if (n == 0) return true;
-    if (!c.needs_all() && !ssl_) return splice_plain(n, c, pos);
+    if (!c.needs_all() && !ssl_) return discard_plain(n, c, pos);
     while (n > 0) {
       if (pos_ == end_ && !fill()) return false;
       size_t k = (size_t)std::min<int64_t>(n, (int64_t)(end_ - pos_));
@@ -524,22 +521,10 @@ class Conn {
     return true;
   }
 
-  // The pipe lives for one body only: an unprivileged user's pipes share one page budget
-  // (fs.pipe-user-pages-soft, 64 MiB by default) with the workers' relays on the same box, and
-  // a pipe per kept-alive connection held it even while the connection idled.
-  bool splice_plain(int64_t n, Consumer& c, uint64_t pos) {
-    struct PipeFd {
-      int fd[2] = {-1, -1};
-      ~PipeFd() {
-        if (fd[0] >= 0) ::close(fd[0]);
-        if (fd[1] >= 0) ::close(fd[1]);
-      }
-    } pp;
-    if (pipe2(pp.fd, O_CLOEXEC) != 0) return false;
-    int* pipe_ = pp.fd;
-    fcntl(pipe_[1], F_SETPIPE_SZ, (int)g_pipe_bytes);
-    const int cap = fcntl(pipe_[1], F_GETPIPE_SZ);
-    if (cap < (int)g_pipe_bytes) g_pipes_short++;
+  // Bytes nobody needs are dropped in the kernel with recv(MSG_TRUNC) (TCP discards them
+  // without copying): no pipe, so the sink holds nothing of the user's pipe page budget
+  // (fs.pipe-user-pages-soft, shared with the workers' relays on the same box).
+  bool discard_plain(int64_t n, Consumer& c, uint64_t pos) {
     uint8_t win[16384];
     while (n > 0) {
       if (c.windows && c.in_window(pos)) {   // a sampled window: recv exactly its bytes
@@ -558,17 +543,11 @@ class Conn {
                                 : pos + (uint64_t)n;
       int64_t run = (int64_t)(stop - pos);
       while (run > 0) {
-        ssize_t in = ::splice(fd_, nullptr, pipe_[1], nullptr, (size_t)std::min<int64_t>(run, cap > 0 ? cap : 65536),
-                              SPLICE_F_MOVE | SPLICE_F_MORE);
+        // no buffer: TCP drops MSG_TRUNC bytes without copying (and a 16 KiB one with a
+        // longer length trips _FORTIFY_SOURCE's recv check)
+        ssize_t in = ::recv(fd_, nullptr, (size_t)std::min<int64_t>(run, 1 << 20), MSG_TRUNC);
         if (in < 0 && errno == EINTR) continue;
         if (in <= 0) return false;
-        ssize_t left = in;
-        while (left > 0) {
-          ssize_t out = ::splice(pipe_[0], nullptr, g_devnull, nullptr, (size_t)left, SPLICE_F_MOVE);
-          if (out < 0 && errno == EINTR) continue;
-          if (out <= 0) return false;
-          left -= out;
-        }
         run -= in;
         n -= in;
         pos += (uint64_t)in;
@@ -1124,12 +1103,11 @@ class Conn {
              ",\"sink\":\"%s\",\"verify_objects\":%" PRIu64 ",\"verify_bytes\":%" PRIu64
              ",\"verify_mismatches\":%" PRIu64 ",\"verify_unknown\":%" PRIu64
              ",\"checksummed_puts\":%" PRIu64 ",\"bad_digests\":%" PRIu64 ",\"corrupted\":%" PRIu64
-             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64
-             ",\"pipes_short\":%" PRIu64 "}",
+             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64 "}",
              g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup, g_s3_faults.load(), sink,
              g_verify_objects.load(), g_verify_bytes.load(), g_verify_mismatch.load(),
              g_verify_unknown.load(), g_checksummed.load(), g_bad_digest.load(), g_corrupted.load(),
-             g_parts.load(), g_mp_objects.load(), g_mp_parts.load(), g_pipes_short.load());
+             g_parts.load(), g_mp_objects.load(), g_mp_parts.load());
     return respond(200, "OK", b, "", "application/json");
   }
 
@@ -1170,7 +1148,6 @@ int main(int argc, char** argv) {
     }
     else if (a == "--sample-stride") g_sample_stride = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
     else if (a == "--sample-len") g_sample_len = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
-    else if (a == "--pipe-kb") g_pipe_bytes = std::max<size_t>(4, strtoull(next(), nullptr, 10)) << 10;
     else if (a == "--s3-corrupt-rate") g_s3_corrupt_rate = atof(next());
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
@@ -1190,7 +1167,7 @@ int main(int argc, char** argv) {
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
                       "[--default-size N] [--files-root DIR] [--sink checksum|discard|sample|verify] "
-                      "[--sample-stride N] [--sample-len N] [--pipe-kb N] [--s3-corrupt-rate P] "
+                      "[--sample-stride N] [--sample-len N] [--s3-corrupt-rate P] "
                       "[--tls-cert PEM --tls-key PEM] [--s3-fail-rate P]\n");
       return 2;
     }
@@ -1215,7 +1192,6 @@ int main(int argc, char** argv) {
     uint64_t v = rng();
     memcpy(g_pool.data() + i, &v, 8);
   }
-  g_devnull = ::open("/dev/null", O_WRONLY | O_CLOEXEC);
   g_pool_fd = memfd_create("blobd-pool", MFD_CLOEXEC);
   if (g_pool_fd >= 0) {
     size_t off = 0;

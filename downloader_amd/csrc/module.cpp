@@ -198,6 +198,8 @@ PYBIND11_MODULE(_native, m) {
     return d;
   }, "splice pipes: created, created below the asked capacity (the user's pipe page budget, "
      "fs.pipe-user-pages-soft, is spent), leased / idle and their capacity");
+  m.def("set_pipes_refused", &set_pipes_refused,
+        "tests: refuse every splice pipe as if the user's pipe budget were spent");
   m.def("set_pipe_sizes", &set_pipe_sizes, py::arg("main"), py::arg("tee") = 0,
         "capacity asked for new splice pipes and tee() duplicate pipes (0 = keep)");
   m.def("relay_pool_stats", []() {

@@ -122,6 +122,8 @@ struct PipeStats {
 PipeStats pipe_stats();
 // Capacity asked for new pipes: the splice pipe, and the tee() duplicate pipe (0 = keep).
 void set_pipe_sizes(size_t main, size_t tee);
+// Tests: refuse every pipe, as when the budget is spent (transfers fall back to copying).
+void set_pipes_refused(bool on);
 
 struct RelayPoolStats {
   size_t idle_buffers, idle_bytes, in_use, max_idle;

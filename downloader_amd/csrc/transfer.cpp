@@ -56,6 +56,7 @@ std::string errstr(const char* what) { return std::string(what) + ": " + strerro
 // Now only running transfers hold pipes (plus a few idle ones for reuse).
 std::atomic<size_t> g_pipe_main{size_t(1) << 20}, g_pipe_tee{size_t(256) << 10};
 std::atomic<uint64_t> g_pipes_created{0}, g_pipes_short{0};
+std::atomic<bool> g_pipes_refused{false};   // tests: behave as if the budget were spent
 
 struct Pipe {
   int r = -1, w = -1;
@@ -64,11 +65,14 @@ struct Pipe {
 
 class PipePool {
  public:
+  // A pipe of `want` bytes, or the largest power-of-two step down to 64 KiB the budget still
+  // allows; IoError when not even that (the caller copies through user space instead: a
+  // two-page pipe would cost a pair of syscalls per 8 KiB).
   Pipe acquire(size_t want) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      for (size_t i = idle_.size(); i-- > 0;)
-        if (idle_[i].cap >= want || idle_[i].cap == short_cap_) {
+      for (size_t i = idle_.size(); i-- > 0 && !g_pipes_refused.load();)
+        if (idle_[i].cap >= want || short_seen_) {
           Pipe p = idle_[i];
           idle_.erase(idle_.begin() + (ptrdiff_t)i);
           ++in_use_;
@@ -76,17 +80,24 @@ class PipePool {
           return p;
         }
     }
+    if (g_pipes_refused.load()) throw IoError("pipe page budget exhausted (test)");
     int fds[2];
     if (pipe2(fds, O_CLOEXEC) != 0) throw IoError(errstr("pipe2"));
     Pipe p{fds[0], fds[1], 0};
-    fcntl(p.w, F_SETPIPE_SZ, (int)want);
+    for (size_t sz = want; sz >= kMinPipe; sz >>= 1)
+      if (fcntl(p.w, F_SETPIPE_SZ, (int)sz) >= 0) break;
     int got = fcntl(p.w, F_GETPIPE_SZ);
     p.cap = got > 0 ? (size_t)got : 4096;
     g_pipes_created++;
     std::lock_guard<std::mutex> g(mu_);
     if (p.cap < want) {
       g_pipes_short++;
-      short_cap_ = p.cap;      // the budget is spent: take what an idle pipe has from now on
+      short_seen_ = true;      // the budget is spent: take what an idle pipe has from now on
+    }
+    if (p.cap < kMinPipe) {
+      ::close(p.r);
+      ::close(p.w);
+      throw IoError("pipe page budget exhausted (fs.pipe-user-pages-soft)");
     }
     ++in_use_;
     in_use_bytes_ += p.cap;
@@ -116,9 +127,11 @@ class PipePool {
 
  private:
   static constexpr size_t kMaxIdle = 8;
+  static constexpr size_t kMinPipe = size_t(64) << 10;
   std::mutex mu_;
   std::vector<Pipe> idle_;
-  size_t in_use_ = 0, in_use_bytes_ = 0, short_cap_ = 0;
+  size_t in_use_ = 0, in_use_bytes_ = 0;
+  bool short_seen_ = false;
 };
 
 PipePool& pipe_pool() {
@@ -738,15 +751,22 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
   if (ssl_ || dst.ssl_ || (crc && !relay_tee_on())) return relay_copy(dst, n, moved, prog, crc);
   if (crc) {
     thread_local std::vector<uint8_t> cbuf(256 * 1024);   // L2-resident CRC staging
-    return relay_tee(
+    int64_t m = relay_tee(
         dst, n, moved, prog,
         [&](size_t& len) {
           len = std::min(len, cbuf.size());
           return cbuf.data();
         },
         [&](const uint8_t* p, size_t k) { *crc = stager::crc32c(p, k, *crc); });
+    return m >= 0 ? m : relay_copy(dst, n, moved, prog, crc);
   }
-  PipeLease pl(g_pipe_main.load());
+  std::unique_ptr<PipeLease> lease;
+  try {
+    lease.reset(new PipeLease(g_pipe_main.load()));
+  } catch (const IoError&) {
+    return relay_copy(dst, n, moved, prog, nullptr);   // no pipe to be had: copy instead
+  }
+  PipeLease& pl = *lease;
   const int pr = pl.p.r, pw = pl.p.w;
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
@@ -787,13 +807,24 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
   return moved;
 }
 
-// The bytes sent and the bytes the caller sees are the same pipe pages: splice moves page
+// -1 (nothing moved) when no pipes can be had. The bytes sent and the bytes the caller sees
+// are the same pipe pages: splice moves page
 // references socket -> pipe -> socket, tee() duplicates the references into a second pipe and
 // only that duplicate is copied out (one user-space copy, where recv + send made two and
 // allocated fresh socket-buffer pages for the send).
 template <class Room, class Got>
 int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
                             Room&& room, Got&& got) {
+  std::unique_ptr<PipeLease> main_l, dup_l;
+  try {
+    main_l.reset(new PipeLease(g_pipe_main.load()));
+    dup_l.reset(new PipeLease(g_pipe_tee.load()));
+  } catch (const IoError&) {
+    if (main_l) main_l->clean = true;
+    return -1;                       // no pipes to be had: the caller copies (recv + send)
+  }
+  PipeLease& main = *main_l;
+  PipeLease& dup = *dup_l;
   auto fail = [&](const char* what) {
     reusable_ = false;
     dst.reusable_ = false;
@@ -815,8 +846,10 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
     moved += (int64_t)len;
     if (prog) prog->bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
   }
-  if (moved == n) return moved;
-  PipeLease main(g_pipe_main.load()), dup(g_pipe_tee.load());
+  if (moved == n) {
+    main.clean = dup.clean = true;
+    return moved;
+  }
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
@@ -953,19 +986,18 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
       k -= t;
     }
   };
-  if (!ssl_ && !dst.ssl_ && relay_tee_on()) {
-    relay_tee(
-        dst, n, 0, prog,
-        [&](size_t& len) {
-          len = std::min(len, buf.size());
-          return buf.data();
-        },
-        [&](const uint8_t* p, size_t k) {
-          if (crc) *crc = stager::crc32c(p, k, *crc);
-          consume(p, (int64_t)k);
-        });
+  if (!ssl_ && !dst.ssl_ && relay_tee_on() &&
+      relay_tee(
+          dst, n, 0, prog,
+          [&](size_t& len) {
+            len = std::min(len, buf.size());
+            return buf.data();
+          },
+          [&](const uint8_t* p, size_t k) {
+            if (crc) *crc = stager::crc32c(p, k, *crc);
+            consume(p, (int64_t)k);
+          }) >= 0)
     return pos;
-  }
   while (pos < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
@@ -1322,6 +1354,7 @@ std::string gpu_part_wait(uint64_t ticket) {
 
 size_t relay_pool_trim() { return part_pool().trim(); }
 PipeStats pipe_stats() { return pipe_pool().stats(); }
+void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
 void set_pipe_sizes(size_t main, size_t tee) {
   if (main) g_pipe_main.store(main);
   if (tee) g_pipe_tee.store(tee);
@@ -1334,10 +1367,11 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
                                        std::string* digests, std::string* head,
                                        std::string* tail, uint32_t* crc,
                                        uint64_t* gpu_ticket) {
-  // The whole part lands in a pooled buffer on its way to `dst` (plain sockets: a tee()d copy
-  // of the spliced pages; TLS: recv into it, send from it), then its pieces are hashed 16 at a time in
-  // the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the per-core rate of a single SHA-NI
-  // chain, which bounds the chunked path once many parts are in flight.
+  // The whole part lands in a pooled buffer on its way to `dst` (plain sockets: a tee()d
+  // copy of the spliced pages; TLS or no pipes: recv into it, send from it), then its pieces
+  // are hashed 16 at a time in the lanes of the AVX-512 multi-buffer SHA-1 - 3-5x the
+  // per-core rate of a single SHA-NI chain, which bounds the chunked path once many parts
+  // are in flight.
   PartLease lease((size_t)n);
   uint8_t* b = lease.b->data;
   int64_t pos = 0;

@@ -34,6 +34,7 @@ from ..s3.client import S3Client, S3Error
 from ..stages import build_stages
 from ..stages.base import EventEmitter, Job, Services, Stage
 from ..stages.jobdir import get_reaper
+from ..utils import limits
 from ..utils.config import Config
 from ..utils.log import Logger, get_logger, redact_text
 from ..utils.metrics import Metrics
@@ -116,6 +117,8 @@ class Worker:
             self.stages = await build_stages(self.cfg.stages, self.cfg, self.services)
         get_reaper(self.services).sweep()   # trash left by a crashed predecessor
         d = self.cfg.download
+        # the uid's pipe page budget is shared: size splice pipes to this worker's share
+        self.pipe_bytes = limits.apply_pipe_size(d.pipe_kb, d.pipe_sharers)
         if d.gpu_prewarm and d.verify_backend != "cpu":
             from ..ops import hashing
             # auto never picks the GPU on a host with the multi-buffer SHA-1: no HIP init

@@ -147,6 +147,13 @@ class DownloadConfig(BaseModel):
     # reuse them without re-faulting ~1 GiB of huge pages (MI355X box, 4 GB torrent: 26.7 -
     # 27.8 GB/s warm vs 19.2 - 20.0 GB/s when every job faults its buffers afresh)
     relay_pool_idle_trim_s: float = 60.0
+    # Splice pipe capacity per transfer in KiB (relays, HTTP bodies to disk). 0: derived from
+    # the user's pipe page budget (fs.pipe-user-pages-soft, 64 MiB by default for non-root
+    # users, shared by every process of that uid - containers of one uid on a host included)
+    # split over `pipe_sharers` processes of ~16 transfers each; 1 MiB when unbounded (root).
+    # Past the budget pipes shrink to two pages, so transfers copy through user space instead.
+    pipe_kb: int = 0
+    pipe_sharers: int = 4
     bucket_concurrency: int = 4                 # ref: sequential fGetObject (lib/download.js:218)
     bucket_secure: bool = True                  # bucket:// is always TLS in the reference
     # bucket:// sources: select media from the object listing and relay only the selected

@@ -53,3 +53,52 @@ def fd_headroom() -> int:
     if soft == resource.RLIM_INFINITY:
         return 1 << 30
     return max(0, soft - open_fds())
+
+
+PIPE_MAX = 1 << 20          # fs.pipe-max-size default: the most an unprivileged pipe gets
+PIPE_MIN = 64 << 10         # below this a splice transfer copies through user space instead
+PIPES_PER_PROC = 16         # transfers in flight per worker process (relays, range GETs)
+
+
+def pipe_budget_bytes() -> int:
+    """Pipe capacity this uid may hold before new pipes shrink to two pages
+    (``fs.pipe-user-pages-soft`` x page size); 0 = unbounded (root, or no soft limit)."""
+    if hasattr(os, "geteuid") and os.geteuid() == 0:
+        return 0
+    try:
+        with open("/proc/sys/fs/pipe-user-pages-soft") as f:
+            pages = int(f.read().strip() or 0)
+    except (OSError, ValueError):
+        return 0
+    return pages * os.sysconf("SC_PAGE_SIZE") if pages > 0 else 0
+
+
+def pipe_size(pipe_kb: int = 0, sharers: int = 4, per_proc: int = PIPES_PER_PROC,
+              budget: int = -1) -> int:
+    """Splice pipe capacity for this process: ``pipe_kb`` when set, else a power of two in
+    [64 KiB, 1 MiB] such that ``sharers`` processes x ``per_proc`` pipes fit in three
+    quarters of the uid's pipe budget (the rest is headroom for other pipes of the uid)."""
+    if pipe_kb > 0:
+        return pipe_kb << 10
+    if budget < 0:
+        budget = pipe_budget_bytes()
+    if budget == 0:
+        return PIPE_MAX
+    share = budget * 3 // 4 // max(1, sharers) // max(1, per_proc)
+    size = PIPE_MIN
+    while size * 2 <= min(share, PIPE_MAX):
+        size *= 2
+    return size
+
+
+def apply_pipe_size(pipe_kb: int = 0, sharers: int = 4) -> int:
+    """Size the native transport's splice pipes (main; tee duplicate a quarter of it);
+    returns the main size, 0 without the native module."""
+    try:
+        from ..ops import native
+        n = native()
+    except Exception:
+        return 0
+    main = pipe_size(pipe_kb, sharers)
+    n.set_pipe_sizes(main, max(PIPE_MIN, main // 4))
+    return main

@@ -481,3 +481,60 @@ def test_cancelled_native_download_never_writes_after_cancel(run, tmp_path):
         srv.close()
         await srv.wait_closed()
     run(go(), timeout=60)
+
+
+def test_pipe_size_follows_the_uid_budget():
+    """Splice pipes are sized so every worker of the uid fits in the pipe page budget
+    (64 MiB default for non-root): 1 MiB when unbounded, power-of-two steps down to 64 KiB."""
+    from downloader_amd.utils import limits
+    mib = 1 << 20
+    assert limits.pipe_size(budget=0) == mib                       # root / no soft limit
+    assert limits.pipe_size(pipe_kb=300) == 300 << 10              # explicit
+    b = 64 * mib
+    assert limits.pipe_size(sharers=2, per_proc=10, budget=b) == mib
+    assert limits.pipe_size(sharers=4, per_proc=10, budget=b) == mib
+    assert limits.pipe_size(sharers=8, per_proc=10, budget=b) == 512 << 10
+    assert limits.pipe_size(sharers=16, per_proc=10, budget=b) == 256 << 10
+    assert limits.pipe_size(sharers=1000, per_proc=16, budget=b) == 64 << 10   # floor
+    for sharers in (1, 2, 4, 8, 16, 32):
+        sz = limits.pipe_size(sharers=sharers, per_proc=10, budget=b)
+        assert sz & (sz - 1) == 0 and (sz == 64 << 10 or sharers * 10 * sz <= b * 3 // 4)
+
+
+def test_transfers_copy_when_no_pipe_can_be_had(run, origin_cls):
+    """With the pipe budget spent, relays (plain, CRC'd, piece-hashed) and bodies to disk
+    copy through user space instead of splicing through two-page pipes - same bytes."""
+    import hashlib
+    import os
+
+    from downloader_amd.ops import native
+    from downloader_amd.s3.client import S3Client
+    from downloader_amd.s3.fake_server import FakeS3
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(9_000_000)
+        origin.blobs["/x.bin"] = blob
+        for policy in ("auto", "always"):
+            c = S3Client(ep, "minioadmin", "minioadmin", checksum=policy)
+            await c.ensure_bucket("b")
+            await c.relay_object("b", f"plain-{policy}", origin.url("/x.bin"), len(blob))
+            assert s3.get("b", f"plain-{policy}") == blob
+            _, h = await c.relay_hashed("b", f"h-{policy}", origin.url("/x.bin"), 0, len(blob),
+                                        True, (1000, 8 << 20, 1 << 20))
+            assert h["digests"] == b"".join(hashlib.sha1(blob[1000 + i:1000 + i + (1 << 20)])
+                                            .digest() for i in range(0, 8 << 20, 1 << 20))
+            assert h["head"] == blob[:1000] and h["tail"] == blob[1000 + (8 << 20):]
+            await c.close()
+        await origin.stop(); await s3.stop()
+
+    n = native()
+    before = n.pipe_stats()["created"]
+    n.set_pipes_refused(True)
+    try:
+        run(go())
+    finally:
+        n.set_pipes_refused(False)
+    assert n.pipe_stats()["created"] == before and n.pipe_stats()["in_use"] == 0
