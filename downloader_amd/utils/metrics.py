@@ -26,7 +26,7 @@ class _RuntimeCollector:
         return []
 
     def collect(self):
-        from prometheus_client.core import GaugeMetricFamily
+        from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
         nt = getattr(self.transports, "native", None)
         if nt is not None:
             yield GaugeMetricFamily(f"{self.ns}_http_idle_connections",
@@ -41,6 +41,14 @@ class _RuntimeCollector:
                                 "relay part buffers in use", value=st["in_use"])
         yield GaugeMetricFamily(f"{self.ns}_relay_pool_idle_bytes",
                                 "bytes held by idle relay part buffers", value=st["idle_bytes"])
+        ps = native().pipe_stats()
+        yield GaugeMetricFamily(f"{self.ns}_splice_pipes_in_use",
+                                "splice pipes leased by running transfers", value=ps["in_use"])
+        # a growing count means the uid's pipe page budget (fs.pipe-user-pages-soft) is spent:
+        # pipes come out smaller than asked, or transfers copy through user space instead
+        yield CounterMetricFamily(f"{self.ns}_splice_pipes_short",
+                                  "splice pipes created below the asked capacity",
+                                  value=ps["short"])
 
 
 class Metrics:

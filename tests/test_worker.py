@@ -204,6 +204,7 @@ def test_health_endpoint_semantics(run, make_cfg, origin_cls):
                 assert "downloader_jobs_total" in txt
                 assert "downloader_http_idle_connections" in txt       # native runtime gauges
                 assert "downloader_relay_pool_idle_bytes" in txt
+                assert "downloader_splice_pipes_short_total" in txt    # pipe budget signal
         w.active.clear()
         await hs.stop()
         await w.stop(); await s3.stop(); await origin.stop()
