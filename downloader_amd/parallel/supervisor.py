@@ -70,6 +70,9 @@ class Supervisor:
     def _spawn(self, s: Slot) -> None:
         env = dict(self.env)
         env["STAGER_WORKER_INDEX"] = str(s.index)
+        # the workers share the uid's pipe page budget: size their splice pipes for all n
+        # (an explicit setting in the environment wins)
+        env.setdefault("STAGER_DOWNLOAD__PIPE_SHARERS", str(max(4, self.n)))
         if self.base_port:
             env["PORT"] = str(self.base_port + s.index)   # distinct /health ports
         cpus = self.cpus[s.index]
