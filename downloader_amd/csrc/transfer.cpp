@@ -117,6 +117,19 @@ class PipePool {
     ::close(p.r);
     ::close(p.w);
   }
+  // Close the idle pipes (their capacity was asked for under other settings).
+  void drop_idle() {
+    std::vector<Pipe> drop;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      drop.swap(idle_);
+      short_seen_ = false;
+    }
+    for (auto& p : drop) {
+      ::close(p.r);
+      ::close(p.w);
+    }
+  }
   PipeStats stats() {
     std::lock_guard<std::mutex> g(mu_);
     size_t idle_bytes = 0;
@@ -1358,6 +1371,7 @@ void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
 void set_pipe_sizes(size_t main, size_t tee) {
   if (main) g_pipe_main.store(main);
   if (tee) g_pipe_tee.store(tee);
+  pipe_pool().drop_idle();
 }
 void relay_pool_set_max_idle(size_t n) { part_pool().set_max_idle(n); }
 RelayPoolStats relay_pool_stats() { return part_pool().stats(); }

@@ -406,3 +406,40 @@ def test_blobd_sink_detects_wrong_torn_and_reordered_objects(sink):
         mp([(1, good[h:2 * h]), (2, good[:h] + good[2 * h:])])              # parts swapped
         st = b.stats()
         assert st["verify_objects"] == 5 and st["verify_mismatches"] == 3, st
+
+
+@pytest.mark.parametrize("main_kb,tee_kb", [(64, 64), (1024, 64), (64, 1024)])
+def test_teed_relays_with_small_and_uneven_pipes(run, origin_cls, main_kb, tee_kb):
+    """The CRC'd and piece-hashed relays splice through a pipe and read a tee()d duplicate:
+    with small or uneven pipes a chunk is duplicated, read and sent in several rounds - the
+    CRC the sink checks and the piece digests must still cover exactly the bytes sent."""
+    from downloader_amd.ops import native
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(5_000_003)
+        origin.blobs["/u.bin"] = blob
+        c = S3Client(ep, *CREDS, checksum="always", part_size=5 << 20,
+                     multipart_threshold=64 << 20)
+        await c.ensure_bucket("b")
+        s3.corrupt_next = 1                       # the first PUT is refused: CRC must differ
+        await c.relay_object("b", "plain", origin.url("/u.bin"), len(blob))
+        assert s3.get("b", "plain") == blob and s3.bad_digests == 1
+        plen = 1 << 18
+        full = ((len(blob) - 777) // plen) * plen
+        _, h = await c.relay_hashed("b", "h", origin.url("/u.bin"), 0, len(blob), True,
+                                    (777, full, plen))
+        assert h["digests"] == b"".join(hashlib.sha1(blob[777 + i:777 + i + plen]).digest()
+                                        for i in range(0, full, plen))
+        assert h["head"] == blob[:777] and h["tail"] == blob[777 + full:]
+        assert s3.get("b", "h") == blob
+        await c.close(); await origin.stop(); await s3.stop()
+
+    n = native()
+    n.set_pipe_sizes(main_kb << 10, tee_kb << 10)
+    try:
+        run(go())
+    finally:
+        n.set_pipe_sizes(1 << 20, 256 << 10)
