@@ -100,5 +100,6 @@ def apply_pipe_size(pipe_kb: int = 0, sharers: int = 4) -> int:
     except Exception:
         return 0
     main = pipe_size(pipe_kb, sharers)
-    n.set_pipe_sizes(main, max(PIPE_MIN, main // 4))
+    tee_kb = int(os.environ.get("STAGER_TEE_PIPE_KB", "0") or 0)     # A/B knob
+    n.set_pipe_sizes(main, tee_kb << 10 if tee_kb > 0 else max(PIPE_MIN, main // 4))
     return main
