@@ -54,7 +54,7 @@ std::string errstr(const char* what) { return std::string(what) + ": " + strerro
 // and new pipes get two pages, and 1 MiB pipes kept on every pooled connection - idle ones
 // included, in the workers and in the S3 peer alike - ran a busy 16-relay worker into it.
 // Now only running transfers hold pipes (plus a few idle ones for reuse).
-std::atomic<size_t> g_pipe_main{size_t(1) << 20}, g_pipe_tee{size_t(256) << 10};
+std::atomic<size_t> g_pipe_main{size_t(1) << 20}, g_pipe_tee{size_t(1) << 20};
 std::atomic<uint64_t> g_pipes_created{0}, g_pipes_short{0};
 std::atomic<bool> g_pipes_refused{false};   // tests: behave as if the budget were spent
 
@@ -71,14 +71,22 @@ class PipePool {
   Pipe acquire(size_t want) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      for (size_t i = idle_.size(); i-- > 0 && !g_pipes_refused.load();)
-        if (idle_[i].cap >= want || short_seen_) {
-          Pipe p = idle_[i];
-          idle_.erase(idle_.begin() + (ptrdiff_t)i);
-          ++in_use_;
-          in_use_bytes_ += p.cap;
-          return p;
+      // an idle pipe of exactly this size, else any large enough (or any, once short)
+      size_t pick = idle_.size();
+      for (size_t i = idle_.size(); i-- > 0 && !g_pipes_refused.load();) {
+        if (idle_[i].cap == want) {
+          pick = i;
+          break;
         }
+        if (pick == idle_.size() && (idle_[i].cap >= want || short_seen_)) pick = i;
+      }
+      if (pick < idle_.size()) {
+        Pipe p = idle_[pick];
+        idle_.erase(idle_.begin() + (ptrdiff_t)pick);
+        ++in_use_;
+        in_use_bytes_ += p.cap;
+        return p;
+      }
     }
     if (g_pipes_refused.load()) throw IoError("pipe page budget exhausted (test)");
     int fds[2];
@@ -139,7 +147,7 @@ class PipePool {
   }
 
  private:
-  static constexpr size_t kMaxIdle = 8;
+  static constexpr size_t kMaxIdle = 32;   // a tee()d relay holds two: 16 relays in flight
   static constexpr size_t kMinPipe = size_t(64) << 10;
   std::mutex mu_;
   std::vector<Pipe> idle_;

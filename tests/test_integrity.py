@@ -134,7 +134,7 @@ def test_plain_relay_checksum_policy(run, origin_cls, policy, expect_crc):
         assert s3.get("b", "one") == blob
         from downloader_amd.ops import native
         ps = native().pipe_stats()      # pipes are leased per transfer, all returned
-        assert ps["in_use"] == 0 and ps["idle"] <= 8
+        assert ps["in_use"] == 0 and ps["idle"] <= 32
         await c.close()
         await origin.stop()
         await s3.stop()
