@@ -828,11 +828,11 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
   return moved;
 }
 
-// -1 (nothing moved) when no pipes can be had. The bytes sent and the bytes the caller sees
-// are the same pipe pages: splice moves page
+// The bytes sent and the bytes the caller sees are the same pipe pages: splice moves page
 // references socket -> pipe -> socket, tee() duplicates the references into a second pipe and
 // only that duplicate is copied out (one user-space copy, where recv + send made two and
-// allocated fresh socket-buffer pages for the send).
+// allocated fresh socket-buffer pages for the send). -1 (nothing moved) when no pipes can be
+// had: the caller copies instead.
 template <class Room, class Got>
 int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
                             Room&& room, Got&& got) {
