@@ -916,7 +916,9 @@ class PartHasher {
     wcv_.wait(lk, [&] { return !j->err.empty() || (phase == GPU_PART_COPIED ? j->copied : j->done); });
     if (!j->err.empty()) {
       std::string e = j->err;
-      if (phase == GPU_PART_DONE || j->done) jobs_.erase(it);
+      // nobody waits again for a failed copy (the relay hashes on the host), and once broken
+      // the dispatcher thread has exited: the job can go
+      if (phase == GPU_PART_DONE || j->done || broken_) jobs_.erase(it);
       return fail(err, errlen, e.c_str());
     }
     if (phase == GPU_PART_DONE) {

@@ -168,8 +168,10 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("ticket"), "Digests (20 B per piece) of a part the relay handed to the GPU");
   py::class_<CpuPartHasher>(m, "CpuPartHasher")
-      .def(py::init<double>(), py::arg("delay_s") = 0.005,
-           "gpu_part_api.h on a host thread (tests of the asynchronous relay-hashing path)")
+      .def(py::init<double, int, int>(), py::arg("delay_s") = 0.005,
+           py::arg("fail_copy_every") = 0, py::arg("fail_done_every") = 0,
+           "gpu_part_api.h on a host thread (tests of the asynchronous relay-hashing path); "
+           "fail_*_every: every Nth job's copy / hash fails")
       .def("api", [](CpuPartHasher& h) {
         return py::capsule((void*)h.api(), "downloader_amd.gpu_part_api");
       })

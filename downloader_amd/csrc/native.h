@@ -142,7 +142,9 @@ std::string gpu_part_wait(uint64_t ticket);
 // `delay_s`): the asynchronous relay-hashing path without a HIP device (tests).
 class CpuPartHasher {
  public:
-  explicit CpuPartHasher(double delay_s);
+  // fail_copy_every / fail_done_every (0 = never): every Nth job's COPIED / DONE wait
+  // fails, as a device that dies before / after the DMA out of the part buffer would.
+  explicit CpuPartHasher(double delay_s, int fail_copy_every = 0, int fail_done_every = 0);
   ~CpuPartHasher();
   const void* api() const;
   uint64_t registered() const;

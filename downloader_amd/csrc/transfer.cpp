@@ -1235,6 +1235,8 @@ struct CpuJob {
   int64_t len, piece_len;
   std::string copy, digests;
   bool copied = false, done = false;
+  bool fail_copy = false, fail_done = false;
+  bool abandoned = false;   // its copy "failed": the relay hashed on the host, nobody waits
 };
 }  // namespace
 
@@ -1246,6 +1248,7 @@ struct CpuPartHasher::Impl {
   uint64_t seq = 0;
   bool stop = false;
   double delay_s;
+  int fail_copy_every = 0, fail_done_every = 0;
   std::thread th;
   GpuPartHashApi api{};
   uint64_t registered = 0;
@@ -1272,14 +1275,18 @@ struct CpuPartHasher::Impl {
       lk.lock();
       j->digests.swap(d);
       j->done = true;
+      if (j->abandoned) jobs.erase(t);
       wcv.notify_all();
     }
   }
 };
 
-CpuPartHasher::CpuPartHasher(double delay_s) : impl_(new Impl) {
+CpuPartHasher::CpuPartHasher(double delay_s, int fail_copy_every, int fail_done_every)
+    : impl_(new Impl) {
   Impl* m = impl_.get();
   m->delay_s = delay_s;
+  m->fail_copy_every = fail_copy_every;
+  m->fail_done_every = fail_done_every;
   m->api.abi = GPU_PART_API_ABI;
   m->api.ctx = m;
   m->api.reg = [](void* c, void*, size_t) {
@@ -1298,6 +1305,8 @@ CpuPartHasher::CpuPartHasher(double delay_s) : impl_(new Impl) {
     j.host = d;
     j.len = len;
     j.piece_len = pl;
+    j.fail_copy = i->fail_copy_every > 0 && t % (uint64_t)i->fail_copy_every == 0;
+    j.fail_done = i->fail_done_every > 0 && t % (uint64_t)i->fail_done_every == 0;
     i->queue.push_back(t);
     i->cv.notify_all();
     return t;
@@ -1313,6 +1322,14 @@ CpuPartHasher::CpuPartHasher(double delay_s) : impl_(new Impl) {
     }
     CpuJob* j = &it->second;
     i->wcv.wait(lk, [&] { return phase == GPU_PART_COPIED ? j->copied : j->done; });
+    if ((phase == GPU_PART_COPIED && j->fail_copy) || (phase == GPU_PART_DONE && j->fail_done)) {
+      snprintf(err, el, "injected device failure (%s)", phase == GPU_PART_COPIED ? "copy" : "hash");
+      if (phase == GPU_PART_DONE)
+        i->jobs.erase(it);        // the worker thread is done with it
+      else
+        j->abandoned = true;      // erased by the worker thread once it is done with it
+      return -1;
+    }
     if (phase == GPU_PART_DONE) {
       if (ol < j->digests.size()) {
         snprintf(err, el, "digest buffer too small");

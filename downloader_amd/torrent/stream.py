@@ -344,7 +344,14 @@ class StreamStager:
         from ..ops import hashing
         etag, h = res
         try:
-            digests = await hashing.gpu_part_digests(h["gpu_ticket"])
+            try:
+                digests = await hashing.gpu_part_digests(h["gpu_ticket"])
+            except RuntimeError as e:
+                # the device failed after the part's buffer went back to the pool: the
+                # bytes are gone, so the part is fetched (and relayed) again - its next
+                # relay hashes on the host if the hasher now refuses work
+                self.stats["gpu_failures"] = self.stats.get("gpu_failures", 0) + 1
+                raise TransportError(f"part {u.num}: {e}") from e
             self.stats["gpu_parts"] = self.stats.get("gpu_parts", 0) + 1
             requeue = await self._after_fetch(u, self._accept(u, etag, h, digests))
         except BaseException as e:

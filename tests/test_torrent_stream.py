@@ -508,3 +508,43 @@ def test_refused_put_releases_its_queued_part(run, origin_cls):
         run(go())
     finally:
         hashing.use_part_hasher(None)
+
+
+def test_stream_survives_part_hasher_failures(run, tmp_path, make_cfg, origin_cls):
+    """A device that fails before the DMA out of a part buffer (the relay hashes that part on
+    the host) or after it (the bytes are gone: the part is fetched again) still stages the
+    exact bytes, and every buffer lease comes back."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Movie"
+        src.mkdir(parents=True)
+        data = os.urandom(19 * (1 << 20) + 4321)
+        (src / "m.mkv").write_bytes(data)
+        origin.blobs["/ws/Movie/m.mkv"] = data
+        origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
+                                                    url_list=[origin.url("/ws/")])
+        w = _worker(make_cfg, ep, download={"stream_verify_backend": "gpu",
+                                            "stream_gpu_min_pieces": 4, "stream_gpu_tail": 0})
+        await w.start(health=False)
+        before = native().gpu_part_stats()
+        await w.submit(api.make_download("hf", "http", origin.url("/t/m.torrent")))
+        await _wait(w, timeout=60)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        t = r.stats["torrent"]
+        assert s3.get("triton-staging", keys.object_key("hf", "m.mkv")) == data
+        after = native().gpu_part_stats()
+        assert after["host_fallbacks"] > before["host_fallbacks"]      # copy failures
+        assert t.get("gpu_failures", 0) >= 1                           # hash failures
+        assert native().relay_pool_stats()["in_use"] == 0
+        await w.stop(); await s3.stop(); await origin.stop()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.005, fail_copy_every=3, fail_done_every=4), 4)
+    try:
+        run(go())
+    finally:
+        hashing.use_part_hasher(None)
