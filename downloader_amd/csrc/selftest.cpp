@@ -528,6 +528,50 @@ int main() {
     CHECK(gs.submitted >= 4 && cph.registered() >= 1);
     set_gpu_part_hasher(nullptr, 0);
   }
+  // ---- the same with a failing device: every 2nd copy fails (host fallback, the job is
+  // abandoned to the hasher thread), every 3rd hash fails (gpu_part_wait throws)
+  {
+    CpuPartHasher bad(0.001, 2, 3);
+    set_gpu_part_hasher(bad.api(), 8);
+    const int64_t plen = 1 << 16, skip = 0, n = (int64_t)body.size();
+    const int64_t full = (n / plen) * plen;
+    std::string want = hash_pieces("sha1", body.data(), (size_t)full, (size_t)plen, 1);
+    std::atomic<int> good{0}, failed{0};
+    std::vector<std::thread> ths;
+    for (int t = 0; t < 6; ++t) {
+      ths.emplace_back([&] {
+        Server origin([&](int fd) {
+          read_head(fd);
+          send_str(fd, "HTTP/1.1 200 OK\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+          send_str(fd, std::string((const char*)body.data(), body.size()));
+        });
+        Server sink([&](int fd) {
+          read_head(fd);
+          drain_body(fd, n);
+          send_str(fd, "HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n");
+        });
+        HttpConn src("127.0.0.1", origin.port, 5, 5), dst("127.0.0.1", sink.port, 5, 5);
+        src.send_request("GET /f HTTP/1.1\r\nHost: x\r\n\r\n", nullptr, 0);
+        ResponseHead g = src.read_head();
+        dst.send_raw("PUT /f HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(n) + "\r\n\r\n");
+        std::string digests, head, tail;
+        uint64_t ticket = 0;
+        src.relay_body_hashed(dst, g.content_length, skip, full, plen, nullptr, &digests, &head,
+                              &tail, nullptr, &ticket);
+        ResponseHead p = dst.read_head();
+        dst.read_body(p, 16);
+        try {
+          if (ticket) digests = gpu_part_wait(ticket);
+          if (digests == want) good.fetch_add(1);
+        } catch (const std::exception&) {
+          failed.fetch_add(1);
+        }
+      });
+    }
+    for (auto& th : ths) th.join();
+    CHECK(good.load() + failed.load() == 6 && good.load() >= 3 && failed.load() >= 1);
+    set_gpu_part_hasher(nullptr, 0);
+  }
   {
     RelayPoolStats st = relay_pool_stats();
     CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);
