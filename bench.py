@@ -24,7 +24,9 @@ last timed job, show (a) at least as many bytes received as the workers claim to
 and (b) with ``--sink sample`` (default) / ``verify``, every timed object matched against the
 bytes the origin generated for it (sampled windows / every byte) with zero mismatches. A
 second, same-call run with the round-2 settings (single PUT up to 128 MiB) is reported as
-``single_put_MBps``.
+``single_put_MBps``, and a third with a CRC32C on every relayed PUT / part (``--checksum
+always``: aws-chunked trailer computed from a tee()d copy of the spliced pages, recomputed and
+checked by the sink) as ``crc_relay_MBps``.
 """
 from __future__ import annotations
 
@@ -80,6 +82,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-compare-single-put", dest="compare_single_put", action="store_false",
                    help="skip the same-call comparison run with round-2 settings (objects up to "
                         "128 MiB in one PUT)")
+    p.add_argument("--no-compare-crc", dest="compare_crc", action="store_false",
+                   help="skip the same-call comparison run with a CRC32C on every relayed PUT "
+                        "and part (--checksum always), checked by the S3 sink")
     p.add_argument("--pipe-kb", type=int, default=0,
                    help="splice pipe KiB per transfer (0: the uid's pipe budget / workers)")
     p.add_argument("--checksum", choices=["auto", "always", "off"], default="",
@@ -233,7 +238,8 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
 
 def _tag(args, mode: str) -> str:
     """Job-id tag of a measurement: each one stages fresh ids (no done-marker skips)."""
-    return mode + ("-1put" if getattr(args, "single_put", False) else "")
+    return (mode + ("-1put" if getattr(args, "single_put", False) else "")
+            + ("-crc" if getattr(args, "crc_run", False) else ""))
 
 
 async def _warmup(args, worker, url, wid: int, mode: str) -> None:
@@ -306,6 +312,7 @@ def _proc_main(conn, args, endpoint: str, mode: str, stage_root: str, wid: int, 
         await worker.stop()
         t = os.times()
         out["worker_cpu_s"] = t.user + t.system
+        out["worker_sys_s"] = t.system
         conn.send(("done", out))
     try:
         asyncio.run(go())
@@ -366,11 +373,13 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
             "loop_busy": max(o["loop_busy"] for o in outs),
             "pipes_created": sum(o["pipes_created"] for o in outs),
             "pipes_short": sum(o["pipes_short"] for o in outs),
-            "child_cpu_s": sum(o["worker_cpu_s"] for o in outs)}
+            "child_cpu_s": sum(o["worker_cpu_s"] for o in outs),
+            "child_sys_s": sum(o["worker_sys_s"] for o in outs)}
 
 
 SINK_KEYS = ("bytes_received", "verify_objects", "verify_bytes", "verify_mismatches",
-             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests")
+             "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests",
+             "checksummed_puts")
 
 
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 1,
@@ -384,6 +393,7 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
     peer_cpu0 = blob.cpu_seconds() if blob is not None else 0.0
     t = os.times()
     cpu0 = t.user + t.system
+    sys0 = t.system
     try:
         if nproc > 1:
             out = rank_procs(args, dist, endpoint, mode, stage_root, nproc, cpus or [], on_go)
@@ -394,6 +404,7 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
             shutil.rmtree(stage_root, ignore_errors=True)
     t = os.times()
     out["worker_cpu_s"] = t.user + t.system - cpu0 + out.pop("child_cpu_s", 0.0)
+    out["worker_sys_s"] = t.system - sys0 + out.pop("child_sys_s", 0.0)
     out["peer_cpu_s"] = (blob.cpu_seconds() - peer_cpu0) if blob is not None else 0.0
     dist.barrier()
     # The S3 peer's own counters, between "go" and the end of the timed jobs (every rank is
@@ -429,6 +440,8 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
             "bytes": total_bytes, "sink": sink,
             "parts_per_object": round(sink["multipart_parts"] / mp, 3) if mp else 1.0,
             "worker_cpu_s_per_GB": sum(r["worker_cpu_s"] for r in allr) / gb_all,
+            "worker_sys_share": sum(r["worker_sys_s"] for r in allr)
+            / max(1e-9, sum(r["worker_cpu_s"] for r in allr)),
             "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all,
             "loop_busy": max(r["loop_busy"] for r in allr),
             "pipes_created": sum(r["pipes_created"] for r in allr),
@@ -498,6 +511,11 @@ def main() -> int:
             args.single_put = True
             single = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
             args.single_put = False
+        crc = None
+        if args.compare_crc and args.mode == "tuned" and args.checksum != "always":
+            saved, args.checksum, args.crc_run = args.checksum, "always", True
+            crc = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
+            args.checksum, args.crc_run = saved, False
         ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
     finally:
         if blob is not None:
@@ -526,6 +544,7 @@ def main() -> int:
             "sink_verified_bytes": tuned["sink"]["verify_bytes"],
             "sink_mismatches": tuned["sink"]["mismatches_total"],
             "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
+            "worker_kernel_share": round(tuned["worker_sys_share"], 3),   # system / (user+system)
             "event_loop_busy": round(tuned["loop_busy"], 3),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
             # splice pipes created below their asked capacity (pipe page budget spent)
@@ -556,6 +575,11 @@ def main() -> int:
             line["single_put_MBps"] = round(single["mbps"], 2)
             line["single_put_p50_s"] = round(single["p50"], 4)
             line["single_put_parts_per_object"] = single["parts_per_object"]
+        if crc is not None:      # same call, a CRC32C on every relayed PUT / part
+            line["crc_relay_MBps"] = round(crc["mbps"], 2)
+            line["crc_relay_p50_s"] = round(crc["p50"], 4)
+            line["crc_relay_worker_cpu_s_per_GB"] = round(crc["worker_cpu_s_per_GB"], 4)
+            line["crc_relay_sink_checked_puts"] = crc["sink"]["checksummed_puts"]
         if ref is not None:
             line["reference_mode_MBps"] = round(ref["mbps"], 2)
             line["reference_mode_p50_s"] = round(ref["p50"], 4)

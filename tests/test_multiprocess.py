@@ -113,6 +113,10 @@ def test_bench_single_rank_defaults_are_valid(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["n_gpus"] == 1 and j["higher_is_better"] is True and j["scaling"] == "weak"
+    # same-call comparisons: one PUT per object, and a CRC32C on every relayed PUT / part that
+    # the sink recomputed (2 MB objects: 1 PUT + the done marker per job, 2 steps x 64 jobs)
+    assert j["single_put_MBps"] > 0 and j["crc_relay_MBps"] > 0
+    assert j["crc_relay_sink_checked_puts"] >= 2 * 64
 
 
 def test_supervisor_auto_pinning_quota_share():
