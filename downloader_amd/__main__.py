@@ -7,6 +7,7 @@
   python -m downloader_amd make-torrent PATH -o F [--webseed URL] [--tracker URL]
   python -m downloader_amd verify      TORRENT DIR [--backend gpu|cpu|auto]
   python -m downloader_amd config                     print the effective config
+  python -m downloader_amd doctor      [--sharers N]  host readiness report (JSON + warnings)
 
 Worker lifecycle mirrors index.js: logger + tracer, load config (named ``downloader``; the
 reference's ``'converter'`` is accepted as an alias), start the service, and on SIGINT/SIGTERM
@@ -143,6 +144,12 @@ def _config(args) -> int:
     return 0
 
 
+def _doctor(args) -> int:
+    from .utils.doctor import report
+    print(json.dumps(report(args.sharers), indent=2))
+    return 0
+
+
 def main(argv=None) -> int:
     p = argparse.ArgumentParser(prog="downloader_amd")
     sub = p.add_subparsers(dest="cmd", required=True)
@@ -187,9 +194,13 @@ def main(argv=None) -> int:
     c.add_argument("--show-secrets", action="store_true", help="do not mask credentials")
     c.add_argument("--reference", action="store_true",
                    help="print the markdown reference of every key (docs/CONFIG.md)")
+    d = sub.add_parser("doctor")
+    d.add_argument("--sharers", type=int, default=4,
+                   help="worker processes of this uid per host (they share the pipe budget)")
     args = p.parse_args(argv)
     return {"worker": _worker, "supervisor": _supervisor, "broker": _broker, "submit": _submit,
-            "make-torrent": _make_torrent, "verify": _verify, "config": _config}[args.cmd](args)
+            "make-torrent": _make_torrent, "verify": _verify, "config": _config,
+            "doctor": _doctor}[args.cmd](args)
 
 
 if __name__ == "__main__":

@@ -448,4 +448,8 @@ std::string crc32c_base64(uint32_t crc) {
   return std::string(b, 8);
 }
 
+const char* crc32c_impl() {
+  return crc32c_detail::have_vpclmul() ? "avx512-vpclmulqdq" : "sse4.2-3way";
+}
+
 }  // namespace stager

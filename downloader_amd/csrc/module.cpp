@@ -138,6 +138,8 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "stager host-native byte paths: hashing (OpenSSL EVP, threaded) and zero-copy HTTP";
 
   m.def("digest_size", &digest_size);
+  m.def("crc32c_impl", []() { return std::string(crc32c_impl()); },
+        "the CRC32C implementation this CPU runs (avx512-vpclmulqdq / sse4.2-3way)");
   m.def("sha1_mb_supported", &sha1_mb_supported,
         "True when the host runs the AVX-512 16-lane multi-buffer SHA-1 (csrc/sha1_mb.cpp)");
   m.def("effective_cpus", &effective_cpus,

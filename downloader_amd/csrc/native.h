@@ -46,6 +46,8 @@ uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
 // CRC32C of a file range (pread through an L2-sized buffer).
 uint32_t crc32c_fd(int fd, int64_t off, int64_t len);
 std::string crc32c_base64(uint32_t crc);
+// "avx512-vpclmulqdq" (folding, >= 1 KiB) or "sse4.2-3way": the CRC32C path this CPU runs.
+const char* crc32c_impl();
 std::string hash_pieces(const std::string& algo, const uint8_t* p, size_t n, size_t piece_len,
                         int threads);
 

@@ -192,3 +192,19 @@ def test_concurrent_builds_never_leave_a_broken_binary(tmp_path):
     r = subprocess.run([exe, "--bogus"], capture_output=True, text=True, timeout=30)
     assert r.returncode == 2 and "usage: blobd" in r.stderr
     assert not [f for f in os.listdir(os.path.dirname(exe)) if ".tmp." in f]
+
+
+def test_doctor_reports_host_readiness():
+    """``doctor``: native SIMD paths, CPUs, open-file limit, the uid's pipe budget and the
+    pipe size the worker would pick, THP, GPUs - as JSON with a warnings list."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-m", "downloader_amd", "doctor", "--sharers", "8"],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=REPO))
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout)
+    assert d["native"]["loaded"] and d["native"]["crc32c"] in ("avx512-vpclmulqdq",
+                                                               "sse4.2-3way")
+    assert d["pipes"]["sharers"] == 8 and d["pipes"]["pipe_bytes"] >= 64 << 10
+    assert d["cpus"]["effective"] >= 1 and isinstance(d["warnings"], list)
+    assert "devices" in d["gpu"]
