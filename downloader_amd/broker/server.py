@@ -431,7 +431,13 @@ class BrokerServer:
             rkey = q.args.get("x-dead-letter-routing-key") or q.name
             hdrs = dict(msg.props.headers or {})
             deaths = list(hdrs.get("x-death") or [])
-            deaths.insert(0, {"queue": q.name, "reason": "expired", "count": 1,
+            # as RabbitMQ: one entry per (queue, reason), its count bumped and moved first
+            prev = next((d for d in deaths if isinstance(d, dict) and d.get("queue") == q.name
+                         and d.get("reason") == "expired"), None)
+            if prev is not None:
+                deaths.remove(prev)
+            deaths.insert(0, {"queue": q.name, "reason": "expired",
+                              "count": int(prev.get("count", 0)) + 1 if prev else 1,
                               "exchange": "", "routing-keys": [q.name]})
             hdrs["x-death"] = deaths
             props = dataclasses.replace(msg.props, headers=hdrs)

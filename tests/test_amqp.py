@@ -498,7 +498,33 @@ def test_ttl_queue_dead_letters_back_with_x_death(run):
         assert asyncio.get_running_loop().time() - t0 >= 0.28
         assert d.headers["x-attempt"] == 1
         assert d.headers["x-death"][0]["queue"] == "work.delay.300"
+        assert d.headers["x-death"][0]["count"] == 1
+        # delayed again with its headers: the same (queue, reason) entry counts up
+        await b.publish_delayed("work", d.body, d.headers, 0.05)
         await d.ack()
+        d2 = None
+        for _ in range(100):
+            d2 = await b.get("work")
+            if d2 is not None:
+                break
+            await asyncio.sleep(0.02)
+        assert d2 is not None
+        deaths = d2.headers["x-death"]
+        assert deaths[0]["queue"] == "work.delay.50" and deaths[0]["count"] == 1
+        assert [x["queue"] for x in deaths] == ["work.delay.50", "work.delay.300"]
+        await d2.ack()
+        await b.publish_delayed("work", d2.body, d2.headers, 0.05)
+        d3 = None
+        for _ in range(100):
+            d3 = await b.get("work")
+            if d3 is not None:
+                break
+            await asyncio.sleep(0.02)
+        assert d3 is not None
+        assert d3.headers["x-death"][0] == {**d3.headers["x-death"][0], "queue": "work.delay.50",
+                                            "count": 2}
+        assert len(d3.headers["x-death"]) == 2
+        await d3.ack()
         await b.close(); await srv.stop()
     run(go())
 
