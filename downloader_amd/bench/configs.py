@@ -212,6 +212,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             # so every rep does the full job); one job is a sub-second sample on this box.
             reps = []
             rss0 = _rss_mb()["rss_MB"]
+            threads0 = _thread_cpu(0)
             for k in range(max(1, getattr(a, "reps", 1))):
                 suffix = f"-r{k}" if k else ""
                 m = api.make_download(f"c{cfg_no}-{a.mode}{suffix}", "http",
@@ -228,6 +229,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 assert r_k[0].outcome == "staged", r_k[0]
                 reps.append((dt_k, r_k, cpu_k, peer_k, cleanup_k))
             rss = _rss_mb()
+            thread_cpu = _thread_cpu_delta(threads0, _thread_cpu(0))
             try:
                 from downloader_amd.ops import native
                 pool = native().relay_pool_stats()
@@ -257,6 +259,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"],
             "worker_rss_peak_MB": rss["rss_peak_MB"],
             "relay_pool_after": pool,
+            **({"thread_cpu": thread_cpu} if os.environ.get("STAGER_THREAD_CPU") else {}),
             **({"stream_verify": a.stream_verify, "gpu_relay": gpu_relay}
                if getattr(a, "stream_verify", "") else {}),
             "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps],
@@ -490,6 +493,44 @@ async def config_swarm(a) -> Dict:
 
 
 # ---------------------------------------------------------------------------- config 9
+def _thread_cpu(top: int = 14) -> List[Dict]:
+    """This process' threads (the ``top`` busiest; 0 = all): OS name or Python thread name,
+    user / system CPU seconds - where a config's worker CPU goes (STAGER_THREAD_CPU=1)."""
+    import threading
+    names = {t.native_id: t.name for t in threading.enumerate()}
+    hz = os.sysconf("SC_CLK_TCK")
+    rows = []
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                comm = f.read().strip()
+        except OSError:
+            continue
+        fields = st[st.rindex(")") + 2:].split()
+        rows.append({"tid": int(tid), "name": names.get(int(tid), comm),
+                     "user_s": int(fields[11]) / hz, "sys_s": int(fields[12]) / hz})
+    rows.sort(key=lambda r: -(r["user_s"] + r["sys_s"]))
+    return rows[:top] if top else rows
+
+
+def _thread_cpu_delta(before: List[Dict], after: List[Dict], top: int = 14) -> List[Dict]:
+    """CPU per thread between two ``_thread_cpu(0)`` snapshots, grouped by name (threads of
+    one pool share a name), busiest first; threads that exited in between are missing."""
+    b = {r["tid"]: r for r in before}
+    groups: Dict[str, Dict] = {}
+    for r in after:
+        p = b.get(r["tid"], {"user_s": 0.0, "sys_s": 0.0})
+        key = r["name"].rstrip("0123456789_-")
+        g = groups.setdefault(key, {"name": key, "threads": 0, "user_s": 0.0, "sys_s": 0.0})
+        g["threads"] += 1
+        g["user_s"] = round(g["user_s"] + r["user_s"] - p["user_s"], 2)
+        g["sys_s"] = round(g["sys_s"] + r["sys_s"] - p["sys_s"], 2)
+    out = sorted(groups.values(), key=lambda g: -(g["user_s"] + g["sys_s"]))
+    return [g for g in out if g["user_s"] + g["sys_s"] > 0][:top]
+
+
 async def config_small(a) -> Dict:
     """Control-plane ceiling (extra): ``--jobs`` tiny HTTP jobs (``--small-kb``) submitted at
     once to ONE worker process with ``--concurrency`` jobs in flight. Every job still does the

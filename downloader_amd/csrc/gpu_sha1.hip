@@ -42,6 +42,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <pthread.h>
 #include <thread>
 #include <unistd.h>
 #include <unordered_map>
@@ -851,6 +852,7 @@ class PartHasher {
       return ((PartHasher*)c)->wait(t, ph, out, ol, err, el);
     };
     thread_ = std::thread([this] { run(); });
+    pthread_setname_np(thread_.native_handle(), "gpu-part-disp");
   }
 
   ~PartHasher() {
@@ -883,11 +885,19 @@ class PartHasher {
 
   int reg(void* p, size_t n) {
     if (hipSetDevice(device_) != hipSuccess) return -1;
-    return hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess ? 0 : -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool ok = hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> g(mu_);
+    registered_++;
+    reg_seconds_ += dt;
+    return ok ? 0 : -1;
   }
   void unreg(void* p) {
     hipSetDevice(device_);
     hipHostUnregister(p);
+    std::lock_guard<std::mutex> g(mu_);
+    unregistered_++;
   }
 
   uint64_t submit(const uint8_t* data, int64_t len, int64_t piece_len) {
@@ -938,6 +948,9 @@ class PartHasher {
     d["max_batch_lanes"] = max_batch_lanes_;
     d["broken"] = broken_;
     d["pending"] = jobs_.size();
+    d["registered"] = registered_;       // part buffers page-locked (hipHostRegister)
+    d["unregistered"] = unregistered_;
+    d["register_s"] = reg_seconds_;
     return d;
   }
 
@@ -1189,6 +1202,8 @@ class PartHasher {
   std::unordered_map<uint64_t, Job> jobs_;
   uint64_t seq_ = 0, submitted_ = 0, launches_ = 0, lanes_total_ = 0, max_batch_lanes_ = 0;
   bool stop_ = false, broken_ = false;
+  uint64_t registered_ = 0, unregistered_ = 0;
+  double reg_seconds_ = 0;
   GpuPartHashApi api_{};
   std::thread thread_;
 };

@@ -213,6 +213,7 @@ PYBIND11_MODULE(_native, m) {
     d["idle_bytes"] = s.idle_bytes;
     d["in_use"] = s.in_use;
     d["max_idle"] = s.max_idle;
+    d["created"] = s.created;
     return d;
   });
   m.def(

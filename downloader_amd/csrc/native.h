@@ -129,6 +129,7 @@ void set_pipes_refused(bool on);
 
 struct RelayPoolStats {
   size_t idle_buffers, idle_bytes, in_use, max_idle;
+  uint64_t created;
 };
 // GPU piece hashing of relayed parts (gpu_part_api.h, implemented by _gpuhash): when set,
 // relay_body_hashed_mb hands parts of >= min_pieces whole pieces to the GPU instead of the

@@ -1112,6 +1112,7 @@ class PartPool {
       in_use_ += 1;
     }
     try {
+      created_.fetch_add(1, std::memory_order_relaxed);
       return std::unique_ptr<PartBuffer>(new PartBuffer(n));
     } catch (...) {
       std::lock_guard<std::mutex> g(mu_);
@@ -1168,13 +1169,14 @@ class PartPool {
   }
   RelayPoolStats stats() {
     std::lock_guard<std::mutex> g(mu_);
-    return RelayPoolStats{idle_.size(), idle_bytes_, in_use_, max_idle_};
+    return RelayPoolStats{idle_.size(), idle_bytes_, in_use_, max_idle_, created_.load()};
   }
 
  private:
   std::mutex mu_;
   std::vector<std::unique_ptr<PartBuffer>> idle_;
   size_t idle_bytes_ = 0, in_use_ = 0, max_idle_ = 16;
+  std::atomic<uint64_t> created_{0};   // buffers mapped (each one faulted in, maybe page-locked)
 };
 
 PartPool& part_pool() {
