@@ -74,7 +74,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--peers", choices=["per-rank", "shared"], default="per-rank",
                    help="one blobd origin+S3 peer per worker, or one shared on rank 0")
     p.add_argument("--sink", choices=["sample", "verify", "discard", "checksum"], default="sample",
-                   help="blobd S3 sink: sample = drop bodies in the kernel (recv MSG_TRUNC) but compare a 4 KiB "
+                   help="blobd S3 sink: sample = drop bodies in the kernel (MSG_TRUNC) but compare a 4 KiB "
                         "window of every MiB (and each body's tail) with the origin generator's "
                         "bytes at the object offset; verify = compare every byte (checksum of the "
                         "body vs checksum of the generated range); discard = no check; checksum "

@@ -548,7 +548,11 @@ def _gpu_relay_on(cfg) -> Optional[str]:
     if hashing._part_hasher is not None:         # already set up (or a test double)
         return None
     try:
-        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8)):
+        # parts wait leased until their DMA, so more buffers are out at once than with host
+        # hashing: keep as many idle for reuse (each new one is faulted in and page-locked;
+        # the pool's default 16 made 240 of 855 parts map, pin, unpin and unmap a buffer)
+        pool_idle = max(16, min(64, int(getattr(d, "stream_gpu_pending", 64) or 64)))
+        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8), pool_idle):
             return None
         return "no usable HIP device"
     except Exception as e:
