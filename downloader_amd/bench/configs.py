@@ -205,8 +205,9 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             s3o = {"part_size": part_mb << 20} if part_mb else {}
             if getattr(a, "checksum", ""):
                 s3o["checksum"] = a.checksum
-            w = Worker(_cfg(a.mode, b.endpoint, stage, cert, concurrency=1, download=dl, s3=s3o),
-                       broker=MemoryBroker())
+            kj = max(1, int(getattr(a, "torrent_jobs", 1) or 1))
+            w = Worker(_cfg(a.mode, b.endpoint, stage, cert, concurrency=kj, download=dl,
+                            s3=s3o), broker=MemoryBroker())
             await w.start(health=False)
             # --reps: the same torrent staged again under a fresh media id (no done marker,
             # so every rep does the full job); one job is a sub-second sample on this box.
@@ -215,10 +216,12 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             threads0 = _thread_cpu(0)
             for k in range(max(1, getattr(a, "reps", 1))):
                 suffix = f"-r{k}" if k else ""
-                m = api.make_download(f"c{cfg_no}-{a.mode}{suffix}", "http",
-                                      b.files_url("job.torrent"), "TV" if cfg_no == 4 else "MOVIE")
+                # --torrent-jobs K: K copies of the job at once (distinct media ids)
+                ms = [api.make_download(f"c{cfg_no}-{a.mode}{suffix}" + (f"-j{i}" if i else ""),
+                                        "http", b.files_url("job.torrent"),
+                                        "TV" if cfg_no == 4 else "MOVIE") for i in range(kj)]
                 cpu0, peer0 = _self_cpu(), b.cpu_seconds()
-                dt_k, r_k = await _run_jobs(w, [m])
+                dt_k, r_k = await _run_jobs(w, ms)
                 cpu_k, peer_k = _self_cpu() - cpu0, b.cpu_seconds() - peer0
                 # job_s ends at the convert publish; the background unlink of the staged
                 # files (instance.background_cleanup) is timed separately here.
@@ -226,7 +229,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 await asyncio.get_running_loop().run_in_executor(
                     None, get_reaper(w.services).drain, 600.0)
                 cleanup_k = time.perf_counter() - tc
-                assert r_k[0].outcome == "staged", r_k[0]
+                assert all(x.outcome == "staged" for x in r_k), r_k
                 reps.append((dt_k, r_k, cpu_k, peer_k, cleanup_k))
             rss = _rss_mb()
             thread_cpu = _thread_cpu_delta(threads0, _thread_cpu(0))
@@ -250,7 +253,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
     return {"config": cfg_no, "mode": a.mode, "bytes": total, "files": len(sizes),
             **({"tls": True} if cert else {}),
             "piece_len": a.piece_mb << 20, "job_s": round(dt, 3),
-            "MBps": round(total / dt / MB, 1), "setup_s": round(setup_s, 2),
+            "MBps": round(kj * total / dt / MB, 1), "setup_s": round(setup_s, 2),
             "s3_bytes_received": st["bytes_received"], "uploaded_bytes": r[0].bytes,
             "torrent": r[0].stats.get("torrent", {}), "stage_s": r[0].stats.get("stage_s", {}),
             "eager_upload_s": r[0].stats.get("eager_upload_s"),
@@ -262,7 +265,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             **({"thread_cpu": thread_cpu} if os.environ.get("STAGER_THREAD_CPU") else {}),
             **({"stream_verify": a.stream_verify, "gpu_relay": gpu_relay}
                if getattr(a, "stream_verify", "") else {}),
-            "reps": len(reps), "MBps_reps": [round(total / x[0] / MB, 1) for x in reps],
+            **({"torrent_jobs": kj} if kj > 1 else {}),
+            "reps": len(reps), "MBps_reps": [round(kj * total / x[0] / MB, 1) for x in reps],
             # per rep (the first is the worker's cold job): job seconds, summed relay seconds
             # of all parts, worker and peer CPU seconds
             "reps_detail": [{"job_s": round(x[0], 3),
@@ -602,6 +606,9 @@ def main(argv=None) -> int:
     ap.add_argument("--object-mb", type=int, default=10,
                     help="config 1: object size (BASELINE: 10 MB)")
     ap.add_argument("--piece-mb", type=int, default=4)
+    ap.add_argument("--torrent-jobs", type=int, default=1,
+                    help="configs 3/4: K copies of the torrent job at once per rep (aggregate "
+                         "MB/s; the worker's concurrency = K)")
     ap.add_argument("--reps", type=int, default=1,
                     help="configs 3/4: stage the torrent this many times, report the median")
     ap.add_argument("--verify-backend", choices=["cpu", "gpu", "auto"], default="auto")
