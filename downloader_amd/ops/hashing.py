@@ -122,11 +122,10 @@ _part_wait_pool = None
 _part_hasher_failed = False
 
 
-def gpu_relay_hashing(min_pieces: int = 8, pool_idle: int = 0) -> bool:
+def gpu_relay_hashing(min_pieces: int = 8) -> bool:
     """Route the hashed relay's parts to the gfx950 ``PartHasher`` (batched, one lane per
     piece; csrc/gpu_sha1.hip) instead of the host multi-buffer SHA-1. Created once per
-    process on the worker's GPU; False (host hashing) when no HIP device is usable.
-    ``pool_idle``: idle part buffers the relay pool keeps (0 = unchanged)."""
+    process on the worker's GPU; False (host hashing) when no HIP device is usable."""
     global _part_hasher, _part_wait_pool, _part_hasher_failed
     with _gpu_lock:
         if _part_hasher is not None:
@@ -137,8 +136,6 @@ def gpu_relay_hashing(min_pieces: int = 8, pool_idle: int = 0) -> bool:
             from concurrent.futures import ThreadPoolExecutor
             ph = gpuhash().PartHasher(gpu_device(), 1 << 30, 8, 4, 16384)
             native().set_gpu_part_hasher(ph.api(), min_pieces)
-            if pool_idle > 0:
-                native().relay_pool_set_max_idle(pool_idle)
         except Exception:
             _part_hasher_failed = True
             raise

@@ -105,6 +105,24 @@ def _trim_relay_buffers() -> None:
         pass
 
 
+POOL_IDLE_DEFAULT = 16         # the native pool's own default
+POOL_IDLE_CAP = 128            # at 64 MiB parts: 8 GiB of idle buffers at most
+_pool_want: Dict[int, int] = {}   # id(stager) -> part buffers it may have out at once
+
+
+def _size_pool() -> None:
+    """Keep as many idle part buffers as the running stream stagers may have out at once:
+    relays in flight, plus parts waiting for their DMA with GPU hashing. Fewer made buffers
+    churn - mapped, faulted in (and page-locked for the GPU), then unmapped again: with two
+    20 GB jobs at once the host path created 214 buffers for 4 reps, the GPU path 356."""
+    want = max(POOL_IDLE_DEFAULT, min(POOL_IDLE_CAP, sum(_pool_want.values())))
+    try:
+        from ..ops import native
+        native().relay_pool_set_max_idle(want)
+    except Exception:
+        pass
+
+
 def _schedule_trim(idle_s: float) -> None:
     """Last stream stager of the process finished: trim after ``idle_s`` quiet seconds (0 =
     now), so back-to-back jobs keep reusing warm buffers while an idle worker holds none."""
@@ -186,6 +204,7 @@ class StreamStager:
         self.stats = {"relay_s": 0.0, "gap_bytes": 0, "units": 0}
         # GPU piece hashing of relayed parts: at most this many parts awaiting digests
         self._gpu_slots: Optional[asyncio.Semaphore] = None
+        self.gpu_pending = 0
         self._continuations: Set[asyncio.Task] = set()
         gpu_pending = int(getattr(getattr(cfg, "download", None), "stream_gpu_pending", 0) or 0)
         if gpu_pending > 0 and getattr(getattr(cfg, "download", None),
@@ -193,6 +212,7 @@ class StreamStager:
             why = _gpu_relay_on(cfg)
             if why is None:
                 self._gpu_slots = asyncio.Semaphore(gpu_pending)
+                self.gpu_pending = gpu_pending
                 self.stats["verify"] = "gpu"
                 # parts still queued below which the rest hash on the host
                 self.gpu_tail = int(getattr(cfg.download, "stream_gpu_tail", 0) or 0)
@@ -239,6 +259,8 @@ class StreamStager:
         global _active_stagers
         multi = [t for t in self.targets if not t.single and t.size]
         _active_stagers += 1
+        _pool_want[id(self)] = self.parallel + (self.gpu_pending if self._gpu_slots else 0)
+        _size_pool()
         try:
             for t in self.targets:
                 if t.size == 0:
@@ -273,6 +295,7 @@ class StreamStager:
             raise
         finally:
             _active_stagers -= 1
+            _pool_want.pop(id(self), None)
             if _active_stagers == 0:
                 _schedule_trim(self.trim_idle_s)
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
@@ -548,11 +571,7 @@ def _gpu_relay_on(cfg) -> Optional[str]:
     if hashing._part_hasher is not None:         # already set up (or a test double)
         return None
     try:
-        # parts wait leased until their DMA, so more buffers are out at once than with host
-        # hashing: keep as many idle for reuse (each new one is faulted in and page-locked;
-        # the pool's default 16 made 240 of 855 parts map, pin, unpin and unmap a buffer)
-        pool_idle = max(16, min(64, int(getattr(d, "stream_gpu_pending", 64) or 64)))
-        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8), pool_idle):
+        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8)):
             return None
         return "no usable HIP device"
     except Exception as e:

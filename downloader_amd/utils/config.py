@@ -145,7 +145,9 @@ class DownloadConfig(BaseModel):
     # idle seconds after the last stream-staged job before the hashed relay's pooled part
     # buffers (one per part in flight, up to 64 MiB each) are unmapped; jobs inside the window
     # reuse them without re-faulting ~1 GiB of huge pages (MI355X box, 4 GB torrent: 26.7 -
-    # 27.8 GB/s warm vs 19.2 - 20.0 GB/s when every job faults its buffers afresh)
+    # 27.8 GB/s warm vs 19.2 - 20.0 GB/s when every job faults its buffers afresh). Meanwhile
+    # the pool keeps as many idle buffers as the running jobs may have out (relays in flight,
+    # plus parts awaiting their DMA with GPU hashing), at most 128.
     relay_pool_idle_trim_s: float = 60.0
     # Splice pipe capacity per transfer in KiB (relays, HTTP bodies to disk). 0: derived from
     # the user's pipe page budget (fs.pipe-user-pages-soft, 64 MiB by default for non-root
