@@ -623,7 +623,7 @@ def main(argv=None) -> int:
                     help="download.stream_verify_backend: relayed parts' pieces hashed by the "
                          "host multi-buffer SHA-1 or the gfx950 PartHasher")
     ap.add_argument("--stream-gpu-pending", type=int, default=0,
-                    help="download.stream_gpu_pending (parts per job awaiting GPU digests)")
+                    help="download.stream_gpu_pending (parts awaiting GPU digests, all jobs)")
     ap.add_argument("--stream-gpu-tail", type=int, default=None,
                     help="download.stream_gpu_tail (queued parts below which the host hashes)")
     ap.add_argument("--stream-parallel", type=int, default=0,

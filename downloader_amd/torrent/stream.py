@@ -27,6 +27,7 @@ import asyncio
 import hashlib
 import os
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set, Tuple
 
@@ -106,8 +107,23 @@ def _trim_relay_buffers() -> None:
 
 
 POOL_IDLE_DEFAULT = 16         # the native pool's own default
-POOL_IDLE_CAP = 128            # at 64 MiB parts: 8 GiB of idle buffers at most
-_pool_want: Dict[int, int] = {}   # id(stager) -> part buffers it may have out at once
+POOL_IDLE_CAP = 192            # at 64 MiB parts: 12 GiB of idle buffers at most
+_pool_want: Dict[int, int] = {}   # id(stager) -> relays it runs at once
+_gpu_pending_want = 0             # process-wide parts awaiting GPU digests (0: no GPU stager)
+_gpu_pending_sems: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
+    """Parts awaiting GPU digests, shared by every stream stager of the process (one per
+    event loop): the device needs ~128 - 160 parts in flight to hide its per-piece latency,
+    whether they come from one job or several, and every one of them holds a part buffer
+    until its DMA. Per-job budgets made two jobs hold twice the buffers (pool churn) or,
+    halved, starved one job (profiles/r3_relayhash3/)."""
+    loop = asyncio.get_running_loop()
+    sem = _gpu_pending_sems.get(loop)
+    if sem is None:
+        sem = _gpu_pending_sems[loop] = asyncio.Semaphore(n)
+    return sem
 
 
 def _size_pool() -> None:
@@ -115,7 +131,8 @@ def _size_pool() -> None:
     relays in flight, plus parts waiting for their DMA with GPU hashing. Fewer made buffers
     churn - mapped, faulted in (and page-locked for the GPU), then unmapped again: with two
     20 GB jobs at once the host path created 214 buffers for 4 reps, the GPU path 356."""
-    want = max(POOL_IDLE_DEFAULT, min(POOL_IDLE_CAP, sum(_pool_want.values())))
+    want = max(POOL_IDLE_DEFAULT,
+               min(POOL_IDLE_CAP, sum(_pool_want.values()) + _gpu_pending_want))
     try:
         from ..ops import native
         native().relay_pool_set_max_idle(want)
@@ -202,7 +219,8 @@ class StreamStager:
         self._outstanding = 0
         self._finished = asyncio.Event()
         self.stats = {"relay_s": 0.0, "gap_bytes": 0, "units": 0}
-        # GPU piece hashing of relayed parts: at most this many parts awaiting digests
+        # GPU piece hashing of relayed parts: at most this many parts awaiting digests,
+        # across every stream stager of the process
         self._gpu_slots: Optional[asyncio.Semaphore] = None
         self.gpu_pending = 0
         self._continuations: Set[asyncio.Task] = set()
@@ -211,8 +229,7 @@ class StreamStager:
                                        "stream_verify_backend", "cpu") == "gpu":
             why = _gpu_relay_on(cfg)
             if why is None:
-                self._gpu_slots = asyncio.Semaphore(gpu_pending)
-                self.gpu_pending = gpu_pending
+                self.gpu_pending = gpu_pending    # the process-wide budget (run())
                 self.stats["verify"] = "gpu"
                 # parts still queued below which the rest hash on the host
                 self.gpu_tail = int(getattr(cfg.download, "stream_gpu_tail", 0) or 0)
@@ -259,7 +276,11 @@ class StreamStager:
         global _active_stagers
         multi = [t for t in self.targets if not t.single and t.size]
         _active_stagers += 1
-        _pool_want[id(self)] = self.parallel + (self.gpu_pending if self._gpu_slots else 0)
+        global _gpu_pending_want
+        _pool_want[id(self)] = self.parallel
+        if self.gpu_pending:
+            self._gpu_slots = _gpu_pending_sem(self.gpu_pending)
+            _gpu_pending_want = max(_gpu_pending_want, self.gpu_pending)
         _size_pool()
         try:
             for t in self.targets:
@@ -297,6 +318,7 @@ class StreamStager:
             _active_stagers -= 1
             _pool_want.pop(id(self), None)
             if _active_stagers == 0:
+                _gpu_pending_want = 0
                 _schedule_trim(self.trim_idle_s)
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
                  "virtual": True} for f in self.selected]

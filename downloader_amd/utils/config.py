@@ -174,7 +174,9 @@ class DownloadConfig(BaseModel):
     # launches; the relay slot is freed when the part's bytes are moved, digests arrive in a
     # continuation)
     stream_verify_backend: Literal["cpu", "gpu"] = "cpu"
-    stream_gpu_pending: int = 64                # parts per job awaiting GPU digests
+    # parts awaiting GPU digests across all jobs of the worker (each holds its part buffer
+    # until its DMA): ~128 - 160 hide the device's per-piece latency (profiles/r3_relayhash*/)
+    stream_gpu_pending: int = 160
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
     # once fewer parts than this are queued, the job's remaining parts hash on the host (the
     # GPU's per-piece latency would otherwise land on the end of the job)
