@@ -119,6 +119,8 @@ class Worker:
         d = self.cfg.download
         # the uid's pipe page budget is shared: size splice pipes to this worker's share
         self.pipe_bytes = limits.apply_pipe_size(d.pipe_kb, d.pipe_sharers)
+        if d.gpu_prewarm and d.stream_verify_backend != "cpu" and d.stream_gpu_pending > 0:
+            await self._prewarm_part_hasher()
         if d.gpu_prewarm and d.verify_backend != "cpu":
             from ..ops import hashing
             # auto never picks the GPU on a host with the multi-buffer SHA-1: no HIP init
@@ -130,6 +132,22 @@ class Worker:
                 self.log.info({"gpu_verifier": warm}, "gpu verifier prewarm")
             except Exception as e:  # a missing device must not stop the worker
                 self.log.warn({"err": str(e)}, "gpu verifier prewarm failed")
+
+    async def _prewarm_part_hasher(self) -> None:
+        """Set up the gfx950 PartHasher for streamed torrents now (HIP init and device slots,
+        off the event loop) so stream_verify_backend auto/gpu never initialises the device
+        inside a job. A missing device leaves auto on the host."""
+        from ..ops import gpu_available, hashing
+        d = self.cfg.download
+        loop = asyncio.get_running_loop()
+        try:
+            if not await loop.run_in_executor(None, gpu_available):
+                return
+            ok = await loop.run_in_executor(None, hashing.gpu_relay_hashing,
+                                            d.stream_gpu_min_pieces)
+            self.log.info({"gpu_part_hasher": ok}, "gpu relay hashing prewarm")
+        except Exception as e:  # a broken device must not stop the worker
+            self.log.warn({"err": str(e)}, "gpu relay hashing prewarm failed")
 
     async def start(self, health: bool = True) -> None:
         await self.init()

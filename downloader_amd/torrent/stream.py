@@ -224,13 +224,24 @@ class StreamStager:
         self._gpu_slots: Optional[asyncio.Semaphore] = None
         self.gpu_pending = 0
         self._continuations: Set[asyncio.Task] = set()
-        gpu_pending = int(getattr(getattr(cfg, "download", None), "stream_gpu_pending", 0) or 0)
-        if gpu_pending > 0 and getattr(getattr(cfg, "download", None),
-                                       "stream_verify_backend", "cpu") == "gpu":
+        d = getattr(cfg, "download", None)
+        gpu_pending = int(getattr(d, "stream_gpu_pending", 0) or 0)
+        self.verify_mode = getattr(d, "stream_verify_backend", "cpu")
+        self._host_mb = True
+        from ..ops import hashing
+        if self.verify_mode == "auto" and hashing._part_hasher is None:
+            # auto never initialises the device inside a job (HIP init would stall the event
+            # loop): only a hasher the worker set up at start (download.gpu_prewarm) is used
+            self.verify_mode = "cpu"
+        if gpu_pending > 0 and self.verify_mode in ("gpu", "auto"):
             why = _gpu_relay_on(cfg)
             if why is None:
                 self.gpu_pending = gpu_pending    # the process-wide budget (run())
-                self.stats["verify"] = "gpu"
+                try:
+                    self._host_mb = hashing.host_multibuffer()
+                except Exception:
+                    self._host_mb = False
+                self.stats["verify"] = "gpu" if self.verify_mode == "gpu" else "auto"
                 # parts still queued below which the rest hash on the host
                 self.gpu_tail = int(getattr(cfg.download, "stream_gpu_tail", 0) or 0)
             else:
@@ -334,7 +345,7 @@ class StreamStager:
                 await self._gpu_slots.acquire()
                 # the job's last parts hash on the host: their GPU latency (~piece_len / 58
                 # MB/s) would land on the end of the job with nothing left to overlap it
-                gpu = queue.qsize() >= self.gpu_tail
+                gpu = self._gpu_now() and queue.qsize() >= self.gpu_tail
                 try:
                     res = await self._relay_part(u, gpu)
                 except BaseException as e:
@@ -365,6 +376,16 @@ class StreamStager:
             if self.error is not None:
                 return
             self._settle(u, requeue, queue)
+
+    def _gpu_now(self) -> bool:
+        """Hash this part's pieces on the device? ``gpu``: always. ``auto``: when the host
+        lacks the AVX-512 multi-buffer SHA-1, or when more than one stream job shares the
+        worker's CPUs - measured on the MI355X box (config 4, steady reps): one job 24.3 -
+        24.5 GB/s on the host vs 21.8 - 22.4 on the GPU, two jobs at once 24.1 - 25.3 vs
+        26.6 - 27.6 GB/s at 28 % less worker CPU (profiles/r3_relayhash4/)."""
+        if self.verify_mode == "gpu":
+            return True
+        return not self._host_mb or _active_stagers >= 2
 
     async def _unit_failed(self, u: _Unit, e: BaseException,
                            queue: "asyncio.Queue[_Unit]") -> bool:

@@ -548,3 +548,80 @@ def test_stream_survives_part_hasher_failures(run, tmp_path, make_cfg, origin_cl
         run(go())
     finally:
         hashing.use_part_hasher(None)
+
+
+@pytest.mark.parametrize("jobs", [1, 2])
+def test_stream_verify_auto_uses_the_device_when_jobs_share_the_worker(run, tmp_path, make_cfg,
+                                                                       origin_cls, jobs):
+    """``stream_verify_backend: auto`` with a hasher set up at worker start: one stream job
+    hashes its parts on the host (faster alone on an AVX-512 host), two at once send parts to
+    the device (more throughput and less worker CPU, profiles/r3_relayhash4/)."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Movie"
+        src.mkdir(parents=True)
+        data = os.urandom(24 * (1 << 20) + 777)
+        (src / "m.mkv").write_bytes(data)
+        origin.blobs["/ws/Movie/m.mkv"] = data
+        origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
+                                                    url_list=[origin.url("/ws/")])
+        # 5 MiB parts one at a time: each job is several sequential relays, so two jobs
+        # submitted together overlap for most of their parts
+        w = _worker(make_cfg, ep, concurrency=2, s3={"part_size": 5 << 20},
+                    download={"stream_verify_backend": "auto", "stream_gpu_min_pieces": 4,
+                              "stream_gpu_tail": 0, "gpu_prewarm": False,
+                              "torrent_stream_parallel": 1})
+        await w.start(health=False)
+        for i in range(jobs):
+            await w.submit(api.make_download(f"au{jobs}-{i}", "http",
+                                             origin.url("/t/m.torrent")))
+        await _wait(w, n=jobs, timeout=60)
+        for i, r in enumerate(sorted(w.results, key=lambda r: r.job_id)):
+            assert r.outcome == "staged", r
+            assert s3.get("triton-staging", keys.object_key(f"au{jobs}-{i}", "m.mkv")) == data
+        gpu_parts = sum(r.stats["torrent"]["gpu_parts"] for r in w.results)
+        assert {r.stats["torrent"]["verify"] for r in w.results} == {"auto"}
+        if jobs == 1 and hashing.host_multibuffer():
+            assert gpu_parts == 0
+        if jobs == 2:
+            assert gpu_parts > 0
+        assert native().relay_pool_stats()["in_use"] == 0
+        await w.stop(); await s3.stop(); await origin.stop()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.01), 4)    # "set up at worker start"
+    try:
+        run(go())
+    finally:
+        hashing.use_part_hasher(None)
+
+
+def test_stream_verify_auto_without_a_prewarmed_device_stays_on_the_host(run, tmp_path,
+                                                                         make_cfg, origin_cls):
+    from downloader_amd.ops import hashing
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Movie"
+        src.mkdir(parents=True)
+        data = os.urandom(6 * (1 << 20) + 5)
+        (src / "m.mkv").write_bytes(data)
+        origin.blobs["/ws/Movie/m.mkv"] = data
+        origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
+                                                    url_list=[origin.url("/ws/")])
+        w = _worker(make_cfg, ep, download={"stream_verify_backend": "auto"})
+        await w.start(health=False)
+        await w.submit(api.make_download("an", "http", origin.url("/t/m.torrent")))
+        await _wait(w, timeout=60)
+        r = w.results[0]
+        assert r.outcome == "staged" and r.stats["torrent"]["verify"] == "host"
+        assert r.stats["torrent"]["gpu_parts"] == 0
+        await w.stop(); await s3.stop(); await origin.stop()
+
+    assert hashing._part_hasher is None
+    run(go())
