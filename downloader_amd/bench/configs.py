@@ -239,7 +239,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             except Exception:
                 pool = {}
             gpu_relay = {}
-            if getattr(a, "stream_verify", "") == "gpu":
+            if getattr(a, "stream_verify", "") in ("gpu", "auto"):
                 from downloader_amd.ops import hashing
                 gpu_relay = hashing.gpu_relay_stats()
             await w.stop()
@@ -619,9 +619,10 @@ def main(argv=None) -> int:
                     help="fetched runs queued per stream when the GPU batcher verifies them")
     ap.add_argument("--torrent-stream", choices=["auto", "always", "off"], default="auto",
                     help="download.torrent_stream: webseed->S3 relay (auto) or disk staging (off)")
-    ap.add_argument("--stream-verify", choices=["cpu", "gpu"], default="",
+    ap.add_argument("--stream-verify", choices=["cpu", "gpu", "auto"], default="",
                     help="download.stream_verify_backend: relayed parts' pieces hashed by the "
-                         "host multi-buffer SHA-1 or the gfx950 PartHasher")
+                         "host multi-buffer SHA-1, the gfx950 PartHasher, or auto (the device "
+                         "when stream jobs share the worker)")
     ap.add_argument("--stream-gpu-pending", type=int, default=0,
                     help="download.stream_gpu_pending (parts awaiting GPU digests, all jobs)")
     ap.add_argument("--stream-gpu-tail", type=int, default=None,
