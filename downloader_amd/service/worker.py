@@ -119,7 +119,7 @@ class Worker:
         d = self.cfg.download
         # the uid's pipe page budget is shared: size splice pipes to this worker's share
         self.pipe_bytes = limits.apply_pipe_size(d.pipe_kb, d.pipe_sharers)
-        if d.gpu_prewarm and d.stream_verify_backend != "cpu" and d.stream_gpu_pending > 0:
+        if d.gpu_prewarm and d.stream_verify_backend == "gpu" and d.stream_gpu_pending > 0:
             await self._prewarm_part_hasher()
         if d.gpu_prewarm and d.verify_backend != "cpu":
             from ..ops import hashing
@@ -134,9 +134,9 @@ class Worker:
                 self.log.warn({"err": str(e)}, "gpu verifier prewarm failed")
 
     async def _prewarm_part_hasher(self) -> None:
-        """Set up the gfx950 PartHasher for streamed torrents now (HIP init and device slots,
-        off the event loop) so stream_verify_backend auto/gpu never initialises the device
-        inside a job. A missing device leaves auto on the host."""
+        """stream_verify_backend gpu: set up the gfx950 PartHasher now (HIP init and device
+        slots, off the event loop) instead of inside the first job. (``auto`` sets it up on
+        an executor thread when a second stream job starts.)"""
         from ..ops import gpu_available, hashing
         d = self.cfg.download
         loop = asyncio.get_running_loop()

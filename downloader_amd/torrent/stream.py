@@ -126,6 +126,34 @@ def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
     return sem
 
 
+_gpu_init_started = False
+
+
+def _start_gpu_init(min_pieces: int) -> None:
+    """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and 8 device
+    slots take a moment; the event loop keeps relaying meanwhile). Once per process; a
+    missing device or a failed init leaves every part on the host."""
+    global _gpu_init_started
+    from ..ops import hashing
+    if _gpu_init_started or hashing._part_hasher is not None or hashing._part_hasher_failed:
+        return
+    _gpu_init_started = True
+
+    def init() -> bool:
+        from ..ops import gpu_available
+        return gpu_available() and hashing.gpu_relay_hashing(min_pieces)
+    fut = asyncio.get_running_loop().run_in_executor(None, init)
+    fut.add_done_callback(lambda f: f.cancelled() or f.exception())   # retrieved
+
+
+def _set_gpu_pending_want(n: int) -> None:
+    global _gpu_pending_want
+    want = n if n == 0 else max(_gpu_pending_want, n)
+    if want != _gpu_pending_want:
+        _gpu_pending_want = want
+        _size_pool()
+
+
 def _size_pool() -> None:
     """Keep as many idle part buffers as the running stream stagers may have out at once:
     relays in flight, plus parts waiting for their DMA with GPU hashing. Fewer made buffers
@@ -226,24 +254,25 @@ class StreamStager:
         self._continuations: Set[asyncio.Task] = set()
         d = getattr(cfg, "download", None)
         gpu_pending = int(getattr(d, "stream_gpu_pending", 0) or 0)
-        self.verify_mode = getattr(d, "stream_verify_backend", "cpu")
-        self._host_mb = True
+        self.verify_mode = getattr(d, "stream_verify_backend", "cpu") if gpu_pending > 0 else "cpu"
+        self._min_pieces = int(getattr(d, "stream_gpu_min_pieces", 8) or 8)
+        # parts still queued below which the rest hash on the host
+        self.gpu_tail = int(getattr(d, "stream_gpu_tail", 0) or 0)
         from ..ops import hashing
-        if self.verify_mode == "auto" and hashing._part_hasher is None:
-            # auto never initialises the device inside a job (HIP init would stall the event
-            # loop): only a hasher the worker set up at start (download.gpu_prewarm) is used
-            self.verify_mode = "cpu"
-        if gpu_pending > 0 and self.verify_mode in ("gpu", "auto"):
+        try:
+            self._host_mb = hashing.host_multibuffer()
+        except Exception:
+            self._host_mb = False
+        if self.verify_mode == "auto":
+            # the device is set up off the event loop when it is first wanted (run()); parts
+            # go to it once it is ready
+            self.gpu_pending = gpu_pending
+            self.stats["verify"] = "auto"
+        if self.verify_mode == "gpu":
             why = _gpu_relay_on(cfg)
             if why is None:
                 self.gpu_pending = gpu_pending    # the process-wide budget (run())
-                try:
-                    self._host_mb = hashing.host_multibuffer()
-                except Exception:
-                    self._host_mb = False
-                self.stats["verify"] = "gpu" if self.verify_mode == "gpu" else "auto"
-                # parts still queued below which the rest hash on the host
-                self.gpu_tail = int(getattr(cfg.download, "stream_gpu_tail", 0) or 0)
+                self.stats["verify"] = "gpu"
             else:
                 self.stats["verify_fallback"] = why
                 job.logger.warn("GPU piece hashing unavailable, hashing on the host", err=why)
@@ -287,11 +316,9 @@ class StreamStager:
         global _active_stagers
         multi = [t for t in self.targets if not t.single and t.size]
         _active_stagers += 1
-        global _gpu_pending_want
         _pool_want[id(self)] = self.parallel
-        if self.gpu_pending:
-            self._gpu_slots = _gpu_pending_sem(self.gpu_pending)
-            _gpu_pending_want = max(_gpu_pending_want, self.gpu_pending)
+        if self.verify_mode == "auto" and self._gpu_wanted():
+            _start_gpu_init(self._min_pieces)
         _size_pool()
         try:
             for t in self.targets:
@@ -329,7 +356,7 @@ class StreamStager:
             _active_stagers -= 1
             _pool_want.pop(id(self), None)
             if _active_stagers == 0:
-                _gpu_pending_want = 0
+                _set_gpu_pending_want(0)
                 _schedule_trim(self.trim_idle_s)
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
                  "virtual": True} for f in self.selected]
@@ -338,7 +365,7 @@ class StreamStager:
         while True:
             u = await queue.get()
             u.state = "running"
-            if self._gpu_slots is not None and u.target is not None:
+            if u.target is not None and self._gpu_sem() is not None:
                 # GPU piece hashing: this worker only moves the part's bytes; waiting for the
                 # digests (~piece_len / 58 MB/s on the device) and the checks run in a
                 # continuation, so the relay slots stay busy relaying meanwhile
@@ -377,6 +404,20 @@ class StreamStager:
                 return
             self._settle(u, requeue, queue)
 
+    def _gpu_wanted(self) -> bool:
+        """``auto``: is the device worth it now? (no AVX-512 SHA-1, or jobs share the worker)"""
+        return not self._host_mb or _active_stagers >= 2
+
+    def _gpu_sem(self) -> Optional[asyncio.Semaphore]:
+        """The process-wide budget of parts awaiting GPU digests, once a hasher is ready
+        (``gpu``: set up in __init__; ``auto``: by ``_start_gpu_init``); None = host only."""
+        if self._gpu_slots is None and self.gpu_pending:
+            from ..ops import hashing
+            if hashing._part_hasher is not None:
+                self._gpu_slots = _gpu_pending_sem(self.gpu_pending)
+                _set_gpu_pending_want(self.gpu_pending)
+        return self._gpu_slots
+
     def _gpu_now(self) -> bool:
         """Hash this part's pieces on the device? ``gpu``: always. ``auto``: when the host
         lacks the AVX-512 multi-buffer SHA-1, or when more than one stream job shares the
@@ -385,7 +426,9 @@ class StreamStager:
         26.6 - 27.6 GB/s at 28 % less worker CPU (profiles/r3_relayhash4/)."""
         if self.verify_mode == "gpu":
             return True
-        return not self._host_mb or _active_stagers >= 2
+        if self._gpu_wanted():
+            return True
+        return False
 
     async def _unit_failed(self, u: _Unit, e: BaseException,
                            queue: "asyncio.Queue[_Unit]") -> bool:

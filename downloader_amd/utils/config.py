@@ -173,8 +173,8 @@ class DownloadConfig(BaseModel):
     # multi-buffer SHA-1 (cpu) or by the gfx950 PartHasher (gpu: batched one-lane-per-piece
     # launches; the relay slot is freed when the part's bytes are moved, digests arrive in a
     # continuation)
-    # auto: the GPU only when the worker set it up at start (gpu_prewarm) and either the host
-    # lacks AVX-512 or more than one stream job is running (profiles/r3_relayhash4/)
+    # auto: the GPU when more than one stream job shares the worker or the host lacks AVX-512
+    # (set up on an executor thread the first time; profiles/r3_relayhash4/, r3_auto/)
     stream_verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
     # parts awaiting GPU digests across all jobs of the worker (each holds its part buffer
     # until its DMA): ~128 - 160 hide the device's per-piece latency (profiles/r3_relayhash*/)
