@@ -405,8 +405,13 @@ class StreamStager:
             self._settle(u, requeue, queue)
 
     def _gpu_wanted(self) -> bool:
-        """``auto``: is the device worth it now? (no AVX-512 SHA-1, or jobs share the worker)"""
-        return not self._host_mb or _active_stagers >= 2
+        """``auto``: is the device worth it? When the host lacks the AVX-512 SHA-1, when jobs
+        share the worker, or when this job has more parts than the host-hashed tail - config
+        4 on the MI355X box, steady reps: one job 26.3 - 28.0 GB/s at 6.5 - 6.6 worker CPU-s
+        with the last 96 parts on the host vs 24.8 - 25.4 at 7.7 - 8.2 all on the host, two
+        jobs 26.5 - 28.4 vs 23.7 - 25.5 at 13 - 14 vs 17 - 18 CPU-s (profiles/r3_tail2/)."""
+        return (not self._host_mb or _active_stagers >= 2
+                or sum(1 for u in self.units if u.target is not None) > self.gpu_tail)
 
     def _gpu_sem(self) -> Optional[asyncio.Semaphore]:
         """The process-wide budget of parts awaiting GPU digests, once a hasher is ready
@@ -419,11 +424,8 @@ class StreamStager:
         return self._gpu_slots
 
     def _gpu_now(self) -> bool:
-        """Hash this part's pieces on the device? ``gpu``: always. ``auto``: when the host
-        lacks the AVX-512 multi-buffer SHA-1, or when more than one stream job shares the
-        worker's CPUs - measured on the MI355X box (config 4, steady reps): one job 24.3 -
-        24.5 GB/s on the host vs 21.8 - 22.4 on the GPU, two jobs at once 24.1 - 25.3 vs
-        26.6 - 27.6 GB/s at 28 % less worker CPU (profiles/r3_relayhash4/)."""
+        """Hash this part's pieces on the device? ``gpu``: always; ``auto``: _gpu_wanted().
+        (Either way the job's last ``stream_gpu_tail`` queued parts stay on the host.)"""
         if self.verify_mode == "gpu":
             return True
         if self._gpu_wanted():

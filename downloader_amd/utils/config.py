@@ -173,16 +173,19 @@ class DownloadConfig(BaseModel):
     # multi-buffer SHA-1 (cpu) or by the gfx950 PartHasher (gpu: batched one-lane-per-piece
     # launches; the relay slot is freed when the part's bytes are moved, digests arrive in a
     # continuation)
-    # auto: the GPU when more than one stream job shares the worker or the host lacks AVX-512
-    # (set up on an executor thread the first time; profiles/r3_relayhash4/, r3_auto/)
+    # auto: the GPU for jobs with more parts than stream_gpu_tail, when stream jobs share the
+    # worker, or when the host lacks AVX-512 (set up on an executor thread the first time it
+    # is wanted; profiles/r3_relayhash4/, r3_tail2/)
     stream_verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
     # parts awaiting GPU digests across all jobs of the worker (each holds its part buffer
     # until its DMA): ~128 - 160 hide the device's per-piece latency (profiles/r3_relayhash*/)
     stream_gpu_pending: int = 160
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
     # once fewer parts than this are queued, the job's remaining parts hash on the host (the
-    # GPU's per-piece latency would otherwise land on the end of the job)
-    stream_gpu_tail: int = 16
+    # GPU's per-piece latency would otherwise land on the end of the job): 16 / 48 / 96 / 128
+    # / 160 gave 21.2 - 21.8 / 22.7 - 23.6 / 25.0 - 29.1 / 25.7 - 28.5 / 24.4 - 27.5 GB/s
+    # for one 20 GB job vs 22.7 - 25.4 on the host (profiles/r3_tail*/)
+    stream_gpu_tail: int = 96
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
     # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of

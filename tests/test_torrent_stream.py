@@ -550,12 +550,12 @@ def test_stream_survives_part_hasher_failures(run, tmp_path, make_cfg, origin_cl
         hashing.use_part_hasher(None)
 
 
-@pytest.mark.parametrize("jobs", [1, 2])
-def test_stream_verify_auto_uses_the_device_when_jobs_share_the_worker(run, tmp_path, make_cfg,
-                                                                       origin_cls, jobs):
-    """``stream_verify_backend: auto`` with a hasher set up at worker start: one stream job
-    hashes its parts on the host (faster alone on an AVX-512 host), two at once send parts to
-    the device (more throughput and less worker CPU, profiles/r3_relayhash4/)."""
+@pytest.mark.parametrize("jobs,tail", [(1, 99), (2, 0), (1, 0)])
+def test_stream_verify_auto_uses_the_device_when_it_pays(run, tmp_path, make_cfg,
+                                                         origin_cls, jobs, tail):
+    """``stream_verify_backend: auto`` with a hasher ready: a job with no more parts than the
+    host-hashed tail stays on the host; jobs with parts beyond the tail - alone or two at
+    once - send those parts to the device (profiles/r3_relayhash4/, r3_tail2/)."""
     from downloader_amd.ops import hashing, native
 
     async def go():
@@ -573,7 +573,7 @@ def test_stream_verify_auto_uses_the_device_when_jobs_share_the_worker(run, tmp_
         # submitted together overlap for most of their parts
         w = _worker(make_cfg, ep, concurrency=2, s3={"part_size": 5 << 20},
                     download={"stream_verify_backend": "auto", "stream_gpu_min_pieces": 4,
-                              "stream_gpu_tail": 0, "gpu_prewarm": False,
+                              "stream_gpu_tail": tail, "gpu_prewarm": False,
                               "torrent_stream_parallel": 1})
         await w.start(health=False)
         for i in range(jobs):
@@ -585,9 +585,9 @@ def test_stream_verify_auto_uses_the_device_when_jobs_share_the_worker(run, tmp_
             assert s3.get("triton-staging", keys.object_key(f"au{jobs}-{i}", "m.mkv")) == data
         gpu_parts = sum(r.stats["torrent"]["gpu_parts"] for r in w.results)
         assert {r.stats["torrent"]["verify"] for r in w.results} == {"auto"}
-        if jobs == 1 and hashing.host_multibuffer():
+        if jobs == 1 and tail and hashing.host_multibuffer():
             assert gpu_parts == 0
-        if jobs == 2:
+        else:
             assert gpu_parts > 0
         assert native().relay_pool_stats()["in_use"] == 0
         await w.stop(); await s3.stop(); await origin.stop()
