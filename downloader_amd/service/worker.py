@@ -121,6 +121,11 @@ class Worker:
         self.pipe_bytes = limits.apply_pipe_size(d.pipe_kb, d.pipe_sharers)
         if d.gpu_prewarm and d.stream_verify_backend == "gpu" and d.stream_gpu_pending > 0:
             await self._prewarm_part_hasher()
+        elif d.gpu_prewarm and d.stream_verify_backend == "auto" and d.stream_gpu_pending > 0:
+            # set the PartHasher up in the background (executor thread): the first big
+            # webseed torrent then finds it ready instead of paying HIP init in its first parts
+            from ..torrent.stream import _start_gpu_init
+            _start_gpu_init(d.stream_gpu_min_pieces)
         if d.gpu_prewarm and d.verify_backend != "cpu":
             from ..ops import hashing
             # auto never picks the GPU on a host with the multi-buffer SHA-1: no HIP init
