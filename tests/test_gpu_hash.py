@@ -290,3 +290,52 @@ def test_stream_torrent_with_gpu_relay_hashing(run, tmp_path, make_cfg, origin_c
         assert st["host_fallbacks"] == 0 and not st["device_broken"]
         await w.stop(); await origin.stop(); await s3.stop()
     run(go(), timeout=120)
+
+
+def test_stream_torrent_auto_sets_the_device_up_lazily(run, tmp_path, make_cfg, origin_cls):
+    """The default ``stream_verify_backend: auto`` on a HIP box: the worker starts the
+    PartHasher on an executor thread (gpu_prewarm), a job with parts beyond the host-hashed
+    tail sends them to the gfx950 kernel once it is ready, and the object is byte-exact."""
+    import asyncio
+
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.ops import hashing
+    from downloader_amd.s3.fake_server import FakeS3
+    from downloader_amd.service.worker import Worker
+    from downloader_amd.torrent.metainfo import make_torrent
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Movie"
+        src.mkdir(parents=True)
+        data = os.urandom(40 * (1 << 20) + 999)
+        (src / "m.mkv").write_bytes(data)
+        origin.blobs["/ws/Movie/m.mkv"] = data
+        origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
+                                                    url_list=[origin.url("/ws/")])
+        cfg = make_cfg(ep, s3={"part_size": 5 << 20},
+                       download={"torrent_enable_dht": False, "stream_gpu_min_pieces": 4,
+                                 "stream_gpu_tail": 2, "torrent_stream_parallel": 2})
+        assert cfg.download.stream_verify_backend == "auto" and cfg.download.gpu_prewarm
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        for _ in range(1500):                      # the background set-up (HIP init)
+            if hashing._part_hasher is not None:
+                break
+            await asyncio.sleep(0.02)
+        assert hashing._part_hasher is not None
+        await w.submit(api.make_download("ga", "http", origin.url("/t/m.torrent")))
+        for _ in range(3000):
+            if w.results:
+                break
+            await asyncio.sleep(0.02)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        t = r.stats["torrent"]
+        assert t["verify"] == "auto" and t["gpu_parts"] >= 1, t
+        assert s3.get("triton-staging", keys.object_key("ga", "m.mkv")) == data
+        await w.stop(); await origin.stop(); await s3.stop()
+    run(go(), timeout=120)
