@@ -258,6 +258,7 @@ class StreamStager:
         self._min_pieces = int(getattr(d, "stream_gpu_min_pieces", 8) or 8)
         # parts still queued below which the rest hash on the host
         self.gpu_tail = int(getattr(d, "stream_gpu_tail", 0) or 0)
+        self._n_parts = sum(1 for u in self.units if u.target is not None)
         from ..ops import hashing
         try:
             self._host_mb = hashing.host_multibuffer()
@@ -410,8 +411,7 @@ class StreamStager:
         4 on the MI355X box, steady reps: one job 26.3 - 28.0 GB/s at 6.5 - 6.6 worker CPU-s
         with the last 96 parts on the host vs 24.8 - 25.4 at 7.7 - 8.2 all on the host, two
         jobs 26.5 - 28.4 vs 23.7 - 25.5 at 13 - 14 vs 17 - 18 CPU-s (profiles/r3_tail2/)."""
-        return (not self._host_mb or _active_stagers >= 2
-                or sum(1 for u in self.units if u.target is not None) > self.gpu_tail)
+        return not self._host_mb or _active_stagers >= 2 or self._n_parts > self.gpu_tail
 
     def _gpu_sem(self) -> Optional[asyncio.Semaphore]:
         """The process-wide budget of parts awaiting GPU digests, once a hasher is ready
