@@ -129,7 +129,7 @@ def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
 _gpu_init_started = False
 
 
-def _start_gpu_init(min_pieces: int) -> None:
+def start_gpu_init(min_pieces: int) -> None:
     """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and 8 device
     slots take a moment; the event loop keeps relaying meanwhile). Once per process; a
     missing device or a failed init leaves every part on the host."""
@@ -319,7 +319,7 @@ class StreamStager:
         _active_stagers += 1
         _pool_want[id(self)] = self.parallel
         if self.verify_mode == "auto" and self._gpu_wanted():
-            _start_gpu_init(self._min_pieces)
+            start_gpu_init(self._min_pieces)
         _size_pool()
         try:
             for t in self.targets:
@@ -415,7 +415,7 @@ class StreamStager:
 
     def _gpu_sem(self) -> Optional[asyncio.Semaphore]:
         """The process-wide budget of parts awaiting GPU digests, once a hasher is ready
-        (``gpu``: set up in __init__; ``auto``: by ``_start_gpu_init``); None = host only."""
+        (``gpu``: set up in __init__; ``auto``: by ``start_gpu_init``); None = host only."""
         if self._gpu_slots is None and self.gpu_pending:
             from ..ops import hashing
             if hashing._part_hasher is not None:
