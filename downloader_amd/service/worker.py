@@ -121,11 +121,8 @@ class Worker:
         self.pipe_bytes = limits.apply_pipe_size(d.pipe_kb, d.pipe_sharers)
         if d.gpu_prewarm and d.stream_verify_backend == "gpu" and d.stream_gpu_pending > 0:
             await self._prewarm_part_hasher()
-        elif d.gpu_prewarm and d.stream_verify_backend == "auto" and d.stream_gpu_pending > 0:
-            # set the PartHasher up in the background (executor thread): the first big
-            # webseed torrent then finds it ready instead of paying HIP init in its first parts
-            from ..torrent.stream import start_gpu_init
-            start_gpu_init(d.stream_gpu_min_pieces)
+        # (auto sets the PartHasher up on an executor thread when a job first wants it - a
+        # worker that never stages a big webseed torrent never initialises HIP)
         if d.gpu_prewarm and d.verify_backend != "cpu":
             from ..ops import hashing
             # auto never picks the GPU on a host with the multi-buffer SHA-1: no HIP init
@@ -141,7 +138,7 @@ class Worker:
     async def _prewarm_part_hasher(self) -> None:
         """stream_verify_backend gpu: set up the gfx950 PartHasher now (HIP init and device
         slots, off the event loop) instead of inside the first job. (``auto`` starts the same
-        set-up in the background instead: torrent.stream.start_gpu_init.)"""
+        set-up in the background when a job first wants it: torrent.stream.start_gpu_init.)"""
         from ..ops import gpu_available, hashing
         d = self.cfg.download
         loop = asyncio.get_running_loop()

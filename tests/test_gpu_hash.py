@@ -293,9 +293,10 @@ def test_stream_torrent_with_gpu_relay_hashing(run, tmp_path, make_cfg, origin_c
 
 
 def test_stream_torrent_auto_sets_the_device_up_lazily(run, tmp_path, make_cfg, origin_cls):
-    """The default ``stream_verify_backend: auto`` on a HIP box: the worker starts the
-    PartHasher on an executor thread (gpu_prewarm), a job with parts beyond the host-hashed
-    tail sends them to the gfx950 kernel once it is ready, and the object is byte-exact."""
+    """The default ``stream_verify_backend: auto`` on a HIP box: the first job with parts
+    beyond the host-hashed tail starts the PartHasher on an executor thread (its first parts
+    hash on the host meanwhile); the next such job sends its parts to the gfx950 kernel, and
+    the objects are byte-exact."""
     import asyncio
 
     from downloader_amd.broker.memory import MemoryBroker
@@ -319,23 +320,28 @@ def test_stream_torrent_auto_sets_the_device_up_lazily(run, tmp_path, make_cfg, 
         cfg = make_cfg(ep, s3={"part_size": 5 << 20},
                        download={"torrent_enable_dht": False, "stream_gpu_min_pieces": 4,
                                  "stream_gpu_tail": 2, "torrent_stream_parallel": 2})
-        assert cfg.download.stream_verify_backend == "auto" and cfg.download.gpu_prewarm
+        assert cfg.download.stream_verify_backend == "auto"
         w = Worker(cfg, broker=MemoryBroker())
         await w.start(health=False)
-        for _ in range(1500):                      # the background set-up (HIP init)
+
+        async def job(jid: str):
+            n = len(w.results)
+            await w.submit(api.make_download(jid, "http", origin.url("/t/m.torrent")))
+            for _ in range(3000):
+                if len(w.results) > n:
+                    break
+                await asyncio.sleep(0.02)
+            r = w.results[-1]
+            assert r.outcome == "staged", r
+            assert s3.get("triton-staging", keys.object_key(jid, "m.mkv")) == data
+            return r.stats["torrent"]
+        await job("ga1")                           # starts the set-up (HIP init)
+        for _ in range(1500):
             if hashing._part_hasher is not None:
                 break
             await asyncio.sleep(0.02)
         assert hashing._part_hasher is not None
-        await w.submit(api.make_download("ga", "http", origin.url("/t/m.torrent")))
-        for _ in range(3000):
-            if w.results:
-                break
-            await asyncio.sleep(0.02)
-        r = w.results[0]
-        assert r.outcome == "staged", r
-        t = r.stats["torrent"]
+        t = await job("ga2")
         assert t["verify"] == "auto" and t["gpu_parts"] >= 1, t
-        assert s3.get("triton-staging", keys.object_key("ga", "m.mkv")) == data
         await w.stop(); await origin.stop(); await s3.stop()
     run(go(), timeout=120)
