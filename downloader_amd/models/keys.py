@@ -13,6 +13,7 @@ reproduced exactly here.
 from __future__ import annotations
 
 import base64
+import hashlib
 import mimetypes
 import os
 
@@ -63,6 +64,13 @@ def object_key(media_id: str, file_path: str) -> str:
 
 def done_key(media_id: str) -> str:
     return node_join(media_id, "original/", "done")
+
+
+def relay_journal_key(media_id: str, file_path: str) -> str:
+    """Resume journal of a streamed relay (``S3Client.relay_object(journal=)``): outside
+    ``<id>/original/`` so nothing that lists the staged originals ever sees it."""
+    return node_join(media_id, ".stager/", "relay-" + hashlib.sha1(
+        os.path.basename(file_path).encode("utf-8")).hexdigest() + ".json")
 
 
 # mime-db types of the media the selector keeps (lib/process.js:15-20): minio-js 7's

@@ -23,6 +23,7 @@ Differences by design:
 from __future__ import annotations
 
 import asyncio
+import json
 import os
 import random
 import re
@@ -149,6 +150,7 @@ class S3Client:
         self.max_inflight_parts = max(1, max_inflight_parts)
         self.unsigned_payload = unsigned_payload
         self.retries = retries
+        self.resumed_parts = 0      # relayed parts a later attempt found already uploaded
 
     @classmethod
     def from_config(cls, s3cfg, transports: Optional[TransportSet] = None) -> "S3Client":
@@ -510,7 +512,8 @@ class S3Client:
                            progress: Optional[Progress] = None,
                            concurrency: Optional[int] = None, src_proxy=None,
                            content_type: str = "", ranges: bool = True,
-                           validator: str = "") -> str:
+                           validator: str = "", journal: str = "",
+                           keep_on_error: bool = False, stats: Optional[dict] = None) -> str:
         """Stage ``src_url`` (``size`` bytes) straight into S3: each multipart part is one Range
         GET relayed socket->socket into one UploadPart; objects up to ``multipart_threshold``
         go in one relayed PUT. ``src_proxy``: the source-fetch proxy policy
@@ -524,7 +527,15 @@ class S3Client:
 
         Over TLS one relay is bound by one thread decrypting and re-encrypting every byte
         (~2 - 3 GB/s), so with ``split_tls_relays`` an object of more than 6 MiB that would go
-        in one PUT is cut into up to ``max_inflight_parts`` parts relayed in parallel."""
+        in one PUT is cut into up to ``max_inflight_parts`` parts relayed in parallel.
+
+        ``journal`` (a key in ``bucket``; multipart only, needs ``validator``): resume across
+        attempts (SURVEY §5.4 "resumable multipart"). The upload id, the source version and
+        the part plan are recorded there; a later call for the same object and the same
+        version relays only the parts the upload does not hold yet (ListParts: same number,
+        same size). ``keep_on_error``: a failure leaves the upload and its journal for that
+        next attempt instead of aborting (a changed source always aborts). ``stats`` gets
+        ``resumed_parts`` when parts were reused."""
         tls = src_url.startswith("https://") or self.scheme == "https"
         crc = self.want_checksum(relay=True, tls=tls)
         if size <= self.multipart_threshold:
@@ -536,9 +547,19 @@ class S3Client:
             parts = self.plan_parts(size, part_size=-(-ps // (1 << 20)) << 20)
         else:
             parts = self.plan_parts(size)
-        upload_id = await self.create_multipart_upload(bucket, key, content_type)
+        journal = journal if validator else ""
+        upload_id, etags = (await self._resume_relay(bucket, key, journal, validator, size,
+                                                     parts) if journal else (None, {}))
+        if upload_id is None:
+            upload_id = await self.create_multipart_upload(bucket, key, content_type)
+            if journal:
+                await self.put_object(bucket, journal, json.dumps(
+                    {"key": key, "upload_id": upload_id, "validator": validator, "size": size,
+                     "parts": [[n, o, ln] for n, o, ln in parts]}), "application/json")
+        reused = len(etags)
+        if progress is not None and reused:
+            progress.add(sum(ln for n, _, ln in parts if n in etags))
         sem = asyncio.Semaphore(concurrency or self.max_inflight_parts)
-        etags: Dict[int, str] = {}
 
         async def one(num: int, off: int, ln: int) -> None:
             async with sem:
@@ -547,15 +568,56 @@ class S3Client:
                     off, ln, False, progress, src_proxy=src_proxy, checksum=crc,
                     validator=validator)
         try:
-            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts))
-            return await self.complete_multipart_upload(bucket, key, upload_id,
+            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts if n not in etags))
+            etag = await self.complete_multipart_upload(bucket, key, upload_id,
                                                         [(n, etags[n]) for n, _, _ in parts])
-        except BaseException:
+        except BaseException as e:
+            if not (keep_on_error and journal and isinstance(e, Exception)
+                    and not isinstance(e, SourceChanged)):
+                try:
+                    await asyncio.shield(self.abort_multipart_upload(bucket, key, upload_id))
+                    if journal:
+                        await asyncio.shield(self.delete_object(bucket, journal))
+                except Exception:
+                    pass
+            raise
+        self.resumed_parts += reused
+        if stats is not None and reused:
+            stats["resumed_parts"] = reused
+        if journal:
             try:
-                await asyncio.shield(self.abort_multipart_upload(bucket, key, upload_id))
+                await self.delete_object(bucket, journal)
             except Exception:
                 pass
-            raise
+        return etag
+
+    async def _resume_relay(self, bucket: str, key: str, journal: str, validator: str,
+                            size: int, parts) -> Tuple[Optional[str], Dict[int, str]]:
+        """(upload id, {part: etag} already held) from a previous attempt's journal, or
+        (None, {}) to start fresh - the journal missing, for another object, version, size or
+        part plan, or its upload gone. Parts count only with the planned size and an ETag."""
+        try:
+            j = json.loads(await self.get_object(bucket, journal))
+        except (S3Error, ValueError):
+            return None, {}
+        plan = [[n, o, ln] for n, o, ln in parts]
+        if not isinstance(j, dict) or not j.get("upload_id"):
+            return None, {}
+        if j.get("key") != key or j.get("validator") != validator or j.get("size") != size \
+                or j.get("parts") != plan:
+            # another version (or plan): its parts are useless - do not leave them behind
+            try:
+                await self.abort_multipart_upload(bucket, j.get("key") or key, j["upload_id"])
+            except Exception:
+                pass
+            return None, {}
+        try:
+            held = await self.list_parts(bucket, key, j["upload_id"])
+        except S3Error:
+            return None, {}
+        want = {n: ln for n, _, ln in parts}
+        return j["upload_id"], {n: e.strip('"') for n, e, sz in held
+                                if want.get(n) == sz and e}
 
     async def copy_object(self, src_bucket: str, src_key: str, bucket: str, key: str, size: int,
                           content_type: str = "", concurrency: Optional[int] = None) -> str:

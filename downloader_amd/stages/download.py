@@ -144,6 +144,11 @@ class DownloadStage(Stage):
         await ensure_staging_bucket(self.sv)
         key = keys.object_key(job.id, name)
         job.logger.info("streaming http source straight to staging", key=key, size=size)
+        # big objects: a resume journal, so the job's retry relays only the missing parts
+        rmin = int(getattr(self.cfg.s3, "relay_resume_min_bytes", 0) or 0)
+        resumable = bool(rmin) and size >= rmin and size > s3.multipart_threshold
+        journal = keys.relay_journal_key(job.id, name) if resumable else ""
+        keep = resumable and job.attempt < self.cfg.broker.max_retries
         for attempt in range(SOURCE_RESTARTS + 1):
             try:
                 # every part GET pinned to the probed version: a mid-job change aborts the
@@ -151,7 +156,8 @@ class DownloadStage(Stage):
                 await s3.relay_object(self.cfg.s3.bucket, key, final, size, Progress(),
                                       src_proxy=self.proxy,
                                       content_type=media_type(self.cfg, name), ranges=ranges,
-                                      validator=validator)
+                                      validator=validator, journal=journal,
+                                      keep_on_error=keep, stats=job.stats)
                 break
             except SourceChanged as e:
                 if attempt == SOURCE_RESTARTS:

@@ -84,6 +84,10 @@ class S3Config(BaseModel):
     request_timeout_s: float = 300.0            # socket idle timeout of one request
     # retries of a retryable S3 error (5xx, SlowDown, resets) with jittered backoff
     retries: int = 3
+    # streamed relays of objects at least this large keep a resume journal (<id>/.stager/):
+    # a failed attempt leaves its multipart upload for the job's retry, which relays only the
+    # parts not uploaded yet from the same (pinned) source version; 0 = off
+    relay_resume_min_bytes: int = 1 << 30
 
 
 class BrokerConfig(BaseModel):

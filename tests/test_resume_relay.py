@@ -1,0 +1,130 @@
+"""Resumable streamed relays (SURVEY §5.4 "resumable multipart (list parts on retry)"): a
+relayed multipart upload that fails part-way keeps its upload and a journal; the retry of the
+same object and source version relays only the parts the upload does not hold yet."""
+from __future__ import annotations
+
+import os
+
+import pytest
+
+from downloader_amd.s3.client import S3Client, S3Error
+from downloader_amd.s3.fake_server import FakeS3
+from downloader_amd.net.http import TransportError
+
+CREDS = ("minioadmin", "minioadmin")
+MiB = 1 << 20
+
+
+def _rng(off: int, ln: int) -> str:
+    return f"bytes={off}-{off + ln - 1}"
+
+
+async def _setup(origin_cls, size=24 * MiB + 77):
+    s3 = FakeS3()
+    ep = await s3.start()
+    origin = await origin_cls().start()
+    blob = os.urandom(size)
+    origin.blobs["/big.mkv"] = blob
+    c = S3Client(ep, *CREDS, part_size=5 * MiB, multipart_threshold=6 * MiB, retries=1,
+                 max_inflight_parts=2)
+    await c.ensure_bucket("b")
+    return s3, origin, c, blob
+
+
+def test_failed_relay_resumes_from_the_journal(run, origin_cls):
+    async def go():
+        s3, origin, c, blob = await _setup(origin_cls)
+        parts = c.plan_parts(len(blob))
+        n, off, ln = parts[-1]
+        origin.fail_ranges[_rng(off, ln)] = 99             # the last part's GET keeps failing
+        v = origin._etag("/big.mkv", blob)
+        with pytest.raises((TransportError, S3Error)):
+            await c.relay_object("b", "o", origin.url("/big.mkv"), len(blob), validator=v,
+                                 journal="j/o.json", keep_on_error=True)
+        assert s3.get("b", "o") is None and s3.get("b", "j/o.json") is not None
+        served = len(origin.requests)
+        origin.fail_ranges.clear()
+        st: dict = {}
+        await c.relay_object("b", "o", origin.url("/big.mkv"), len(blob), validator=v,
+                             journal="j/o.json", keep_on_error=True, stats=st)
+        assert s3.get("b", "o") == blob
+        assert st["resumed_parts"] == len(parts) - 1           # only the failed part again
+        assert len(origin.requests) - served == 1
+        assert s3.get("b", "j/o.json") is None                  # journal gone with the upload
+        assert await c.find_upload("b", "o") is None
+        await c.close(); await origin.stop(); await s3.stop()
+    run(go())
+
+
+def test_changed_version_or_no_keep_starts_over_and_cleans_up(run, origin_cls):
+    async def go():
+        s3, origin, c, blob = await _setup(origin_cls)
+        parts = c.plan_parts(len(blob))
+        n, off, ln = parts[-1]
+        origin.fail_ranges[_rng(off, ln)] = 99
+        with pytest.raises((TransportError, S3Error)):
+            await c.relay_object("b", "o", origin.url("/big.mkv"), len(blob),
+                                 validator=origin._etag("/big.mkv", blob),
+                                 journal="j/o.json", keep_on_error=True)
+        old = await c.find_upload("b", "o")
+        assert old is not None
+        origin.fail_ranges.clear()
+        # the origin moved on to another version: nothing of the old upload is reused, and
+        # the old upload is aborted rather than left behind
+        blob = os.urandom(len(blob))
+        origin.blobs["/big.mkv"] = blob
+        st: dict = {}
+        await c.relay_object("b", "o", origin.url("/big.mkv"), len(blob),
+                             validator=origin._etag("/big.mkv", blob),
+                             journal="j/o.json", keep_on_error=True, stats=st)
+        assert s3.get("b", "o") == blob and "resumed_parts" not in st
+        assert await c.find_upload("b", "o") is None
+        # keep_on_error=False (the job's last attempt): a failure aborts and drops the journal
+        origin.fail_ranges[_rng(off, ln)] = 99
+        with pytest.raises((TransportError, S3Error)):
+            await c.relay_object("b", "o2", origin.url("/big.mkv"), len(blob),
+                                 validator=origin._etag("/big.mkv", blob),
+                                 journal="j/o2.json", keep_on_error=False)
+        assert await c.find_upload("b", "o2") is None and s3.get("b", "j/o2.json") is None
+        await c.close(); await origin.stop(); await s3.stop()
+    run(go())
+
+
+def test_worker_retry_resumes_a_streamed_http_object(run, tmp_path, make_cfg, origin_cls):
+    """End to end: the job's first attempt fails on one part, the broker-held retry resumes
+    the upload (only that part is relayed again) and the staged object is byte-exact."""
+    import asyncio
+
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.service.worker import Worker
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(24 * MiB + 5)
+        origin.blobs["/movie.mkv"] = blob
+        cfg = make_cfg(ep, s3={"part_size": 5 * MiB, "multipart_threshold": 6 * MiB,
+                               "retries": 0, "relay_resume_min_bytes": 10 * MiB},
+                       broker={"retry_backoff_s": 0.05})
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        c = w.s3
+        parts = c.plan_parts(len(blob))
+        n, off, ln = parts[2]
+        origin.fail_ranges[_rng(off, ln)] = 1                  # one failure of part 3
+        await w.submit(api.make_download("rs", "http", origin.url("/movie.mkv")))
+        for _ in range(1500):
+            if any(r.outcome == "staged" for r in w.results):
+                break
+            await asyncio.sleep(0.02)
+        staged = [r for r in w.results if r.outcome == "staged"]
+        assert staged, w.results
+        assert s3.get("triton-staging", keys.object_key("rs", "movie.mkv")) == blob
+        assert staged[0].stats.get("resumed_parts", 0) >= 1
+        assert s3.get("triton-staging", keys.relay_journal_key("rs", "movie.mkv")) is None
+        assert not [k for k in s3.objects("triton-staging") if "/original/" in k
+                    and k != keys.object_key("rs", "movie.mkv") and not k.endswith("/done")]
+        await w.stop(); await origin.stop(); await s3.stop()
+    run(go())
