@@ -583,7 +583,7 @@ class S3Client:
             raise
         self.resumed_parts += reused
         if stats is not None and reused:
-            stats["resumed_parts"] = reused
+            stats["resumed_parts"] = stats.get("resumed_parts", 0) + reused
         if journal:
             try:
                 await self.delete_object(bucket, journal)

@@ -261,6 +261,11 @@ class DownloadStage(Stage):
                 and src.access_key == s3.access_key and d.bucket_server_copy)
         job.stats["bucket_server_copy"] = same
 
+        # big objects keep a resume journal: the job's retry relays only their missing parts
+        rmin = int(getattr(self.cfg.s3, "relay_resume_min_bytes", 0) or 0)
+        keep = job.attempt < self.cfg.broker.max_retries
+        rstats: Dict[str, int] = {}
+
         async def one(key: str, f: str) -> None:
             it = by_path[f]
             async with sem:
@@ -268,6 +273,7 @@ class DownloadStage(Stage):
                     await s3.copy_object(src.bucket, it.name, self.cfg.s3.bucket, key, it.size,
                                          content_type=media_type(self.cfg, f))
                     return
+                resumable = bool(rmin) and it.size >= rmin and it.size > s3.multipart_threshold
                 await s3.relay_object(self.cfg.s3.bucket, key,
                                       # every Range part is its own request: the URL must
                                       # outlive the slowest object's last part
@@ -275,8 +281,13 @@ class DownloadStage(Stage):
                                       it.size, prog,
                                       content_type=media_type(self.cfg, f),
                                       # parts pinned to the listed version (If-Match)
-                                      validator=f'"{it.etag}"' if it.etag else "")
+                                      validator=f'"{it.etag}"' if it.etag else "",
+                                      journal=keys.relay_journal_key(job.id, f)
+                                      if resumable else "",
+                                      keep_on_error=resumable and keep, stats=rstats)
         await asyncio.gather(*(one(k, f) for k, f in owner.items()))
+        if rstats:
+            job.stats["resumed_parts"] = rstats["resumed_parts"]
         staged = sum(by_path[f].size for f in owner.values())
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + staged
         job.stats.setdefault("streamed", []).extend(
