@@ -28,7 +28,7 @@ import os
 import random
 import re
 import xml.etree.ElementTree as ET
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import quote
 
@@ -75,6 +75,7 @@ class ObjectInfo:
     size: int
     etag: str = ""
     last_modified: str = ""
+    meta: Dict[str, str] = field(default_factory=dict)   # x-amz-meta-<k> -> value (HEAD)
 
 
 def _strip(tag: str) -> str:
@@ -317,7 +318,8 @@ class S3Client:
         if r.status == 404:
             raise S3Error("NoSuchKey", "", 404, key, bucket)
         return ObjectInfo(key, int(r.header("content-length", "0") or 0),
-                          (r.header("etag") or "").strip('"'), r.header("last-modified") or "")
+                          (r.header("etag") or "").strip('"'), r.header("last-modified") or "",
+                          {k[11:]: v for k, v in r.headers if k.startswith("x-amz-meta-")})
 
     async def object_exists(self, bucket: str, key: str) -> bool:
         try:
@@ -457,7 +459,7 @@ class S3Client:
                          src_url: str, offset: int, length: int, whole: bool,
                          progress: Optional[Progress], split=None, src_proxy=None,
                          content_type: str = "", checksum: bool = False, validator: str = "",
-                         gpu: bool = False):
+                         gpu: bool = False, meta: Optional[Dict[str, str]] = None):
         """One relayed PUT (object or part) with retries; returns the ETag, or with ``split``
         (see ``NativeTransport.relay``) ``(etag, {"digests", "head", "tail"})``.
         ``checksum``: aws-chunked body with a trailing CRC32C of the relayed bytes.
@@ -466,6 +468,7 @@ class S3Client:
         src_hdrs = [] if whole else [("Range", f"bytes={offset}-{offset + length - 1}")]
         src_hdrs += pin_headers(validator, not whole)
         put_hdrs: Dict[str, str] = {"content-type": content_type} if content_type else {}
+        put_hdrs.update({f"x-amz-meta-{k}": v for k, v in (meta or {}).items()})
         phash = sigv4.UNSIGNED
         if checksum:
             put_hdrs.update({"content-encoding": "aws-chunked",
@@ -513,7 +516,8 @@ class S3Client:
                            concurrency: Optional[int] = None, src_proxy=None,
                            content_type: str = "", ranges: bool = True,
                            validator: str = "", journal: str = "",
-                           keep_on_error: bool = False, stats: Optional[dict] = None) -> str:
+                           keep_on_error: bool = False, stats: Optional[dict] = None,
+                           meta: Optional[Dict[str, str]] = None) -> str:
         """Stage ``src_url`` (``size`` bytes) straight into S3: each multipart part is one Range
         GET relayed socket->socket into one UploadPart; objects up to ``multipart_threshold``
         go in one relayed PUT. ``src_proxy``: the source-fetch proxy policy
@@ -535,14 +539,15 @@ class S3Client:
         version relays only the parts the upload does not hold yet (ListParts: same number,
         same size). ``keep_on_error``: a failure leaves the upload and its journal for that
         next attempt instead of aborting (a changed source always aborts). ``stats`` gets
-        ``resumed_parts`` when parts were reused."""
+        ``resumed_parts`` when parts were reused. ``meta``: user metadata (x-amz-meta-*) of
+        the staged object."""
         tls = src_url.startswith("https://") or self.scheme == "https"
         crc = self.want_checksum(relay=True, tls=tls)
         if size <= self.multipart_threshold:
             if not (tls and self.split_tls_relays and ranges and size > MIN_PART + (1 << 20)):
                 return await self._relay_put(bucket, key, [], src_url, 0, size, True, progress,
                                              src_proxy=src_proxy, content_type=content_type,
-                                             checksum=crc, validator=validator)
+                                             checksum=crc, validator=validator, meta=meta)
             ps = -(-size // max(1, self.max_inflight_parts))
             parts = self.plan_parts(size, part_size=-(-ps // (1 << 20)) << 20)
         else:
@@ -551,7 +556,7 @@ class S3Client:
         upload_id, etags = (await self._resume_relay(bucket, key, journal, validator, size,
                                                      parts) if journal else (None, {}))
         if upload_id is None:
-            upload_id = await self.create_multipart_upload(bucket, key, content_type)
+            upload_id = await self.create_multipart_upload(bucket, key, content_type, meta)
             if journal:
                 await self.put_object(bucket, journal, json.dumps(
                     {"key": key, "upload_id": upload_id, "validator": validator, "size": size,
@@ -683,9 +688,12 @@ class S3Client:
                                      checksum=self.want_checksum(relay=True, tls=tls,
                                                                  hashed=True), gpu=gpu)
 
-    async def create_multipart_upload(self, bucket: str, key: str, content_type: str = "") -> str:
+    async def create_multipart_upload(self, bucket: str, key: str, content_type: str = "",
+                                      meta: Optional[Dict[str, str]] = None) -> str:
+        hdrs = {"content-type": content_type} if content_type else {}
+        hdrs.update({f"x-amz-meta-{k}": v for k, v in (meta or {}).items()})
         r = await self._request("POST", bucket, key, query=[("uploads", "")],
-                                headers={"content-type": content_type} if content_type else None)
+                                headers=hdrs or None)
         return _text(ET.fromstring(r.body), "UploadId")
 
     async def upload_part(self, bucket: str, key: str, upload_id: str, num: int, body,

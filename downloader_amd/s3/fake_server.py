@@ -41,6 +41,7 @@ class StoredObject:
     etag: str
     mtime: float = field(default_factory=time.time)
     content_type: str = "application/octet-stream"
+    meta: Dict[str, str] = field(default_factory=dict)     # x-amz-meta-* (user metadata)
 
 
 @dataclass
@@ -49,6 +50,11 @@ class Upload:
     content_type: str = "application/octet-stream"
     parts: Dict[int, Tuple[bytes, str]] = field(default_factory=dict)
     initiated: float = field(default_factory=time.time)
+    meta: Dict[str, str] = field(default_factory=dict)
+
+
+def _user_meta(headers) -> Dict[str, str]:
+    return {k.lower(): v for k, v in headers.items() if k.lower().startswith("x-amz-meta-")}
 
 
 @dataclass
@@ -446,7 +452,8 @@ class FakeS3:
         m = req.method
         if m == "POST" and "uploads" in q:
             uid = secrets.token_hex(16)
-            ups[uid] = Upload(key, req.headers.get("Content-Type", "application/octet-stream"))
+            ups[uid] = Upload(key, req.headers.get("Content-Type", "application/octet-stream"),
+                              meta=_user_meta(req.headers))
             return _xml(f'<InitiateMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
                         f"<Key>{escape(key)}</Key><UploadId>{uid}</UploadId>"
                         "</InitiateMultipartUploadResult>")
@@ -510,7 +517,7 @@ class FakeS3:
                     md5s += bytes.fromhex(got[1])
                 data = b"".join(datas)
                 etag = f"{hashlib.md5(md5s).hexdigest()}-{len(want)}"
-                objs[key] = StoredObject(data, etag, content_type=up.content_type)
+                objs[key] = StoredObject(data, etag, content_type=up.content_type, meta=up.meta)
                 del ups[q["uploadId"]]
                 return _xml(f'<CompleteMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}'
                             f"</Bucket><Key>{escape(key)}</Key><ETag>&quot;{etag}&quot;</ETag>"
@@ -528,7 +535,7 @@ class FakeS3:
         if m == "PUT":
             etag = hashlib.md5(body).hexdigest()
             objs[key] = StoredObject(body, etag, content_type=req.headers.get(
-                "Content-Type", "application/octet-stream"))
+                "Content-Type", "application/octet-stream"), meta=_user_meta(req.headers))
             return web.Response(status=200, headers={"ETag": f'"{etag}"'})
         o = objs.get(key)
         if m == "DELETE":
@@ -539,7 +546,8 @@ class FakeS3:
                 return web.Response(status=404)
             return _err(404, "NoSuchKey", "The specified key does not exist.", key)
         hdrs = {"ETag": f'"{o.etag}"', "Last-Modified": time.strftime(
-            "%a, %d %b %Y %H:%M:%S GMT", time.gmtime(o.mtime)), "Accept-Ranges": "bytes"}
+            "%a, %d %b %Y %H:%M:%S GMT", time.gmtime(o.mtime)), "Accept-Ranges": "bytes",
+                **o.meta}
         im = req.headers.get("If-Match")
         if im and im != "*" and im.strip('"') != o.etag:        # S3 conditional GET / HEAD
             return _err(412, "PreconditionFailed", "At least one of the pre-conditions you "

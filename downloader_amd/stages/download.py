@@ -8,8 +8,9 @@ emit progress 50 (:272) and return ``{'path': dir}``.
 from __future__ import annotations
 
 import asyncio
+import hashlib
 import os
-from typing import Any, Awaitable, Callable, Dict
+from typing import Any, Awaitable, Callable, Dict, List
 
 from ..fetch import bucket as bucket_src
 from ..fetch import http as http_src
@@ -17,6 +18,7 @@ from ..fetch import local as file_src
 from ..models import api, keys
 from ..net.http import Progress, SourceChanged
 from ..net.proxy import ProxyConfig
+from ..s3.client import S3Error
 from ..utils.log import redact_url
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket, media_type)
@@ -266,9 +268,23 @@ class DownloadStage(Stage):
         keep = job.attempt < self.cfg.broker.max_retries
         rstats: Dict[str, int] = {}
 
+        reused: List[str] = []
+
         async def one(key: str, f: str) -> None:
             it = by_path[f]
+            # the staged object records which source version it holds: a retry of the job
+            # skips objects an earlier attempt already staged from the same version
+            tag = hashlib.sha1(f"{src.bucket}/{it.name}@{it.etag}".encode()).hexdigest() \
+                if it.etag else ""
             async with sem:
+                if tag and job.attempt > 0 and not same:
+                    try:
+                        info = await s3.head_object(self.cfg.s3.bucket, key)
+                        if info.size == it.size and info.meta.get("stager-source") == tag:
+                            reused.append(f)
+                            return
+                    except S3Error:
+                        pass
                 if same:
                     await s3.copy_object(src.bucket, it.name, self.cfg.s3.bucket, key, it.size,
                                          content_type=media_type(self.cfg, f))
@@ -284,10 +300,13 @@ class DownloadStage(Stage):
                                       validator=f'"{it.etag}"' if it.etag else "",
                                       journal=keys.relay_journal_key(job.id, f)
                                       if resumable else "",
-                                      keep_on_error=resumable and keep, stats=rstats)
+                                      keep_on_error=resumable and keep, stats=rstats,
+                                      meta={"stager-source": tag} if tag else None)
         await asyncio.gather(*(one(k, f) for k, f in owner.items()))
         if rstats:
             job.stats["resumed_parts"] = rstats["resumed_parts"]
+        if reused:
+            job.stats["reused_objects"] = len(reused)
         staged = sum(by_path[f].size for f in owner.values())
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + staged
         job.stats.setdefault("streamed", []).extend(

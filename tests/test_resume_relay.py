@@ -128,3 +128,45 @@ def test_worker_retry_resumes_a_streamed_http_object(run, tmp_path, make_cfg, or
                     and k != keys.object_key("rs", "movie.mkv") and not k.endswith("/done")]
         await w.stop(); await origin.stop(); await s3.stop()
     run(go())
+
+
+def test_bucket_retry_skips_objects_already_staged(run, make_cfg, origin_cls):
+    """A bucket:// season whose first attempt fails on one object: the retry HEADs the
+    staged keys and skips the objects an earlier attempt staged from the same source version
+    (x-amz-meta-stager-source), relaying only the rest; a changed source object is redone."""
+    import asyncio
+
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.service.worker import Worker
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        s3.buckets["src"] = {}
+        eps = {f"e{i}.mkv": os.urandom((2 << 20) + i) for i in range(1, 5)}
+        for n, d in eps.items():
+            s3.put("src", f"lib/Show/Season 1/{n}", d)
+        cfg = make_cfg(ep, download={"bucket_secure": False, "bucket_server_copy": False,
+                                     "bucket_concurrency": 1},
+                       s3={"retries": 0}, broker={"retry_backoff_s": 0.05})
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        # e3's source GET fails (503) once: attempt 1 stages e1 and e2 (objects one at a
+        # time), then fails; with S3 retries off the job itself is retried
+        from downloader_amd.s3.fake_server import FaultRule
+        s3.faults.add(FaultRule(method="GET", path_contains="e3.mkv", times=1))
+        uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,lib"
+        await w.submit(api.make_download("bk", "bucket", uri, "TV"))
+        for _ in range(1500):
+            if any(r.outcome == "staged" for r in w.results):
+                break
+            await asyncio.sleep(0.02)
+        staged = [r for r in w.results if r.outcome == "staged"]
+        assert staged, w.results
+        for n, d in eps.items():
+            assert s3.get("triton-staging", keys.object_key("bk", n)) == d
+        assert staged[0].stats.get("reused_objects", 0) >= 1
+        await w.stop(); await origin.stop(); await s3.stop()
+    run(go())
