@@ -15,6 +15,7 @@ from typing import List, Optional
 
 from ..models.keys import node_join
 from ..stages.jobdir import inside
+from ..utils.aio import gather_strict
 from ..utils.log import Logger, NullLogger
 
 
@@ -69,7 +70,7 @@ async def fetch_bucket(uri: str, download_dir: str, secure: bool = True, concurr
                 await client.fget_object(src.bucket, name, dst, progress=progress)
             out.append(dst)
 
-        await asyncio.gather(*(one(it.name) for it in items if it.name and not it.name.endswith("/")))
+        await gather_strict(*(one(it.name) for it in items if it.name and not it.name.endswith("/")))
         return out
     finally:
         await client.close()

@@ -24,6 +24,7 @@ from urllib.parse import urlsplit
 from ..net.http import FileSink, HttpError, Progress, SourceChanged, TransportSet, pin_headers
 from ..net.proxy import ProxyConfig
 from ..stages.select import node_extname
+from ..utils.aio import gather_strict
 from ..utils.log import Logger, NullLogger, redact_url
 
 
@@ -178,7 +179,7 @@ async def _download_once(t: TransportSet, url: str, path: str, streams: int, min
                 _save_journal(state_path, validator, size, done)
                 return r.written
 
-            task = asyncio.ensure_future(asyncio.gather(*(part(o, ln) for o, ln in todo)))
+            task = asyncio.ensure_future(gather_strict(*(part(o, ln) for o, ln in todo)))
             written = sum(await _guard(task, progress, min_rate, stall_window))
         else:
             have = os.fstat(fd).st_size if (resumable and ranges and size > 0 and not done) \

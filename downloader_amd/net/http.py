@@ -253,6 +253,7 @@ class NativeTransport(Transport):
         # close() can abort() the socket a blocked native transfer sits on
         self._inflight: Set[int] = set()
         self._slots: Dict[int, List[object]] = {}
+        self._aborted: Set[int] = set()     # slots whose request was cancelled
         self.connect_timeout = connect_timeout
         self.io_timeout = io_timeout
         self.max_idle = max_idle_per_host
@@ -349,6 +350,8 @@ class NativeTransport(Transport):
     def _track(self, slot: int, conn) -> None:
         with self._lock:
             self._slots.setdefault(slot, []).append(conn)
+            if slot in self._aborted:      # cancelled while this connection was being set up
+                conn.abort()
 
     def _untrack(self, slot: int, conn) -> None:
         """Before the owner releases or closes ``conn``: afterwards an abort must not reach it
@@ -359,9 +362,18 @@ class NativeTransport(Transport):
                 lst.remove(conn)
 
     def _abort_slot(self, slot: int) -> None:
+        """Cancel one request: shut its sockets down (a blocked recv / send / splice returns
+        at once) and make any connection it sets up later dead on arrival. Only this request
+        ends - a Progress shared with sibling requests (a job's parts) is not flagged, so a
+        fan-out that cancels its other parts can restart with the same counter."""
         with self._lock:   # under the lock: the owner cannot close the fd meanwhile
-            for c in self._slots.pop(slot, []):
+            self._aborted.add(slot)
+            for c in self._slots.get(slot, []):
                 c.abort()
+
+    def _slot_aborted(self, slot: int) -> bool:
+        with self._lock:
+            return slot in self._aborted
 
     def _do(self, method: str, host: str, port: int, host_hdr: str, path: str,
             headers: Headers, body, sink: Optional[FileSink], nprog,
@@ -385,7 +397,8 @@ class NativeTransport(Transport):
                 conn.close()
                 # A pooled keep-alive socket may have been closed by the peer: retry once on
                 # a fresh connection (the whole request is re-sent; bodies are re-readable).
-                if reused and attempt == 0 and not (nprog is not None and nprog.cancelled):
+                if reused and attempt == 0 and not (nprog is not None and nprog.cancelled) \
+                        and not self._slot_aborted(slot):
                     continue
                 raise TransportError(f"{method} {host}:{port}{path}: {e}") from e
             self._untrack(slot, conn)
@@ -419,8 +432,6 @@ class NativeTransport(Transport):
         try:
             return await asyncio.shield(fut)
         except asyncio.CancelledError:
-            if nprog is not None:
-                nprog.cancel()
             self._abort_slot(slot)
             await _drain(fut)
             raise
@@ -437,6 +448,7 @@ class NativeTransport(Transport):
         with self._lock:
             self._inflight.discard(slot)
             self._slots.pop(slot, None)
+            self._aborted.discard(slot)
 
     def _relay(self, src_url: str, src_headers: Headers, dst_url: str, dst_headers: Headers,
                length: int, nprog, slot: int = 0, split: Optional[Tuple[int, int, int]] = None,
@@ -526,8 +538,6 @@ class NativeTransport(Transport):
             try:
                 out = await asyncio.shield(fut)
             except asyncio.CancelledError:
-                if nprog is not None:
-                    nprog.cancel()
                 self._abort_slot(slot)
                 await _drain(fut)
                 self._forget_ticket(fut)

@@ -34,6 +34,7 @@ from urllib.parse import quote
 
 from ..net.http import (FileRange, FileSink, Progress, Response, SourceChanged,
                         TransportError, TransportSet, make_transports, pin_headers)
+from ..utils.aio import drain, gather_strict
 from ..utils.log import redact_url
 from . import sigv4
 
@@ -409,7 +410,7 @@ class S3Client:
                                                     FileRange(fd, off, ln), progress)
 
         try:
-            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts if n not in done))
+            await gather_strict(*(one(n, o, ln) for n, o, ln in parts if n not in done))
             return await self.complete_multipart_upload(
                 bucket, key, upload_id, [(n, etags[n]) for n, _, _ in parts])
         except BaseException:
@@ -566,19 +567,34 @@ class S3Client:
             progress.add(sum(ln for n, _, ln in parts if n in etags))
         sem = asyncio.Semaphore(concurrency or self.max_inflight_parts)
 
+        failed = False
+
         async def one(num: int, off: int, ln: int) -> None:
             async with sem:
+                if failed:
+                    return
                 etags[num] = await self._relay_put(
                     bucket, key, [("partNumber", str(num)), ("uploadId", upload_id)], src_url,
                     off, ln, False, progress, src_proxy=src_proxy, checksum=crc,
                     validator=validator)
+        tasks = [asyncio.ensure_future(one(n, o, ln)) for n, o, ln in parts if n not in etags]
         try:
-            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts if n not in etags))
+            await asyncio.gather(*tasks)
             etag = await self.complete_multipart_upload(bucket, key, upload_id,
                                                         [(n, etags[n]) for n, _, _ in parts])
         except BaseException as e:
-            if not (keep_on_error and journal and isinstance(e, Exception)
-                    and not isinstance(e, SourceChanged)):
+            failed = True
+            keep = (keep_on_error and journal and isinstance(e, Exception)
+                    and not isinstance(e, SourceChanged))
+            # gather() leaves the siblings of a failed part running. None may outlive this
+            # call (a part landing in an upload being aborted, or after the next attempt
+            # listed the parts): parts not begun are skipped; those in flight finish when
+            # the upload is kept (the next attempt reuses them), else they are cancelled.
+            if not keep:
+                for t in tasks:
+                    t.cancel()
+            await drain(tasks)
+            if not keep:
                 try:
                     await asyncio.shield(self.abort_multipart_upload(bucket, key, upload_id))
                     if journal:
@@ -648,7 +664,7 @@ class S3Client:
                              "x-amz-copy-source-range": f"bytes={off}-{off + ln - 1}"})
                 etags[num] = self._copy_etag(r, bucket, key)
         try:
-            await asyncio.gather(*(one(n, o, ln) for n, o, ln in parts))
+            await gather_strict(*(one(n, o, ln) for n, o, ln in parts))
             return await self.complete_multipart_upload(bucket, key, upload_id,
                                                         [(n, etags[n]) for n, _, _ in parts])
         except BaseException:
@@ -782,7 +798,7 @@ class S3Client:
                     await self._request("GET", bucket, key,
                                         headers={"range": f"bytes={off}-{off + ln - 1}"},
                                         sink=FileSink(fd, off, ln), progress=progress)
-                await asyncio.gather(*(one(o, ln) for o, ln in rngs))
+                await gather_strict(*(one(o, ln) for o, ln in rngs))
                 written = size
             else:
                 r = await self._request("GET", bucket, key, sink=FileSink(fd, 0),

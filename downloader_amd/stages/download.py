@@ -19,6 +19,7 @@ from ..models import api, keys
 from ..net.http import Progress, SourceChanged
 from ..net.proxy import ProxyConfig
 from ..s3.client import S3Error
+from ..utils.aio import gather_strict
 from ..utils.log import redact_url
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket, media_type)
@@ -302,7 +303,7 @@ class DownloadStage(Stage):
                                       if resumable else "",
                                       keep_on_error=resumable and keep, stats=rstats,
                                       meta={"stager-source": tag} if tag else None)
-        await asyncio.gather(*(one(k, f) for k, f in owner.items()))
+        await gather_strict(*(one(k, f) for k, f in owner.items()))
         if rstats:
             job.stats["resumed_parts"] = rstats["resumed_parts"]
         if reused:

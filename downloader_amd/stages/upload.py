@@ -18,6 +18,7 @@ import os
 from typing import Any, Dict, List
 
 from ..models import keys
+from ..utils.aio import gather_strict
 from ..net.http import Progress
 from .base import DOWNLOADING, Job, Services, Stage, ensure_staging_bucket, media_type
 from .jobdir import get_reaper
@@ -89,7 +90,7 @@ class UploadStage(Stage):
                 await self.sv.telemetry.emit_progress(media_id, DOWNLOADING, pct)
                 job.emitter.emit("progress", pct)
 
-        await asyncio.gather(*(one(i, f) for i, f in enumerate(files)))
+        await gather_strict(*(one(i, f) for i, f in enumerate(files)))
         job.stats["uploaded_bytes"] = sum(uploaded)
 
         await self.sv.s3.put_object(bucket, keys.done_key(media_id), keys.DONE_BODY)
