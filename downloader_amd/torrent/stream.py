@@ -34,6 +34,7 @@ from typing import Dict, List, Optional, Set, Tuple
 from ..models import keys
 from ..stages.base import media_type
 from ..net.http import TransportError
+from ..utils.aio import gather_strict
 from ..utils.log import redact_url
 from .metainfo import Metainfo
 from .session import TorrentError, webseed_url
@@ -50,6 +51,7 @@ class _Target:
     single: bool                # one PUT (<= multipart threshold) instead of multipart
     upload_id: str = ""
     etags: Dict[int, str] = field(default_factory=dict)
+    completed: bool = False     # CompleteMultipartUpload succeeded (abort deletes the object)
 
 
 @dataclass(eq=False)
@@ -325,11 +327,12 @@ class StreamStager:
             for t in self.targets:
                 if t.size == 0:
                     await self.s3.put_object(self.bucket, t.key, b"", self._ctype(t))
-            ids = await asyncio.gather(*(self.s3.create_multipart_upload(self.bucket, t.key,
-                                                                         self._ctype(t))
-                                         for t in multi))
-            for t, uid in zip(multi, ids):
-                t.upload_id = uid
+            async def create(t: _Target) -> None:
+                t.upload_id = await self.s3.create_multipart_upload(self.bucket, t.key,
+                                                                    self._ctype(t))
+            # all creations settle before a failure propagates: abort() then sees every
+            # upload that was opened (none is left behind on the bucket)
+            await gather_strict(*(create(t) for t in multi), cancel=False)
             queue: "asyncio.Queue[_Unit]" = asyncio.Queue()
             for u in self.units:
                 queue.put_nowait(u)
@@ -348,8 +351,11 @@ class StreamStager:
             unverified = [p for p in self.frags if p not in self.verified]
             if unverified:
                 raise TorrentError(f"pieces {unverified[:5]} never verified")
-            await asyncio.gather(*(self.s3.complete_multipart_upload(
-                self.bucket, t.key, t.upload_id, sorted(t.etags.items())) for t in multi))
+            async def complete(t: _Target) -> None:
+                await self.s3.complete_multipart_upload(self.bucket, t.key, t.upload_id,
+                                                        sorted(t.etags.items()))
+                t.completed = True
+            await gather_strict(*(complete(t) for t in multi), cancel=False)
         except BaseException:
             await asyncio.shield(self.abort())
             raise
@@ -638,9 +644,9 @@ class StreamStager:
         """Drop what a failed attempt staged: open multipart uploads, single-PUT objects."""
         for t in self.targets:
             try:
-                if t.upload_id:
+                if t.upload_id and not t.completed:
                     await self.s3.abort_multipart_upload(self.bucket, t.key, t.upload_id)
-                elif t.single:
+                elif t.single or t.completed:
                     await self.s3.delete_object(self.bucket, t.key)
             except Exception:
                 pass

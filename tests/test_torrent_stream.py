@@ -627,3 +627,31 @@ def test_stream_verify_auto_without_a_device_stays_on_the_host(run, tmp_path, ma
 
     assert hashing._part_hasher is None
     run(go())
+
+
+def test_failed_upload_creation_leaves_no_open_upload(run, tmp_path, make_cfg, origin_cls):
+    """One file's CreateMultipartUpload fails while another's is still in flight: the job
+    fails and every upload that was opened is aborted (the slow creation is not orphaned)."""
+    from downloader_amd.s3.fake_server import FaultRule
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        await _show(tmp_path, origin)
+        s3.faults.add(FaultRule(method="POST", path_contains=keys.object_key("st9", "e1.mkv"),
+                                query_contains="uploads",
+                                status=0, delay_s=0.3, times=1))
+        s3.faults.add(FaultRule(method="POST", path_contains=keys.object_key("st9", "e2.mkv"),
+                                query_contains="uploads",
+                                status=500, code="InternalError", times=99))
+        w = _worker(make_cfg, ep, broker={"max_retries": 0},
+                    s3={"multipart_threshold": 200_000, "retries": 0})
+        await w.start(health=False)
+        await w.submit(api.make_download("st9", "http", origin.url("/t/show.torrent"), "TV"))
+        await _wait(w)
+        assert w.results[0].outcome == "dead", w.results
+        await asyncio.sleep(0.5)
+        assert not s3.uploads.get("triton-staging"), s3.uploads
+        await w.stop(); await s3.stop(); await origin.stop()
+    run(go())
