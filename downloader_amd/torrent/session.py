@@ -26,6 +26,7 @@ from urllib.parse import quote
 
 from ..net.http import FileSink, TransportError
 from ..ops import hashing
+from ..utils.aio import drain
 from ..utils.log import redact_url
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
@@ -876,9 +877,15 @@ class TorrentSession:
             if verifying:
                 await asyncio.gather(*verifying)
         finally:
-            for t in verifying:
+            pending = list(verifying)
+            for t in pending:
                 t.cancel()
+            # a verification may sit in an executor reading the storage fds: it finishes
+            # before this webseed loop counts as gone (the session closes those fds after)
+            interrupted = await drain(pending)
             self._webseed_exit()
+            if interrupted:
+                raise asyncio.CancelledError()
 
     async def _webseed_fetch(self, base: str, first: int, pieces: List[int]) -> None:
         off = first * self.meta.piece_length
