@@ -270,14 +270,24 @@ class DownloadStage(Stage):
         rstats: Dict[str, int] = {}
 
         reused: List[str] = []
+        halted = []        # set by the first failure: objects not begun yet are not started
 
         async def one(key: str, f: str) -> None:
+            try:
+                await stage_one(key, f)
+            except Exception:
+                halted.append(f)
+                raise
+
+        async def stage_one(key: str, f: str) -> None:
             it = by_path[f]
             # the staged object records which source version it holds: a retry of the job
             # skips objects an earlier attempt already staged from the same version
             tag = hashlib.sha1(f"{src.bucket}/{it.name}@{it.etag}".encode()).hexdigest() \
                 if it.etag else ""
             async with sem:
+                if halted:
+                    return
                 if tag and job.attempt > 0 and not same:
                     try:
                         info = await s3.head_object(self.cfg.s3.bucket, key)
@@ -303,7 +313,10 @@ class DownloadStage(Stage):
                                       if resumable else "",
                                       keep_on_error=resumable and keep, stats=rstats,
                                       meta={"stager-source": tag} if tag else None)
-        await gather_strict(*(one(k, f) for k, f in owner.items()))
+        # one object failing: with a retry still to come, the objects already moving finish
+        # (the retry reuses them, and a big one keeps its resumable upload); on the last
+        # attempt they are cancelled
+        await gather_strict(*(one(k, f) for k, f in owner.items()), cancel=not keep)
         if rstats:
             job.stats["resumed_parts"] = rstats["resumed_parts"]
         if reused:

@@ -170,3 +170,43 @@ def test_bucket_retry_skips_objects_already_staged(run, make_cfg, origin_cls):
         assert staged[0].stats.get("reused_objects", 0) >= 1
         await w.stop(); await origin.stop(); await s3.stop()
     run(go())
+
+
+def test_bucket_failure_lets_objects_in_flight_finish(run, make_cfg, origin_cls):
+    """Objects relayed in parallel: one fails while another is still moving. With a retry to
+    come, the one in flight finishes (not cancelled), so the retry reuses it."""
+    import asyncio
+
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.s3.fake_server import FaultRule
+    from downloader_amd.service.worker import Worker
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        s3.buckets["src"] = {}
+        eps = {f"e{i}.mkv": os.urandom((2 << 20) + i) for i in range(1, 5)}
+        for n, d in eps.items():
+            s3.put("src", f"lib/Show/Season 1/{n}", d)
+        cfg = make_cfg(ep, download={"bucket_secure": False, "bucket_server_copy": False,
+                                     "bucket_concurrency": 4},
+                       s3={"retries": 0}, broker={"retry_backoff_s": 0.05})
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        s3.faults.add(FaultRule(method="GET", path_contains="e1.mkv", status=0, delay_s=0.4,
+                                times=1))                  # e1 still moving when e3 fails
+        s3.faults.add(FaultRule(method="GET", path_contains="e3.mkv", times=1))
+        uri = f"bucket://{s3.endpoint},src,minioadmin,minioadmin,lib"
+        await w.submit(api.make_download("bf", "bucket", uri, "TV"))
+        for _ in range(1500):
+            if any(r.outcome == "staged" for r in w.results):
+                break
+            await asyncio.sleep(0.02)
+        staged = [r for r in w.results if r.outcome == "staged"]
+        assert staged, w.results
+        for n, d in eps.items():
+            assert s3.get("triton-staging", keys.object_key("bf", n)) == d
+        assert staged[0].stats.get("reused_objects", 0) == 3     # e1, e2, e4
+        await w.stop(); await s3.stop()
+    run(go())
