@@ -66,6 +66,16 @@ def done_key(media_id: str) -> str:
     return node_join(media_id, "original/", "done")
 
 
+def originals_prefix(media_id: str) -> str:
+    """Prefix of every staged original of a job (``object_key`` without the name)."""
+    return node_join(media_id, "original/")
+
+
+def journal_prefix(media_id: str) -> str:
+    """Prefix of a job's relay resume journals (``relay_journal_key``)."""
+    return node_join(media_id, ".stager/")
+
+
 def relay_journal_key(media_id: str, file_path: str) -> str:
     """Resume journal of a streamed relay (``S3Client.relay_object(journal=)``): outside
     ``<id>/original/`` so nothing that lists the staged originals ever sees it."""

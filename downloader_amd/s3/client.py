@@ -768,6 +768,25 @@ class S3Client:
                 return out
             marker = _text(root, "NextPartNumberMarker")
 
+    async def list_uploads(self, bucket: str, prefix: str) -> List[Tuple[str, str]]:
+        """(key, upload id) of every multipart upload in progress under ``prefix``
+        (ListMultipartUploads, paginated by key / upload-id marker)."""
+        out: List[Tuple[str, str]] = []
+        km = um = ""
+        while True:
+            q = [("uploads", ""), ("prefix", prefix)]
+            if km:
+                q += [("key-marker", km), ("upload-id-marker", um)]
+            r = await self._request("GET", bucket, query=q)
+            root = ET.fromstring(r.body)
+            for u in root:
+                if _strip(u.tag) == "Upload":
+                    out.append((_text(u, "Key"), _text(u, "UploadId")))
+            nk, nu = _text(root, "NextKeyMarker"), _text(root, "NextUploadIdMarker")
+            if _text(root, "IsTruncated") != "true" or not nk or (nk, nu) == (km, um):
+                return out
+            km, um = nk, nu
+
     async def find_upload(self, bucket: str, key: str) -> Optional[str]:
         r = await self._request("GET", bucket, query=[("uploads", ""), ("prefix", key)])
         root = ET.fromstring(r.body)

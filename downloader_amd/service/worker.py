@@ -242,9 +242,15 @@ class Worker:
                                                           time.perf_counter() - t0, error=str(e)))
                         await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
                         outcome = await self._retry(d, attempt, str(e))
+                        if outcome == "dead":
+                            await self._sweep_uploads(job, child)
                         return self._finish(job, JobResult(job_id, outcome, time.perf_counter() - t0,
                                                       error=str(e)))
                     child.info("creating convert job")
+                    if attempt > 0 or d.redelivered:
+                        # an earlier attempt may have left uploads open (killed worker, kept
+                        # resumable relay that this attempt did not need)
+                        await self._sweep_uploads(job, child)
                 else:
                     outcome = "skipped"
                     child.warn("skipping download due to files existing in triton-staging")
@@ -266,6 +272,8 @@ class Worker:
             child.error("job failed outside stages", err=err)
             await self.telemetry.emit_status(job_id, api.STATUS_ERRORED)
             outcome = await self._retry(d, attempt, err)
+            if outcome == "dead":
+                await self._sweep_uploads(job, child)
             return self._finish(job, JobResult(job_id, outcome, time.perf_counter() - t0, error=err))
         finally:
             self.active.pop(slot, None)
@@ -302,6 +310,35 @@ class Worker:
         if self.on_result is not None:
             self.on_result(r)
         return r
+
+    async def _sweep_uploads(self, job: Job, log: Logger) -> None:
+        """The job is finished for good: abort the multipart uploads still open under its
+        originals (a worker killed mid-relay, a resumable upload kept for a retry that then
+        went another way, a disk upload kept for resume) and delete its relay journals.
+        Best effort - a failure here never changes the job's outcome. The reference leaves
+        this to a bucket lifecycle rule (minio-js aborts only its own failed uploads)."""
+        if not self.cfg.s3.sweep_stale_uploads:
+            return
+        b = self.cfg.s3.bucket
+        job_id = job.media.id
+        try:
+            n = 0
+            for key, uid in await self.s3.list_uploads(b, keys.originals_prefix(job_id)):
+                try:
+                    await self.s3.abort_multipart_upload(b, key, uid)
+                    n += 1
+                except S3Error:
+                    pass
+            for it in await self.s3.list_objects(b, keys.journal_prefix(job_id)):
+                try:
+                    await self.s3.delete_object(b, it.name)
+                except S3Error:
+                    pass
+            if n:
+                job.stats["stale_uploads_aborted"] = n
+                log.info("aborted stale multipart uploads", count=n)
+        except Exception as e:        # noqa: BLE001 - cleanup must not fail the job
+            log.warn("stale upload sweep failed", err=str(e))
 
     async def _already_staged(self, job_id: str, log: Logger) -> bool:
         log.info("checking s3 bucket to see if files already exist for id", job_id)

@@ -88,6 +88,10 @@ class S3Config(BaseModel):
     # a failed attempt leaves its multipart upload for the job's retry, which relays only the
     # parts not uploaded yet from the same (pinned) source version; 0 = off
     relay_resume_min_bytes: int = 1 << 30
+    # when a job ends for good (staged after a retry or a redelivery, or dead-lettered),
+    # abort the multipart uploads still open under <id>/original/ and drop its resume
+    # journals: what a killed worker or a kept attempt left behind is not billed forever
+    sweep_stale_uploads: bool = True
 
 
 class BrokerConfig(BaseModel):

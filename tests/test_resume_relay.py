@@ -210,3 +210,59 @@ def test_bucket_failure_lets_objects_in_flight_finish(run, make_cfg, origin_cls)
         assert staged[0].stats.get("reused_objects", 0) == 3     # e1, e2, e4
         await w.stop(); await s3.stop()
     run(go())
+
+
+def test_finished_jobs_sweep_stale_uploads(run, make_cfg, origin_cls):
+    """Uploads a killed worker left open under a job's originals are aborted when the
+    redelivered job is staged, and a dead-lettered job leaves neither uploads nor journals."""
+    import asyncio
+
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.service.worker import Worker
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(3 << 20)
+        origin.blobs["/a.mkv"] = blob
+        cfg = make_cfg(ep, s3={"retries": 0}, broker={"max_retries": 0})
+        broker = MemoryBroker()
+        w = Worker(cfg, broker=broker)
+        await w.start(health=False)
+        c = w.s3
+        await c.ensure_bucket("triton-staging")
+        # what a worker killed mid-relay leaves: an open upload (+ a journal)
+        await c.create_multipart_upload("triton-staging", keys.object_key("sw", "a.mkv"))
+        await c.put_object("triton-staging", keys.relay_journal_key("sw", "a.mkv"), b"{}")
+        await c.create_multipart_upload("triton-staging", keys.object_key("swx", "a.mkv"))
+        msg = api.make_download("sw", "http", origin.url("/a.mkv"))
+        from collections import deque
+
+        from downloader_amd.broker.memory import _Msg
+        q = cfg.broker.download_queue      # redelivered: its first consumer died mid-job
+        broker.queues.setdefault(q, deque()).append(_Msg(api.encode(msg), {}, redelivered=True))
+        broker._pump(q)
+        for _ in range(500):
+            if w.results:
+                break
+            await asyncio.sleep(0.02)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        assert s3.get("triton-staging", keys.object_key("sw", "a.mkv")) == blob
+        left = await c.list_uploads("triton-staging", "")
+        assert [k for k, _ in left] == [keys.object_key("swx", "a.mkv")]   # other job untouched
+        assert s3.get("triton-staging", keys.relay_journal_key("sw", "a.mkv")) is None
+        # a job that fails for good cleans up after itself too
+        await c.create_multipart_upload("triton-staging", keys.object_key("sd", "b.mkv"))
+        await w.submit(api.make_download("sd", "http", origin.url("/missing.mkv")))
+        for _ in range(500):
+            if len(w.results) > 1:
+                break
+            await asyncio.sleep(0.02)
+        assert w.results[1].outcome == "dead", w.results
+        assert [k for k, _ in await c.list_uploads("triton-staging", "")] == \
+            [keys.object_key("swx", "a.mkv")]
+        await w.stop(); await origin.stop(); await s3.stop()
+    run(go())
