@@ -1,0 +1,8 @@
+set -o pipefail
+F=gpurun_out/r3_ab_regress; mkdir -p $F
+export LOG_LEVEL=error TMPDIR=/tmp
+for i in 1 2 3; do
+  (cd ab_old && timeout -k 10 300 python bench.py > ../$F/old_$i.json 2>> ../$F/err.txt) || exit 1
+  timeout -k 10 300 python bench.py > $F/new_$i.json 2>> $F/err.txt || exit 1
+  python -c "import json;a=json.load(open('$F/old_$i.json'));b=json.load(open('$F/new_$i.json'));print('old', a['value'], a['single_put_MBps'], 'new', b['value'], b['single_put_MBps'])"
+done
