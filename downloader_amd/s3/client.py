@@ -768,13 +768,14 @@ class S3Client:
                 return out
             marker = _text(root, "NextPartNumberMarker")
 
-    async def list_uploads(self, bucket: str, prefix: str) -> List[Tuple[str, str]]:
+    async def list_uploads(self, bucket: str, prefix: str,
+                           page: int = 1000) -> List[Tuple[str, str]]:
         """(key, upload id) of every multipart upload in progress under ``prefix``
         (ListMultipartUploads, paginated by key / upload-id marker)."""
         out: List[Tuple[str, str]] = []
         km = um = ""
         while True:
-            q = [("uploads", ""), ("prefix", prefix)]
+            q = [("uploads", ""), ("prefix", prefix), ("max-uploads", str(page))]
             if km:
                 q += [("key-marker", km), ("upload-id-marker", um)]
             r = await self._request("GET", bucket, query=q)
@@ -788,12 +789,11 @@ class S3Client:
             km, um = nk, nu
 
     async def find_upload(self, bucket: str, key: str) -> Optional[str]:
-        r = await self._request("GET", bucket, query=[("uploads", ""), ("prefix", key)])
-        root = ET.fromstring(r.body)
+        """Upload id of an upload in progress for exactly ``key`` (the last listed)."""
         best = None
-        for u in root:
-            if _strip(u.tag) == "Upload" and _text(u, "Key") == key:
-                best = _text(u, "UploadId")
+        for k, uid in await self.list_uploads(bucket, key):
+            if k == key:
+                best = uid
         return best
 
     async def fget_object(self, bucket: str, key: str, path: str, streams: int = 1,

@@ -396,11 +396,22 @@ class FakeS3:
             del self.buckets[bucket]
             return web.Response(status=204)
         if method == "GET" and "uploads" in q:
+            # ListMultipartUploads, sorted by (key, upload id) and paginated like S3
+            # (max-uploads, key-marker / upload-id-marker -> NextKeyMarker / NextUploadIdMarker)
             prefix = q.get("prefix", "")
-            ups = "".join(
-                f"<Upload><Key>{escape(u.key)}</Key><UploadId>{uid}</UploadId></Upload>"
-                for uid, u in self.uploads.get(bucket, {}).items() if u.key.startswith(prefix))
+            limit = max(1, min(1000, int(q.get("max-uploads", "1000") or 1000)))
+            marker = (q.get("key-marker", ""), q.get("upload-id-marker", ""))
+            allu = sorted((u.key, uid) for uid, u in self.uploads.get(bucket, {}).items()
+                          if u.key.startswith(prefix))
+            if marker[0]:
+                allu = [ku for ku in allu if ku > marker]
+            page, more = allu[:limit], len(allu) > limit
+            ups = "".join(f"<Upload><Key>{escape(k)}</Key><UploadId>{uid}</UploadId></Upload>"
+                          for k, uid in page)
+            nxt = (f"<NextKeyMarker>{escape(page[-1][0])}</NextKeyMarker>"
+                   f"<NextUploadIdMarker>{page[-1][1]}</NextUploadIdMarker>") if more else ""
             return _xml(f'<ListMultipartUploadsResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
+                        f"<IsTruncated>{'true' if more else 'false'}</IsTruncated>{nxt}"
                         f"{ups}</ListMultipartUploadsResult>")
         if method == "GET":
             return self._list_v2(bucket, q)

@@ -266,3 +266,21 @@ def test_finished_jobs_sweep_stale_uploads(run, make_cfg, origin_cls):
             [keys.object_key("swx", "a.mkv")]
         await w.stop(); await origin.stop(); await s3.stop()
     run(go())
+
+
+def test_list_uploads_pages(run):
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        c = S3Client(ep, *CREDS)
+        await c.ensure_bucket("b")
+        ids = set()
+        for i in range(7):
+            k = f"j/original/k{i % 3}"
+            ids.add((k, await c.create_multipart_upload("b", k)))
+        await c.create_multipart_upload("b", "other/original/x")
+        got = await c.list_uploads("b", "j/original/", page=2)
+        assert sorted(got) == sorted(ids) and len(got) == 7
+        assert (await c.find_upload("b", "other/original/x")) is not None
+        await c.close(); await s3.stop()
+    run(go())
