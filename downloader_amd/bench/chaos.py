@@ -86,6 +86,10 @@ async def config_chaos(a) -> Dict:
                    STAGER_HEALTH__ENABLED="false", STAGER_DOWNLOAD__TORRENT_ENABLE_DHT="false",
                    STAGER_BROKER__RETRY_BACKOFF_S="0.05", STAGER_BROKER__MAX_RETRIES="5",
                    STAGER_CONCURRENCY=str(a.concurrency))
+        mp = int(getattr(a, "chaos_multipart_mb", 0) or 0)
+        if mp:      # the 50 MB torrents stage as multipart uploads a SIGKILL can leave open
+            env.update(STAGER_S3__MULTIPART_THRESHOLD=str(mp * MB),
+                       STAGER_S3__PART_SIZE=str(max(5, mp // 2) * MB))
         sup = Supervisor(a.workers, worker_argv(), env=env, backoff=0.2,
                          max_restarts=10_000)
         client = AmqpBroker(srv.url)
@@ -189,7 +193,10 @@ async def config_chaos(a) -> Dict:
         # drain: let redelivered duplicates settle, then stop the pool
         await asyncio.sleep(1.0)
         codes = await asyncio.get_running_loop().run_in_executor(None, sup.stop)
-        s3_faults = b.stats().get("s3_faults", 0)
+        bst = b.stats()
+        s3_faults = bst.get("s3_faults", 0)
+        # multipart uploads still open: what killed workers left and no sweep reclaimed
+        open_uploads = bst.get("open_uploads", 0)
         restarts = sum(s.restarts for s in sup.slots)
         await client.close()
         await srv.stop()
@@ -218,5 +225,6 @@ async def config_chaos(a) -> Dict:
             "p50_latency_s": round(statistics.median(lat), 4) if lat else None,
             "p99_latency_s": round(sorted(lat)[int(0.99 * (len(lat) - 1))], 4) if lat else None,
             "worker_rss_high_MB": round(hw["rss_MB"], 1), "worker_fds_high": hw["fds"],
-            "stage_leftover_bytes": leftover, "worker_exit_codes": codes,
+            "stage_leftover_bytes": leftover, "s3_open_uploads": open_uploads,
+            "worker_exit_codes": codes,
             "long_lived_workers": growth}

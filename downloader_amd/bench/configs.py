@@ -590,6 +590,9 @@ def main(argv=None) -> int:
                          "long-lived workers show RSS / fd growth")
     ap.add_argument("--s3-fail-rate", type=float, default=0.02,
                     help="config 7: share of S3 object/part PUTs the peer answers 503 SlowDown")
+    ap.add_argument("--chaos-multipart-mb", type=int, default=0,
+                    help="config 7: multipart threshold in MB for the workers (0 = default); "
+                         "16 stages the 50 MB torrents as multipart uploads")
     ap.add_argument("--chaos-timeout", type=float, default=900.0,
                     help="config 7: give up waiting for every job's convert after this long")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")

@@ -6,7 +6,7 @@
 // bench far below what one worker can move, so the peers are native too.
 //
 //   origin:  GET|HEAD /media/<name>?size=N&seed=S   deterministic random bytes, Range support
-//   s3:      HEAD|PUT /<bucket>, GET /<bucket>?list-type=2,
+//   s3:      HEAD|PUT /<bucket>, GET /<bucket>?list-type=2, GET /<bucket>?uploads,
 //            PUT|GET|HEAD|DELETE /<bucket>/<key>, multipart (POST ?uploads, PUT ?partNumber,
 //            POST ?uploadId, DELETE ?uploadId)
 //   stats:   GET /_stats  (JSON: bytes received/served, objects, requests)
@@ -878,6 +878,17 @@ class Conn {
         return respond(200, "OK", "");
       }
       if (!exists) return s3_error(404, "Not Found", "NoSuchBucket", bucket);
+      if (m == "GET" && r.q.count("uploads")) {   // ListMultipartUploads (one page)
+        std::string prefix = r.q.count("prefix") ? r.q.at("prefix") : "";
+        std::string body = "<?xml version=\"1.0\" encoding=\"UTF-8\"?><ListMultipartUploadsResult><Bucket>" +
+                           bucket + "</Bucket><IsTruncated>false</IsTruncated>";
+        for (auto& kv : g_uploads)
+          if (kv.second.bucket == bucket && kv.second.key.compare(0, prefix.size(), prefix) == 0)
+            body += "<Upload><Key>" + xml_escape(kv.second.key) + "</Key><UploadId>" + kv.first +
+                    "</UploadId></Upload>";
+        body += "</ListMultipartUploadsResult>";
+        return respond(200, "OK", body);
+      }
       if (m == "GET") {
         std::string prefix = r.q.count("prefix") ? r.q.at("prefix") : "";
         std::string body = "<?xml version=\"1.0\" encoding=\"UTF-8\"?><ListBucketResult><Name>" + bucket +

@@ -284,3 +284,22 @@ def test_list_uploads_pages(run):
         assert (await c.find_upload("b", "other/original/x")) is not None
         await c.close(); await s3.stop()
     run(go())
+
+
+def test_blobd_lists_open_uploads(run):
+    """The bench peer answers ListMultipartUploads, so the stale-upload sweep works against it
+    (and the chaos soak's open_uploads count is what the sweeps left)."""
+    from downloader_amd.bench.infra import Blobd
+
+    async def go():
+        with Blobd(default_size=1 << 20) as blob:
+            c = S3Client(blob.endpoint, *CREDS)
+            await c.ensure_bucket("bk")
+            a = await c.create_multipart_upload("bk", "j1/original/a")
+            await c.create_multipart_upload("bk", "j2/original/b")
+            assert await c.list_uploads("bk", "j1/original/") == [("j1/original/a", a)]
+            await c.abort_multipart_upload("bk", "j1/original/a", a)
+            assert await c.list_uploads("bk", "j1/") == []
+            assert blob.stats()["open_uploads"] == 1
+            await c.close()
+    run(go())
