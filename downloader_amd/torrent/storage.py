@@ -9,7 +9,9 @@ from __future__ import annotations
 
 import errno
 import os
-from typing import List, Optional, Sequence, Tuple
+import threading
+from contextlib import contextmanager
+from typing import Iterator, List, Optional, Sequence, Tuple
 
 from ..ops import hashing
 from ..utils import limits
@@ -73,6 +75,12 @@ class Storage:
         self.root = root
         self.paths = meta.local_files(root)
         self.fds: List[int] = []
+        # executor threads inside write()/read() hold the fds: close() waits for them (a
+        # cancelled piece task does not stop its thread's pwrite, and a closed fd number can
+        # be reused by the next open of any job in the process)
+        self._cv = threading.Condition()
+        self._users = 0
+        self._closed = False
         # one descriptor per file for the session, plus the verifier's own opens and the
         # job's connections: fail with a clear error instead of EMFILE halfway through
         need = len(self.paths) * 2 + FD_MARGIN
@@ -97,27 +105,43 @@ class Storage:
         """(fd, file_offset, length, file_index) for a storage byte range."""
         return [(self.fds[idx], foff, ln, idx) for idx, foff, ln in self.meta.file_spans(offset, length)]
 
+    @contextmanager
+    def _use(self) -> Iterator[None]:
+        with self._cv:
+            if self._closed:
+                raise OSError(errno.EBADF, "torrent storage is closed")
+            self._users += 1
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._users -= 1
+                if not self._users:
+                    self._cv.notify_all()
+
     def write(self, offset: int, data: bytes) -> None:
         mv = memoryview(data)
         pos = 0
-        for fd, foff, ln, _ in self.segments(offset, len(data)):
-            chunk = mv[pos:pos + ln]
-            while chunk:
-                w = os.pwrite(fd, chunk, foff)
-                chunk = chunk[w:]
-                foff += w
-            pos += ln
+        with self._use():
+            for fd, foff, ln, _ in self.segments(offset, len(data)):
+                chunk = mv[pos:pos + ln]
+                while chunk:
+                    w = os.pwrite(fd, chunk, foff)
+                    chunk = chunk[w:]
+                    foff += w
+                pos += ln
 
     def read(self, offset: int, length: int) -> bytes:
         out = bytearray()
-        for fd, foff, ln, _ in self.segments(offset, length):
-            while ln > 0:
-                b = os.pread(fd, ln, foff)
-                if not b:
-                    raise OSError("short read from torrent storage")
-                out += b
-                foff += len(b)
-                ln -= len(b)
+        with self._use():
+            for fd, foff, ln, _ in self.segments(offset, length):
+                while ln > 0:
+                    b = os.pread(fd, ln, foff)
+                    if not b:
+                        raise OSError("short read from torrent storage")
+                    out += b
+                    foff += len(b)
+                    ln -= len(b)
         return bytes(out)
 
     def read_block(self, piece: int, begin: int, length: int) -> bytes:
@@ -147,10 +171,15 @@ class Storage:
             except OSError:
                 pass
 
-    def close(self) -> None:
-        for fd in self.fds:
+    def close(self, timeout: float = 30.0) -> None:
+        """Close the files once no thread is inside write()/read() (bounded wait: one
+        piece's pwrite); later calls fail with EBADF instead of touching a reused fd."""
+        with self._cv:
+            self._closed = True
+            self._cv.wait_for(lambda: not self._users, timeout)
+            fds, self.fds = self.fds, []
+        for fd in fds:
             try:
                 os.close(fd)
             except OSError:
                 pass
-        self.fds = []

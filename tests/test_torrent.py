@@ -1036,3 +1036,40 @@ def test_picker_verifying_pieces_are_not_reclaimed_or_verified_twice():
     assert 3 not in claimed and claimed == {0, 1, 2}
     start, count = pk.claim_run(8 * 16384)
     assert set(range(start, start + count)) == {4, 5, 6, 7}
+
+
+def test_storage_close_waits_for_inflight_writes(tmp_path):
+    """A piece write running on an executor thread when the session closes its storage
+    finishes before the fds are closed; later I/O fails with EBADF, not on a reused fd."""
+    import errno
+    import threading
+    import time
+
+    from downloader_amd.torrent.metainfo import FileEntry, Metainfo
+    from downloader_amd.torrent.storage import Storage
+
+    m = Metainfo(b"x" * 20, "t", 1 << 20, b"\0" * 20 * 4, [FileEntry(["t.bin"], 4 << 20, 0)],
+                 4 << 20)
+    st = Storage(m, str(tmp_path))
+    entered = threading.Event()
+    real_pwrite = os.pwrite
+
+    def slow_pwrite(fd, data, off):
+        entered.set()
+        time.sleep(0.2)
+        return real_pwrite(fd, data, off)
+
+    os.pwrite = slow_pwrite
+    try:
+        t = threading.Thread(target=st.write, args=(0, b"a" * (1 << 20)))
+        t.start()
+        entered.wait(5)
+        st.close()                         # waits for the write above
+        assert not t.is_alive()
+    finally:
+        os.pwrite = real_pwrite
+    with open(st.paths[0][0], "rb") as f:
+        assert f.read(1 << 20) == b"a" * (1 << 20)
+    with pytest.raises(OSError) as ei:
+        st.write(0, b"b")
+    assert ei.value.errno == errno.EBADF
