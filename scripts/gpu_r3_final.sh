@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-3 closing validation of the tree: GPU tier, smoke, the driver's default bench twice,
 # config 4 (one and two 20 GB jobs, GPU relay hashing in auto) and config 3, then the config 7
-# chaos soak (worker SIGKILLs, AMQP drops, S3 503s) - the paths that cancel transfers.
+# chaos soak (worker SIGKILLs, AMQP drops, S3 503s; torrents staged as multipart so kills
+# leave uploads open for the sweep) - the paths that cancel transfers.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 F=${OUT:-gpurun_out/r3_final}
@@ -24,5 +25,5 @@ print('$1', j['MBps_reps'], 'worker', [r['worker_cpu_s'] for r in j['reps_detail
 run c4 4 1
 run c4_j2 4 2
 run c3 3 1
-timeout -k 10 600 python -m downloader_amd.bench.configs --config 7 --scale 2 --workers 4 --concurrency 4 --qps 40 --chaos-interval 1.0 --s3-fail-rate 0.03 --chaos-timeout 400 > $F/chaos.jsonl 2> $F/chaos.err || exit 1
+timeout -k 10 600 python -m downloader_amd.bench.configs --config 7 --scale 2 --workers 4 --concurrency 4 --qps 40 --chaos-interval 1.0 --s3-fail-rate 0.03 --chaos-timeout 400 --chaos-multipart-mb 16 > $F/chaos.jsonl 2> $F/chaos.err || exit 1
 tail -1 $F/chaos.jsonl
