@@ -653,8 +653,15 @@ class AiohttpTransport(Transport):
                             raise TransportError("cancelled")
                         if written + len(chunk) > sink.max_bytes:
                             raise HttpError("response body exceeds limit", resp.status)
-                        await loop.run_in_executor(None, _pwrite_all, sink.fd, chunk,
-                                                   sink.offset + written)
+                        # a cancel must not return while the thread still writes: the
+                        # caller closes sink.fd next, and that number can be reused
+                        wf = loop.run_in_executor(None, _pwrite_all, sink.fd, chunk,
+                                                  sink.offset + written)
+                        try:
+                            await asyncio.shield(wf)
+                        except asyncio.CancelledError:
+                            await _drain(wf)
+                            raise
                         written += len(chunk)
                         if progress is not None:
                             progress.add(len(chunk))
