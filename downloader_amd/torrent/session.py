@@ -1004,7 +1004,8 @@ class TorrentSession:
             p.close()
         await asyncio.gather(*self._tasks, return_exceptions=True)
         if self.storage is not None:
-            self.storage.close()
+            # may wait for a piece write still on an executor thread: not on the loop
+            await asyncio.get_running_loop().run_in_executor(None, self.storage.close)
         stop = [self._announce_once(t, "stopped") for t in self.trackers]
         if stop:
             try:
