@@ -70,7 +70,7 @@ def _broker(args) -> int:
     from .broker.server import run_broker
     try:
         asyncio.run(run_broker(args.host, args.port, args.consumer_timeout, args.certfile,
-                               args.keyfile))
+                               args.keyfile, args.client_ca))
     except KeyboardInterrupt:
         pass
     return 0
@@ -172,6 +172,8 @@ def main(argv=None) -> int:
                    help="close a channel whose delivery stays unacked this long (s, 0: never)")
     b.add_argument("--certfile", default="", help="PEM certificate: serve amqps://")
     b.add_argument("--keyfile", default="")
+    b.add_argument("--client-ca", default="",
+                   help="PEM CA: require client certificates from it (mutual TLS)")
     su = sub.add_parser("submit")
     su.add_argument("id")
     su.add_argument("source", choices=["http", "torrent", "file", "bucket"])

@@ -45,12 +45,18 @@ def is_tls_url(url: str) -> bool:
     return urlsplit(url).scheme == "amqps"
 
 
-def client_ssl_context(verify: bool = True, ca_file: str = "") -> ssl.SSLContext:
+def client_ssl_context(verify: bool = True, ca_file: str = "", cert_file: str = "",
+                       key_file: str = "") -> ssl.SSLContext:
     """TLS for ``amqps://``: the system trust store plus ``ca_file`` (a private CA, the
-    usual RabbitMQ setup); ``verify=False`` accepts any certificate."""
+    usual RabbitMQ setup); ``verify=False`` accepts any certificate. ``cert_file`` (+
+    ``key_file``, else the key is in the same PEM): a client certificate for brokers that
+    require one (RabbitMQ ``ssl_options.fail_if_no_peer_cert``; amqplib's ``cert`` / ``key``
+    socket options)."""
     ctx = ssl.create_default_context()
     if ca_file:
         ctx.load_verify_locations(cafile=ca_file)
+    if cert_file:
+        ctx.load_cert_chain(cert_file, key_file or None)
     if not verify:
         ctx.check_hostname = False
         ctx.verify_mode = ssl.CERT_NONE
@@ -318,6 +324,18 @@ class Connection:
                                                    "server_hostname": self.host}
         self.reader, self.writer = await asyncio.wait_for(
             asyncio.open_connection(self.host, self.port, **tls), self.connect_timeout)
+        try:
+            return await self._handshake()
+        except BaseException as e:
+            self.writer.close()          # no half-open socket left behind
+            if isinstance(e, asyncio.IncompleteReadError):
+                # the broker hung up mid-handshake (starting up, or a TLS peer that refused
+                # our certificate after the handshake): retryable like a refused connect
+                raise ConnectionError("broker closed the connection during the handshake") \
+                    from e
+            raise
+
+    async def _handshake(self) -> "Connection":
         self.writer.write(C.PROTOCOL_HEADER)
         m, a = await self._expect_method(C.CONNECTION_START)
         self.server_properties = a[2]

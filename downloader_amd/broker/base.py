@@ -114,7 +114,8 @@ def make_broker(cfg, metrics=None) -> Broker:
     url = cfg.broker.url or dyn("rabbitmq")
     ctx = None
     if is_tls_url(url):     # amqps://: the same trust settings as every other TLS peer
-        ctx = client_ssl_context(cfg.tls.verify, cfg.broker.ca_file or cfg.tls.ca_file)
+        ctx = client_ssl_context(cfg.tls.verify, cfg.broker.ca_file or cfg.tls.ca_file,
+                                 cfg.broker.cert_file, cfg.broker.key_file)
     return AmqpBroker(url, heartbeat=cfg.broker.heartbeat_s,
                       reconnect_delay=cfg.broker.reconnect_delay_s, metrics=metrics,
                       connect_retry_s=cfg.broker.connect_retry_s, ssl_context=ctx,

@@ -505,11 +505,14 @@ class BrokerServer:
 
 
 async def run_broker(host: str = "0.0.0.0", port: int = 5672, consumer_timeout: float = 0.0,
-                     certfile: str = "", keyfile: str = "") -> None:
+                     certfile: str = "", keyfile: str = "", client_ca: str = "") -> None:
     ctx = None
     if certfile:
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
         ctx.load_cert_chain(certfile, keyfile or None)
+        if client_ca:      # mutual TLS: clients must present a certificate from this CA
+            ctx.load_verify_locations(cafile=client_ca)
+            ctx.verify_mode = ssl.CERT_REQUIRED
     srv = BrokerServer(host, port, consumer_timeout=consumer_timeout, ssl_context=ctx)
     await srv.start()
     print(f"broker listening on {host}:{srv.port}", flush=True)

@@ -119,6 +119,10 @@ class BrokerConfig(BaseModel):
     retry_delay: Literal["queue", "sleep"] = "queue"
     # PEM CA bundle for amqps:// (default: tls.ca_file)
     ca_file: str = ""
+    # client certificate (PEM) for amqps:// brokers that require one (mutual TLS); key_file
+    # empty: the key is in cert_file
+    cert_file: str = ""
+    key_file: str = ""
 
 
 class TelemetryConfig(BaseModel):

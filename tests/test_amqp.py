@@ -592,3 +592,48 @@ def test_amqps_round_trip(run, tmp_path):
         await d.ack()
         await b.close(); await srv.stop()
     run(go())
+
+
+@pytest.mark.skipif(__import__("shutil").which("openssl") is None, reason="needs openssl")
+def test_amqps_client_certificate(run, tmp_path):
+    """Mutual TLS: a broker that requires client certificates refuses a worker without one
+    and accepts the configured cert_file / key_file (make_broker from the config)."""
+    async def go():
+        import ssl as _ssl
+        import subprocess
+
+        from downloader_amd.broker.base import make_broker
+        from downloader_amd.utils.config import load_config
+
+        def cert(name, cn):
+            key, crt = str(tmp_path / f"{name}.key"), str(tmp_path / f"{name}.pem")
+            subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes",
+                            "-keyout", key, "-out", crt, "-days", "1", "-subj", f"/CN={cn}",
+                            "-addext", "subjectAltName=IP:127.0.0.1"], check=True,
+                           capture_output=True)
+            return crt, key
+        scrt, skey = cert("server", "127.0.0.1")
+        ccrt, ckey = cert("client", "worker")
+        sctx = _ssl.SSLContext(_ssl.PROTOCOL_TLS_SERVER)
+        sctx.load_cert_chain(scrt, skey)
+        sctx.load_verify_locations(cafile=ccrt)          # the client cert is its own CA
+        sctx.verify_mode = _ssl.CERT_REQUIRED
+        srv = await BrokerServer(ssl_context=sctx).start()
+
+        def cfg(**tls):
+            return load_config(overrides={"broker": {"backend": "amqp", "url": srv.url,
+                                                     "ca_file": scrt, "connect_retry_s": 0.5,
+                                                     **tls}})
+        bad = make_broker(cfg())
+        with pytest.raises((_ssl.SSLError, ConnectionError, OSError)):
+            await asyncio.wait_for(bad.connect(), 10)
+        await bad.close()
+        good = make_broker(cfg(cert_file=ccrt, key_file=ckey))
+        await good.connect()
+        await good.declare("m")
+        await good.publish("m", b"x")
+        d = await good.get("m")
+        assert d.body == b"x"
+        await d.ack()
+        await good.close(); await srv.stop()
+    run(go())
