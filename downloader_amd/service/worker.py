@@ -335,6 +335,7 @@ class Worker:
                 except S3Error:
                     pass
             if n:
+                self.metrics.stale_uploads.inc(n)
                 job.stats["stale_uploads_aborted"] = n
                 log.info("aborted stale multipart uploads", count=n)
         except Exception as e:        # noqa: BLE001 - cleanup must not fail the job

@@ -77,6 +77,9 @@ class Metrics:
                                       namespace=ns, registry=r)
         self.messages = Counter("broker_messages_total", "broker traffic", ["queue", "op"],
                                 namespace=ns, registry=r)
+        self.stale_uploads = Counter("stale_uploads_aborted_total",
+                                     "multipart uploads left open by earlier attempts, aborted "
+                                     "when their job ended", namespace=ns, registry=r)
 
     def watch_runtime(self, transports=None, namespace: str = "downloader") -> None:
         """Gauges read at scrape time from the native runtime: idle keep-alive connections

@@ -254,6 +254,8 @@ def test_finished_jobs_sweep_stale_uploads(run, make_cfg, origin_cls):
         left = await c.list_uploads("triton-staging", "")
         assert [k for k, _ in left] == [keys.object_key("swx", "a.mkv")]   # other job untouched
         assert s3.get("triton-staging", keys.relay_journal_key("sw", "a.mkv")) is None
+        assert r.stats["stale_uploads_aborted"] == 1
+        assert w.metrics.sample("downloader_stale_uploads_aborted_total") == 1
         # a job that fails for good cleans up after itself too
         await c.create_multipart_upload("triton-staging", keys.object_key("sd", "b.mkv"))
         await w.submit(api.make_download("sd", "http", origin.url("/missing.mkv")))
