@@ -579,7 +579,7 @@ class S3Client:
                     validator=validator)
         tasks = [asyncio.ensure_future(one(n, o, ln)) for n, o, ln in parts if n not in etags]
         try:
-            await asyncio.gather(*tasks)
+            await asyncio.gather(*tasks)   # noqa: the except below settles the siblings
             etag = await self.complete_multipart_upload(bucket, key, upload_id,
                                                         [(n, etags[n]) for n, _, _ in parts])
         except BaseException as e:

@@ -26,7 +26,7 @@ from urllib.parse import quote
 
 from ..net.http import FileSink, TransportError
 from ..ops import hashing
-from ..utils.aio import drain
+from ..utils.aio import drain, gather_strict
 from ..utils.log import redact_url
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
@@ -875,7 +875,7 @@ class TorrentSession:
                 while len(verifying) >= depth:
                     await asyncio.wait(verifying, return_when=asyncio.FIRST_COMPLETED)
             if verifying:
-                await asyncio.gather(*verifying)
+                await gather_strict(*verifying)
         finally:
             pending = list(verifying)
             for t in pending:

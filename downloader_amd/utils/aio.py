@@ -42,7 +42,7 @@ async def gather_strict(*aws: Awaitable[Any], cancel: bool = True) -> List[Any]:
     (``cancel=False``) - and in both cases awaited - before the exception propagates."""
     tasks = [asyncio.ensure_future(a) for a in aws]
     try:
-        return list(await asyncio.gather(*tasks))
+        return list(await asyncio.gather(*tasks))      # noqa: settled below
     except BaseException:
         if cancel:
             for t in tasks:

@@ -5,6 +5,8 @@ are implemented here:
   E999 syntax error          F401 unused import           E501 line too long
   W191 tab indentation       W291 trailing whitespace     E722 bare ``except:``
   B006 mutable default arg   F811 redefined function in the same scope
+  A001 ``asyncio.gather`` without ``return_exceptions=True`` (its failure leaves the
+       sibling awaitables running: use ``utils.aio.gather_strict``)
 
 Settings live in ``pyproject.toml`` under ``[tool.stager-lint]``; ``# noqa`` on a line skips it.
 Usage: ``python -m downloader_amd.utils.lint [paths...]``.
@@ -71,6 +73,12 @@ def lint_source(path: str, src: str, max_line: int = MAX_LINE) -> List[Finding]:
     for n in ast.walk(tree):
         if isinstance(n, ast.ExceptHandler) and n.type is None and n.lineno not in noqa:
             out.append(Finding(path, n.lineno, "E722", "bare except"))
+        if isinstance(n, ast.Call) and isinstance(n.func, ast.Attribute) and \
+                n.func.attr == "gather" and isinstance(n.func.value, ast.Name) and \
+                n.func.value.id == "asyncio" and n.lineno not in noqa and not any(
+                    k.arg == "return_exceptions" for k in n.keywords):
+            out.append(Finding(path, n.lineno, "A001", "asyncio.gather leaves siblings running "
+                                                       "on failure: use utils.aio.gather_strict"))
         if isinstance(n, (ast.FunctionDef, ast.AsyncFunctionDef)):
             for d in n.args.defaults + n.args.kw_defaults:
                 if isinstance(d, (ast.List, ast.Dict, ast.Set)) and n.lineno not in noqa:
