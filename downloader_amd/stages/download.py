@@ -19,7 +19,7 @@ from ..models import api, keys
 from ..net.http import Progress, SourceChanged
 from ..net.proxy import ProxyConfig
 from ..s3.client import S3Error
-from ..utils.aio import gather_strict
+from ..utils.aio import gather_strict, run_settled
 from ..utils.log import redact_url
 from .base import (DOWNLOADING, Job, ProtocolNotSupported, Services, Stage,
                    ensure_staging_bucket, media_type)
@@ -200,7 +200,7 @@ class DownloadStage(Stage):
             self._count("file", size)
             return
         job.logger.debug("file", src, "->", out)
-        n = await asyncio.get_running_loop().run_in_executor(None, file_src.copy_file, src, out)
+        n = await run_settled(file_src.copy_file, src, out)
         job.stats["downloaded_bytes"] = job.stats.get("downloaded_bytes", 0) + n
         self._count("file", n)
 

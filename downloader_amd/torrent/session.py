@@ -26,7 +26,7 @@ from urllib.parse import quote
 
 from ..net.http import FileSink, TransportError
 from ..ops import hashing
-from ..utils.aio import drain, gather_strict
+from ..utils.aio import drain, gather_strict, run_settled
 from ..utils.log import redact_url
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
@@ -452,7 +452,9 @@ class TorrentSession:
         loop = asyncio.get_running_loop()
         meta = self.meta
         assert meta is not None
-        self.storage = await loop.run_in_executor(None, Storage, meta, self.root)
+        # a cancel during the opens waits for them and closes what was opened
+        self.storage = await run_settled(Storage, meta, self.root,
+                                         discard=lambda st: st.close())
         self.have = await loop.run_in_executor(None, self.storage.recheck,
                                                self.client.verify_backend)
         self.verified_bytes = sum(meta.piece_size(i) for i in range(meta.num_pieces)

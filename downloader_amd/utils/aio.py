@@ -14,7 +14,7 @@ contract the parallel paths keep instead.
 from __future__ import annotations
 
 import asyncio
-from typing import Any, Awaitable, Iterable, List
+from typing import Any, Awaitable, Callable, Iterable, List, Optional
 
 
 async def drain(tasks: Iterable[asyncio.Future]) -> bool:
@@ -48,4 +48,20 @@ async def gather_strict(*aws: Awaitable[Any], cancel: bool = True) -> List[Any]:
             for t in tasks:
                 t.cancel()
         await drain(tasks)
+        raise
+
+
+async def run_settled(fn: Callable[..., Any], *args: Any,
+                      discard: Optional[Callable[[Any], None]] = None) -> Any:
+    """``fn(*args)`` on the default executor. A cancellation of the caller returns only
+    after the thread is done (it may be writing into a directory or descriptor the caller
+    releases next); a result that arrives after the cancellation goes to ``discard`` (e.g.
+    close the files it opened) instead of being dropped."""
+    fut = asyncio.get_running_loop().run_in_executor(None, fn, *args)
+    try:
+        return await asyncio.shield(fut)
+    except asyncio.CancelledError:
+        await drain([fut])
+        if discard is not None and not fut.cancelled() and fut.exception() is None:
+            discard(fut.result())
         raise

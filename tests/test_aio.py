@@ -101,3 +101,27 @@ def test_failed_range_download_leaves_no_transfer_behind(run, tmp_path, origin_c
         assert not set(ours()) - before, ours()      # nothing new left running
         await t.close(); await origin.stop()
     run(go())
+
+
+def test_run_settled_waits_and_discards(run):
+    import threading
+    import time
+
+    from downloader_amd.utils.aio import run_settled
+
+    async def go():
+        done, discarded = threading.Event(), []
+
+        def work():
+            time.sleep(0.1)
+            done.set()
+            return "opened"
+
+        t = asyncio.ensure_future(run_settled(work, discard=discarded.append))
+        await asyncio.sleep(0.02)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        assert done.is_set() and discarded == ["opened"]     # waited, result handed back
+        assert await run_settled(lambda: 7) == 7
+    run(go())
