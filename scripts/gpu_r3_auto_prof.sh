@@ -3,7 +3,7 @@
 # (the gfx950 sha1_lanes launches on the streamed-torrent hot path).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-F=$R/gpurun_out/r3_auto_prof
+F=$R/gpurun_out/${OUT_NAME:-r3_auto_prof}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=$R
 cd /tmp
