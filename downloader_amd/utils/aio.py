@@ -37,9 +37,10 @@ async def drain(tasks: Iterable[asyncio.Future]) -> bool:
 
 
 async def gather_strict(*aws: Awaitable[Any], cancel: bool = True) -> List[Any]:
-    """Like ``asyncio.gather`` (results in order, first failure raised), but on a failure or
-    cancellation the siblings are cancelled (``cancel=True``) or allowed to finish
-    (``cancel=False``) - and in both cases awaited - before the exception propagates."""
+    """Like ``asyncio.gather`` (results in order, first failure raised), but when one branch
+    fails the others are cancelled (``cancel=True``) or allowed to finish (``cancel=False``)
+    - and in both cases awaited - before the exception propagates. A cancellation of the
+    caller always cancels every branch (``gather`` forwards it) and likewise waits for them."""
     tasks = [asyncio.ensure_future(a) for a in aws]
     try:
         return list(await asyncio.gather(*tasks))      # noqa: settled below
