@@ -176,8 +176,12 @@ class Storage:
         piece's pwrite); later calls fail with EBADF instead of touching a reused fd."""
         with self._cv:
             self._closed = True
-            self._cv.wait_for(lambda: not self._users, timeout)
+            idle = self._cv.wait_for(lambda: not self._users, timeout)
             fds, self.fds = self.fds, []
+        if not idle:
+            # a write still stuck in the kernel after `timeout` (hung disk): leave its fds
+            # open - a leaked descriptor is harmless, a closed-and-reused one is not
+            return
         for fd in fds:
             try:
                 os.close(fd)
