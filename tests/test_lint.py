@@ -21,3 +21,11 @@ def test_linter_catches_problems():
     codes = sorted(f.code for f in lint_source("x.py", src))
     assert codes == ["B006", "E722", "F401"]
     assert [f.code for f in lint_source("y.py", "def (:\n")] == ["E999"]
+
+
+def test_a001_flags_gather_that_leaves_siblings_running():
+    bad = "import asyncio\n\n\nasync def f(a, b):\n    await asyncio.gather(a, b)\n"
+    ok = ("import asyncio\n\n\nasync def f(a, b):\n"
+          "    await asyncio.gather(a, b, return_exceptions=True)\n")
+    assert [f.code for f in lint_source("a.py", bad)] == ["A001"]
+    assert lint_source("b.py", ok) == []
