@@ -1,3 +1,6 @@
+#!/bin/bash
+# Same-box A/B of the default bench: an older tree in ./ab_old (git archive <commit> |
+# tar -x -C ab_old, native modules built in it; git-ignored) vs this tree, alternating.
 set -o pipefail
 F=gpurun_out/r3_ab_regress; mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp
