@@ -201,6 +201,10 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["stream_gpu_tail"] = a.stream_gpu_tail
             if getattr(a, "relay_trim_s", None) is not None:
                 dl["relay_pool_idle_trim_s"] = a.relay_trim_s
+            if getattr(a, "relay_memory_mb", 0):
+                dl["relay_memory_mb"] = a.relay_memory_mb
+            if getattr(a, "stream_gpu_slots", 0):
+                dl["stream_gpu_slots"] = a.stream_gpu_slots
             part_mb = getattr(a, "part_mb", 0)
             s3o = {"part_size": part_mb << 20} if part_mb else {}
             if getattr(a, "checksum", ""):
@@ -212,6 +216,11 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             # --reps: the same torrent staged again under a fresh media id (no done marker,
             # so every rep does the full job); one job is a sub-second sample on this box.
             reps = []
+            try:
+                from downloader_amd.ops import native
+                native().relay_pool_reset_peak()
+            except Exception:
+                pass
             rss0 = _rss_mb()["rss_MB"]
             threads0 = _thread_cpu(0)
             for k in range(max(1, getattr(a, "reps", 1))):
@@ -262,6 +271,9 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             "worker_rss_before_MB": rss0, "worker_rss_after_MB": rss["rss_MB"],
             "worker_rss_peak_MB": rss["rss_peak_MB"],
             "relay_pool_after": pool,
+            "part_budget_MiB": r[0].stats.get("torrent", {}).get("budget", {}).get("capacity", 0)
+            >> 20,
+            "part_pool_peak_MiB": pool.get("peak_bytes", 0) >> 20,
             **({"thread_cpu": thread_cpu} if os.environ.get("STAGER_THREAD_CPU") else {}),
             **({"stream_verify": a.stream_verify, "gpu_relay": gpu_relay}
                if getattr(a, "stream_verify", "") else {}),
@@ -636,6 +648,10 @@ def main(argv=None) -> int:
                     help="configs 3/4: override s3.part_size (MiB; one relayed part per unit)")
     ap.add_argument("--relay-trim-s", type=float, default=None,
                     help="configs 3/4: download.relay_pool_idle_trim_s (0: trim after every job)")
+    ap.add_argument("--relay-memory-mb", type=int, default=0,
+                    help="configs 3/4: download.relay_memory_mb (part-buffer budget per worker)")
+    ap.add_argument("--stream-gpu-slots", type=int, default=0,
+                    help="configs 3/4: download.stream_gpu_slots (PartHasher HBM slots)")
     ap.add_argument("--no-gpu-prewarm", action="store_true",
                     help="do not init the GPU verifier at worker start (download.gpu_prewarm)")
     ap.add_argument("--retry-backoff-s", type=float, default=0.05,

@@ -851,6 +851,12 @@ class PartHasher {
     api_.wait = [](void* c, uint64_t t, int ph, uint8_t* out, size_t ol, char* err, size_t el) {
       return ((PartHasher*)c)->wait(t, ph, out, ol, err, el);
     };
+    api_.set_notify = [](void* c, gpu_part_notify_fn fn, void* arg) {
+      PartHasher* h = (PartHasher*)c;
+      std::lock_guard<std::mutex> g(h->mu_);
+      h->notify_ = fn;
+      h->notify_arg_ = arg;
+    };
     thread_ = std::thread([this] { run(); });
     pthread_setname_np(thread_.native_handle(), "gpu-part-disp");
   }
@@ -991,6 +997,20 @@ class PartHasher {
     return -1;
   }
 
+  // Tell the relay module about finished phases: outside mu_ (the callback calls wait() and may
+  // unregister buffers), on this dispatcher thread.
+  void tell(const std::vector<uint64_t>& tickets, int phase) {
+    gpu_part_notify_fn fn;
+    void* arg;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn = notify_;
+      arg = notify_arg_;
+    }
+    if (fn)
+      for (uint64_t t : tickets) fn(arg, t, phase);
+  }
+
   hipEvent_t take_event() {
     if (!free_events_.empty()) {
       hipEvent_t e = free_events_.back();
@@ -1021,7 +1041,8 @@ class PartHasher {
             return;
           fresh.swap(queue_);
         }
-        bool progressed = !fresh.empty();
+        bool progressed = false;
+        std::vector<uint64_t> copied_now, done_now;
         // 1. DMA new parts into the open slot (a new one when it is full)
         while (!fresh.empty()) {
           const uint64_t t = fresh.front();
@@ -1069,8 +1090,10 @@ class PartHasher {
           f.jobs.push_back(t);
           copying.push_back(t);
           fresh.pop_front();
+          progressed = true;
         }
-        if (!fresh.empty()) {                   // no free slot: back to the head of the queue
+        const bool slot_bound = !fresh.empty();
+        if (slot_bound) {                       // no free slot: back to the head of the queue
           std::lock_guard<std::mutex> g(mu_);
           for (auto it = fresh.rbegin(); it != fresh.rend(); ++it) queue_.push_front(*it);
         }
@@ -1091,9 +1114,11 @@ class PartHasher {
             j->copy_ev = nullptr;
           }
           wcv_.notify_all();
+          copied_now.push_back(copying.front());
           copying.pop_front();
           progressed = true;
         }
+        tell(copied_now, GPU_PART_COPIED);
         // 3. finished kernels: publish digests, free slot and stream
         for (auto& st : streams_) {
           if (st.slot < 0) continue;
@@ -1107,6 +1132,7 @@ class PartHasher {
               Job& j = jobs_.at(t);
               j.digests.assign((const char*)sl.h_dig + (size_t)j.lane0 * 20, (size_t)j.np * 20);
               j.done = true;
+              done_now.push_back(t);
             }
           }
           wcv_.notify_all();
@@ -1128,18 +1154,35 @@ class PartHasher {
           launch(pick, st);
           progressed = true;
         }
+        tell(done_now, GPU_PART_DONE);
         if (!progressed) {
+          // nothing moved: poll the device's events again after a short sleep. New parts
+          // only end the sleep early when there is a slot to put them in - with every slot
+          // busy the predicate would be true at once and the thread would spin on mu_ and
+          // hipEventQuery against submit() / wait().
           std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait_for(lk, std::chrono::microseconds(200), [&] { return stop_ || !queue_.empty(); });
+          cv_.wait_for(lk, std::chrono::microseconds(200),
+                       [&] { return stop_ || (!slot_bound && !queue_.empty()); });
         }
       }
     } catch (const std::exception& e) {
-      std::lock_guard<std::mutex> g(mu_);
-      broken_ = true;
-      for (auto& kv : jobs_)
-        if (!kv.second.done) kv.second.err = std::string("GPU part hasher: ") + e.what();
-      queue_.clear();
-      wcv_.notify_all();
+      // DMAs already queued on copy_ may still read part buffers: let them end before any
+      // waiter learns of the failure and hands its buffer back to the pool (which may unmap it)
+      hipStreamSynchronize(copy_);
+      std::vector<uint64_t> failed_copy, failed_hash;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        broken_ = true;
+        for (auto& kv : jobs_)
+          if (!kv.second.done) {
+            kv.second.err = std::string("GPU part hasher: ") + e.what();
+            (kv.second.copied ? failed_hash : failed_copy).push_back(kv.first);
+          }
+        queue_.clear();
+        wcv_.notify_all();
+      }
+      tell(failed_copy, GPU_PART_COPIED);
+      tell(failed_hash, GPU_PART_DONE);
     }
   }
 
@@ -1205,6 +1248,8 @@ class PartHasher {
   uint64_t registered_ = 0, unregistered_ = 0;
   double reg_seconds_ = 0;
   GpuPartHashApi api_{};
+  gpu_part_notify_fn notify_ = nullptr;
+  void* notify_arg_ = nullptr;
   std::thread thread_;
 };
 

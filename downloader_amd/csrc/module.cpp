@@ -44,14 +44,10 @@ py::dict head_to_dict(const ResponseHead& h) {
 
 }  // namespace
 
-// Wait a GPU part ticket out and drop its digests (the relay failed after queueing the part):
-// returns the part's buffer to the pool and the hasher's slot state.
-void forget_ticket(uint64_t ticket) {
-  if (!ticket) return;
-  try {
-    gpu_part_wait(ticket);
-  } catch (...) {
-  }
+// The relay failed after queueing its part to the GPU hasher: nobody asks for the digests.
+// Returns once the part's buffer is back in the pool (its DMA is over).
+void forget_ticket(uint64_t id) {
+  if (id) gpu_part_forget(id);
 }
 
 struct PieceSplit {
@@ -126,7 +122,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
   d["moved"] = moved;
   d["crc32c"] = crc_b64;
   if (split) {
-    d["gpu_ticket"] = ticket;      // != 0: digests come from gpu_part_wait(ticket)
+    d["gpu_ticket"] = ticket;      // != 0: a part id; digests via gpu_part_poll / gpu_part_wait
     d["digests"] = py::bytes(digests);
     d["head"] = py::bytes(head);
     d["tail"] = py::bytes(tail);
@@ -160,15 +156,41 @@ PYBIND11_MODULE(_native, m) {
       "ABI capsule is `api` (_gpuhash.PartHasher.api()); None: host multi-buffer SHA-1");
   m.def(
       "gpu_part_wait",
-      [](uint64_t ticket) {
+      [](uint64_t id) {
         std::string d;
         {
           py::gil_scoped_release rel;
-          d = gpu_part_wait(ticket);
+          d = gpu_part_wait(id);
         }
         return py::bytes(d);
       },
-      py::arg("ticket"), "Digests (20 B per piece) of a part the relay handed to the GPU");
+      py::arg("id"), "Block until part `id` (the relay's gpu_ticket) is hashed: its digests");
+  m.def(
+      "gpu_part_forget",
+      [](uint64_t id) {
+        py::gil_scoped_release rel;
+        gpu_part_forget(id);
+      },
+      py::arg("id"),
+      "Nobody will ask for part `id`: returns once its buffer is back in the pool; the result "
+      "is dropped when it arrives");
+  m.def("gpu_part_eventfd", &gpu_part_eventfd,
+        "eventfd that turns readable when gpu_part_poll has news");
+  m.def(
+      "gpu_part_poll",
+      []() {
+        std::vector<GpuPartEvent> ev;
+        {
+          py::gil_scoped_release rel;
+          ev = gpu_part_poll();
+        }
+        py::list out;
+        for (auto& e : ev)
+          out.append(py::make_tuple(e.id, e.kind, py::bytes(e.data)));
+        return out;
+      },
+      "Drain completions: [(id, kind, data)] with kind 1 = copied (the part's buffer is back in "
+      "the pool), 2 = done (data = 20 B digests per piece), 3 = failed (data = error message)");
   py::class_<CpuPartHasher>(m, "CpuPartHasher")
       .def(py::init<double, int, int>(), py::arg("delay_s") = 0.005,
            py::arg("fail_copy_every") = 0, py::arg("fail_done_every") = 0,
@@ -184,10 +206,15 @@ PYBIND11_MODULE(_native, m) {
     d["submitted"] = s.submitted;
     d["host_fallbacks"] = s.host_fallbacks;
     d["refused"] = s.refused;
+    d["pending"] = s.pending;
     return d;
   });
-  m.def("relay_pool_trim", &relay_pool_trim,
-        "Unmap every idle hashed-relay part buffer; returns the bytes freed");
+  m.def("relay_pool_trim", &relay_pool_trim, py::arg("keep_bytes") = 0,
+        "Unmap idle hashed-relay part buffers beyond keep_bytes; returns the bytes freed");
+  m.def("relay_pool_set_budget", &relay_pool_set_budget, py::arg("bytes"),
+        "Bound leased + idle part buffers (0 = no bound): idle ones are unmapped to make room");
+  m.def("relay_pool_reset_peak", &relay_pool_reset_peak,
+        "Restart the pool's high-water mark (peak_bytes) and its over_budget count");
   m.def("relay_pool_set_max_idle", &relay_pool_set_max_idle, py::arg("n"),
         "Keep at most n idle part buffers (the rest are unmapped on release)");
   m.def("pipe_stats", []() {
@@ -214,6 +241,11 @@ PYBIND11_MODULE(_native, m) {
     d["in_use"] = s.in_use;
     d["max_idle"] = s.max_idle;
     d["created"] = s.created;
+    d["in_use_bytes"] = s.in_use_bytes;
+    d["budget"] = s.budget;
+    d["peak_bytes"] = s.peak_bytes;
+    d["evicted"] = s.evicted;
+    d["over_budget"] = s.over_budget;
     return d;
   });
   m.def(

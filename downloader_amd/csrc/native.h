@@ -130,17 +130,34 @@ void set_pipes_refused(bool on);
 struct RelayPoolStats {
   size_t idle_buffers, idle_bytes, in_use, max_idle;
   uint64_t created;
+  size_t in_use_bytes, budget, peak_bytes;   // peak of in_use_bytes + idle_bytes
+  uint64_t evicted, over_budget;             // idle buffers unmapped to stay in budget; leases past it
 };
 // GPU piece hashing of relayed parts (gpu_part_api.h, implemented by _gpuhash): when set,
 // relay_body_hashed_mb hands parts of >= min_pieces whole pieces to the GPU instead of the
-// host multi-buffer SHA-1 and returns a ticket; gpu_part_wait(ticket) gives the digests
-// (the part buffer goes back to the pool once its DMA has completed).
+// host multi-buffer SHA-1 and returns a part id. The part's buffer goes back to the pool as
+// soon as its DMA has completed (the hasher's COPIED notification); the digests arrive with
+// DONE. Completions are reported through an eventfd (gpu_part_eventfd) and drained with
+// gpu_part_poll, or waited for with gpu_part_wait. Part ids are this module's own (never a
+// hasher's ticket), so replacing the hasher cannot make two pending parts collide.
 void set_gpu_part_hasher(const void* api, int min_pieces);
 struct GpuPartStats {
-  uint64_t submitted, host_fallbacks, refused;
+  uint64_t submitted, host_fallbacks, refused, pending;
 };
 GpuPartStats gpu_part_stats();
-std::string gpu_part_wait(uint64_t ticket);
+// Blocks until part `id` is hashed; its digests (throws when the device failed after the DMA).
+std::string gpu_part_wait(uint64_t id);
+// A part nobody will ask for (the relay failed after queueing it): blocks until its buffer is
+// back in the pool, then drops its result when it arrives.
+void gpu_part_forget(uint64_t id);
+// Readable (eventfd counter) whenever gpu_part_poll has something new.
+int gpu_part_eventfd();
+struct GpuPartEvent {
+  uint64_t id;
+  int kind;                 // 1 copied (buffer released), 2 done (digests), 3 failed (error)
+  std::string data;         // digests / error message
+};
+std::vector<GpuPartEvent> gpu_part_poll();
 // gpu_part_api.h served by a host thread (copy, then multi-buffer SHA-1, each after
 // `delay_s`): the asynchronous relay-hashing path without a HIP device (tests).
 class CpuPartHasher {
@@ -156,9 +173,14 @@ class CpuPartHasher {
   struct Impl;
   std::unique_ptr<Impl> impl_;
 };
-// Idle part buffers are unmapped (returns the bytes freed); max_idle bounds the idle list.
-size_t relay_pool_trim();
+// Idle part buffers beyond `keep_bytes` are unmapped (returns the bytes freed); max_idle
+// bounds the idle list. A budget (bytes, 0 = none) bounds leased + idle buffers: idle ones are
+// unmapped first to make room for a new lease; a lease past the budget is counted
+// (over_budget) - admission is the caller's job (torrent/stream.py's PartBudget).
+size_t relay_pool_trim(size_t keep_bytes = 0);
 void relay_pool_set_max_idle(size_t n);
+void relay_pool_set_budget(size_t bytes);
+void relay_pool_reset_peak();
 RelayPoolStats relay_pool_stats();
 
 // Byte counter shared between a transfer running on a worker thread and the asyncio side

@@ -33,6 +33,8 @@
 #include <sys/types.h>
 #include <unistd.h>
 #include <unordered_map>
+#include <map>
+#include <sys/eventfd.h>
 
 #include <openssl/err.h>
 #include <openssl/ssl.h>
@@ -1090,33 +1092,56 @@ struct PartBuffer {
 // One process-wide pool instead of a buffer per transfer thread: a thread_local buffer as
 // large as the biggest part ever relayed stayed resident on each of the 32 transfer threads
 // (up to 4-8 GiB per worker after one torrent job). Buffers in use are bounded by the
-// caller's relays in flight (torrent_stream_parallel per job); at most `max_idle` idle
-// buffers are kept for the next part, the rest are unmapped on release, and trim() unmaps
-// every idle one (the stream stager calls it when a job's relays are done).
+// caller's admission (torrent/stream.py's PartBudget: relays in flight and parts awaiting
+// their DMA draw bytes from one process-wide budget); idle buffers are kept for the next
+// part only while leased + idle stays within that budget - an idle buffer is unmapped to make
+// room before a new one is mapped - and trim() unmaps the idle ones down to what the caller
+// keeps warm.
 class PartPool {
  public:
+  static size_t need(size_t n) { return (n + PartBuffer::kHuge - 1) & ~(PartBuffer::kHuge - 1); }
+
   std::unique_ptr<PartBuffer> acquire(size_t n) {
+    const size_t want = need(n);
+    std::vector<std::unique_ptr<PartBuffer>> drop;   // unmapped outside the lock
     {
       std::lock_guard<std::mutex> g(mu_);
+      // reuse an idle buffer of about the asked size: a much larger one would lease more
+      // bytes than the caller's budget accounted for
       size_t best = idle_.size();
-      for (size_t i = 0; i < idle_.size(); ++i)
-        if (idle_[i]->cap >= n && (best == idle_.size() || idle_[i]->cap < idle_[best]->cap))
+      for (size_t i = 0; i < idle_.size(); ++i) {
+        const size_t c = idle_[i]->cap;
+        if (c >= want && c - want <= std::max(want / 4, PartBuffer::kHuge) &&
+            (best == idle_.size() || c < idle_[best]->cap))
           best = i;
+      }
       if (best < idle_.size()) {
         std::unique_ptr<PartBuffer> b = std::move(idle_[best]);
         idle_.erase(idle_.begin() + (ptrdiff_t)best);
         idle_bytes_ -= b->cap;
-        in_use_ += 1;
+        lease(b->cap);
         return b;
       }
-      in_use_ += 1;
+      // a new mapping: unmap idle buffers (largest first) until it fits in the budget
+      while (budget_ && !idle_.empty() && in_use_bytes_ + idle_bytes_ + want > budget_) {
+        size_t big = 0;
+        for (size_t i = 1; i < idle_.size(); ++i)
+          if (idle_[i]->cap > idle_[big]->cap) big = i;
+        idle_bytes_ -= idle_[big]->cap;
+        drop.push_back(std::move(idle_[big]));
+        idle_.erase(idle_.begin() + (ptrdiff_t)big);
+        evicted_++;
+      }
+      lease(want);
     }
+    drop.clear();
     try {
       created_.fetch_add(1, std::memory_order_relaxed);
       return std::unique_ptr<PartBuffer>(new PartBuffer(n));
     } catch (...) {
       std::lock_guard<std::mutex> g(mu_);
       in_use_ -= 1;
+      in_use_bytes_ -= want;
       throw;
     }
   }
@@ -1125,9 +1150,11 @@ class PartPool {
     {
       std::lock_guard<std::mutex> g(mu_);
       in_use_ -= 1;
+      in_use_bytes_ -= b->cap;
       if (b->reg_api && b->reg_api != g_gpu_api.load()) {
         drop = std::move(b);         // registered with a hasher no longer in use: unlock
-      } else if (idle_.size() < max_idle_) {
+      } else if (idle_.size() < max_idle_ &&
+                 (!budget_ || in_use_bytes_ + idle_bytes_ + b->cap <= budget_)) {
         idle_bytes_ += b->cap;
         idle_.push_back(std::move(b));
       } else {
@@ -1152,14 +1179,17 @@ class PartPool {
       }
     }
   }
-  size_t trim() {
+  size_t trim(size_t keep_bytes) {
     std::vector<std::unique_ptr<PartBuffer>> drop;
-    size_t freed;
+    size_t freed = 0;
     {
       std::lock_guard<std::mutex> g(mu_);
-      drop.swap(idle_);
-      freed = idle_bytes_;
-      idle_bytes_ = 0;
+      while (!idle_.empty() && idle_bytes_ > keep_bytes) {
+        idle_bytes_ -= idle_.back()->cap;
+        freed += idle_.back()->cap;
+        drop.push_back(std::move(idle_.back()));
+        idle_.pop_back();
+      }
     }
     return freed;
   }
@@ -1167,15 +1197,46 @@ class PartPool {
     std::lock_guard<std::mutex> g(mu_);
     max_idle_ = n;
   }
+  void set_budget(size_t bytes) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      budget_ = bytes;
+    }
+    if (bytes) {
+      std::lock_guard<std::mutex> g(mu_);
+      // idle buffers beyond the new budget go at once
+      std::vector<std::unique_ptr<PartBuffer>> drop;
+      while (!idle_.empty() && in_use_bytes_ + idle_bytes_ > budget_) {
+        idle_bytes_ -= idle_.back()->cap;
+        drop.push_back(std::move(idle_.back()));
+        idle_.pop_back();
+        evicted_++;
+      }
+    }
+  }
+  void reset_peak() {
+    std::lock_guard<std::mutex> g(mu_);
+    peak_ = in_use_bytes_ + idle_bytes_;
+    over_budget_ = 0;
+  }
   RelayPoolStats stats() {
     std::lock_guard<std::mutex> g(mu_);
-    return RelayPoolStats{idle_.size(), idle_bytes_, in_use_, max_idle_, created_.load()};
+    return RelayPoolStats{idle_.size(), idle_bytes_, in_use_, max_idle_, created_.load(),
+                          in_use_bytes_, budget_, peak_, evicted_, over_budget_};
   }
 
  private:
+  void lease(size_t bytes) {   // mu_ held
+    in_use_ += 1;
+    in_use_bytes_ += bytes;
+    if (budget_ && in_use_bytes_ > budget_) over_budget_++;
+    peak_ = std::max(peak_, in_use_bytes_ + idle_bytes_);
+  }
   std::mutex mu_;
   std::vector<std::unique_ptr<PartBuffer>> idle_;
   size_t idle_bytes_ = 0, in_use_ = 0, max_idle_ = 16;
+  size_t in_use_bytes_ = 0, budget_ = 0, peak_ = 0;
+  uint64_t evicted_ = 0, over_budget_ = 0;
   std::atomic<uint64_t> created_{0};   // buffers mapped (each one faulted in, maybe page-locked)
 };
 
@@ -1193,17 +1254,42 @@ struct PartLease {
 };
 
 // ---- GPU part hashing (gpu_part_api.h) -------------------------------------------------
+// The hasher notifies each part's COPIED / DONE from its own thread (gpu_notify); the part's
+// buffer goes back to the pool right there, and the news is queued for gpu_part_poll (the
+// asyncio side reads the eventfd) or for a blocked gpu_part_wait. No thread waits per part.
 std::atomic<int> g_gpu_min_pieces{8};
 std::atomic<uint64_t> g_gpu_submitted{0}, g_gpu_fallbacks{0}, g_gpu_refused{0};
 
-// A part handed to the GPU: its buffer stays leased until the DMA out of it has completed.
 struct GpuPending {
-  std::unique_ptr<PartBuffer> buf;
+  std::unique_ptr<PartBuffer> buf;   // leased until the DMA out of it completed
   const GpuPartHashApi* api = nullptr;
+  uint64_t ticket = 0;
   int64_t skip = 0, full_len = 0, piece_len = 0;
+  bool copied = false, finished = false, failed = false;
+  bool forgotten = false, copied_reported = false;
+  std::string result;                // digests, or the error
 };
 std::mutex g_gpu_mu;
-std::unordered_map<uint64_t, GpuPending> g_gpu_pending;
+std::condition_variable g_gpu_cv;
+std::unordered_map<uint64_t, GpuPending> g_gpu_parts;                      // by part id
+std::map<std::pair<const GpuPartHashApi*, uint64_t>, uint64_t> g_gpu_ids;  // (hasher, ticket)
+std::deque<uint64_t> g_gpu_news;                                           // ids for gpu_part_poll
+uint64_t g_gpu_next_id = 0;
+
+int gpu_efd() {
+  static int fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  return fd;
+}
+
+void gpu_signal(uint64_t id) {   // g_gpu_mu held
+  g_gpu_news.push_back(id);
+  g_gpu_cv.notify_all();
+  const uint64_t one = 1;
+  if (gpu_efd() >= 0) {
+    ssize_t w = write(gpu_efd(), &one, sizeof one);
+    (void)w;   // EAGAIN: the counter is saturated, the reader wakes anyway
+  }
+}
 
 void host_digests(const uint8_t* p, int64_t full_len, int64_t piece_len, std::string* out) {
   const int64_t np = (full_len + piece_len - 1) / piece_len;
@@ -1216,11 +1302,93 @@ void host_digests(const uint8_t* p, int64_t full_len, int64_t piece_len, std::st
   out->resize((size_t)np * 20);
   sha1_mb(ptrs.data(), lens.data(), (size_t)np, (uint8_t*)&(*out)[0]);
 }
+
+// COPIED: the buffer returns to the pool (or, when the device failed before the DMA ended,
+// the bytes are still ours: hashed here and the part finishes at once).
+void gpu_copied(const GpuPartHashApi* a, uint64_t ticket, uint64_t id) {
+  char err[256] = {0};
+  const int rc = a->wait(a->ctx, ticket, GPU_PART_COPIED, nullptr, 0, err, sizeof err);
+  std::unique_ptr<PartBuffer> buf;
+  int64_t skip = 0, full = 0, plen = 0;
+  {
+    std::lock_guard<std::mutex> g(g_gpu_mu);
+    auto it = g_gpu_parts.find(id);
+    if (it == g_gpu_parts.end() || it->second.copied || !it->second.buf) return;
+    buf = std::move(it->second.buf);
+    skip = it->second.skip;
+    full = it->second.full_len;
+    plen = it->second.piece_len;
+  }
+  std::string digests;
+  if (rc != 0) {
+    host_digests(buf->data + skip, full, plen, &digests);
+    g_gpu_fallbacks++;
+  }
+  part_pool().release(std::move(buf));
+  std::lock_guard<std::mutex> g(g_gpu_mu);
+  auto it = g_gpu_parts.find(id);
+  GpuPending& p = it->second;
+  p.copied = true;
+  if (rc != 0) {            // the hasher forgets a job whose copy failed: no DONE follows
+    p.finished = true;
+    p.result.swap(digests);
+    g_gpu_ids.erase({a, ticket});
+  }
+  if (p.forgotten && p.finished)
+    g_gpu_parts.erase(it);
+  else if (!p.forgotten)
+    gpu_signal(id);
+  else
+    g_gpu_cv.notify_all();
+}
+
+void gpu_done(const GpuPartHashApi* a, uint64_t ticket, uint64_t id) {
+  int64_t np = 0;
+  {
+    std::lock_guard<std::mutex> g(g_gpu_mu);
+    auto it = g_gpu_parts.find(id);
+    if (it == g_gpu_parts.end() || it->second.finished) return;
+    np = (it->second.full_len + it->second.piece_len - 1) / it->second.piece_len;
+  }
+  std::string out((size_t)np * 20, '\0');
+  char err[256] = {0};
+  const int rc = a->wait(a->ctx, ticket, GPU_PART_DONE, (uint8_t*)&out[0], out.size(), err,
+                         sizeof err);
+  std::lock_guard<std::mutex> g(g_gpu_mu);
+  g_gpu_ids.erase({a, ticket});
+  auto it = g_gpu_parts.find(id);
+  if (it == g_gpu_parts.end()) return;
+  GpuPending& p = it->second;
+  p.finished = true;
+  p.failed = rc != 0;
+  p.result = rc ? std::string("GPU piece hashing failed: ") + err : out;
+  if (p.forgotten)
+    g_gpu_parts.erase(it);
+  else
+    gpu_signal(id);
+}
+
+// gpu_notify_fn: called on the hasher's thread without its lock held.
+void gpu_notify(void* arg, uint64_t ticket, int phase) {
+  const GpuPartHashApi* a = (const GpuPartHashApi*)arg;
+  uint64_t id;
+  bool copied;
+  {
+    std::lock_guard<std::mutex> g(g_gpu_mu);
+    auto it = g_gpu_ids.find({a, ticket});
+    if (it == g_gpu_ids.end()) return;
+    id = it->second;
+    copied = g_gpu_parts.at(id).copied;
+  }
+  if (!copied) gpu_copied(a, ticket, id);   // a DONE implies the copy is over
+  if (phase == GPU_PART_DONE) gpu_done(a, ticket, id);
+}
 }  // namespace
 
 void set_gpu_part_hasher(const void* api, int min_pieces) {
   const GpuPartHashApi* a = (const GpuPartHashApi*)api;
   if (a && a->abi != GPU_PART_API_ABI) throw std::invalid_argument("gpu_part_api ABI mismatch");
+  if (a) a->set_notify(a->ctx, &gpu_notify, (void*)a);
   g_gpu_min_pieces.store(std::max(1, min_pieces));
   g_gpu_api.store(a);
   part_pool().drop_foreign(a);
@@ -1228,9 +1396,10 @@ void set_gpu_part_hasher(const void* api, int min_pieces) {
 
 // ---- CpuPartHasher: the gpu_part_api.h contract served by a host thread ------------------
 // A test double with the device's timing shape: the "DMA" (a copy into its own buffer) and
-// the "kernel" (multi-buffer SHA-1) each complete after a delay on a worker thread, so the
-// stream stager's asynchronous GPU path (tickets, lease release at copy completion,
-// continuations) runs and is tested on hosts without a HIP device.
+// the "kernel" (multi-buffer SHA-1) each complete after a delay on a worker thread, which
+// notifies COPIED / DONE like the device's dispatcher, so the stream stager's asynchronous
+// GPU path (part ids, buffer release at copy completion, eventfd completions) runs and is
+// tested on hosts without a HIP device.
 namespace {
 struct CpuJob {
   const uint8_t* host;
@@ -1254,6 +1423,16 @@ struct CpuPartHasher::Impl {
   std::thread th;
   GpuPartHashApi api{};
   uint64_t registered = 0;
+  gpu_part_notify_fn notify = nullptr;
+  void* notify_arg = nullptr;
+
+  void tell(uint64_t t, int phase, std::unique_lock<std::mutex>& lk) {
+    gpu_part_notify_fn fn = notify;
+    void* arg = notify_arg;
+    lk.unlock();
+    if (fn) fn(arg, t, phase);
+    lk.lock();
+  }
 
   void run() {
     std::unique_lock<std::mutex> lk(mu);
@@ -1270,6 +1449,8 @@ struct CpuPartHasher::Impl {
       j->copy.swap(c);
       j->copied = true;
       wcv.notify_all();
+      tell(t, GPU_PART_COPIED, lk);
+      j = &jobs.at(t);
       lk.unlock();
       std::this_thread::sleep_for(std::chrono::duration<double>(delay_s));
       std::string d;
@@ -1277,8 +1458,11 @@ struct CpuPartHasher::Impl {
       lk.lock();
       j->digests.swap(d);
       j->done = true;
-      if (j->abandoned) jobs.erase(t);
       wcv.notify_all();
+      if (j->abandoned)
+        jobs.erase(t);
+      else
+        tell(t, GPU_PART_DONE, lk);
     }
   }
 };
@@ -1342,6 +1526,12 @@ CpuPartHasher::CpuPartHasher(double delay_s, int fail_copy_every, int fail_done_
     }
     return 0;
   };
+  m->api.set_notify = [](void* c, gpu_part_notify_fn fn, void* arg) {
+    Impl* i = (Impl*)c;
+    std::lock_guard<std::mutex> g(i->mu);
+    i->notify = fn;
+    i->notify_arg = arg;
+  };
   m->th = std::thread([m] { m->run(); });
 }
 
@@ -1362,37 +1552,63 @@ uint64_t CpuPartHasher::registered() const {
 }
 
 GpuPartStats gpu_part_stats() {
-  return GpuPartStats{g_gpu_submitted.load(), g_gpu_fallbacks.load(), g_gpu_refused.load()};
-}
-
-std::string gpu_part_wait(uint64_t ticket) {
-  GpuPending pend;
+  size_t pending;
   {
     std::lock_guard<std::mutex> g(g_gpu_mu);
-    auto it = g_gpu_pending.find(ticket);
-    if (it == g_gpu_pending.end()) throw IoError("gpu_part_wait: unknown ticket");
-    pend = std::move(it->second);
-    g_gpu_pending.erase(it);
+    pending = g_gpu_parts.size();
   }
-  char err[256] = {0};
-  std::string out;
-  const GpuPartHashApi* a = pend.api;
-  if (a->wait(a->ctx, ticket, GPU_PART_COPIED, nullptr, 0, err, sizeof err) != 0) {
-    // the device failed before the DMA finished: the bytes are still ours, hash them here
-    host_digests(pend.buf->data + pend.skip, pend.full_len, pend.piece_len, &out);
-    part_pool().release(std::move(pend.buf));
-    g_gpu_fallbacks++;
-    return out;
+  return GpuPartStats{g_gpu_submitted.load(), g_gpu_fallbacks.load(), g_gpu_refused.load(),
+                      pending};
+}
+
+std::string gpu_part_wait(uint64_t id) {
+  std::unique_lock<std::mutex> lk(g_gpu_mu);
+  auto it = g_gpu_parts.find(id);
+  if (it == g_gpu_parts.end()) throw IoError("gpu_part_wait: unknown part");
+  g_gpu_cv.wait(lk, [&] { return it->second.finished; });
+  GpuPending p = std::move(it->second);
+  g_gpu_parts.erase(it);
+  if (p.failed) throw IoError(p.result);
+  return p.result;
+}
+
+void gpu_part_forget(uint64_t id) {
+  std::unique_lock<std::mutex> lk(g_gpu_mu);
+  auto it = g_gpu_parts.find(id);
+  if (it == g_gpu_parts.end()) return;
+  it->second.forgotten = true;
+  // the caller's buffer lease ends when this returns, as for a part hashed on the host
+  g_gpu_cv.wait(lk, [&] { return it->second.copied; });
+  if (it->second.finished) g_gpu_parts.erase(it);
+}
+
+int gpu_part_eventfd() { return gpu_efd(); }
+
+std::vector<GpuPartEvent> gpu_part_poll() {
+  uint64_t cnt;
+  ssize_t r = read(gpu_efd(), &cnt, sizeof cnt);   // reset the counter before draining
+  (void)r;
+  std::vector<GpuPartEvent> out;
+  std::lock_guard<std::mutex> g(g_gpu_mu);
+  while (!g_gpu_news.empty()) {
+    const uint64_t id = g_gpu_news.front();
+    g_gpu_news.pop_front();
+    auto it = g_gpu_parts.find(id);
+    if (it == g_gpu_parts.end() || it->second.forgotten) continue;
+    GpuPending& p = it->second;
+    if (p.copied && !p.copied_reported) {
+      p.copied_reported = true;
+      out.push_back(GpuPartEvent{id, 1, std::string()});
+    }
+    if (p.finished) {
+      out.push_back(GpuPartEvent{id, p.failed ? 3 : 2, std::move(p.result)});
+      g_gpu_parts.erase(it);
+    }
   }
-  part_pool().release(std::move(pend.buf));     // DMA done: the buffer serves the next part
-  const int64_t np = (pend.full_len + pend.piece_len - 1) / pend.piece_len;
-  out.resize((size_t)np * 20);
-  if (a->wait(a->ctx, ticket, GPU_PART_DONE, (uint8_t*)&out[0], out.size(), err, sizeof err) != 0)
-    throw IoError(std::string("GPU piece hashing failed: ") + err);
   return out;
 }
 
-size_t relay_pool_trim() { return part_pool().trim(); }
+size_t relay_pool_trim(size_t keep_bytes) { return part_pool().trim(keep_bytes); }
 PipeStats pipe_stats() { return pipe_pool().stats(); }
 void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
 void set_pipe_sizes(size_t main, size_t tee) {
@@ -1401,6 +1617,8 @@ void set_pipe_sizes(size_t main, size_t tee) {
   pipe_pool().drop_idle();
 }
 void relay_pool_set_max_idle(size_t n) { part_pool().set_max_idle(n); }
+void relay_pool_set_budget(size_t bytes) { part_pool().set_budget(bytes); }
+void relay_pool_reset_peak() { part_pool().reset_peak(); }
 RelayPoolStats relay_pool_stats() { return part_pool().stats(); }
 
 int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
@@ -1469,20 +1687,26 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
     PartBuffer* pb = lease.b.get();
     if (!pb->reg_api && api->reg(api->ctx, pb->data, pb->cap) == 0)
       pb->reg_api = api;
-    uint64_t t = pb->reg_api == api ? api->submit(api->ctx, b + skip, full_len, piece_len) : 0;
-    if (t) {
-      GpuPending pend;
-      pend.buf = std::move(lease.b);            // leased until the DMA is done
-      pend.api = api;
-      pend.skip = skip;
-      pend.full_len = full_len;
-      pend.piece_len = piece_len;
+    if (pb->reg_api == api) {
+      // held across submit: the hasher's COPIED for this ticket cannot overtake the record
       std::lock_guard<std::mutex> g(g_gpu_mu);
-      g_gpu_pending.emplace(t, std::move(pend));
-      g_gpu_submitted++;
-      digests->clear();
-      *gpu_ticket = t;
-      return pos;
+      const uint64_t t = api->submit(api->ctx, b + skip, full_len, piece_len);
+      if (t) {
+        const uint64_t id = ++g_gpu_next_id;
+        GpuPending& pend = g_gpu_parts[id];
+        pend.buf = std::move(lease.b);            // leased until the DMA is done
+        pend.api = api;
+        pend.ticket = t;
+        pend.skip = skip;
+        pend.full_len = full_len;
+        pend.piece_len = piece_len;
+        const bool fresh = g_gpu_ids.emplace(std::make_pair(api, t), id).second;
+        if (!fresh) throw std::logic_error("gpu part hasher reused a pending ticket");
+        g_gpu_submitted++;
+        digests->clear();
+        *gpu_ticket = id;
+        return pos;
+      }
     }
     g_gpu_refused++;
   }

@@ -560,17 +560,15 @@ class NativeTransport(Transport):
 
     def _forget_ticket(self, fut: "asyncio.Future") -> None:
         """A cancelled relay that had queued its part to the GPU hasher: nobody will ask for
-        the digests, but the wait must still run to return the part's buffer to the pool."""
+        the digests; the native side returns the part's buffer to the pool when its DMA is
+        over and drops the result (``gpu_part_forget`` blocks until the DMA is, so it runs on
+        a thread of its own)."""
         if not fut.done() or fut.cancelled() or fut.exception() is not None:
             return
         hashed = fut.result()[3]
         if hashed and hashed.get("gpu_ticket"):
-            def wait(n=self._n, t=hashed["gpu_ticket"]) -> None:
-                try:
-                    n.gpu_part_wait(t)
-                except Exception:
-                    pass
-            threading.Thread(target=wait, name="gpu-part-forget", daemon=True).start()
+            threading.Thread(target=self._n.gpu_part_forget, args=(hashed["gpu_ticket"],),
+                             name="gpu-part-forget", daemon=True).start()
 
     async def close(self) -> None:
         with self._lock:

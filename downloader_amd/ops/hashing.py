@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import os
 import threading
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 from . import gpu_available, gpuhash, native
@@ -118,59 +119,150 @@ def prewarm_gpu() -> bool:
 
 
 _part_hasher = None
-_part_wait_pool = None
 _part_hasher_failed = False
+_retired_hashers: list = []      # replaced hashers: kept alive while their parts may be pending
+
+# PartHasher geometry: device slots of slot_bytes each. A part's host buffer is only held
+# until its DMA into a slot completes, so enough slots that a DMA never waits for a kernel to
+# free one keeps host memory at a few parts (the slots are HBM: 16 x 1 GiB of 288 GB).
+PART_SLOT_BYTES = 1 << 30
+PART_SLOTS = 16
 
 
-def gpu_relay_hashing(min_pieces: int = 8) -> bool:
+def gpu_relay_hashing(min_pieces: int = 8, slots: int = PART_SLOTS,
+                      slot_bytes: int = PART_SLOT_BYTES) -> bool:
     """Route the hashed relay's parts to the gfx950 ``PartHasher`` (batched, one lane per
     piece; csrc/gpu_sha1.hip) instead of the host multi-buffer SHA-1. Created once per
     process on the worker's GPU; False (host hashing) when no HIP device is usable."""
-    global _part_hasher, _part_wait_pool, _part_hasher_failed
+    global _part_hasher, _part_hasher_failed
     with _gpu_lock:
         if _part_hasher is not None:
             return True
         if _part_hasher_failed or not gpu_available():
             return False
         try:
-            from concurrent.futures import ThreadPoolExecutor
-            ph = gpuhash().PartHasher(gpu_device(), 1 << 30, 8, 4, 16384)
+            ph = gpuhash().PartHasher(gpu_device(), int(slot_bytes), int(slots), 4, 16384)
             native().set_gpu_part_hasher(ph.api(), min_pieces)
         except Exception:
             _part_hasher_failed = True
             raise
         _part_hasher = ph
-        # digest waits block a thread each (no CPU while the device hashes)
-        _part_wait_pool = ThreadPoolExecutor(max_workers=128, thread_name_prefix="gpu-part")
         return True
 
 
 def use_part_hasher(hasher, min_pieces: int = 8) -> None:
     """Install ``hasher`` (anything with ``api()`` returning the gpu_part_api.h capsule, e.g.
     ``_native.CpuPartHasher`` in tests) as the relay's part hasher; None restores host
-    hashing. The object is kept alive here."""
-    global _part_hasher, _part_wait_pool
-    from concurrent.futures import ThreadPoolExecutor
+    hashing. The object is kept alive here (a replaced one too: its parts may be pending)."""
+    global _part_hasher
     with _gpu_lock:
         native().set_gpu_part_hasher(hasher.api() if hasher is not None else None, min_pieces)
+        if _part_hasher is not None and _part_hasher is not hasher:
+            _retired_hashers.append(_part_hasher)
         _part_hasher = hasher
-        if _part_wait_pool is None:
-            _part_wait_pool = ThreadPoolExecutor(max_workers=128, thread_name_prefix="gpu-part")
 
 
-async def gpu_part_digests(ticket: int) -> bytes:
-    """Digests of a part the relay queued to the GPU (``gpu_ticket``). Always call it once
-    per ticket: it also returns the part's buffer to the relay pool."""
-    import asyncio
-    loop = asyncio.get_running_loop()
-    # shielded: a cancelled caller (aborted job) must not cancel a wait still queued in the
-    # pool, or the ticket's part buffer would never return to the relay pool
-    return await asyncio.shield(
-        loop.run_in_executor(_part_wait_pool, native().gpu_part_wait, ticket))
+class GpuPart:
+    """Completion of one part handed to the GPU hasher: ``copied`` resolves when the DMA out
+    of its buffer is over (the buffer is back in the relay pool), ``done`` with its digests
+    (or a RuntimeError when the device failed after the DMA)."""
+
+    def __init__(self, loop: "asyncio.AbstractEventLoop"):
+        self.loop = loop
+        self.copied = loop.create_future()
+        self.done = loop.create_future()
+        self.done.add_done_callback(_retrieve)
+
+    def _deliver(self, kind: int, data: bytes) -> None:
+        if not self.copied.done():
+            self.copied.set_result(None)
+        if self.done.done():
+            return
+        if kind == 2:
+            self.done.set_result(data)
+        elif kind == 3:
+            self.done.set_exception(RuntimeError(data.decode(errors="replace")))
+
+
+def _retrieve(fut) -> None:
+    if not fut.cancelled():
+        fut.exception()
+
+
+class _GpuParts:
+    """Routes the native completion queue (``gpu_part_poll``, signalled through an eventfd
+    the event loop watches) to per-part futures: no thread blocks per part."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._parts: dict = {}
+        self._early: dict = {}        # news for a part not tracked yet
+        self._loops: "weakref.WeakSet" = weakref.WeakSet()
+
+    def track(self, gid: int) -> GpuPart:
+        import asyncio
+        loop = asyncio.get_running_loop()
+        self._watch(loop)
+        part = GpuPart(loop)
+        with self._lock:
+            self._parts[gid] = part
+            early = self._early.pop(gid, [])
+        for kind, data in early:
+            self._dispatch(gid, part, kind, data)
+        self.drain()                  # news that came before this loop watched the fd
+        return part
+
+    def _watch(self, loop) -> None:
+        if loop in self._loops:
+            return
+        loop.add_reader(native().gpu_part_eventfd(), self.drain)
+        self._loops.add(loop)
+
+    def _dispatch(self, gid: int, part: GpuPart, kind: int, data: bytes) -> None:
+        if kind != 1:
+            with self._lock:
+                self._parts.pop(gid, None)
+        import asyncio
+        try:
+            running = asyncio.get_running_loop()
+        except RuntimeError:
+            running = None
+        if running is part.loop:
+            part._deliver(kind, data)
+        elif not part.loop.is_closed():
+            part.loop.call_soon_threadsafe(part._deliver, kind, data)
+
+    def drain(self) -> None:
+        for gid, kind, data in native().gpu_part_poll():
+            with self._lock:
+                part = self._parts.get(gid)
+                if part is None:
+                    self._early.setdefault(gid, []).append((kind, data))
+                    continue
+            self._dispatch(gid, part, kind, data)
+
+    def pending(self) -> int:
+        with self._lock:
+            return len(self._parts)
+
+
+_gpu_parts = _GpuParts()
+
+
+def gpu_part_track(gid: int) -> GpuPart:
+    """Futures of a part the relay queued to the GPU (``gpu_ticket``). Track every id once:
+    a tracked part's buffer returns to the pool whether or not anybody awaits it."""
+    return _gpu_parts.track(gid)
+
+
+async def gpu_part_digests(gid: int) -> bytes:
+    """Digests of a part the relay queued to the GPU (``gpu_ticket``)."""
+    return await gpu_part_track(gid).done
 
 
 def gpu_relay_stats() -> dict:
     d = dict(native().gpu_part_stats())
+    d["tracked"] = _gpu_parts.pending()
     if _part_hasher is not None and hasattr(_part_hasher, "stats"):
         d.update({f"device_{k}": v for k, v in _part_hasher.stats().items()})
     return d

@@ -35,6 +35,7 @@ from ..models import keys
 from ..stages.base import media_type
 from ..net.http import TransportError
 from ..utils.aio import gather_strict
+from ..utils import membudget
 from ..utils.log import redact_url
 from .metainfo import Metainfo
 from .session import TorrentError, webseed_url
@@ -108,19 +109,17 @@ def _trim_relay_buffers() -> None:
         pass
 
 
-POOL_IDLE_DEFAULT = 16         # the native pool's own default
-POOL_IDLE_CAP = 192            # at 64 MiB parts: 12 GiB of idle buffers at most
-_pool_want: Dict[int, int] = {}   # id(stager) -> relays it runs at once
-_gpu_pending_want = 0             # process-wide parts awaiting GPU digests (0: no GPU stager)
+# Idle part buffers are bounded in BYTES by the part budget (utils/membudget.py: leased +
+# idle <= budget, enforced by the native pool), so their count needs no cap of its own.
+POOL_IDLE_MAX = 4096
 _gpu_pending_sems: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
     """Parts awaiting GPU digests, shared by every stream stager of the process (one per
     event loop): the device needs ~128 - 160 parts in flight to hide its per-piece latency,
-    whether they come from one job or several, and every one of them holds a part buffer
-    until its DMA. Per-job budgets made two jobs hold twice the buffers (pool churn) or,
-    halved, starved one job (profiles/r3_relayhash3/)."""
+    whether they come from one job or several. Since round 4 such a part holds no host memory
+    once its DMA is over - only HBM (profiles/r3_relayhash3/ for the count)."""
     loop = asyncio.get_running_loop()
     sem = _gpu_pending_sems.get(loop)
     if sem is None:
@@ -131,8 +130,8 @@ def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
 _gpu_init_started = False
 
 
-def start_gpu_init(min_pieces: int) -> None:
-    """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and 8 device
+def start_gpu_init(min_pieces: int, slots: int = 16) -> None:
+    """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and the device
     slots take a moment; the event loop keeps relaying meanwhile). Once per process; a
     missing device or a failed init leaves every part on the host."""
     global _gpu_init_started
@@ -143,31 +142,9 @@ def start_gpu_init(min_pieces: int) -> None:
 
     def init() -> bool:
         from ..ops import gpu_available
-        return gpu_available() and hashing.gpu_relay_hashing(min_pieces)
+        return gpu_available() and hashing.gpu_relay_hashing(min_pieces, slots)
     fut = asyncio.get_running_loop().run_in_executor(None, init)
     fut.add_done_callback(lambda f: f.cancelled() or f.exception())   # retrieved
-
-
-def _set_gpu_pending_want(n: int) -> None:
-    global _gpu_pending_want
-    want = n if n == 0 else max(_gpu_pending_want, n)
-    if want != _gpu_pending_want:
-        _gpu_pending_want = want
-        _size_pool()
-
-
-def _size_pool() -> None:
-    """Keep as many idle part buffers as the running stream stagers may have out at once:
-    relays in flight, plus parts waiting for their DMA with GPU hashing. Fewer made buffers
-    churn - mapped, faulted in (and page-locked for the GPU), then unmapped again: with two
-    20 GB jobs at once the host path created 214 buffers for 4 reps, the GPU path 356."""
-    want = max(POOL_IDLE_DEFAULT,
-               min(POOL_IDLE_CAP, sum(_pool_want.values()) + _gpu_pending_want))
-    try:
-        from ..ops import native
-        native().relay_pool_set_max_idle(want)
-    except Exception:
-        pass
 
 
 def _schedule_trim(idle_s: float) -> None:
@@ -210,6 +187,9 @@ class StreamStager:
         self.cfg = cfg
         self.trim_idle_s = float(getattr(getattr(cfg, "download", None),
                                          "relay_pool_idle_trim_s", 0.0) or 0.0)
+        # every relayed part draws its buffer's bytes from the process-wide budget
+        self.budget_bytes = membudget.relay_budget_bytes(getattr(cfg, "download", None))
+        self._budget: Optional[membudget.PartBudget] = None
         index = {os.path.abspath(p): i for i, (p, _) in enumerate(meta.local_files(root))}
         self.selected = [os.path.abspath(f) for f in selected]
         self.sizes = {f: meta.files[index[f]].length for f in self.selected}
@@ -258,6 +238,7 @@ class StreamStager:
         gpu_pending = int(getattr(d, "stream_gpu_pending", 0) or 0)
         self.verify_mode = getattr(d, "stream_verify_backend", "cpu") if gpu_pending > 0 else "cpu"
         self._min_pieces = int(getattr(d, "stream_gpu_min_pieces", 8) or 8)
+        self._gpu_dev_slots = int(getattr(d, "stream_gpu_slots", 16) or 16)
         # parts still queued below which the rest hash on the host
         self.gpu_tail = int(getattr(d, "stream_gpu_tail", 0) or 0)
         self._n_parts = sum(1 for u in self.units if u.target is not None)
@@ -319,10 +300,16 @@ class StreamStager:
         global _active_stagers
         multi = [t for t in self.targets if not t.single and t.size]
         _active_stagers += 1
-        _pool_want[id(self)] = self.parallel
+        if _trim_handle is not None:           # a job started inside the warm window
+            _trim_handle.cancel()
+        self._budget = membudget.part_budget(self.budget_bytes)
+        try:
+            from ..ops import native
+            native().relay_pool_set_max_idle(POOL_IDLE_MAX)
+        except Exception:
+            pass
         if self.verify_mode == "auto" and self._gpu_wanted():
-            start_gpu_init(self._min_pieces)
-        _size_pool()
+            start_gpu_init(self._min_pieces, self._gpu_dev_slots)
         try:
             for t in self.targets:
                 if t.size == 0:
@@ -361,9 +348,8 @@ class StreamStager:
             raise
         finally:
             _active_stagers -= 1
-            _pool_want.pop(id(self), None)
+            self.stats["budget"] = self._budget.stats()
             if _active_stagers == 0:
-                _set_gpu_pending_want(0)
                 _schedule_trim(self.trim_idle_s)
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
                  "virtual": True} for f in self.selected]
@@ -377,21 +363,33 @@ class StreamStager:
                 # digests (~piece_len / 58 MB/s on the device) and the checks run in a
                 # continuation, so the relay slots stay busy relaying meanwhile
                 await self._gpu_slots.acquire()
+                try:
+                    nb = await self._budget.acquire(u.length)
+                except BaseException:
+                    self._gpu_slots.release()
+                    raise
                 # the job's last parts hash on the host: their GPU latency (~piece_len / 58
                 # MB/s) would land on the end of the job with nothing left to overlap it
                 gpu = self._gpu_now() and queue.qsize() >= self.gpu_tail
                 try:
                     res = await self._relay_part(u, gpu)
                 except BaseException as e:
+                    self._budget.release(nb)
                     self._gpu_slots.release()
                     if not await self._unit_failed(u, e, queue):
                         return
                     continue
-                if res[1].get("gpu_ticket"):
-                    t = asyncio.ensure_future(self._complete(u, res, queue))
+                gid = res[1].get("gpu_ticket")
+                if gid:
+                    from ..ops import hashing
+                    part = hashing.gpu_part_track(gid)
+                    # the buffer is back in the pool once the DMA is over: so are its bytes
+                    part.copied.add_done_callback(lambda _f, nb=nb: self._budget.release(nb))
+                    t = asyncio.ensure_future(self._complete(u, res, part, queue))
                     self._continuations.add(t)
                     t.add_done_callback(self._continuations.discard)
                     continue
+                self._budget.release(nb)
                 self._gpu_slots.release()         # hashed on the host after all (refused)
                 try:
                     requeue = await self._after_fetch(u, self._accept(u, *res,
@@ -426,7 +424,6 @@ class StreamStager:
             from ..ops import hashing
             if hashing._part_hasher is not None:
                 self._gpu_slots = _gpu_pending_sem(self.gpu_pending)
-                _set_gpu_pending_want(self.gpu_pending)
         return self._gpu_slots
 
     def _gpu_now(self) -> bool:
@@ -456,13 +453,12 @@ class StreamStager:
         self._settle(u, [u], queue)
         return True
 
-    async def _complete(self, u: _Unit, res, queue: "asyncio.Queue[_Unit]") -> None:
+    async def _complete(self, u: _Unit, res, part, queue: "asyncio.Queue[_Unit]") -> None:
         """Continuation of a part whose pieces the GPU hashes: digests, checks, settle."""
-        from ..ops import hashing
         etag, h = res
         try:
             try:
-                digests = await hashing.gpu_part_digests(h["gpu_ticket"])
+                digests = await part.done
             except RuntimeError as e:
                 # the device failed after the part's buffer went back to the pool: the
                 # bytes are gone, so the part is fetched (and relayed) again - its next
@@ -530,7 +526,11 @@ class StreamStager:
         """Fetch one unit; return the units that must be fetched again (bad pieces)."""
         if u.target is None:
             return await self._after_fetch(u, [(u.start, await self._fetch_gap(u))])
-        etag, h = await self._relay_part(u)
+        nb = await self._budget.acquire(u.length)
+        try:
+            etag, h = await self._relay_part(u)
+        finally:
+            self._budget.release(nb)
         return await self._after_fetch(u, self._accept(u, etag, h, h["digests"]))
 
     async def _after_fetch(self, u: _Unit, got: Optional[List[Tuple[int, bytes]]]) -> List[_Unit]:
@@ -665,7 +665,8 @@ def _gpu_relay_on(cfg) -> Optional[str]:
     if hashing._part_hasher is not None:         # already set up (or a test double)
         return None
     try:
-        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8)):
+        if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8),
+                                     getattr(d, "stream_gpu_slots", 16)):
             return None
         return "no usable HIP device"
     except Exception as e:

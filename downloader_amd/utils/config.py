@@ -154,12 +154,17 @@ class DownloadConfig(BaseModel):
     # only (a retry takes the disk path with every source); always: whenever webseeds exist.
     torrent_stream: Literal["auto", "always", "off"] = "auto"
     torrent_stream_parallel: int = 16           # parts (Range GETs) in flight per job
+    # Byte budget of the streamed relay's part buffers (one per part in flight, as large as
+    # the part): relays in flight, parts awaiting their DMA to the GPU and idle pooled buffers
+    # of ALL jobs of the worker draw from it, so their resident memory never exceeds it
+    # (utils/membudget.py). 0 = relay_memory_fraction of this worker's share of the memory
+    # limit (cgroup memory.max, else RAM, / worker processes in the container).
+    relay_memory_mb: int = 0
+    relay_memory_fraction: float = 0.25
     # idle seconds after the last stream-staged job before the hashed relay's pooled part
-    # buffers (one per part in flight, up to 64 MiB each) are unmapped; jobs inside the window
-    # reuse them without re-faulting ~1 GiB of huge pages (MI355X box, 4 GB torrent: 26.7 -
-    # 27.8 GB/s warm vs 19.2 - 20.0 GB/s when every job faults its buffers afresh). Meanwhile
-    # the pool keeps as many idle buffers as the running jobs may have out (relays in flight,
-    # plus parts awaiting their DMA with GPU hashing), at most 128.
+    # buffers are unmapped; jobs inside the window reuse them without re-faulting ~1 GiB of
+    # huge pages (MI355X box, 4 GB torrent: 26.7 - 27.8 GB/s warm vs 19.2 - 20.0 GB/s when
+    # every job faults its buffers afresh). Idle buffers always stay inside the budget above.
     relay_pool_idle_trim_s: float = 60.0
     # Splice pipe capacity per transfer in KiB (relays, HTTP bodies to disk). 0: derived from
     # the user's pipe page budget (fs.pipe-user-pages-soft, 64 MiB by default for non-root
@@ -189,9 +194,13 @@ class DownloadConfig(BaseModel):
     # worker, or when the host lacks AVX-512 (set up on an executor thread the first time it
     # is wanted; profiles/r3_relayhash4/, r3_tail2/)
     stream_verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
-    # parts awaiting GPU digests across all jobs of the worker (each holds its part buffer
-    # until its DMA): ~128 - 160 hide the device's per-piece latency (profiles/r3_relayhash*/)
+    # parts awaiting GPU digests across all jobs of the worker: ~128 - 160 hide the device's
+    # per-piece latency (profiles/r3_relayhash*/). A part holds its host buffer (and budget)
+    # only until its DMA into an HBM slot is over.
     stream_gpu_pending: int = 160
+    # PartHasher device slots (1 GiB of HBM each): enough that a part's DMA never waits for a
+    # kernel to free a slot, which is what keeps the host buffers short-lived
+    stream_gpu_slots: int = 16
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
     # once fewer parts than this are queued, the job's remaining parts hash on the host (the
     # GPU's per-piece latency would otherwise land on the end of the job): 16 / 48 / 96 / 128

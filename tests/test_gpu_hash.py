@@ -345,3 +345,64 @@ def test_stream_torrent_auto_sets_the_device_up_lazily(run, tmp_path, make_cfg, 
         assert t["verify"] == "auto" and t["gpu_parts"] >= 1, t
         await w.stop(); await origin.stop(); await s3.stop()
     run(go(), timeout=120)
+
+
+def test_two_stream_torrents_inside_the_part_budget_on_the_device(run, tmp_path, make_cfg,
+                                                                  origin_cls):
+    """The gfx950 PartHasher under a part-buffer budget: two streamed torrents at once, 16
+    relays in flight each, 24 MiB budget. A part's bytes return to the budget when the
+    hasher notifies its DMA's end (eventfd, no waiting thread), so the pool's high-water mark
+    stays inside the budget while both jobs' parts are hashed on the device."""
+    import asyncio
+
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.ops import hashing, native
+    from downloader_amd.s3.fake_server import FakeS3
+    from downloader_amd.service.worker import Worker
+    from downloader_amd.torrent.metainfo import make_torrent
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blobs = {}
+        for j in range(2):
+            src = tmp_path / f"src{j}" / "Movie"
+            src.mkdir(parents=True)
+            data = os.urandom(40 * (1 << 20) + 777 * j)
+            (src / "m.mkv").write_bytes(data)
+            origin.blobs[f"/ws{j}/Movie/m.mkv"] = data
+            origin.blobs[f"/t/m{j}.torrent"] = make_torrent(str(src), 1 << 18,
+                                                           url_list=[origin.url(f"/ws{j}/")])
+            blobs[j] = data
+        native().relay_pool_trim()
+        native().relay_pool_reset_peak()
+        cfg = make_cfg(ep, concurrency=2, s3={"part_size": 5 << 20},
+                       download={"torrent_enable_dht": False, "stream_verify_backend": "gpu",
+                                 "stream_gpu_min_pieces": 4, "stream_gpu_tail": 0,
+                                 "torrent_stream_parallel": 16, "relay_memory_mb": 24,
+                                 "relay_pool_idle_trim_s": 0})
+        w = Worker(cfg, broker=MemoryBroker())
+        await w.start(health=False)
+        for j in range(2):
+            await w.submit(api.make_download(f"gb{j}", "http", origin.url(f"/t/m{j}.torrent")))
+        for _ in range(3000):
+            if len(w.results) >= 2:
+                break
+            await asyncio.sleep(0.02)
+        assert len(w.results) == 2
+        for r in w.results:
+            assert r.outcome == "staged", r
+            assert r.stats["torrent"]["verify"] == "gpu"
+        for j in range(2):
+            assert s3.get("triton-staging", keys.object_key(f"gb{j}", "m.mkv")) == blobs[j]
+        assert sum(r.stats["torrent"]["gpu_parts"] for r in w.results) >= 8
+        st = native().relay_pool_stats()
+        assert 0 < st["peak_bytes"] <= 24 << 20 and st["over_budget"] == 0, st
+        assert st["in_use"] == 0
+        gs = hashing.gpu_relay_stats()
+        assert gs["host_fallbacks"] == 0 and not gs["device_broken"] and gs["pending"] == 0
+        await w.stop(); await origin.stop(); await s3.stop()
+        native().relay_pool_set_budget(0)
+    run(go(), timeout=120)

@@ -426,11 +426,10 @@ def test_stream_async_part_hashing_with_host_double(run, tmp_path, make_cfg, ori
         hashing.use_part_hasher(None)
 
 
-def test_cancelled_digest_wait_still_returns_the_part_buffer(run, origin_cls):
-    """An aborted job cancels its pending ``gpu_part_digests``; a wait still queued behind
-    others in the wait pool must run anyway, or its part buffer never returns to the pool."""
-    from concurrent.futures import ThreadPoolExecutor
-
+def test_untracked_gpu_parts_still_return_their_buffers(run, origin_cls):
+    """Parts queued to the hasher return their buffers to the pool when their DMA is over,
+    whether or not anybody waits for the digests (an aborted job cancels its waits): no
+    thread blocks per part - completions come through the native eventfd."""
     from downloader_amd.ops import hashing, native
     from downloader_amd.s3.client import S3Client
     from downloader_amd.s3.fake_server import FakeS3
@@ -443,34 +442,36 @@ def test_cancelled_digest_wait_still_returns_the_part_buffer(run, origin_cls):
         origin.blobs["/p.bin"] = blob
         c = S3Client(ep, "minioadmin", "minioadmin")
         await c.ensure_bucket("b")
-        tickets = []
+        ids = []
         for i in range(3):
             _, h = await c.relay_hashed("b", f"k{i}", origin.url("/p.bin"), 0, len(blob), True,
                                         (0, len(blob), 1 << 18), gpu=True)
             assert h["gpu_ticket"] and not h["digests"]
-            tickets.append(h["gpu_ticket"])
-        assert native().relay_pool_stats()["in_use"] == 3
-        first = asyncio.ensure_future(hashing.gpu_part_digests(tickets[0]))
-        queued = [asyncio.ensure_future(hashing.gpu_part_digests(t)) for t in tickets[1:]]
+            ids.append(h["gpu_ticket"])
+        assert len(set(ids)) == 3
+        parts = [hashing.gpu_part_track(i) for i in ids]
+        waits = [asyncio.ensure_future(p.done) for p in parts]
         await asyncio.sleep(0.01)
-        for q in queued:                      # still queued behind the first wait
-            q.cancel()
-        assert len(await first) == 20 * 16
+        for w in waits[1:]:
+            w.cancel()                        # nobody asks for these digests any more
+        want = b"".join(hashlib.sha1(blob[i:i + (1 << 18)]).digest()
+                        for i in range(0, len(blob), 1 << 18))
+        assert await waits[0] == want
+        for p in parts:
+            await p.copied
+        assert native().relay_pool_stats()["in_use"] == 0
         for _ in range(300):
-            if native().relay_pool_stats()["in_use"] == 0:
+            if native().gpu_part_stats()["pending"] == 0 and hashing._gpu_parts.pending() == 0:
                 break
             await asyncio.sleep(0.02)
-        assert native().relay_pool_stats()["in_use"] == 0
+        assert native().gpu_part_stats()["pending"] == 0
+        assert hashing._gpu_parts.pending() == 0
         await c.close(); await origin.stop(); await s3.stop()
 
-    saved = hashing._part_wait_pool
     hashing.use_part_hasher(native().CpuPartHasher(0.2), 4)
-    hashing._part_wait_pool = ThreadPoolExecutor(max_workers=1)
     try:
         run(go())
     finally:
-        hashing._part_wait_pool.shutdown(wait=True)
-        hashing._part_wait_pool = saved
         hashing.use_part_hasher(None)
 
 
@@ -496,7 +497,8 @@ def test_refused_put_releases_its_queued_part(run, origin_cls):
                                     (0, len(blob), 1 << 18), gpu=True)
         assert s3.bad_digests == 1 and s3.get("b", "k") == blob
         assert native().gpu_part_stats()["submitted"] - before == 2      # refused + retry
-        assert native().relay_pool_stats()["in_use"] == 1                # the retry's lease
+        # the retry's lease ends when its DMA does, digests asked for or not
+        assert native().relay_pool_stats()["in_use"] <= 1
         digests = await hashing.gpu_part_digests(h["gpu_ticket"])
         assert digests == b"".join(hashlib.sha1(blob[i:i + (1 << 18)]).digest()
                                    for i in range(0, len(blob), 1 << 18))
@@ -655,3 +657,63 @@ def test_failed_upload_creation_leaves_no_open_upload(run, tmp_path, make_cfg, o
         assert not s3.uploads.get("triton-staging"), s3.uploads
         await w.stop(); await s3.stop(); await origin.stop()
     run(go())
+
+
+@pytest.mark.parametrize("backend", ["cpu", "gpu"])
+def test_two_streamed_torrents_stay_inside_the_part_budget(run, tmp_path, make_cfg, origin_cls,
+                                                           backend):
+    """Two streamed torrents at once, 16 relays in flight each, 5 MiB parts (6 MiB buffers):
+    unbounded they would lease 192 MiB of part buffers. Under a 24 MiB budget the native pool's
+    high-water mark (leased + idle) never passes it, no lease is granted past it, and both jobs
+    stage the exact bytes - on the host path and on the asynchronous GPU path (host double),
+    where a part's bytes return to the budget when its DMA is over."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blobs = {}
+        for j in range(2):
+            src = tmp_path / f"src{j}" / "Movie"
+            src.mkdir(parents=True)
+            data = os.urandom(40 * (1 << 20) + 4321 * j)
+            (src / "m.mkv").write_bytes(data)
+            origin.blobs[f"/ws{j}/Movie/m.mkv"] = data
+            origin.blobs[f"/t/m{j}.torrent"] = make_torrent(str(src), 1 << 18,
+                                                           url_list=[origin.url(f"/ws{j}/")])
+            blobs[j] = data
+        native().relay_pool_trim()
+        native().relay_pool_reset_peak()
+        w = _worker(make_cfg, ep, concurrency=2, s3={"part_size": 5 << 20},
+                    download={"stream_verify_backend": backend, "stream_gpu_min_pieces": 4,
+                              "stream_gpu_tail": 0, "torrent_stream_parallel": 16,
+                              "relay_memory_mb": 24, "relay_pool_idle_trim_s": 0})
+        await w.start(health=False)
+        for j in range(2):
+            await w.submit(api.make_download(f"bud{j}", "http", origin.url(f"/t/m{j}.torrent")))
+        await _wait(w, n=2, timeout=120)
+        for r in w.results:
+            assert r.outcome == "staged", r
+        for j in range(2):
+            assert s3.get("triton-staging", keys.object_key(f"bud{j}", "m.mkv")) == blobs[j]
+        st = native().relay_pool_stats()
+        assert st["budget"] == 24 << 20
+        assert 0 < st["peak_bytes"] <= 24 << 20, st
+        assert st["over_budget"] == 0, st
+        assert st["in_use"] == 0 and st["idle_bytes"] == 0      # trimmed after the last job
+        tstats = [r.stats["torrent"] for r in w.results]
+        assert sum(t["budget"]["waits"] for t in tstats) > 0     # the budget did the bounding
+        assert all(t["budget"]["peak"] <= 24 << 20 for t in tstats)
+        if backend == "gpu":
+            assert sum(t["gpu_parts"] for t in tstats) > 0
+        await w.stop(); await s3.stop(); await origin.stop()
+        native().relay_pool_set_budget(0)
+
+    if backend == "gpu":
+        hashing.use_part_hasher(native().CpuPartHasher(0.01), 4)
+    try:
+        run(go())
+    finally:
+        if backend == "gpu":
+            hashing.use_part_hasher(None)
