@@ -119,4 +119,5 @@ def make_broker(cfg, metrics=None) -> Broker:
     return AmqpBroker(url, heartbeat=cfg.broker.heartbeat_s,
                       reconnect_delay=cfg.broker.reconnect_delay_s, metrics=metrics,
                       connect_retry_s=cfg.broker.connect_retry_s, ssl_context=ctx,
-                      recover_delay=cfg.broker.recover_delay_s)
+                      recover_delay=cfg.broker.recover_delay_s,
+                      publish_retry_s=cfg.broker.publish_retry_s)

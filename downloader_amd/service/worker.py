@@ -90,7 +90,8 @@ class Worker:
             ssl_verify=cfg.tls.verify, ca_file=cfg.tls.ca_file, native_tls=cfg.tls.native)
         self.s3 = s3 or S3Client.from_config(cfg.s3, self.transports)
         self.metrics.watch_runtime(self.transports)
-        self.telemetry = telemetry or Telemetry.from_config(cfg, self.broker, self.log)
+        self.telemetry = telemetry or Telemetry.from_config(cfg, self.broker, self.log,
+                                                            self.metrics)
         self.tracer = tracer or init_tracer("downloader", cfg.trace.enabled, cfg.trace.path)
         self.services = Services(cfg, self.telemetry, self.s3, self.transports, self.metrics,
                                  self.tracer, self.log)
@@ -183,6 +184,8 @@ class Worker:
             await st.close()
         await asyncio.get_running_loop().run_in_executor(None, get_reaper(self.services).close,
                                                          drain_timeout)
+        # events of the drained jobs: flushed while the broker takes them (bounded)
+        await self.telemetry.close(timeout=2 * self.cfg.telemetry.publish_timeout_s)
         try:
             await self.broker.close()
         except Exception:

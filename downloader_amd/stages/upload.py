@@ -63,7 +63,6 @@ class UploadStage(Stage):
                 raise FileNotFoundError(f"{f} not found.")
 
         done = 0
-        lock = asyncio.Lock()
         sem = asyncio.Semaphore(max(1, self.cfg.s3.concurrent_files))
         uploaded: List[int] = []
 
@@ -84,11 +83,12 @@ class UploadStage(Stage):
                     uploaded.append(size)
                     if self.sv.metrics is not None:
                         self.sv.metrics.bytes_uploaded.inc(size)
-            async with lock:
-                done += 1
-                pct = int(done / n * 50 + 50)
-                await self.sv.telemetry.emit_progress(media_id, DOWNLOADING, pct)
-                job.emitter.emit("progress", pct)
+            # progress after each finished file (lib/upload.js:48-51): emitted outside any
+            # lock - telemetry only queues the event (service/telemetry.py)
+            done += 1
+            pct = int(done / n * 50 + 50)
+            await self.sv.telemetry.emit_progress(media_id, DOWNLOADING, pct)
+            job.emitter.emit("progress", pct)
 
         await gather_strict(*(one(i, f) for i, f in enumerate(files)))
         job.stats["uploaded_bytes"] = sum(uploaded)

@@ -107,6 +107,9 @@ class BrokerConfig(BaseModel):
     retry_backoff_s: float = 0.5
     retry_backoff_max_s: float = 30.0
     heartbeat_s: int = 30                       # AMQP heartbeat (0: off)
+    # a publish (convert job, retry, dead letter) waits this long for a lost connection to
+    # come back before it fails (amqp-connection-manager keeps retrying forever)
+    publish_retry_s: float = 120.0
     # first reconnect delay after a lost connection (doubles, max 30 s)
     reconnect_delay_s: float = 1.0
     connect_retry_s: float = 60.0               # keep retrying the first connect this long
@@ -129,6 +132,12 @@ class TelemetryConfig(BaseModel):
     enabled: bool = True                        # status / progress messages (triton-core telemetry)
     status_queue: str = "v1.telemetry.status"
     progress_queue: str = "v1.telemetry.progress"
+    # emits never wait for the broker: they go to a bounded outbox that one task flushes in
+    # order, each publish bounded by this; a failed one is retried (backoff up to
+    # retry_max_s) while newer events queue behind it
+    publish_timeout_s: float = 1.0
+    retry_max_s: float = 5.0
+    buffer_max: int = 10_000                    # outbox bound: past it the oldest is dropped
 
 
 class DownloadConfig(BaseModel):

@@ -75,6 +75,13 @@ class Metrics:
         self.key_collisions = Counter("key_collisions_total",
                                       "files whose staging key collided within a job",
                                       namespace=ns, registry=r)
+        self.telemetry_events = Counter("telemetry_events_total",
+                                        "telemetry events by fate (published, dropped from "
+                                        "the full outbox, failed publish attempts)",
+                                        ["outcome"], namespace=ns, registry=r)
+        self.telemetry_buffered = Gauge("telemetry_buffered",
+                                        "telemetry events waiting in the outbox",
+                                        namespace=ns, registry=r)
         self.messages = Counter("broker_messages_total", "broker traffic", ["queue", "op"],
                                 namespace=ns, registry=r)
         self.stale_uploads = Counter("stale_uploads_aborted_total",

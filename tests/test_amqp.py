@@ -637,3 +637,108 @@ def test_amqps_client_certificate(run, tmp_path):
         await d.ack()
         await good.close(); await srv.stop()
     run(go())
+
+
+def test_telemetry_never_stalls_a_job_during_a_broker_outage(run, make_cfg, origin_cls, tmp_path):
+    """with the telemetry broker down for 10 s, a 20-file job stages at
+    full speed - every emit only queues its event (service/telemetry.py) - and once the broker
+    is back the buffered events are published in order; failed attempts are counted in
+    downloader_telemetry_events_total. Before, each emit waited publish_retry_s (120 s) and
+    the upload stage awaited one per file."""
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api, keys
+    from downloader_amd.s3.fake_server import FakeS3
+    from downloader_amd.service.telemetry import Telemetry
+    from downloader_amd.service.worker import Worker
+    from downloader_amd.torrent.metainfo import make_torrent
+    from downloader_amd.utils.metrics import Metrics
+
+    async def go():
+        srv = await BrokerServer().start()
+        port = srv.port
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Pack"
+        src.mkdir(parents=True)
+        files = {}
+        for i in range(20):
+            d = os.urandom(50_000 + i)
+            (src / f"f{i:02d}.mkv").write_bytes(d)
+            origin.blobs[f"/ws/Pack/f{i:02d}.mkv"] = d
+            files[f"f{i:02d}.mkv"] = d
+        origin.blobs["/t/pack.torrent"] = make_torrent(str(src), 1 << 16,
+                                                      url_list=[origin.url("/ws/")])
+        tb = AmqpBroker(srv.url, reconnect_delay=0.05, max_reconnect_delay=0.5,
+                        publish_retry_s=120.0)
+        await tb.connect()
+        metrics = Metrics(registry=None)
+        cfg = make_cfg(ep, download={"torrent_enable_dht": False, "progress_interval_s": 0.05},
+                       telemetry={"publish_timeout_s": 0.5})
+        tel = Telemetry.from_config(cfg, tb, metrics=metrics)
+        w = Worker(cfg, broker=MemoryBroker(), telemetry=tel, metrics=metrics)
+        await w.start(health=False)
+        # the broker goes away for 10 s
+        await srv.stop()
+        for c in list(srv.conns):
+            c.writer.transport.abort()
+        for _ in range(250):               # a fire-and-forget publish into a socket the
+            if not tb.connected:           # client has not seen die yet would be lost
+                break
+            await asyncio.sleep(0.02)
+        assert not tb.connected
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        await w.submit(api.make_download("out", "http", origin.url("/t/pack.torrent")))
+        for _ in range(500):
+            if w.results:
+                break
+            await asyncio.sleep(0.02)
+        job_s = loop.time() - t0
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        for name, d in files.items():
+            assert s3.get("triton-staging", keys.object_key("out", name)) == d
+        assert job_s < 3.0, job_s                                   # not 20 x 120 s
+        assert r.stats["stage_s"]["upload"] < 2.0, r.stats["stage_s"]
+        assert tel.progress_of("out")[-1] == 100 and len(tel.progress_of("out")) >= 22
+        emitted = len(tel.history)
+        assert tel.buffered == emitted
+        await asyncio.sleep(max(0.0, 10.0 - (loop.time() - t0)))
+        assert metrics.sample("downloader_telemetry_events_total", outcome="failed") >= 1
+        assert metrics.sample("downloader_telemetry_buffered") == emitted
+        srv2 = BrokerServer(port=port)
+        await srv2.start()
+        assert await tel.flush(15.0), tel.buffered
+        assert tel.buffered == 0 and tel.counts["dropped"] == 0
+        assert metrics.sample("downloader_telemetry_events_total", outcome="published") == emitted
+        for _ in range(250):               # fire-and-forget: the server reads them a bit later
+            if srv2.depth("v1.telemetry.progress") == len(tel.progress_of("out")):
+                break
+            await asyncio.sleep(0.02)
+        assert srv2.depth("v1.telemetry.progress") == len(tel.progress_of("out"))
+        assert srv2.depth("v1.telemetry.status") == len(tel.statuses_of("out"))
+        await w.stop(); await tb.close(); await srv2.stop(); await s3.stop(); await origin.stop()
+    run(go(), timeout=60)
+
+
+def test_telemetry_outbox_drops_the_oldest_when_full(run):
+    """The outbox is bounded: with the broker away, past ``buffer_max`` the oldest event is
+    dropped (counted), and emit never waits."""
+    from downloader_amd.service.telemetry import Telemetry
+
+    class Down:
+        async def publish(self, *a, **k):
+            await asyncio.sleep(3600)
+
+    async def go():
+        tel = Telemetry(Down(), publish_timeout_s=0.05, buffer_max=5)
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        for i in range(12):
+            await tel.emit_progress("m", 2, i)
+        assert loop.time() - t0 < 0.05
+        assert tel.buffered == 5 and tel.counts["dropped"] == 7
+        await tel.close(timeout=0.1)
+        assert tel.buffered == 0 and tel.counts["dropped"] == 12
+    run(go())
