@@ -276,6 +276,7 @@ class S3Client:
                 retry = True
             else:
                 if 200 <= resp.status < 300 or resp.status in ok:
+                    resp.sent_checksum = (headers or {}).get("x-amz-checksum-crc32c", "")
                     return resp
                 hint = None if relocated else self._region_hint(resp, bucket)
                 if hint:                # re-sign for the bucket's region, at once
@@ -400,7 +401,8 @@ class S3Client:
             if upload_id:
                 done = await self._reusable_parts(bucket, key, upload_id, path, parts)
         if not upload_id:
-            upload_id = await self.create_multipart_upload(bucket, key, content_type)
+            upload_id = await self.create_multipart_upload(bucket, key, content_type,
+                                                           checksum=self.want_checksum())
         sem = asyncio.Semaphore(concurrency)
         etags: Dict[int, str] = dict(done)
 
@@ -498,7 +500,8 @@ class S3Client:
                                          f"(Content-Length {get.header('content-length')}) "
                                          f"for {length} bytes at {offset}", get.status)
                 if put.ok:
-                    etag = (put.header("etag") or "").strip('"')
+                    etag = PartTag.of((put.header("etag") or "").strip('"'),
+                                      getattr(put, "sent_crc32c", "") if checksum else "")
                     return etag if split is None else (etag, hashed)
                 hint = None if relocated else self._region_hint(put, bucket)
                 if hint:
@@ -557,7 +560,8 @@ class S3Client:
         upload_id, etags = (await self._resume_relay(bucket, key, journal, validator, size,
                                                      parts) if journal else (None, {}))
         if upload_id is None:
-            upload_id = await self.create_multipart_upload(bucket, key, content_type, meta)
+            upload_id = await self.create_multipart_upload(bucket, key, content_type, meta,
+                                                           checksum=crc)
             if journal:
                 await self.put_object(bucket, journal, json.dumps(
                     {"key": key, "upload_id": upload_id, "validator": validator, "size": size,
@@ -637,7 +641,8 @@ class S3Client:
         except S3Error:
             return None, {}
         want = {n: ln for n, _, ln in parts}
-        return j["upload_id"], {n: e.strip('"') for n, e, sz in held
+        return j["upload_id"], {n: PartTag.of(e.strip('"'), getattr(e, "crc32c", ""))
+                                for n, e, sz in held
                                 if want.get(n) == sz and e}
 
     async def copy_object(self, src_bucket: str, src_key: str, bucket: str, key: str, size: int,
@@ -705,8 +710,14 @@ class S3Client:
                                                                  hashed=True), gpu=gpu)
 
     async def create_multipart_upload(self, bucket: str, key: str, content_type: str = "",
-                                      meta: Optional[Dict[str, str]] = None) -> str:
+                                      meta: Optional[Dict[str, str]] = None,
+                                      checksum: bool = False) -> str:
+        """``checksum``: the parts will carry x-amz-checksum-crc32c - declared here
+        (x-amz-checksum-algorithm), since S3 refuses part checksums of a type the upload was
+        not created with."""
         hdrs = {"content-type": content_type} if content_type else {}
+        if checksum:
+            hdrs["x-amz-checksum-algorithm"] = "CRC32C"
         hdrs.update({f"x-amz-meta-{k}": v for k, v in (meta or {}).items()})
         r = await self._request("POST", bucket, key, query=[("uploads", "")],
                                 headers=hdrs or None)
@@ -714,10 +725,12 @@ class S3Client:
 
     async def upload_part(self, bucket: str, key: str, upload_id: str, num: int, body,
                           progress: Optional[Progress] = None) -> str:
+        ck = self.want_checksum()
         r = await self._request("PUT", bucket, key,
                                 query=[("partNumber", str(num)), ("uploadId", upload_id)],
-                                body=body, progress=progress, checksum=self.want_checksum())
-        return (r.header("etag") or "").strip('"')
+                                body=body, progress=progress, checksum=ck)
+        return PartTag.of((r.header("etag") or "").strip('"'),
+                          (r.sent_checksum if ck else "") or "")
 
     async def complete_multipart_upload(self, bucket: str, key: str, upload_id: str,
                                         parts: Sequence[Tuple[int, str]]) -> str:
@@ -725,7 +738,9 @@ class S3Client:
         answers NoSuchUpload because the first attempt DID complete: then the object's
         multipart ETag ("<md5 of part md5s>-<n>") is checked against the parts sent, and a
         match counts as success instead of failing a job whose object is in place."""
-        xml = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>\"{e}\"</ETag></Part>"
+        xml = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>\"{e}\"</ETag>"
+                      + (f"<ChecksumCRC32C>{e.crc32c}</ChecksumCRC32C>"
+                         if getattr(e, "crc32c", "") else "") + "</Part>"
                       for n, e in parts)
         body = f"<CompleteMultipartUpload>{xml}</CompleteMultipartUpload>".encode()
         try:
@@ -762,7 +777,9 @@ class S3Client:
             root = ET.fromstring(r.body)
             for p in root:
                 if _strip(p.tag) == "Part":
-                    out.append((int(_text(p, "PartNumber")), _text(p, "ETag").strip('"'),
+                    out.append((int(_text(p, "PartNumber")),
+                                PartTag.of(_text(p, "ETag").strip('"'),
+                                           _text(p, "ChecksumCRC32C")),
                                 int(_text(p, "Size", "0"))))
             if _text(root, "IsTruncated") != "true":
                 return out
@@ -854,6 +871,18 @@ class S3Client:
             if not token:    # truncated without a continuation token: would loop forever
                 raise S3Error("InvalidResponse", "IsTruncated without NextContinuationToken",
                               200, "", bucket)
+
+
+class PartTag(str):
+    """A part's ETag that also carries the CRC32C it was uploaded with (base64, "" = none):
+    CompleteMultipartUpload lists it as <ChecksumCRC32C> when the upload declared CRC32C."""
+    crc32c = ""
+
+    @classmethod
+    def of(cls, etag: str, crc32c: str = "") -> "PartTag":
+        t = cls(etag)
+        t.crc32c = crc32c or ""
+        return t
 
 
 def multipart_etag(part_etags: Sequence[str]) -> str:

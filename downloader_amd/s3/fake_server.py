@@ -51,6 +51,10 @@ class Upload:
     parts: Dict[int, Tuple[bytes, str]] = field(default_factory=dict)
     initiated: float = field(default_factory=time.time)
     meta: Dict[str, str] = field(default_factory=dict)
+    # x-amz-checksum-algorithm declared at CreateMultipartUpload ("" = none): a part that
+    # carries another checksum type is refused, as S3 does ("Checksum Type mismatch")
+    algorithm: str = ""
+    crcs: Dict[int, str] = field(default_factory=dict)      # part -> its CRC32C (base64)
 
 
 def _user_meta(headers) -> Dict[str, str]:
@@ -167,6 +171,8 @@ class FakeS3:
         self.corrupted = 0
         self.bad_digests = 0                    # PUTs refused: payload checksum mismatch
         self.checksummed = 0                    # PUTs that carried a payload checksum
+        self.checksum_type_mismatches = 0       # parts refused: checksum type not declared
+        self.complete_part_checksums = 0        # <ChecksumCRC32C> checked at Complete
 
     # ---------------------------------------------------------------- lifecycle
     @property
@@ -350,7 +356,7 @@ class FakeS3:
             return self._list_buckets()
         if not key:
             return self._bucket_op(req.method, bucket, q)
-        resp = self._object_op(req, bucket, key, q, body)
+        resp = self._object_op(req, bucket, key, q, body, echo)
         if echo and resp.status == 200:
             resp.headers["x-amz-checksum-crc32c"] = echo
         return resp
@@ -455,7 +461,7 @@ class FakeS3:
                     f"</IsTruncated>{nxt}{''.join(contents)}{cps}</ListBucketResult>")
 
     def _object_op(self, req: web.Request, bucket: str, key: str, q: Dict[str, str],
-                   body: bytes) -> web.Response:
+                   body: bytes, crc: str = "") -> web.Response:
         if bucket not in self.buckets:
             return _err(404, "NoSuchBucket", "", bucket)
         objs = self.buckets[bucket]
@@ -463,8 +469,11 @@ class FakeS3:
         m = req.method
         if m == "POST" and "uploads" in q:
             uid = secrets.token_hex(16)
+            algo = req.headers.get("x-amz-checksum-algorithm", "").upper()
+            if algo and algo not in ("CRC32C", "CRC32", "SHA1", "SHA256"):
+                return _err(400, "InvalidRequest", f"bad checksum algorithm {algo}", key)
             ups[uid] = Upload(key, req.headers.get("Content-Type", "application/octet-stream"),
-                              meta=_user_meta(req.headers))
+                              meta=_user_meta(req.headers), algorithm=algo)
             return _xml(f'<InitiateMultipartUploadResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
                         f"<Key>{escape(key)}</Key><UploadId>{uid}</UploadId>"
                         "</InitiateMultipartUploadResult>")
@@ -486,12 +495,23 @@ class FakeS3:
                     self.server_copies += 1
                     return _xml(f'<CopyPartResult xmlns="{XMLNS}"><ETag>&quot;{etag}&quot;</ETag>'
                                 "</CopyPartResult>")
+                if crc and up.algorithm != "CRC32C":
+                    self.checksum_type_mismatches += 1
+                    return _err(400, "InvalidRequest", "Checksum Type mismatch occurred, "
+                                f"expected checksum Type: {up.algorithm.lower() or 'null'}, "
+                                "actual checksum Type: crc32c", key)
                 etag = hashlib.md5(body).hexdigest()
                 up.parts[num] = (body, etag)
+                if crc:
+                    up.crcs[num] = crc
+                else:
+                    up.crcs.pop(num, None)
                 return web.Response(status=200, headers={"ETag": f'"{etag}"'})
             if m == "GET":
                 ps = "".join(f"<Part><PartNumber>{n}</PartNumber><ETag>&quot;{e}&quot;</ETag>"
-                             f"<Size>{len(d)}</Size></Part>"
+                             + (f"<ChecksumCRC32C>{up.crcs[n]}</ChecksumCRC32C>"
+                                if n in up.crcs else "")
+                             + f"<Size>{len(d)}</Size></Part>"
                              for n, (d, e) in sorted(up.parts.items()))
                 return _xml(f'<ListPartsResult xmlns="{XMLNS}"><Bucket>{bucket}</Bucket>'
                             f"<Key>{escape(key)}</Key><UploadId>{q['uploadId']}</UploadId>"
@@ -508,12 +528,20 @@ class FakeS3:
                 want = []
                 for p in root:
                     n = e = None
+                    ck = None
                     for c in p:
                         t = c.tag.split("}")[-1]
                         if t == "PartNumber":
                             n = int(c.text or 0)
                         elif t == "ETag":
                             e = (c.text or "").strip('"')
+                        elif t == "ChecksumCRC32C":
+                            ck = (c.text or "").strip()
+                    # a part checksum in Complete must be the one the part was stored with
+                    if ck is not None and (up.algorithm != "CRC32C" or up.crcs.get(n) != ck):
+                        return _err(400, "InvalidPart", f"part {n}: checksum", key)
+                    if ck is not None:
+                        self.complete_part_checksums += 1
                     want.append((n, e))
                 if [n for n, _ in want] != sorted(n for n, _ in want):
                     return _err(400, "InvalidPartOrder", "", key)

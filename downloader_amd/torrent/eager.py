@@ -126,7 +126,8 @@ class EagerUploader:
                     async with f.lock:
                         if not f.upload_id:
                             f.upload_id = await self.s3.create_multipart_upload(
-                                self.bucket, f.key, media_type(self.cfg, f.path))
+                                self.bucket, f.key, media_type(self.cfg, f.path),
+                                checksum=self.s3.want_checksum())
                     f.etags[num] = await self.s3.upload_part(self.bucket, f.key, f.upload_id, num,
                                                              FileRange(f.fd, off, ln))
                 self.uploaded_bytes += ln

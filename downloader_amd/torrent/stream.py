@@ -315,8 +315,9 @@ class StreamStager:
                 if t.size == 0:
                     await self.s3.put_object(self.bucket, t.key, b"", self._ctype(t))
             async def create(t: _Target) -> None:
-                t.upload_id = await self.s3.create_multipart_upload(self.bucket, t.key,
-                                                                    self._ctype(t))
+                t.upload_id = await self.s3.create_multipart_upload(
+                    self.bucket, t.key, self._ctype(t),
+                    checksum=self.s3.want_checksum(relay=True, hashed=True))
             # all creations settle before a failure propagates: abort() then sees every
             # upload that was opened (none is left behind on the bucket)
             await gather_strict(*(create(t) for t in multi), cancel=False)

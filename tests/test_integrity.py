@@ -80,6 +80,52 @@ def test_memory_disk_and_multipart_uploads_survive_corruption(run, tmp_path):
     run(go())
 
 
+def test_multipart_declares_its_checksum_algorithm(run, tmp_path, origin_cls):
+    """parts that carry x-amz-checksum-crc32c belong to an upload created with
+    x-amz-checksum-algorithm: CRC32C, and CompleteMultipartUpload lists each part's checksum.
+    FakeS3 refuses a part checksum the upload did not declare (S3's "Checksum Type mismatch")
+    and checks Complete's <ChecksumCRC32C> against the stored parts - for disk uploads,
+    relayed parts and resumed relays alike."""
+    from downloader_amd.s3.client import PartTag
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blob = os.urandom(13_000_000)
+        origin.blobs["/r.mkv"] = blob
+        c = S3Client(ep, *CREDS, part_size=5 << 20, multipart_threshold=6 << 20,
+                     checksum="always")
+        await c.ensure_bucket("b")
+        big = tmp_path / "big.bin"
+        big.write_bytes(blob)
+        await c.fput_object("b", "disk", str(big))
+        await c.relay_object("b", "relay", origin.url("/r.mkv"), len(blob))
+        for k in ("disk", "relay"):
+            assert s3.get("b", k) == blob
+        assert s3.complete_part_checksums == 6 and s3.checksum_type_mismatches == 0
+        # an upload created WITHOUT the algorithm refuses checksummed parts
+        uid = await c.create_multipart_upload("b", "legacy")
+        with pytest.raises(S3Error) as ei:
+            await c.upload_part("b", "legacy", uid, 1, b"q" * 100)
+        assert ei.value.code == "InvalidRequest" and s3.checksum_type_mismatches == 1
+        # ... and a Complete whose part checksum differs from the stored one is refused
+        uid = await c.create_multipart_upload("b", "wrong", checksum=True)
+        tag = await c.upload_part("b", "wrong", uid, 1, b"w" * 100)
+        assert isinstance(tag, PartTag) and tag.crc32c
+        with pytest.raises(S3Error) as ei:
+            await c.complete_multipart_upload("b", "wrong", uid,
+                                              [(1, PartTag.of(str(tag), "AAAAAA=="))])
+        assert ei.value.code == "InvalidPart"
+        # list_parts carries the checksums (a resumed relay completes with them)
+        parts = await c.list_parts("b", "wrong", uid)
+        assert parts[0][1].crc32c == tag.crc32c
+        assert await c.complete_multipart_upload("b", "wrong", uid, [(1, parts[0][1])])
+        assert s3.get("b", "wrong") == b"w" * 100
+        await c.close(); await origin.stop(); await s3.stop()
+    run(go())
+
+
 def test_checksum_off_stores_corruption_silently(run):
     async def go():
         s3 = FakeS3()
