@@ -9,8 +9,11 @@
 * on success or failure the session is always removed (App. A #7: the reference leaks the
   stall interval and the torrent on the stall path).
 
-``uri`` may be a magnet link, an http(s) URL of a ``.torrent`` (the reference's
-``.torrent``-over-HTTP chain, lib/download.js:143-155) or a local ``.torrent`` path.
+``uri`` may be a magnet link, a bare infohash (40 hex / 32 base32 characters, which
+webtorrent's parse-torrent accepts: it becomes a magnet with the DHT and
+``download.torrent_default_trackers`` as sources), an http(s) URL of a ``.torrent`` (the
+reference's ``.torrent``-over-HTTP chain, lib/download.js:143-155) or a local ``.torrent``
+path.
 
 A ``.torrent`` whose only source is webseeds is staged by ``torrent/stream.py`` (webseed ->
 S3 relay with in-flight piece verification, no disk) under the same watchdogs; everything
@@ -27,7 +30,7 @@ from typing import Awaitable, Callable, List, Optional
 from ..fetch.http import fetch_bytes
 from ..stages.base import DOWNLOADING, DownloadStalled, Job, Services
 from .client import TorrentClient
-from .magnet import parse_magnet
+from .magnet import parse_magnet, torrent_id_uri
 from .metainfo import Metainfo, parse_torrent
 from .session import TorrentSession
 
@@ -188,6 +191,7 @@ async def download_torrent(uri: str, job: Job, path: str, cfg, sv: Services,
                            client: Optional[TorrentClient] = None) -> int:
     d = cfg.download
     t0 = time.perf_counter()
+    uri = torrent_id_uri(uri, d.torrent_default_trackers)
     meta = await load_metainfo(uri, sv)
     if meta is not None and client is None:
         seeds = stream_webseeds(meta, job, cfg, sv)

@@ -69,6 +69,8 @@ class TorrentClient:
     def from_config(cls, cfg, transports=None, **kw) -> "TorrentClient":
         d = cfg.download
         boot = kw.pop("dht_bootstrap", None)
+        if boot is None and d.torrent_dht_bootstrap:
+            boot = [_hostport(x) for x in d.torrent_dht_bootstrap]
         return cls(transports=transports, listen_port=d.torrent_listen_port,
                    max_peers=d.torrent_max_peers, pipeline=d.torrent_request_pipeline,
                    enable_dht=d.torrent_enable_dht, verify_backend=d.verify_backend,
@@ -178,3 +180,9 @@ class TorrentClient:
 
 DEFAULT_BOOTSTRAP: List[Peer] = [("router.bittorrent.com", 6881), ("dht.transmissionbt.com", 6881),
                                  ("router.utorrent.com", 6881)]
+
+
+def _hostport(s: str) -> Peer:
+    """``host:port`` (``[v6]:port``) of a DHT bootstrap node."""
+    h, _, p = s.strip().rpartition(":")
+    return h.strip("[]"), int(p)

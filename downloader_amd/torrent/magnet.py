@@ -7,6 +7,7 @@ peer addresses, ``xl`` exact length, ``kt`` keywords."""
 from __future__ import annotations
 
 import base64
+import re
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 from urllib.parse import parse_qsl, quote, urlsplit
@@ -99,3 +100,27 @@ def parse_magnet(uri: str) -> Magnet:
         raise MagnetError("magnet URI has no urn:btih infohash")
     m.info_hash = ih
     return m
+
+
+_HEX40 = re.compile(r"[0-9a-fA-F]{40}")
+_B32 = re.compile(r"[A-Za-z2-7]{32}")
+
+
+def bare_infohash(s: str) -> Optional[bytes]:
+    """The infohash when ``s`` is nothing but one (40 hex or 32 base32 characters), as
+    parse-torrent 7 accepts it for ``client.add`` (/root/reference/yarn.lock:2519;
+    /root/reference/lib/download.js:64 passes media.sourceURI straight through)."""
+    s = s.strip()
+    if _HEX40.fullmatch(s) or _B32.fullmatch(s):
+        return parse_btih(s)
+    return None
+
+
+def torrent_id_uri(torrent_id: str, trackers: List[str] = ()) -> str:
+    """A torrent id as this backend takes it: a bare infohash becomes a magnet link with no
+    metadata source but the swarm - the DHT and the configured ``trackers`` (webtorrent's
+    ``announce`` option) - everything else is returned unchanged."""
+    ih = bare_infohash(torrent_id)
+    if ih is None:
+        return torrent_id
+    return Magnet(ih, trackers=list(trackers)).to_uri()

@@ -224,6 +224,11 @@ class DownloadConfig(BaseModel):
     torrent_listen_port: int = 0                # incoming peer connections (0: any free port)
     torrent_max_peers: int = 32
     torrent_enable_dht: bool = True             # BEP-5 mainline DHT
+    # DHT bootstrap nodes ("host:port"); empty = the public mainline routers
+    torrent_dht_bootstrap: List[str] = Field(default_factory=list)
+    # trackers announced to for a bare-infohash torrent id (it carries none itself;
+    # webtorrent's `announce` option) - the DHT finds peers either way
+    torrent_default_trackers: List[str] = Field(default_factory=list)
     torrent_enable_trackers: bool = True        # HTTP / UDP trackers
     torrent_enable_webseeds: bool = True        # BEP-19 url-list
     torrent_request_pipeline: int = 16          # 16 KiB block requests in flight per peer

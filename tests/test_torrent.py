@@ -1073,3 +1073,73 @@ def test_storage_close_waits_for_inflight_writes(tmp_path):
     with pytest.raises(OSError) as ei:
         st.write(0, b"b")
     assert ei.value.errno == errno.EBADF
+
+
+def test_bare_infohash_torrent_ids():
+    """parse-torrent 7 (/root/reference/yarn.lock:2519) accepts a bare infohash as the
+    torrent id of client.add (/root/reference/lib/download.js:64): 40 hex or 32 base32."""
+    import base64
+
+    from downloader_amd.torrent.magnet import bare_infohash, parse_magnet, torrent_id_uri
+    ih = hashlib.sha1(b"bare").digest()
+    assert bare_infohash(ih.hex()) == ih
+    assert bare_infohash(ih.hex().upper()) == ih
+    assert bare_infohash(base64.b32encode(ih).decode()) == ih
+    assert bare_infohash(base64.b32encode(ih).decode().lower()) == ih
+    for other in ("magnet:?xt=urn:btih:" + ih.hex(), "http://x/" + ih.hex() + ".torrent",
+                  "/tmp/" + ih.hex(), ih.hex()[:39], ih.hex() + "0", "z" * 40):
+        assert bare_infohash(other) is None
+        assert torrent_id_uri(other) == other
+    m = parse_magnet(torrent_id_uri(ih.hex(), ["udp://127.0.0.1:1/announce"]))
+    assert m.info_hash == ih and m.trackers == ["udp://127.0.0.1:1/announce"]
+    assert parse_magnet(torrent_id_uri(ih.hex())).trackers == []
+
+
+def test_worker_stages_a_bare_infohash_via_configured_tracker(run, tmp_path, make_cfg):
+    async def go():
+        from downloader_amd.models import api, keys
+        from downloader_amd.s3.fake_server import FakeS3
+        s3 = FakeS3()
+        ep = await s3.start()
+        tr = await Tracker().start()
+        raw, data, seeder, _ = await _seed(tmp_path, {"movie.mkv": 250_000}, trackers=[tr.http_url])
+        m = parse_torrent(raw)
+        w = _worker(make_cfg, ep, download={"torrent_default_trackers": [tr.http_url]})
+        await w.start(health=False)
+        await w.submit(api.make_download("bih", "torrent", m.info_hash.hex()))
+        await _wait_results(w)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert s3.get("triton-staging", keys.object_key("bih", "movie.mkv")) == data["movie.mkv"]
+        await w.stop(); await seeder.close(); await tr.stop(); await s3.stop()
+    run(go())
+
+
+def test_worker_stages_a_base32_infohash_via_the_dht(run, tmp_path, make_cfg):
+    """No tracker anywhere: the seeder announces on a local DHT, the worker's client finds
+    it from the base32 infohash alone (metadata over ut_metadata, then the pieces)."""
+    import base64
+
+    async def go():
+        from downloader_amd.models import api, keys
+        from downloader_amd.s3.fake_server import FakeS3
+        from downloader_amd.torrent.dht import DHTNode
+        s3 = FakeS3()
+        ep = await s3.start()
+        boot = await DHTNode(host="127.0.0.1").start()
+        raw, data, _, src = await _seed(tmp_path, {"film.mkv": 180_000})
+        seeder = TorrentClient(enable_dht=True, dht_bootstrap=[("127.0.0.1", boot.port)])
+        seeder.dht_interval = 0.5
+        await seeder.start()
+        await seeder.add_torrent(parse_torrent(raw), str(src))
+        await asyncio.sleep(1.0)
+        ih = parse_torrent(raw).info_hash
+        w = _worker(make_cfg, ep, download={"torrent_enable_dht": True,
+                                            "torrent_dht_bootstrap": [f"127.0.0.1:{boot.port}"],
+                                            "torrent_metadata_timeout_s": 30})
+        await w.start(health=False)
+        await w.submit(api.make_download("b32", "torrent", base64.b32encode(ih).decode()))
+        await _wait_results(w, timeout=45)
+        assert w.results[0].outcome == "staged", w.results[0]
+        assert s3.get("triton-staging", keys.object_key("b32", "film.mkv")) == data["film.mkv"]
+        await w.stop(); await seeder.close(); await boot.close(); await s3.stop()
+    run(go(), timeout=60)
