@@ -470,8 +470,34 @@ def pin_rank(dist: Dist, per_rank: int = 0) -> list:
     return cpus.pin_share(local, nlocal, per_rank)
 
 
+def integrity(args, checksum: str) -> str:
+    """Payload integrity of the measured uploads: ``crc32c`` when every PUT / part carries an
+    x-amz-checksum-crc32c the sink recomputes, ``none`` when the relay is spliced unchecked
+    (``s3.checksum: auto`` on a plain-http relay: bytes never cross user space)."""
+    pol = checksum or "auto"
+    if pol == "off":
+        return "none"
+    if pol == "always":
+        return "crc32c"
+    return "crc32c" if (args.tls != "off" or args.staging == "disk" or args.mode != "tuned") \
+        else "none"
+
+
+def slot_budget() -> tuple:
+    """(GPU slots of the node, CPUs one slot may use = min(mask, cgroup quota) / slots): the
+    CPU share a rank is pinned to (``pin_rank``), whatever N is."""
+    import math
+    from downloader_amd.utils import cpus
+    slots = cpus.gpu_slots()
+    mask = len(os.sched_getaffinity(0))
+    q = cpus.cgroup_cpu_quota()
+    budget = mask if q == math.inf else min(mask, max(1, math.ceil(q)))
+    return slots, budget // max(1, slots)
+
+
 def main() -> int:
     args = parse()
+    slots, slot_cpus = slot_budget()      # before pin_rank narrows the mask
     dist = Dist(args.gpus)
     pinned = pin_rank(dist, args.cpus_per_rank)
     from downloader_amd.bench.infra import Blobd, self_signed_cert
@@ -550,6 +576,12 @@ def main() -> int:
             # splice pipes created below their asked capacity (pipe page budget spent)
             "pipes_short": {"workers": tuned["pipes_short"], "of": tuned["pipes_created"]},
             "pipe_kb": args.pipe_kb_eff,
+            "pipe_budget_bytes": limits.pipe_budget_bytes(),
+            # what the headline's bytes were checked with on the way to S3 (the CRC'd relay
+            # of the same call is crc_relay_MBps)
+            "integrity": integrity(args, args.checksum),
+            "gpu_slots": slots,
+            "slot_budget_cpus": slot_cpus,
             "peers": args.peers,
             "cpus_per_rank": len(pinned) if pinned else len(os.sched_getaffinity(0)),
             "rank_cpus": [t["cpus"] for t in topo],
@@ -580,6 +612,7 @@ def main() -> int:
             line["crc_relay_p50_s"] = round(crc["p50"], 4)
             line["crc_relay_worker_cpu_s_per_GB"] = round(crc["worker_cpu_s_per_GB"], 4)
             line["crc_relay_sink_checked_puts"] = crc["sink"]["checksummed_puts"]
+            line["crc_relay_integrity"] = "crc32c"
         if ref is not None:
             line["reference_mode_MBps"] = round(ref["mbps"], 2)
             line["reference_mode_p50_s"] = round(ref["p50"], 4)

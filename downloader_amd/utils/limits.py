@@ -62,7 +62,12 @@ PIPES_PER_PROC = 16         # transfers in flight per worker process (relays, ra
 
 def pipe_budget_bytes() -> int:
     """Pipe capacity this uid may hold before new pipes shrink to two pages
-    (``fs.pipe-user-pages-soft`` x page size); 0 = unbounded (root, or no soft limit)."""
+    (``fs.pipe-user-pages-soft`` x page size); 0 = unbounded (root, or no soft limit).
+    ``STAGER_PIPE_BUDGET_BYTES`` overrides it (an operator who knows the uid's budget, or a
+    rehearsal of an unprivileged node's sizing as root)."""
+    env = os.environ.get("STAGER_PIPE_BUDGET_BYTES", "")
+    if env.strip().isdigit():
+        return int(env)
     if hasattr(os, "geteuid") and os.geteuid() == 0:
         return 0
     try:

@@ -154,6 +154,45 @@ def test_bench_four_ranks_disjoint_cpus_and_own_peers(tmp_path):
 
 
 @pytest.mark.slow
+def test_bench_eight_ranks_as_the_driver_launches_them(tmp_path):
+    """The driver's N=8 scaling launch rehearsed on CPU (gloo, 8 ranks, STAGER_GPU_SLOTS=8)
+    with the GPU boxes' unprivileged pipe budget (64 MiB for the uid): every rank pinned to
+    its own equal CPU slice, 8 distinct blobd peers, splice pipes of the size the budget math
+    predicts for 8 ranks x their worker processes with none created short, and every timed
+    object checked by its rank's sink."""
+    from downloader_amd.utils import limits
+    budget = 64 << 20
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error", STAGER_GPU_SLOTS="8",
+               STAGER_PIPE_BUDGET_BYTES=str(budget), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(REPO, "bench.py"),
+           "--gpus", "8", "--steps", "2", "--warmup", "1", "--size-mb", "2", "--jobs-per-step", "2",
+           "--no-compare-single-put", "--no-compare-crc"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout                        # rank 0 prints the one line
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 8 and j["config"]["jobs_timed"] == 8 * 2 * 2
+    assert j["gpu_slots"] == 8 and j["integrity"] == "none"
+    cpus = [set(c) for c in j["rank_cpus"]]
+    assert len(cpus) == 8
+    if len(os.sched_getaffinity(0)) >= 8:
+        assert all(cpus) and len({len(c) for c in cpus}) == 1
+        assert sum(len(c) for c in cpus) == len(set().union(*cpus))      # pairwise disjoint
+        assert j["cpus_per_rank"] == j["slot_budget_cpus"]
+    peers = j["rank_peers"]
+    assert len(peers) == 8 and all(peers) and len(set(peers)) == 8
+    nproc = j["procs_per_rank"]
+    want = limits.pipe_size(0, sharers=8 * nproc, per_proc=j["concurrency_per_worker"] * 2 + 2,
+                            budget=budget) >> 10
+    assert j["pipe_budget_bytes"] == budget and j["pipe_kb"] == want
+    assert j["pipes_short"]["workers"] == 0
+    assert j["timed_sink_bytes"] >= 8 * 2 * 2 * 2_000_000 and j["sink_mismatches"] == 0
+    assert j["sink_verified_objects"] >= 8 * 2 * 2
+
+
+@pytest.mark.slow
 def test_bench_rank_with_two_worker_processes(tmp_path):
     """--procs-per-rank 2: the rank spawns two worker processes, splits the timed jobs, and
     still prints exactly one JSON line whose byte count the S3 peer confirmed."""
