@@ -59,10 +59,10 @@ def parse() -> argparse.Namespace:
     p.add_argument("--concurrency", type=int, default=4,
                    help="jobs in flight per worker process (4: with 2-part multipart jobs this "
                         "keeps 16 relays in flight per rank - 70.3 GB/s, p50 11 ms vs 49.3 GB/s, "
-                        "27 ms at 8: profiles/r3_mp_sweep)")
+                        "27 ms at 8: profiles/archive/r3_mp_sweep)")
     p.add_argument("--jobs-per-step", type=int, default=64,
                    help="jobs per worker per step (64: ~1 s timed at N=1 for 10 steps; 16/32/64 "
-                        "give the same MB/s, profiles/s2_r1/jobs_ab.jsonl)")
+                        "give the same MB/s, profiles/archive/s2_r1/jobs_ab.jsonl)")
     p.add_argument("--stage-dir", default="", help="download_path (default: a temp dir)")
     p.add_argument("--http-streams", type=int, default=0, help="override download.http_streams")
     p.add_argument("--part-mb", type=int, default=0, help="override s3.part_size (MiB)")
@@ -453,7 +453,7 @@ def pin_rank(dist: Dist, per_rank: int = 0) -> list:
     of the allowed CPUs: no cross-rank cache thrash, and sockets/threads stay on a few CCDs
     of one NUMA node instead of migrating over the whole mask (build box: 256 CPUs in the
     mask, 16-CPU quota; 35.8 - 37.6 GB/s pinned vs 23.5 - 28.7 GB/s unpinned,
-    profiles/bench_pinning_r1.jsonl).
+    profiles/archive/bench_pinning_r1.jsonl).
 
     ``per_rank`` 0 = auto: the rank's GPU slot share, min(mask, quota) / visible GPUs
     (``utils.cpus.pin_slot``) - NOT divided by the number of ranks, so a rank owns the same
@@ -611,6 +611,8 @@ def main() -> int:
             line["crc_relay_MBps"] = round(crc["mbps"], 2)
             line["crc_relay_p50_s"] = round(crc["p50"], 4)
             line["crc_relay_worker_cpu_s_per_GB"] = round(crc["worker_cpu_s_per_GB"], 4)
+            # the sink recomputes every CRC (recv + CRC instead of splice) on the same CPUs
+            line["crc_relay_peer_cpu_s_per_GB"] = round(crc["peer_cpu_s_per_GB"], 4)
             line["crc_relay_sink_checked_puts"] = crc["sink"]["checksummed_puts"]
             line["crc_relay_integrity"] = "crc32c"
         if ref is not None:

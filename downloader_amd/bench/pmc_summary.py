@@ -1,4 +1,4 @@
-"""Summarise a rocprofv3 ``--pmc`` CSV of the SHA-1 kernels (``scripts/gpu_r2_pmc.sh``).
+"""Summarise a rocprofv3 ``--pmc`` CSV of the SHA-1 kernels (``scripts/archive/gpu_r2_pmc.sh``).
 
 Groups dispatches by kernel (template arguments kept, so the prefetch / bitop3 variants stay
 apart) and grid size, and derives per-wave VALU instruction counts and the fraction of wave

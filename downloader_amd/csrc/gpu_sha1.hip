@@ -10,7 +10,7 @@
 //     v_bitop3 for parity/majority, plus the message schedule). Each lane loads block k+1
 //     into registers while it hashes block k (sha1_run16): without that every block waited
 //     for its own global loads and one wave per SIMD had nothing to hide the wait with.
-//     Measured (profiles/r2_kpf, kernel A/B in one process): ~58 MB/s per lane with the
+//     Measured (profiles/archive/r2_kpf, kernel A/B in one process): ~58 MB/s per lane with the
 //     prefetch vs ~43 MB/s without (1.37x; ~2,600 cycles per block, 95 % of the 4-cycle
 //     VALU issue bound), so throughput is pieces-in-flight x 58 MB/s: ~930 GB/s at 16k
 //     pieces (one wave per CU - a quarter of the SIMDs), ~234 GB/s

@@ -98,6 +98,19 @@ def build_blobd(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
+def build_relaybench(force: bool = False, verbose: bool = True) -> Path:
+    """Per-byte CPU of the relay modes (csrc/relaybench.cpp): the copy / CRC floor."""
+    srcs = [CSRC / "relaybench.cpp"]
+    BIN.mkdir(exist_ok=True)
+    out = BIN / "relaybench"
+    if force or _stale(out, srcs + [CSRC / "crc32c.h"]):
+        cxx = os.environ.get("CXX", "g++")
+        cmd = [cxx, "-O3", "-std=c++17", "-march=x86-64-v3", "-Wall", str(srcs[0]),
+               "-lpthread", "-o", str(out)]
+        _run(cmd, verbose)
+    return out
+
+
 SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"],
               "tsan": ["-fsanitize=thread"]}
 
@@ -122,6 +135,8 @@ def build_all(force: bool = False, verbose: bool = True, gpu: bool = True) -> No
     build_native(force, verbose)
     if (CSRC / "blobd.cpp").exists():
         build_blobd(force, verbose)
+    if (CSRC / "relaybench.cpp").exists():
+        build_relaybench(force, verbose)
     if gpu and (CSRC / "gpu_sha1.hip").exists():
         if not (ROCM / "bin" / "hipcc").exists():
             raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")

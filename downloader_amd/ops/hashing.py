@@ -2,7 +2,7 @@
 (gfx950 SHA-1) backends.
 
 ``verify_backend=auto`` follows measurements on the MI355X box (EPYC 9575F, 16-CPU quota,
-``profiles/s2_r1/``): with the 16-lane multi-buffer SHA-1 the host verifies a 4 GiB recheck at
+``profiles/archive/s2_r1/``): with the 16-lane multi-buffer SHA-1 the host verifies a 4 GiB recheck at
 57-62 GB/s vs 41-52 GB/s for the chunk-streamed gfx950 path (both bound by reading the bytes,
 the GPU additionally by the pinned H2D hop), and a disk-staged 20 GB torrent at 13.1-13.8 vs
 12.3-13.0 GB/s with less worker CPU. So auto keeps SHA-1 on the host whenever it has AVX-512

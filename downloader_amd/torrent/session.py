@@ -38,7 +38,7 @@ from .tracker import decode_compact, encode_compact, supported as tracker_suppor
 # ~100 ms whatever its size (a lane hashes a 4 MiB piece serially), so a short job pays that as
 # a tail. Measured on the build box with OpenSSL host hashing: 4 GB single file 6.7 GB/s host
 # vs 5.0 GB/s GPU; 20 GB / 50 files 12.1 vs 14.7 GB/s. With the AVX-512 multi-buffer SHA-1
-# the host wins both (20 GB: 13.1-13.8 vs 12.3-13.0 GB/s, profiles/s2_r1/verify_ab.jsonl), so
+# the host wins both (20 GB: 13.1-13.8 vs 12.3-13.0 GB/s, profiles/archive/s2_r1/verify_ab.jsonl), so
 # auto uses the GPU only on hosts without it (``hashing.auto_may_use_gpu``).
 GPU_INCREMENTAL_MIN_BYTES = 8 << 30
 

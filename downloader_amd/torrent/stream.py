@@ -19,7 +19,7 @@ bytes need not land on disk at all:
 
 Files the selector drops are never fetched (apart from gap bytes). Measured on the build box:
 page-cache writes of ONE file top out at ~8 GB/s (inode lock, page allocation; tmpfs is
-slower still, ``profiles/s2_r1/stage_fs.jsonl``), which capped the 4 GB single-file config.
+slower still, ``profiles/archive/s2_r1/stage_fs.jsonl``), which capped the 4 GB single-file config.
 """
 from __future__ import annotations
 
@@ -119,7 +119,7 @@ def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
     """Parts awaiting GPU digests, shared by every stream stager of the process (one per
     event loop): the device needs ~128 - 160 parts in flight to hide its per-piece latency,
     whether they come from one job or several. Since round 4 such a part holds no host memory
-    once its DMA is over - only HBM (profiles/r3_relayhash3/ for the count)."""
+    once its DMA is over - only HBM (profiles/archive/r3_relayhash3/ for the count)."""
     loop = asyncio.get_running_loop()
     sem = _gpu_pending_sems.get(loop)
     if sem is None:
@@ -415,7 +415,7 @@ class StreamStager:
         share the worker, or when this job has more parts than the host-hashed tail - config
         4 on the MI355X box, steady reps: one job 26.3 - 28.0 GB/s at 6.5 - 6.6 worker CPU-s
         with the last 96 parts on the host vs 24.8 - 25.4 at 7.7 - 8.2 all on the host, two
-        jobs 26.5 - 28.4 vs 23.7 - 25.5 at 13 - 14 vs 17 - 18 CPU-s (profiles/r3_tail2/)."""
+        jobs 26.5 - 28.4 vs 23.7 - 25.5 at 13 - 14 vs 17 - 18 CPU-s (profiles/archive/r3_tail2/)."""
         return not self._host_mb or _active_stagers >= 2 or self._n_parts > self.gpu_tail
 
     def _gpu_sem(self) -> Optional[asyncio.Semaphore]:

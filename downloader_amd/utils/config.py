@@ -201,10 +201,10 @@ class DownloadConfig(BaseModel):
     # continuation)
     # auto: the GPU for jobs with more parts than stream_gpu_tail, when stream jobs share the
     # worker, or when the host lacks AVX-512 (set up on an executor thread the first time it
-    # is wanted; profiles/r3_relayhash4/, r3_tail2/)
+    # is wanted; profiles/archive/r3_relayhash4/, r3_tail2/)
     stream_verify_backend: Literal["cpu", "gpu", "auto"] = "auto"
     # parts awaiting GPU digests across all jobs of the worker: ~128 - 160 hide the device's
-    # per-piece latency (profiles/r3_relayhash*/). A part holds its host buffer (and budget)
+    # per-piece latency (profiles/archive/r3_relayhash*/). A part holds its host buffer (and budget)
     # only until its DMA into an HBM slot is over.
     stream_gpu_pending: int = 160
     # PartHasher device slots (1 GiB of HBM each): enough that a part's DMA never waits for a
@@ -214,7 +214,7 @@ class DownloadConfig(BaseModel):
     # once fewer parts than this are queued, the job's remaining parts hash on the host (the
     # GPU's per-piece latency would otherwise land on the end of the job): 16 / 48 / 96 / 128
     # / 160 gave 21.2 - 21.8 / 22.7 - 23.6 / 25.0 - 29.1 / 25.7 - 28.5 / 24.4 - 27.5 GB/s
-    # for one 20 GB job vs 22.7 - 25.4 on the host (profiles/r3_tail*/)
+    # for one 20 GB job vs 22.7 - 25.4 on the host (profiles/archive/r3_tail*/)
     stream_gpu_tail: int = 96
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op

@@ -106,7 +106,7 @@ def apply_pipe_size(pipe_kb: int = 0, sharers: int = 4) -> int:
         return 0
     main = pipe_size(pipe_kb, sharers)
     # the tee() duplicate pipe as large as the main one: 38.7 - 38.8 vs 32.1 - 35.6 GB/s for
-    # the CRC'd headline at 1 MiB vs 256 KiB (profiles/r3_teepipe/)
+    # the CRC'd headline at 1 MiB vs 256 KiB (profiles/archive/r3_teepipe/)
     tee_kb = int(os.environ.get("STAGER_TEE_PIPE_KB", "0") or 0)     # A/B knob
     n.set_pipe_sizes(main, tee_kb << 10 if tee_kb > 0 else main)
     return main

@@ -49,7 +49,7 @@ def test_kernel_ab_timings(gv):
 
 
 def test_kernel_prefetch_keeps_its_speedup(gv):
-    """Perf guard for the block prefetch (profiles/r2_kpf: 1.37x per lane, A/B in one
+    """Perf guard for the block prefetch (profiles/archive/r2_kpf: 1.37x per lane, A/B in one
     process, so box-to-box variance cancels)."""
     pf, nopf = gv.kernel_bench_prefetch(1 << 20, 4096, 2)
     assert nopf / pf > 1.15, (pf, nopf)

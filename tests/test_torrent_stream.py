@@ -557,7 +557,7 @@ def test_stream_verify_auto_uses_the_device_when_it_pays(run, tmp_path, make_cfg
                                                          origin_cls, jobs, tail):
     """``stream_verify_backend: auto`` with a hasher ready: a job with no more parts than the
     host-hashed tail stays on the host; jobs with parts beyond the tail - alone or two at
-    once - send those parts to the device (profiles/r3_relayhash4/, r3_tail2/)."""
+    once - send those parts to the device (profiles/archive/r3_relayhash4/, r3_tail2/)."""
     from downloader_amd.ops import hashing, native
 
     async def go():
