@@ -231,6 +231,10 @@ PYBIND11_MODULE(_native, m) {
      "fs.pipe-user-pages-soft, is spent), leased / idle and their capacity");
   m.def("set_pipes_refused", &set_pipes_refused,
         "tests: refuse every splice pipe as if the user's pipe budget were spent");
+  m.def("set_relay_dup", &set_relay_dup, py::arg("mode"),
+        "relays that need the bytes (CRC, piece hashing): 'peek' (recv(MSG_PEEK) + splice, one "
+        "pipe) or 'tee' (tee() into a second pipe)");
+  m.def("relay_dup_mode", &relay_dup_mode);
   m.def("set_pipe_sizes", &set_pipe_sizes, py::arg("main"), py::arg("tee") = 0,
         "capacity asked for new splice pipes and tee() duplicate pipes (0 = keep)");
   m.def("relay_pool_stats", []() {

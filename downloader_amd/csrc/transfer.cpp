@@ -774,7 +774,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
   if (ssl_ || dst.ssl_ || (crc && !relay_tee_on())) return relay_copy(dst, n, moved, prog, crc);
   if (crc) {
     thread_local std::vector<uint8_t> cbuf(256 * 1024);   // L2-resident CRC staging
-    int64_t m = relay_tee(
+    int64_t m = relay_dup(
         dst, n, moved, prog,
         [&](size_t& len) {
           len = std::min(len, cbuf.size());
@@ -934,6 +934,111 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
   return moved;
 }
 
+// STAGER_RELAY_DUP=tee (or set_relay_dup("tee")): the tee() duplicate instead of
+// recv(MSG_PEEK) (A/B knob).
+static std::atomic<int> g_relay_peek{[] {
+  const char* e = getenv("STAGER_RELAY_DUP");
+  return (e && strcmp(e, "tee") == 0) ? 0 : 1;
+}()};
+static bool relay_peek_on() { return g_relay_peek.load(std::memory_order_relaxed) != 0; }
+
+template <class Room, class Got>
+int64_t HttpConn::relay_dup(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
+                            Room&& room, Got&& got) {
+  return relay_peek_on() ? relay_peek(dst, n, moved, prog, room, got)
+                         : relay_tee(dst, n, moved, prog, room, got);
+}
+
+// recv(MSG_PEEK) copies the next bytes of the receive queue into the caller's memory without
+// consuming them, then exactly those bytes are spliced socket -> pipe -> socket: the S3 leg
+// still moves page references, the one copy is the peek, and only one pipe is leased (the
+// tee() path needs a second one, which a uid's 64 MiB pipe budget feels at 8 ranks).
+template <class Room, class Got>
+int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
+                             Room&& room, Got&& got) {
+  std::unique_ptr<PipeLease> main_l;
+  try {
+    main_l.reset(new PipeLease(g_pipe_main.load()));
+  } catch (const IoError&) {
+    return -1;                       // no pipe to be had: the caller copies (recv + send)
+  }
+  PipeLease& main = *main_l;
+  auto fail = [&](const char* what) {
+    reusable_ = false;
+    dst.reusable_ = false;
+    throw IoError(errstr(what));
+  };
+  // bytes that arrived with the response head
+  while (moved < n && rpos_ < rend_) {
+    size_t len = (size_t)std::min<int64_t>(n - moved, (int64_t)(rend_ - rpos_));
+    uint8_t* p = room(len);
+    memcpy(p, rbuf_.data() + rpos_, len);
+    rpos_ += len;
+    got(p, len);
+    try {
+      dst.send_all(p, len);
+    } catch (...) {
+      reusable_ = false;
+      throw;
+    }
+    moved += (int64_t)len;
+    if (prog) prog->bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
+  }
+  while (moved < n) {
+    if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("cancelled");
+    }
+    size_t len = (size_t)std::min<int64_t>(n - moved, (int64_t)main.p.cap);
+    uint8_t* p = room(len);
+    ssize_t k = ::recv(fd_, p, len, MSG_PEEK);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError("recv timeout");
+      }
+      fail("recv(peek)");
+    }
+    if (k == 0) {
+      reusable_ = false;
+      dst.reusable_ = false;
+      throw IoError("source closed mid-body");
+    }
+    got(p, (size_t)k);
+    for (ssize_t left = k; left > 0;) {
+      // the peeked bytes are queued already: this splice moves them without waiting
+      ssize_t in = ::splice(fd_, nullptr, main.p.w, nullptr, (size_t)left,
+                            SPLICE_F_MOVE | SPLICE_F_MORE);
+      if (in < 0) {
+        if (errno == EINTR) continue;
+        fail("splice(src)");
+      }
+      if (in == 0) {
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError("source closed mid-body");
+      }
+      for (ssize_t chunk = in; chunk > 0;) {
+        ssize_t out = ::splice(main.p.r, nullptr, dst.fd_, nullptr, (size_t)chunk,
+                               SPLICE_F_MOVE | SPLICE_F_MORE);
+        if (out < 0) {
+          if (errno == EINTR) continue;
+          fail("splice(dst)");
+        }
+        chunk -= out;
+      }
+      left -= in;
+    }
+    moved += k;
+    if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
+  }
+  main.clean = true;
+  return moved;
+}
+
 int64_t HttpConn::relay_copy(HttpConn& dst, int64_t n, int64_t moved, Progress* prog,
                              uint32_t* crc) {
   thread_local std::vector<uint8_t> buf(256 * 1024);
@@ -1010,7 +1115,7 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
     }
   };
   if (!ssl_ && !dst.ssl_ && relay_tee_on() &&
-      relay_tee(
+      relay_dup(
           dst, n, 0, prog,
           [&](size_t& len) {
             len = std::min(len, buf.size());
@@ -1608,6 +1713,12 @@ std::vector<GpuPartEvent> gpu_part_poll() {
   return out;
 }
 
+void set_relay_dup(const std::string& mode) {
+  if (mode != "peek" && mode != "tee") throw std::invalid_argument("relay dup mode: peek or tee");
+  g_relay_peek.store(mode == "peek" ? 1 : 0);
+}
+std::string relay_dup_mode() { return relay_peek_on() ? "peek" : "tee"; }
+
 size_t relay_pool_trim(size_t keep_bytes) { return part_pool().trim(keep_bytes); }
 PipeStats pipe_stats() { return pipe_pool().stats(); }
 void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
@@ -1635,7 +1746,7 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
   uint8_t* b = lease.b->data;
   int64_t pos = 0;
   if (!ssl_ && !dst.ssl_ && relay_tee_on()) {
-    relay_tee(
+    relay_dup(
         dst, n, 0, prog,
         [&](size_t& len) {
           len = std::min<size_t>(len, (size_t)(n - pos));

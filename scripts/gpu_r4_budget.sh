@@ -9,6 +9,19 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 F=${OUT:-gpurun_out/r4_budget}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp
+# resident memory HIP itself adds to a worker: RSS before / after the PartHasher's set-up
+timeout -k 10 120 python -c "
+import resource
+def rss(): return int(open('/proc/self/statm').read().split()[1]) * 4096 >> 20
+from downloader_amd.ops import native, gpuhash
+native(); a = rss()
+g = gpuhash(); b = rss()
+ph = g.PartHasher(0, 1 << 30, 16, 4, 16384); c = rss()
+native().set_gpu_part_hasher(ph.api(), 8); d = rss()
+print({'rss_MiB_modules': a, 'after_import_gpuhash': b, 'after_parthasher': c, 'after_install': d,
+       'peak_MiB': resource.getrusage(resource.RUSAGE_SELF).ru_maxrss >> 10})
+" > $F/hip_rss.txt 2>&1 || { cat $F/hip_rss.txt; exit 1; }
+cat $F/hip_rss.txt
 for mb in ${BUDGETS:-1024 2048 4096}; do
   for jobs in 1 2; do
     for pair in 1 2 3; do

@@ -454,11 +454,13 @@ def test_blobd_sink_detects_wrong_torn_and_reordered_objects(sink):
         assert st["verify_objects"] == 5 and st["verify_mismatches"] == 3, st
 
 
+@pytest.mark.parametrize("dup", ["peek", "tee"])
 @pytest.mark.parametrize("main_kb,tee_kb", [(64, 64), (1024, 64), (64, 1024)])
-def test_teed_relays_with_small_and_uneven_pipes(run, origin_cls, main_kb, tee_kb):
-    """The CRC'd and piece-hashed relays splice through a pipe and read a tee()d duplicate:
-    with small or uneven pipes a chunk is duplicated, read and sent in several rounds - the
-    CRC the sink checks and the piece digests must still cover exactly the bytes sent."""
+def test_teed_relays_with_small_and_uneven_pipes(run, origin_cls, main_kb, tee_kb, dup):
+    """The CRC'd and piece-hashed relays splice through a pipe and copy the same bytes out -
+    peeked from the socket (default) or read from a tee()d duplicate: with small or uneven
+    pipes a chunk is copied and sent in several rounds - the CRC the sink checks and the piece
+    digests must still cover exactly the bytes sent."""
     from downloader_amd.ops import native
 
     async def go():
@@ -485,7 +487,9 @@ def test_teed_relays_with_small_and_uneven_pipes(run, origin_cls, main_kb, tee_k
 
     n = native()
     n.set_pipe_sizes(main_kb << 10, tee_kb << 10)
+    n.set_relay_dup(dup)
     try:
         run(go())
     finally:
+        n.set_relay_dup("peek")
         n.set_pipe_sizes(1 << 20, 256 << 10)
