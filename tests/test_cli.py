@@ -179,6 +179,21 @@ def test_k8s_manifest_matches_the_cli_and_probes():
     assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
     src = open(os.path.join(REPO, "downloader_amd", "service", "health.py")).read()
     assert '"/readyz"' in src and '"/healthz"' in src and '"/metrics"' in src
+    # memory: the request covers every worker's worst case - fixed part (interpreter, native
+    # modules, HIP runtime) + its part-buffer budget, which the worker derives from the limit
+    from downloader_amd.utils import membudget
+
+    def gib(q: str) -> float:
+        assert q.endswith("Gi"), q
+        return float(q[:-2])
+    n = int(c["command"][c["command"].index("-n") + 1])
+    res = c["resources"]
+    limit, request = gib(res["limits"]["memory"]), gib(res["requests"]["memory"])
+    budget = limit / n * cfg.download.relay_memory_fraction
+    assert cfg.download.relay_memory_mb == 0          # the budget follows the limit
+    assert request >= n * (2.3 + budget), (request, n, budget)
+    assert limit >= request
+    assert membudget.MIN_BUDGET <= budget * (1 << 30)
 
 
 def test_concurrent_builds_never_leave_a_broken_binary(tmp_path):
