@@ -1,0 +1,69 @@
+"""Summarise a rocprofv3 ``--kernel-trace`` CSV: per kernel, launches, duration statistics and
+the grid size (threads) per launch - for ``sha1_lanes`` one thread is one piece (lane), so
+the grid tells how many pieces each launch hashed in parallel - plus the concurrency of the
+launches (how many overlap in time).
+
+    python -m downloader_amd.bench.trace_summary <kernel_trace.csv> [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import statistics
+import sys
+from typing import Dict, List
+
+
+def summarise(path: str) -> Dict[str, dict]:
+    rows: Dict[str, List[dict]] = {}
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name", "")
+            short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+            rows.setdefault(short, []).append(r)
+    out: Dict[str, dict] = {}
+    for k, rs in rows.items():
+        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rs]
+        grid = [int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) for r in rs]
+        spans = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rs)
+        # max launches running at once
+        ev = sorted([(s, 1) for s, _ in spans] + [(e, -1) for _, e in spans])
+        cur = peak = 0
+        for _, d in ev:
+            cur += d
+            peak = max(peak, cur)
+        busy = 0
+        last = 0
+        for s, e in spans:              # union of the launches' intervals
+            s = max(s, last)
+            if e > s:
+                busy += e - s
+                last = e
+        wall = (spans[-1][1] - spans[0][0]) if spans else 0
+        out[k] = {"launches": len(rs), "ms_mean": round(statistics.mean(dur), 3),
+                  "ms_min": round(min(dur), 3), "ms_max": round(max(dur), 3),
+                  "ms_total": round(sum(dur), 1),
+                  "grid_threads_mean": round(statistics.mean(grid), 1),
+                  "grid_threads_min": min(grid), "grid_threads_max": max(grid),
+                  "max_concurrent": peak,
+                  "device_busy_share": round(busy / wall, 3) if wall else 0.0}
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--json", default="")
+    a = ap.parse_args(argv)
+    s = summarise(a.trace)
+    txt = json.dumps(s, indent=1)
+    if a.json:
+        with open(a.json, "w") as f:
+            f.write(txt + "\n")
+    print(txt)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -538,3 +538,21 @@ def test_transfers_copy_when_no_pipe_can_be_had(run, origin_cls):
     finally:
         n.set_pipes_refused(False)
     assert n.pipe_stats()["created"] == before and n.pipe_stats()["in_use"] == 0
+
+
+def test_trace_summary_counts_lanes_and_overlap(tmp_path):
+    """bench/trace_summary.py on a rocprofv3 kernel-trace CSV: launches, duration stats,
+    grid threads per launch (lanes for sha1_lanes) and the peak of overlapping launches."""
+    from downloader_amd.bench.trace_summary import summarise
+    hdr = ('"Kind","Kernel_Name","Start_Timestamp","End_Timestamp","Grid_Size_X",'
+           '"Grid_Size_Y"\n')
+    rows = [('void (anonymous namespace)::sha1_lanes<16>(unsigned char const*, long)', 0, 10_000_000, 128),
+            ('void (anonymous namespace)::sha1_lanes<16>(unsigned char const*, long)', 5_000_000, 20_000_000, 256),
+            ('__amd_rocclr_copyBuffer', 30_000_000, 30_000_100, 512)]
+    p = tmp_path / "t.csv"
+    p.write_text(hdr + "".join(f'"KERNEL_DISPATCH","{n}",{s},{e},{g},1\n' for n, s, e, g in rows))
+    s = summarise(str(p))
+    k = s["sha1_lanes<16>"]
+    assert k["launches"] == 2 and k["grid_threads_min"] == 128 and k["grid_threads_max"] == 256
+    assert k["max_concurrent"] == 2 and k["ms_max"] == 15.0 and k["device_busy_share"] == 1.0
+    assert s["__amd_rocclr_copyBuffer"]["launches"] == 1
