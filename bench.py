@@ -59,7 +59,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--concurrency", type=int, default=4,
                    help="jobs in flight per worker process (4: with 2-part multipart jobs this "
                         "keeps 16 relays in flight per rank - 70.3 GB/s, p50 11 ms vs 49.3 GB/s, "
-                        "27 ms at 8: profiles/archive/r3_mp_sweep)")
+                        "27 ms at 8: profiles/archive/r3_mp_sweep); lowered when the uid's pipe "
+                        "budget could not give every relay a 512 KiB pipe (utils/limits.relay_plan)")
     p.add_argument("--jobs-per-step", type=int, default=64,
                    help="jobs per worker per step (64: ~1 s timed at N=1 for 10 steps; 16/32/64 "
                         "give the same MB/s, profiles/archive/s2_r1/jobs_ab.jsonl)")
@@ -525,11 +526,13 @@ def main() -> int:
     if args.mode == "reference" and args.procs_per_rank <= 0:
         nproc = 1    # the reference is one serial consumer per container (explicit N: N of them)
     # Splice pipes: every worker process on the node shares one uid's pipe page budget
-    # (64 MiB for the unprivileged user of the GPU boxes); size them for world x procs workers
-    # with concurrency x 2 parts (+2 spare) relays each, or take --pipe-kb as given.
+    # (64 MiB for the unprivileged user of the GPU boxes); each relay in flight holds one.
     from downloader_amd.utils import limits
-    args.pipe_kb_eff = args.pipe_kb or limits.pipe_size(
-        0, sharers=dist.world * nproc, per_proc=args.concurrency * 2 + 2) >> 10
+    if args.pipe_kb:
+        args.pipe_kb_eff = args.pipe_kb
+    else:
+        args.concurrency, pipe = limits.relay_plan(args.concurrency, 2, dist.world * nproc)
+        args.pipe_kb_eff = pipe >> 10
     try:
         tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
         single = None

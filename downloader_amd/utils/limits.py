@@ -96,6 +96,36 @@ def pipe_size(pipe_kb: int = 0, sharers: int = 4, per_proc: int = PIPES_PER_PROC
     return size
 
 
+PIPE_GOOD = 512 << 10       # pipes this large relay within ~2 % of 1 MiB ones; 256 KiB cost 13 %
+
+
+def relay_plan(concurrency: int, parts_per_job: int, sharers: int,
+               budget: int = -1) -> tuple:
+    """(jobs in flight per process, pipe bytes) for ``sharers`` processes of one uid, each
+    running ``concurrency`` jobs of ``parts_per_job`` relays (one pipe each): the largest pipe
+    (<= 1 MiB) that fits 7/8 of the uid's pipe budget, lowering the concurrency (to 2 at
+    least) while the pipe would be smaller than 512 KiB. MI355X box, one 16-CPU rank
+    (profiles/r4/pipes/): 1 MiB 66.7 / 66.1 GB/s, 512 KiB 63.2 / 65.8, 512 KiB at 3 jobs
+    67.7 / 62.2, 256 KiB 53.6 / 62.5 - so at 8 ranks x 2 processes (64 MiB budget) 3 jobs on
+    512 KiB pipes beat 4 jobs on 256 KiB ones."""
+    if budget < 0:
+        budget = pipe_budget_bytes()
+    if budget == 0:
+        return concurrency, PIPE_MAX
+    usable = budget * 7 // 8
+    conc = max(1, concurrency)
+
+    def size_for(c: int) -> int:
+        share = usable // max(1, sharers) // max(1, c * parts_per_job)
+        size = PIPE_MIN
+        while size * 2 <= min(share, PIPE_MAX):
+            size *= 2
+        return size
+    while conc > 2 and size_for(conc) < PIPE_GOOD:
+        conc -= 1
+    return conc, size_for(conc)
+
+
 def apply_pipe_size(pipe_kb: int = 0, sharers: int = 4) -> int:
     """Size the native transport's splice pipes (main and tee() duplicate alike);
     returns the main size, 0 without the native module."""

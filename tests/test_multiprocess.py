@@ -184,9 +184,10 @@ def test_bench_eight_ranks_as_the_driver_launches_them(tmp_path):
     peers = j["rank_peers"]
     assert len(peers) == 8 and all(peers) and len(set(peers)) == 8
     nproc = j["procs_per_rank"]
-    want = limits.pipe_size(0, sharers=8 * nproc, per_proc=j["concurrency_per_worker"] * 2 + 2,
-                            budget=budget) >> 10
-    assert j["pipe_budget_bytes"] == budget and j["pipe_kb"] == want
+    conc, pipe = limits.relay_plan(4, 2, 8 * nproc, budget)
+    assert j["pipe_budget_bytes"] == budget
+    assert (j["concurrency_per_worker"], j["pipe_kb"]) == (conc, pipe >> 10)
+    assert pipe >= limits.PIPE_GOOD
     assert j["pipes_short"]["workers"] == 0
     assert j["timed_sink_bytes"] >= 8 * 2 * 2 * 2_000_000 and j["sink_mismatches"] == 0
     assert j["sink_verified_objects"] >= 8 * 2 * 2

@@ -556,3 +556,20 @@ def test_trace_summary_counts_lanes_and_overlap(tmp_path):
     assert k["launches"] == 2 and k["grid_threads_min"] == 128 and k["grid_threads_max"] == 256
     assert k["max_concurrent"] == 2 and k["ms_max"] == 15.0 and k["device_busy_share"] == 1.0
     assert s["__amd_rocclr_copyBuffer"]["launches"] == 1
+
+
+def test_relay_plan_keeps_pipes_at_512k_under_the_uid_budget():
+    """bench.py's splice plan for N ranks x 2 processes on a 64 MiB uid pipe budget: 1 MiB
+    pipes while they fit, 512 KiB at 4 ranks, and at 8 ranks 3 jobs per process on 512 KiB
+    pipes rather than 4 on 256 KiB (measured 13 % slower); root / no budget: unchanged."""
+    from downloader_amd.utils.limits import PIPE_GOOD, PIPE_MAX, relay_plan
+    b = 64 << 20
+    assert relay_plan(4, 2, 2, b) == (4, PIPE_MAX)
+    assert relay_plan(4, 2, 4, b) == (4, PIPE_MAX)
+    assert relay_plan(4, 2, 8, b) == (4, PIPE_GOOD)
+    assert relay_plan(4, 2, 16, b) == (3, PIPE_GOOD)
+    for sharers in (2, 4, 8, 16):
+        c, p = relay_plan(4, 2, sharers, b)
+        assert sharers * c * 2 * p <= b * 7 // 8
+    assert relay_plan(4, 2, 64, b)[0] == 2                # never below 2 jobs
+    assert relay_plan(4, 2, 16, 0) == (4, PIPE_MAX)
