@@ -546,8 +546,8 @@ def test_trace_summary_counts_lanes_and_overlap(tmp_path):
     from downloader_amd.bench.trace_summary import summarise
     hdr = ('"Kind","Kernel_Name","Start_Timestamp","End_Timestamp","Grid_Size_X",'
            '"Grid_Size_Y"\n')
-    rows = [('void (anonymous namespace)::sha1_lanes<16>(unsigned char const*, long)', 0, 10_000_000, 128),
-            ('void (anonymous namespace)::sha1_lanes<16>(unsigned char const*, long)', 5_000_000, 20_000_000, 256),
+    k16 = 'void (anonymous namespace)::sha1_lanes<16>(unsigned char const*, long)'
+    rows = [(k16, 0, 10_000_000, 128), (k16, 5_000_000, 20_000_000, 256),
             ('__amd_rocclr_copyBuffer', 30_000_000, 30_000_100, 512)]
     p = tmp_path / "t.csv"
     p.write_text(hdr + "".join(f'"KERNEL_DISPATCH","{n}",{s},{e},{g},1\n' for n, s, e, g in rows))
