@@ -1432,6 +1432,7 @@ void gpu_copied(const GpuPartHashApi* a, uint64_t ticket, uint64_t id) {
   part_pool().release(std::move(buf));
   std::lock_guard<std::mutex> g(g_gpu_mu);
   auto it = g_gpu_parts.find(id);
+  if (it == g_gpu_parts.end()) return;   // only a finished part is ever erased: not this one
   GpuPending& p = it->second;
   p.copied = true;
   if (rc != 0) {            // the hasher forgets a job whose copy failed: no DONE follows

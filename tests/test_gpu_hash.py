@@ -241,6 +241,45 @@ def test_part_hasher_batches_concurrent_parts(part_hasher):
     assert 1 <= launches < 48 and st["max_batch_lanes"] > 18 and not st["broken"], st
 
 
+def _disp_threads():
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                if f.read().strip() == "gpu-part-disp":
+                    with open(f"/proc/self/task/{tid}/stat") as g:
+                        st = g.read().rsplit(")", 1)[1].split()
+                    out[tid] = (int(st[11]) + int(st[12])) / os.sysconf("SC_CLK_TCK")
+        except OSError:
+            pass
+    return out
+
+
+def test_part_hasher_dispatcher_idles_while_every_slot_is_busy():
+    """with every device slot busy, queued parts used to keep the dispatcher thread
+    spinning on its lock and hipEventQuery. 2 slots of one 4 MiB piece each, one stream, 16
+    parts from 16 threads: ~1 s of kernels with parts waiting for a slot most of the time -
+    the dispatcher must sleep between polls (its CPU well under the wall time)."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    from downloader_amd.ops import gpuhash
+    before = set(_disp_threads())
+    h = gpuhash().PartHasher(0, 4 << 20, 2, 1, 64)
+    tid = next(t for t in _disp_threads() if t not in before)
+    parts = [os.urandom(4 << 20) for _ in range(16)]
+    cpu0, t0 = _disp_threads()[tid], time.perf_counter()
+    with ThreadPoolExecutor(16) as ex:
+        got = list(ex.map(lambda d: h.hash(d, 4 << 20), parts))
+    wall = time.perf_counter() - t0
+    cpu = _disp_threads()[tid] - cpu0
+    assert got == [ref(d, 4 << 20) for d in parts]
+    st = h.stats()
+    assert st["launches"] >= 8 and not st["broken"], st
+    assert wall > 0.3 and cpu < 0.35 * wall, (cpu, wall)
+    del h
+
+
 @pytest.mark.parametrize("corrupt", [False, True])
 def test_stream_torrent_with_gpu_relay_hashing(run, tmp_path, make_cfg, origin_cls, corrupt):
     """Webseed torrent staged webseed -> S3 with the relayed parts' pieces hashed by the
