@@ -573,3 +573,71 @@ def test_relay_plan_keeps_pipes_at_512k_under_the_uid_budget():
         assert sharers * c * 2 * p <= b * 7 // 8
     assert relay_plan(4, 2, 64, b)[0] == 2                # never below 2 jobs
     assert relay_plan(4, 2, 16, 0) == (4, PIPE_MAX)
+
+
+def test_part_budget_fifo_oversize_and_cancellation(run):
+    """utils/membudget.PartBudget: grants in arrival order (a big request is not starved by
+    later small ones), a request larger than the whole budget runs alone, and a cancelled
+    waiter neither leaks bytes nor blocks the ones behind it."""
+    import asyncio
+
+    from downloader_amd.utils.membudget import BUFFER_ALIGN, PartBudget, buffer_bytes
+    MiB = 1 << 20
+    assert buffer_bytes(1) == BUFFER_ALIGN and buffer_bytes(5 * MiB) == 6 * MiB
+
+    async def go():
+        b = PartBudget(8 * MiB)
+        a = await b.acquire(6 * MiB)                 # 6 of 8 used
+        order = []
+
+        async def want(tag, n):
+            got = await b.acquire(n)
+            order.append(tag)
+            return got
+        big = asyncio.ensure_future(want("big", 4 * MiB))
+        await asyncio.sleep(0)
+        small = asyncio.ensure_future(want("small", 2 * MiB))   # would fit now, but queues
+        await asyncio.sleep(0.01)
+        assert order == [] and b.stats()["queued"] == 2
+        b.release(a)                                   # big first, then small fits too
+        await asyncio.gather(big, small)
+        assert order == ["big", "small"] and b.used == 6 * MiB
+        b.release(4 * MiB)
+        b.release(2 * MiB)
+        huge = await b.acquire(20 * MiB)               # alone: granted past the capacity
+        assert b.used == 20 * MiB
+        w1 = asyncio.ensure_future(b.acquire(2 * MiB))
+        w2 = asyncio.ensure_future(b.acquire(2 * MiB))
+        await asyncio.sleep(0.01)
+        w1.cancel()
+        await asyncio.sleep(0)
+        b.release(huge)
+        assert await w2 == 2 * MiB and b.used == 2 * MiB
+        assert w1.cancelled() and b.stats()["queued"] == 0 and b.peak == 20 * MiB
+    run(go())
+
+
+def test_relay_budget_follows_the_memory_limit(monkeypatch):
+    from downloader_amd.utils import membudget
+    from downloader_amd.utils.config import DownloadConfig
+    MiB = 1 << 20
+    monkeypatch.setattr(membudget, "memory_limit", lambda: 32 << 30)
+    monkeypatch.setenv("STAGER_POOL_WORKERS", "2")
+    assert membudget.relay_budget_bytes(DownloadConfig()) == 4 << 30          # 32 / 2 / 4
+    assert membudget.relay_budget_bytes(DownloadConfig(relay_memory_mb=300)) == 300 * MiB
+    monkeypatch.setattr(membudget, "memory_limit", lambda: 256 * MiB)
+    assert membudget.relay_budget_bytes(DownloadConfig()) == membudget.MIN_BUDGET
+
+
+def test_cgroup_memory_limit_v1_v2(tmp_path):
+    from downloader_amd.utils.membudget import cgroup_memory_limit
+    (tmp_path / "memory.max").write_text("max\n")
+    assert cgroup_memory_limit(str(tmp_path)) == 0
+    (tmp_path / "memory.max").write_text("34359738368\n")
+    assert cgroup_memory_limit(str(tmp_path)) == 32 << 30
+    v1 = tmp_path / "v1"
+    (v1 / "memory").mkdir(parents=True)
+    (v1 / "memory" / "memory.limit_in_bytes").write_text("9223372036854771712\n")   # unlimited
+    assert cgroup_memory_limit(str(v1)) == 0
+    (v1 / "memory" / "memory.limit_in_bytes").write_text("8589934592\n")
+    assert cgroup_memory_limit(str(v1)) == 8 << 30
