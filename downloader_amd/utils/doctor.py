@@ -3,7 +3,8 @@
 What a worker's throughput depends on besides its config, checked in one place: the native
 extension and which SIMD paths it runs (AVX-512 multi-buffer SHA-1, VPCLMULQDQ CRC32C), the
 usable CPUs (affinity and cgroup quota), the open-file limit (one descriptor per torrent file),
-the uid's pipe page budget that splice transfers share (fs.pipe-user-pages-soft), transparent
+the uid's pipe page budget that splice transfers share (fs.pipe-user-pages-soft), the memory
+limit and the streamed relay's part-buffer budget derived from it, transparent
 huge pages for the relay's part buffers, and the HIP devices for the gfx950 kernels. Each
 finding that costs performance comes with a warning saying what to change.
 """
@@ -57,6 +58,21 @@ def report(pipe_sharers: int = 4) -> Dict[str, Any]:
     if budget and size < (256 << 10):
         warn.append(f"splice pipes of {size >> 10} KiB for {pipe_sharers} workers of this uid: "
                     "raise fs.pipe-user-pages-soft or run fewer workers per uid")
+
+    from . import membudget
+    from .config import DownloadConfig
+    lim = membudget.memory_limit()
+    part = membudget.relay_budget_bytes(DownloadConfig())
+    out["memory"] = {"limit_bytes": lim or None,
+                     "cgroup_limit_bytes": membudget.cgroup_memory_limit() or None,
+                     "workers": membudget.pool_workers(),
+                     "part_budget_bytes": part,
+                     # docs/OPERATIONS.md "Memory": fixed part + HIP runtime + part budget
+                     "worst_case_worker_bytes": part + int(2.3e9)}
+    if lim and membudget.pool_workers() * (part + int(2.3e9)) > lim:
+        warn.append(f"{membudget.pool_workers()} workers x ({part >> 20} MiB part budget + "
+                    f"~2.3 GB) exceed the memory limit of {lim >> 20} MiB: lower "
+                    "download.relay_memory_mb or run fewer workers")
 
     thp = _read("/sys/kernel/mm/transparent_hugepage/enabled")
     out["thp"] = thp

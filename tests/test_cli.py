@@ -222,4 +222,6 @@ def test_doctor_reports_host_readiness():
                                                                "sse4.2-3way")
     assert d["pipes"]["sharers"] == 8 and d["pipes"]["pipe_bytes"] >= 64 << 10
     assert d["cpus"]["effective"] >= 1 and isinstance(d["warnings"], list)
+    m = d["memory"]
+    assert m["part_budget_bytes"] > 0 and m["worst_case_worker_bytes"] > m["part_budget_bytes"]
     assert "devices" in d["gpu"]
