@@ -205,6 +205,10 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["relay_memory_mb"] = a.relay_memory_mb
             if getattr(a, "stream_gpu_slots", 0):
                 dl["stream_gpu_slots"] = a.stream_gpu_slots
+            if getattr(a, "gpu_copy_streams", 0):
+                dl["stream_gpu_copy_streams"] = a.gpu_copy_streams
+            if getattr(a, "gpu_compute_streams", 0):
+                dl["stream_gpu_compute_streams"] = a.gpu_compute_streams
             part_mb = getattr(a, "part_mb", 0)
             s3o = {"part_size": part_mb << 20} if part_mb else {}
             if getattr(a, "checksum", ""):
@@ -652,6 +656,10 @@ def main(argv=None) -> int:
                     help="configs 3/4: download.relay_memory_mb (part-buffer budget per worker)")
     ap.add_argument("--stream-gpu-slots", type=int, default=0,
                     help="configs 3/4: download.stream_gpu_slots (PartHasher HBM slots)")
+    ap.add_argument("--gpu-copy-streams", type=int, default=0,
+                    help="configs 3/4: download.stream_gpu_copy_streams")
+    ap.add_argument("--gpu-compute-streams", type=int, default=0,
+                    help="configs 3/4: download.stream_gpu_compute_streams (0: the queues left)")
     ap.add_argument("--no-gpu-prewarm", action="store_true",
                     help="do not init the GPU verifier at worker start (download.gpu_prewarm)")
     ap.add_argument("--retry-backoff-s", type=float, default=0.05,

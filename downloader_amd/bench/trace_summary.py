@@ -3,7 +3,8 @@ the grid size (threads) per launch - for ``sha1_lanes`` one thread is one piece 
 the grid tells how many pieces each launch hashed in parallel - plus the concurrency of the
 launches (how many overlap in time).
 
-    python -m downloader_amd.bench.trace_summary <kernel_trace.csv> [--json out.json]
+    python -m downloader_amd.bench.trace_summary <kernel_trace.csv> [--copies
+        <memory_copy_trace.csv>] [--json out.json]
 """
 from __future__ import annotations
 
@@ -51,12 +52,46 @@ def summarise(path: str) -> Dict[str, dict]:
     return out
 
 
+def summarise_copies(path: str) -> Dict[str, dict]:
+    """A rocprofv3 ``--memory-copy-trace`` CSV: per direction, copies, duration statistics,
+    bytes and GB/s when the trace has a size column, and the peak of overlapping copies
+    (copies on separate SDMA engines run at once)."""
+    rows: Dict[str, List[dict]] = {}
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            rows.setdefault(r.get("Direction", r.get("Operation", "?")), []).append(r)
+    out: Dict[str, dict] = {}
+    for k, rs in rows.items():
+        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rs]
+        size_key = next((c for c in rs[0] if c.lower() in ("size", "bytes", "copy_bytes")), None)
+        d = {"copies": len(rs), "ms_mean": round(statistics.mean(dur), 3),
+             "ms_median": round(statistics.median(dur), 3), "ms_max": round(max(dur), 3)}
+        if size_key:
+            sizes = [int(r[size_key]) for r in rs]
+            big = [(b, t) for b, t in zip(sizes, dur) if b >= 1 << 20 and t > 0]
+            d["bytes"] = sum(sizes)
+            if big:
+                d["GBps_median_1MiB_plus"] = round(statistics.median(b / t / 1e6 for b, t in big), 2)
+        ev = sorted([(int(r["Start_Timestamp"]), 1) for r in rs] +
+                    [(int(r["End_Timestamp"]), -1) for r in rs])
+        cur = peak = 0
+        for _, x in ev:
+            cur += x
+            peak = max(peak, cur)
+        d["max_concurrent"] = peak
+        out[k] = d
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
+    ap.add_argument("--copies", default="", help="a memory_copy_trace.csv as well")
     ap.add_argument("--json", default="")
     a = ap.parse_args(argv)
     s = summarise(a.trace)
+    if a.copies:
+        s["memory_copies"] = summarise_copies(a.copies)
     txt = json.dumps(s, indent=1)
     if a.json:
         with open(a.json, "w") as f:

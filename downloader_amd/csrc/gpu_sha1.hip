@@ -811,21 +811,35 @@ class GpuVerifier {
 //     slot keeps filling, so batches grow with the arrival rate (self-balancing: at R bytes/s
 //     and T = per-piece kernel time over Q streams, a batch holds ~R*T/Q bytes);
 //   * digests return with one D2H per slot; waiters are woken per ticket.
-// Compute streams are capped at 4 = GPU_MAX_HW_QUEUES (more would share hardware queues and
-// serialise). A HIP error marks the hasher broken: queued and later parts are refused or
-// failed, and the relay falls back to the host multi-buffer SHA-1.
+// Copy streams + compute streams fit in GPU_MAX_HW_QUEUES (4) hardware queues: a stream that
+// shares its queue serialises behind the other's packets, so a copy stream next to a compute
+// stream saw its copy-done markers wait for 77 ms kernels (round 3: 1 copy + 4 compute).
+// A HIP error marks the hasher broken: queued and later parts are refused or failed, and the
+// relay falls back to the host multi-buffer SHA-1.
 class PartHasher {
  public:
-  PartHasher(int device, int64_t slot_bytes, int slots, int streams, int max_lanes)
+  PartHasher(int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
+             int copy_streams = 1)
       : device_(device), slot_bytes_(slot_bytes), max_lanes_(max_lanes) {
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) throw std::runtime_error("no such HIP device");
-    if (slots < 2 || streams < 1 || slot_bytes < (1 << 20) || max_lanes < 64)
+    if (slots < 2 || slot_bytes < (1 << 20) || max_lanes < 64 ||
+        copy_streams < 1 || copy_streams > 4)
       throw std::invalid_argument("PartHasher: bad geometry");
     HIP_CHECK(hipSetDevice(device_));
-    HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
-    streams_.resize((size_t)std::min(streams, 4));
+    // Parts are DMA'd round-robin over copy_streams streams: each is its own hardware queue,
+    // so H2D copies of consecutive parts run on separate SDMA engines instead of queueing
+    // behind one another (a part's host buffer is held until its copy ends).
+    copies_.resize((size_t)copy_streams);
+    for (auto& c : copies_) HIP_CHECK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    // Every HIP stream is mapped onto one of GPU_MAX_HW_QUEUES (4) hardware queues; a copy
+    // stream that shares a queue with a compute stream has its copy-completion marker wait
+    // behind a ~77 ms sha1_lanes kernel, and the part's host buffer with it. streams <= 0:
+    // as many compute streams as the queues left over by the copy streams.
+    const int hwq = hw_queues();
+    const int compute = streams > 0 ? std::min(streams, 4) : std::max(1, hwq - copy_streams);
+    streams_.resize((size_t)compute);
     for (auto& st : streams_) {
       HIP_CHECK(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
       st.slot = -1;
@@ -838,7 +852,7 @@ class PartHasher {
       HIP_CHECK(hipHostMalloc((void**)&sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
                               hipHostMallocDefault));
       HIP_CHECK(hipHostMalloc((void**)&sl.h_dig, (size_t)max_lanes_ * 20, hipHostMallocDefault));
-      HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+      for (auto& e : sl.copied) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     }
     api_.abi = GPU_PART_API_ABI;
@@ -869,25 +883,31 @@ class PartHasher {
     cv_.notify_all();
     if (thread_.joinable()) thread_.join();
     hipSetDevice(device_);
-    hipStreamSynchronize(copy_);
+    for (auto c : copies_) hipStreamSynchronize(c);
     for (auto& st : streams_) {
       hipStreamSynchronize(st.s);
       hipStreamDestroy(st.s);
     }
-    hipStreamDestroy(copy_);
+    for (auto c : copies_) hipStreamDestroy(c);
     for (auto& sl : slots_) {
       hipFree(sl.d_data);
       hipFree(sl.d_lane);
       hipFree(sl.d_dig);
       hipHostFree(sl.h_lane);
       hipHostFree(sl.h_dig);
-      hipEventDestroy(sl.copied);
+      for (auto e : sl.copied) hipEventDestroy(e);
       hipEventDestroy(sl.done);
     }
     for (hipEvent_t e : free_events_) hipEventDestroy(e);
   }
 
   const GpuPartHashApi* api() const { return &api_; }
+
+  static int hw_queues() {
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    const int n = e ? atoi(e) : 0;
+    return n > 0 ? n : 4;            // HIP's default
+  }
 
   int reg(void* p, size_t n) {
     if (hipSetDevice(device_) != hipSuccess) return -1;
@@ -957,6 +977,8 @@ class PartHasher {
     d["registered"] = registered_;       // part buffers page-locked (hipHostRegister)
     d["unregistered"] = unregistered_;
     d["register_s"] = reg_seconds_;
+    d["copy_streams"] = copies_.size();
+    d["compute_streams"] = streams_.size();
     return d;
   }
 
@@ -976,7 +998,8 @@ class PartHasher {
     uint8_t* d_dig = nullptr;
     int64_t* h_lane = nullptr;   // [off x max_lanes][len x max_lanes]
     uint8_t* h_dig = nullptr;
-    hipEvent_t copied = nullptr, done = nullptr;
+    hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};   // one per copy stream
+    hipEvent_t done = nullptr;
     int64_t used = 0;
     int lanes = 0;
     bool align16 = true;
@@ -1056,7 +1079,7 @@ class PartHasher {
             const int64_t off = (f.used + 255) & ~(int64_t)255;
             if (off + j->len > slot_bytes_ || f.lanes + j->np > max_lanes_) {
               f.state = 2;                    // full: closed, launched when a stream frees
-              HIP_CHECK(hipEventRecord(f.copied, copy_));
+              close_copies(f);
               filling = -1;
             }
           }
@@ -1073,10 +1096,11 @@ class PartHasher {
           }
           Slot& f = slots_[(size_t)filling];
           const int64_t off = (f.used + 255) & ~(int64_t)255;
+          hipStream_t cs = copies_[next_copy_++ % copies_.size()];
           HIP_CHECK(hipMemcpyAsync(f.d_data + off, j->host, (size_t)j->len, hipMemcpyHostToDevice,
-                                   copy_));
+                                   cs));
           j->copy_ev = take_event();
-          HIP_CHECK(hipEventRecord(j->copy_ev, copy_));
+          HIP_CHECK(hipEventRecord(j->copy_ev, cs));
           j->slot = filling;
           j->lane0 = f.lanes;
           for (int k = 0; k < j->np; ++k) {
@@ -1097,15 +1121,19 @@ class PartHasher {
           std::lock_guard<std::mutex> g(mu_);
           for (auto it = fresh.rbegin(); it != fresh.rend(); ++it) queue_.push_front(*it);
         }
-        // 2. completed copies: the relay may reuse those buffers
-        while (!copying.empty()) {
+        // 2. completed copies: the relay may reuse those buffers (copies on different
+        // streams finish out of order: every pending one is checked)
+        for (auto it = copying.begin(); it != copying.end();) {
           Job* j;
           {
             std::lock_guard<std::mutex> g(mu_);
-            j = &jobs_.at(copying.front());
+            j = &jobs_.at(*it);
           }
           hipError_t q = hipEventQuery(j->copy_ev);
-          if (q == hipErrorNotReady) break;
+          if (q == hipErrorNotReady) {
+            ++it;
+            continue;
+          }
           HIP_CHECK(q);
           {
             std::lock_guard<std::mutex> g(mu_);
@@ -1114,8 +1142,8 @@ class PartHasher {
             j->copy_ev = nullptr;
           }
           wcv_.notify_all();
-          copied_now.push_back(copying.front());
-          copying.pop_front();
+          copied_now.push_back(*it);
+          it = copying.erase(it);
           progressed = true;
         }
         tell(copied_now, GPU_PART_COPIED);
@@ -1147,7 +1175,7 @@ class PartHasher {
           int pick = oldest(2);
           if (pick < 0 && filling >= 0 && slots_[(size_t)filling].lanes > 0) {
             pick = filling;
-            HIP_CHECK(hipEventRecord(slots_[(size_t)pick].copied, copy_));
+            close_copies(slots_[(size_t)pick]);
             filling = -1;
           }
           if (pick < 0) break;
@@ -1166,9 +1194,10 @@ class PartHasher {
         }
       }
     } catch (const std::exception& e) {
-      // DMAs already queued on copy_ may still read part buffers: let them end before any
-      // waiter learns of the failure and hands its buffer back to the pool (which may unmap it)
-      hipStreamSynchronize(copy_);
+      // DMAs already queued on the copy streams may still read part buffers: let them end
+      // before any waiter learns of the failure and hands its buffer back to the pool (which
+      // may unmap it)
+      for (auto c : copies_) hipStreamSynchronize(c);
       std::vector<uint64_t> failed_copy, failed_hash;
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -1209,9 +1238,14 @@ class PartHasher {
     return best;
   }
 
+  // A slot's parts went over any of the copy streams: mark the end of what each has queued.
+  void close_copies(Slot& sl) {
+    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipEventRecord(sl.copied[k], copies_[k]));
+  }
+
   void launch(int si, Stream& st) {
     Slot& sl = slots_[(size_t)si];
-    HIP_CHECK(hipStreamWaitEvent(st.s, sl.copied, 0));
+    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipStreamWaitEvent(st.s, sl.copied[k], 0));
     HIP_CHECK(hipMemcpyAsync(sl.d_lane, sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
                              hipMemcpyHostToDevice, st.s));
     const int block = 64, grid = (sl.lanes + block - 1) / block;
@@ -1235,7 +1269,8 @@ class PartHasher {
   int device_;
   int64_t slot_bytes_;
   int max_lanes_;
-  hipStream_t copy_ = nullptr;
+  std::vector<hipStream_t> copies_;
+  size_t next_copy_ = 0;
   std::vector<Stream> streams_;
   std::vector<Slot> slots_;
   std::vector<hipEvent_t> free_events_;
@@ -1354,12 +1389,13 @@ PYBIND11_MODULE(_gpuhash, m) {
           "(ms_prefetch, ms_no_prefetch): kernel time per launch, device-resident data")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
   py::class_<PartHasher>(m, "PartHasher")
-      .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes) {
+      .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
+                       int copy_streams) {
              py::gil_scoped_release rel;
-             return new PartHasher(device, slot_bytes, slots, streams, max_lanes);
+             return new PartHasher(device, slot_bytes, slots, streams, max_lanes, copy_streams);
            }),
            py::arg("device") = 0, py::arg("slot_bytes") = (int64_t)1 << 30, py::arg("slots") = 8,
-           py::arg("streams") = 4, py::arg("max_lanes") = 16384)
+           py::arg("streams") = 0, py::arg("max_lanes") = 16384, py::arg("copy_streams") = 1)
       .def(
           "api",
           [](PartHasher& h) {

@@ -130,7 +130,8 @@ PART_SLOTS = 16
 
 
 def gpu_relay_hashing(min_pieces: int = 8, slots: int = PART_SLOTS,
-                      slot_bytes: int = PART_SLOT_BYTES) -> bool:
+                      slot_bytes: int = PART_SLOT_BYTES, copy_streams: int = 1,
+                      compute_streams: int = 0) -> bool:
     """Route the hashed relay's parts to the gfx950 ``PartHasher`` (batched, one lane per
     piece; csrc/gpu_sha1.hip) instead of the host multi-buffer SHA-1. Created once per
     process on the worker's GPU; False (host hashing) when no HIP device is usable."""
@@ -141,7 +142,8 @@ def gpu_relay_hashing(min_pieces: int = 8, slots: int = PART_SLOTS,
         if _part_hasher_failed or not gpu_available():
             return False
         try:
-            ph = gpuhash().PartHasher(gpu_device(), int(slot_bytes), int(slots), 4, 16384)
+            ph = gpuhash().PartHasher(gpu_device(), int(slot_bytes), int(slots),
+                                      int(compute_streams), 16384, int(copy_streams))
             native().set_gpu_part_hasher(ph.api(), min_pieces)
         except Exception:
             _part_hasher_failed = True

@@ -146,8 +146,11 @@ class Worker:
         try:
             if not await loop.run_in_executor(None, gpu_available):
                 return
-            ok = await loop.run_in_executor(None, hashing.gpu_relay_hashing,
-                                            d.stream_gpu_min_pieces, d.stream_gpu_slots)
+            ok = await loop.run_in_executor(
+                None, lambda: hashing.gpu_relay_hashing(
+                    d.stream_gpu_min_pieces, d.stream_gpu_slots,
+                    copy_streams=d.stream_gpu_copy_streams,
+                    compute_streams=d.stream_gpu_compute_streams))
             self.log.info({"gpu_part_hasher": ok}, "gpu relay hashing prewarm")
         except Exception as e:  # a broken device must not stop the worker
             self.log.warn({"err": str(e)}, "gpu relay hashing prewarm failed")

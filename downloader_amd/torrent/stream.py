@@ -130,7 +130,8 @@ def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
 _gpu_init_started = False
 
 
-def start_gpu_init(min_pieces: int, slots: int = 16) -> None:
+def start_gpu_init(min_pieces: int, slots: int = 16, copy_streams: int = 1,
+                   compute_streams: int = 0) -> None:
     """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and the device
     slots take a moment; the event loop keeps relaying meanwhile). Once per process; a
     missing device or a failed init leaves every part on the host."""
@@ -142,7 +143,9 @@ def start_gpu_init(min_pieces: int, slots: int = 16) -> None:
 
     def init() -> bool:
         from ..ops import gpu_available
-        return gpu_available() and hashing.gpu_relay_hashing(min_pieces, slots)
+        return gpu_available() and hashing.gpu_relay_hashing(min_pieces, slots,
+                                                             copy_streams=copy_streams,
+                                                             compute_streams=compute_streams)
     fut = asyncio.get_running_loop().run_in_executor(None, init)
     fut.add_done_callback(lambda f: f.cancelled() or f.exception())   # retrieved
 
@@ -239,6 +242,8 @@ class StreamStager:
         self.verify_mode = getattr(d, "stream_verify_backend", "cpu") if gpu_pending > 0 else "cpu"
         self._min_pieces = int(getattr(d, "stream_gpu_min_pieces", 8) or 8)
         self._gpu_dev_slots = int(getattr(d, "stream_gpu_slots", 16) or 16)
+        self._gpu_copy_streams = int(getattr(d, "stream_gpu_copy_streams", 1) or 1)
+        self._gpu_compute_streams = int(getattr(d, "stream_gpu_compute_streams", 0) or 0)
         # parts still queued below which the rest hash on the host
         self.gpu_tail = int(getattr(d, "stream_gpu_tail", 0) or 0)
         self._n_parts = sum(1 for u in self.units if u.target is not None)
@@ -309,7 +314,8 @@ class StreamStager:
         except Exception:
             pass
         if self.verify_mode == "auto" and self._gpu_wanted():
-            start_gpu_init(self._min_pieces, self._gpu_dev_slots)
+            start_gpu_init(self._min_pieces, self._gpu_dev_slots, self._gpu_copy_streams,
+                           self._gpu_compute_streams)
         try:
             for t in self.targets:
                 if t.size == 0:
@@ -667,7 +673,10 @@ def _gpu_relay_on(cfg) -> Optional[str]:
         return None
     try:
         if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8),
-                                     getattr(d, "stream_gpu_slots", 16)):
+                                     getattr(d, "stream_gpu_slots", 16),
+                                     copy_streams=getattr(d, "stream_gpu_copy_streams", 1),
+                                     compute_streams=getattr(d, "stream_gpu_compute_streams",
+                                                             0)):
             return None
         return "no usable HIP device"
     except Exception as e:

@@ -210,6 +210,11 @@ class DownloadConfig(BaseModel):
     # PartHasher device slots (1 GiB of HBM each): enough that a part's DMA never waits for a
     # kernel to free a slot, which is what keeps the host buffers short-lived
     stream_gpu_slots: int = 16
+    # PartHasher streams: copy streams for the parts' DMAs, compute streams for the kernels
+    # (0 = the hardware queues the copy streams leave, GPU_MAX_HW_QUEUES = 4 by default): a
+    # copy stream sharing a hardware queue with a compute stream waits behind its kernels
+    stream_gpu_copy_streams: int = 1
+    stream_gpu_compute_streams: int = 0
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
     # once fewer parts than this are queued, the job's remaining parts hash on the host (the
     # GPU's per-piece latency would otherwise land on the end of the job): 16 / 48 / 96 / 128

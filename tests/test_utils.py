@@ -600,7 +600,8 @@ def test_part_budget_fifo_oversize_and_cancellation(run):
         await asyncio.sleep(0.01)
         assert order == [] and b.stats()["queued"] == 2
         b.release(a)                                   # big first, then small fits too
-        await asyncio.gather(big, small)
+        await big
+        await small
         assert order == ["big", "small"] and b.used == 6 * MiB
         b.release(4 * MiB)
         b.release(2 * MiB)
