@@ -819,7 +819,7 @@ class GpuVerifier {
 class PartHasher {
  public:
   PartHasher(int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
-             int copy_streams = 1)
+             int copy_streams = 2)
       : device_(device), slot_bytes_(slot_bytes), max_lanes_(max_lanes) {
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
@@ -1395,7 +1395,7 @@ PYBIND11_MODULE(_gpuhash, m) {
              return new PartHasher(device, slot_bytes, slots, streams, max_lanes, copy_streams);
            }),
            py::arg("device") = 0, py::arg("slot_bytes") = (int64_t)1 << 30, py::arg("slots") = 8,
-           py::arg("streams") = 0, py::arg("max_lanes") = 16384, py::arg("copy_streams") = 1)
+           py::arg("streams") = 0, py::arg("max_lanes") = 16384, py::arg("copy_streams") = 2)
       .def(
           "api",
           [](PartHasher& h) {

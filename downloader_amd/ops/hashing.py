@@ -130,7 +130,7 @@ PART_SLOTS = 16
 
 
 def gpu_relay_hashing(min_pieces: int = 8, slots: int = PART_SLOTS,
-                      slot_bytes: int = PART_SLOT_BYTES, copy_streams: int = 1,
+                      slot_bytes: int = PART_SLOT_BYTES, copy_streams: int = 2,
                       compute_streams: int = 0) -> bool:
     """Route the hashed relay's parts to the gfx950 ``PartHasher`` (batched, one lane per
     piece; csrc/gpu_sha1.hip) instead of the host multi-buffer SHA-1. Created once per

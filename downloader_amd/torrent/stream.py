@@ -130,7 +130,7 @@ def _gpu_pending_sem(n: int) -> asyncio.Semaphore:
 _gpu_init_started = False
 
 
-def start_gpu_init(min_pieces: int, slots: int = 16, copy_streams: int = 1,
+def start_gpu_init(min_pieces: int, slots: int = 16, copy_streams: int = 2,
                    compute_streams: int = 0) -> None:
     """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and the device
     slots take a moment; the event loop keeps relaying meanwhile). Once per process; a
@@ -242,7 +242,7 @@ class StreamStager:
         self.verify_mode = getattr(d, "stream_verify_backend", "cpu") if gpu_pending > 0 else "cpu"
         self._min_pieces = int(getattr(d, "stream_gpu_min_pieces", 8) or 8)
         self._gpu_dev_slots = int(getattr(d, "stream_gpu_slots", 16) or 16)
-        self._gpu_copy_streams = int(getattr(d, "stream_gpu_copy_streams", 1) or 1)
+        self._gpu_copy_streams = int(getattr(d, "stream_gpu_copy_streams", 2) or 2)
         self._gpu_compute_streams = int(getattr(d, "stream_gpu_compute_streams", 0) or 0)
         # parts still queued below which the rest hash on the host
         self.gpu_tail = int(getattr(d, "stream_gpu_tail", 0) or 0)
@@ -674,7 +674,7 @@ def _gpu_relay_on(cfg) -> Optional[str]:
     try:
         if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8),
                                      getattr(d, "stream_gpu_slots", 16),
-                                     copy_streams=getattr(d, "stream_gpu_copy_streams", 1),
+                                     copy_streams=getattr(d, "stream_gpu_copy_streams", 2),
                                      compute_streams=getattr(d, "stream_gpu_compute_streams",
                                                              0)):
             return None
