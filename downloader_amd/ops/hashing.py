@@ -191,6 +191,9 @@ def _retrieve(fut) -> None:
         fut.exception()
 
 
+EARLY_MAX = 4096
+
+
 class _GpuParts:
     """Routes the native completion queue (``gpu_part_poll``, signalled through an eventfd
     the event loop watches) to per-part futures: no thread blocks per part."""
@@ -239,7 +242,12 @@ class _GpuParts:
             with self._lock:
                 part = self._parts.get(gid)
                 if part is None:
+                    # news before track() (the relay's executor thread returned the id, the
+                    # loop has not run the tracker yet); bounded: an id nobody tracks (a
+                    # caller that waits with gpu_part_wait) must not grow it for good
                     self._early.setdefault(gid, []).append((kind, data))
+                    while len(self._early) > EARLY_MAX:
+                        self._early.pop(next(iter(self._early)))
                     continue
             self._dispatch(gid, part, kind, data)
 
