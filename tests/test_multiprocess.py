@@ -117,6 +117,11 @@ def test_bench_single_rank_defaults_are_valid(tmp_path):
     # the sink recomputed (2 MB objects: 1 PUT + the done marker per job, 2 steps x 64 jobs)
     assert j["single_put_MBps"] > 0 and j["crc_relay_MBps"] > 0
     assert j["crc_relay_sink_checked_puts"] >= 2 * 64
+    # the line says what the headline's bytes were checked with (a spliced plain-http relay:
+    # nothing) and what the CRC'd run's were, with the CPU both sides spent on them
+    assert j["integrity"] == "none" and j["crc_relay_integrity"] == "crc32c"
+    assert j["crc_relay_worker_cpu_s_per_GB"] > 0 and j["crc_relay_peer_cpu_s_per_GB"] > 0
+    assert j["gpu_slots"] >= 1 and j["slot_budget_cpus"] >= 1
 
 
 def test_supervisor_auto_pinning_quota_share():
