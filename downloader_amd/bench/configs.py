@@ -243,7 +243,15 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                     None, get_reaper(w.services).drain, 600.0)
                 cleanup_k = time.perf_counter() - tc
                 assert all(x.outcome == "staged" for x in r_k), r_k
-                reps.append((dt_k, r_k, cpu_k, peer_k, cleanup_k))
+                try:
+                    from downloader_amd.ops import native
+                    pool_k = native().relay_pool_stats()
+                except Exception:
+                    pool_k = {}
+                reps.append((dt_k, r_k, cpu_k, peer_k, cleanup_k,
+                             {"rss_MB": _rss_mb()["rss_MB"],
+                              "pool_MiB": (pool_k.get("in_use_bytes", 0)
+                                           + pool_k.get("idle_bytes", 0)) >> 20}))
             rss = _rss_mb()
             thread_cpu = _thread_cpu_delta(threads0, _thread_cpu(0))
             try:
@@ -258,7 +266,7 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             await w.stop()
             # the median rep is the one reported in full
             reps_sorted = sorted(reps, key=lambda x: x[0])
-            dt, r, cpu_s, peer_cpu_s, cleanup_s = reps_sorted[len(reps_sorted) // 2]
+            dt, r, cpu_s, peer_cpu_s, cleanup_s, _ = reps_sorted[len(reps_sorted) // 2]
             st = b.stats()
     finally:
         shutil.rmtree(src, ignore_errors=True)
@@ -287,7 +295,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
             # of all parts, worker and peer CPU seconds
             "reps_detail": [{"job_s": round(x[0], 3),
                              "relay_s": x[1][0].stats.get("torrent", {}).get("webseed_fetch_s"),
-                             "worker_cpu_s": round(x[2], 2), "peer_cpu_s": round(x[3], 2)}
+                             "worker_cpu_s": round(x[2], 2), "peer_cpu_s": round(x[3], 2),
+                             **x[5]}
                             for x in reps]}
 
 
