@@ -41,6 +41,28 @@ class _RuntimeCollector:
                                 "relay part buffers in use", value=st["in_use"])
         yield GaugeMetricFamily(f"{self.ns}_relay_pool_idle_bytes",
                                 "bytes held by idle relay part buffers", value=st["idle_bytes"])
+        yield GaugeMetricFamily(f"{self.ns}_relay_pool_in_use_bytes",
+                                "bytes of leased relay part buffers", value=st["in_use_bytes"])
+        yield GaugeMetricFamily(f"{self.ns}_relay_pool_budget_bytes",
+                                "part-buffer budget (leased + idle never exceed it; 0 = none)",
+                                value=st["budget"])
+        yield GaugeMetricFamily(f"{self.ns}_relay_pool_peak_bytes",
+                                "high-water mark of leased + idle part buffers",
+                                value=st["peak_bytes"])
+        # > 0 means a lease was granted past the budget (a part larger than the whole budget)
+        yield CounterMetricFamily(f"{self.ns}_relay_pool_over_budget",
+                                  "part-buffer leases granted past the budget",
+                                  value=st["over_budget"])
+        gs = native().gpu_part_stats()
+        yield GaugeMetricFamily(f"{self.ns}_gpu_parts_pending",
+                                "relayed parts handed to the GPU hasher, not yet finished",
+                                value=gs["pending"])
+        yield CounterMetricFamily(f"{self.ns}_gpu_parts_submitted",
+                                  "relayed parts handed to the GPU hasher",
+                                  value=gs["submitted"])
+        yield CounterMetricFamily(f"{self.ns}_gpu_parts_host_fallbacks",
+                                  "GPU-queued parts hashed on the host (device failed before "
+                                  "the DMA ended)", value=gs["host_fallbacks"])
         ps = native().pipe_stats()
         yield GaugeMetricFamily(f"{self.ns}_splice_pipes_in_use",
                                 "splice pipes leased by running transfers", value=ps["in_use"])

@@ -205,6 +205,10 @@ def test_health_endpoint_semantics(run, make_cfg, origin_cls):
                 assert "downloader_http_idle_connections" in txt       # native runtime gauges
                 assert "downloader_relay_pool_idle_bytes" in txt
                 assert "downloader_splice_pipes_short_total" in txt    # pipe budget signal
+                assert "downloader_relay_pool_budget_bytes" in txt     # part-buffer budget
+                assert "downloader_relay_pool_over_budget_total" in txt
+                assert "downloader_gpu_parts_pending" in txt
+                assert "downloader_telemetry_buffered" in txt
         w.active.clear()
         await hs.stop()
         await w.stop(); await s3.stop(); await origin.stop()
