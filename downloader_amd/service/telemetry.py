@@ -13,7 +13,8 @@ the transfer (lib/download.js:78-88) and a progress emit is fire-and-forget
 (lib/upload.js:51). Here ``emit_*`` appends to a bounded outbox and returns at once. One
 flusher task publishes the outbox in order, each publish bounded by
 ``telemetry.publish_timeout_s``. While the broker is away the events wait in the outbox; once
-it is back they are flushed in order. When the outbox is full the oldest event is dropped.
+it is back they are flushed in order. When the outbox is full the oldest progress event is
+dropped (a later one supersedes it; status events go last).
 ``downloader_telemetry_events_total{outcome=published|dropped|failed}`` counts each event's
 fate, and ``downloader_telemetry_buffered`` shows the outbox depth.
 """
@@ -97,7 +98,14 @@ class Telemetry:
 
     def _enqueue(self, queue: str, body: bytes) -> None:
         if len(self._outbox) >= self.buffer_max:
-            self._outbox.popleft()               # drop the oldest: progress supersedes it
+            # drop the oldest progress event (a later one supersedes it); statuses (2, 6) go
+            # only when nothing but statuses is left. The head is never dropped: the flusher
+            # may be publishing it right now.
+            drop = next((i for i, (q, _) in enumerate(self._outbox)
+                         if i and q == self.progress_queue), None)
+            if drop is None:
+                drop = 1 if len(self._outbox) > 1 else 0
+            del self._outbox[drop]
             self._count("dropped")
         self._outbox.append((queue, body))
         self._gauge()

@@ -735,10 +735,15 @@ def test_telemetry_outbox_drops_the_oldest_when_full(run):
         tel = Telemetry(Down(), publish_timeout_s=0.05, buffer_max=5)
         loop = asyncio.get_running_loop()
         t0 = loop.time()
+        await tel.emit_status("m", 2)
         for i in range(12):
             await tel.emit_progress("m", 2, i)
+        await tel.emit_status("m", 6)
         assert loop.time() - t0 < 0.05
-        assert tel.buffered == 5 and tel.counts["dropped"] == 7
+        assert tel.buffered == 5 and tel.counts["dropped"] == 9
+        # progress is dropped before statuses: both statuses and the newest progress survive
+        qs = [q for q, _ in tel._outbox]
+        assert qs.count(tel.status_queue) == 2 and qs[-1] == tel.status_queue
         await tel.close(timeout=0.1)
-        assert tel.buffered == 0 and tel.counts["dropped"] == 12
+        assert tel.buffered == 0 and tel.counts["dropped"] == 14
     run(go())
