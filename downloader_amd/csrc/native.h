@@ -281,8 +281,9 @@ class HttpConn {
   int64_t relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* prog, Room&& room,
                     Got&& got);
   // The same contract with recv(MSG_PEEK) into `room` and a splice of exactly the peeked
-  // bytes: one copy like tee, one pipe instead of two (csrc/relaybench.cpp, MI355X box at 8
-  // relay threads: 38.7 vs 29.9 GB/s, 0.164 vs 0.211 relay CPU-s per GB).
+  // bytes: one copy like tee, one pipe instead of two (csrc/relaybench.cpp at 8 relay
+  // threads: 38.7 vs 29.9 GB/s on one MI355X box, 37.5 vs 38.4 on another - the copy costs
+  // the same; the pipe is what peek saves).
   template <class Room, class Got>
   int64_t relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* prog, Room&& room,
                      Got&& got);
