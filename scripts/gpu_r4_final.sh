@@ -9,7 +9,7 @@ F=${OUT:-gpurun_out/r4_final}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
-PART=${PART:-ab}
+PART=${PART:-abc}
 if [[ $PART == *a* ]]; then
 step gpu; timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $F/pytest_gpu.txt 2>&1 || { tail -30 $F/pytest_gpu.txt; exit 1; }
 tail -1 $F/pytest_gpu.txt
@@ -33,6 +33,14 @@ fi
 if [[ $PART == *b* ]]; then
 step chaos; timeout -k 10 600 python -m downloader_amd.bench.configs --config 7 --scale 2 --workers 4 --concurrency 4 --qps 40 --chaos-interval 1.0 --s3-fail-rate 0.03 --chaos-timeout 400 --chaos-multipart-mb 16 > $F/chaos.jsonl 2> $F/chaos.err || { tail -20 $F/chaos.err; exit 1; }
 tail -1 $F/chaos.jsonl
+fi
+if [[ $PART == *c* ]]; then
+# PMC pass (its own run, counters only): the PartHasher's sha1_lanes in the relay context -
+# config 4, one job, GPU hashing, 2 GiB budget; 5 SQ + 1 GRBM counters fit one pass
+R=$PWD
+step pmc; ( cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/$F/pmc -o pmc -- python3 -m downloader_amd.bench.configs --config 4 --reps 1 --stream-verify gpu --relay-memory-mb 2048 > $R/$F/pmc_c4.json 2> $R/$F/pmc.err ) || { tail -20 $F/pmc.err; exit 1; }
+P=$(find $F/pmc -name '*counter_collection.csv' | head -1)
+[ -n "$P" ] && python -m downloader_amd.bench.pmc_summary "$P" 4194304 > $F/pmc_summary.json && cat $F/pmc_summary.json
 fi
 python3 - <<PY
 import json
