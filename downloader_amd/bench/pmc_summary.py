@@ -45,6 +45,25 @@ def summarise(path: str, piece_len: int = 0):
             row["valu_active_frac_of_wave_cycles"] = round(
                 c.get("SQ_ACTIVE_INST_VALU", 0.0) / c["SQ_WAVE_CYCLES"], 3)
         out.append(row)
+    # one row per kernel over every grid size (the relay's launches vary in lanes)
+    names = sorted({k[0] for k in acc})
+    for n in names:
+        keys = [k for k in acc if k[0] == n]
+        if len(keys) < 2:
+            continue
+        tot = defaultdict(float)
+        for k in keys:
+            for cname, v in acc[k].items():
+                tot[cname] += v
+        row = {"kernel": n, "lanes": "all", "dispatches": sum(len(dispatches[k]) for k in keys),
+               "lanes_mean": round(sum(k[1] * len(dispatches[k]) for k in keys)
+                                   / max(1, sum(len(dispatches[k]) for k in keys)), 1)}
+        if tot.get("SQ_WAVES"):
+            row["valu_insts_per_wave"] = round(tot.get("SQ_INSTS_VALU", 0.0) / tot["SQ_WAVES"], 1)
+        if tot.get("SQ_WAVE_CYCLES"):
+            row["valu_active_frac_of_wave_cycles"] = round(
+                tot.get("SQ_ACTIVE_INST_VALU", 0.0) / tot["SQ_WAVE_CYCLES"], 3)
+        out.append(row)
     return out
 
 
