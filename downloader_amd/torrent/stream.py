@@ -150,13 +150,21 @@ def start_gpu_init(min_pieces: int, slots: int = 16, copy_streams: int = 2,
     fut.add_done_callback(lambda f: f.cancelled() or f.exception())   # retrieved
 
 
-def _schedule_trim(idle_s: float) -> None:
-    """Last stream stager of the process finished: trim after ``idle_s`` quiet seconds (0 =
-    now), so back-to-back jobs keep reusing warm buffers while an idle worker holds none."""
+def _schedule_trim(idle_s: float, keep_bytes: int = 0) -> None:
+    """Last stream stager of the process finished: at once, idle buffers beyond ``keep_bytes``
+    (what one job's relays in flight use) are unmapped; the rest after ``idle_s`` quiet
+    seconds (0 = now), so back-to-back jobs reuse warm buffers while an idle worker holds
+    none."""
     global _trim_handle
     if _trim_handle is not None:
         _trim_handle.cancel()
         _trim_handle = None
+    if idle_s > 0 and keep_bytes > 0:
+        try:
+            from ..ops import native
+            native().relay_pool_trim(keep_bytes)
+        except Exception:
+            pass
     if idle_s <= 0:
         _trim_relay_buffers()
     else:
@@ -357,7 +365,9 @@ class StreamStager:
             _active_stagers -= 1
             self.stats["budget"] = self._budget.stats()
             if _active_stagers == 0:
-                _schedule_trim(self.trim_idle_s)
+                # keep warm what one job's relays take, the rest goes now
+                _schedule_trim(self.trim_idle_s,
+                               self.parallel * membudget.buffer_bytes(self.s3.part_size))
         return [{"file": f, "key": keys.object_key(self.job.id, f), "size": self.sizes[f],
                  "virtual": True} for f in self.selected]
 
