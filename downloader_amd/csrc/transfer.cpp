@@ -1486,7 +1486,10 @@ void gpu_notify(void* arg, uint64_t ticket, int phase) {
     auto it = g_gpu_ids.find({a, ticket});
     if (it == g_gpu_ids.end()) return;
     id = it->second;
-    copied = g_gpu_parts.at(id).copied;
+    // never throw on the hasher's thread (its dispatcher would take it for a device error)
+    auto p = g_gpu_parts.find(id);
+    if (p == g_gpu_parts.end()) return;
+    copied = p->second.copied;
   }
   if (!copied) gpu_copied(a, ticket, id);   // a DONE implies the copy is over
   if (phase == GPU_PART_DONE) gpu_done(a, ticket, id);
