@@ -205,6 +205,8 @@ async def config_torrent(a, cfg_no: int) -> Dict:
                 dl["relay_memory_mb"] = a.relay_memory_mb
             if getattr(a, "stream_gpu_slots", 0):
                 dl["stream_gpu_slots"] = a.stream_gpu_slots
+            if getattr(a, "gpu_slot_mb", 0):
+                dl["stream_gpu_slot_mb"] = a.gpu_slot_mb
             if getattr(a, "gpu_copy_streams", 0):
                 dl["stream_gpu_copy_streams"] = a.gpu_copy_streams
             if getattr(a, "gpu_compute_streams", 0):
@@ -665,6 +667,8 @@ def main(argv=None) -> int:
                     help="configs 3/4: download.relay_memory_mb (part-buffer budget per worker)")
     ap.add_argument("--stream-gpu-slots", type=int, default=0,
                     help="configs 3/4: download.stream_gpu_slots (PartHasher HBM slots)")
+    ap.add_argument("--gpu-slot-mb", type=int, default=0,
+                    help="configs 3/4: download.stream_gpu_slot_mb (PartHasher slot size)")
     ap.add_argument("--gpu-copy-streams", type=int, default=0,
                     help="configs 3/4: download.stream_gpu_copy_streams")
     ap.add_argument("--gpu-compute-streams", type=int, default=0,

@@ -148,7 +148,7 @@ class Worker:
                 return
             ok = await loop.run_in_executor(
                 None, lambda: hashing.gpu_relay_hashing(
-                    d.stream_gpu_min_pieces, d.stream_gpu_slots,
+                    d.stream_gpu_min_pieces, d.stream_gpu_slots, d.stream_gpu_slot_mb << 20,
                     copy_streams=d.stream_gpu_copy_streams,
                     compute_streams=d.stream_gpu_compute_streams))
             self.log.info({"gpu_part_hasher": ok}, "gpu relay hashing prewarm")

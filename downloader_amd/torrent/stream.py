@@ -131,7 +131,7 @@ _gpu_init_started = False
 
 
 def start_gpu_init(min_pieces: int, slots: int = 16, copy_streams: int = 2,
-                   compute_streams: int = 0) -> None:
+                   compute_streams: int = 0, slot_bytes: int = 1 << 30) -> None:
     """``auto``: set up the gfx950 PartHasher on an executor thread (HIP init and the device
     slots take a moment; the event loop keeps relaying meanwhile). Once per process; a
     missing device or a failed init leaves every part on the host."""
@@ -143,7 +143,7 @@ def start_gpu_init(min_pieces: int, slots: int = 16, copy_streams: int = 2,
 
     def init() -> bool:
         from ..ops import gpu_available
-        return gpu_available() and hashing.gpu_relay_hashing(min_pieces, slots,
+        return gpu_available() and hashing.gpu_relay_hashing(min_pieces, slots, slot_bytes,
                                                              copy_streams=copy_streams,
                                                              compute_streams=compute_streams)
     fut = asyncio.get_running_loop().run_in_executor(None, init)
@@ -252,6 +252,7 @@ class StreamStager:
         self._gpu_dev_slots = int(getattr(d, "stream_gpu_slots", 16) or 16)
         self._gpu_copy_streams = int(getattr(d, "stream_gpu_copy_streams", 2) or 2)
         self._gpu_compute_streams = int(getattr(d, "stream_gpu_compute_streams", 0) or 0)
+        self._gpu_slot_bytes = int(getattr(d, "stream_gpu_slot_mb", 1024) or 1024) << 20
         # parts still queued below which the rest hash on the host
         self.gpu_tail = int(getattr(d, "stream_gpu_tail", 0) or 0)
         self._n_parts = sum(1 for u in self.units if u.target is not None)
@@ -323,7 +324,7 @@ class StreamStager:
             pass
         if self.verify_mode == "auto" and self._gpu_wanted():
             start_gpu_init(self._min_pieces, self._gpu_dev_slots, self._gpu_copy_streams,
-                           self._gpu_compute_streams)
+                           self._gpu_compute_streams, self._gpu_slot_bytes)
         try:
             for t in self.targets:
                 if t.size == 0:
@@ -684,6 +685,7 @@ def _gpu_relay_on(cfg) -> Optional[str]:
     try:
         if hashing.gpu_relay_hashing(getattr(d, "stream_gpu_min_pieces", 8),
                                      getattr(d, "stream_gpu_slots", 16),
+                                     int(getattr(d, "stream_gpu_slot_mb", 1024) or 1024) << 20,
                                      copy_streams=getattr(d, "stream_gpu_copy_streams", 2),
                                      compute_streams=getattr(d, "stream_gpu_compute_streams",
                                                              0)):

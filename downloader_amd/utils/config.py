@@ -210,6 +210,9 @@ class DownloadConfig(BaseModel):
     # PartHasher device slots (1 GiB of HBM each): enough that a part's DMA never waits for a
     # kernel to free a slot, which is what keeps the host buffers short-lived
     stream_gpu_slots: int = 16
+    # bytes per slot (MiB): one sha1_lanes launch hashes up to slot / piece_len pieces, so
+    # with 4 MiB pieces a 1 GiB slot caps a launch at 256 lanes (~15 GB/s per busy stream)
+    stream_gpu_slot_mb: int = 1024
     # PartHasher streams: copy streams for the parts' DMAs, compute streams for the kernels
     # (0 = the hardware queues the copy streams leave, GPU_MAX_HW_QUEUES = 4 by default): a
     # copy stream sharing a hardware queue with a compute stream waits behind its kernels.
