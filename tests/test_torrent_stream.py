@@ -761,3 +761,21 @@ def test_job_end_trims_idle_buffers_to_one_jobs_worth(run, tmp_path, make_cfg, o
         run(go())
     finally:
         hashing.use_part_hasher(None)
+
+
+def test_part_hasher_layout_comes_from_the_config(monkeypatch):
+    """``download.stream_gpu_slots / _slot_mb / _copy_streams / _compute_streams`` reach the
+    PartHasher's constructor arguments (slot size sets how many lanes one launch can hash)."""
+    from downloader_amd.ops import hashing
+    from downloader_amd.torrent import stream
+    from downloader_amd.utils.config import Config
+    seen = []
+    monkeypatch.setattr(hashing, "_part_hasher", None)
+    monkeypatch.setattr(hashing, "gpu_relay_hashing",
+                        lambda *a, **k: seen.append((a, k)) or True)
+    cfg = Config.model_validate({"download": {"stream_gpu_slots": 8, "stream_gpu_slot_mb": 2048,
+                                              "stream_gpu_copy_streams": 1,
+                                              "stream_gpu_compute_streams": 3}})
+    assert stream._gpu_relay_on(cfg) is None
+    (a, k), = seen
+    assert a[1:] == (8, 2 << 30) and k == {"copy_streams": 1, "compute_streams": 3}
