@@ -1305,20 +1305,15 @@ class PartPool {
     max_idle_ = n;
   }
   void set_budget(size_t bytes) {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      budget_ = bytes;
-    }
-    if (bytes) {
-      std::lock_guard<std::mutex> g(mu_);
-      // idle buffers beyond the new budget go at once
-      std::vector<std::unique_ptr<PartBuffer>> drop;
-      while (!idle_.empty() && in_use_bytes_ + idle_bytes_ > budget_) {
-        idle_bytes_ -= idle_.back()->cap;
-        drop.push_back(std::move(idle_.back()));
-        idle_.pop_back();
-        evicted_++;
-      }
+    std::vector<std::unique_ptr<PartBuffer>> drop;   // unmapped outside the lock
+    std::lock_guard<std::mutex> g(mu_);
+    budget_ = bytes;
+    // idle buffers beyond the new budget go at once
+    while (bytes && !idle_.empty() && in_use_bytes_ + idle_bytes_ > budget_) {
+      idle_bytes_ -= idle_.back()->cap;
+      drop.push_back(std::move(idle_.back()));
+      idle_.pop_back();
+      evicted_++;
     }
   }
   void reset_peak() {
