@@ -167,10 +167,8 @@ class Telemetry:
         await self.flush(timeout)
         if self._flusher is not None:
             self._flusher.cancel()
-            try:
-                await self._flusher
-            except BaseException:
-                pass
+            # wait() neither raises the flusher's CancelledError nor swallows our own
+            await asyncio.wait({self._flusher})
             self._flusher = None
         if self._outbox:
             self._count("dropped", len(self._outbox))
