@@ -949,7 +949,7 @@ class PartHasher {
     auto it = jobs_.find(t);
     if (it == jobs_.end()) return fail(err, errlen, "unknown ticket");
     Job* j = &it->second;
-    wcv_.wait(lk, [&] { return !j->err.empty() || (phase == GPU_PART_COPIED ? j->copied : j->done); });
+    wcv_.wait(lk, [&] { return !j->err.empty() || j->done || (phase == GPU_PART_COPIED && j->copied); });
     if (!j->err.empty()) {
       std::string e = j->err;
       // nobody waits again for a failed copy (the relay hashes on the host), and once broken
@@ -1065,7 +1065,7 @@ class PartHasher {
           fresh.swap(queue_);
         }
         bool progressed = false;
-        std::vector<uint64_t> copied_now, done_now;
+        std::vector<uint64_t> copied_now, done_now, late_copied;
         // 1. DMA new parts into the open slot (a new one when it is full)
         while (!fresh.empty()) {
           const uint64_t t = fresh.front();
@@ -1160,6 +1160,14 @@ class PartHasher {
               Job& j = jobs_.at(t);
               j.digests.assign((const char*)sl.h_dig + (size_t)j.lane0 * 20, (size_t)j.np * 20);
               j.done = true;
+              if (!j.copied) {
+                // its copy ended after step 2 looked (the kernel waited for it): a DONE implies
+                // COPIED, and a job the relay may now erase must leave `copying`
+                j.copied = true;
+                free_events_.push_back(j.copy_ev);
+                j.copy_ev = nullptr;
+                late_copied.push_back(t);
+              }
               done_now.push_back(t);
             }
           }
@@ -1168,6 +1176,13 @@ class PartHasher {
           sl.jobs.clear();
           st.slot = -1;
           progressed = true;
+        }
+        if (!late_copied.empty()) {
+          for (uint64_t t : late_copied) {
+            auto c = std::find(copying.begin(), copying.end(), t);
+            if (c != copying.end()) copying.erase(c);
+          }
+          tell(late_copied, GPU_PART_COPIED);
         }
         // 4. launch: closed slots first (oldest first), then the open one, on idle streams
         for (auto& st : streams_) {

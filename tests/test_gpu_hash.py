@@ -280,6 +280,60 @@ def test_part_hasher_dispatcher_idles_while_every_slot_is_busy():
     del h
 
 
+def test_part_hasher_small_parts_through_the_relay(run, origin_cls):
+    """Many small parts (64 pieces of 4 KiB: kernels of well under a millisecond) through the
+    relay's asynchronous path. A kernel can then finish between the dispatcher's poll of its
+    copies and its poll of the kernels, so a part's DONE may be the first news of its copy:
+    every part still completes with the right digests, every buffer returns to the pool, and
+    the hasher neither hangs nor breaks."""
+    import asyncio
+
+    from downloader_amd.ops import gpu_available, gpuhash, hashing, native
+    from downloader_amd.s3.client import S3Client
+    from downloader_amd.s3.fake_server import FakeS3
+    from downloader_amd.utils.aio import gather_strict
+
+    if not gpu_available():
+        pytest.fail("HIP device not visible: the GPU test tier must run on a MI355X")
+    piece, size = 4096, 256 << 10
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        blobs = [os.urandom(size) for _ in range(8)]
+        for i, b in enumerate(blobs):
+            origin.blobs[f"/p{i}.bin"] = b
+        c = S3Client(ep, "minioadmin", "minioadmin")
+        await c.ensure_bucket("b")
+
+        async def one(k):
+            b = k % len(blobs)
+            _, h = await c.relay_hashed("b", f"k{k}", origin.url(f"/p{b}.bin"), 0, size, True,
+                                        (0, size, piece), gpu=True)
+            assert h["gpu_ticket"] and not h["digests"]
+            return b, await asyncio.wait_for(hashing.gpu_part_digests(h["gpu_ticket"]), 30)
+
+        got = []
+        for r in range(12):
+            got += await gather_strict(*(one(r * 16 + i) for i in range(16)))
+        want = [b"".join(hashlib.sha1(x[i:i + piece]).digest() for i in range(0, size, piece))
+                for x in blobs]
+        assert all(d == want[b] for b, d in got)
+        st = ph.stats()
+        assert st["submitted"] >= 192 and not st["broken"] and st["pending"] == 0, st
+        assert native().relay_pool_stats()["in_use"] == 0
+        await c.close(); await origin.stop(); await s3.stop()
+
+    prev = hashing._part_hasher
+    ph = gpuhash().PartHasher(0, 64 << 20, 4, 0, 4096, 2)
+    hashing.use_part_hasher(ph, 4)
+    try:
+        run(go(), timeout=120)
+    finally:
+        hashing.use_part_hasher(prev)
+
+
 @pytest.mark.parametrize("corrupt", [False, True])
 def test_stream_torrent_with_gpu_relay_hashing(run, tmp_path, make_cfg, origin_cls, corrupt):
     """Webseed torrent staged webseed -> S3 with the relayed parts' pieces hashed by the
