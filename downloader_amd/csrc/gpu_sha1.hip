@@ -459,6 +459,32 @@ void parallel_for(size_t n, int threads, F&& fn) {
   for (auto& th : pool) th.join();
 }
 
+// Scoped device memory and events: released on every exit path, a thrown HIP error included
+// (hipFree waits for work still using the memory).
+template <class T>
+struct DevMem {
+  T* p = nullptr;
+  explicit DevMem(size_t n) {
+    if (n) HIP_CHECK(hipMalloc((void**)&p, n * sizeof(T)));
+  }
+  ~DevMem() {
+    if (p) hipFree(p);
+  }
+  DevMem(const DevMem&) = delete;
+  DevMem& operator=(const DevMem&) = delete;
+};
+struct DevEvent {
+  hipEvent_t e = nullptr;
+  explicit DevEvent(unsigned flags = hipEventDisableTiming) {
+    HIP_CHECK(hipEventCreateWithFlags(&e, flags));
+  }
+  ~DevEvent() {
+    if (e) hipEventDestroy(e);
+  }
+  DevEvent(const DevEvent&) = delete;
+  DevEvent& operator=(const DevEvent&) = delete;
+};
+
 class GpuVerifier {
  public:
   GpuVerifier(int device, int64_t batch_bytes, int reader_threads)
@@ -467,14 +493,21 @@ class GpuVerifier {
     HIP_CHECK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) throw std::runtime_error("no such HIP device");
     HIP_CHECK(hipSetDevice(device_));
-    for (int s = 0; s < 2; ++s) {
-      HIP_CHECK(hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking));
-      HIP_CHECK(hipHostMalloc((void**)&h_buf_[s], (size_t)batch_bytes_, hipHostMallocDefault));
-      HIP_CHECK(hipMalloc((void**)&d_buf_[s], (size_t)batch_bytes_));
-      HIP_CHECK(hipEventCreateWithFlags(&done_[s], hipEventDisableTiming));
+    try {
+      for (int s = 0; s < 2; ++s) {
+        HIP_CHECK(hipStreamCreateWithFlags(&stream_[s], hipStreamNonBlocking));
+        HIP_CHECK(hipHostMalloc((void**)&h_buf_[s], (size_t)batch_bytes_, hipHostMallocDefault));
+        HIP_CHECK(hipMalloc((void**)&d_buf_[s], (size_t)batch_bytes_));
+        HIP_CHECK(hipEventCreateWithFlags(&done_[s], hipEventDisableTiming));
+      }
+    } catch (...) {
+      release();                       // a failed set-up leaves nothing allocated
+      throw;
     }
   }
-  ~GpuVerifier() {
+  ~GpuVerifier() { release(); }
+
+  void release() {
     hipSetDevice(device_);
     for (int s = 0; s < 2; ++s) {
       if (stream_[s]) hipStreamSynchronize(stream_[s]);
@@ -485,6 +518,8 @@ class GpuVerifier {
     }
     if (d_meta_) hipFree(d_meta_);
     if (h_meta_) hipHostFree(h_meta_);
+    for (int s = 0; s < 2; ++s) stream_[s] = nullptr, h_buf_[s] = d_buf_[s] = nullptr, done_[s] = nullptr;
+    d_meta_ = h_meta_ = nullptr;
   }
 
   // Digests of a contiguous host buffer split into pieces (used by tests and torrent
@@ -555,24 +590,19 @@ class GpuVerifier {
     const int64_t CH = std::max<int64_t>(64, std::min<int64_t>(chunk, piece_len) & ~(int64_t)63);
     const int64_t W = std::max<int64_t>(1, std::min<int64_t>(m, batch_bytes_ / CH));
     const int64_t last_len = fs.total - (np - 1) * piece_len;
-    uint8_t *d_exp = nullptr, *d_ok = nullptr;
-    uint32_t* d_state = nullptr;
-    int* d_lanes = nullptr;
-    HIP_CHECK(hipMalloc((void**)&d_exp, (size_t)np * 20));
-    HIP_CHECK(hipMalloc((void**)&d_ok, (size_t)np));
-    HIP_CHECK(hipMalloc((void**)&d_state, (size_t)W * 20));
+    DevMem<uint8_t> exp_buf((size_t)np * 20), ok_buf((size_t)np);
+    DevMem<uint32_t> state_buf((size_t)W * 5);
+    DevMem<int> lanes_buf(subset ? (size_t)m : 0);
+    uint8_t *d_exp = exp_buf.p, *d_ok = ok_buf.p;
+    uint32_t* d_state = state_buf.p;
+    int* d_lanes = lanes_buf.p;
     HIP_CHECK(hipMemcpy(d_exp, hashes.data(), (size_t)np * 20, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemset(d_ok, 0, (size_t)np));
-    if (subset) {
-      HIP_CHECK(hipMalloc((void**)&d_lanes, (size_t)m * sizeof(int)));
+    if (subset)
       HIP_CHECK(hipMemcpy(d_lanes, which.data(), (size_t)m * sizeof(int), hipMemcpyHostToDevice));
-    }
     std::vector<uint8_t> readable((size_t)np, 1);
-    hipEvent_t copied[2], kdone[2];
-    for (int s = 0; s < 2; ++s) {
-      HIP_CHECK(hipEventCreateWithFlags(&copied[s], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&kdone[s], hipEventDisableTiming));
-    }
+    DevEvent copied_ev[2], kdone_ev[2];
+    hipEvent_t copied[2] = {copied_ev[0].e, copied_ev[1].e}, kdone[2] = {kdone_ev[0].e, kdone_ev[1].e};
     bool slot_busy[2] = {false, false};
     bool have_prev_kernel = false;
     int prev_slot = 0;
@@ -618,14 +648,6 @@ class GpuVerifier {
     HIP_CHECK(hipStreamSynchronize(stream_[0]));
     HIP_CHECK(hipStreamSynchronize(stream_[1]));
     HIP_CHECK(hipMemcpy(ok.data(), d_ok, (size_t)np, hipMemcpyDeviceToHost));
-    for (int q = 0; q < 2; ++q) {
-      hipEventDestroy(copied[q]);
-      hipEventDestroy(kdone[q]);
-    }
-    hipFree(d_exp);
-    hipFree(d_ok);
-    hipFree(d_state);
-    if (d_lanes) hipFree(d_lanes);
     for (int64_t i = 0; i < np; ++i)
       if (!readable[(size_t)i]) ok[(size_t)i] = 0;
     if (timing) *timing = {t_fill, t_wait};
@@ -640,13 +662,11 @@ class GpuVerifier {
   std::vector<double> kernel_bench_prefetch(int64_t piece_len, int n_pieces, int iters) {
     HIP_CHECK(hipSetDevice(device_));
     size_t bytes = (size_t)piece_len * (size_t)n_pieces;
-    uint8_t *d = nullptr, *dout = nullptr;
-    HIP_CHECK(hipMalloc((void**)&d, bytes));
-    HIP_CHECK(hipMalloc((void**)&dout, (size_t)n_pieces * 20));
+    DevMem<uint8_t> data_buf(bytes), out_buf((size_t)n_pieces * 20);
+    uint8_t *d = data_buf.p, *dout = out_buf.p;
     HIP_CHECK(hipMemset(d, 0x5a, bytes));
-    hipEvent_t e0, e1;
-    HIP_CHECK(hipEventCreate(&e0));
-    HIP_CHECK(hipEventCreate(&e1));
+    DevEvent ev0(hipEventDefault), ev1(hipEventDefault);
+    hipEvent_t e0 = ev0.e, e1 = ev1.e;
     const int block = 64, grid = (n_pieces + block - 1) / block;
     double t[2] = {0, 0};
     for (int it = 0; it < iters + 1; ++it) {
@@ -668,10 +688,6 @@ class GpuVerifier {
         if (it > 0) t[v] += ms;
       }
     }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipFree(d);
-    hipFree(dout);
     return {t[0] / iters, t[1] / iters};
   }
 
@@ -681,13 +697,11 @@ class GpuVerifier {
   std::vector<double> kernel_bench(int64_t piece_len, int n_pieces, int iters) {
     HIP_CHECK(hipSetDevice(device_));
     size_t bytes = (size_t)piece_len * (size_t)n_pieces;
-    uint8_t *d = nullptr, *dout = nullptr;
-    HIP_CHECK(hipMalloc((void**)&d, bytes));
-    HIP_CHECK(hipMalloc((void**)&dout, (size_t)n_pieces * 20));
+    DevMem<uint8_t> data_buf(bytes), out_buf((size_t)n_pieces * 20);
+    uint8_t *d = data_buf.p, *dout = out_buf.p;
     HIP_CHECK(hipMemset(d, 0x5a, bytes));
-    hipEvent_t e0, e1;
-    HIP_CHECK(hipEventCreate(&e0));
-    HIP_CHECK(hipEventCreate(&e1));
+    DevEvent ev0(hipEventDefault), ev1(hipEventDefault);
+    hipEvent_t e0 = ev0.e, e1 = ev1.e;
     const int block = 64, grid = (n_pieces + block - 1) / block;
     double t[2] = {0, 0};
     for (int it = 0; it < iters + 1; ++it) {
@@ -707,10 +721,6 @@ class GpuVerifier {
         if (it > 0) t[v] += ms;  // first round is warm-up
       }
     }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipFree(d);
-    hipFree(dout);
     return {t[0] / iters, t[1] / iters};
   }
 
@@ -764,10 +774,13 @@ class GpuVerifier {
   }
 
   void grow(int64_t bytes) {
+    batch_bytes_ = 0;                  // a failed grow makes the next batch try again
     for (int s = 0; s < 2; ++s) {
       HIP_CHECK(hipStreamSynchronize(stream_[s]));
       HIP_CHECK(hipHostFree(h_buf_[s]));
+      h_buf_[s] = nullptr;             // never freed twice if an allocation below throws
       HIP_CHECK(hipFree(d_buf_[s]));
+      d_buf_[s] = nullptr;
       HIP_CHECK(hipHostMalloc((void**)&h_buf_[s], (size_t)bytes, hipHostMallocDefault));
       HIP_CHECK(hipMalloc((void**)&d_buf_[s], (size_t)bytes));
     }
@@ -778,10 +791,13 @@ class GpuVerifier {
     size_t need = (size_t)per * 21;  // ok byte + 20-byte expected digest (or 20-byte output)
     if (need <= meta_stride_) return;
     if (d_meta_) HIP_CHECK(hipFree(d_meta_));
+    d_meta_ = nullptr;
     if (h_meta_) HIP_CHECK(hipHostFree(h_meta_));
+    h_meta_ = nullptr;
+    meta_stride_ = 0;                  // set once both allocations are in
+    HIP_CHECK(hipMalloc((void**)&d_meta_, need * 2));
+    HIP_CHECK(hipHostMalloc((void**)&h_meta_, need * 2, hipHostMallocDefault));
     meta_stride_ = need;
-    HIP_CHECK(hipMalloc((void**)&d_meta_, meta_stride_ * 2));
-    HIP_CHECK(hipHostMalloc((void**)&h_meta_, meta_stride_ * 2, hipHostMallocDefault));
   }
 
   int device_;
@@ -828,32 +844,11 @@ class PartHasher {
         copy_streams < 1 || copy_streams > 4)
       throw std::invalid_argument("PartHasher: bad geometry");
     HIP_CHECK(hipSetDevice(device_));
-    // Parts are DMA'd round-robin over copy_streams streams: each is its own hardware queue,
-    // so H2D copies of consecutive parts run on separate SDMA engines instead of queueing
-    // behind one another (a part's host buffer is held until its copy ends).
-    copies_.resize((size_t)copy_streams);
-    for (auto& c : copies_) HIP_CHECK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
-    // Every HIP stream is mapped onto one of GPU_MAX_HW_QUEUES (4) hardware queues; a copy
-    // stream that shares a queue with a compute stream has its copy-completion marker wait
-    // behind a ~77 ms sha1_lanes kernel, and the part's host buffer with it. streams <= 0:
-    // as many compute streams as the queues left over by the copy streams.
-    const int hwq = hw_queues();
-    const int compute = streams > 0 ? std::min(streams, 4) : std::max(1, hwq - copy_streams);
-    streams_.resize((size_t)compute);
-    for (auto& st : streams_) {
-      HIP_CHECK(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
-      st.slot = -1;
-    }
-    slots_.resize((size_t)slots);
-    for (auto& sl : slots_) {
-      HIP_CHECK(hipMalloc((void**)&sl.d_data, (size_t)slot_bytes_));
-      HIP_CHECK(hipMalloc((void**)&sl.d_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t)));
-      HIP_CHECK(hipMalloc((void**)&sl.d_dig, (size_t)max_lanes_ * 20));
-      HIP_CHECK(hipHostMalloc((void**)&sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
-                              hipHostMallocDefault));
-      HIP_CHECK(hipHostMalloc((void**)&sl.h_dig, (size_t)max_lanes_ * 20, hipHostMallocDefault));
-      for (auto& e : sl.copied) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    try {
+      create(slots, streams, copy_streams);
+    } catch (...) {
+      release();                       // a failed set-up leaves no HBM or streams behind
+      throw;
     }
     api_.abi = GPU_PART_API_ABI;
     api_.ctx = this;
@@ -882,25 +877,70 @@ class PartHasher {
     }
     cv_.notify_all();
     if (thread_.joinable()) thread_.join();
-    hipSetDevice(device_);
-    for (auto c : copies_) hipStreamSynchronize(c);
-    for (auto& st : streams_) {
-      hipStreamSynchronize(st.s);
-      hipStreamDestroy(st.s);
-    }
-    for (auto c : copies_) hipStreamDestroy(c);
-    for (auto& sl : slots_) {
-      hipFree(sl.d_data);
-      hipFree(sl.d_lane);
-      hipFree(sl.d_dig);
-      hipHostFree(sl.h_lane);
-      hipHostFree(sl.h_dig);
-      for (auto e : sl.copied) hipEventDestroy(e);
-      hipEventDestroy(sl.done);
-    }
-    for (hipEvent_t e : free_events_) hipEventDestroy(e);
+    release();
   }
 
+ private:
+  void create(int slots, int streams, int copy_streams) {
+    // Parts are DMA'd round-robin over copy_streams streams: each is its own hardware queue,
+    // so H2D copies of consecutive parts run on separate SDMA engines instead of queueing
+    // behind one another (a part's host buffer is held until its copy ends).
+    copies_.resize((size_t)copy_streams);
+    for (auto& c : copies_) HIP_CHECK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    // Every HIP stream is mapped onto one of GPU_MAX_HW_QUEUES (4) hardware queues; a copy
+    // stream that shares a queue with a compute stream has its copy-completion marker wait
+    // behind a ~77 ms sha1_lanes kernel, and the part's host buffer with it. streams <= 0:
+    // as many compute streams as the queues left over by the copy streams.
+    const int hwq = hw_queues();
+    const int compute = streams > 0 ? std::min(streams, 4) : std::max(1, hwq - copy_streams);
+    streams_.resize((size_t)compute);
+    for (auto& st : streams_) {
+      HIP_CHECK(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
+      st.slot = -1;
+    }
+    slots_.resize((size_t)slots);
+    for (auto& sl : slots_) {
+      HIP_CHECK(hipMalloc((void**)&sl.d_data, (size_t)slot_bytes_));
+      HIP_CHECK(hipMalloc((void**)&sl.d_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t)));
+      HIP_CHECK(hipMalloc((void**)&sl.d_dig, (size_t)max_lanes_ * 20));
+      HIP_CHECK(hipHostMalloc((void**)&sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
+                              hipHostMallocDefault));
+      HIP_CHECK(hipHostMalloc((void**)&sl.h_dig, (size_t)max_lanes_ * 20, hipHostMallocDefault));
+      for (auto& e : sl.copied) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+  }
+
+  // Everything create() made, also when it stopped half-way (null handles are skipped).
+  void release() {
+    hipSetDevice(device_);
+    for (auto c : copies_)
+      if (c) hipStreamSynchronize(c);
+    for (auto& st : streams_)
+      if (st.s) {
+        hipStreamSynchronize(st.s);
+        hipStreamDestroy(st.s);
+      }
+    for (auto c : copies_)
+      if (c) hipStreamDestroy(c);
+    for (auto& sl : slots_) {
+      if (sl.d_data) hipFree(sl.d_data);
+      if (sl.d_lane) hipFree(sl.d_lane);
+      if (sl.d_dig) hipFree(sl.d_dig);
+      if (sl.h_lane) hipHostFree(sl.h_lane);
+      if (sl.h_dig) hipHostFree(sl.h_dig);
+      for (auto e : sl.copied)
+        if (e) hipEventDestroy(e);
+      if (sl.done) hipEventDestroy(sl.done);
+    }
+    for (hipEvent_t e : free_events_) hipEventDestroy(e);
+    copies_.clear();
+    streams_.clear();
+    slots_.clear();
+    free_events_.clear();
+  }
+
+ public:
   const GpuPartHashApi* api() const { return &api_; }
 
   static int hw_queues() {
@@ -1314,6 +1354,15 @@ int device_count() {
 PYBIND11_MODULE(_gpuhash, m) {
   m.doc() = "gfx950 batched SHA-1 piece verification (one lane per piece)";
   m.def("device_count", &device_count);
+  m.def(
+      "mem_info",
+      [](int device) {
+        size_t free_b = 0, total_b = 0;
+        HIP_CHECK(hipSetDevice(device));
+        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        return py::make_tuple(free_b, total_b);
+      },
+      py::arg("device") = 0, "(free, total) bytes of device memory (hipMemGetInfo)");
   m.def("arch", [] {
     hipDeviceProp_t p;
     HIP_CHECK(hipGetDeviceProperties(&p, 0));

@@ -280,6 +280,19 @@ def test_part_hasher_dispatcher_idles_while_every_slot_is_busy():
     del h
 
 
+def test_part_hasher_failed_setup_frees_what_it_allocated():
+    """A PartHasher whose slots do not fit in HBM fails to construct - and hands back the
+    slots, streams and events it had already made (no HBM leaked for the process's life
+    while the relay carries on hashing on the host)."""
+    from downloader_amd.ops import gpuhash
+    free0, total = gpuhash().mem_info(0)
+    slot = 32 << 30
+    with pytest.raises(Exception):
+        gpuhash().PartHasher(0, slot, int(total // slot) + 2, 1, 64)
+    free1, _ = gpuhash().mem_info(0)
+    assert free1 > free0 - (1 << 30), (free0, free1)
+
+
 def test_part_hasher_small_parts_through_the_relay(run, origin_cls):
     """Many small parts (64 pieces of 4 KiB: kernels of well under a millisecond) through the
     relay's asynchronous path. A kernel can then finish between the dispatcher's poll of its
