@@ -698,6 +698,10 @@ int64_t HttpConn::read_body_to_fd(const ResponseHead& h, int fd, int64_t offset,
             reusable_ = false;
             throw IoError(errstr("splice(file)"));
           }
+          if (out == 0) {                // nothing taken: a retry would spin
+            reusable_ = false;
+            throw IoError("splice(file) made no progress");
+          }
           left -= out;
           written += out;
           if (prog) prog->bytes.fetch_add(out, std::memory_order_relaxed);
@@ -823,6 +827,11 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
         dst.reusable_ = false;
         throw IoError(errstr("splice(dst)"));
       }
+      if (out == 0) {                    // nothing taken: a retry would spin
+        reusable_ = false;
+        dst.reusable_ = false;
+        throw IoError("splice(dst) made no progress");
+      }
       left -= out;
     }
     moved += in;
@@ -923,6 +932,10 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
                                SPLICE_F_MOVE | SPLICE_F_MORE);
         if (out < 0) {
           if (errno == EINTR) continue;
+          fail("splice(dst)");
+        }
+        if (out == 0) {                  // nothing taken: a retry would spin
+          errno = EPIPE;
           fail("splice(dst)");
         }
         chunk -= out;
@@ -1028,6 +1041,10 @@ int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* 
                                SPLICE_F_MOVE | SPLICE_F_MORE);
         if (out < 0) {
           if (errno == EINTR) continue;
+          fail("splice(dst)");
+        }
+        if (out == 0) {                  // nothing taken: a retry would spin
+          errno = EPIPE;
           fail("splice(dst)");
         }
         chunk -= out;
