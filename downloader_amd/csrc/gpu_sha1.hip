@@ -994,13 +994,14 @@ class PartHasher {
       std::string e = j->err;
       // nobody waits again for a failed copy (the relay hashes on the host), and once broken
       // the dispatcher thread has exited: the job can go
-      if (phase == GPU_PART_DONE || j->done || broken_) jobs_.erase(it);
+      if (phase == GPU_PART_DONE || j->done || broken_) jobs_.erase(t);   // by key: `it` may
+                                                                           // be stale after the wait
       return fail(err, errlen, e.c_str());
     }
     if (phase == GPU_PART_DONE) {
       if (out_len < j->digests.size()) return fail(err, errlen, "digest buffer too small");
       memcpy(out, j->digests.data(), j->digests.size());
-      jobs_.erase(it);
+      jobs_.erase(t);                // submit() may have rehashed jobs_ while this waited
     }
     return 0;
   }

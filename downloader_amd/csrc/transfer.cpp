@@ -1634,7 +1634,8 @@ CpuPartHasher::CpuPartHasher(double delay_s, int fail_copy_every, int fail_done_
     if ((phase == GPU_PART_COPIED && j->fail_copy) || (phase == GPU_PART_DONE && j->fail_done)) {
       snprintf(err, el, "injected device failure (%s)", phase == GPU_PART_COPIED ? "copy" : "hash");
       if (phase == GPU_PART_DONE)
-        i->jobs.erase(it);        // the worker thread is done with it
+        i->jobs.erase(t);         // the worker thread is done with it (by key: `it` may be
+                                  // stale after the wait)
       else
         j->abandoned = true;      // erased by the worker thread once it is done with it
       return -1;
@@ -1645,7 +1646,7 @@ CpuPartHasher::CpuPartHasher(double delay_s, int fail_copy_every, int fail_done_
         return -1;
       }
       memcpy(out, j->digests.data(), j->digests.size());
-      i->jobs.erase(it);
+      i->jobs.erase(t);
     }
     return 0;
   };
@@ -1684,11 +1685,17 @@ GpuPartStats gpu_part_stats() {
                       pending};
 }
 
+// Iterators into g_gpu_parts do not survive a wait: relays insert (and may rehash) while the
+// lock is released, so every wake looks the part up again.
 std::string gpu_part_wait(uint64_t id) {
   std::unique_lock<std::mutex> lk(g_gpu_mu);
+  if (g_gpu_parts.find(id) == g_gpu_parts.end()) throw IoError("gpu_part_wait: unknown part");
+  g_gpu_cv.wait(lk, [&] {
+    auto f = g_gpu_parts.find(id);
+    return f == g_gpu_parts.end() || f->second.finished;
+  });
   auto it = g_gpu_parts.find(id);
-  if (it == g_gpu_parts.end()) throw IoError("gpu_part_wait: unknown part");
-  g_gpu_cv.wait(lk, [&] { return it->second.finished; });
+  if (it == g_gpu_parts.end()) throw IoError("gpu_part_wait: part already collected");
   GpuPending p = std::move(it->second);
   g_gpu_parts.erase(it);
   if (p.failed) throw IoError(p.result);
@@ -1701,8 +1708,12 @@ void gpu_part_forget(uint64_t id) {
   if (it == g_gpu_parts.end()) return;
   it->second.forgotten = true;
   // the caller's buffer lease ends when this returns, as for a part hashed on the host
-  g_gpu_cv.wait(lk, [&] { return it->second.copied; });
-  if (it->second.finished) g_gpu_parts.erase(it);
+  g_gpu_cv.wait(lk, [&] {
+    auto f = g_gpu_parts.find(id);
+    return f == g_gpu_parts.end() || f->second.copied;
+  });
+  it = g_gpu_parts.find(id);
+  if (it != g_gpu_parts.end() && it->second.finished) g_gpu_parts.erase(it);
 }
 
 int gpu_part_eventfd() { return gpu_efd(); }
