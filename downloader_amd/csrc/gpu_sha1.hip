@@ -40,6 +40,7 @@
 #include <deque>
 #include <fcntl.h>
 #include <mutex>
+#include <exception>
 #include <stdexcept>
 #include <string>
 #include <pthread.h>
@@ -450,13 +451,29 @@ void parallel_for(size_t n, int threads, F&& fn) {
     for (size_t i = 0; i < n; ++i) fn(i);
     return;
   }
+  // An exception in a reader (or a thread that cannot be started) reaches the caller instead
+  // of std::terminate: the first one is rethrown once every started thread has joined.
   std::atomic<size_t> next{0};
-  std::vector<std::thread> pool;
-  for (int t = 0; t < threads; ++t)
-    pool.emplace_back([&] {
+  std::mutex err_mu;
+  std::exception_ptr err;
+  auto work = [&] {
+    try {
       for (size_t i; (i = next.fetch_add(1)) < n;) fn(i);
-    });
+    } catch (...) {
+      next.store(n);
+      std::lock_guard<std::mutex> g(err_mu);
+      if (!err) err = std::current_exception();
+    }
+  };
+  std::vector<std::thread> pool;
+  try {
+    for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+  } catch (...) {
+    // fewer threads than asked: the ones running (and this one) share the work
+  }
+  work();
   for (auto& th : pool) th.join();
+  if (err) std::rethrow_exception(err);
 }
 
 // Scoped device memory and events: released on every exit path, a thrown HIP error included
