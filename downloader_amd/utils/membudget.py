@@ -175,6 +175,13 @@ def part_budget(capacity: int) -> PartBudget:
     try:
         from ..ops import native
         native().relay_pool_set_budget(int(capacity))
-    except Exception:
-        pass
+    except Exception as e:           # no native module: nothing pools part buffers anyway
+        global _native_warned
+        if not _native_warned:
+            _native_warned = True
+            import logging
+            logging.getLogger(__name__).warning("native part pool budget not set: %s", e)
     return b
+
+
+_native_warned = False
