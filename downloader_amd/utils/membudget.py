@@ -179,8 +179,8 @@ def part_budget(capacity: int) -> PartBudget:
         global _native_warned
         if not _native_warned:
             _native_warned = True
-            import logging
-            logging.getLogger(__name__).warning("native part pool budget not set: %s", e)
+            from .log import get_logger
+            get_logger("membudget").warn("native part pool budget not set", err=str(e))
     return b
 
 
