@@ -100,6 +100,11 @@ def parse() -> argparse.Namespace:
     p.add_argument("--tls", choices=["off", "native", "aiohttp"], default="off",
                    help="origin and S3 over https (self-signed blobd certificate): TLS in the "
                         "native transport's threads, or through aiohttp on the event loop")
+    p.add_argument("--torrent-gb", type=float, default=20.0,
+                   help="same-call GPU vs host A/B of the streamed torrent path on a config-4 "
+                        "shaped torrent of this many GB (50 files, 4 MiB pieces; 0 = skip)")
+    p.add_argument("--torrent-pairs", type=int, default=3,
+                   help="timed jobs per backend in the torrent A/B (alternating)")
     p.add_argument("--compare-reference", action="store_true",
                    help="also time reference-equivalent mode and report the ratio")
     return p.parse_args()
@@ -251,22 +256,73 @@ async def _warmup(args, worker, url, wid: int, mode: str) -> None:
         raise RuntimeError(f"warmup job failed: {bad[0]}")
 
 
+def _cpu() -> tuple:
+    """(user+system, system) CPU seconds of this whole process: every thread, the native
+    transport's included."""
+    t = os.times()
+    return t.user + t.system, t.system
+
+
 async def _timed(args, worker, url, wid: int, mode: str, count: int) -> dict:
-    """The timed jobs of one worker process; ``elapsed`` is this process' own view."""
+    """The timed jobs of one worker process; ``elapsed`` is this process' own view and
+    ``cpu_s`` / ``sys_s`` the CPU it spent inside that window only (no interpreter start,
+    imports or warmup jobs)."""
     B = args.jobs_per_step
+    rc0 = _relay_counters()
+    cpu0, sys0 = _cpu()
     t0 = time.perf_counter()
     loop_cpu0 = time.thread_time()
     dt, res = await run_phase(worker, url, wid, args.warmup * B, count,
                               int(args.size_mb * 1e6), _tag(args, mode))
     loop_cpu = time.thread_time() - loop_cpu0
     t1 = time.perf_counter()
+    cpu1, sys1 = _cpu()
+    rc1 = _relay_counters()
     bad = [r for r in res if r.outcome != "staged"]
     pipes = _pipe_stats()
     # event-loop thread CPU / wall: ~1.0 means the Python side (one thread) is the limit
     return {"elapsed": t1 - t0, "latencies": [r.seconds for r in res],
             "bytes": sum(r.bytes for r in res), "failed": len(bad),
             "err": bad[0].error if bad else "", "loop_busy": loop_cpu / max(1e-9, t1 - t0),
+            "cpu_s": cpu1 - cpu0, "sys_s": sys1 - sys0,
+            "relay": {k: rc1[k] - rc0.get(k, 0) for k in rc1},
             "pipes_created": pipes.get("created", 0), "pipes_short": pipes.get("short", 0)}
+
+
+def _relay_counters() -> dict:
+    """The native transport's per-phase relay counters (``relay_counters``) of this process."""
+    try:
+        from downloader_amd.ops import native
+        return dict(native().relay_counters())
+    except Exception:
+        return {}
+
+
+def _sum_dicts(ds) -> dict:
+    out: dict = {}
+    for d in ds:
+        for k, v in d.items():
+            out[k] = out.get(k, 0) + v
+    return out
+
+
+def relay_breakdown(rc: dict, worker_cpu_s: float, gb: float) -> dict:
+    """Where the workers' CPU per GB went, from the native relay counters: the relaying
+    threads' own CPU (splice / peek-copy + CRC / copy modes), its CRC share, syscalls per MiB
+    and bytes per copy call; ``other`` = the rest of the worker processes (event loop, HTTP
+    heads, SigV4, job bookkeeping)."""
+    gb = max(1e-9, gb)
+    relay_ns = sum(rc.get(f"{m}_cpu_ns", 0) for m in ("splice", "dup", "copy"))
+    moved = sum(rc.get(f"{m}_bytes", 0) for m in ("splice", "dup", "copy"))
+    mib = max(1e-9, moved / (1 << 20))
+    return {"relay_threads_cpu_s_per_GB": round(relay_ns / 1e9 / gb, 4),
+            "crc_cpu_s_per_GB": round(rc.get("crc_ns", 0) / 1e9 / gb, 4),
+            "other_worker_cpu_s_per_GB": round(max(0.0, worker_cpu_s - relay_ns / 1e9) / gb, 4),
+            "splices_per_MiB": round((rc.get("splice_in_calls", 0)
+                                      + rc.get("splice_out_calls", 0)) / mib, 2),
+            "copy_KiB_per_call": round(rc.get("dup_copied_bytes", 0) / 1024
+                                       / max(1, rc.get("dup_calls", 0)), 1),
+            "relays": {m: rc.get(f"{m}_relays", 0) for m in ("splice", "dup", "copy")}}
 
 
 def _pipe_stats() -> dict:
@@ -279,7 +335,8 @@ def _pipe_stats() -> dict:
         return {}
 
 
-async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str, on_go=None):
+async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str, on_go=None,
+                    on_end=None):
     worker, url = await _start_worker(args, endpoint, mode, stage_root)
     await _warmup(args, worker, url, dist.rank, mode)
     dist.barrier()
@@ -290,17 +347,22 @@ async def rank_main(args, dist: Dist, endpoint: str, mode: str, stage_root: str,
     out = await _timed(args, worker, url, dist.rank, mode, args.steps * args.jobs_per_step)
     cuda_sync()
     out["elapsed"] = time.perf_counter() - t0
+    if on_end is not None:
+        on_end()
     await worker.stop()
     return out
 
 
 def _proc_main(conn, args, endpoint: str, mode: str, stage_root: str, wid: int, cpus: list,
-               count: int) -> None:
+               count: int, pool_workers: int = 0) -> None:
     """One worker process of a rank (``--procs-per-rank``): warm up, report ready, wait for
-    the rank's go, run its share of the timed jobs, report."""
+    the rank's go, run its share of the timed jobs, report (its CPU counted from "go" to its
+    last timed job only)."""
     if cpus:
         os.sched_setaffinity(0, cpus)
     os.environ.setdefault("LOG_LEVEL", "error")
+    if pool_workers:     # this process' share of the node's memory (utils/membudget)
+        os.environ["STAGER_POOL_WORKERS"] = str(pool_workers)
 
     async def go():
         worker, url = await _start_worker(args, endpoint, mode, stage_root)
@@ -310,11 +372,8 @@ def _proc_main(conn, args, endpoint: str, mode: str, stage_root: str, wid: int, 
             await worker.stop()
             return
         out = await _timed(args, worker, url, wid, mode, count)
-        await worker.stop()
-        t = os.times()
-        out["worker_cpu_s"] = t.user + t.system
-        out["worker_sys_s"] = t.system
         conn.send(("done", out))
+        await worker.stop()
     try:
         asyncio.run(go())
     except BaseException as e:   # the rank turns this into a failed run
@@ -323,7 +382,7 @@ def _proc_main(conn, args, endpoint: str, mode: str, stage_root: str, wid: int, 
 
 
 def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, nproc: int,
-               cpus: list, on_go=None) -> dict:
+               cpus: list, on_go=None, on_end=None) -> dict:
     """Run a rank as ``nproc`` worker processes (like ``downloader_amd supervisor -n`` does for
     a GPU slot): one asyncio worker saturates its event loop + GIL long before the rank's CPU
     share (two single-process ranks on one 16-CPU box: 82 GB/s vs 55 GB/s for one). Each
@@ -334,12 +393,15 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
     total = args.steps * args.jobs_per_step
     shares = [total // nproc + (1 if i < total % nproc else 0) for i in range(nproc)]
     per = len(cpus) // nproc if cpus else 0
+    # memory: every worker process of the node takes limit / (slots x processes per slot)
+    from downloader_amd.utils.cpus import gpu_slots
+    pool = max(gpu_slots(), int(os.environ.get("LOCAL_WORLD_SIZE", dist.world))) * nproc
     procs, conns = [], []
     for i in range(nproc):
         a, b = ctx.Pipe()
         sub = cpus[i * per:(i + 1) * per] if per >= 1 else []
         p = ctx.Process(target=_proc_main, args=(b, args, endpoint, mode, stage_root,
-                                                 dist.rank * 64 + i, sub, shares[i]),
+                                                 dist.rank * 64 + i, sub, shares[i], pool),
                         daemon=True)
         p.start()
         procs.append(p)
@@ -357,12 +419,16 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
         if on_go is not None:
             on_go()
         cuda_sync()
+        cpu0, sys0 = _cpu()                   # the rank's own process (it mostly waits)
         t0 = time.perf_counter()
         for c in conns:
             c.send("go")
         outs = [recv(c) for c in conns]
         cuda_sync()
         elapsed = time.perf_counter() - t0
+        cpu1, sys1 = _cpu()
+        if on_end is not None:
+            on_end()
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -374,8 +440,9 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
             "loop_busy": max(o["loop_busy"] for o in outs),
             "pipes_created": sum(o["pipes_created"] for o in outs),
             "pipes_short": sum(o["pipes_short"] for o in outs),
-            "child_cpu_s": sum(o["worker_cpu_s"] for o in outs),
-            "child_sys_s": sum(o["worker_sys_s"] for o in outs)}
+            "cpu_s": cpu1 - cpu0 + sum(o["cpu_s"] for o in outs),
+            "sys_s": sys1 - sys0 + sum(o["sys_s"] for o in outs),
+            "relay": _sum_dicts(o["relay"] for o in outs)}
 
 
 SINK_KEYS = ("bytes_received", "verify_objects", "verify_bytes", "verify_mismatches",
@@ -387,26 +454,32 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
             cpus: Optional[list] = None):
     stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
     at_go: dict = {}
+    peer_cpu = [0.0, 0.0]
 
+    # Timed-window CPU only: the peer's CPU from "go" to the rank's last timed job, the
+    # workers' from "go" to each one's last timed job (_timed) - never start-up or warmup.
     def on_go() -> None:
         if blob is not None:
             at_go.update(blob.stats())
-    peer_cpu0 = blob.cpu_seconds() if blob is not None else 0.0
-    t = os.times()
-    cpu0 = t.user + t.system
-    sys0 = t.system
+            peer_cpu[0] = blob.cpu_seconds()
+
+    def on_end() -> None:
+        if blob is not None:
+            peer_cpu[1] = blob.cpu_seconds()
     try:
         if nproc > 1:
-            out = rank_procs(args, dist, endpoint, mode, stage_root, nproc, cpus or [], on_go)
+            out = rank_procs(args, dist, endpoint, mode, stage_root, nproc, cpus or [], on_go,
+                             on_end)
         else:
-            out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root, on_go))
+            out = asyncio.run(rank_main(args, dist, endpoint, mode, stage_root, on_go, on_end))
     finally:
         if not args.stage_dir:
             shutil.rmtree(stage_root, ignore_errors=True)
-    t = os.times()
-    out["worker_cpu_s"] = t.user + t.system - cpu0 + out.pop("child_cpu_s", 0.0)
-    out["worker_sys_s"] = t.system - sys0 + out.pop("child_sys_s", 0.0)
-    out["peer_cpu_s"] = (blob.cpu_seconds() - peer_cpu0) if blob is not None else 0.0
+    out["worker_cpu_s"] = out.pop("cpu_s")
+    out["worker_sys_s"] = out.pop("sys_s")
+    # with --peers shared only rank 0 has a peer: its CPU is the whole job's
+    out["peer_cpu_s"] = peer_cpu[1] - peer_cpu[0]
+    out["cpus"] = len(cpus) if cpus else len(os.sched_getaffinity(0))
     dist.barrier()
     # The S3 peer's own counters, between "go" and the end of the timed jobs (every rank is
     # past the barrier): bytes it received, objects it matched against the origin generator.
@@ -435,18 +508,45 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
                                f"region < {jobs} timed jobs")
     gb_all = max(1e-9, sink["bytes_received"] / 1e9)
     mp = sink["multipart_objects"]
+    worker_cpu = sum(r["worker_cpu_s"] for r in allr)
+    peer_cpu = sum(r["peer_cpu_s"] for r in allr)
+    # what the ranks' CPU slices could have delivered in their timed windows: the measured
+    # CPU must fit inside it (a CPU-per-GB figure above it is an accounting error)
+    capacity = sum(r["elapsed"] * r["cpus"] for r in allr)
+    relay = _sum_dicts(r["relay"] for r in allr)
     return {"mbps": total_bytes / elapsed / 1e6, "elapsed": elapsed,
             "p50": statistics.median(lats) if lats else 0.0,
             "p90": sorted(lats)[int(0.9 * (len(lats) - 1))] if lats else 0.0,
             "bytes": total_bytes, "sink": sink,
             "parts_per_object": round(sink["multipart_parts"] / mp, 3) if mp else 1.0,
-            "worker_cpu_s_per_GB": sum(r["worker_cpu_s"] for r in allr) / gb_all,
-            "worker_sys_share": sum(r["worker_sys_s"] for r in allr)
-            / max(1e-9, sum(r["worker_cpu_s"] for r in allr)),
-            "peer_cpu_s_per_GB": sum(r["peer_cpu_s"] for r in allr) / gb_all,
+            "worker_cpu_s_per_GB": worker_cpu / gb_all,
+            "worker_sys_share": sum(r["worker_sys_s"] for r in allr) / max(1e-9, worker_cpu),
+            "peer_cpu_s_per_GB": peer_cpu / gb_all,
+            "timed_cpu_s": worker_cpu + peer_cpu, "cpu_capacity_s": capacity,
+            "breakdown": relay_breakdown(relay, worker_cpu, gb_all),
             "loop_busy": max(r["loop_busy"] for r in allr),
             "pipes_created": sum(r["pipes_created"] for r in allr),
             "pipes_short": sum(r["pipes_short"] for r in allr)}
+
+
+def torrent_measure(args, dist: Dist) -> dict:
+    """After the config-2 lines: the streamed-torrent path with its pieces hashed on this
+    rank's GPU (PartHasher, ``stream_verify_backend: auto``) vs on the host (``cpu``),
+    alternating, same call (``bench/torrent_ab.py``). Ranks start together; totals are summed
+    over ranks (they run at once), device counters too."""
+    from downloader_amd.bench.torrent_ab import torrent_ab
+    dist.barrier()
+    r = asyncio.run(torrent_ab(total_bytes=int(args.torrent_gb * 1e9), pairs=args.torrent_pairs,
+                               tag=f"ab-r{dist.rank}"))
+    allr = dist.gather(r)
+    out = dict(allr[0])
+    for k in ("torrent_gpu_MBps", "torrent_host_MBps", "gpu_parts", "gpu_host_fallbacks",
+              "gpu_refused", "gpu_launches"):
+        if k in out:
+            out[k] = round(sum(x[k] for x in allr), 1) if "MBps" in k else sum(x[k] for x in allr)
+    if len(allr) > 1:
+        out["torrent_ranks"] = len(allr)
+    return out
 
 
 def pin_rank(dist: Dist, per_rank: int = 0) -> list:
@@ -546,6 +646,7 @@ def main() -> int:
             crc = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
             args.checksum, args.crc_run = saved, False
         ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
+        tor = torrent_measure(args, dist) if args.torrent_gb > 0 and args.mode == "tuned" else None
     finally:
         if blob is not None:
             blob.stop()
@@ -576,6 +677,10 @@ def main() -> int:
             "worker_kernel_share": round(tuned["worker_sys_share"], 3),   # system / (user+system)
             "event_loop_busy": round(tuned["loop_busy"], 3),
             "peer_cpu_s_per_GB": round(tuned["peer_cpu_s_per_GB"], 4),
+            # worker + peer CPU-seconds of the timed window / what the ranks' CPU slices could
+            # give in it (elapsed x CPUs): <= 1 for physically consistent CPU figures
+            "cpu_utilisation": round(tuned["timed_cpu_s"] / max(1e-9, tuned["cpu_capacity_s"]), 3),
+            "worker_breakdown": tuned["breakdown"],
             # splice pipes created below their asked capacity (pipe page budget spent)
             "pipes_short": {"workers": tuned["pipes_short"], "of": tuned["pipes_created"]},
             "pipe_kb": args.pipe_kb_eff,
@@ -616,8 +721,13 @@ def main() -> int:
             line["crc_relay_worker_cpu_s_per_GB"] = round(crc["worker_cpu_s_per_GB"], 4)
             # the sink recomputes every CRC (recv + CRC instead of splice) on the same CPUs
             line["crc_relay_peer_cpu_s_per_GB"] = round(crc["peer_cpu_s_per_GB"], 4)
+            line["crc_relay_cpu_utilisation"] = round(
+                crc["timed_cpu_s"] / max(1e-9, crc["cpu_capacity_s"]), 3)
+            line["crc_relay_worker_breakdown"] = crc["breakdown"]
             line["crc_relay_sink_checked_puts"] = crc["sink"]["checksummed_puts"]
             line["crc_relay_integrity"] = "crc32c"
+        if tor is not None:      # same call: streamed torrent, GPU vs host piece hashing
+            line.update(tor)
         if ref is not None:
             line["reference_mode_MBps"] = round(ref["mbps"], 2)
             line["reference_mode_p50_s"] = round(ref["p50"], 4)

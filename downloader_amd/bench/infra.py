@@ -30,8 +30,11 @@ class Blobd:
                  host: str = "127.0.0.1", files_root: str = "", sink: str = "checksum",
                  tls: Optional[Tuple[str, str]] = None, s3_fail_rate: float = 0.0,
                  synth_bucket: str = "", synth_objects: Optional[Dict[str, int]] = None,
-                 s3_corrupt_rate: float = 0.0):
+                 s3_corrupt_rate: float = 0.0,
+                 synth_files: Optional[Dict[str, Tuple[int, int]]] = None):
         self.files_root = files_root
+        # webseed files served from the origin pool: relpath -> (size, seed)
+        self.synth_files = dict(synth_files or {})
         self.tls = tls                  # (cert PEM, key PEM): serve https
         self.s3_fail_rate = s3_fail_rate  # share of object/part PUTs answered 503 SlowDown
         # share of checksummed PUT bodies with one byte flipped on arrival (-> 400 BadDigest)
@@ -58,7 +61,8 @@ class Blobd:
             + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else [])
             + (["--s3-corrupt-rate", str(self.s3_corrupt_rate)] if self.s3_corrupt_rate else [])
             + (["--synth-bucket", self.synth_bucket, "--synth-manifest",
-                self._manifest(d)] if self.synth_bucket else []),
+                self._manifest(d)] if self.synth_bucket else [])
+            + (["--synth-files", self._files_manifest(d)] if self.synth_files else []),
             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         t0 = time.time()
         while not os.path.exists(pf):
@@ -81,6 +85,18 @@ class Blobd:
             for k, n in self.synth_objects.items():
                 f.write(f"{k} {n}\n")
         return p
+
+    def _files_manifest(self, d: str) -> str:
+        p = os.path.join(d, "synth-files")
+        with open(p, "w") as f:
+            for rel, (n, seed) in self.synth_files.items():
+                f.write(f"{rel} {n} {seed}\n")
+        return p
+
+    def pool(self) -> bytes:
+        """The origin's 64 MiB byte pool: synthetic byte o of seed s = pool[(o + 7919 s) % 64 MiB]."""
+        with urllib.request.urlopen(f"http://{self.endpoint}/_pool", timeout=60) as r:
+            return r.read()
 
     @property
     def scheme(self) -> str:

@@ -1,0 +1,131 @@
+"""Same-call A/B of the streamed torrent path: pieces hashed by the gfx950 PartHasher
+(``download.stream_verify_backend: auto``) vs the host multi-buffer SHA-1 (``cpu``).
+
+A config-4-shaped torrent (BASELINE.json config 4: 20 GB, 50 files, full piece verification,
+one S3 object per file; 4 MiB pieces) is served by a ``blobd`` webseed from its synthetic
+pool (``bench/synth_torrent.py``: no data on disk) and staged by two workers of this process,
+one per backend, alternating job by job after one untimed job each (HIP initialisation,
+connection pools). The reference verifies every piece with SHA-1 in webtorrent
+(/root/reference/lib/download.js:64); this measures both of our ways of doing that under the
+same clock, in the call that produces the driver's bench line.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import shutil
+import statistics
+import tempfile
+import time
+from typing import Dict, List
+
+from .infra import Blobd
+from .synth_torrent import config4_files, make_synth_torrent, served_paths
+
+MB = 1_000_000
+
+
+def _cpu() -> float:
+    t = os.times()
+    return t.user + t.system
+
+
+async def _stage(w, msg) -> tuple:
+    done = asyncio.get_running_loop().create_future()
+
+    def cb(r):
+        if not done.done():
+            done.set_result(r)
+    w.on_result = cb
+    t0 = time.perf_counter()
+    await w.submit(msg)
+    r = await asyncio.wait_for(done, 900)
+    w.on_result = None
+    return time.perf_counter() - t0, r
+
+
+async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len: int = 4 << 20,
+                     pairs: int = 3, stage_root: str = "", tag: str = "ab",
+                     backends=("auto", "cpu")) -> Dict:
+    """Stage the torrent ``pairs`` times per backend, alternating; medians of the timed jobs."""
+    from ..broker.memory import MemoryBroker
+    from ..models import api
+    from ..ops import hashing
+    from ..service.worker import Worker
+    from ..utils.config import load_config
+
+    name = "Show"
+    fl = config4_files(total_bytes, files, name)
+    total = sum(n for _, n, _ in fl)
+    root = tempfile.mkdtemp(prefix="torrent-ab-")
+    stage = stage_root or tempfile.mkdtemp(prefix="torrent-ab-stage-")
+    workers = {}
+    try:
+        with Blobd(sink="discard", files_root=root, synth_files=served_paths(name, fl)) as b:
+            t0 = time.perf_counter()
+            raw = make_synth_torrent(b.pool(), name, fl, piece_len, b.files_url(),
+                                     threads=min(16, os.cpu_count() or 1))
+            setup_s = time.perf_counter() - t0
+            with open(os.path.join(root, "job.torrent"), "wb") as f:
+                f.write(raw)
+            for be in backends:
+                cfg = load_config(overrides={
+                    "instance": {"download_path": os.path.join(stage, be)},
+                    "s3": {"endpoint": b.endpoint}, "broker": {"backend": "memory"},
+                    "health": {"enabled": False},
+                    "download": {"torrent_enable_dht": False, "progress_interval_s": 5.0,
+                                 "stream_verify_backend": be, "gpu_prewarm": be != "cpu"}},
+                    env={})
+                w = Worker(cfg, broker=MemoryBroker())
+                await w.start(health=False)
+                workers[be] = w
+            url = b.files_url("job.torrent")
+            runs: Dict[str, List[dict]] = {be: [] for be in backends}
+            dev0 = None
+            for k in range(pairs + 1):                 # round 0: one untimed job each
+                for be in backends:
+                    if be != "cpu" and k == 1:
+                        dev0 = hashing.gpu_relay_stats()
+                    msg = api.make_download(f"{tag}-{be}-{k}", "http", url, "TV")
+                    c0, p0 = _cpu(), b.cpu_seconds()
+                    dt, r = await _stage(workers[be], msg)
+                    c1, p1 = _cpu(), b.cpu_seconds()
+                    if r.outcome != "staged":
+                        raise RuntimeError(f"torrent A/B job ({be}) failed: {r.error}")
+                    if r.bytes != total:
+                        raise RuntimeError(f"torrent A/B job ({be}) staged {r.bytes} of {total}")
+                    if k:
+                        t = r.stats.get("torrent", {})
+                        runs[be].append({"s": dt, "worker_cpu_s": c1 - c0, "peer_cpu_s": p1 - p0,
+                                         "hash_fails": t.get("hash_fails", 0)})
+            dev1 = hashing.gpu_relay_stats() if any(be != "cpu" for be in backends) else {}
+            st = b.stats()
+    finally:
+        for w in workers.values():
+            await w.stop()
+        shutil.rmtree(root, ignore_errors=True)
+        if not stage_root:
+            shutil.rmtree(stage, ignore_errors=True)
+
+    out: Dict = {"torrent_bytes": total, "torrent_files": len(fl), "torrent_piece_len": piece_len,
+                 "torrent_pairs": pairs, "torrent_setup_s": round(setup_s, 2),
+                 "torrent_sink_bytes": st.get("bytes_received", 0)}
+    for be in backends:
+        xs = runs[be]
+        key = "gpu" if be != "cpu" else "host"
+        med = statistics.median(x["s"] for x in xs)
+        out[f"torrent_{key}_MBps"] = round(total / med / MB, 1)
+        out[f"torrent_{key}_MBps_runs"] = [round(total / x["s"] / MB, 1) for x in xs]
+        out[f"torrent_{key}_worker_cpu_s_per_GB"] = round(
+            statistics.median(x["worker_cpu_s"] for x in xs) / (total / 1e9), 4)
+        out[f"torrent_{key}_hash_fails"] = sum(x["hash_fails"] for x in xs)
+    if dev0 is not None:
+        d = {k: dev1.get(k, 0) - dev0.get(k, 0) for k in
+             ("submitted", "host_fallbacks", "refused", "device_launches", "device_lanes")}
+        out["gpu_parts"] = d["submitted"]
+        out["gpu_host_fallbacks"] = d["host_fallbacks"]
+        out["gpu_refused"] = d["refused"]
+        out["gpu_launches"] = d["device_launches"]
+        out["gpu_lanes_per_launch"] = round(d["device_lanes"] / d["device_launches"], 1) \
+            if d["device_launches"] else 0.0
+    return out

@@ -10,6 +10,9 @@
 //            PUT|GET|HEAD|DELETE /<bucket>/<key>, multipart (POST ?uploads, PUT ?partNumber,
 //            POST ?uploadId, DELETE ?uploadId)
 //   stats:   GET /_stats  (JSON: bytes received/served, objects, requests)
+//   pool:    GET /_pool   (the 64 MiB pool every synthetic byte is taken from)
+//   --synth-files FILE ("<path> <size> <seed>" lines): BEP-19 webseed files under
+//            /files/<path> made of pool bytes (a 20 GB torrent without 20 GB on disk)
 //   --synth-bucket NAME --synth-manifest FILE ("<key> <size>" lines): a read-only source
 //            bucket of synthetic objects (List v2, HEAD, GET with Range) for bucket:// jobs;
 //            query-string auth (presigned URLs) is accepted, signatures are not checked
@@ -121,6 +124,9 @@ std::string g_files_root;  // --files-root: GET|HEAD /files/<path> served with s
 uint64_t g_default_size = 100ull << 20;
 SSL_CTX* g_tls = nullptr;  // --tls-cert / --tls-key
 std::string g_synth_bucket;                       // --synth-bucket
+// --synth-files FILE ("<path> <size> <seed>" lines): webseed files under /files/<path> whose
+// bytes are the origin pool's (no disk, sendfile from the pool's memfd)
+std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> g_synth_files;
 std::map<std::string, uint64_t> g_synth_objects;  // key -> size (--synth-manifest)
 double g_s3_fail_rate = 0;  // --s3-fail-rate: this share of object/part PUTs answer 503 SlowDown
 std::atomic<uint64_t> g_s3_faults{0};
@@ -710,9 +716,14 @@ class Conn {
       std::lock_guard<std::mutex> lk(g_media_mu);  // what a staged copy of it must contain
       g_media[r.path.substr(7)] = {size, seed};
     }
+    return serve_pool(r, size, seed, "Content-Type: video/x-matroska\r\n");
+  }
+
+  // GET|HEAD (with Range) of a synthetic object: byte o = pool[(o + seed * 7919) % kPool].
+  bool serve_pool(const Request& r, uint64_t size, uint64_t seed, const char* ctype) {
     uint64_t start = 0, end = size ? size - 1 : 0;
     bool ranged = false;
-    it = r.h.find("range");
+    auto it = r.h.find("range");
     if (it != r.h.end() && it->second.rfind("bytes=", 0) == 0) {
       std::string spec = it->second.substr(6);
       size_t dash = spec.find('-');
@@ -731,9 +742,9 @@ class Conn {
     uint64_t len = size ? end - start + 1 : 0;
     char hdr[512];
     int n = snprintf(hdr, sizeof hdr,
-                     "HTTP/1.1 %d %s\r\nServer: blobd\r\nContent-Type: video/x-matroska\r\n"
+                     "HTTP/1.1 %d %s\r\nServer: blobd\r\n%s"
                      "Accept-Ranges: bytes\r\nContent-Length: %" PRIu64 "\r\n",
-                     ranged ? 206 : 200, ranged ? "Partial Content" : "OK", len);
+                     ranged ? 206 : 200, ranged ? "Partial Content" : "OK", ctype, len);
     std::string out(hdr, (size_t)n);
     if (ranged)
       out += "Content-Range: bytes " + std::to_string(start) + "-" + std::to_string(end) + "/" +
@@ -769,6 +780,8 @@ class Conn {
   // Static files for BEP-19 webseeds: Range support, zero-copy sendfile from the page cache.
   bool files(const Request& r) {
     std::string rel = r.path.substr(7);
+    auto sy = g_synth_files.find(rel);      // a synthetic file (--synth-files): the origin pool
+    if (sy != g_synth_files.end()) return serve_pool(r, sy->second.first, sy->second.second, "");
     if (g_files_root.empty() || rel.find("..") != std::string::npos)
       return respond(404, "Not Found", "no such file", "", "text/plain");
     std::string full = g_files_root + "/" + rel;
@@ -1124,6 +1137,8 @@ class Conn {
 
   bool dispatch(const Request& r) {
     if (r.path == "/_stats") return stats();
+    // the origin pool itself: lets a client build metainfo (piece hashes) for --synth-files
+    if (r.path == "/_pool" && r.method == "GET") return serve_pool(r, kPool, 0, "");
     if (r.path.rfind("/media/", 0) == 0 && (r.method == "GET" || r.method == "HEAD")) return origin(r);
     if (r.path.rfind("/files/", 0) == 0 && (r.method == "GET" || r.method == "HEAD")) return files(r);
     return s3(r);
@@ -1164,6 +1179,20 @@ int main(int argc, char** argv) {
     else if (a == "--tls-key") tls_key = next();
     else if (a == "--s3-fail-rate") g_s3_fail_rate = atof(next());
     else if (a == "--synth-bucket") g_synth_bucket = next();
+    else if (a == "--synth-files") {
+      FILE* f = fopen(next(), "r");
+      char line[4096];
+      while (f && fgets(line, sizeof line, f)) {
+        std::string l(line);
+        while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+        size_t b = l.rfind(' ');
+        size_t a2 = b == std::string::npos || b == 0 ? std::string::npos : l.rfind(' ', b - 1);
+        if (a2 == std::string::npos) continue;
+        g_synth_files[l.substr(0, a2)] = {strtoull(l.c_str() + a2 + 1, nullptr, 10),
+                                          strtoull(l.c_str() + b + 1, nullptr, 10)};
+      }
+      if (f) fclose(f);
+    }
     else if (a == "--synth-manifest") {
       FILE* f = fopen(next(), "r");
       char line[4096];

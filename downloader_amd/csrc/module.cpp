@@ -217,6 +217,24 @@ PYBIND11_MODULE(_native, m) {
         "Restart the pool's high-water mark (peak_bytes) and its over_budget count");
   m.def("relay_pool_set_max_idle", &relay_pool_set_max_idle, py::arg("n"),
         "Keep at most n idle part buffers (the rest are unmapped on release)");
+  m.def("relay_counters", []() {
+    RelayCounters c = relay_counters();
+    py::dict d;
+    const char* modes[3] = {"splice", "dup", "copy"};
+    for (int i = 0; i < 3; ++i) {
+      d[(std::string(modes[i]) + "_relays").c_str()] = c.relays[i];
+      d[(std::string(modes[i]) + "_bytes").c_str()] = c.bytes[i];
+      d[(std::string(modes[i]) + "_cpu_ns").c_str()] = c.cpu_ns[i];
+    }
+    d["splice_in_calls"] = c.splice_in_calls;
+    d["splice_out_calls"] = c.splice_out_calls;
+    d["dup_calls"] = c.dup_calls;
+    d["dup_copied_bytes"] = c.dup_bytes;
+    d["crc_ns"] = c.crc_ns;
+    d["crc_bytes"] = c.crc_bytes;
+    return d;
+  }, "Per-phase relay counters since start (relay_body_to): relays / bytes / relaying-thread "
+     "CPU per mode (splice, dup = peek|tee copy + CRC, copy), syscalls, copy and CRC time");
   m.def("pipe_stats", []() {
     PipeStats s = pipe_stats();
     py::dict d;

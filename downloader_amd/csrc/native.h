@@ -122,6 +122,17 @@ struct PipeStats {
   size_t in_use, in_use_bytes, idle, idle_bytes;
 };
 PipeStats pipe_stats();
+// Per-phase counters of relay_body_to (process-wide, since start): where a checksummed
+// relay's CPU goes next to the plain splice one. Modes: 0 splice (no user-space copy),
+// 1 dup (recv(MSG_PEEK) or tee() copy + CRC, splice), 2 copy (recv + send: TLS, no pipe).
+// `cpu_ns` is the relaying thread's own CPU (CLOCK_THREAD_CPUTIME_ID around the call).
+struct RelayCounters {
+  uint64_t relays[3], bytes[3], cpu_ns[3];
+  uint64_t splice_in_calls, splice_out_calls;   // socket -> pipe, pipe -> socket (all modes)
+  uint64_t dup_calls, dup_bytes;                // recv(MSG_PEEK) / read(tee) copies
+  uint64_t crc_ns, crc_bytes;                   // CRC32C over the copied bytes
+};
+RelayCounters relay_counters();
 // Capacity asked for new pipes: the splice pipe, and the tee() duplicate pipe (0 = keep).
 void set_pipe_sizes(size_t main, size_t tee);
 // Tests: refuse every pipe, as when the budget is spent (transfers fall back to copying).

@@ -57,6 +57,52 @@ std::string errstr(const char* what) { return std::string(what) + ": " + strerro
 // included, in the workers and in the S3 peer alike - ran a busy 16-relay worker into it.
 // Now only running transfers hold pipes (plus a few idle ones for reuse).
 std::atomic<size_t> g_pipe_main{size_t(1) << 20}, g_pipe_tee{size_t(1) << 20};
+
+// ---- relay counters (RelayCounters) ---------------------------------------------------------
+// The hot loops bump a thread_local tally (no shared cache line per syscall); relay_body_to
+// folds it into the process-wide atomics once per relay.
+struct RelayTally {
+  uint64_t splice_in = 0, splice_out = 0, dup_calls = 0, dup_bytes = 0, crc_ns = 0, crc_bytes = 0;
+};
+thread_local RelayTally t_tally;
+struct {
+  std::atomic<uint64_t> relays[3], bytes[3], cpu_ns[3];
+  std::atomic<uint64_t> splice_in{0}, splice_out{0}, dup_calls{0}, dup_bytes{0}, crc_ns{0},
+      crc_bytes{0};
+} g_rc;
+
+uint64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+// Scope of one relay_body_to: thread CPU and the tally's growth go to mode `mode`.
+struct RelayScope {
+  int mode = 0;
+  int64_t* moved;
+  uint64_t cpu0 = thread_cpu_ns();
+  RelayTally t0 = t_tally;
+  explicit RelayScope(int64_t* m) : moved(m) {}
+  ~RelayScope() {
+    const RelayTally& t = t_tally;
+    g_rc.relays[mode].fetch_add(1, std::memory_order_relaxed);
+    g_rc.bytes[mode].fetch_add((uint64_t)std::max<int64_t>(0, *moved), std::memory_order_relaxed);
+    g_rc.cpu_ns[mode].fetch_add(thread_cpu_ns() - cpu0, std::memory_order_relaxed);
+    g_rc.splice_in.fetch_add(t.splice_in - t0.splice_in, std::memory_order_relaxed);
+    g_rc.splice_out.fetch_add(t.splice_out - t0.splice_out, std::memory_order_relaxed);
+    g_rc.dup_calls.fetch_add(t.dup_calls - t0.dup_calls, std::memory_order_relaxed);
+    g_rc.dup_bytes.fetch_add(t.dup_bytes - t0.dup_bytes, std::memory_order_relaxed);
+    g_rc.crc_ns.fetch_add(t.crc_ns - t0.crc_ns, std::memory_order_relaxed);
+    g_rc.crc_bytes.fetch_add(t.crc_bytes - t0.crc_bytes, std::memory_order_relaxed);
+  }
+};
 std::atomic<uint64_t> g_pipes_created{0}, g_pipes_short{0};
 std::atomic<bool> g_pipes_refused{false};   // tests: behave as if the budget were spent
 
@@ -765,7 +811,13 @@ static bool relay_tee_on() {
 }
 
 int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32_t* crc) {
-  int64_t moved = 0;
+  int64_t moved = 0, done = 0;
+  RelayScope scope(&done);
+  auto fin = [&](int mode, int64_t m) {
+    scope.mode = mode;
+    done = m;
+    return m;
+  };
   if (rpos_ < rend_) {
     int64_t k = std::min<int64_t>(n, (int64_t)(rend_ - rpos_));
     if (crc) *crc = stager::crc32c(rbuf_.data() + rpos_, (size_t)k, *crc);
@@ -774,8 +826,9 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     moved += k;
     if (prog) prog->bytes.fetch_add(k, std::memory_order_relaxed);
   }
-  if (moved == n) return moved;
-  if (ssl_ || dst.ssl_ || (crc && !relay_tee_on())) return relay_copy(dst, n, moved, prog, crc);
+  if (moved == n) return fin(0, moved);
+  if (ssl_ || dst.ssl_ || (crc && !relay_tee_on()))
+    return fin(2, relay_copy(dst, n, moved, prog, crc));
   if (crc) {
     // CRC staging, L2-sized: relaybench peekcrc at 8 threads, 64 / 128 / 256 / 512 / 1024
     // KiB: 36.3 / 36.7 / 37.5 / 39.4 / 38.1 GB/s (profiles/r4/peekbuf/)
@@ -786,14 +839,19 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
           len = std::min(len, cbuf.size());
           return cbuf.data();
         },
-        [&](const uint8_t* p, size_t k) { *crc = stager::crc32c(p, k, *crc); });
-    return m >= 0 ? m : relay_copy(dst, n, moved, prog, crc);
+        [&](const uint8_t* p, size_t k) {
+          uint64_t t0 = mono_ns();
+          *crc = stager::crc32c(p, k, *crc);
+          t_tally.crc_ns += mono_ns() - t0;
+          t_tally.crc_bytes += k;
+        });
+    return m >= 0 ? fin(1, m) : fin(2, relay_copy(dst, n, moved, prog, crc));
   }
   std::unique_ptr<PipeLease> lease;
   try {
     lease.reset(new PipeLease(g_pipe_main.load()));
   } catch (const IoError&) {
-    return relay_copy(dst, n, moved, prog, nullptr);   // no pipe to be had: copy instead
+    return fin(2, relay_copy(dst, n, moved, prog, nullptr));   // no pipe to be had: copy
   }
   PipeLease& pl = *lease;
   const int pr = pl.p.r, pw = pl.p.w;
@@ -805,6 +863,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     }
     size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)pl.p.cap);
     ssize_t in = ::splice(fd_, nullptr, pw, nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+    ++t_tally.splice_in;
     if (in < 0) {
       if (errno == EINTR) continue;
       reusable_ = false;
@@ -821,6 +880,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     while (left > 0) {
       ssize_t out = ::splice(pr, nullptr, dst.fd_, nullptr, (size_t)left,
                              SPLICE_F_MOVE | SPLICE_F_MORE);
+      ++t_tally.splice_out;
       if (out < 0) {
         if (errno == EINTR) continue;
         reusable_ = false;
@@ -838,7 +898,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     if (prog) prog->bytes.fetch_add(in, std::memory_order_relaxed);
   }
   pl.clean = true;
-  return moved;
+  return fin(0, moved);
 }
 
 // The bytes sent and the bytes the caller sees are the same pipe pages: splice moves page
@@ -892,6 +952,7 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
     }
     size_t want = (size_t)std::min<int64_t>(n - moved, (int64_t)main.p.cap);
     ssize_t in = ::splice(fd_, nullptr, main.p.w, nullptr, want, SPLICE_F_MOVE | SPLICE_F_MORE);
+    ++t_tally.splice_in;
     if (in < 0) {
       if (errno == EINTR) continue;
       if (errno == EAGAIN) {
@@ -924,12 +985,15 @@ int64_t HttpConn::relay_tee(HttpConn& dst, int64_t n, int64_t moved, Progress* p
         ssize_t r = ::read(dup.p.r, p, len);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) fail("read(tee)");
+        ++t_tally.dup_calls;
+        t_tally.dup_bytes += (uint64_t)r;
         got(p, (size_t)r);
         seen += r;
       }
       for (ssize_t chunk = t; chunk > 0;) {
         ssize_t out = ::splice(main.p.r, nullptr, dst.fd_, nullptr, (size_t)chunk,
                                SPLICE_F_MOVE | SPLICE_F_MORE);
+        ++t_tally.splice_out;
         if (out < 0) {
           if (errno == EINTR) continue;
           fail("splice(dst)");
@@ -1008,6 +1072,7 @@ int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* 
     size_t len = (size_t)std::min<int64_t>(n - moved, (int64_t)main.p.cap);
     uint8_t* p = room(len);
     ssize_t k = ::recv(fd_, p, len, MSG_PEEK);
+    ++t_tally.dup_calls;
     if (k < 0) {
       if (errno == EINTR) continue;
       if (errno == EAGAIN || errno == EWOULDBLOCK) {
@@ -1022,11 +1087,13 @@ int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* 
       dst.reusable_ = false;
       throw IoError("source closed mid-body");
     }
+    t_tally.dup_bytes += (uint64_t)k;
     got(p, (size_t)k);
     for (ssize_t left = k; left > 0;) {
       // the peeked bytes are queued already: this splice moves them without waiting
       ssize_t in = ::splice(fd_, nullptr, main.p.w, nullptr, (size_t)left,
                             SPLICE_F_MOVE | SPLICE_F_MORE);
+      ++t_tally.splice_in;
       if (in < 0) {
         if (errno == EINTR) continue;
         fail("splice(src)");
@@ -1039,6 +1106,7 @@ int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* 
       for (ssize_t chunk = in; chunk > 0;) {
         ssize_t out = ::splice(main.p.r, nullptr, dst.fd_, nullptr, (size_t)chunk,
                                SPLICE_F_MOVE | SPLICE_F_MORE);
+        ++t_tally.splice_out;
         if (out < 0) {
           if (errno == EINTR) continue;
           fail("splice(dst)");
@@ -1750,6 +1818,22 @@ std::string relay_dup_mode() { return relay_peek_on() ? "peek" : "tee"; }
 
 size_t relay_pool_trim(size_t keep_bytes) { return part_pool().trim(keep_bytes); }
 PipeStats pipe_stats() { return pipe_pool().stats(); }
+
+RelayCounters relay_counters() {
+  RelayCounters c{};
+  for (int i = 0; i < 3; ++i) {
+    c.relays[i] = g_rc.relays[i].load();
+    c.bytes[i] = g_rc.bytes[i].load();
+    c.cpu_ns[i] = g_rc.cpu_ns[i].load();
+  }
+  c.splice_in_calls = g_rc.splice_in.load();
+  c.splice_out_calls = g_rc.splice_out.load();
+  c.dup_calls = g_rc.dup_calls.load();
+  c.dup_bytes = g_rc.dup_bytes.load();
+  c.crc_ns = g_rc.crc_ns.load();
+  c.crc_bytes = g_rc.crc_bytes.load();
+  return c;
+}
 void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
 void set_pipe_sizes(size_t main, size_t tee) {
   if (main) g_pipe_main.store(main);

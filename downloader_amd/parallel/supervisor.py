@@ -73,8 +73,9 @@ class Supervisor:
         # the workers share the uid's pipe page budget: size their splice pipes for all n
         # (an explicit setting in the environment wins)
         env.setdefault("STAGER_DOWNLOAD__PIPE_SHARERS", str(max(4, self.n)))
-        # ... and the container's memory: each sizes its part-buffer budget to its share
-        env.setdefault("STAGER_POOL_WORKERS", str(self.n))
+        # ... and the slot's memory: each sizes its part-buffer budget to its share, memory
+        # limit / (GPU slots x workers per slot) (utils/membudget.pool_workers)
+        env.setdefault("STAGER_PROCS_PER_SLOT", str(self.n))
         if self.base_port:
             env["PORT"] = str(self.base_port + s.index)   # distinct /health ports
         cpus = self.cpus[s.index]

@@ -17,8 +17,11 @@ idle buffers before it maps a new one, and records its high-water mark (``peak_b
 
 Default: ``download.relay_memory_fraction`` (0.25) of this worker's share of the memory
 limit - the cgroup's ``memory.max`` (else physical memory) divided by the worker processes
-the supervisor started in the same container (``STAGER_POOL_WORKERS``).
-``download.relay_memory_mb`` overrides it.
+that share it (``pool_workers``): ``STAGER_POOL_WORKERS`` when set, else the node's GPU slots
+(``utils.cpus.gpu_slots``, as the CPU budget is divided) x the worker processes of one slot
+(``STAGER_PROCS_PER_SLOT``, set by the supervisor and the bench, default 1). A worker on a
+shared 8-GPU node therefore takes 1/8 of the node's budget even when nothing told it how many
+neighbours it has. ``download.relay_memory_mb`` overrides it.
 """
 from __future__ import annotations
 
@@ -69,12 +72,27 @@ def memory_limit() -> int:
     return lim or phys
 
 
-def pool_workers() -> int:
-    """Worker processes sharing the container's memory (set by parallel/supervisor.py)."""
+def _env_int(name: str) -> int:
     try:
-        return max(1, int(os.environ.get("STAGER_POOL_WORKERS", "1") or 1))
+        return max(0, int(os.environ.get(name, "") or 0))
     except ValueError:
-        return 1
+        return 0
+
+
+def procs_per_slot() -> int:
+    """Worker processes one GPU slot runs (``STAGER_PROCS_PER_SLOT``; supervisor ``-n``,
+    bench ``--procs-per-rank``)."""
+    return max(1, _env_int("STAGER_PROCS_PER_SLOT"))
+
+
+def pool_workers() -> int:
+    """Worker processes sharing this memory limit: ``STAGER_POOL_WORKERS`` if set, else
+    GPU slots of the node x processes per slot (the per-slot share, like the CPU budget)."""
+    n = _env_int("STAGER_POOL_WORKERS")
+    if n:
+        return n
+    from .cpus import gpu_slots
+    return max(1, gpu_slots()) * procs_per_slot()
 
 
 def relay_budget_bytes(download_cfg) -> int:

@@ -92,7 +92,8 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4", "--jobs-per-step", "2"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4", "--jobs-per-step", "2",
+           "--torrent-gb", "0.05", "--torrent-pairs", "1"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -103,12 +104,15 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
         assert k in j
     assert j["n_gpus"] == 2 and j["steps"] == 2 and j["value"] > 0
     assert j["config"]["jobs_timed"] == 2 * 2 * 2   # ranks x steps x jobs-per-step
+    # the torrent A/B ran on both ranks at once: rates and device counters are summed
+    assert j["torrent_ranks"] == 2 and j["torrent_gpu_MBps"] > 0 and j["torrent_host_MBps"] > 0
 
 
 def test_bench_single_rank_defaults_are_valid(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
-                        "--warmup", "1", "--size-mb", "2"], env=env, capture_output=True,
+                        "--warmup", "1", "--size-mb", "2", "--torrent-gb", "0.2",
+                        "--torrent-pairs", "1"], env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
@@ -122,6 +126,14 @@ def test_bench_single_rank_defaults_are_valid(tmp_path):
     assert j["integrity"] == "none" and j["crc_relay_integrity"] == "crc32c"
     assert j["crc_relay_worker_cpu_s_per_GB"] > 0 and j["crc_relay_peer_cpu_s_per_GB"] > 0
     assert j["gpu_slots"] >= 1 and j["slot_budget_cpus"] >= 1
+    # CPU counted over the timed window only: worker + peer CPU fits in elapsed x the
+    # rank's CPUs (BENCH_r04 claimed 19.9 CPU-s per second on a 16-CPU slice)
+    assert 0 < j["cpu_utilisation"] <= 1.05 and 0 < j["crc_relay_cpu_utilisation"] <= 1.05
+    # the same-call torrent A/B (config 4's shape in miniature; no GPU here: both backends
+    # hash on the host, so the device counters stay 0 - on a GPU box gpu_parts > 0)
+    assert j["torrent_files"] == 50 and j["torrent_gpu_MBps"] > 0 and j["torrent_host_MBps"] > 0
+    assert j["torrent_gpu_hash_fails"] == 0 and j["torrent_host_hash_fails"] == 0
+    assert j["gpu_host_fallbacks"] == 0
 
 
 def test_supervisor_auto_pinning_quota_share():
@@ -144,7 +156,7 @@ def test_bench_four_ranks_disjoint_cpus_and_own_peers(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
            "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
            "--gpus", "4", "--steps", "2", "--warmup", "1", "--size-mb", "2", "--jobs-per-step", "2",
-           "--no-compare-single-put"]
+           "--no-compare-single-put", "--torrent-gb", "0"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
@@ -172,7 +184,7 @@ def test_bench_eight_ranks_as_the_driver_launches_them(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(REPO, "bench.py"),
            "--gpus", "8", "--steps", "2", "--warmup", "1", "--size-mb", "2", "--jobs-per-step", "2",
-           "--no-compare-single-put", "--no-compare-crc"]
+           "--no-compare-single-put", "--no-compare-crc", "--torrent-gb", "0"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -205,7 +217,7 @@ def test_bench_rank_with_two_worker_processes(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
                         "--warmup", "1", "--jobs-per-step", "3", "--size-mb", "4",
-                        "--procs-per-rank", "2"],
+                        "--procs-per-rank", "2", "--torrent-gb", "0"],
                        env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -229,7 +241,7 @@ def test_bench_multipart_objects_checked_against_the_origin(tmp_path, sink):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
                         "--warmup", "1", "--jobs-per-step", "2", "--size-mb", "12",
                         "--part-mb", "5", "--threshold-mb", "5", "--sink", sink,
-                        "--no-compare-single-put"],
+                        "--no-compare-single-put", "--torrent-gb", "0"],
                        env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])

@@ -556,7 +556,7 @@ def test_webseed_gpu_verify_path_through_batcher(run, tmp_path, origin_cls, monk
             origin.blobs["/seed/Pack/" + rel] = d
         # the first GET of a.mkv's head serves a corrupt byte -> hash fail -> refetch
         good = data["a.mkv"]
-        origin.blobs["/seed/Pack/a.mkv"] = b"\xff" + good[1:]
+        origin.blobs["/seed/Pack/a.mkv"] = bytes([good[0] ^ 0xFF]) + good[1:]
         c = TorrentClient(webseed_chunk=200_000, webseed_streams=3, verify_backend="gpu")
         await c.start()
         s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))
@@ -624,7 +624,9 @@ def test_webseed_serving_corrupt_data_fails_session(run, tmp_path, origin_cls):
         src = tmp_path / "ws"
         data = _tree(src / "Pack", {"a.mkv": 300_000})
         raw = make_torrent(str(src / "Pack"), 65536, url_list=[origin.url("/seed/")])
-        origin.blobs["/seed/Pack/a.mkv"] = data["a.mkv"][:70_000] + b"\x00" + data["a.mkv"][70_001:]
+        bad = bytearray(data["a.mkv"])
+        bad[70_000] ^= 0xFF                  # flip, never a no-op (writing a constant is 1/256)
+        origin.blobs["/seed/Pack/a.mkv"] = bytes(bad)
         c = TorrentClient(webseed_chunk=65536, webseed_streams=2, webseed_max_failures=2)
         await c.start()
         s = await c.add_torrent(parse_torrent(raw), str(tmp_path / "dl"))

@@ -630,6 +630,38 @@ def test_relay_budget_follows_the_memory_limit(monkeypatch):
     assert membudget.relay_budget_bytes(DownloadConfig()) == membudget.MIN_BUDGET
 
 
+def test_relay_budget_is_a_per_slot_share(monkeypatch):
+    """No STAGER_POOL_WORKERS (bench ranks, standalone workers on a shared 8-GPU node): the
+    divisor is GPU slots x worker processes per slot, as for the CPU budget."""
+    from downloader_amd.utils import membudget
+    from downloader_amd.utils.config import DownloadConfig
+    lim = 1536 << 30
+    monkeypatch.setattr(membudget, "memory_limit", lambda: lim)
+    monkeypatch.delenv("STAGER_POOL_WORKERS", raising=False)
+    monkeypatch.setenv("STAGER_GPU_SLOTS", "8")
+    monkeypatch.setenv("STAGER_PROCS_PER_SLOT", "2")
+    assert membudget.pool_workers() == 16
+    assert membudget.relay_budget_bytes(DownloadConfig()) == int(lim // 16 * 0.25)
+    monkeypatch.delenv("STAGER_PROCS_PER_SLOT")
+    assert membudget.pool_workers() == 8
+    monkeypatch.setenv("STAGER_POOL_WORKERS", "3")                 # explicit wins
+    assert membudget.pool_workers() == 3
+
+
+def test_supervisor_and_bench_children_declare_procs_per_slot(monkeypatch):
+    from downloader_amd.parallel.supervisor import Supervisor
+    monkeypatch.delenv("STAGER_PROCS_PER_SLOT", raising=False)
+    seen = {}
+
+    class P:
+        def __init__(self, argv, env, preexec_fn):
+            seen.update(env)
+    monkeypatch.setattr("subprocess.Popen", P)
+    s = Supervisor(2, ["true"], env={})
+    s._spawn(s.slots[0])
+    assert seen["STAGER_PROCS_PER_SLOT"] == "2" and "STAGER_POOL_WORKERS" not in seen
+
+
 def test_cgroup_memory_limit_v1_v2(tmp_path):
     from downloader_amd.utils.membudget import cgroup_memory_limit
     (tmp_path / "memory.max").write_text("max\n")
