@@ -50,6 +50,7 @@
 #include <vector>
 
 #include "gpu_part_api.h"
+#include "part_dispatch.h"
 
 namespace py = pybind11;
 
@@ -849,16 +850,20 @@ class GpuVerifier {
 // stream saw its copy-done markers wait for 77 ms kernels (round 3: 1 copy + 4 compute).
 // A HIP error marks the hasher broken: queued and later parts are refused or failed, and the
 // relay falls back to the host multi-buffer SHA-1.
-class PartHasher {
+// The scheduling state machine (queue, slots, streams, notify) is PartDispatcher in
+// part_dispatch.h, shared with the CPU fake device of selftest.cpp; this class is its HIP side.
+class HipPartDevice {
  public:
-  PartHasher(int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
-             int copy_streams = 2)
+  using Event = hipEvent_t;
+
+  HipPartDevice(int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
+                int copy_streams)
       : device_(device), slot_bytes_(slot_bytes), max_lanes_(max_lanes) {
     int n = 0;
     HIP_CHECK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) throw std::runtime_error("no such HIP device");
-    if (slots < 2 || slot_bytes < (1 << 20) || max_lanes < 64 ||
-        copy_streams < 1 || copy_streams > 4)
+    if (slots < 2 || slot_bytes < (1 << 20) || max_lanes < 64 || copy_streams < 1 ||
+        copy_streams > 4)
       throw std::invalid_argument("PartHasher: bad geometry");
     HIP_CHECK(hipSetDevice(device_));
     try {
@@ -867,37 +872,89 @@ class PartHasher {
       release();                       // a failed set-up leaves no HBM or streams behind
       throw;
     }
-    api_.abi = GPU_PART_API_ABI;
-    api_.ctx = this;
-    api_.reg = [](void* c, void* p, size_t n) { return ((PartHasher*)c)->reg(p, n); };
-    api_.unreg = [](void* c, void* p) { ((PartHasher*)c)->unreg(p); };
-    api_.submit = [](void* c, const uint8_t* d, int64_t len, int64_t pl) {
-      return ((PartHasher*)c)->submit(d, len, pl);
-    };
-    api_.wait = [](void* c, uint64_t t, int ph, uint8_t* out, size_t ol, char* err, size_t el) {
-      return ((PartHasher*)c)->wait(t, ph, out, ol, err, el);
-    };
-    api_.set_notify = [](void* c, gpu_part_notify_fn fn, void* arg) {
-      PartHasher* h = (PartHasher*)c;
-      std::lock_guard<std::mutex> g(h->mu_);
-      h->notify_ = fn;
-      h->notify_arg_ = arg;
-    };
-    thread_ = std::thread([this] { run(); });
-    pthread_setname_np(thread_.native_handle(), "gpu-part-disp");
+  }
+  ~HipPartDevice() { release(); }
+  HipPartDevice(const HipPartDevice&) = delete;
+  HipPartDevice& operator=(const HipPartDevice&) = delete;
+
+  static int hw_queues() {
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    const int n = e ? atoi(e) : 0;
+    return n > 0 ? n : 4;            // HIP's default
   }
 
-  ~PartHasher() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    if (thread_.joinable()) thread_.join();
-    release();
+  int copy_streams() const { return (int)copies_.size(); }
+  int compute_streams() const { return (int)streams_.size(); }
+  int slots() const { return (int)slots_.size(); }
+  void bind_thread() { HIP_CHECK(hipSetDevice(device_)); }
+  int64_t* lane_table(int s) { return slots_[(size_t)s].h_lane; }
+
+  Event copy(int s, int64_t off, const uint8_t* host, int64_t len, int cs) {
+    hipStream_t st = copies_[(size_t)cs];
+    HIP_CHECK(hipMemcpyAsync(slots_[(size_t)s].d_data + off, host, (size_t)len,
+                             hipMemcpyHostToDevice, st));
+    Event e = take_event();
+    HIP_CHECK(hipEventRecord(e, st));
+    return e;
+  }
+  bool copied(Event e) { return query(e); }
+  void recycle(Event e) {
+    if (e) free_events_.push_back(e);
+  }
+  // A slot's parts went over any of the copy streams: mark the end of what each has queued.
+  void close_copies(int s) {
+    Slot& sl = slots_[(size_t)s];
+    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipEventRecord(sl.copied[k], copies_[k]));
+  }
+  void launch(int s, int stream, int lanes, bool align16) {
+    Slot& sl = slots_[(size_t)s];
+    hipStream_t st = streams_[(size_t)stream];
+    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipStreamWaitEvent(st, sl.copied[k], 0));
+    HIP_CHECK(hipMemcpyAsync(sl.d_lane, sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
+                             hipMemcpyHostToDevice, st));
+    const int block = 64, grid = (lanes + block - 1) / block;
+    if (align16)
+      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, sl.d_data, sl.d_lane,
+                         sl.d_lane + max_lanes_, lanes, sl.d_dig);
+    else
+      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st, sl.d_data, sl.d_lane,
+                         sl.d_lane + max_lanes_, lanes, sl.d_dig);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(sl.h_dig, sl.d_dig, (size_t)lanes * 20, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(sl.done, st));
+  }
+  bool finished(int s) { return query(slots_[(size_t)s].done); }
+  const uint8_t* digests(int s) { return slots_[(size_t)s].h_dig; }
+  void drain_copies() noexcept {
+    for (auto c : copies_) hipStreamSynchronize(c);
+  }
+  int reg(void* p, size_t n) {
+    if (hipSetDevice(device_) != hipSuccess) return -1;
+    return hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess ? 0 : -1;
+  }
+  void unreg(void* p) {
+    hipSetDevice(device_);
+    hipHostUnregister(p);
   }
 
  private:
+  struct Slot {
+    uint8_t* d_data = nullptr;
+    int64_t* d_lane = nullptr;
+    uint8_t* d_dig = nullptr;
+    int64_t* h_lane = nullptr;   // [off x max_lanes][len x max_lanes]
+    uint8_t* h_dig = nullptr;
+    hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};   // one per copy stream
+    hipEvent_t done = nullptr;
+  };
+
+  static bool query(hipEvent_t e) {
+    hipError_t q = hipEventQuery(e);
+    if (q == hipErrorNotReady) return false;
+    HIP_CHECK(q);
+    return true;
+  }
+
   void create(int slots, int streams, int copy_streams) {
     // Parts are DMA'd round-robin over copy_streams streams: each is its own hardware queue,
     // so H2D copies of consecutive parts run on separate SDMA engines instead of queueing
@@ -911,10 +968,7 @@ class PartHasher {
     const int hwq = hw_queues();
     const int compute = streams > 0 ? std::min(streams, 4) : std::max(1, hwq - copy_streams);
     streams_.resize((size_t)compute);
-    for (auto& st : streams_) {
-      HIP_CHECK(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
-      st.slot = -1;
-    }
+    for (auto& st : streams_) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     slots_.resize((size_t)slots);
     for (auto& sl : slots_) {
       HIP_CHECK(hipMalloc((void**)&sl.d_data, (size_t)slot_bytes_));
@@ -933,10 +987,10 @@ class PartHasher {
     hipSetDevice(device_);
     for (auto c : copies_)
       if (c) hipStreamSynchronize(c);
-    for (auto& st : streams_)
-      if (st.s) {
-        hipStreamSynchronize(st.s);
-        hipStreamDestroy(st.s);
+    for (auto st : streams_)
+      if (st) {
+        hipStreamSynchronize(st);
+        hipStreamDestroy(st);
       }
     for (auto c : copies_)
       if (c) hipStreamDestroy(c);
@@ -957,141 +1011,6 @@ class PartHasher {
     free_events_.clear();
   }
 
- public:
-  const GpuPartHashApi* api() const { return &api_; }
-
-  static int hw_queues() {
-    const char* e = getenv("GPU_MAX_HW_QUEUES");
-    const int n = e ? atoi(e) : 0;
-    return n > 0 ? n : 4;            // HIP's default
-  }
-
-  int reg(void* p, size_t n) {
-    if (hipSetDevice(device_) != hipSuccess) return -1;
-    const auto t0 = std::chrono::steady_clock::now();
-    const bool ok = hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess;
-    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::lock_guard<std::mutex> g(mu_);
-    registered_++;
-    reg_seconds_ += dt;
-    return ok ? 0 : -1;
-  }
-  void unreg(void* p) {
-    hipSetDevice(device_);
-    hipHostUnregister(p);
-    std::lock_guard<std::mutex> g(mu_);
-    unregistered_++;
-  }
-
-  uint64_t submit(const uint8_t* data, int64_t len, int64_t piece_len) {
-    if (len <= 0 || piece_len <= 0) return 0;
-    const int64_t np = (len + piece_len - 1) / piece_len;
-    if (np > max_lanes_ || len > slot_bytes_) return 0;
-    std::lock_guard<std::mutex> g(mu_);
-    if (broken_ || stop_) return 0;
-    uint64_t t = ++seq_;
-    Job& j = jobs_[t];
-    j.host = data;
-    j.len = len;
-    j.piece_len = piece_len;
-    j.np = (int)np;
-    queue_.push_back(t);
-    submitted_++;
-    cv_.notify_all();
-    return t;
-  }
-
-  int wait(uint64_t t, int phase, uint8_t* out, size_t out_len, char* err, size_t errlen) {
-    std::unique_lock<std::mutex> lk(mu_);
-    auto it = jobs_.find(t);
-    if (it == jobs_.end()) return fail(err, errlen, "unknown ticket");
-    Job* j = &it->second;
-    wcv_.wait(lk, [&] { return !j->err.empty() || j->done || (phase == GPU_PART_COPIED && j->copied); });
-    if (!j->err.empty()) {
-      std::string e = j->err;
-      // nobody waits again for a failed copy (the relay hashes on the host), and once broken
-      // the dispatcher thread has exited: the job can go
-      if (phase == GPU_PART_DONE || j->done || broken_) jobs_.erase(t);   // by key: `it` may
-                                                                           // be stale after the wait
-      return fail(err, errlen, e.c_str());
-    }
-    if (phase == GPU_PART_DONE) {
-      if (out_len < j->digests.size()) return fail(err, errlen, "digest buffer too small");
-      memcpy(out, j->digests.data(), j->digests.size());
-      jobs_.erase(t);                // submit() may have rehashed jobs_ while this waited
-    }
-    return 0;
-  }
-
-  py::dict stats() {
-    std::lock_guard<std::mutex> g(mu_);
-    py::dict d;
-    d["submitted"] = submitted_;
-    d["launches"] = launches_;
-    d["lanes"] = lanes_total_;
-    d["max_batch_lanes"] = max_batch_lanes_;
-    d["broken"] = broken_;
-    d["pending"] = jobs_.size();
-    d["registered"] = registered_;       // part buffers page-locked (hipHostRegister)
-    d["unregistered"] = unregistered_;
-    d["register_s"] = reg_seconds_;
-    d["copy_streams"] = copies_.size();
-    d["compute_streams"] = streams_.size();
-    return d;
-  }
-
- private:
-  struct Job {
-    const uint8_t* host = nullptr;
-    int64_t len = 0, piece_len = 0;
-    int np = 0;
-    int slot = -1, lane0 = 0;
-    hipEvent_t copy_ev = nullptr;
-    bool copied = false, done = false;
-    std::string err, digests;
-  };
-  struct Slot {
-    uint8_t* d_data = nullptr;
-    int64_t* d_lane = nullptr;
-    uint8_t* d_dig = nullptr;
-    int64_t* h_lane = nullptr;   // [off x max_lanes][len x max_lanes]
-    uint8_t* h_dig = nullptr;
-    hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};   // one per copy stream
-    hipEvent_t done = nullptr;
-    int64_t used = 0;
-    int lanes = 0;
-    bool align16 = true;
-    std::vector<uint64_t> jobs;
-    int state = 0;               // 0 free, 1 filling, 2 closed (waiting for a stream), 3 running
-    std::chrono::steady_clock::time_point opened;
-  };
-  struct Stream {
-    hipStream_t s = nullptr;
-    int slot = -1;
-  };
-
-  static int fail(char* err, size_t errlen, const char* msg) {
-    if (err && errlen) {
-      strncpy(err, msg, errlen - 1);
-      err[errlen - 1] = 0;
-    }
-    return -1;
-  }
-
-  // Tell the relay module about finished phases: outside mu_ (the callback calls wait() and may
-  // unregister buffers), on this dispatcher thread.
-  void tell(const std::vector<uint64_t>& tickets, int phase) {
-    gpu_part_notify_fn fn;
-    void* arg;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      fn = notify_;
-      arg = notify_arg_;
-    }
-    if (fn)
-      for (uint64_t t : tickets) fn(arg, t, phase);
-  }
-
   hipEvent_t take_event() {
     if (!free_events_.empty()) {
       hipEvent_t e = free_events_.back();
@@ -1103,263 +1022,33 @@ class PartHasher {
     return e;
   }
 
-  // Everything below runs on the dispatcher thread; mu_ guards jobs_/queue_ and flags.
-  void run() {
-    try {
-      HIP_CHECK(hipSetDevice(device_));
-      int filling = -1;
-      std::deque<uint64_t> copying;            // tickets whose H2D is in flight, in order
-      for (;;) {
-        std::deque<uint64_t> fresh;
-        {
-          std::unique_lock<std::mutex> lk(mu_);
-          if (queue_.empty() && copying.empty() && !any_running() && !any_closed() &&
-              !(filling >= 0 && slots_[(size_t)filling].lanes > 0)) {
-            cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
-          }
-          if (stop_ && queue_.empty() && copying.empty() && !any_running() && !any_closed() &&
-              !(filling >= 0 && slots_[(size_t)filling].lanes > 0))
-            return;
-          fresh.swap(queue_);
-        }
-        bool progressed = false;
-        std::vector<uint64_t> copied_now, done_now, late_copied;
-        // 1. DMA new parts into the open slot (a new one when it is full)
-        while (!fresh.empty()) {
-          const uint64_t t = fresh.front();
-          Job* j;
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            j = &jobs_.at(t);
-          }
-          if (filling >= 0) {
-            Slot& f = slots_[(size_t)filling];
-            const int64_t off = (f.used + 255) & ~(int64_t)255;
-            if (off + j->len > slot_bytes_ || f.lanes + j->np > max_lanes_) {
-              f.state = 2;                    // full: closed, launched when a stream frees
-              close_copies(f);
-              filling = -1;
-            }
-          }
-          if (filling < 0) {
-            filling = free_slot();
-            if (filling < 0) break;            // every slot busy: the part waits queued
-            Slot& f = slots_[(size_t)filling];
-            f.state = 1;
-            f.used = 0;
-            f.lanes = 0;
-            f.align16 = true;
-            f.jobs.clear();
-            f.opened = std::chrono::steady_clock::now();
-          }
-          Slot& f = slots_[(size_t)filling];
-          const int64_t off = (f.used + 255) & ~(int64_t)255;
-          hipStream_t cs = copies_[next_copy_++ % copies_.size()];
-          HIP_CHECK(hipMemcpyAsync(f.d_data + off, j->host, (size_t)j->len, hipMemcpyHostToDevice,
-                                   cs));
-          j->copy_ev = take_event();
-          HIP_CHECK(hipEventRecord(j->copy_ev, cs));
-          j->slot = filling;
-          j->lane0 = f.lanes;
-          for (int k = 0; k < j->np; ++k) {
-            const int64_t po = (int64_t)k * j->piece_len;
-            f.h_lane[f.lanes + k] = off + po;
-            f.h_lane[max_lanes_ + f.lanes + k] = std::min(j->piece_len, j->len - po);
-          }
-          if (j->piece_len % 16) f.align16 = false;
-          f.lanes += j->np;
-          f.used = off + j->len;
-          f.jobs.push_back(t);
-          copying.push_back(t);
-          fresh.pop_front();
-          progressed = true;
-        }
-        const bool slot_bound = !fresh.empty();
-        if (slot_bound) {                       // no free slot: back to the head of the queue
-          std::lock_guard<std::mutex> g(mu_);
-          for (auto it = fresh.rbegin(); it != fresh.rend(); ++it) queue_.push_front(*it);
-        }
-        // 2. completed copies: the relay may reuse those buffers (copies on different
-        // streams finish out of order: every pending one is checked)
-        for (auto it = copying.begin(); it != copying.end();) {
-          Job* j;
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            j = &jobs_.at(*it);
-          }
-          hipError_t q = hipEventQuery(j->copy_ev);
-          if (q == hipErrorNotReady) {
-            ++it;
-            continue;
-          }
-          HIP_CHECK(q);
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            j->copied = true;
-            free_events_.push_back(j->copy_ev);
-            j->copy_ev = nullptr;
-          }
-          wcv_.notify_all();
-          copied_now.push_back(*it);
-          it = copying.erase(it);
-          progressed = true;
-        }
-        tell(copied_now, GPU_PART_COPIED);
-        // 3. finished kernels: publish digests, free slot and stream
-        for (auto& st : streams_) {
-          if (st.slot < 0) continue;
-          Slot& sl = slots_[(size_t)st.slot];
-          hipError_t q = hipEventQuery(sl.done);
-          if (q == hipErrorNotReady) continue;
-          HIP_CHECK(q);
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            for (uint64_t t : sl.jobs) {
-              Job& j = jobs_.at(t);
-              j.digests.assign((const char*)sl.h_dig + (size_t)j.lane0 * 20, (size_t)j.np * 20);
-              j.done = true;
-              if (!j.copied) {
-                // its copy ended after step 2 looked (the kernel waited for it): a DONE implies
-                // COPIED, and a job the relay may now erase must leave `copying`
-                j.copied = true;
-                free_events_.push_back(j.copy_ev);
-                j.copy_ev = nullptr;
-                late_copied.push_back(t);
-              }
-              done_now.push_back(t);
-            }
-          }
-          wcv_.notify_all();
-          sl.state = 0;
-          sl.jobs.clear();
-          st.slot = -1;
-          progressed = true;
-        }
-        if (!late_copied.empty()) {
-          for (uint64_t t : late_copied) {
-            auto c = std::find(copying.begin(), copying.end(), t);
-            if (c != copying.end()) copying.erase(c);
-          }
-          tell(late_copied, GPU_PART_COPIED);
-        }
-        // 4. launch: closed slots first (oldest first), then the open one, on idle streams
-        for (auto& st : streams_) {
-          if (st.slot >= 0) continue;
-          int pick = oldest(2);
-          if (pick < 0 && filling >= 0 && slots_[(size_t)filling].lanes > 0) {
-            pick = filling;
-            close_copies(slots_[(size_t)pick]);
-            filling = -1;
-          }
-          if (pick < 0) break;
-          launch(pick, st);
-          progressed = true;
-        }
-        tell(done_now, GPU_PART_DONE);
-        if (!progressed) {
-          // nothing moved: poll the device's events again after a short sleep. New parts
-          // only end the sleep early when there is a slot to put them in - with every slot
-          // busy the predicate would be true at once and the thread would spin on mu_ and
-          // hipEventQuery against submit() / wait().
-          std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait_for(lk, std::chrono::microseconds(200),
-                       [&] { return stop_ || (!slot_bound && !queue_.empty()); });
-        }
-      }
-    } catch (const std::exception& e) {
-      // DMAs already queued on the copy streams may still read part buffers: let them end
-      // before any waiter learns of the failure and hands its buffer back to the pool (which
-      // may unmap it)
-      for (auto c : copies_) hipStreamSynchronize(c);
-      std::vector<uint64_t> failed_copy, failed_hash;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        broken_ = true;
-        for (auto& kv : jobs_)
-          if (!kv.second.done) {
-            kv.second.err = std::string("GPU part hasher: ") + e.what();
-            (kv.second.copied ? failed_hash : failed_copy).push_back(kv.first);
-          }
-        queue_.clear();
-        wcv_.notify_all();
-      }
-      tell(failed_copy, GPU_PART_COPIED);
-      tell(failed_hash, GPU_PART_DONE);
-    }
-  }
-
-  bool any_running() const {
-    for (auto& st : streams_)
-      if (st.slot >= 0) return true;
-    return false;
-  }
-  bool any_closed() const {
-    for (auto& sl : slots_)
-      if (sl.state == 2) return true;
-    return false;
-  }
-  int free_slot() const {
-    for (size_t i = 0; i < slots_.size(); ++i)
-      if (slots_[i].state == 0) return (int)i;
-    return -1;
-  }
-  int oldest(int state) const {
-    int best = -1;
-    for (size_t i = 0; i < slots_.size(); ++i)
-      if (slots_[i].state == state && (best < 0 || slots_[i].opened < slots_[(size_t)best].opened))
-        best = (int)i;
-    return best;
-  }
-
-  // A slot's parts went over any of the copy streams: mark the end of what each has queued.
-  void close_copies(Slot& sl) {
-    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipEventRecord(sl.copied[k], copies_[k]));
-  }
-
-  void launch(int si, Stream& st) {
-    Slot& sl = slots_[(size_t)si];
-    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipStreamWaitEvent(st.s, sl.copied[k], 0));
-    HIP_CHECK(hipMemcpyAsync(sl.d_lane, sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
-                             hipMemcpyHostToDevice, st.s));
-    const int block = 64, grid = (sl.lanes + block - 1) / block;
-    if (sl.align16)
-      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st.s, sl.d_data, sl.d_lane,
-                         sl.d_lane + max_lanes_, sl.lanes, sl.d_dig);
-    else
-      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st.s, sl.d_data, sl.d_lane,
-                         sl.d_lane + max_lanes_, sl.lanes, sl.d_dig);
-    HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMemcpyAsync(sl.h_dig, sl.d_dig, (size_t)sl.lanes * 20, hipMemcpyDeviceToHost, st.s));
-    HIP_CHECK(hipEventRecord(sl.done, st.s));
-    sl.state = 3;
-    st.slot = si;
-    std::lock_guard<std::mutex> g(mu_);
-    launches_++;
-    lanes_total_ += (uint64_t)sl.lanes;
-    max_batch_lanes_ = std::max<uint64_t>(max_batch_lanes_, (uint64_t)sl.lanes);
-  }
-
   int device_;
   int64_t slot_bytes_;
   int max_lanes_;
   std::vector<hipStream_t> copies_;
-  size_t next_copy_ = 0;
-  std::vector<Stream> streams_;
+  std::vector<hipStream_t> streams_;
   std::vector<Slot> slots_;
-  std::vector<hipEvent_t> free_events_;
-  std::mutex mu_;
-  std::condition_variable cv_, wcv_;
-  std::deque<uint64_t> queue_;
-  std::unordered_map<uint64_t, Job> jobs_;
-  uint64_t seq_ = 0, submitted_ = 0, launches_ = 0, lanes_total_ = 0, max_batch_lanes_ = 0;
-  bool stop_ = false, broken_ = false;
-  uint64_t registered_ = 0, unregistered_ = 0;
-  double reg_seconds_ = 0;
-  GpuPartHashApi api_{};
-  gpu_part_notify_fn notify_ = nullptr;
-  void* notify_arg_ = nullptr;
-  std::thread thread_;
+  std::vector<hipEvent_t> free_events_;   // dispatcher thread only
 };
+
+using PartHasher = stager::PartDispatcher<HipPartDevice>;
+
+py::dict part_stats(PartHasher& h) {
+  const stager::PartDispatchStats s = h.stats();
+  py::dict d;
+  d["submitted"] = s.submitted;
+  d["launches"] = s.launches;
+  d["lanes"] = s.lanes;
+  d["max_batch_lanes"] = s.max_batch_lanes;
+  d["broken"] = s.broken;
+  d["pending"] = s.pending;
+  d["registered"] = s.registered;       // part buffers page-locked (hipHostRegister)
+  d["unregistered"] = s.unregistered;
+  d["register_s"] = s.register_s;
+  d["copy_streams"] = s.copy_streams;
+  d["compute_streams"] = s.compute_streams;
+  return d;
+}
 
 int device_count() {
   int n = 0;
@@ -1474,7 +1163,8 @@ PYBIND11_MODULE(_gpuhash, m) {
       .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
                        int copy_streams) {
              py::gil_scoped_release rel;
-             return new PartHasher(device, slot_bytes, slots, streams, max_lanes, copy_streams);
+             return new PartHasher(slot_bytes, max_lanes, device, slot_bytes, slots, streams,
+                                   max_lanes, copy_streams);
            }),
            py::arg("device") = 0, py::arg("slot_bytes") = (int64_t)1 << 30, py::arg("slots") = 8,
            py::arg("streams") = 0, py::arg("max_lanes") = 16384, py::arg("copy_streams") = 2)
@@ -1508,5 +1198,5 @@ PYBIND11_MODULE(_gpuhash, m) {
             return py::bytes(out);
           },
           py::arg("data"), py::arg("piece_len"))
-      .def("stats", &PartHasher::stats);
+      .def("stats", &part_stats);
 }

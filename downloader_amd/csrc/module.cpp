@@ -217,6 +217,57 @@ PYBIND11_MODULE(_native, m) {
         "Restart the pool's high-water mark (peak_bytes) and its over_budget count");
   m.def("relay_pool_set_max_idle", &relay_pool_set_max_idle, py::arg("n"),
         "Keep at most n idle part buffers (the rest are unmapped on release)");
+  py::class_<SwarmWire>(m, "SwarmWire",
+                        "Native peer-wire receive path of one torrent session (peerwire.cpp)")
+      .def(py::init<int>(), py::arg("verify_threads") = 2)
+      .def("set_storage",
+           [](SwarmWire& w, int64_t piece_length, int64_t total, const py::bytes& hashes,
+              const std::vector<std::pair<int, int64_t>>& files) {
+             w.set_storage(piece_length, total, std::string(hashes), files);
+           },
+           py::arg("piece_length"), py::arg("total"), py::arg("hashes"), py::arg("files"))
+      .def("begin_piece", &SwarmWire::begin_piece, py::arg("idx"))
+      .def("drop_piece", &SwarmWire::drop_piece, py::arg("idx"))
+      .def("attach",
+           [](SwarmWire& w, int fd, uint64_t id, const py::bytes& prefix) {
+             w.attach(fd, id, std::string(prefix));
+           },
+           py::arg("fd"), py::arg("conn_id"), py::arg("prefix") = py::bytes(),
+           "Hand a connected socket over (the fd is owned from here on, closed by detach)")
+      .def("send",
+           [](SwarmWire& w, uint64_t id, const py::bytes& data) {
+             std::string s(data);
+             return w.send(id, std::move(s));
+           },
+           py::arg("conn_id"), py::arg("data"))
+      .def("pending_out", &SwarmWire::pending_out, py::arg("conn_id"))
+      .def("detach", &SwarmWire::detach, py::arg("conn_id"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("eventfd", &SwarmWire::eventfd)
+      .def("poll",
+           [](SwarmWire& w) {
+             std::vector<WireEvent> ev = w.poll();
+             py::list out;
+             for (auto& e : ev) out.append(py::make_tuple(e.conn, e.kind, py::bytes(e.data)));
+             return out;
+           },
+           "[(conn_id, kind, data)]: 1 message, 2 blocks, 3 closed, 4 piece (conn 0)")
+      .def("stats",
+           [](SwarmWire& w) {
+             SwarmWireStats s = w.stats();
+             py::dict d;
+             d["begun"] = s.begun;
+             d["blocks"] = s.blocks;
+             d["block_bytes"] = s.block_bytes;
+             d["blocks_ignored"] = s.blocks_ignored;
+             d["verified"] = s.verified;
+             d["hash_fails"] = s.hash_fails;
+             d["rx_bytes"] = s.rx_bytes;
+             d["recvs"] = s.recvs;
+             d["active_pieces"] = s.active_pieces;
+             return d;
+           })
+      .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());
   m.def("relay_counters", []() {
     RelayCounters c = relay_counters();
     py::dict d;

@@ -2,9 +2,14 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -161,6 +166,8 @@ struct GpuPartStats {
 };
 GpuPartStats gpu_part_stats();
 // Blocks until part `id` is hashed; its digests (throws when the device failed after the DMA).
+// A part is consumed once: by gpu_part_wait (which claims it - gpu_part_poll then skips it)
+// or by gpu_part_poll (a wait called after the poll collected it throws "already collected").
 std::string gpu_part_wait(uint64_t id);
 // A part nobody will ask for (the relay failed after queueing it): blocks until its buffer is
 // back in the pool, then drops its result when it arrives.
@@ -188,6 +195,76 @@ class CpuPartHasher {
   struct Impl;
   std::unique_ptr<Impl> impl_;
 };
+// ---- peerwire.cpp: native BitTorrent peer-wire receive path ---------------------------
+// One per torrent session. Connections are handed over after the handshake (attach: the fd is
+// owned from then on); a reader thread per connection frames messages, copies PIECE payloads
+// into the piece being assembled (begin_piece), and queues every other message for Python; a
+// writer thread sends what Python queues. Complete pieces are SHA-1'd 16 at a time (sha1_mb),
+// written to the storage files (set_storage: the torrent's (fd, length) list in order) and
+// reported. Events (poll(), signalled on eventfd()): kEvMsg = one message (id byte +
+// payload), kEvBlocks = 16-byte records (piece, begin, length, status: 0 not taken, 1 taken, 2
+// taken and the piece is complete) in wire order, coalesced while not polled, kEvClosed =
+// reason; kEvPiece (conn 0) = piece index + status byte (1 verified and written, 0 hash
+// mismatch, 2 write error + message).
+struct WireEvent {
+  uint64_t conn;
+  int kind;
+  std::string data;
+};
+struct SwarmWireStats {
+  uint64_t begun = 0, blocks = 0, block_bytes = 0, blocks_ignored = 0, verified = 0,
+           hash_fails = 0, rx_bytes = 0, recvs = 0;
+  size_t active_pieces = 0;
+};
+class SwarmWire {
+ public:
+  static constexpr int kEvMsg = 1, kEvBlocks = 2, kEvClosed = 3, kEvPiece = 4;
+  explicit SwarmWire(int verify_threads = 2);
+  ~SwarmWire();
+  void set_storage(int64_t piece_length, int64_t total, const std::string& hashes,
+                   const std::vector<std::pair<int, int64_t>>& files);
+  void begin_piece(uint32_t idx);
+  void drop_piece(uint32_t idx);
+  void attach(int fd, uint64_t id, const std::string& prefix);
+  size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
+  size_t pending_out(uint64_t id);
+  void detach(uint64_t id);                     // shut down, join, close the fd
+  int eventfd() const { return efd_; }
+  std::vector<WireEvent> poll();
+  SwarmWireStats stats();
+  void close();                                 // every connection, then the verifiers
+  int take_block(uint32_t idx, uint32_t begin, const uint8_t* p, uint32_t len);
+
+ private:
+  struct Piece;
+  struct Conn;
+  uint32_t piece_size(uint32_t idx) const;
+  void verify_loop();
+  std::string write_piece(const Piece& p);
+  void push(uint64_t conn, int kind, std::string data);
+  void read_loop(Conn& c);
+  void write_loop(Conn& c);
+
+  std::mutex mu_;                               // pieces_, geometry, stats_
+  int64_t piece_length_ = 0, total_ = 0;
+  std::string hashes_;
+  std::vector<std::pair<int, int64_t>> files_;
+  std::unordered_map<uint32_t, std::shared_ptr<Piece>> pieces_;
+  uint64_t epoch_ = 0;
+  SwarmWireStats stats_;
+  std::atomic<uint64_t> rx_bytes_{0}, recvs_{0};
+  std::mutex cmu_;
+  std::unordered_map<uint64_t, std::shared_ptr<Conn>> conns_;
+  std::mutex vmu_;
+  std::condition_variable vcv_;
+  std::deque<std::shared_ptr<Piece>> vq_;
+  bool vstop_ = false;
+  std::vector<std::thread> verifiers_;
+  std::mutex emu_;
+  std::deque<WireEvent> events_;
+  int efd_ = -1;
+};
+
 // Idle part buffers beyond `keep_bytes` are unmapped (returns the bytes freed); max_idle
 // bounds the idle list. A budget (bytes, 0 = none) bounds leased + idle buffers: idle ones are
 // unmapped first to make room for a new lease; a lease past the budget is counted

@@ -10,6 +10,11 @@
 // in-process loopback servers: Content-Length body spliced to a file, chunked body, a
 // sendfile request body, the socket->socket relay, the hashed relay, and the same transfers
 // over TLS (throwaway in-memory certificate; handshake, verification failure, TLS relay).
+// Then the GPU part hasher's completion machinery end to end on a CPU: PartDispatcher
+// (part_dispatch.h, the state machine gfx950's PartHasher runs) over a fake device of host
+// threads, behind the relay module's part ids / notify / wait / forget / poll, with 64 relays
+// at once, hashers replaced mid-flight, the part budget oscillating and injected device faults.
+// A run that would hang (a part nobody is told about) is ended by a watchdog and fails.
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -23,10 +28,17 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 
+#include <poll.h>
+
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <random>
 #include <string>
 #include <atomic>
@@ -34,6 +46,8 @@
 #include <vector>
 
 #include "native.h"
+#include "part_dispatch.h"
+#include "part_fake_device.h"
 
 using namespace stager;
 
@@ -224,8 +238,310 @@ struct TlsServerConn {
   }
 };
 
+// Keep-alive loopback peer for the part-hashing stress: on one connection, answers
+// `GET /p?off=O&len=N` with data[O, O + N) and drains PUT bodies (200, empty body), until the
+// client closes.
+struct KeepAlivePeer {
+  int ls = -1, port = 0;
+  std::thread th;
+  explicit KeepAlivePeer(const std::vector<uint8_t>& data) {
+    ls = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    bind(ls, (sockaddr*)&a, sizeof a);
+    listen(ls, 4);
+    socklen_t sl = sizeof a;
+    getsockname(ls, (sockaddr*)&a, &sl);
+    port = ntohs(a.sin_port);
+    th = std::thread([this, &data] {
+      int c = accept(ls, nullptr, nullptr);
+      if (c < 0) return;
+      for (;;) {
+        std::string h = read_head(c);
+        if (h.empty()) break;
+        long long off = 0, len = 0;
+        if (h.compare(0, 4, "GET ") == 0 &&
+            sscanf(h.c_str(), "GET /p?off=%lld&len=%lld", &off, &len) == 2) {
+          send_str(c, "HTTP/1.1 200 OK\r\nContent-Length: " + std::to_string(len) + "\r\n\r\n");
+          send_str(c, std::string((const char*)data.data() + off, (size_t)len));
+        } else {
+          const char* cl = strcasestr(h.c_str(), "content-length:");
+          drain_body(c, cl ? atoll(cl + 15) : 0);
+          send_str(c, "HTTP/1.1 200 OK\r\nContent-Length: 0\r\n\r\n");
+        }
+      }
+      close(c);
+    });
+  }
+  ~KeepAlivePeer() {
+    th.join();
+    close(ls);
+  }
+};
+
+using FakeHasher = PartDispatcher<FakePartDevice>;
+
+static std::unique_ptr<FakeHasher> fake_hasher(FakeDeviceKnobs k) {
+  const int64_t slot_bytes = 4 << 20;
+  const int max_lanes = 256;
+  return std::unique_ptr<FakeHasher>(
+      new FakeHasher(slot_bytes, max_lanes, slot_bytes, /*slots*/ 4, /*compute*/ 2, /*copy*/ 2,
+                     max_lanes, k));
+}
+
+// Ends the process (failing) if a section does not finish in time: a part whose phase nobody
+// reports leaves its waiter blocked for good, which is exactly what must be caught.
+// Where each stress relay thread is (for the watchdog's report): phase and part id.
+static std::atomic<int> g_stress_phase[64];
+static std::atomic<uint64_t> g_stress_id[64];
+
+struct Watchdog {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  std::thread th;
+  Watchdog(const char* what, int seconds) {
+    th = std::thread([this, what, seconds] {
+      std::unique_lock<std::mutex> lk(mu);
+      // system_clock: see the wait in part_dispatch.h (steady waits are invisible to TSan)
+      if (!cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::seconds(seconds),
+                         [&] { return done; })) {
+        fprintf(stderr, "selftest: %s did not finish in %d s (a part was never reported)\n",
+                what, seconds);
+        static const char* names[] = {"idle", "relay", "forget", "wait", "poll", "done"};
+        for (int i = 0; i < 64; ++i)
+          if (g_stress_phase[i].load() != 0 && g_stress_phase[i].load() != 5)
+            fprintf(stderr, "  relay %d: %s, part %llu\n", i, names[g_stress_phase[i].load()],
+                    (unsigned long long)g_stress_id[i].load());
+        GpuPartStats st = gpu_part_stats();
+        fprintf(stderr, "  parts: %llu submitted, %llu pending\n",
+                (unsigned long long)st.submitted, (unsigned long long)st.pending);
+        _exit(3);
+      }
+    });
+  }
+  ~Watchdog() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      done = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+};
+
+struct PartStress {
+  int threads = 64, parts = 32;          // relays at once x parts each
+  int64_t piece = 16 << 10;
+  int pieces = 8;                        // the relay module hands parts of >= 8 pieces over
+  int replace_every_ms = 5;              // a fresh hasher installed while tickets are pending
+  FakeDeviceKnobs knobs;
+  FakeDeviceKnobs first;                 // the knobs of the first hasher (a faulty one)
+  bool oscillate_budget = true;
+};
+
+struct PartStressResult {
+  int good = 0, failed = 0, forgotten = 0, polled = 0, hashers = 0;
+  bool digests_ok = true;
+};
+
+// 64 relays (one keep-alive origin + S3 peer pair each) stage parts through the hashed relay;
+// each part is then waited for (gpu_part_wait), left to a poller thread (gpu_part_poll on the
+// eventfd) or forgotten as if its job was cancelled (gpu_part_forget), a third each.
+static PartStressResult part_stress(const PartStress& cfg) {
+  PartStressResult res;
+  const int64_t part = cfg.piece * cfg.pieces;
+  auto data = rnd(8 << 20, 77);
+  std::vector<std::unique_ptr<FakeHasher>> hashers;
+  std::mutex hmu;
+  hashers.push_back(fake_hasher(cfg.first));
+  set_gpu_part_hasher(hashers.back()->api(), cfg.pieces);
+  std::atomic<bool> stop{false};
+  // the poller: what the asyncio side does (eventfd readable -> gpu_part_poll)
+  std::mutex pmu;
+  std::condition_variable pcv;
+  std::map<uint64_t, std::pair<bool, std::string>> polled;   // id -> (ok, digests / error)
+  std::thread poller([&] {
+    pollfd pf{gpu_part_eventfd(), POLLIN, 0};
+    while (!stop.load()) {
+      poll(&pf, 1, 5);
+      for (auto& ev : gpu_part_poll()) {
+        if (ev.kind == 1) continue;
+        std::lock_guard<std::mutex> g(pmu);
+        polled[ev.id] = {ev.kind == 2, ev.data};
+        pcv.notify_all();
+      }
+    }
+  });
+  std::thread replacer([&] {
+    uint32_t seed = 100;
+    for (int n = 0; n < 200 && !stop.load(); ++n) {   // bounded: a hang must not eat memory
+      std::this_thread::sleep_for(std::chrono::milliseconds(cfg.replace_every_ms));
+      FakeDeviceKnobs k = cfg.knobs;
+      k.seed = ++seed;
+      auto h = fake_hasher(k);
+      set_gpu_part_hasher(h->api(), cfg.pieces);   // the old one keeps serving its tickets
+      std::lock_guard<std::mutex> g(hmu);
+      hashers.push_back(std::move(h));
+    }
+  });
+  std::thread budget([&] {
+    std::mt19937 g(5);
+    while (!stop.load() && cfg.oscillate_budget) {
+      relay_pool_set_budget((size_t)(1 + g() % 16) << 20);
+      std::this_thread::sleep_for(std::chrono::microseconds(500));
+    }
+  });
+  std::atomic<int> good{0}, failed{0}, forgotten{0}, by_poll{0};
+  std::atomic<bool> digests_ok{true};
+  std::vector<std::thread> ths;
+  for (int t = 0; t < cfg.threads; ++t) {
+    ths.emplace_back([&, t] {
+      g_stress_phase[t] = 1;
+      KeepAlivePeer origin(data), sink(data);
+      std::mt19937 g(1000 + t);
+      try {
+        HttpConn src("127.0.0.1", origin.port, 30, 30), dst("127.0.0.1", sink.port, 30, 30);
+        for (int i = 0; i < cfg.parts; ++i) {
+          const int64_t off = (int64_t)(g() % (uint32_t)(data.size() - part)) & ~(int64_t)63;
+          g_stress_phase[t] = 1;
+          src.send_request("GET /p?off=" + std::to_string(off) + "&len=" + std::to_string(part) +
+                               " HTTP/1.1\r\nHost: x\r\n\r\n", nullptr, 0);
+          ResponseHead gh = src.read_head();
+          dst.send_raw("PUT /s HTTP/1.1\r\nHost: x\r\nContent-Length: " + std::to_string(part) +
+                       "\r\n\r\n");
+          std::string digests, head, tail;
+          uint64_t id = 0;
+          src.relay_body_hashed(dst, gh.content_length, 0, part, cfg.piece, nullptr, &digests,
+                                &head, &tail, nullptr, &id);
+          ResponseHead ph = dst.read_head();
+          dst.read_body(ph, 16);
+          const std::string want =
+              hash_pieces("sha1", data.data() + off, (size_t)part, (size_t)cfg.piece, 1);
+          const int mode = (int)(g() % 3);
+          g_stress_id[t] = id;
+          if (id && mode == 0) {                       // cancelled job: nobody asks
+            g_stress_phase[t] = 2;
+            gpu_part_forget(id);
+            forgotten++;
+            continue;
+          }
+          std::string got = digests;
+          bool err = false;
+          auto from_poll = [&] {
+            g_stress_phase[t] = 4;
+            std::unique_lock<std::mutex> lk(pmu);
+            if (!pcv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::seconds(60),
+                                [&] { return polled.count(id) > 0; })) {
+              fprintf(stderr, "part stress: part %llu never reported\n", (unsigned long long)id);
+              err = true;
+              return;
+            }
+            err = !polled[id].first;
+            got = polled[id].second;
+            polled.erase(id);
+            by_poll++;
+          };
+          if (id && mode == 1) {
+            try {
+              g_stress_phase[t] = 3;
+              got = gpu_part_wait(id);
+            } catch (const std::exception& e) {
+              // the poller collected it first (before this wait claimed it / while it waited)
+              if (strstr(e.what(), "already collected") || strstr(e.what(), "unknown part"))
+                from_poll();
+              else
+                err = true;
+            }
+          } else if (id) {
+            from_poll();
+          }
+          if (err && getenv("SELFTEST_VERBOSE")) fprintf(stderr, "failed: %s\n", got.c_str());
+          if (err) {
+            failed++;
+          } else if (got == want) {
+            good++;
+          } else {
+            digests_ok = false;
+          }
+        }
+      } catch (const std::exception& e) {
+        fprintf(stderr, "part stress relay %d: %s\n", t, e.what());
+        digests_ok = false;
+      }
+      g_stress_phase[t] = 5;
+    });
+  }
+  for (auto& th : ths) th.join();
+  stop = true;
+  replacer.join();
+  budget.join();
+  poller.join();
+  relay_pool_set_budget(0);
+  set_gpu_part_hasher(nullptr, 0);
+  res.hashers = (int)hashers.size();
+  hashers.clear();                 // each drains what it still holds before its thread ends
+  res.good = good;
+  res.failed = failed;
+  res.forgotten = forgotten;
+  res.polled = by_poll;
+  res.digests_ok = digests_ok;
+  return res;
+}
+
+static void stress_sections() {
+  // ---- the completion machinery under load: 64 relays x 32 parts (2,048) through
+  // PartDispatcher<FakePartDevice>, copies that complete before they are seen, hashers
+  // replaced every few ms, the part budget oscillating, a third of the parts forgotten
+  {
+    Watchdog wd("part stress", 90);
+    PartStress cfg;
+    GpuPartStats before = gpu_part_stats();
+    PartStressResult r = part_stress(cfg);
+    GpuPartStats after = gpu_part_stats();
+    fprintf(stderr, "part stress: %d good, %d forgotten, %d via poll, %d failed, %d hashers\n",
+            r.good, r.forgotten, r.polled, r.failed, r.hashers);
+    CHECK(r.digests_ok && r.failed == 0);
+    CHECK(r.good + r.forgotten == cfg.threads * cfg.parts);
+    CHECK(r.forgotten > 0 && r.hashers > 2);
+    // every part went to a hasher, or was hashed on the host because its pooled buffer was
+    // page-locked for a hasher replaced meanwhile (refused)
+    CHECK(after.submitted - before.submitted + after.refused - before.refused ==
+          (uint64_t)(cfg.threads * cfg.parts));
+    CHECK(after.submitted - before.submitted > (uint64_t)(cfg.threads * cfg.parts) / 2);
+    CHECK(after.pending == 0);     // every part collected, or forgotten and dropped
+  }
+  // ---- device faults: every hasher fails at its 3rd / 4th launch (parts it had finished in
+  // the same pass must still be reported) or at its 400th event query
+  {
+    Watchdog wd("part stress with device faults", 90);
+    PartStress cfg;
+    cfg.threads = 16;
+    cfg.parts = 24;
+    cfg.replace_every_ms = 20;
+    cfg.first.fail_launch_at = 3;
+    cfg.knobs.fail_launch_at = 4;      // every replacement fails too, at its 4th launch
+    cfg.knobs.fail_query_at = 400;
+    GpuPartStats before = gpu_part_stats();
+    PartStressResult r = part_stress(cfg);
+    GpuPartStats after = gpu_part_stats();
+    fprintf(stderr, "part stress (faults): %d good, %d forgotten, %d failed, %d host fallbacks\n",
+            r.good, r.forgotten, r.failed, (int)(after.host_fallbacks - before.host_fallbacks));
+    CHECK(r.digests_ok);
+    CHECK(r.good + r.forgotten + r.failed == cfg.threads * cfg.parts);
+    CHECK(r.failed + (int)(after.host_fallbacks - before.host_fallbacks) > 0);
+    CHECK(after.pending == 0);
+  }
+}
+
 int main() {
-  signal(SIGPIPE, SIG_IGN);  // SSL_write on a reset socket (Python does the same at start)
+  signal(SIGPIPE, SIG_IGN);
+  if (getenv("SELFTEST_ONLY") && strcmp(getenv("SELFTEST_ONLY"), "stress") == 0) {
+    stress_sections();                 // the part-hasher sections alone (quick iteration)
+    printf(g_fail ? "selftest: failures\n" : "selftest ok\n");
+    return g_fail ? 1 : 0;
+  }  // SSL_write on a reset socket (Python does the same at start)
   // ---- digests
   const uint8_t* abc = (const uint8_t*)"abc";
   CHECK(hex(digest("sha1", abc, 3)) == "a9993e364706816aba3e25717850c26c9cd0d89d");
@@ -572,6 +888,7 @@ int main() {
     CHECK(good.load() + failed.load() == 6 && good.load() >= 3 && failed.load() >= 1);
     set_gpu_part_hasher(nullptr, 0);
   }
+  stress_sections();
   {
     RelayPoolStats st = relay_pool_stats();
     CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);

@@ -1454,6 +1454,7 @@ struct GpuPending {
   int64_t skip = 0, full_len = 0, piece_len = 0;
   bool copied = false, finished = false, failed = false;
   bool forgotten = false, copied_reported = false;
+  bool waited = false;               // claimed by gpu_part_wait: gpu_part_poll leaves it alone
   std::string result;                // digests, or the error
 };
 std::mutex g_gpu_mu;
@@ -1523,11 +1524,12 @@ void gpu_copied(const GpuPartHashApi* a, uint64_t ticket, uint64_t id) {
     g_gpu_ids.erase({a, ticket});
   }
   if (p.forgotten && p.finished)
-    g_gpu_parts.erase(it);
+    g_gpu_parts.erase(it);          // (a failed copy finishes the part at once)
   else if (!p.forgotten)
     gpu_signal(id);
-  else
-    g_gpu_cv.notify_all();
+  // a gpu_part_forget blocked on this part wakes on any change, the erase included (the
+  // selftest's fault section hung here when a forgotten part's copy failed)
+  g_gpu_cv.notify_all();
 }
 
 void gpu_done(const GpuPartHashApi* a, uint64_t ticket, uint64_t id) {
@@ -1550,10 +1552,12 @@ void gpu_done(const GpuPartHashApi* a, uint64_t ticket, uint64_t id) {
   p.finished = true;
   p.failed = rc != 0;
   p.result = rc ? std::string("GPU piece hashing failed: ") + err : out;
-  if (p.forgotten)
+  if (p.forgotten) {
     g_gpu_parts.erase(it);
-  else
+    g_gpu_cv.notify_all();
+  } else {
     gpu_signal(id);
+  }
 }
 
 // gpu_notify_fn: called on the hasher's thread without its lock held.
@@ -1757,7 +1761,9 @@ GpuPartStats gpu_part_stats() {
 // lock is released, so every wake looks the part up again.
 std::string gpu_part_wait(uint64_t id) {
   std::unique_lock<std::mutex> lk(g_gpu_mu);
-  if (g_gpu_parts.find(id) == g_gpu_parts.end()) throw IoError("gpu_part_wait: unknown part");
+  auto w = g_gpu_parts.find(id);
+  if (w == g_gpu_parts.end()) throw IoError("gpu_part_wait: unknown part");
+  w->second.waited = true;           // from here on gpu_part_poll does not collect it
   g_gpu_cv.wait(lk, [&] {
     auto f = g_gpu_parts.find(id);
     return f == g_gpu_parts.end() || f->second.finished;
@@ -1796,7 +1802,7 @@ std::vector<GpuPartEvent> gpu_part_poll() {
     const uint64_t id = g_gpu_news.front();
     g_gpu_news.pop_front();
     auto it = g_gpu_parts.find(id);
-    if (it == g_gpu_parts.end() || it->second.forgotten) continue;
+    if (it == g_gpu_parts.end() || it->second.forgotten || it->second.waited) continue;
     GpuPending& p = it->second;
     if (p.copied && !p.copied_reported) {
       p.copied_reported = true;

@@ -540,7 +540,7 @@ class NativeTransport(Transport):
             except asyncio.CancelledError:
                 self._abort_slot(slot)
                 await _drain(fut)
-                self._forget_ticket(fut)
+                await self._forget_ticket(fut)
                 raise
             finally:
                 self._end_slot(slot)
@@ -558,17 +558,39 @@ class NativeTransport(Transport):
             src_url = nxt
         raise TransportError(f"relay source: more than {MAX_REDIRECTS} redirects", 310)
 
-    def _forget_ticket(self, fut: "asyncio.Future") -> None:
+    async def _forget_ticket(self, fut: "asyncio.Future") -> None:
         """A cancelled relay that had queued its part to the GPU hasher: nobody will ask for
         the digests; the native side returns the part's buffer to the pool when its DMA is
-        over and drops the result (``gpu_part_forget`` blocks until the DMA is, so it runs on
-        a thread of its own)."""
+        over and drops the result. ``gpu_part_forget`` blocks until the DMA is (milliseconds),
+        so it runs on a thread of its own - and this waits for it: the caller gives the part's
+        bytes back to its PartBudget when the cancellation reaches it, which must not happen
+        while the buffer is still leased (the budget's bound was briefly exceeded)."""
         if not fut.done() or fut.cancelled() or fut.exception() is not None:
             return
         hashed = fut.result()[3]
-        if hashed and hashed.get("gpu_ticket"):
-            threading.Thread(target=self._n.gpu_part_forget, args=(hashed["gpu_ticket"],),
-                             name="gpu-part-forget", daemon=True).start()
+        gid = hashed.get("gpu_ticket") if hashed else 0
+        if not gid:
+            return
+        loop = asyncio.get_running_loop()
+        over = loop.create_future()
+
+        def settle() -> None:
+            if not over.done():
+                over.set_result(None)
+
+        def forget() -> None:
+            try:
+                self._n.gpu_part_forget(gid)
+            finally:
+                try:
+                    loop.call_soon_threadsafe(settle)
+                except RuntimeError:          # the loop is gone: nobody waits any more
+                    pass
+        threading.Thread(target=forget, name="gpu-part-forget", daemon=True).start()
+        try:
+            await asyncio.shield(over)
+        except asyncio.CancelledError:
+            pass
 
     async def close(self) -> None:
         with self._lock:

@@ -62,7 +62,7 @@ def _run(cmd: List[str], verbose: bool) -> None:
 
 def build_native(force: bool = False, verbose: bool = True) -> Path:
     srcs = [CSRC / "module.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp",
-            CSRC / "tls.cpp"]
+            CSRC / "tls.cpp", CSRC / "peerwire.cpp"]
     out = OPS / f"_native{EXT}"
     if force or _stale(out, srcs + [CSRC / "native.h", CSRC / "crc32c.h",
                                     CSRC / "gpu_part_api.h"]):
@@ -78,7 +78,7 @@ def build_native(force: bool = False, verbose: bool = True) -> Path:
 def build_gpuhash(force: bool = False, verbose: bool = True) -> Path:
     srcs = [CSRC / "gpu_sha1.hip"]
     out = OPS / f"_gpuhash{EXT}"
-    if force or _stale(out, srcs + [CSRC / "gpu_part_api.h"]):
+    if force or _stale(out, srcs + [CSRC / "gpu_part_api.h", CSRC / "part_dispatch.h"]):
         hipcc = str(ROCM / "bin" / "hipcc")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
                "-fvisibility=hidden", *_pybind_includes(), str(srcs[0]), "-o", str(out)]
@@ -118,11 +118,11 @@ SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"
 def build_selftest(kind: str, force: bool = False, verbose: bool = True) -> Path:
     """Host-only sanitizer build of the native code's self-test."""
     srcs = [CSRC / "selftest.cpp", CSRC / "hashing.cpp", CSRC / "sha1_mb.cpp", CSRC / "transfer.cpp",
-            CSRC / "tls.cpp"]
+            CSRC / "tls.cpp", CSRC / "peerwire.cpp"]
     BIN.mkdir(exist_ok=True)
     out = BIN / f"selftest_{kind}"
     if force or _stale(out, srcs + [CSRC / "native.h", CSRC / "crc32c.h",
-                                    CSRC / "gpu_part_api.h"]):
+                                    CSRC / "gpu_part_api.h", CSRC / "part_dispatch.h"]):
         cxx = os.environ.get("CXX", "g++")
         cmd = [cxx, "-O1", "-g", "-std=c++17", "-msse4.2", *SANITIZERS[kind],
                *[str(s) for s in srcs],

@@ -13,6 +13,7 @@ torrent creation (bench fixtures), S3 SigV4 payload hashes and Content-MD5 / ETa
 """
 from __future__ import annotations
 
+import collections
 import os
 import threading
 import weakref
@@ -202,7 +203,8 @@ class _GpuParts:
         self._lock = threading.Lock()
         self._parts: dict = {}
         self._early: dict = {}        # news for a part not tracked yet
-        self._loops: "weakref.WeakSet" = weakref.WeakSet()
+        self._evicted: "collections.OrderedDict" = collections.OrderedDict()  # ids whose news
+        self._loops: "weakref.WeakSet" = weakref.WeakSet()                     # were dropped
 
     def track(self, gid: int) -> GpuPart:
         import asyncio
@@ -210,8 +212,16 @@ class _GpuParts:
         self._watch(loop)
         part = GpuPart(loop)
         with self._lock:
-            self._parts[gid] = part
+            lost = self._evicted.pop(gid, None) is not None
+            if not lost:
+                self._parts[gid] = part
             early = self._early.pop(gid, [])
+        if lost:
+            # its news was dropped from a full _early buffer (gpu_part_poll had already
+            # collected the part natively): fail it now instead of waiting for good - the
+            # caller refetches the part
+            part._deliver(3, b"GPU part completion lost before it was tracked")
+            return part
         for kind, data in early:
             self._dispatch(gid, part, kind, data)
         self.drain()                  # news that came before this loop watched the fd
@@ -247,7 +257,11 @@ class _GpuParts:
                     # caller that waits with gpu_part_wait) must not grow it for good
                     self._early.setdefault(gid, []).append((kind, data))
                     while len(self._early) > EARLY_MAX:
-                        self._early.pop(next(iter(self._early)))
+                        old = next(iter(self._early))
+                        self._early.pop(old)
+                        self._evicted[old] = True          # track(old) fails it fast
+                        while len(self._evicted) > 4 * EARLY_MAX:
+                            self._evicted.popitem(last=False)
                     continue
             self._dispatch(gid, part, kind, data)
 

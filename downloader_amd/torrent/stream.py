@@ -400,7 +400,18 @@ class StreamStager:
                 gid = res[1].get("gpu_ticket")
                 if gid:
                     from ..ops import hashing
-                    part = hashing.gpu_part_track(gid)
+                    try:
+                        part = hashing.gpu_part_track(gid)
+                    except BaseException as e:
+                        # untracked, the part would keep its budget bytes, its GPU slot and
+                        # its native record for good: drop it - the bytes come
+                        # back once its DMA is over - then fail the unit as usual
+                        await self._forget_part(gid)
+                        self._budget.release(nb)
+                        self._gpu_slots.release()
+                        if not await self._unit_failed(u, e, queue):
+                            return
+                        continue
                     # the buffer is back in the pool once the DMA is over: so are its bytes
                     part.copied.add_done_callback(lambda _f, nb=nb: self._budget.release(nb))
                     t = asyncio.ensure_future(self._complete(u, res, part, queue))
@@ -426,6 +437,15 @@ class StreamStager:
             if self.error is not None:
                 return
             self._settle(u, requeue, queue)
+
+    async def _forget_part(self, gid: int) -> None:
+        """Drop a queued GPU part nobody will collect (blocks until its DMA is over, so on a
+        thread)."""
+        from ..ops import native
+        try:
+            await asyncio.get_running_loop().run_in_executor(None, native().gpu_part_forget, gid)
+        except Exception:
+            pass
 
     def _gpu_wanted(self) -> bool:
         """``auto``: is the device worth it? When the host lacks the AVX-512 SHA-1, when jobs

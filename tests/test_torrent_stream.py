@@ -426,6 +426,91 @@ def test_stream_async_part_hashing_with_host_double(run, tmp_path, make_cfg, ori
         hashing.use_part_hasher(None)
 
 
+def test_gpu_part_track_failure_releases_budget_and_refetches(run, tmp_path, make_cfg,
+                                                            origin_cls, monkeypatch):
+    """when tracking a queued GPU part raises (e.g. the eventfd cannot be watched),
+    the part is forgotten natively, its budget bytes and GPU slot come back, and the unit is
+    refetched - the job still stages every byte and nothing stays leased or pending."""
+    from downloader_amd.ops import hashing, native
+    real = hashing.gpu_part_track
+    calls = {"n": 0}
+
+    def flaky(gid):
+        calls["n"] += 1
+        if calls["n"] <= 2:
+            raise OSError("add_reader failed")
+        return real(gid)
+    monkeypatch.setattr(hashing, "gpu_part_track", flaky)
+
+    async def go():
+        s3 = FakeS3()
+        ep = await s3.start()
+        origin = await origin_cls().start()
+        src = tmp_path / "src" / "Movie"
+        src.mkdir(parents=True)
+        data = os.urandom(23 * (1 << 20) + 12345)
+        (src / "m.mkv").write_bytes(data)
+        origin.blobs["/ws/Movie/m.mkv"] = data
+        origin.blobs["/t/m.torrent"] = make_torrent(str(src), 1 << 18,
+                                                    url_list=[origin.url("/ws/")])
+        w = _worker(make_cfg, ep, download={"stream_verify_backend": "gpu",
+                                            "stream_gpu_min_pieces": 4, "stream_gpu_tail": 0})
+        await w.start(health=False)
+        await w.submit(api.make_download("tf", "http", origin.url("/t/m.torrent")))
+        await _wait(w, timeout=60)
+        r = w.results[0]
+        assert r.outcome == "staged", r
+        assert s3.get("triton-staging", keys.object_key("tf", "m.mkv")) == data
+        budget = r.stats["torrent"]["budget"]
+        assert budget["used"] == 0 and budget["queued"] == 0     # every byte came back
+        assert native().relay_pool_stats()["in_use"] == 0
+        assert native().gpu_part_stats()["pending"] == 0
+        await w.stop(); await s3.stop(); await origin.stop()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.01), 4)
+    try:
+        run(go())
+    finally:
+        hashing.use_part_hasher(None)
+    assert calls["n"] >= 3
+
+
+def test_gpu_part_news_evicted_before_tracking_fails_fast(monkeypatch):
+    """news for more untracked parts than the early buffer holds is dropped oldest
+    first; tracking such a part later fails it at once (the caller refetches) instead of
+    waiting forever for news that already went."""
+    import asyncio
+    from downloader_amd.ops import hashing
+
+    class FakeNative:
+        def __init__(self):
+            self.batch = []
+            self.rfd, self.wfd = os.pipe()
+
+        def gpu_part_poll(self):
+            b, self.batch = self.batch, []
+            return b
+
+        def gpu_part_eventfd(self):
+            return self.rfd
+    fake = FakeNative()
+    monkeypatch.setattr(hashing, "native", lambda: fake)
+    monkeypatch.setattr(hashing, "EARLY_MAX", 8)
+    parts = hashing._GpuParts()
+    fake.batch = [(gid, 2, b"d" * 20) for gid in range(1, 13)]     # 12 parts, room for 8
+    parts.drain()
+
+    async def go():
+        lost = parts.track(1)                   # evicted: fails now
+        with pytest.raises(RuntimeError, match="lost"):
+            await asyncio.wait_for(lost.done, 1)
+        assert lost.copied.done()
+        kept = parts.track(12)                  # still buffered: delivered normally
+        assert await asyncio.wait_for(kept.done, 1) == b"d" * 20
+    asyncio.run(go())
+    os.close(fake.rfd); os.close(fake.wfd)
+
+
 def test_untracked_gpu_parts_still_return_their_buffers(run, origin_cls):
     """Parts queued to the hasher return their buffers to the pool when their DMA is over,
     whether or not anybody waits for the digests (an aborted job cancels its waits): no
