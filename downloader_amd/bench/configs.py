@@ -435,7 +435,7 @@ async def config_bucket(a) -> Dict:
     return out
 
 
-def _seed_proc(conn, raw: bytes, src: str, n: int) -> None:
+def _seed_proc(conn, raw: bytes, src: str, n: int, native_wire: bool = True) -> None:
     """Seeding clients in their own process (remote peers are not on our event loop)."""
     from downloader_amd.torrent.client import TorrentClient
     from downloader_amd.torrent.metainfo import parse_torrent
@@ -444,7 +444,7 @@ def _seed_proc(conn, raw: bytes, src: str, n: int) -> None:
         meta = parse_torrent(raw)
         cs = []
         for _ in range(n):
-            c = await TorrentClient(max_uploads=64).start()
+            c = await TorrentClient(max_uploads=64, native_wire=native_wire).start()
             await c.add_torrent(meta, src)
             cs.append(c)
         conn.send([c.listen_port for c in cs])
@@ -464,6 +464,7 @@ async def config_swarm(a) -> Dict:
     from downloader_amd.torrent.client import TorrentClient
     from downloader_amd.torrent.metainfo import make_torrent, parse_torrent
     total = int(2e9 * a.scale)
+    wire = getattr(a, "wire", "native") == "native"
     src = tempfile.mkdtemp(prefix="swarm-src-", dir=a.src_dir)
     dst = tempfile.mkdtemp(prefix="swarm-dst-", dir=a.stage_dir or None)
     procs: List = []
@@ -475,7 +476,7 @@ async def config_swarm(a) -> Dict:
         meta = parse_torrent(raw)
         if getattr(a, "seed_inproc", False):
             for _ in range(a.seeders):
-                c = await TorrentClient(max_uploads=64).start()
+                c = await TorrentClient(max_uploads=64, native_wire=wire).start()
                 await c.add_torrent(meta, src)
                 seeders.append(c)
             ports = [c.listen_port for c in seeders]
@@ -488,19 +489,22 @@ async def config_swarm(a) -> Dict:
                      for i in range(nproc)]
             for n in share:
                 conn, child = ctx.Pipe()
-                proc = ctx.Process(target=_seed_proc, args=(child, raw, src, n), daemon=True)
+                proc = ctx.Process(target=_seed_proc, args=(child, raw, src, n, wire),
+                                   daemon=True)
                 proc.start()
                 procs.append((proc, conn))
             ports = []
             for _, conn in procs:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
-        leech = await TorrentClient(max_peers=64, pipeline=a.pipeline).start()
+        leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire).start()
         cpu0 = _self_cpu()
         t0 = time.perf_counter()
         s = await leech.add_torrent(meta, dst, peers=[("127.0.0.1", port) for port in ports])
         await asyncio.wait_for(s.wait(), 1800)
         dt = time.perf_counter() - t0
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
+               "wire": "native" if s.wire is not None else "python",
+               **({"wire_stats": s.wire.stats()} if s.wire is not None else {}),
                "seeders_in_process": bool(seeders), "seeder_procs": len(procs),
                "piece_len": a.piece_mb << 20,
                "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
@@ -623,6 +627,9 @@ def main(argv=None) -> int:
     ap.add_argument("--chaos-timeout", type=float, default=900.0,
                     help="config 7: give up waiting for every job's convert after this long")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")
+    ap.add_argument("--wire", choices=["native", "python"], default="native",
+                    help="config 6: peer connections on the native wire (csrc/peerwire.cpp) or "
+                         "framed in Python (torrent/peer.py), leecher and seeders alike")
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
     ap.add_argument("--seeder-procs", type=int, default=0,
                     help="config 6: processes the seeders run in (0: one per seeder)")

@@ -240,6 +240,23 @@ PYBIND11_MODULE(_native, m) {
              return w.send(id, std::move(s));
            },
            py::arg("conn_id"), py::arg("data"))
+      .def("sendv",
+           [](SwarmWire& w, uint64_t id, const py::list& parts) {
+             // one copy of the parts (bytes, memoryviews of cached pieces) into the queue
+             size_t n = 0;
+             std::vector<py::buffer_info> infos;
+             infos.reserve(parts.size());
+             for (auto h : parts) {
+               infos.push_back(py::reinterpret_borrow<py::buffer>(h).request());
+               n += (size_t)infos.back().size * (size_t)infos.back().itemsize;
+             }
+             std::string s;
+             s.reserve(n);
+             for (auto& i : infos) s.append((const char*)i.ptr, (size_t)i.size * (size_t)i.itemsize);
+             return w.send(id, std::move(s));
+           },
+           py::arg("conn_id"), py::arg("parts"),
+           "Queue the concatenation of `parts` (buffers) for sending; the queued bytes after it")
       .def("pending_out", &SwarmWire::pending_out, py::arg("conn_id"))
       .def("detach", &SwarmWire::detach, py::arg("conn_id"),
            py::call_guard<py::gil_scoped_release>())
@@ -265,6 +282,9 @@ PYBIND11_MODULE(_native, m) {
              d["rx_bytes"] = s.rx_bytes;
              d["recvs"] = s.recvs;
              d["active_pieces"] = s.active_pieces;
+             d["verify_batches"] = s.verify_batches;
+             d["sha_s"] = s.sha_ns / 1e9;
+             d["write_s"] = s.write_ns / 1e9;
              return d;
            })
       .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());

@@ -214,6 +214,8 @@ struct WireEvent {
 struct SwarmWireStats {
   uint64_t begun = 0, blocks = 0, block_bytes = 0, blocks_ignored = 0, verified = 0,
            hash_fails = 0, rx_bytes = 0, recvs = 0;
+  uint64_t verify_batches = 0, sha_ns = 0, write_ns = 0;   // verifier: batches, time hashing /
+                                                            // writing
   size_t active_pieces = 0;
 };
 class SwarmWire {

@@ -30,6 +30,7 @@
 
 #include <poll.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -490,6 +491,123 @@ static PartStressResult part_stress(const PartStress& cfg) {
   return res;
 }
 
+// ---- the native peer wire (peerwire.cpp): 4 connections (socketpairs) feed PIECE messages
+// for the same 24 pieces in random order, split at random points, with duplicates, a bogus
+// block, control messages in between and one corrupt copy of a piece on one connection;
+// every piece must be verified once, written to the two storage files, and reported.
+static void wire_section() {
+  const int64_t plen = 65536, total = 24 * plen - 1000;      // short last piece
+  auto data = rnd((size_t)total, 99);
+  std::string hashes;
+  for (int64_t off = 0; off < total; off += plen)
+    hashes += digest("sha1", data.data() + off, (size_t)std::min(plen, total - off));
+  char p1[] = "/tmp/stager-selftest-wire-XXXXXX", p2[] = "/tmp/stager-selftest-wire-XXXXXX";
+  int f1 = mkstemp(p1), f2 = mkstemp(p2);
+  const int64_t n1 = 500000, n2 = total - n1;                 // pieces straddle the files
+  SwarmWire w(2);
+  w.set_storage(plen, total, hashes, {{f1, n1}, {f2, n2}});
+  const int npieces = (int)((total + plen - 1) / plen);
+  for (int i = 0; i < npieces; ++i) w.begin_piece((uint32_t)i);
+  std::vector<std::thread> feeders;
+  std::vector<int> ours;
+  for (int c = 0; c < 4; ++c) {
+    int sv[2];
+    socketpair(AF_UNIX, SOCK_STREAM, 0, sv);
+    w.attach(sv[0], (uint64_t)(c + 1), c == 0 ? std::string("\0\0\0\0", 4) : "");
+    ours.push_back(sv[1]);
+    feeders.emplace_back([&, c, fd = sv[1]] {
+      std::mt19937 g(7 + c);
+      std::string out;
+      auto msg = [&](uint8_t id, const std::string& pl) {
+        uint32_t n = htonl((uint32_t)(pl.size() + 1));
+        out.append((const char*)&n, 4);
+        out.push_back((char)id);
+        out += pl;
+      };
+      std::vector<int> order(npieces);
+      for (int i = 0; i < npieces; ++i) order[i] = i;
+      std::shuffle(order.begin(), order.end(), g);
+      for (int i : order) {
+        for (int64_t b = 0; b < plen; b += 16384) {
+          const int64_t off = (int64_t)i * plen + b;
+          if (off >= total) break;
+          const int64_t len = std::min<int64_t>(16384, total - off);
+          std::string pl(8, '\0');
+          uint32_t be[2] = {htonl((uint32_t)i), htonl((uint32_t)b)};
+          memcpy(&pl[0], be, 8);
+          std::string blk((const char*)data.data() + off, (size_t)len);
+          if (c == 0 && i == 5 && b == 0) blk[7] ^= 0x5A;      // a corrupt copy
+          msg(7, pl + blk);
+        }
+        if (g() % 4 == 0) msg(4, std::string("\0\0\0\x01", 4));   // HAVE in between
+      }
+      msg(7, std::string("\0\0\0\x63\0\0\0\0xyz", 11));       // no such piece
+      for (size_t off = 0; off < out.size();) {                   // random split points
+        size_t k = std::min(out.size() - off, (size_t)(1 + g() % 70000));
+        ssize_t wr = send(fd, out.data() + off, k, MSG_NOSIGNAL);
+        if (wr <= 0) break;
+        off += (size_t)wr;
+      }
+    });
+    if (c == 0) feeders.back().join();   // connection 0 first: its corrupt piece 5 arrives first
+  }
+  for (auto& t : feeders)
+    if (t.joinable()) t.join();
+  // collect until every piece is verified (a corrupt first copy is re-begun and fed again)
+  std::vector<int> verified(npieces, 0);
+  int bad = 0, msgs = 0, done = 0;
+  uint64_t blocks_taken = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (done < npieces && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60)) {
+    pollfd pf{w.eventfd(), POLLIN, 0};
+    ::poll(&pf, 1, 100);
+    for (auto& e : w.poll()) {
+      if (e.kind == SwarmWire::kEvMsg) msgs++;
+      if (e.kind == SwarmWire::kEvBlocks)
+        for (size_t k = 0; k + 16 <= e.data.size(); k += 16)
+          blocks_taken += e.data[k + 15] != 0;
+      if (e.kind == SwarmWire::kEvPiece) {
+        const uint32_t idx = ntohl(*(const uint32_t*)e.data.data());
+        if (e.data[4] == 1) {
+          verified[idx]++;
+          done++;
+        } else {
+          bad++;
+          w.begin_piece(idx);                 // wanted again: the next copy fills it
+          int fd = ours[0];
+          std::string out;
+          for (int64_t b = 0; b < plen; b += 16384) {
+            const int64_t off = (int64_t)idx * plen + b;
+            const int64_t len = std::min<int64_t>(16384, total - off);
+            uint32_t hdr[3] = {htonl((uint32_t)(len + 9)), htonl(idx), htonl((uint32_t)b)};
+            out.append((const char*)hdr, 4);
+            out.push_back(7);
+            out.append((const char*)&hdr[1], 8);
+            out.append((const char*)data.data() + off, (size_t)len);
+          }
+          send(fd, out.data(), out.size(), MSG_NOSIGNAL);
+        }
+      }
+    }
+  }
+  CHECK(done == npieces);
+  for (int i = 0; i < npieces; ++i) CHECK(verified[i] == 1);
+  CHECK(msgs > 0 && blocks_taken >= (uint64_t)(npieces * 4));
+  SwarmWireStats st = w.stats();
+  CHECK(bad == 1 && st.verified == (uint64_t)npieces && st.hash_fails == 1);
+  w.close();
+  std::vector<uint8_t> back((size_t)total);
+  CHECK(pread(f1, back.data(), (size_t)n1, 0) == n1);
+  CHECK(pread(f2, back.data() + n1, (size_t)n2, 0) == n2);
+  CHECK(back == data);
+  for (int fd : ours) close(fd);
+  close(f1);
+  close(f2);
+  unlink(p1);
+  unlink(p2);
+  fprintf(stderr, "wire: %d pieces verified, %d corrupt copies refused\n", done, bad);
+}
+
 static void stress_sections() {
   // ---- the completion machinery under load: 64 relays x 32 parts (2,048) through
   // PartDispatcher<FakePartDevice>, copies that complete before they are seen, hashers
@@ -537,6 +655,11 @@ static void stress_sections() {
 
 int main() {
   signal(SIGPIPE, SIG_IGN);
+  if (getenv("SELFTEST_ONLY") && strcmp(getenv("SELFTEST_ONLY"), "wire") == 0) {
+    wire_section();
+    printf(g_fail ? "selftest: failures\n" : "selftest ok\n");
+    return g_fail ? 1 : 0;
+  }
   if (getenv("SELFTEST_ONLY") && strcmp(getenv("SELFTEST_ONLY"), "stress") == 0) {
     stress_sections();                 // the part-hasher sections alone (quick iteration)
     printf(g_fail ? "selftest: failures\n" : "selftest ok\n");
@@ -889,6 +1012,7 @@ int main() {
     set_gpu_part_hasher(nullptr, 0);
   }
   stress_sections();
+  wire_section();
   {
     RelayPoolStats st = relay_pool_stats();
     CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);

@@ -31,7 +31,8 @@ class TorrentClient:
                  webseed_verify_depth_gpu: int = 32, verify_threads: int = 0,
                  webseed_max_failures: int = 5,
                  idle_timeout: float = 120.0, connect_timeout: float = 10.0,
-                 seed_after_done: bool = False, listen: bool = True):
+                 seed_after_done: bool = False, listen: bool = True,
+                 native_wire: bool = True, wire_verify_threads: int = 2):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -57,6 +58,9 @@ class TorrentClient:
         self.connect_timeout = connect_timeout
         self.seed_after_done = seed_after_done
         self.listen = listen
+        # peer connections handed to the native wire after the handshake (csrc/peerwire.cpp)
+        self.native_wire = native_wire
+        self.wire_verify_threads = wire_verify_threads
         self.pex_interval = 60.0
         self.piece_cache_bytes = 64 << 20   # per-session LRU of pieces being served to peers
         self.dht_interval = 30.0
@@ -78,6 +82,7 @@ class TorrentClient:
                    webseed_chunk=d.webseed_chunk, webseed_verify_depth=d.webseed_verify_depth,
                    webseed_verify_depth_gpu=d.webseed_verify_depth_gpu,
                    verify_threads=d.verify_threads,
+                   native_wire=d.torrent_native_wire,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

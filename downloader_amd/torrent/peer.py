@@ -5,10 +5,17 @@ from the reference's webtorrent stack (yarn.lock:389-398).
 A ``PeerConn`` owns one TCP connection: it keeps a request pipeline full while unchoked and
 interested, serves blocks of verified pieces to peers it has unchoked, and forwards
 metadata/PEX traffic to the session.
+
+With the session's native wire (``csrc/peerwire.cpp``, ``download.torrent_native_wire``) the
+socket is handed over right after the handshake: native threads frame the messages, copy
+PIECE payloads into the assembling piece and send what this class queues; this class keeps
+every protocol decision (what to request, interest, choking, serving, extensions) and gets
+the other messages, and the blocks that arrived, as events (``_wq``).
 """
 from __future__ import annotations
 
 import asyncio
+import os
 import struct
 import time
 from typing import TYPE_CHECKING, Dict, Optional, Set, Tuple
@@ -24,6 +31,9 @@ BLOCK = 16384
 MAX_MSG = 2 * 1024 * 1024
 CHOKE, UNCHOKE, INTERESTED, NOT_INTERESTED, HAVE, BITFIELD, REQUEST, PIECE, CANCEL, PORT = range(10)
 EXTENDED = 20
+# native wire event kinds (SwarmWire.poll) and this class' own queue markers
+EV_MSG, EV_BLOCKS, EV_CLOSED, EV_PIECE = 1, 2, 3, 4
+EV_FILL, EV_CANCEL_DUPS = 101, 102
 # our extension message ids (what peers must use when talking to us)
 UT_METADATA_ID = 1
 UT_PEX_ID = 2
@@ -83,6 +93,32 @@ class PeerConn:
         self._out: list = []
         self._out_bytes = 0
         self._flush_due = False
+        self.wire = None               # the session's SwarmWire once the socket is handed over
+        self._wq: Optional[asyncio.Queue] = None
+        self.fill_queued = False
+
+    def attach_wire(self, wire) -> None:
+        """Hand the socket to the native wire: asyncio stops reading it (what its buffer
+        already holds goes along as the first bytes), native threads read and write it from
+        here on, and events come back through the session (``TorrentSession._wire_drain``)."""
+        transport = self.writer.transport
+        sock = transport.get_extra_info("socket")
+        if sock is None or transport.get_write_buffer_size():
+            return          # (unsent asyncio bytes would be overtaken: stay on the Python path)
+        transport.pause_reading()
+        buf = getattr(self.reader, "_buffer", None)
+        prefix = bytes(buf) if buf else b""
+        if buf:
+            buf.clear()
+        fd = os.dup(sock.fileno())
+        try:
+            wire.attach(fd, id(self), prefix)
+        except Exception:
+            os.close(fd)
+            transport.resume_reading()
+            raise
+        self.wire = wire
+        self._wq = asyncio.Queue()
 
     # ---------------------------------------------------------------- sending
     # Every message goes through one small output queue that is written out when the
@@ -104,11 +140,18 @@ class PeerConn:
     def _flush(self) -> None:
         self._flush_due = False
         if self._out and not self.closed:
-            self.writer.write(b"".join(self._out))
+            if self.wire is not None:
+                self.wire.sendv(id(self), self._out)     # one copy, into the native queue
+            else:
+                self.writer.write(b"".join(self._out))
         self._out.clear()
         self._out_bytes = 0
 
     async def _maybe_drain(self) -> None:
+        if self.wire is not None:
+            while not self.closed and self.wire.pending_out(id(self)) > 1 << 20:
+                await asyncio.sleep(0.001)
+            return
         if self.writer.transport.get_write_buffer_size() > 1 << 20:
             async with self._wlock:
                 await self.writer.drain()
@@ -186,6 +229,11 @@ class PeerConn:
         except Exception:
             pass
         self.closed = True
+        if self.wire is not None:
+            try:
+                self.wire.detach(id(self))        # FIN, threads joined, its fd closed
+            except Exception:
+                pass
         try:
             self.writer.close()
         except Exception:
@@ -210,6 +258,8 @@ class PeerConn:
             await self.send_bitfield()
             if self.s.client.dht is not None and self.supports_dht:
                 await self.send(PORT, struct.pack(">H", self.s.client.dht.port))
+            if self._wq is not None:
+                await self._run_wire()
             while not self.closed:
                 await self._read_batch(read)
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError, OSError,
@@ -259,6 +309,23 @@ class PeerConn:
             else:                                          # a cut message body
                 body = bytes(mv[pos:]) + await readexactly(n - (end - pos))
                 await self._dispatch(body[0], memoryview(body)[1:])
+                return
+
+    async def _run_wire(self) -> None:
+        """Events of the native wire, in wire order: messages, endgame cancels and refills
+        the session's drain queued for this connection, and the close."""
+        q = self._wq
+        while not self.closed:
+            kind, data = await q.get()
+            if kind == EV_MSG:
+                if data:
+                    await self._dispatch(data[0], memoryview(data)[1:])
+            elif kind == EV_FILL:
+                self.fill_queued = False
+                await self.s.fill(self)
+            elif kind == EV_CANCEL_DUPS:
+                await self.s.cancel_dups(self, *data)
+            elif kind == EV_CLOSED:
                 return
 
     def attach_meta(self) -> None:

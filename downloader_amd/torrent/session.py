@@ -19,6 +19,7 @@ import asyncio
 import hashlib
 import os
 import random
+import struct
 import time
 from collections import OrderedDict
 from typing import TYPE_CHECKING, Dict, List, Optional, Set, Tuple
@@ -30,7 +31,7 @@ from ..utils.aio import drain, gather_strict, run_settled
 from ..utils.log import redact_url
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
-from .peer import BLOCK, METADATA_PIECE, PeerConn
+from .peer import BLOCK, EV_BLOCKS, EV_CANCEL_DUPS, EV_FILL, EV_PIECE, METADATA_PIECE, PeerConn
 from .storage import Bitfield, Storage
 from .tracker import decode_compact, encode_compact, supported as tracker_supported
 
@@ -55,11 +56,12 @@ class TorrentError(Exception):
 class _Active:
     __slots__ = ("idx", "size", "nblocks", "buf", "state", "req", "got", "peers")
 
-    def __init__(self, idx: int, size: int):
+    def __init__(self, idx: int, size: int, buffered: bool = True):
         self.idx = idx
         self.size = size
         self.nblocks = (size + BLOCK - 1) // BLOCK
-        self.buf = bytearray(size)
+        # with the native wire the piece is assembled (and verified, written) natively
+        self.buf = bytearray(size) if buffered else None
         self.state = bytearray(self.nblocks)   # 0 free, 1 requested, 2 received
         self.req: Dict[int, Set[int]] = {}     # block -> ids of peers that requested it
         self.got = 0
@@ -93,6 +95,8 @@ class PiecePicker:
         self._slot = [-1] * self.n            # bucket a piece's live entry sits in (-1: none)
         self._peers: Dict[int, Bitfield] = {}
         self.want_count: Dict[int, int] = {}      # peer id -> pieces it has that we lack
+        # native wire: called when a piece becomes active (its native buffer starts over)
+        self.on_activate = None
         for i in range(self.n):
             self._push(i)
 
@@ -203,7 +207,9 @@ class PiecePicker:
         # 2. start the rarest piece this peer has
         best = self._take_rarest(bf)
         if best >= 0:
-            ap = _Active(best, self.meta.piece_size(best))
+            ap = _Active(best, self.meta.piece_size(best), self.on_activate is None)
+            if self.on_activate is not None:
+                self.on_activate(best)
             self.active[best] = ap
             ap.state[0] = 1
             ap.req[0] = {peer_id}
@@ -395,6 +401,17 @@ class TorrentSession:
         # block_followup of the same dispatch
         self._followup: Dict[Tuple[int, int], tuple] = {}
         self._piece_cache_bytes = 0
+        # native peer wire (csrc/peerwire.cpp): sockets handed over after the handshake
+        self.wire = None
+        self._wire_loop = None
+        self._wire_pieces: "asyncio.Queue" = asyncio.Queue()
+        self._verifying_ap: Dict[int, _Active] = {}   # natively verified pieces: contributors
+        if client.native_wire:
+            try:
+                from ..ops import native
+                self.wire = native().SwarmWire(max(1, client.wire_verify_threads))
+            except Exception:
+                self.wire = None
         self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0,
                       # summed over webseed streams: time in Range GETs / in piece verification
                       "webseed_fetch_s": 0.0, "webseed_verify_s": 0.0}
@@ -419,6 +436,10 @@ class TorrentSession:
         return self.meta.total_length - self.verified_bytes
 
     async def start(self) -> None:
+        if self.wire is not None:
+            self._wire_loop = asyncio.get_running_loop()
+            self._wire_loop.add_reader(self.wire.eventfd(), self._wire_drain)
+            self._spawn(self._wire_piece_loop())
         if self.meta is not None:
             await self._init_storage()
         self._spawn(self._connector())
@@ -460,6 +481,11 @@ class TorrentSession:
         self.verified_bytes = sum(meta.piece_size(i) for i in range(meta.num_pieces)
                                   if i in self.have)
         self.picker = PiecePicker(meta, self.have)
+        if self.wire is not None:
+            self.wire.set_storage(meta.piece_length, meta.total_length, meta.pieces,
+                                  [(fd, n) for fd, (_, n) in zip(self.storage.fds,
+                                                                  self.storage.paths)])
+            self.picker.on_activate = self.wire.begin_piece
         self.meta_ready.set()
         for p in list(self.peers.values()):
             p.attach_meta()
@@ -533,6 +559,11 @@ class TorrentSession:
             return False
         self.peers[id(pc)] = pc
         self.stats["peers_connected"] += 1
+        if self.wire is not None:
+            try:
+                pc.attach_wire(self.wire)
+            except Exception:
+                pass                      # this connection stays on the Python path
         if self.meta is not None and pc.bitfield is None:
             pc.bitfield = Bitfield(self.meta.num_pieces)
         return True
@@ -540,10 +571,13 @@ class TorrentSession:
     def peer_closed(self, pc: PeerConn) -> None:
         if self.peers.pop(id(pc), None) is None:
             return
+        released = bool(pc.inflight)
         self.release_inflight(pc)
         if pc.bitfield is not None and self.picker is not None:
             self.picker.remove_peer(pc.bitfield, id(pc))
         self._wake.set()
+        if released and not self._closed:
+            self._refill_all()
 
     def release_inflight(self, pc: PeerConn) -> None:
         if self.picker is not None:
@@ -560,6 +594,108 @@ class TorrentSession:
         unchoked = sum(1 for p in self.peers.values() if not p.am_choking)
         if pc.am_choking and unchoked < self.client.max_uploads and self.have is not None:
             await pc.set_choking(False)
+
+    # ---------------------------------------------------------------- native wire
+    def _wire_drain(self) -> None:
+        """eventfd readable: route the wire's events. Block arrivals are booked right here
+        (no await, no copy: the bytes are already in their native piece); messages, endgame
+        cancels and refills go to the connection's own queue, piece results to the piece
+        task."""
+        if self.wire is None:
+            return
+        now = time.monotonic()
+        for conn, kind, data in self.wire.poll():
+            if kind == EV_PIECE:
+                self._wire_pieces.put_nowait(data)
+                continue
+            pc = self.peers.get(conn)
+            if pc is None or pc._wq is None:
+                continue
+            pc.last_rx = now
+            if kind == EV_BLOCKS:
+                self._wire_blocks(pc, data)
+            else:
+                pc._wq.put_nowait((kind, data))
+
+    def _wire_blocks(self, pc: PeerConn, data: bytes) -> None:
+        picker = self.picker
+        inflight = pc.inflight
+        me = id(pc)
+        for idx, begin, ln, st in struct.iter_unpack(">IIII", data):
+            inflight.pop((idx, begin), None)
+            if not st or picker is None:
+                continue
+            self.downloaded += ln
+            pc.down_bytes += ln
+            ap = picker.active.get(idx)
+            if ap is None:
+                continue
+            b = begin // BLOCK
+            if ap.state[b] != 2:
+                ap.state[b] = 2
+                ap.got += 1
+            ap.peers.add(me)
+            rs = ap.req.pop(b, None)
+            if rs is not None and (len(rs) > 1 or me not in rs):     # endgame duplicates
+                pc._wq.put_nowait((EV_CANCEL_DUPS, (rs, idx, begin, ln)))
+            if st == 2 and picker.complete_blocks(idx):
+                self._verifying_ap[idx] = ap          # verified + written natively
+        if not pc.fill_queued and self.refill_due(pc):
+            pc.fill_queued = True
+            pc._wq.put_nowait((EV_FILL, None))
+
+    async def cancel_dups(self, pc: PeerConn, dup: Set[int], idx: int, begin: int,
+                          ln: int) -> None:
+        for other_id in dup:
+            if other_id != id(pc):
+                other = self.peers.get(other_id)
+                if other is not None:
+                    await other.cancel(idx, begin, ln)
+
+    async def _wire_piece_loop(self) -> None:
+        """Native verification results, in order: 1 verified and written, 0 hash mismatch,
+        2 storage write failed."""
+        while True:
+            data = await self._wire_pieces.get()
+            idx, status = struct.unpack(">IB", data[:5])
+            ap = self._verifying_ap.pop(idx, None)
+            if self.picker is None:
+                continue
+            if status == 1:
+                await self._piece_complete(idx)
+            elif status == 2:
+                self.picker.requeue(idx)
+                self.fail(TorrentError(f"storage write of piece {idx} failed: "
+                                       f"{data[5:].decode(errors='replace')}"))
+            else:
+                self.stats["hash_fails"] += 1
+                self.picker.requeue(idx)
+                for pid in (ap.peers if ap is not None else ()):
+                    p = self.peers.get(pid)
+                    if p is not None:
+                        p.hash_fails += 1
+                        if p.hash_fails >= 3:
+                            p.close()
+                # the verdict came after the blocks: no arrival will refill the pipelines, so
+                # the requeued piece is offered to every connection now
+                self._refill_all()
+
+    def _refill_all(self) -> None:
+        """Offer freed blocks (a requeued piece, a closed peer's requests) to every
+        connection: an idle pipeline is otherwise only refilled by its own next arrival."""
+        for p in list(self.peers.values()):
+            if p.closed or p.fill_queued:
+                continue
+            p.fill_queued = True
+            if p._wq is not None:
+                p._wq.put_nowait((EV_FILL, None))
+            else:
+                self._spawn(self._fill_once(p))
+
+    async def _fill_once(self, pc: PeerConn) -> None:
+        pc.fill_queued = False
+        if not pc.closed:
+            await self.fill(pc)
 
     def refill_due(self, pc: PeerConn) -> bool:
         """Whether ``fill`` would send anything (checked without a coroutine per block)."""
@@ -1005,6 +1141,11 @@ class TorrentSession:
         for p in list(self.peers.values()):
             p.close()
         await asyncio.gather(*self._tasks, return_exceptions=True)
+        if self.wire is not None:
+            # its verifiers write into the storage's fds: stopped before those close
+            if self._wire_loop is not None and not self._wire_loop.is_closed():
+                self._wire_loop.remove_reader(self.wire.eventfd())
+            await asyncio.get_running_loop().run_in_executor(None, self.wire.close)
         if self.storage is not None:
             # may wait for a piece write still on an executor thread: not on the loop
             await asyncio.get_running_loop().run_in_executor(None, self.storage.close)

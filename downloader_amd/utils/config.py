@@ -242,6 +242,9 @@ class DownloadConfig(BaseModel):
     torrent_enable_trackers: bool = True        # HTTP / UDP trackers
     torrent_enable_webseeds: bool = True        # BEP-19 url-list
     torrent_request_pipeline: int = 16          # 16 KiB block requests in flight per peer
+    # peer connections framed, assembled, SHA-1'd (16 pieces at a time) and written by the
+    # native wire after the handshake (csrc/peerwire.cpp); False: all in Python (peer.py)
+    torrent_native_wire: bool = True
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -235,6 +235,66 @@ def test_bad_peer_data_is_rejected_and_refetched(run, tmp_path):
     run(go(), timeout=90)
 
 
+@pytest.mark.parametrize("native_wire", [True, False])
+def test_swarm_native_and_python_wire(run, tmp_path, native_wire):
+    """The peer wire both ways (download.torrent_native_wire): multi-file pieces straddling
+    file boundaries from two seeders. Natively every piece is assembled, SHA-1'd and written
+    by csrc/peerwire.cpp (its counters say so); in Python by peer.py/session.py."""
+    async def go():
+        src = tmp_path / "seed"
+        data = _tree(src / "Pack", {"a.mkv": 1_000_003, "S1/b.mkv": 377_777, "S1/c.mkv": 5})
+        raw = make_torrent(str(src / "Pack"), 65536)
+        seeders = []
+        for _ in range(2):
+            c = await TorrentClient(native_wire=native_wire).start()
+            await c.add_torrent(parse_torrent(raw), str(src))
+            seeders.append(c)
+        leech = await TorrentClient(native_wire=native_wire, pipeline=32).start()
+        meta = parse_torrent(raw)
+        s = await leech.add_torrent(meta, str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", c.listen_port) for c in seeders])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        assert s.stats["hash_fails"] == 0
+        if native_wire:
+            st = s.wire.stats()
+            assert st["verified"] == meta.num_pieces and st["hash_fails"] == 0
+            assert st["block_bytes"] == meta.total_length and st["active_pieces"] == 0
+            assert all(p.wire is not None for p in s.peers.values())
+        else:
+            assert s.wire is None
+        await leech.close()
+        for c in seeders:
+            await c.close()
+    run(go(), timeout=90)
+
+
+def test_native_wire_bad_piece_is_refetched_and_peer_blamed(run, tmp_path):
+    """A seeder serving a corrupt piece over the native wire: the native verifier rejects
+    it (hash_fails), the session requeues it and gets it from the good seeder."""
+    async def go():
+        raw, data, seeder, src = await _seed(tmp_path, {"x.mkv": 300_000})
+        p = src / "Pack" / "x.mkv"
+        b = bytearray(p.read_bytes())
+        b[40_000] ^= 0xFF                        # piece 1 of 32 KiB pieces
+        p.write_bytes(bytes(b))
+        good = await TorrentClient().start()
+        gdir = tmp_path / "good"
+        (gdir / "Pack").mkdir(parents=True)
+        (gdir / "Pack" / "x.mkv").write_bytes(data["x.mkv"])
+        await good.add_torrent(parse_torrent(raw), str(gdir))
+        leech = await TorrentClient(pipeline=64).start()
+        s = await leech.add_torrent(parse_torrent(raw), str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.sleep(0.5)                 # the bad seeder alone first: piece 1 fails
+        s.add_peers([("127.0.0.1", good.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        assert s.wire.stats()["hash_fails"] >= 1 and s.stats["hash_fails"] >= 1
+        await leech.close(); await seeder.close(); await good.close()
+    run(go(), timeout=90)
+
+
 def test_webseed_single_and_multi_file(run, tmp_path, origin_cls):
     async def go():
         origin = await origin_cls().start()
