@@ -497,18 +497,24 @@ async def config_swarm(a) -> Dict:
             for _, conn in procs:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire).start()
+        threads0 = _thread_cpu(0)
         cpu0 = _self_cpu()
         t0 = time.perf_counter()
         s = await leech.add_torrent(meta, dst, peers=[("127.0.0.1", port) for port in ports])
         await asyncio.wait_for(s.wait(), 1800)
         dt = time.perf_counter() - t0
+        cpu_s = _self_cpu() - cpu0
+        # where the leecher's CPU went (before close: the wire's threads still exist)
+        per_thread = _thread_cpu_delta(threads0, _thread_cpu(0))
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
                "wire": "native" if s.wire is not None else "python",
                **({"wire_stats": s.wire.stats()} if s.wire is not None else {}),
                "seeders_in_process": bool(seeders), "seeder_procs": len(procs),
                "piece_len": a.piece_mb << 20,
                "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
-               "leech_cpu_s": round(_self_cpu() - cpu0, 2), "hash_fails": s.stats["hash_fails"]}
+               "leech_cpu_s": round(cpu_s, 2), "hash_fails": s.stats["hash_fails"],
+               "leech_cpu_s_per_GB": round(cpu_s / (total / 1e9), 3),
+               "leech_thread_cpu": per_thread}
         await leech.close()
         return out
     finally:

@@ -228,6 +228,11 @@ PYBIND11_MODULE(_native, m) {
            py::arg("piece_length"), py::arg("total"), py::arg("hashes"), py::arg("files"))
       .def("begin_piece", &SwarmWire::begin_piece, py::arg("idx"))
       .def("drop_piece", &SwarmWire::drop_piece, py::arg("idx"))
+      .def("set_have",
+           [](SwarmWire& w, const py::bytes& bits) { w.set_have(std::string(bits)); },
+           py::arg("bits"))
+      .def("set_have_piece", &SwarmWire::set_have_piece, py::arg("idx"))
+      .def("set_serving", &SwarmWire::set_serving, py::arg("conn_id"), py::arg("on"))
       .def("attach",
            [](SwarmWire& w, int fd, uint64_t id, const py::bytes& prefix) {
              w.attach(fd, id, std::string(prefix));
@@ -285,6 +290,7 @@ PYBIND11_MODULE(_native, m) {
              d["verify_batches"] = s.verify_batches;
              d["sha_s"] = s.sha_ns / 1e9;
              d["write_s"] = s.write_ns / 1e9;
+             d["served_bytes"] = s.served_bytes;
              return d;
            })
       .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());

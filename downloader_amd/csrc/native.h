@@ -216,6 +216,7 @@ struct SwarmWireStats {
            hash_fails = 0, rx_bytes = 0, recvs = 0;
   uint64_t verify_batches = 0, sha_ns = 0, write_ns = 0;   // verifier: batches, time hashing /
                                                             // writing
+  uint64_t served_bytes = 0;                                // blocks served with sendfile
   size_t active_pieces = 0;
 };
 class SwarmWire {
@@ -227,6 +228,11 @@ class SwarmWire {
                    const std::vector<std::pair<int, int64_t>>& files);
   void begin_piece(uint32_t idx);
   void drop_piece(uint32_t idx);
+  // Serving: pieces we have (storage recheck; natively verified ones are added as they pass)
+  // are served to connections Python unchoked, straight from the storage files.
+  void set_have(const std::string& bits);
+  void set_have_piece(uint32_t idx);
+  void set_serving(uint64_t id, bool on);
   void attach(int fd, uint64_t id, const std::string& prefix);
   size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
   size_t pending_out(uint64_t id);
@@ -246,12 +252,18 @@ class SwarmWire {
   void push(uint64_t conn, int kind, std::string data);
   void read_loop(Conn& c);
   void write_loop(Conn& c);
+  bool has(uint32_t idx);
+  bool servable(uint32_t idx, uint32_t begin, uint32_t len);
+  bool serve_block(Conn& c, const std::string& req);
+  bool send_all(Conn& c, const char* p, size_t n, int flags);
 
   std::mutex mu_;                               // pieces_, geometry, stats_
   int64_t piece_length_ = 0, total_ = 0;
   std::string hashes_;
   std::vector<std::pair<int, int64_t>> files_;
   std::unordered_map<uint32_t, std::shared_ptr<Piece>> pieces_;
+  std::vector<uint8_t> have_;                   // bitfield (BEP-3 bit order)
+  std::atomic<uint64_t> served_bytes_{0};
   uint64_t epoch_ = 0;
   SwarmWireStats stats_;
   std::atomic<uint64_t> rx_bytes_{0}, recvs_{0};

@@ -13,13 +13,17 @@
 //     while Python has not polled: the busier the loop, the bigger the batches);
 //   * complete pieces are verified 16 at a time on the AVX-512 multi-buffer SHA-1 (sha1_mb),
 //     written to the storage files with pwrite, and reported as PIECE events;
-//   * one writer thread per connection sends what Python queues (requests, blocks it serves).
+//   * one writer thread per connection sends what Python queues (requests, handshake-time
+//     messages) and serves the REQUESTs of peers Python has unchoked for pieces we have: the
+//     PIECE header, then the block straight from the storage files with sendfile (no copy
+//     through user space; Python only decides who is unchoked).
 // Events reach the event loop through an eventfd, like gpu_part_poll.
 #include "native.h"
 
 #include <poll.h>
 #include <pthread.h>
 #include <sys/eventfd.h>
+#include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -44,6 +48,8 @@ namespace {
 constexpr uint32_t kBlock = 16384;
 constexpr uint32_t kMaxMsg = 2u << 20;     // torrent/peer.py MAX_MSG
 constexpr uint8_t kPiece = 7;
+constexpr uint8_t kRequest = 6;
+constexpr uint32_t kMaxServe = 131072;     // session.py serve_request's bound
 
 uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
@@ -70,7 +76,15 @@ struct SwarmWire::Conn {
   std::thread reader, writer;
   std::mutex wmu;
   std::condition_variable wcv;
-  std::deque<std::string> out;
+  // FIFO of what to send: bytes from Python, or (serve != 0) a block to serve from storage:
+  // piece, begin, length packed into `data`
+  struct Item {
+    std::string data;
+    bool serve = false;
+  };
+  std::deque<Item> out;
+  std::atomic<bool> serving{false};      // Python unchoked the peer: REQUESTs served natively
+  std::atomic<uint64_t> served{0};
   size_t out_bytes = 0;
   bool stop = false;                     // under wmu
   std::atomic<bool> dead{false};
@@ -124,6 +138,27 @@ void SwarmWire::set_storage(int64_t piece_length, int64_t total, const std::stri
 uint32_t SwarmWire::piece_size(uint32_t idx) const {
   const int64_t off = (int64_t)idx * piece_length_;
   return (uint32_t)std::min<int64_t>(piece_length_, total_ - off);
+}
+
+void SwarmWire::set_have(const std::string& bits) {
+  std::lock_guard<std::mutex> g(mu_);
+  have_.assign(bits.begin(), bits.end());
+}
+
+void SwarmWire::set_have_piece(uint32_t idx) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (have_.size() <= idx / 8) have_.resize(idx / 8 + 1, 0);
+  have_[idx / 8] |= (uint8_t)(0x80 >> (idx % 8));
+}
+
+bool SwarmWire::has(uint32_t idx) {      // mu_ held
+  return idx / 8 < have_.size() && (have_[idx / 8] & (0x80 >> (idx % 8)));
+}
+
+void SwarmWire::set_serving(uint64_t id, bool on) {
+  std::lock_guard<std::mutex> g(cmu_);
+  auto it = conns_.find(id);
+  if (it != conns_.end()) it->second->serving.store(on);
 }
 
 void SwarmWire::begin_piece(uint32_t idx) {
@@ -246,8 +281,13 @@ void SwarmWire::verify_loop() {
       ev += err;
       {
         std::lock_guard<std::mutex> g(mu_);
-        if (ok && err.empty()) stats_.verified++;
-        else if (!ok) stats_.hash_fails++;
+        if (ok && err.empty()) {
+          stats_.verified++;
+          if (have_.size() <= p.idx / 8) have_.resize(p.idx / 8 + 1, 0);
+          have_[p.idx / 8] |= (uint8_t)(0x80 >> (p.idx % 8));   // servable from now on
+        } else if (!ok) {
+          stats_.hash_fails++;
+        }
       }
       push(0, kEvPiece, std::move(ev));
     }
@@ -368,6 +408,13 @@ void SwarmWire::read_loop(Conn& c) {
           put32(blocks, begin);
           put32(blocks, len);
           put32(blocks, (uint32_t)st);
+        } else if (m[0] == kRequest && n == 13 && c.serving.load() &&
+                   servable(be32(m + 1), be32(m + 5), be32(m + 9))) {
+          std::string it(12, '\0');          // served by the writer, in order with the rest
+          memcpy(&it[0], m + 1, 12);
+          std::lock_guard<std::mutex> g(c.wmu);
+          c.out.push_back(Conn::Item{std::move(it), true});
+          c.wcv.notify_one();
         } else {
           flush_blocks();                 // keep the order of blocks and control messages
           push(c.id, kEvMsg, std::string((const char*)m, n));
@@ -412,16 +459,92 @@ void SwarmWire::read_loop(Conn& c) {
   push(c.id, kEvClosed, reason);
 }
 
+bool SwarmWire::servable(uint32_t idx, uint32_t begin, uint32_t len) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (piece_length_ <= 0 || (int64_t)idx * piece_length_ >= total_ || !has(idx)) return false;
+  return len > 0 && len <= kMaxServe && (uint64_t)begin + len <= piece_size(idx);
+}
+
+// PIECE header + the block from the storage files (sendfile: page cache -> socket).
+bool SwarmWire::serve_block(Conn& c, const std::string& req) {
+  const uint32_t idx = be32((const uint8_t*)req.data()), begin = be32((const uint8_t*)req.data() + 4),
+                 len = be32((const uint8_t*)req.data() + 8);
+  std::vector<std::pair<int, int64_t>> files;
+  int64_t off;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    files = files_;
+    off = (int64_t)idx * piece_length_ + begin;
+  }
+  std::string hdr;
+  put32(hdr, len + 9);
+  hdr.push_back((char)kPiece);
+  put32(hdr, idx);
+  put32(hdr, begin);
+  if (!send_all(c, hdr.data(), hdr.size(), MSG_MORE)) return false;
+  int64_t left = len, fstart = 0;
+  for (auto& f : files) {
+    const int64_t fend = fstart + f.second;
+    while (left > 0 && off >= fstart && off < fend) {
+      off_t fo = (off_t)(off - fstart);
+      const size_t k = (size_t)std::min<int64_t>(left, fend - off);
+      ssize_t w = ::sendfile(c.fd, f.first, &fo, k);
+      if (w < 0 && errno == EINTR) continue;
+      if (w < 0 && errno == EAGAIN) {
+        pollfd pf{c.fd, POLLOUT, 0};
+        ::poll(&pf, 1, 500);
+        if (c.dead.load()) return false;
+        continue;
+      }
+      if (w <= 0) return false;
+      off += w;
+      left -= w;
+    }
+    fstart = fend;
+  }
+  c.served.fetch_add(len, std::memory_order_relaxed);
+  served_bytes_.fetch_add(len, std::memory_order_relaxed);
+  return left == 0;
+}
+
+bool SwarmWire::send_all(Conn& c, const char* p, size_t n, int flags) {
+  size_t off = 0;
+  while (off < n) {
+    if (c.dead.load()) return false;
+    ssize_t w = ::send(c.fd, p + off, n - off, MSG_NOSIGNAL | flags);
+    if (w > 0) {
+      off += (size_t)w;
+      continue;
+    }
+    if (w < 0 && errno == EINTR) continue;
+    if (w < 0 && errno == EAGAIN) {
+      pollfd pf{c.fd, POLLOUT, 0};
+      ::poll(&pf, 1, 500);
+      continue;
+    }
+    return false;
+  }
+  return true;
+}
+
 void SwarmWire::write_loop(Conn& c) {
   for (;;) {
-    std::string s;
+    Conn::Item item;
     {
       std::unique_lock<std::mutex> lk(c.wmu);
       c.wcv.wait(lk, [&] { return c.stop || !c.out.empty(); });
       if (c.stop) return;
-      s = std::move(c.out.front());
+      item = std::move(c.out.front());
       c.out.pop_front();
     }
+    if (item.serve) {
+      if (!serve_block(c, item.data)) {
+        c.dead.store(true);               // the reader notices and reports the close
+        ::shutdown(c.fd, SHUT_RDWR);
+      }
+      continue;
+    }
+    std::string& s = item.data;
     size_t off = 0;
     while (off < s.size() && !c.dead.load()) {
       ssize_t w = ::send(c.fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
@@ -455,7 +578,7 @@ size_t SwarmWire::send(uint64_t id, std::string data) {
   std::lock_guard<std::mutex> g(c->wmu);
   if (c->stop || c->dead.load()) return 0;
   c->out_bytes += data.size();
-  c->out.push_back(std::move(data));
+  c->out.push_back(Conn::Item{std::move(data), false});
   c->wcv.notify_one();
   return c->out_bytes;
 }
@@ -495,6 +618,7 @@ SwarmWireStats SwarmWire::stats() {
   s.active_pieces = pieces_.size();
   s.rx_bytes = rx_bytes_.load();
   s.recvs = recvs_.load();
+  s.served_bytes = served_bytes_.load();
   return s;
 }
 

@@ -199,7 +199,12 @@ class PeerConn:
     async def set_choking(self, v: bool) -> None:
         if v != self.am_choking:
             self.am_choking = v
+            if self.wire is not None and v:
+                self.wire.set_serving(id(self), False)    # before the CHOKE is queued
             await self.send(CHOKE if v else UNCHOKE)
+            if self.wire is not None and not v:
+                self._flush()                             # the UNCHOKE goes out first, then
+                self.wire.set_serving(id(self), True)     # REQUESTs are served natively
 
     async def request(self, piece: int, begin: int, length: int) -> None:
         self.inflight[(piece, begin)] = time.monotonic()

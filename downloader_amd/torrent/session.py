@@ -486,6 +486,7 @@ class TorrentSession:
                                   [(fd, n) for fd, (_, n) in zip(self.storage.fds,
                                                                   self.storage.paths)])
             self.picker.on_activate = self.wire.begin_piece
+            self.wire.set_have(self.have.to_bytes())     # what unchoked peers may be served
         self.meta_ready.set()
         for p in list(self.peers.values()):
             p.attach_meta()
@@ -794,6 +795,8 @@ class TorrentSession:
     async def _piece_complete(self, idx: int) -> None:
         if not self.have.set(idx):
             return
+        if self.wire is not None:
+            self.wire.set_have_piece(idx)        # (natively verified pieces are set already)
         self.picker.piece_done(idx)
         self.verified_bytes += self.meta.piece_size(idx)
         for cb in self.piece_listeners:

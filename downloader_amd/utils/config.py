@@ -217,7 +217,7 @@ class DownloadConfig(BaseModel):
     # (0 = the hardware queues the copy streams leave, GPU_MAX_HW_QUEUES = 4 by default): a
     # copy stream sharing a hardware queue with a compute stream waits behind its kernels.
     # Config 4 at a 1 GiB part budget, 6 steady reps each: 2 copy + 2 compute 29.3 GB/s
-    # median, 1 + 3 27.1, round 3's 1 + 4 25.8 (profiles/r4/copies/)
+    # median, 1 + 3 27.1, round 3's 1 + 4 25.8 (profiles/archive/r4/copies/)
     stream_gpu_copy_streams: int = 2
     stream_gpu_compute_streams: int = 0
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host

@@ -105,7 +105,7 @@ def relay_plan(concurrency: int, parts_per_job: int, sharers: int,
     running ``concurrency`` jobs of ``parts_per_job`` relays (one pipe each): the largest pipe
     (<= 1 MiB) that fits 7/8 of the uid's pipe budget, lowering the concurrency (to 2 at
     least) while the pipe would be smaller than 512 KiB. MI355X box, one 16-CPU rank
-    (profiles/r4/pipes/): 1 MiB 66.7 / 66.1 GB/s, 512 KiB 63.2 / 65.8, 512 KiB at 3 jobs
+    (profiles/archive/r4/pipes/): 1 MiB 66.7 / 66.1 GB/s, 512 KiB 63.2 / 65.8, 512 KiB at 3 jobs
     67.7 / 62.2, 256 KiB 53.6 / 62.5 - so at 8 ranks x 2 processes (64 MiB budget) 3 jobs on
     512 KiB pipes beat 4 jobs on 256 KiB ones."""
     if budget < 0:

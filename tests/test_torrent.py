@@ -261,6 +261,10 @@ def test_swarm_native_and_python_wire(run, tmp_path, native_wire):
             assert st["verified"] == meta.num_pieces and st["hash_fails"] == 0
             assert st["block_bytes"] == meta.total_length and st["active_pieces"] == 0
             assert all(p.wire is not None for p in s.peers.values())
+            # the seeders served every block from their storage files natively (sendfile)
+            served = sum(ss.wire.stats()["served_bytes"] for c in seeders
+                         for ss in c.sessions.values())
+            assert served >= meta.total_length
         else:
             assert s.wire is None
         await leech.close()
