@@ -496,7 +496,8 @@ async def config_swarm(a) -> Dict:
             ports = []
             for _, conn in procs:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
-        leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire).start()
+        leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire,
+                                    swarm_verify=getattr(a, "swarm_verify", "auto")).start()
         threads0 = _thread_cpu(0)
         cpu0 = _self_cpu()
         t0 = time.perf_counter()
@@ -508,6 +509,7 @@ async def config_swarm(a) -> Dict:
         per_thread = _thread_cpu_delta(threads0, _thread_cpu(0))
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
                "wire": "native" if s.wire is not None else "python",
+               "swarm_verify": s.stats.get("swarm_verify", "python"),
                **({"wire_stats": s.wire.stats()} if s.wire is not None else {}),
                "seeders_in_process": bool(seeders), "seeder_procs": len(procs),
                "piece_len": a.piece_mb << 20,
@@ -633,6 +635,8 @@ def main(argv=None) -> int:
     ap.add_argument("--chaos-timeout", type=float, default=900.0,
                     help="config 7: give up waiting for every job's convert after this long")
     ap.add_argument("--seeders", type=int, default=4, help="config 6: seeding clients")
+    ap.add_argument("--swarm-verify", choices=["auto", "gpu", "cpu"], default="auto",
+                    help="config 6: piece SHA-1 of the native wire on the gfx950 or the host")
     ap.add_argument("--wire", choices=["native", "python"], default="native",
                     help="config 6: peer connections on the native wire (csrc/peerwire.cpp) or "
                          "framed in Python (torrent/peer.py), leecher and seeders alike")

@@ -233,6 +233,8 @@ PYBIND11_MODULE(_native, m) {
            py::arg("bits"))
       .def("set_have_piece", &SwarmWire::set_have_piece, py::arg("idx"))
       .def("set_serving", &SwarmWire::set_serving, py::arg("conn_id"), py::arg("on"))
+      .def("set_gpu", &SwarmWire::set_gpu, py::arg("on"),
+           "Verify complete pieces on the installed GPU part hasher (set_gpu_part_hasher)")
       .def("attach",
            [](SwarmWire& w, int fd, uint64_t id, const py::bytes& prefix) {
              w.attach(fd, id, std::string(prefix));
@@ -291,6 +293,10 @@ PYBIND11_MODULE(_native, m) {
              d["sha_s"] = s.sha_ns / 1e9;
              d["write_s"] = s.write_ns / 1e9;
              d["served_bytes"] = s.served_bytes;
+             d["gpu_pieces"] = s.gpu_pieces;
+             d["gpu_refused"] = s.gpu_refused;
+             d["gpu_errors"] = s.gpu_errors;
+             d["pool_buffers"] = s.pool_buffers;
              return d;
            })
       .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());

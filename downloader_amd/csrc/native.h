@@ -161,6 +161,7 @@ struct RelayPoolStats {
 // gpu_part_poll, or waited for with gpu_part_wait. Part ids are this module's own (never a
 // hasher's ticket), so replacing the hasher cannot make two pending parts collide.
 void set_gpu_part_hasher(const void* api, int min_pieces);
+const void* gpu_part_hasher_current();        // the installed hasher's API (null: none)
 struct GpuPartStats {
   uint64_t submitted, host_fallbacks, refused, pending;
 };
@@ -217,6 +218,8 @@ struct SwarmWireStats {
   uint64_t verify_batches = 0, sha_ns = 0, write_ns = 0;   // verifier: batches, time hashing /
                                                             // writing
   uint64_t served_bytes = 0;                                // blocks served with sendfile
+  uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
+  size_t pool_buffers = 0;                                  // page-locked piece buffers
   size_t active_pieces = 0;
 };
 class SwarmWire {
@@ -233,6 +236,12 @@ class SwarmWire {
   void set_have(const std::string& bits);
   void set_have_piece(uint32_t idx);
   void set_serving(uint64_t id, bool on);
+  // Verify complete pieces on the installed GPU part hasher (gpu_part_api.h, the gfx950
+  // PartHasher) instead of sha1_mb: piece buffers come from a pool page-locked for it, each
+  // complete piece is submitted at once (the device batches them into sha1_lanes launches),
+  // a collector thread takes the digests in order, compares, writes. No hasher installed, or
+  // a part refused: sha1_mb as before.
+  void set_gpu(bool on);
   void attach(int fd, uint64_t id, const std::string& prefix);
   size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
   size_t pending_out(uint64_t id);
@@ -256,6 +265,10 @@ class SwarmWire {
   bool servable(uint32_t idx, uint32_t begin, uint32_t len);
   bool serve_block(Conn& c, const std::string& req);
   bool send_all(Conn& c, const char* p, size_t n, int flags);
+  void finish_piece(const Piece& p, const uint8_t* dig);   // compare, write, report
+  void gpu_loop();
+  uint8_t* take_buffer(size_t n, const void** reg);
+  void give_buffer(uint8_t* b, size_t n, const void* reg);
 
   std::mutex mu_;                               // pieces_, geometry, stats_
   int64_t piece_length_ = 0, total_ = 0;
@@ -263,6 +276,15 @@ class SwarmWire {
   std::vector<std::pair<int, int64_t>> files_;
   std::unordered_map<uint32_t, std::shared_ptr<Piece>> pieces_;
   std::vector<uint8_t> have_;                   // bitfield (BEP-3 bit order)
+  std::atomic<bool> gpu_{false};
+  std::mutex pmu_;                              // piece buffer pool (GPU mode)
+  std::vector<std::pair<uint8_t*, const void*>> pool_;   // idle buffers, their hasher
+  size_t pool_cap_ = 0, pool_total_ = 0;
+  std::mutex gmu_;
+  std::condition_variable gcv_;
+  std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order
+  bool gstop_ = false;
+  std::thread gthread_;
   std::atomic<uint64_t> served_bytes_{0};
   uint64_t epoch_ = 0;
   SwarmWireStats stats_;

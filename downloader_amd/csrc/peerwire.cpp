@@ -19,6 +19,7 @@
 //     through user space; Python only decides who is unchoked).
 // Events reach the event loop through an eventfd, like gpu_part_poll.
 #include "native.h"
+#include "gpu_part_api.h"
 
 #include <poll.h>
 #include <pthread.h>
@@ -64,10 +65,17 @@ void put32(std::string& s, uint32_t v) {
 struct SwarmWire::Piece {
   uint32_t idx = 0;
   uint32_t size = 0, nblocks = 0;
-  std::unique_ptr<uint8_t[]> buf;
+  uint8_t* data = nullptr;               // heap, or a pooled page-locked buffer (GPU mode)
+  size_t cap = 0;
+  const void* reg = nullptr;             // hasher API the pooled buffer is page-locked for
+  SwarmWire* pool = nullptr;             // owner of a pooled buffer
   std::vector<uint8_t> claimed;          // per block: taken by a reader (under mu_)
   std::atomic<uint32_t> filled{0};       // blocks copied in
   uint64_t epoch = 0;                    // begin_piece generation (a re-begun piece is new)
+  ~Piece() {
+    if (pool) pool->give_buffer(data, cap, reg);
+    else free(data);
+  }
 };
 
 struct SwarmWire::Conn {
@@ -98,6 +106,8 @@ SwarmWire::SwarmWire(int verify_threads) {
     verifiers_.emplace_back([this] { verify_loop(); });
     pthread_setname_np(verifiers_.back().native_handle(), "wire-verify");
   }
+  gthread_ = std::thread([this] { gpu_loop(); });
+  pthread_setname_np(gthread_.native_handle(), "wire-gpu");
 }
 
 SwarmWire::~SwarmWire() { close(); }
@@ -117,6 +127,23 @@ void SwarmWire::close() {
   for (auto& t : verifiers_)
     if (t.joinable()) t.join();
   verifiers_.clear();
+  {
+    std::lock_guard<std::mutex> g(gmu_);
+    gstop_ = true;
+  }
+  gcv_.notify_all();
+  if (gthread_.joinable()) gthread_.join();   // after the verifiers: nothing submits any more
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    pieces_.clear();                        // their pooled buffers go back before the pool
+  }
+  std::lock_guard<std::mutex> g(pmu_);
+  for (auto& b : pool_) {
+    if (b.second) ((const GpuPartHashApi*)b.second)->unreg(((const GpuPartHashApi*)b.second)->ctx, b.first);
+    free(b.first);
+  }
+  pool_total_ -= pool_.size();
+  pool_.clear();
   if (efd_ >= 0) {
     ::close(efd_);
     efd_ = -1;
@@ -169,7 +196,15 @@ void SwarmWire::begin_piece(uint32_t idx) {
   p->idx = idx;
   p->size = piece_size(idx);
   p->nblocks = (p->size + kBlock - 1) / kBlock;
-  p->buf.reset(new uint8_t[p->size]);
+  if (gpu_.load()) {                      // pooled: page-locked once, reused
+    p->cap = ((size_t)piece_length_ + 4095) & ~(size_t)4095;
+    p->data = take_buffer(p->cap, &p->reg);
+    p->pool = this;
+  } else {
+    p->cap = p->size;
+    p->data = (uint8_t*)malloc(std::max<size_t>(1, p->size));
+    if (!p->data) throw std::bad_alloc();
+  }
   p->claimed.assign(p->nblocks, 0);
   p->epoch = ++epoch_;
   pieces_[idx] = std::move(p);          // a re-begun piece (failed its check) starts over
@@ -203,7 +238,7 @@ int SwarmWire::take_block(uint32_t idx, uint32_t begin, const uint8_t* p, uint32
     stats_.blocks++;
     stats_.block_bytes += len;
   }
-  memcpy(pc->buf.get() + begin, p, len);   // outside the lock: readers copy in parallel
+  memcpy(pc->data + begin, p, len);        // outside the lock: readers copy in parallel
   const uint32_t f = pc->filled.fetch_add(1, std::memory_order_acq_rel) + 1;
   if (f < pc->nblocks) return 1;
   {
@@ -229,8 +264,8 @@ void SwarmWire::verify_loop() {
       // sha1_mb costs the same for 1 lane as for 16: let more pieces complete (at 4 GB/s a
       // 4 MiB piece completes every ~1 ms) before hashing a short batch - a piece's HAVE is
       // late by at most this much (system_clock: steady-clock waits are invisible to GCC 11's
-      // TSan, part_dispatch.h)
-      if (vq_.size() < 16 && !vstop_)
+      // TSan, part_dispatch.h). The GPU batches by itself: no wait there.
+      if (vq_.size() < 16 && !vstop_ && !gpu_.load())
         vcv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(20),
                         [&] { return vstop_ || vq_.size() >= 16; });
       while (!vq_.empty() && batch.size() < 16) {
@@ -238,18 +273,44 @@ void SwarmWire::verify_loop() {
         vq_.pop_front();
       }
     }
+    // GPU mode: submit each piece to the installed hasher, the collector finishes it
+    const GpuPartHashApi* api =
+        gpu_.load() ? (const GpuPartHashApi*)gpu_part_hasher_current() : nullptr;
+    std::vector<std::shared_ptr<Piece>> host;
+    for (auto& p : batch) {
+      uint64_t t = 0;
+      if (api && p->pool) {
+        if (p->reg != api) {
+          if (p->reg) ((const GpuPartHashApi*)p->reg)->unreg(((const GpuPartHashApi*)p->reg)->ctx, p->data);
+          p->reg = api->reg(api->ctx, p->data, p->cap) == 0 ? api : nullptr;
+        }
+        if (p->reg == api) t = api->submit(api->ctx, p->data, p->size, p->size);
+      }
+      if (t) {
+        std::lock_guard<std::mutex> g(gmu_);
+        gq_.push_back({std::move(p), t});
+        gcv_.notify_one();
+      } else {
+        if (api) {
+          std::lock_guard<std::mutex> g(mu_);
+          stats_.gpu_refused++;
+        }
+        host.push_back(std::move(p));
+      }
+    }
+    if (host.empty()) continue;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<const uint8_t*> ptrs;
     std::vector<size_t> lens;
-    for (auto& p : batch) {
-      ptrs.push_back(p->buf.get());
+    for (auto& p : host) {
+      ptrs.push_back(p->data);
       lens.push_back(p->size);
     }
-    std::string dig(batch.size() * 20, '\0');
-    if (sha1_mb_supported() && batch.size() >= 4) {   // below 4 lanes one SHA-NI chain each wins
-      sha1_mb(ptrs.data(), lens.data(), batch.size(), (uint8_t*)&dig[0]);
+    std::string dig(host.size() * 20, '\0');
+    if (sha1_mb_supported() && host.size() >= 4) {   // below 4 lanes one SHA-NI chain each wins
+      sha1_mb(ptrs.data(), lens.data(), host.size(), (uint8_t*)&dig[0]);
     } else {
-      for (size_t i = 0; i < batch.size(); ++i) {
+      for (size_t i = 0; i < host.size(); ++i) {
         std::string d = digest("sha1", ptrs[i], lens[i]);
         memcpy(&dig[i * 20], d.data(), 20);
       }
@@ -260,45 +321,116 @@ void SwarmWire::verify_loop() {
       stats_.verify_batches++;
       stats_.sha_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     }
-    for (size_t i = 0; i < batch.size(); ++i) {
-      Piece& p = *batch[i];
-      bool ok;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        ok = memcmp(&dig[i * 20], hashes_.data() + (size_t)p.idx * 20, 20) == 0;
-      }
-      std::string err;
-      if (ok) {
-        const auto w0 = std::chrono::steady_clock::now();
-        err = write_piece(p);
-        std::lock_guard<std::mutex> g(mu_);
-        stats_.write_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-            std::chrono::steady_clock::now() - w0).count();
-      }
-      std::string ev;
-      put32(ev, p.idx);
-      ev.push_back(ok ? (err.empty() ? 1 : 2) : 0);   // 1 verified + written, 0 bad, 2 I/O
-      ev += err;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        if (ok && err.empty()) {
-          stats_.verified++;
-          if (have_.size() <= p.idx / 8) have_.resize(p.idx / 8 + 1, 0);
-          have_[p.idx / 8] |= (uint8_t)(0x80 >> (p.idx % 8));   // servable from now on
-        } else if (!ok) {
-          stats_.hash_fails++;
-        }
-      }
-      push(0, kEvPiece, std::move(ev));
+    for (size_t i = 0; i < host.size(); ++i) finish_piece(*host[i], (const uint8_t*)&dig[i * 20]);
+  }
+}
+
+// The GPU's digests, in submission order (the device hashes them in parallel anyway).
+void SwarmWire::gpu_loop() {
+  for (;;) {
+    std::pair<std::shared_ptr<Piece>, uint64_t> job;
+    {
+      std::unique_lock<std::mutex> lk(gmu_);
+      gcv_.wait(lk, [&] { return gstop_ || !gq_.empty(); });
+      if (gq_.empty()) return;
+      job = std::move(gq_.front());
+      gq_.pop_front();
+    }
+    Piece& p = *job.first;
+    const GpuPartHashApi* api = (const GpuPartHashApi*)p.reg;
+    uint8_t dig[20];
+    char err[256] = {0};
+    if (api->wait(api->ctx, job.second, GPU_PART_DONE, dig, sizeof dig, err, sizeof err) != 0) {
+      // the device failed: the bytes are still in the buffer - hash them here
+      std::string d = digest("sha1", p.data, p.size);
+      memcpy(dig, d.data(), 20);
+      std::lock_guard<std::mutex> g(mu_);
+      stats_.gpu_errors++;
+    } else {
+      std::lock_guard<std::mutex> g(mu_);
+      stats_.gpu_pieces++;
+    }
+    finish_piece(p, dig);
+  }
+}
+
+void SwarmWire::finish_piece(const Piece& p, const uint8_t* dig) {
+  bool ok;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ok = memcmp(dig, hashes_.data() + (size_t)p.idx * 20, 20) == 0;
+  }
+  std::string err;
+  if (ok) {
+    const auto w0 = std::chrono::steady_clock::now();
+    err = write_piece(p);
+    std::lock_guard<std::mutex> g(mu_);
+    stats_.write_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+        std::chrono::steady_clock::now() - w0).count();
+  }
+  std::string ev;
+  put32(ev, p.idx);
+  ev.push_back(ok ? (err.empty() ? 1 : 2) : 0);   // 1 verified + written, 0 bad, 2 I/O
+  ev += err;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (ok && err.empty()) {
+      stats_.verified++;
+      if (have_.size() <= p.idx / 8) have_.resize(p.idx / 8 + 1, 0);
+      have_[p.idx / 8] |= (uint8_t)(0x80 >> (p.idx % 8));   // servable from now on
+    } else if (!ok) {
+      stats_.hash_fails++;
     }
   }
+  push(0, kEvPiece, std::move(ev));
+}
+
+void SwarmWire::set_gpu(bool on) { gpu_.store(on); }
+
+uint8_t* SwarmWire::take_buffer(size_t n, const void** reg) {
+  {
+    std::lock_guard<std::mutex> g(pmu_);
+    if (pool_cap_ != n) {                 // geometry changed (set_storage): start over
+      for (auto& b : pool_) {
+        if (b.second) ((const GpuPartHashApi*)b.second)->unreg(((const GpuPartHashApi*)b.second)->ctx, b.first);
+        free(b.first);
+      }
+      pool_total_ -= pool_.size();
+      pool_.clear();
+      pool_cap_ = n;
+    }
+    if (!pool_.empty()) {
+      auto b = pool_.back();
+      pool_.pop_back();
+      *reg = b.second;
+      return b.first;
+    }
+    pool_total_++;
+  }
+  void* b = aligned_alloc(4096, n);
+  if (!b) throw std::bad_alloc();
+  *reg = nullptr;
+  return (uint8_t*)b;
+}
+
+void SwarmWire::give_buffer(uint8_t* b, size_t n, const void* reg) {
+  {
+    std::lock_guard<std::mutex> g(pmu_);
+    if (n == pool_cap_ && pool_.size() < 96) {   // ~400 MB of 4 MiB pieces kept locked
+      pool_.push_back({b, reg});
+      return;
+    }
+    pool_total_--;
+  }
+  if (reg) ((const GpuPartHashApi*)reg)->unreg(((const GpuPartHashApi*)reg)->ctx, b);
+  free(b);
 }
 
 // The piece's bytes into the files it spans (pwrite; the storage owns the fds).
 std::string SwarmWire::write_piece(const Piece& p) {
   int64_t off = (int64_t)p.idx * piece_length_;
   int64_t left = p.size;
-  const uint8_t* src = p.buf.get();
+  const uint8_t* src = p.data;
   int64_t fstart = 0;
   std::vector<std::pair<int, int64_t>> files;
   {
@@ -619,6 +751,10 @@ SwarmWireStats SwarmWire::stats() {
   s.rx_bytes = rx_bytes_.load();
   s.recvs = recvs_.load();
   s.served_bytes = served_bytes_.load();
+  {
+    std::lock_guard<std::mutex> g2(pmu_);
+    s.pool_buffers = pool_total_;
+  }
   return s;
 }
 

@@ -495,8 +495,17 @@ static PartStressResult part_stress(const PartStress& cfg) {
 // for the same 24 pieces in random order, split at random points, with duplicates, a bogus
 // block, control messages in between and one corrupt copy of a piece on one connection;
 // every piece must be verified once, written to the two storage files, and reported.
-static void wire_section() {
+static void wire_section(bool gpu) {
   const int64_t plen = 65536, total = 24 * plen - 1000;      // short last piece
+  // gpu: pieces verified on a GPU part hasher - PartDispatcher over the fake device, the
+  // state machine of the gfx950 PartHasher - from page-locked pooled buffers
+  std::unique_ptr<FakeHasher> hasher;
+  if (gpu) {
+    FakeDeviceKnobs k;
+    k.seed = 3;
+    hasher = fake_hasher(k);
+    set_gpu_part_hasher(hasher->api(), 8);
+  }
   auto data = rnd((size_t)total, 99);
   std::string hashes;
   for (int64_t off = 0; off < total; off += plen)
@@ -505,6 +514,7 @@ static void wire_section() {
   int f1 = mkstemp(p1), f2 = mkstemp(p2);
   const int64_t n1 = 500000, n2 = total - n1;                 // pieces straddle the files
   SwarmWire w(2);
+  w.set_gpu(gpu);
   w.set_storage(plen, total, hashes, {{f1, n1}, {f2, n2}});
   const int npieces = (int)((total + plen - 1) / plen);
   for (int i = 0; i < npieces; ++i) w.begin_piece((uint32_t)i);
@@ -595,7 +605,13 @@ static void wire_section() {
   CHECK(msgs > 0 && blocks_taken >= (uint64_t)(npieces * 4));
   SwarmWireStats st = w.stats();
   CHECK(bad == 1 && st.verified == (uint64_t)npieces && st.hash_fails == 1);
+  if (gpu) CHECK(st.gpu_pieces == (uint64_t)npieces + 1 && st.gpu_errors == 0);
   w.close();
+  CHECK(w.stats().pool_buffers == 0);
+  if (gpu) {
+    set_gpu_part_hasher(nullptr, 0);
+    hasher.reset();
+  }
   std::vector<uint8_t> back((size_t)total);
   CHECK(pread(f1, back.data(), (size_t)n1, 0) == n1);
   CHECK(pread(f2, back.data() + n1, (size_t)n2, 0) == n2);
@@ -605,7 +621,8 @@ static void wire_section() {
   close(f2);
   unlink(p1);
   unlink(p2);
-  fprintf(stderr, "wire: %d pieces verified, %d corrupt copies refused\n", done, bad);
+  fprintf(stderr, "wire%s: %d pieces verified, %d corrupt copies refused\n",
+          gpu ? " (gpu hasher)" : "", done, bad);
 }
 
 static void stress_sections() {
@@ -656,7 +673,8 @@ static void stress_sections() {
 int main() {
   signal(SIGPIPE, SIG_IGN);
   if (getenv("SELFTEST_ONLY") && strcmp(getenv("SELFTEST_ONLY"), "wire") == 0) {
-    wire_section();
+    wire_section(false);
+    wire_section(true);
     printf(g_fail ? "selftest: failures\n" : "selftest ok\n");
     return g_fail ? 1 : 0;
   }
@@ -1012,7 +1030,8 @@ int main() {
     set_gpu_part_hasher(nullptr, 0);
   }
   stress_sections();
-  wire_section();
+  wire_section(false);
+  wire_section(true);
   {
     RelayPoolStats st = relay_pool_stats();
     CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);

@@ -1580,6 +1580,8 @@ void gpu_notify(void* arg, uint64_t ticket, int phase) {
 }
 }  // namespace
 
+const void* gpu_part_hasher_current() { return g_gpu_api.load(); }
+
 void set_gpu_part_hasher(const void* api, int min_pieces) {
   const GpuPartHashApi* a = (const GpuPartHashApi*)api;
   if (a && a->abi != GPU_PART_API_ABI) throw std::invalid_argument("gpu_part_api ABI mismatch");

@@ -32,7 +32,8 @@ class TorrentClient:
                  webseed_max_failures: int = 5,
                  idle_timeout: float = 120.0, connect_timeout: float = 10.0,
                  seed_after_done: bool = False, listen: bool = True,
-                 native_wire: bool = True, wire_verify_threads: int = 2):
+                 native_wire: bool = True, wire_verify_threads: int = 2,
+                 swarm_verify: str = "auto"):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -61,6 +62,7 @@ class TorrentClient:
         # peer connections handed to the native wire after the handshake (csrc/peerwire.cpp)
         self.native_wire = native_wire
         self.wire_verify_threads = wire_verify_threads
+        self.swarm_verify = swarm_verify          # auto / gpu / cpu (native wire only)
         self.pex_interval = 60.0
         self.piece_cache_bytes = 64 << 20   # per-session LRU of pieces being served to peers
         self.dht_interval = 30.0
@@ -83,6 +85,7 @@ class TorrentClient:
                    webseed_verify_depth_gpu=d.webseed_verify_depth_gpu,
                    verify_threads=d.verify_threads,
                    native_wire=d.torrent_native_wire,
+                   swarm_verify=d.swarm_verify_backend,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

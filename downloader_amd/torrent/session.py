@@ -481,6 +481,18 @@ class TorrentSession:
         self.verified_bytes = sum(meta.piece_size(i) for i in range(meta.num_pieces)
                                   if i in self.have)
         self.picker = PiecePicker(meta, self.have)
+        if self.wire is not None and self.client.swarm_verify in ("auto", "gpu") \
+                and meta.num_pieces > 1:
+            # swarm pieces SHA-1'd by the gfx950 PartHasher (set up once per worker, off the
+            # loop); without a usable device the host multi-buffer SHA-1 does it
+            try:
+                on = await loop.run_in_executor(None, hashing.gpu_relay_hashing)
+            except Exception:
+                on = False
+            if not on and self.client.swarm_verify == "gpu":
+                raise TorrentError("swarm_verify_backend=gpu but no GPU part hasher")
+            self.wire.set_gpu(bool(on))
+            self.stats["swarm_verify"] = "gpu" if on else "cpu"
         if self.wire is not None:
             self.wire.set_storage(meta.piece_length, meta.total_length, meta.pieces,
                                   [(fd, n) for fd, (_, n) in zip(self.storage.fds,

@@ -273,6 +273,47 @@ def test_swarm_native_and_python_wire(run, tmp_path, native_wire):
     run(go(), timeout=90)
 
 
+def test_native_wire_pieces_verified_on_the_part_hasher(run, tmp_path):
+    """swarm_verify_backend=gpu: complete pieces go from page-locked pooled buffers to the
+    installed GPU part hasher (here its host double, the same C ABI as the gfx950 PartHasher),
+    the digests come back in order and every piece is verified and written; a corrupt piece
+    is caught from the device's digest."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 900_000, "b.mkv": 300_001})
+        p = src / "Pack" / "a.mkv"
+        b = bytearray(p.read_bytes())
+        b[100_000] ^= 0xFF                       # piece 3 served corrupt by this seeder
+        p.write_bytes(bytes(b))
+        good = await TorrentClient().start()
+        gdir = tmp_path / "good"
+        (gdir / "Pack").mkdir(parents=True)
+        for rel, d in data.items():
+            (gdir / "Pack" / rel).write_bytes(d)
+        await good.add_torrent(parse_torrent(raw), str(gdir))
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=64).start()
+        meta = parse_torrent(raw)
+        s = await leech.add_torrent(meta, str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.sleep(0.5)
+        s.add_peers([("127.0.0.1", good.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        st = s.wire.stats()
+        assert s.stats["swarm_verify"] == "gpu"
+        assert st["gpu_pieces"] >= meta.num_pieces and st["gpu_errors"] == 0
+        assert st["hash_fails"] >= 1 and st["verified"] == meta.num_pieces
+        await leech.close(); await seeder.close(); await good.close()
+        assert s.wire.stats()["pool_buffers"] == 0      # every pooled buffer freed at close
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.002), 4)
+    try:
+        run(go(), timeout=90)
+    finally:
+        hashing.use_part_hasher(None)
+
+
 def test_native_wire_bad_piece_is_refetched_and_peer_blamed(run, tmp_path):
     """A seeder serving a corrupt piece over the native wire: the native verifier rejects
     it (hash_fails), the session requeues it and gets it from the good seeder."""
