@@ -481,10 +481,14 @@ class TorrentSession:
         self.verified_bytes = sum(meta.piece_size(i) for i in range(meta.num_pieces)
                                   if i in self.have)
         self.picker = PiecePicker(meta, self.have)
-        if self.wire is not None and self.client.swarm_verify in ("auto", "gpu") \
-                and meta.num_pieces > 1:
+        want_gpu = self.client.swarm_verify == "gpu" or (
+            self.client.swarm_verify == "auto" and hashing.auto_may_use_gpu())
+        if self.wire is not None and want_gpu and meta.num_pieces > 1:
             # swarm pieces SHA-1'd by the gfx950 PartHasher (set up once per worker, off the
-            # loop); without a usable device the host multi-buffer SHA-1 does it
+            # loop). `auto` only where the host lacks the AVX-512 multi-buffer SHA-1: config 6
+            # (2 GB, 4 seeders) on the MI355X box ran 6.2 - 6.3 GB/s verified on the host vs
+            # 2.5 - 2.8 GB/s on the device, whose ~75 ms per-piece latency lands on a job that
+            # short (profiles/r5/swarm/)
             try:
                 on = await loop.run_in_executor(None, hashing.gpu_relay_hashing)
             except Exception:

@@ -245,9 +245,10 @@ class DownloadConfig(BaseModel):
     # peer connections framed, assembled, SHA-1'd (16 pieces at a time) and written by the
     # native wire after the handshake (csrc/peerwire.cpp); False: all in Python (peer.py)
     torrent_native_wire: bool = True
-    # SHA-1 of swarm pieces on the native wire: "gpu" / "auto" = the gfx950 PartHasher (set up
-    # once per worker; auto falls back to the host without a HIP device), "cpu" = the host
-    # multi-buffer SHA-1 (16 pieces at a time)
+    # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
+    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the host
+    # when it has the AVX-512 multi-buffer SHA-1, else the device. Config 6 (2 GB, 4 seeders):
+    # 6.2 - 6.3 GB/s on the host vs 2.5 - 2.8 on the device (profiles/r5/swarm/)
     swarm_verify_backend: str = "auto"
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
