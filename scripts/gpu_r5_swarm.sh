@@ -7,7 +7,7 @@
 # per-thread split. GPU tier first (the wire's GPU mode shares the PartHasher).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm}
+F=${OUT:-gpurun_out/r5_swarm4}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
