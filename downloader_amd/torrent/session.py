@@ -635,28 +635,40 @@ class TorrentSession:
                 pc._wq.put_nowait((kind, data))
 
     def _wire_blocks(self, pc: PeerConn, data: bytes) -> None:
+        """Book one batch of arrivals (16-byte records: piece, begin, length, status). The
+        per-block work is what the Python wire did minus the copy and the framing: ~1.6 us a
+        block, 0.1 CPU-s per GB (profiles/r5/swarm/)."""
         picker = self.picker
-        inflight = pc.inflight
+        if picker is None:
+            return
+        inflight_pop = pc.inflight.pop
+        active_get = picker.active.get
         me = id(pc)
+        got_bytes = 0
+        last_idx, ap = -1, None
         for idx, begin, ln, st in struct.iter_unpack(">IIII", data):
-            inflight.pop((idx, begin), None)
-            if not st or picker is None:
+            inflight_pop((idx, begin), None)
+            if not st:
                 continue
-            self.downloaded += ln
-            pc.down_bytes += ln
-            ap = picker.active.get(idx)
+            got_bytes += ln
+            if idx != last_idx:                    # blocks of one piece come in runs
+                last_idx, ap = idx, active_get(idx)
+                if ap is not None:
+                    ap.peers.add(me)
             if ap is None:
                 continue
-            b = begin // BLOCK
+            b = begin >> 14                        # BLOCK = 16 KiB
             if ap.state[b] != 2:
                 ap.state[b] = 2
                 ap.got += 1
-            ap.peers.add(me)
             rs = ap.req.pop(b, None)
             if rs is not None and (len(rs) > 1 or me not in rs):     # endgame duplicates
                 pc._wq.put_nowait((EV_CANCEL_DUPS, (rs, idx, begin, ln)))
             if st == 2 and picker.complete_blocks(idx):
                 self._verifying_ap[idx] = ap          # verified + written natively
+                last_idx, ap = -1, None
+        self.downloaded += got_bytes
+        pc.down_bytes += got_bytes
         if not pc.fill_queued and self.refill_due(pc):
             pc.fill_queued = True
             pc._wq.put_nowait((EV_FILL, None))
