@@ -496,27 +496,45 @@ async def config_swarm(a) -> Dict:
             ports = []
             for _, conn in procs:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
+        verify = getattr(a, "swarm_verify", "auto")
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire,
-                                    swarm_verify=getattr(a, "swarm_verify", "auto")).start()
-        threads0 = _thread_cpu(0)
-        cpu0 = _self_cpu()
-        t0 = time.perf_counter()
-        s = await leech.add_torrent(meta, dst, peers=[("127.0.0.1", port) for port in ports])
-        await asyncio.wait_for(s.wait(), 1800)
-        dt = time.perf_counter() - t0
-        cpu_s = _self_cpu() - cpu0
-        # where the leecher's CPU went (before close: the wire's threads still exist)
-        per_thread = _thread_cpu_delta(threads0, _thread_cpu(0))
+                                    swarm_verify=verify).start()
+        if wire and verify == "gpu":
+            # a worker sets its GPU up at start (download.gpu_prewarm), not inside a job
+            from downloader_amd.ops import hashing
+            await asyncio.get_running_loop().run_in_executor(None, hashing.gpu_relay_hashing)
+        # --reps K: the torrent downloaded K times by the same leecher (fresh directories, a
+        # new session each); the first is the process' cold one (pools, page locking), the
+        # last is reported in full
+        runs = []
+        for k in range(max(1, getattr(a, "reps", 1) or 1)):
+            d = os.path.join(dst, f"r{k}")
+            threads0 = _thread_cpu(0)
+            cpu0 = _self_cpu()
+            t0 = time.perf_counter()
+            s = await leech.add_torrent(meta, d, peers=[("127.0.0.1", port) for port in ports])
+            await asyncio.wait_for(s.wait(), 1800)
+            dt = time.perf_counter() - t0
+            cpu_s = _self_cpu() - cpu0
+            # where the leecher's CPU went (before close: the wire's threads still exist)
+            per_thread = _thread_cpu_delta(threads0, _thread_cpu(0))
+            stats = s.wire.stats() if s.wire is not None else None
+            runs.append((dt, cpu_s, per_thread, stats, s))
+            await leech.remove(s)
+            shutil.rmtree(d, ignore_errors=True)
+        dt, cpu_s, per_thread, stats, s = runs[-1]
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
                "wire": "native" if s.wire is not None else "python",
                "swarm_verify": s.stats.get("swarm_verify", "python"),
-               **({"wire_stats": s.wire.stats()} if s.wire is not None else {}),
+               **({"wire_stats": stats} if stats is not None else {}),
                "seeders_in_process": bool(seeders), "seeder_procs": len(procs),
                "piece_len": a.piece_mb << 20,
                "s": round(dt, 3), "MBps": round(total / dt / MB, 1),
                "leech_cpu_s": round(cpu_s, 2), "hash_fails": s.stats["hash_fails"],
                "leech_cpu_s_per_GB": round(cpu_s / (total / 1e9), 3),
-               "leech_thread_cpu": per_thread}
+               "leech_thread_cpu": per_thread,
+               "reps": len(runs), "MBps_reps": [round(total / r[0] / MB, 1) for r in runs],
+               "leech_cpu_s_per_GB_reps": [round(r[1] / (total / 1e9), 3) for r in runs]}
         await leech.close()
         return out
     finally:

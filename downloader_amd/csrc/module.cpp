@@ -296,7 +296,8 @@ PYBIND11_MODULE(_native, m) {
              d["gpu_pieces"] = s.gpu_pieces;
              d["gpu_refused"] = s.gpu_refused;
              d["gpu_errors"] = s.gpu_errors;
-             d["pool_buffers"] = s.pool_buffers;
+             d["pool_in_use"] = s.pool_in_use;      // process-wide piece buffers
+             d["pool_idle"] = s.pool_idle;
              return d;
            })
       .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());

@@ -219,7 +219,7 @@ struct SwarmWireStats {
                                                             // writing
   uint64_t served_bytes = 0;                                // blocks served with sendfile
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
-  size_t pool_buffers = 0;                                  // page-locked piece buffers
+  size_t pool_in_use = 0, pool_idle = 0;                    // process-wide piece buffers
   size_t active_pieces = 0;
 };
 class SwarmWire {
@@ -267,8 +267,6 @@ class SwarmWire {
   bool send_all(Conn& c, const char* p, size_t n, int flags);
   void finish_piece(const Piece& p, const uint8_t* dig);   // compare, write, report
   void gpu_loop();
-  uint8_t* take_buffer(size_t n, const void** reg);
-  void give_buffer(uint8_t* b, size_t n, const void* reg);
 
   std::mutex mu_;                               // pieces_, geometry, stats_
   int64_t piece_length_ = 0, total_ = 0;
@@ -277,9 +275,6 @@ class SwarmWire {
   std::unordered_map<uint32_t, std::shared_ptr<Piece>> pieces_;
   std::vector<uint8_t> have_;                   // bitfield (BEP-3 bit order)
   std::atomic<bool> gpu_{false};
-  std::mutex pmu_;                              // piece buffer pool (GPU mode)
-  std::vector<std::pair<uint8_t*, const void*>> pool_;   // idle buffers, their hasher
-  size_t pool_cap_ = 0, pool_total_ = 0;
   std::mutex gmu_;
   std::condition_variable gcv_;
   std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order

@@ -60,21 +60,73 @@ void put32(std::string& s, uint32_t v) {
   s.append(b, 4);
 }
 
+// Piece buffers, process-wide: reused across pieces and sessions (no page faults per piece),
+// and in GPU mode page-locked once for the hasher (hipHostRegister costs milliseconds per 4 MiB
+// buffer - paid per session, it landed inside short jobs). Never destroyed: pieces may be
+// released by a wire's threads during interpreter shutdown.
+struct PiecePool {
+  std::mutex mu;
+  std::unordered_map<size_t, std::vector<std::pair<uint8_t*, const void*>>> idle;
+  size_t in_use = 0, idle_count = 0;
+  static constexpr size_t kMaxIdle = 128;   // ~512 MiB of 4 MiB pieces kept
+
+  uint8_t* take(size_t n, const void** reg) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      in_use++;
+      auto it = idle.find(n);
+      if (it != idle.end() && !it->second.empty()) {
+        auto b = it->second.back();
+        it->second.pop_back();
+        idle_count--;
+        *reg = b.second;
+        return b.first;
+      }
+    }
+    void* b = aligned_alloc(4096, n);
+    if (!b) {
+      std::lock_guard<std::mutex> g(mu);
+      in_use--;
+      throw std::bad_alloc();
+    }
+    *reg = nullptr;
+    return (uint8_t*)b;
+  }
+  void give(uint8_t* b, size_t n, const void* reg) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      in_use--;
+      // a buffer locked for a hasher no longer installed goes (the API stays valid: retired
+      // hashers are kept alive, ops/hashing.py)
+      if (idle_count < kMaxIdle && (!reg || reg == gpu_part_hasher_current())) {
+        idle[n].push_back({b, reg});
+        idle_count++;
+        return;
+      }
+    }
+    if (reg) ((const GpuPartHashApi*)reg)->unreg(((const GpuPartHashApi*)reg)->ctx, b);
+    free(b);
+  }
+};
+
+PiecePool& piece_pool() {
+  static PiecePool* p = new PiecePool();
+  return *p;
+}
+
 }  // namespace
 
 struct SwarmWire::Piece {
   uint32_t idx = 0;
   uint32_t size = 0, nblocks = 0;
-  uint8_t* data = nullptr;               // heap, or a pooled page-locked buffer (GPU mode)
+  uint8_t* data = nullptr;               // from the process-wide PiecePool
   size_t cap = 0;
-  const void* reg = nullptr;             // hasher API the pooled buffer is page-locked for
-  SwarmWire* pool = nullptr;             // owner of a pooled buffer
+  const void* reg = nullptr;             // hasher API the buffer is page-locked for (GPU mode)
   std::vector<uint8_t> claimed;          // per block: taken by a reader (under mu_)
   std::atomic<uint32_t> filled{0};       // blocks copied in
   uint64_t epoch = 0;                    // begin_piece generation (a re-begun piece is new)
   ~Piece() {
-    if (pool) pool->give_buffer(data, cap, reg);
-    else free(data);
+    if (data) piece_pool().give(data, cap, reg);
   }
 };
 
@@ -137,13 +189,7 @@ void SwarmWire::close() {
     std::lock_guard<std::mutex> g(mu_);
     pieces_.clear();                        // their pooled buffers go back before the pool
   }
-  std::lock_guard<std::mutex> g(pmu_);
-  for (auto& b : pool_) {
-    if (b.second) ((const GpuPartHashApi*)b.second)->unreg(((const GpuPartHashApi*)b.second)->ctx, b.first);
-    free(b.first);
-  }
-  pool_total_ -= pool_.size();
-  pool_.clear();
+  // (piece buffers go back to the process-wide pool, kept for the next session)
   if (efd_ >= 0) {
     ::close(efd_);
     efd_ = -1;
@@ -199,8 +245,7 @@ void SwarmWire::begin_piece(uint32_t idx) {
   // pooled and reused: a fresh 4 MiB buffer per piece cost ~1,000 page faults in the reader
   // that first writes it; in GPU mode the pool's buffers are also page-locked once
   p->cap = ((size_t)piece_length_ + 4095) & ~(size_t)4095;
-  p->data = take_buffer(p->cap, &p->reg);
-  p->pool = this;
+  p->data = piece_pool().take(p->cap, &p->reg);
   p->claimed.assign(p->nblocks, 0);
   p->epoch = ++epoch_;
   pieces_[idx] = std::move(p);          // a re-begun piece (failed its check) starts over
@@ -275,7 +320,7 @@ void SwarmWire::verify_loop() {
     std::vector<std::shared_ptr<Piece>> host;
     for (auto& p : batch) {
       uint64_t t = 0;
-      if (api && p->pool) {
+      if (api) {
         if (p->reg != api) {
           if (p->reg) ((const GpuPartHashApi*)p->reg)->unreg(((const GpuPartHashApi*)p->reg)->ctx, p->data);
           p->reg = api->reg(api->ctx, p->data, p->cap) == 0 ? api : nullptr;
@@ -383,44 +428,6 @@ void SwarmWire::finish_piece(const Piece& p, const uint8_t* dig) {
 
 void SwarmWire::set_gpu(bool on) { gpu_.store(on); }
 
-uint8_t* SwarmWire::take_buffer(size_t n, const void** reg) {
-  {
-    std::lock_guard<std::mutex> g(pmu_);
-    if (pool_cap_ != n) {                 // geometry changed (set_storage): start over
-      for (auto& b : pool_) {
-        if (b.second) ((const GpuPartHashApi*)b.second)->unreg(((const GpuPartHashApi*)b.second)->ctx, b.first);
-        free(b.first);
-      }
-      pool_total_ -= pool_.size();
-      pool_.clear();
-      pool_cap_ = n;
-    }
-    if (!pool_.empty()) {
-      auto b = pool_.back();
-      pool_.pop_back();
-      *reg = b.second;
-      return b.first;
-    }
-    pool_total_++;
-  }
-  void* b = aligned_alloc(4096, n);
-  if (!b) throw std::bad_alloc();
-  *reg = nullptr;
-  return (uint8_t*)b;
-}
-
-void SwarmWire::give_buffer(uint8_t* b, size_t n, const void* reg) {
-  {
-    std::lock_guard<std::mutex> g(pmu_);
-    if (n == pool_cap_ && pool_.size() < 96) {   // ~400 MB of 4 MiB pieces kept locked
-      pool_.push_back({b, reg});
-      return;
-    }
-    pool_total_--;
-  }
-  if (reg) ((const GpuPartHashApi*)reg)->unreg(((const GpuPartHashApi*)reg)->ctx, b);
-  free(b);
-}
 
 // The piece's bytes into the files it spans (pwrite; the storage owns the fds).
 std::string SwarmWire::write_piece(const Piece& p) {
@@ -748,8 +755,10 @@ SwarmWireStats SwarmWire::stats() {
   s.recvs = recvs_.load();
   s.served_bytes = served_bytes_.load();
   {
-    std::lock_guard<std::mutex> g2(pmu_);
-    s.pool_buffers = pool_total_;
+    PiecePool& pp = piece_pool();
+    std::lock_guard<std::mutex> g2(pp.mu);
+    s.pool_in_use = pp.in_use;
+    s.pool_idle = pp.idle_count;
   }
   return s;
 }

@@ -607,7 +607,7 @@ static void wire_section(bool gpu) {
   CHECK(bad == 1 && st.verified == (uint64_t)npieces && st.hash_fails == 1);
   if (gpu) CHECK(st.gpu_pieces == (uint64_t)npieces + 1 && st.gpu_errors == 0);
   w.close();
-  CHECK(w.stats().pool_buffers == 0);
+  CHECK(w.stats().pool_in_use == 0);   // every piece buffer back in the process-wide pool
   if (gpu) {
     set_gpu_part_hasher(nullptr, 0);
     hasher.reset();

@@ -305,7 +305,7 @@ def test_native_wire_pieces_verified_on_the_part_hasher(run, tmp_path):
         assert st["gpu_pieces"] >= meta.num_pieces and st["gpu_errors"] == 0
         assert st["hash_fails"] >= 1 and st["verified"] == meta.num_pieces
         await leech.close(); await seeder.close(); await good.close()
-        assert s.wire.stats()["pool_buffers"] == 0      # every pooled buffer freed at close
+        assert s.wire.stats()["pool_in_use"] == 0       # every piece buffer back in the pool
 
     hashing.use_part_hasher(native().CpuPartHasher(0.002), 4)
     try:
