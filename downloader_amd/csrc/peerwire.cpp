@@ -509,7 +509,16 @@ void SwarmWire::attach(int fd, uint64_t id, const std::string& prefix) {
 }
 
 void SwarmWire::read_loop(Conn& c) {
-  std::vector<uint8_t> buf((size_t)kMaxMsg + 64 + (1u << 20));
+  // room for the largest message plus a receive batch; not value-initialised, so a
+  // connection's pages are only touched as far as its data reaches (a vector zeroed all 3 MiB)
+  const size_t bufn = (size_t)kMaxMsg + 64 + (1u << 20);
+  std::unique_ptr<uint8_t[]> bufp(new uint8_t[bufn]);
+  struct {
+    uint8_t* d;
+    size_t n;
+    uint8_t* data() { return d; }
+    size_t size() const { return n; }
+  } buf{bufp.get(), bufn};
   size_t start = 0, end = 0;
   if (!c.prefix.empty()) {
     memcpy(buf.data(), c.prefix.data(), std::min(c.prefix.size(), buf.size()));
