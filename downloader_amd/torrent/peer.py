@@ -264,9 +264,10 @@ class PeerConn:
             if self.s.client.dht is not None and self.supports_dht:
                 await self.send(PORT, struct.pack(">H", self.s.client.dht.port))
             if self._wq is not None:
-                await self._run_wire()
-            while not self.closed:
-                await self._read_batch(read)
+                await self._run_wire()            # returns when the wire closed
+            else:
+                while not self.closed:
+                    await self._read_batch(read)
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.TimeoutError, OSError,
                 ProtocolError):
             pass

@@ -841,6 +841,42 @@ def test_malformed_remote_input_never_escapes(run, tmp_path):
     run(go())
 
 
+def test_native_wire_hostile_peer(run, tmp_path):
+    """Garbage over the native wire ends that connection only: a length prefix past 2 MiB is
+    refused by the native framer, PIECE messages for pieces nobody asked for are dropped, a
+    REQUEST while choked or for a piece out of range never reaches the storage; the seeder
+    keeps serving a well-behaved leecher."""
+    from downloader_amd.torrent.peer import handshake_bytes, read_handshake
+
+    async def go():
+        raw, data, seeder, _ = await _seed(tmp_path, {"x.mkv": 200_000})
+        m = parse_torrent(raw)
+        sess = seeder.sessions[m.info_hash]
+        assert sess.wire is not None
+        for bad in (struct.pack(">I", 0xFFFFFFF0) + b"x" * 64,              # oversize frame
+                    struct.pack(">IBII", 9 + 5, 7, 3, 0) + b"junk!" +      # unrequested PIECE
+                    struct.pack(">IBIII", 13, 6, 99, 0, 16384) +            # REQUEST, choked
+                    struct.pack(">IBIII", 13, 6, 0, 0, 1 << 30) +           # absurd length
+                    struct.pack(">I", 0xFFFFFFF0)):
+            r, w = await asyncio.open_connection("127.0.0.1", seeder.listen_port)
+            w.write(handshake_bytes(m.info_hash, b"-XX0001-" + b"1" * 12, True))
+            await read_handshake(r)
+            w.write(bad)
+            await w.drain()
+            got = await asyncio.wait_for(r.read(), 5)          # the seeder hangs up on us
+            assert struct.pack(">IB", 9 + 16384, 7) not in got   # nothing was served
+            w.close()
+        assert sess.error is None and not sess.failed.is_set()
+        assert sess.wire.stats()["served_bytes"] == 0
+        leech = await TorrentClient().start()
+        s = await leech.add_torrent(m, str(tmp_path / "dl"), peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 30)
+        _check(tmp_path / "dl", data)
+        assert sess.wire.stats()["served_bytes"] >= m.total_length
+        await leech.close(); await seeder.close()
+    run(go())
+
+
 def test_piece_picker_buckets_and_interest_counts():
     """Randomised check of the bucketed rarest-first picker against brute force: every piece
     started is a candidate of minimal availability among those the peer has; per-peer
