@@ -497,8 +497,9 @@ async def config_swarm(a) -> Dict:
             for _, conn in procs:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         verify = getattr(a, "swarm_verify", "auto")
+        native_req = getattr(a, "wire_requests", "native") == "native"
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire,
-                                    swarm_verify=verify).start()
+                                    swarm_verify=verify, wire_requests=native_req).start()
         if wire and verify == "gpu":
             # a worker sets its GPU up at start (download.gpu_prewarm), not inside a job
             from downloader_amd.ops import hashing
@@ -525,6 +526,8 @@ async def config_swarm(a) -> Dict:
         dt, cpu_s, per_thread, stats, s = runs[-1]
         out = {"config": "swarm", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
                "wire": "native" if s.wire is not None else "python",
+               "wire_requests": ("native" if native_req else "python") if s.wire is not None
+               else "python",
                "swarm_verify": s.stats.get("swarm_verify", "python"),
                **({"wire_stats": stats} if stats is not None else {}),
                "seeders_in_process": bool(seeders), "seeder_procs": len(procs),
@@ -659,6 +662,9 @@ def main(argv=None) -> int:
                     help="config 6: peer connections on the native wire (csrc/peerwire.cpp) or "
                          "framed in Python (torrent/peer.py), leecher and seeders alike")
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
+    ap.add_argument("--wire-requests", choices=["native", "python"], default="native",
+                    help="config 6, native wire: whole pieces requested by the wire itself, or "
+                         "every block requested and booked in Python")
     ap.add_argument("--seeder-procs", type=int, default=0,
                     help="config 6: processes the seeders run in (0: one per seeder)")
     ap.add_argument("--seed-inproc", action="store_true",

@@ -228,6 +228,38 @@ PYBIND11_MODULE(_native, m) {
            py::arg("piece_length"), py::arg("total"), py::arg("hashes"), py::arg("files"))
       .def("begin_piece", &SwarmWire::begin_piece, py::arg("idx"))
       .def("drop_piece", &SwarmWire::drop_piece, py::arg("idx"))
+      .def("set_pipeline", &SwarmWire::set_pipeline, py::arg("depth"))
+      .def("assign", &SwarmWire::assign, py::arg("conn_id"), py::arg("idx"),
+           "Own piece idx on the connection: the wire requests its blocks (returns the "
+           "connection's blocks still to request)")
+      .def("todo", &SwarmWire::todo, py::arg("conn_id"))
+      .def("release",
+           [](SwarmWire& w, uint64_t id) {
+             py::list out;
+             for (auto& r : w.release(id)) out.append(py::make_tuple(r.first, py::bytes(r.second)));
+             return out;
+           },
+           py::arg("conn_id"),
+           "[(idx, states)] of the pieces the connection owned, now ordinary (2 received, "
+           "1 requested and unanswered, 0 neither)")
+      .def("release_piece",
+           [](SwarmWire& w, uint32_t idx) -> py::object {
+             uint64_t owner = 0;
+             std::string st;
+             if (!w.release_piece(idx, &owner, &st)) return py::none();
+             return py::make_tuple(owner, py::bytes(st));
+           },
+           py::arg("idx"), "(owner, states) of an owned piece made ordinary, or None")
+      .def("rx_idle", &SwarmWire::rx_idle, py::arg("conn_id"))
+      .def("take_block",
+           [](SwarmWire& w, uint32_t idx, uint32_t begin, const py::buffer& b) {
+             py::buffer_info i = b.request();
+             return w.take_block(idx, begin, (const uint8_t*)i.ptr,
+                                 (uint32_t)(i.size * i.itemsize));
+           },
+           py::arg("idx"), py::arg("begin"), py::arg("data"),
+           "A block received on a Python-framed connection: 0 not taken, 1 taken, 2 taken "
+           "and the piece complete")
       .def("set_have",
            [](SwarmWire& w, const py::bytes& bits) { w.set_have(std::string(bits)); },
            py::arg("bits"))
@@ -275,7 +307,8 @@ PYBIND11_MODULE(_native, m) {
              for (auto& e : ev) out.append(py::make_tuple(e.conn, e.kind, py::bytes(e.data)));
              return out;
            },
-           "[(conn_id, kind, data)]: 1 message, 2 blocks, 3 closed, 4 piece (conn 0)")
+           "[(conn_id, kind, data)]: 1 message, 2 blocks, 3 closed, 4 piece (conn 0), "
+           "5 the connection's request queue runs low")
       .def("stats",
            [](SwarmWire& w) {
              SwarmWireStats s = w.stats();
@@ -293,11 +326,16 @@ PYBIND11_MODULE(_native, m) {
              d["sha_s"] = s.sha_ns / 1e9;
              d["write_s"] = s.write_ns / 1e9;
              d["served_bytes"] = s.served_bytes;
+             d["assigned"] = s.assigned;            // owned pieces (SwarmWire.assign)
+             d["requests"] = s.requests;            // REQUESTs the wire sent by itself
              d["gpu_pieces"] = s.gpu_pieces;
              d["gpu_refused"] = s.gpu_refused;
              d["gpu_errors"] = s.gpu_errors;
              d["pool_in_use"] = s.pool_in_use;      // process-wide piece buffers
              d["pool_idle"] = s.pool_idle;
+             d["pool_allocs"] = s.pool_allocs;      // (process lifetime)
+             d["pool_frees"] = s.pool_frees;
+             d["pool_locks"] = s.pool_locks;
              return d;
            })
       .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());

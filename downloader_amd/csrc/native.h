@@ -162,6 +162,9 @@ struct RelayPoolStats {
 // hasher's ticket), so replacing the hasher cannot make two pending parts collide.
 void set_gpu_part_hasher(const void* api, int min_pieces);
 const void* gpu_part_hasher_current();        // the installed hasher's API (null: none)
+// The swarm wire's idle piece buffers page-locked for this hasher API are unlocked and freed
+// (before the hasher itself is destroyed; peerwire.cpp).
+void swarm_piece_pool_forget(const void* api);
 struct GpuPartStats {
   uint64_t submitted, host_fallbacks, refused, pending;
 };
@@ -218,19 +221,37 @@ struct SwarmWireStats {
   uint64_t verify_batches = 0, sha_ns = 0, write_ns = 0;   // verifier: batches, time hashing /
                                                             // writing
   uint64_t served_bytes = 0;                                // blocks served with sendfile
+  uint64_t assigned = 0, requests = 0;                      // owned pieces, REQUESTs the wire sent
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
   size_t pool_in_use = 0, pool_idle = 0;                    // process-wide piece buffers
+  uint64_t pool_allocs = 0, pool_frees = 0, pool_locks = 0; // since start: buffers made /
+                                                            // unmade, page-locked for a hasher
   size_t active_pieces = 0;
 };
 class SwarmWire {
  public:
-  static constexpr int kEvMsg = 1, kEvBlocks = 2, kEvClosed = 3, kEvPiece = 4;
+  // kEvNeed: the connection's native request queue fell below one pipeline (assign more)
+  static constexpr int kEvMsg = 1, kEvBlocks = 2, kEvClosed = 3, kEvPiece = 4, kEvNeed = 5;
   explicit SwarmWire(int verify_threads = 2);
   ~SwarmWire();
   void set_storage(int64_t piece_length, int64_t total, const std::string& hashes,
                    const std::vector<std::pair<int, int64_t>>& files);
   void begin_piece(uint32_t idx);
   void drop_piece(uint32_t idx);
+  // Owned pieces: a piece assigned to a connection is requested by the wire itself, block by
+  // block, keeping `depth` requests in flight on that connection (refilled as blocks arrive,
+  // on the reader thread); only its owner may fill it, and its blocks are not reported one by
+  // one (the PIECE result is the first Python hears of it). assign returns the connection's
+  // queue of blocks still to request; kEvNeed fires once when that queue drops below a
+  // pipeline. release (the peer choked us, or closed) and release_piece (endgame) turn owned
+  // pieces back into ordinary ones and return their per-block state: 2 received, 1 requested
+  // from the owner and not answered yet, 0 neither.
+  void set_pipeline(uint32_t depth);
+  size_t assign(uint64_t conn, uint32_t idx);
+  size_t todo(uint64_t conn);
+  std::vector<std::pair<uint32_t, std::string>> release(uint64_t conn);
+  bool release_piece(uint32_t idx, uint64_t* owner, std::string* states);
+  double rx_idle(uint64_t conn);                // seconds since the connection last received
   // Serving: pieces we have (storage recheck; natively verified ones are added as they pass)
   // are served to connections Python unchoked, straight from the storage files.
   void set_have(const std::string& bits);
@@ -267,8 +288,15 @@ class SwarmWire {
   bool send_all(Conn& c, const char* p, size_t n, int flags);
   void finish_piece(const Piece& p, const uint8_t* dig);   // compare, write, report
   void gpu_loop();
+  int take_from(Conn* c, uint32_t idx, uint32_t begin, const uint8_t* p, uint32_t len,
+                bool* owned, std::string* reqs, bool* need);
+  bool pump(Conn& c, std::string* reqs);        // mu_ held
+  void queue_out(Conn& c, std::string data);
+  std::shared_ptr<Conn> conn(uint64_t id);
+  std::string block_states(const Piece& p, const Conn* owner);   // mu_ held
 
-  std::mutex mu_;                               // pieces_, geometry, stats_
+  std::mutex mu_;                               // pieces_, geometry, stats_, request queues
+  uint32_t depth_ = 64;
   int64_t piece_length_ = 0, total_ = 0;
   std::string hashes_;
   std::vector<std::pair<int, int64_t>> files_;

@@ -9,8 +9,15 @@
 //     payloads are copied once, straight into the assembling piece's buffer (first arrival of a
 //     block wins); every other message goes up to Python, which stays the protocol and
 //     state-machine owner (torrent/peer.py, torrent/session.py);
-//   * Python learns which blocks arrived from one BLOCKS event per receive batch (coalesced
-//     while Python has not polled: the busier the loop, the bigger the batches);
+//   * a piece Python assigns to a connection (assign) is requested by the wire itself: the
+//     reader that takes a block answering one of that connection's requests appends the next
+//     REQUEST, so `depth` stay in flight without Python, whose work per 4 MiB piece is one
+//     assignment and one result instead of 256 block bookings (~0.1 CPU-s/GB on the event
+//     loop); NEED tells Python when a connection's queue runs low, release / release_piece
+//     hand a choked, closed or endgame piece back to per-block requesting;
+//   * for the other pieces, Python learns which blocks arrived from one BLOCKS event per
+//     receive batch (coalesced while Python has not polled: the busier the loop, the bigger
+//     the batches);
 //   * complete pieces are verified 16 at a time on the AVX-512 multi-buffer SHA-1 (sha1_mb),
 //     written to the storage files with pwrite, and reported as PIECE events;
 //   * one writer thread per connection sends what Python queues (requests, handshake-time
@@ -40,6 +47,7 @@
 #include <stdexcept>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace stager {
@@ -68,6 +76,7 @@ struct PiecePool {
   std::mutex mu;
   std::unordered_map<size_t, std::vector<std::pair<uint8_t*, const void*>>> idle;
   size_t in_use = 0, idle_count = 0;
+  uint64_t allocs = 0, frees = 0, locks = 0;
   static constexpr size_t kMaxIdle = 128;   // ~512 MiB of 4 MiB pieces kept
 
   uint8_t* take(size_t n, const void** reg) {
@@ -84,10 +93,13 @@ struct PiecePool {
       }
     }
     void* b = aligned_alloc(4096, n);
-    if (!b) {
+    {
       std::lock_guard<std::mutex> g(mu);
-      in_use--;
-      throw std::bad_alloc();
+      if (!b) {
+        in_use--;
+        throw std::bad_alloc();
+      }
+      allocs++;
     }
     *reg = nullptr;
     return (uint8_t*)b;
@@ -103,9 +115,35 @@ struct PiecePool {
         idle_count++;
         return;
       }
+      frees++;
     }
     if (reg) ((const GpuPartHashApi*)reg)->unreg(((const GpuPartHashApi*)reg)->ctx, b);
     free(b);
+  }
+  // Idle buffers page-locked for `api` are unlocked and freed (the hasher is going away).
+  void forget(const void* api) {
+    std::vector<std::pair<uint8_t*, const void*>> drop;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (auto& kv : idle) {
+        auto& v = kv.second;
+        for (size_t i = 0; i < v.size();) {
+          if (v[i].second == api) {
+            drop.push_back(v[i]);
+            v[i] = v.back();
+            v.pop_back();
+            idle_count--;
+            frees++;
+          } else {
+            ++i;
+          }
+        }
+      }
+    }
+    for (auto& b : drop) {
+      ((const GpuPartHashApi*)api)->unreg(((const GpuPartHashApi*)api)->ctx, b.first);
+      free(b.first);
+    }
   }
 };
 
@@ -116,6 +154,10 @@ PiecePool& piece_pool() {
 
 }  // namespace
 
+void swarm_piece_pool_forget(const void* api) {
+  if (api) piece_pool().forget(api);
+}
+
 struct SwarmWire::Piece {
   uint32_t idx = 0;
   uint32_t size = 0, nblocks = 0;
@@ -125,6 +167,7 @@ struct SwarmWire::Piece {
   std::vector<uint8_t> claimed;          // per block: taken by a reader (under mu_)
   std::atomic<uint32_t> filled{0};       // blocks copied in
   uint64_t epoch = 0;                    // begin_piece generation (a re-begun piece is new)
+  uint64_t owner = 0;                    // connection requesting it natively (under mu_)
   ~Piece() {
     if (data) piece_pool().give(data, cap, reg);
   }
@@ -149,7 +192,21 @@ struct SwarmWire::Conn {
   bool stop = false;                     // under wmu
   std::atomic<bool> dead{false};
   std::string prefix;                    // bytes read before the handoff (asyncio buffer)
+  std::atomic<int64_t> last_rx_ns{0};    // steady clock of the last receive
+  // native request pipeline of its owned pieces (under the wire's mu_): blocks still to
+  // request (piece << 32 | begin) and blocks requested and not answered yet
+  std::deque<uint64_t> todo;
+  std::unordered_set<uint64_t> asked;
+  bool need_sent = false;
 };
+
+namespace {
+inline uint64_t block_key(uint32_t idx, uint32_t begin) { return (uint64_t)idx << 32 | begin; }
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
 
 SwarmWire::SwarmWire(int verify_threads) {
   efd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
@@ -260,9 +317,23 @@ void SwarmWire::drop_piece(uint32_t idx) {
 // 0 not taken (no such active piece, a duplicate, a bad offset / length), 1 taken, 2 taken and
 // the piece is complete (queued for verification).
 int SwarmWire::take_block(uint32_t idx, uint32_t begin, const uint8_t* p, uint32_t len) {
+  bool owned = false, need = false;
+  return take_from(nullptr, idx, begin, p, len, &owned, nullptr, &need);
+}
+
+// A block that arrived on connection `c` (nullptr: handed in by Python). An answer to one of
+// the connection's own requests makes room in its pipeline: the next REQUESTs are appended to
+// `reqs`, and `need` set when its queue fell below a pipeline.
+int SwarmWire::take_from(Conn* c, uint32_t idx, uint32_t begin, const uint8_t* p, uint32_t len,
+                         bool* owned, std::string* reqs, bool* need) {
   std::shared_ptr<Piece> pc;
   {
     std::lock_guard<std::mutex> g(mu_);
+    // an answer to the wire's own request: not reported unless it lands in an ordinary piece
+    // (a released one, whose blocks Python books again)
+    const bool ours = c && c->asked.erase(block_key(idx, begin));
+    if (ours && pump(*c, reqs)) *need = true;
+    *owned = ours;
     auto it = pieces_.find(idx);
     if (it == pieces_.end()) {
       stats_.blocks_ignored++;
@@ -270,11 +341,19 @@ int SwarmWire::take_block(uint32_t idx, uint32_t begin, const uint8_t* p, uint32
     }
     pc = it->second;
     const uint32_t b = begin / kBlock;
-    if (begin % kBlock || b >= pc->nblocks ||
-        len != std::min(kBlock, pc->size - b * kBlock) || pc->claimed[b]) {
+    // an owned piece takes blocks from its owner only: bytes nobody asked that peer for must
+    // not mix into a piece whose hash failure is blamed on the owner
+    if (pc->owner && (!c || pc->owner != c->id)) {
+      *owned = true;        // (not reported either: Python did not ask this peer for it)
       stats_.blocks_ignored++;
       return 0;
     }
+    if (begin % kBlock || b >= pc->nblocks || len != std::min(kBlock, pc->size - b * kBlock) ||
+        pc->claimed[b]) {
+      stats_.blocks_ignored++;
+      return 0;
+    }
+    *owned = pc->owner != 0;
     pc->claimed[b] = 1;
     stats_.blocks++;
     stats_.block_bytes += len;
@@ -293,6 +372,136 @@ int SwarmWire::take_block(uint32_t idx, uint32_t begin, const uint8_t* p, uint32
   }
   vcv_.notify_one();
   return 2;
+}
+
+// Next REQUESTs of `c`'s owned pieces, up to depth_ in flight (mu_ held). True the first time
+// the queue of blocks to request drops below a pipeline since Python last filled it.
+bool SwarmWire::pump(Conn& c, std::string* reqs) {
+  while (c.asked.size() < depth_ && !c.todo.empty()) {
+    const uint64_t k = c.todo.front();
+    c.todo.pop_front();
+    const uint32_t idx = (uint32_t)(k >> 32), begin = (uint32_t)k;
+    auto it = pieces_.find(idx);
+    if (it == pieces_.end() || it->second->owner != c.id) continue;   // complete or released
+    const Piece& p = *it->second;
+    if (p.claimed[begin / kBlock]) continue;
+    c.asked.insert(k);
+    stats_.requests++;
+    if (reqs) {
+      put32(*reqs, 13);
+      reqs->push_back((char)kRequest);
+      put32(*reqs, idx);
+      put32(*reqs, begin);
+      put32(*reqs, std::min(kBlock, p.size - begin));
+    }
+  }
+  if (c.todo.size() < depth_ && !c.need_sent) {
+    c.need_sent = true;
+    return true;
+  }
+  return false;
+}
+
+void SwarmWire::queue_out(Conn& c, std::string data) {
+  std::lock_guard<std::mutex> g(c.wmu);
+  if (c.stop) return;
+  c.out_bytes += data.size();
+  c.out.push_back(Conn::Item{std::move(data), false});
+  c.wcv.notify_one();
+}
+
+std::shared_ptr<SwarmWire::Conn> SwarmWire::conn(uint64_t id) {
+  std::lock_guard<std::mutex> g(cmu_);
+  auto it = conns_.find(id);
+  return it == conns_.end() ? nullptr : it->second;
+}
+
+void SwarmWire::set_pipeline(uint32_t depth) {
+  std::lock_guard<std::mutex> g(mu_);
+  depth_ = std::max<uint32_t>(1, depth);
+}
+
+size_t SwarmWire::assign(uint64_t id, uint32_t idx) {
+  std::shared_ptr<Conn> c = conn(id);
+  if (!c) throw std::invalid_argument("assign: no such connection");
+  std::string reqs;
+  size_t n;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = pieces_.find(idx);
+    if (it == pieces_.end()) throw std::out_of_range("assign: piece not active");
+    Piece& p = *it->second;
+    if (p.owner && p.owner != id) throw std::invalid_argument("assign: piece owned elsewhere");
+    if (p.owner != id) stats_.assigned++;
+    p.owner = id;
+    for (uint32_t b = 0; b < p.nblocks; ++b) {
+      const uint64_t k = block_key(idx, b * kBlock);
+      if (!p.claimed[b] && !c->asked.count(k)) c->todo.push_back(k);
+    }
+    pump(*c, &reqs);
+    n = c->todo.size();
+    // Python sees the queue length in the return value: kEvNeed next when it falls below a
+    // pipeline again, not while Python is still the one filling it
+    c->need_sent = n < depth_;
+  }
+  if (!reqs.empty()) queue_out(*c, std::move(reqs));
+  return n;
+}
+
+size_t SwarmWire::todo(uint64_t id) {
+  std::shared_ptr<Conn> c = conn(id);
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(mu_);
+  return c->todo.size();
+}
+
+std::string SwarmWire::block_states(const Piece& p, const Conn* owner) {
+  std::string s(p.nblocks, '\0');
+  for (uint32_t b = 0; b < p.nblocks; ++b)
+    s[b] = p.claimed[b] ? 2 : (owner && owner->asked.count(block_key(p.idx, b * kBlock)) ? 1 : 0);
+  return s;
+}
+
+std::vector<std::pair<uint32_t, std::string>> SwarmWire::release(uint64_t id) {
+  std::shared_ptr<Conn> c = conn(id);   // (gone after detach: its requests count as unanswered)
+  std::vector<std::pair<uint32_t, std::string>> out;
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& kv : pieces_) {
+    Piece& p = *kv.second;
+    if (p.owner != id) continue;
+    out.emplace_back(p.idx, block_states(p, c.get()));
+    p.owner = 0;
+  }
+  if (c) {
+    c->todo.clear();
+    c->asked.clear();      // a choking peer drops what we asked for (BEP-3)
+    c->need_sent = false;
+  }
+  return out;
+}
+
+bool SwarmWire::release_piece(uint32_t idx, uint64_t* owner, std::string* states) {
+  uint64_t id;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = pieces_.find(idx);
+    if (it == pieces_.end() || !it->second->owner) return false;
+    id = it->second->owner;
+  }
+  std::shared_ptr<Conn> c = conn(id);
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pieces_.find(idx);
+  if (it == pieces_.end() || it->second->owner != id) return false;
+  *owner = id;
+  *states = block_states(*it->second, c.get());
+  it->second->owner = 0;      // its entries left in the owner's queue are skipped by pump
+  return true;
+}
+
+double SwarmWire::rx_idle(uint64_t id) {
+  std::shared_ptr<Conn> c = conn(id);
+  if (!c) return 0.0;
+  return (double)(now_ns() - c->last_rx_ns.load(std::memory_order_relaxed)) / 1e9;
 }
 
 void SwarmWire::verify_loop() {
@@ -324,6 +533,10 @@ void SwarmWire::verify_loop() {
         if (p->reg != api) {
           if (p->reg) ((const GpuPartHashApi*)p->reg)->unreg(((const GpuPartHashApi*)p->reg)->ctx, p->data);
           p->reg = api->reg(api->ctx, p->data, p->cap) == 0 ? api : nullptr;
+          if (p->reg) {
+            std::lock_guard<std::mutex> g(piece_pool().mu);
+            piece_pool().locks++;
+          }
         }
         if (p->reg == api) t = api->submit(api->ctx, p->data, p->size, p->size);
       }
@@ -497,6 +710,7 @@ void SwarmWire::attach(int fd, uint64_t id, const std::string& prefix) {
   c->id = id;
   c->fd = fd;
   c->prefix = prefix;
+  c->last_rx_ns.store(now_ns());
   {
     std::lock_guard<std::mutex> g(cmu_);
     if (conns_.count(id)) throw std::invalid_argument("connection already attached");
@@ -525,6 +739,8 @@ void SwarmWire::read_loop(Conn& c) {
     end = std::min(c.prefix.size(), buf.size());
   }
   std::string blocks;                     // records of this batch: idx, begin, len, status
+  std::string reqs;                       // REQUESTs the batch's answers made room for
+  bool need = false;
   std::string reason = "closed";
   auto flush_blocks = [&] {
     if (!blocks.empty()) {
@@ -547,11 +763,14 @@ void SwarmWire::read_loop(Conn& c) {
       if (n > 0) {
         if (m[0] == kPiece && n >= 9) {
           const uint32_t idx = be32(m + 1), begin = be32(m + 5), len = n - 9;
-          const int st = take_block(idx, begin, m + 9, len);
-          put32(blocks, idx);
-          put32(blocks, begin);
-          put32(blocks, len);
-          put32(blocks, (uint32_t)st);
+          bool owned = false;
+          const int st = take_from(&c, idx, begin, m + 9, len, &owned, &reqs, &need);
+          if (!owned) {                   // an owned piece's blocks are the wire's business
+            put32(blocks, idx);
+            put32(blocks, begin);
+            put32(blocks, len);
+            put32(blocks, (uint32_t)st);
+          }
         } else if (m[0] == kRequest && n == 13 && c.serving.load() &&
                    servable(be32(m + 1), be32(m + 5), be32(m + 9))) {
           std::string it(12, '\0');          // served by the writer, in order with the rest
@@ -567,6 +786,14 @@ void SwarmWire::read_loop(Conn& c) {
       start += 4 + (size_t)n;
     }
     flush_blocks();
+    if (!reqs.empty()) {
+      queue_out(c, std::move(reqs));      // one write for the whole batch's refill
+      reqs.clear();
+    }
+    if (need) {
+      push(c.id, kEvNeed, std::string());
+      need = false;
+    }
     if (bad) break;
     if (start == end) {
       start = end = 0;
@@ -591,6 +818,7 @@ void SwarmWire::read_loop(Conn& c) {
       break;
     }
     end += (size_t)r;
+    c.last_rx_ns.store(now_ns(), std::memory_order_relaxed);
     rx_bytes_.fetch_add((uint64_t)r, std::memory_order_relaxed);
     recvs_.fetch_add(1, std::memory_order_relaxed);
   }
@@ -768,6 +996,9 @@ SwarmWireStats SwarmWire::stats() {
     std::lock_guard<std::mutex> g2(pp.mu);
     s.pool_in_use = pp.in_use;
     s.pool_idle = pp.idle_count;
+    s.pool_allocs = pp.allocs;
+    s.pool_frees = pp.frees;
+    s.pool_locks = pp.locks;
   }
   return s;
 }

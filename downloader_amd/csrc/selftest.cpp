@@ -71,6 +71,12 @@ static std::string hex(const std::string& s) {
   return o;
 }
 
+static uint32_t rd32(const char* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return ntohl(v);
+}
+
 static std::vector<uint8_t> rnd(size_t n, uint32_t seed) {
   std::mt19937 g(seed);
   std::vector<uint8_t> v(n);
@@ -610,6 +616,7 @@ static void wire_section(bool gpu) {
   CHECK(w.stats().pool_in_use == 0);   // every piece buffer back in the process-wide pool
   if (gpu) {
     set_gpu_part_hasher(nullptr, 0);
+    swarm_piece_pool_forget(hasher->api());   // idle buffers page-locked for it go first
     hasher.reset();
   }
   std::vector<uint8_t> back((size_t)total);
@@ -623,6 +630,144 @@ static void wire_section(bool gpu) {
   unlink(p2);
   fprintf(stderr, "wire%s: %d pieces verified, %d corrupt copies refused\n",
           gpu ? " (gpu hasher)" : "", done, bad);
+}
+
+// ---- owned pieces: the wire requests the blocks itself. Two seeders answer every REQUEST
+// (the first copy of piece 7 served is corrupt; seeder 2 adds a block of a piece nobody asked
+// it for); the driver assigns pieces while a connection's queue is low, re-assigns the failed
+// piece to connection 1, and half-way releases connection 2's pieces (as on a CHOKE) and
+// hands them to connection 1, while seeder 2 still answers the requests it had. Every piece
+// must be verified once and written, no block reported one by one, and the late answers
+// refused.
+static void wire_owned_section() {
+  const int64_t plen = 65536, total = 40 * plen - 5000;
+  const int npieces = (int)((total + plen - 1) / plen);
+  auto data = rnd((size_t)total, 17);
+  std::string hashes;
+  for (int64_t off = 0; off < total; off += plen)
+    hashes += digest("sha1", data.data() + off, (size_t)std::min(plen, total - off));
+  char p1[] = "/tmp/stager-selftest-owned-XXXXXX";
+  int f1 = mkstemp(p1);
+  SwarmWire w(2);
+  w.set_storage(plen, total, hashes, {{f1, total}});
+  w.set_pipeline(6);
+  std::vector<std::thread> seeders;
+  std::vector<int> theirs;
+  std::atomic<int> requests{0};
+  std::atomic<bool> corrupted{false};
+  for (int c = 0; c < 2; ++c) {
+    int sv[2];
+    socketpair(AF_UNIX, SOCK_STREAM, 0, sv);
+    w.attach(sv[0], (uint64_t)(c + 1), "");
+    theirs.push_back(sv[1]);
+    seeders.emplace_back([&, c, fd = sv[1]] {
+      std::string in;
+      bool stray = false;
+      char buf[65536];
+      for (;;) {
+        ssize_t r = recv(fd, buf, sizeof buf, 0);
+        if (r <= 0) return;
+        in.append(buf, (size_t)r);
+        std::string out;
+        size_t pos = 0;
+        while (in.size() - pos >= 4) {
+          const uint32_t n = rd32(in.data() + pos);
+          if (in.size() - pos < 4 + (size_t)n) break;
+          const char* m = in.data() + pos + 4;
+          if (n == 13 && m[0] == 6) {
+            requests++;
+            const uint32_t idx = rd32(m + 1), begin = rd32(m + 5), len = rd32(m + 9);
+            uint32_t hdr[3] = {htonl(len + 9), htonl(idx), htonl(begin)};
+            out.append((const char*)hdr, 4);
+            out.push_back(7);
+            out.append((const char*)&hdr[1], 8);
+            std::string blk((const char*)data.data() + (int64_t)idx * plen + begin, len);
+            if (idx == 7 && !corrupted.exchange(true)) blk[3] ^= 0x21;   // the first copy
+            out += blk;
+            if (c == 1 && !stray) {               // unrequested: piece 1 is not ours
+              stray = true;
+              uint32_t h2[3] = {htonl(9 + 16384), htonl(1), htonl(16384)};
+              out.append((const char*)h2, 4);
+              out.push_back(7);
+              out.append((const char*)&h2[1], 8);
+              out.append(16384, 'x');
+            }
+          }
+          pos += 4 + n;
+        }
+        in.erase(0, pos);
+        for (size_t off = 0; off < out.size();) {
+          ssize_t wr = send(fd, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+          if (wr <= 0) return;
+          off += (size_t)wr;
+        }
+      }
+    });
+  }
+  // (between release and re-assignment a released piece is an ordinary one: a late answer
+  // from seeder 2 may land in it and be reported block by block)
+  int next = 0, done = 0, bad = 0, block_records = 0, records_before = -1, needs = 0;
+  bool released = false;
+  std::vector<int> verified(npieces, 0);
+  auto top_up = [&](uint64_t conn) {
+    size_t t = w.todo(conn);
+    while (t < 12 && next < npieces) {
+      w.begin_piece((uint32_t)next);
+      t = w.assign(conn, (uint32_t)next++);
+    }
+  };
+  top_up(1);
+  top_up(2);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (done < npieces && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60)) {
+    pollfd pf{w.eventfd(), POLLIN, 0};
+    ::poll(&pf, 1, 100);
+    for (auto& e : w.poll()) {
+      if (e.kind == SwarmWire::kEvBlocks)       // blocks taken one by one (stray junk is
+        for (size_t k = 0; k + 16 <= e.data.size(); k += 16)   // reported as not taken)
+          block_records += e.data[k + 15] != 0;
+      if (e.kind == SwarmWire::kEvNeed) {
+        needs++;
+        top_up(e.conn);
+      }
+      if (e.kind == SwarmWire::kEvPiece) {
+        const uint32_t idx = rd32(e.data.data());
+        if (e.data[4] == 1) {
+          verified[idx]++;
+          done++;
+        } else {
+          bad++;
+          w.begin_piece(idx);
+          w.assign(1, idx);                  // fetched again, a fresh copy
+        }
+        if (!released && done >= npieces / 2) {
+          released = true;                   // connection 2 "choked": its pieces go to 1
+          records_before = block_records;
+          for (auto& r : w.release(2)) {
+            CHECK(r.second.size() == (size_t)((std::min<int64_t>(plen, total - (int64_t)r.first * plen) + 16383) / 16384));
+            w.assign(1, r.first);
+          }
+        }
+      }
+    }
+  }
+  CHECK(done == npieces);
+  for (int i = 0; i < npieces; ++i) CHECK(verified[i] == 1);
+  SwarmWireStats st = w.stats();
+  CHECK(bad == 1 && st.hash_fails == 1 && st.verified == (uint64_t)npieces);
+  CHECK(released && records_before == 0);
+  CHECK(needs > 0);
+  CHECK(st.blocks_ignored >= 1);            // the stray block at least
+  w.close();
+  for (auto& t : seeders) t.join();          // close() shut their peers' sockets down
+  std::vector<uint8_t> back((size_t)total);
+  CHECK(pread(f1, back.data(), (size_t)total, 0) == total);
+  CHECK(back == data);
+  for (int fd : theirs) close(fd);
+  close(f1);
+  unlink(p1);
+  fprintf(stderr, "wire (owned): %d pieces, %d requests, %d NEED events, %llu blocks refused\n",
+          done, requests.load(), needs, (unsigned long long)st.blocks_ignored);
 }
 
 static void stress_sections() {
@@ -675,6 +820,7 @@ int main() {
   if (getenv("SELFTEST_ONLY") && strcmp(getenv("SELFTEST_ONLY"), "wire") == 0) {
     wire_section(false);
     wire_section(true);
+    wire_owned_section();
     printf(g_fail ? "selftest: failures\n" : "selftest ok\n");
     return g_fail ? 1 : 0;
   }
@@ -1032,6 +1178,7 @@ int main() {
   stress_sections();
   wire_section(false);
   wire_section(true);
+  wire_owned_section();
   {
     RelayPoolStats st = relay_pool_stats();
     CHECK(st.in_use == 0 && st.idle_buffers <= st.max_idle);

@@ -33,7 +33,7 @@ class TorrentClient:
                  idle_timeout: float = 120.0, connect_timeout: float = 10.0,
                  seed_after_done: bool = False, listen: bool = True,
                  native_wire: bool = True, wire_verify_threads: int = 2,
-                 swarm_verify: str = "auto"):
+                 swarm_verify: str = "auto", wire_requests: bool = True):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -63,6 +63,8 @@ class TorrentClient:
         self.native_wire = native_wire
         self.wire_verify_threads = wire_verify_threads
         self.swarm_verify = swarm_verify          # auto / gpu / cpu (native wire only)
+        # whole pieces requested by the native wire itself (SwarmWire.assign), not per block
+        self.wire_requests = wire_requests
         self.pex_interval = 60.0
         self.piece_cache_bytes = 64 << 20   # per-session LRU of pieces being served to peers
         self.dht_interval = 30.0
@@ -86,6 +88,7 @@ class TorrentClient:
                    verify_threads=d.verify_threads,
                    native_wire=d.torrent_native_wire,
                    swarm_verify=d.swarm_verify_backend,
+                   wire_requests=d.torrent_wire_requests,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

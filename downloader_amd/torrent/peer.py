@@ -10,7 +10,8 @@ With the session's native wire (``csrc/peerwire.cpp``, ``download.torrent_native
 socket is handed over right after the handshake: native threads frame the messages, copy
 PIECE payloads into the assembling piece and send what this class queues; this class keeps
 every protocol decision (what to request, interest, choking, serving, extensions) and gets
-the other messages, and the blocks that arrived, as events (``_wq``).
+the other messages, and the blocks that arrived, as events (``_wq``). Whole pieces the session
+assigns to the connection are requested by the wire itself (``SwarmWire.assign``).
 """
 from __future__ import annotations
 
@@ -32,7 +33,7 @@ MAX_MSG = 2 * 1024 * 1024
 CHOKE, UNCHOKE, INTERESTED, NOT_INTERESTED, HAVE, BITFIELD, REQUEST, PIECE, CANCEL, PORT = range(10)
 EXTENDED = 20
 # native wire event kinds (SwarmWire.poll) and this class' own queue markers
-EV_MSG, EV_BLOCKS, EV_CLOSED, EV_PIECE = 1, 2, 3, 4
+EV_MSG, EV_BLOCKS, EV_CLOSED, EV_PIECE, EV_NEED = 1, 2, 3, 4, 5
 EV_FILL, EV_CANCEL_DUPS = 101, 102
 # our extension message ids (what peers must use when talking to us)
 UT_METADATA_ID = 1
@@ -250,7 +251,15 @@ class PeerConn:
         period = max(1.0, self.s.idle_timeout / 4)
         while not self.closed:
             await asyncio.sleep(period)
-            if time.monotonic() - self.last_rx > self.s.idle_timeout:
+            idle = time.monotonic() - self.last_rx
+            if self.wire is not None and idle > self.s.idle_timeout:
+                # blocks of a piece the wire requests itself are not reported one by one: ask
+                # the wire when the socket last received
+                try:
+                    idle = min(idle, self.wire.rx_idle(id(self)))
+                except Exception:
+                    pass
+            if idle > self.s.idle_timeout:
                 self.close()
                 return
 

@@ -31,7 +31,8 @@ from ..utils.aio import drain, gather_strict, run_settled
 from ..utils.log import redact_url
 from .bencode import bencode
 from .metainfo import Metainfo, MetainfoError, parse_info
-from .peer import BLOCK, EV_BLOCKS, EV_CANCEL_DUPS, EV_FILL, EV_PIECE, METADATA_PIECE, PeerConn
+from .peer import (BLOCK, EV_BLOCKS, EV_CANCEL_DUPS, EV_FILL, EV_NEED, EV_PIECE, METADATA_PIECE,
+                   PeerConn)
 from .storage import Bitfield, Storage
 from .tracker import decode_compact, encode_compact, supported as tracker_supported
 
@@ -54,7 +55,7 @@ class TorrentError(Exception):
 
 
 class _Active:
-    __slots__ = ("idx", "size", "nblocks", "buf", "state", "req", "got", "peers")
+    __slots__ = ("idx", "size", "nblocks", "buf", "state", "req", "got", "peers", "owner")
 
     def __init__(self, idx: int, size: int, buffered: bool = True):
         self.idx = idx
@@ -66,6 +67,9 @@ class _Active:
         self.req: Dict[int, Set[int]] = {}     # block -> ids of peers that requested it
         self.got = 0
         self.peers: Set[int] = set()           # peers that contributed blocks
+        # native wire: the connection whose wire requests this piece by itself (its blocks
+        # are then not booked here: ``state`` reads all-requested until it is released)
+        self.owner: Optional[int] = None
 
     def block_len(self, b: int) -> int:
         return min(BLOCK, self.size - b * BLOCK)
@@ -195,17 +199,18 @@ class PiecePicker:
         return any(i in bf and i not in self.have for i in range(self.n))
 
     # ---------------------------------------------------------------- blocks
-    def next_block(self, peer_id: int, bf: Bitfield) -> Optional[Tuple[int, int, int]]:
+    def next_block(self, peer_id: int, bf: Bitfield, fresh: bool = True,
+                   dups: bool = True) -> Optional[Tuple[int, int, int]]:
         # 1. a free block of an active piece this peer has
         for ap in self.active.values():
-            if ap.idx in bf:
+            if ap.idx in bf and ap.owner is None:
                 for b in range(ap.nblocks):
                     if ap.state[b] == 0:
                         ap.state[b] = 1
                         ap.req.setdefault(b, set()).add(peer_id)
                         return ap.idx, b * BLOCK, ap.block_len(b)
         # 2. start the rarest piece this peer has
-        best = self._take_rarest(bf)
+        best = self._take_rarest(bf) if fresh else -1
         if best >= 0:
             ap = _Active(best, self.meta.piece_size(best), self.on_activate is None)
             if self.on_activate is not None:
@@ -215,22 +220,26 @@ class PiecePicker:
             ap.req[0] = {peer_id}
             return best, 0, ap.block_len(0)
         # 3. endgame: duplicate an outstanding block this peer has not requested yet
+        if not dups:
+            return None
         for ap in self.active.values():
-            if ap.idx in bf:
+            if ap.idx in bf and ap.owner is None:
                 for b in range(ap.nblocks):
                     if ap.state[b] == 1 and peer_id not in ap.req.get(b, ()):
                         ap.req.setdefault(b, set()).add(peer_id)
                         return ap.idx, b * BLOCK, ap.block_len(b)
         return None
 
-    def next_blocks(self, peer_id: int, bf: Bitfield, k: int) -> List[Tuple[int, int, int]]:
+    def next_blocks(self, peer_id: int, bf: Bitfield, k: int, fresh: bool = True,
+                    dups: bool = True) -> List[Tuple[int, int, int]]:
         """Up to ``k`` blocks for one peer in one pass: free blocks of active pieces first,
-        then whole new (rarest) pieces, then endgame duplicates."""
+        then whole new (rarest) pieces (``fresh``), then endgame duplicates (``dups``)."""
         out: List[Tuple[int, int, int]] = []
         for ap in self.active.values():
             if len(out) >= k:
                 return out
-            if ap.idx not in bf or ap.got + len(ap.req) >= ap.nblocks and 0 not in ap.state:
+            if ap.idx not in bf or ap.owner is not None or \
+                    ap.got + len(ap.req) >= ap.nblocks and 0 not in ap.state:
                 continue
             for b in range(ap.nblocks):
                 if ap.state[b] == 0:
@@ -240,7 +249,7 @@ class PiecePicker:
                     if len(out) >= k:
                         return out
         while len(out) < k:
-            nb = self.next_block(peer_id, bf)
+            nb = self.next_block(peer_id, bf, fresh, dups)
             if nb is None:
                 break
             out.append(nb)
@@ -254,6 +263,26 @@ class PiecePicker:
                         ap.req.setdefault(b, set()).add(peer_id)
                         out.append((ap.idx, b * BLOCK, ap.block_len(b)))
         return out
+
+    def take_piece(self, peer_id: int, bf: Bitfield) -> int:
+        """The rarest piece ``bf`` has, activated whole for one connection's native wire to
+        request (-1: none)."""
+        best = self._take_rarest(bf)
+        if best < 0:
+            return -1
+        ap = _Active(best, self.meta.piece_size(best), False)
+        if self.on_activate is not None:
+            self.on_activate(best)
+        ap.owner = peer_id
+        ap.state = bytearray(b"\x01") * ap.nblocks
+        self.active[best] = ap
+        return best
+
+    def no_candidates(self) -> bool:
+        """Every missing piece is active, being verified or claimed by a webseed: the
+        endgame."""
+        return self.n - self.have.count - len(self.active) - len(self.verifying) \
+            - len(self.claimed) <= 0
 
     def complete_blocks(self, idx: int) -> bool:
         """All blocks of active piece ``idx`` arrived: it leaves ``active`` for ``verifying``
@@ -406,6 +435,9 @@ class TorrentSession:
         self._wire_loop = None
         self._wire_pieces: "asyncio.Queue" = asyncio.Queue()
         self._verifying_ap: Dict[int, _Active] = {}   # natively verified pieces: contributors
+        # whole pieces requested by the wire itself (SwarmWire.assign) until the endgame
+        self._owned_mode = bool(client.native_wire and client.wire_requests)
+        self._endgame = False
         if client.native_wire:
             try:
                 from ..ops import native
@@ -413,6 +445,9 @@ class TorrentSession:
             except Exception:
                 self.wire = None
         self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0,
+                      # native wire: owned pieces handed back by a choking / closing peer, and
+                      # made ordinary when the endgame began
+                      "wire_released": 0, "wire_endgame_pieces": 0,
                       # summed over webseed streams: time in Range GETs / in piece verification
                       "webseed_fetch_s": 0.0, "webseed_verify_s": 0.0}
         self.add_peers(list(peers), "magnet")
@@ -502,6 +537,7 @@ class TorrentSession:
                                   [(fd, n) for fd, (_, n) in zip(self.storage.fds,
                                                                   self.storage.paths)])
             self.picker.on_activate = self.wire.begin_piece
+            self.wire.set_pipeline(self.client.pipeline)
             self.wire.set_have(self.have.to_bytes())     # what unchoked peers may be served
         self.meta_ready.set()
         for p in list(self.peers.values()):
@@ -588,19 +624,100 @@ class TorrentSession:
     def peer_closed(self, pc: PeerConn) -> None:
         if self.peers.pop(id(pc), None) is None:
             return
-        released = bool(pc.inflight)
-        self.release_inflight(pc)
         if pc.bitfield is not None and self.picker is not None:
             self.picker.remove_peer(pc.bitfield, id(pc))
+        self.release_inflight(pc)
         self._wake.set()
-        if released and not self._closed:
-            self._refill_all()
 
     def release_inflight(self, pc: PeerConn) -> None:
+        """The peer choked us or went away: what it was asked for is free again - its block
+        requests, and the pieces its native wire was requesting (made ordinary, their received
+        blocks kept). Every other connection is offered them."""
+        released = bool(pc.inflight)
         if self.picker is not None:
             for (piece, begin) in list(pc.inflight):
                 self.picker.release(id(pc), piece, begin)
+            if pc.wire is not None and self._owned_mode:
+                try:
+                    back = self.wire.release(id(pc))
+                except Exception:
+                    back = []
+                for idx, states in back:
+                    ap = self.picker.active.get(idx)
+                    if ap is not None and ap.owner == id(pc):
+                        self._to_block_mode(ap, states, None)
+                        self.stats["wire_released"] += 1
+                        released = True
         pc.inflight.clear()
+        if released and not self._closed:
+            self._refill_all()
+
+    def _to_block_mode(self, ap: "_Active", states: bytes, owner: Optional[PeerConn]) -> None:
+        """An owned piece goes back to per-block requesting: received blocks stay, blocks the
+        owner still has requests out for stay its (``owner``: endgame) or are freed."""
+        oid = ap.owner
+        ap.owner = None
+        ap.state = bytearray(states)
+        ap.req = {}
+        ap.got = 0
+        now = time.monotonic()
+        for b, st in enumerate(ap.state):
+            if st == 2:
+                ap.got += 1
+            elif st == 1:
+                if owner is not None and not owner.closed:
+                    ap.req[b] = {oid}
+                    owner.inflight[(ap.idx, b * BLOCK)] = now
+                else:
+                    ap.state[b] = 0
+        if ap.got:
+            ap.peers.add(oid)
+            self.downloaded += min(ap.size, ap.got * BLOCK)
+
+    def _assign(self, pc: PeerConn) -> bool:
+        """Keep two pipelines of blocks queued on the connection's native wire, a whole piece
+        at a time. False when no piece was left for it (the endgame may begin)."""
+        me, want = id(pc), 2 * self.client.pipeline
+        wire, picker = self.wire, self.picker
+        try:
+            t = wire.todo(me)
+            while t < want:
+                idx = picker.take_piece(me, pc.bitfield)
+                if idx < 0:
+                    # nothing left to start: once this connection is down to its last
+                    # pipeline, the endgame begins (the others' queues become duplicable)
+                    if t < self.client.pipeline and picker.no_candidates():
+                        self._enter_endgame()
+                    return False
+                try:
+                    t = wire.assign(me, idx)
+                except Exception:
+                    # the connection is gone: the piece stays active, all blocks free
+                    ap = picker.active[idx]
+                    ap.owner = None
+                    ap.state = bytearray(ap.nblocks)
+                    raise
+        except Exception:
+            return False
+        return True
+
+    def _enter_endgame(self) -> None:
+        """Every missing piece is being fetched: owned pieces go back to per-block requesting
+        (their outstanding requests kept as the owner's), so idle connections can duplicate
+        the last blocks like on the Python wire."""
+        if self._endgame or self.wire is None:
+            return
+        self._endgame = True
+        for idx, ap in list(self.picker.active.items()):
+            if ap.owner is None:
+                continue
+            r = self.wire.release_piece(idx)
+            if r is None:
+                continue            # complete, being verified: its result still finds the owner
+            oid, states = r
+            self._to_block_mode(ap, states, self.peers.get(oid))
+            self.stats["wire_endgame_pieces"] += 1
+        self._refill_all()
 
     async def update_interest(self, pc: PeerConn) -> None:
         if self.picker is None or pc.bitfield is None:
@@ -631,6 +748,10 @@ class TorrentSession:
             pc.last_rx = now
             if kind == EV_BLOCKS:
                 self._wire_blocks(pc, data)
+            elif kind == EV_NEED:
+                if not pc.fill_queued:
+                    pc.fill_queued = True
+                    pc._wq.put_nowait((EV_FILL, None))
             else:
                 pc._wq.put_nowait((kind, data))
 
@@ -690,6 +811,18 @@ class TorrentSession:
             ap = self._verifying_ap.pop(idx, None)
             if self.picker is None:
                 continue
+            if ap is None:
+                # an owned piece (or one released with every block already in): its blocks
+                # were never booked one by one, this result is the first Python hears of it
+                ap = self.picker.active.get(idx)
+                if ap is not None:
+                    self.picker.complete_blocks(idx)
+                    if ap.owner is not None:
+                        ap.peers.add(ap.owner)
+                        self.downloaded += ap.size
+                        owner = self.peers.get(ap.owner)
+                        if owner is not None:
+                            owner.down_bytes += ap.size
             if status == 1:
                 await self._piece_complete(idx)
             elif status == 2:
@@ -741,6 +874,11 @@ class TorrentSession:
         b = begin // BLOCK
         if ap.state[b] == 2 or len(data) != ap.block_len(b):
             return False
+        if ap.buf is None:
+            # a Python-framed connection of a native-wire session (its socket could not be
+            # handed over): the piece is assembled natively
+            self._native_take(pc, ap, idx, begin, data)
+            return False
         ap.buf[begin:begin + len(data)] = data
         ap.state[b] = 2
         ap.got += 1
@@ -753,20 +891,43 @@ class TorrentSession:
             return True
         return False
 
+    def _native_take(self, pc: PeerConn, ap: "_Active", idx: int, begin: int, data) -> None:
+        st = self.wire.take_block(idx, begin, data) if self.wire is not None else 0
+        if not st:
+            return
+        b = begin // BLOCK
+        ap.state[b] = 2
+        ap.got += 1
+        ap.peers.add(id(pc))
+        self.downloaded += len(data)
+        rs = ap.req.pop(b, None)
+        if rs is not None and (len(rs) > 1 or id(pc) not in rs):
+            self._spawn(self.cancel_dups(pc, rs, idx, begin, len(data)))
+        if st == 2 and self.picker.complete_blocks(idx):
+            self._verifying_ap[idx] = ap
+
     async def block_followup(self, pc: PeerConn, idx: int, begin: int, ln: int) -> None:
         ent = self._followup.pop((idx, begin // BLOCK), None)
         if ent is not None:
             await self._block_done(pc, ent[0], ent[1], idx, begin, ln)
 
     async def fill(self, pc: PeerConn) -> None:
-        if self.picker is None or pc.peer_choking or not pc.am_interested or pc.bitfield is None:
+        if self.picker is None or pc.closed or pc.peer_choking or not pc.am_interested \
+                or pc.bitfield is None:
             return
+        fresh = dups = True
+        if pc.wire is not None and self._owned_mode and not self._endgame:
+            # whole pieces go to the wire; below, only free blocks of ordinary pieces (one a
+            # choked or closed peer left) are requested per block, and duplicates once every
+            # missing piece is being fetched
+            fresh = False
+            dups = not self._assign(pc) and self._endgame
         room = self.client.pipeline - len(pc.inflight)
         # Refill in batches (at least a quarter of the pipeline) so one write carries many
         # REQUEST messages instead of one syscall per 17-byte message.
         if room < max(1, self.client.pipeline // 4):
             return
-        blocks = self.picker.next_blocks(id(pc), pc.bitfield, room)
+        blocks = self.picker.next_blocks(id(pc), pc.bitfield, room, fresh, dups)
         if blocks:
             await pc.request_many(blocks)
 

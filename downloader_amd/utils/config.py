@@ -245,6 +245,10 @@ class DownloadConfig(BaseModel):
     # peer connections framed, assembled, SHA-1'd (16 pieces at a time) and written by the
     # native wire after the handshake (csrc/peerwire.cpp); False: all in Python (peer.py)
     torrent_native_wire: bool = True
+    # the native wire requests whole pieces assigned to a connection by itself, keeping the
+    # pipeline full from its reader thread (Python books a piece, not 256 blocks); the endgame
+    # and pieces a choking / closing peer leaves go back to per-block requests
+    torrent_wire_requests: bool = True
     # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
     # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the host
     # when it has the AVX-512 multi-buffer SHA-1, else the device. Config 6 (2 GB, 4 seeders):

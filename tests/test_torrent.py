@@ -235,11 +235,14 @@ def test_bad_peer_data_is_rejected_and_refetched(run, tmp_path):
     run(go(), timeout=90)
 
 
-@pytest.mark.parametrize("native_wire", [True, False])
-def test_swarm_native_and_python_wire(run, tmp_path, native_wire):
+@pytest.mark.parametrize("native_wire,wire_requests", [(True, True), (True, False),
+                                                       (False, False)])
+def test_swarm_native_and_python_wire(run, tmp_path, native_wire, wire_requests):
     """The peer wire both ways (download.torrent_native_wire): multi-file pieces straddling
     file boundaries from two seeders. Natively every piece is assembled, SHA-1'd and written
-    by csrc/peerwire.cpp (its counters say so); in Python by peer.py/session.py."""
+    by csrc/peerwire.cpp (its counters say so), its blocks requested by the wire itself
+    (download.torrent_wire_requests) or one by one from Python; in Python by
+    peer.py/session.py."""
     async def go():
         src = tmp_path / "seed"
         data = _tree(src / "Pack", {"a.mkv": 1_000_003, "S1/b.mkv": 377_777, "S1/c.mkv": 5})
@@ -249,7 +252,8 @@ def test_swarm_native_and_python_wire(run, tmp_path, native_wire):
             c = await TorrentClient(native_wire=native_wire).start()
             await c.add_torrent(parse_torrent(raw), str(src))
             seeders.append(c)
-        leech = await TorrentClient(native_wire=native_wire, pipeline=32).start()
+        leech = await TorrentClient(native_wire=native_wire, pipeline=32,
+                                    wire_requests=wire_requests).start()
         meta = parse_torrent(raw)
         s = await leech.add_torrent(meta, str(tmp_path / "dl"),
                                     peers=[("127.0.0.1", c.listen_port) for c in seeders])
@@ -265,6 +269,14 @@ def test_swarm_native_and_python_wire(run, tmp_path, native_wire):
             served = sum(ss.wire.stats()["served_bytes"] for c in seeders
                          for ss in c.sessions.values())
             assert served >= meta.total_length
+            if wire_requests:
+                # whole pieces were handed to the wire, which asked for their blocks itself
+                # (on a torrent this small every piece is handed out at once, and the endgame
+                # soon turns most back to per-block requests; config 6 has the wire request
+                # 99.6 % of the blocks of 2 GB itself, profiles/r5/)
+                assert st["assigned"] > 0 and st["requests"] > 0
+            else:
+                assert st["assigned"] == 0 and st["requests"] == 0
         else:
             assert s.wire is None
         await leech.close()
@@ -337,6 +349,68 @@ def test_native_wire_bad_piece_is_refetched_and_peer_blamed(run, tmp_path):
         _check(tmp_path / "dl", data)
         assert s.wire.stats()["hash_fails"] >= 1 and s.stats["hash_fails"] >= 1
         await leech.close(); await seeder.close(); await good.close()
+    run(go(), timeout=90)
+
+
+@pytest.mark.parametrize("then", ["choke", "close"])
+def test_native_wire_choked_or_closed_owner_releases_its_pieces(run, tmp_path, then):
+    """Pieces the native wire requests by itself for one connection go back to per-block
+    requesting when that peer chokes us or hangs up half-way: the blocks it delivered are
+    kept, the rest are fetched from the other seeder, and every piece verifies."""
+    from downloader_amd.torrent.peer import handshake_bytes
+
+    async def go():
+        raw, data, seeder, _ = await _seed(tmp_path, {"x.mkv": 3_000_000}, piece=65536)
+        m = parse_torrent(raw)
+        blob = data["x.mkv"]
+        answered = []
+
+        async def fake_peer(r, w):
+            # handshake, all pieces, unchoke; answer 10 requests, then choke (or close)
+            await r.readexactly(68)
+            w.write(handshake_bytes(m.info_hash, b"-XX0001-" + b"2" * 12, False))
+            bits = bytearray((m.num_pieces + 7) // 8)
+            for i in range(m.num_pieces):
+                bits[i // 8] |= 0x80 >> (i % 8)
+            w.write(struct.pack(">IB", 1 + len(bits), 5) + bytes(bits))
+            w.write(struct.pack(">IB", 1, 1))
+            try:
+                while True:
+                    n = int.from_bytes(await r.readexactly(4), "big")
+                    body = await r.readexactly(n) if n else b""
+                    if not body or body[0] != 6:
+                        continue
+                    if len(answered) >= 10:
+                        if then == "close":
+                            w.close()
+                            return
+                        if len(answered) == 10:
+                            answered.append(None)
+                            w.write(struct.pack(">IB", 1, 0))          # CHOKE
+                        continue
+                    idx, begin, ln = struct.unpack(">III", body[1:13])
+                    off = idx * m.piece_length + begin
+                    w.write(struct.pack(">IBII", 9 + ln, 7, idx, begin) + blob[off:off + ln])
+                    answered.append((idx, begin))
+                    await w.drain()
+            except (asyncio.IncompleteReadError, ConnectionError):
+                pass
+
+        srv = await asyncio.start_server(fake_peer, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        leech = await TorrentClient(pipeline=8).start()
+        s = await leech.add_torrent(m, str(tmp_path / "dl"), peers=[("127.0.0.1", port)])
+        while len(answered) < 10:
+            await asyncio.sleep(0.01)
+        await asyncio.sleep(0.2)
+        assert not s.done.is_set()
+        s.add_peers([("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        assert s.stats["wire_released"] >= 1 and s.stats["hash_fails"] == 0
+        assert s.wire.stats()["assigned"] >= 2
+        await leech.close(); await seeder.close()
+        srv.close()
     run(go(), timeout=90)
 
 
