@@ -260,7 +260,7 @@ class SwarmWire {
   // Verify complete pieces on the installed GPU part hasher (gpu_part_api.h, the gfx950
   // PartHasher) instead of sha1_mb: piece buffers come from a pool page-locked for it, each
   // complete piece is submitted at once (the device batches them into sha1_lanes launches),
-  // a collector thread takes the digests in order, compares, writes. No hasher installed, or
+  // collector threads (one per verifier) take the digests in order, compare, write. No hasher installed, or
   // a part refused: sha1_mb as before.
   void set_gpu(bool on);
   void attach(int fd, uint64_t id, const std::string& prefix);
@@ -307,7 +307,7 @@ class SwarmWire {
   std::condition_variable gcv_;
   std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order
   bool gstop_ = false;
-  std::thread gthread_;
+  std::vector<std::thread> gthreads_;
   std::atomic<uint64_t> served_bytes_{0};
   uint64_t epoch_ = 0;
   SwarmWireStats stats_;

@@ -215,8 +215,12 @@ SwarmWire::SwarmWire(int verify_threads) {
     verifiers_.emplace_back([this] { verify_loop(); });
     pthread_setname_np(verifiers_.back().native_handle(), "wire-verify");
   }
-  gthread_ = std::thread([this] { gpu_loop(); });
-  pthread_setname_np(gthread_.native_handle(), "wire-gpu");
+  // digest collectors: each takes the oldest submitted piece, waits for it, compares and writes
+  // it (the page-cache write, ~0.1 CPU-s/GB, is spread like the host verifiers')
+  for (int i = 0; i < std::max(1, verify_threads); ++i) {
+    gthreads_.emplace_back([this] { gpu_loop(); });
+    pthread_setname_np(gthreads_.back().native_handle(), "wire-gpu");
+  }
 }
 
 SwarmWire::~SwarmWire() { close(); }
@@ -241,7 +245,9 @@ void SwarmWire::close() {
     gstop_ = true;
   }
   gcv_.notify_all();
-  if (gthread_.joinable()) gthread_.join();   // after the verifiers: nothing submits any more
+  for (auto& t : gthreads_)                 // after the verifiers: nothing submits any more
+    if (t.joinable()) t.join();
+  gthreads_.clear();
   {
     std::lock_guard<std::mutex> g(mu_);
     pieces_.clear();                        // their pooled buffers go back before the pool
@@ -579,7 +585,8 @@ void SwarmWire::verify_loop() {
   }
 }
 
-// The GPU's digests, in submission order (the device hashes them in parallel anyway).
+// The GPU's digests: each collector takes the oldest piece submitted and not yet claimed (the
+// device hashes them in parallel anyway), so results come back in about submission order.
 void SwarmWire::gpu_loop() {
   for (;;) {
     std::pair<std::shared_ptr<Piece>, uint64_t> job;
