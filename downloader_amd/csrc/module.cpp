@@ -333,12 +333,15 @@ PYBIND11_MODULE(_native, m) {
              d["gpu_errors"] = s.gpu_errors;
              d["pool_in_use"] = s.pool_in_use;      // process-wide piece buffers
              d["pool_idle"] = s.pool_idle;
+             d["pool_idle_bytes"] = s.pool_idle_bytes;
              d["pool_allocs"] = s.pool_allocs;      // (process lifetime)
              d["pool_frees"] = s.pool_frees;
              d["pool_locks"] = s.pool_locks;
              return d;
            })
       .def("close", &SwarmWire::close, py::call_guard<py::gil_scoped_release>());
+  m.def("swarm_piece_pool_limit", &swarm_piece_pool_limit, py::arg("bytes"),
+        "Keep at most `bytes` of idle swarm piece buffers (process-wide; the rest are freed)");
   m.def("relay_counters", []() {
     RelayCounters c = relay_counters();
     py::dict d;

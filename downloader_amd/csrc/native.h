@@ -165,6 +165,9 @@ const void* gpu_part_hasher_current();        // the installed hasher's API (nul
 // The swarm wire's idle piece buffers page-locked for this hasher API are unlocked and freed
 // (before the hasher itself is destroyed; peerwire.cpp).
 void swarm_piece_pool_forget(const void* api);
+// At most this many bytes of idle piece buffers are kept (beyond it they are freed now and on
+// release; download.swarm_pool_mb).
+void swarm_piece_pool_limit(size_t bytes);
 struct GpuPartStats {
   uint64_t submitted, host_fallbacks, refused, pending;
 };
@@ -223,7 +226,7 @@ struct SwarmWireStats {
   uint64_t served_bytes = 0;                                // blocks served with sendfile
   uint64_t assigned = 0, requests = 0;                      // owned pieces, REQUESTs the wire sent
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
-  size_t pool_in_use = 0, pool_idle = 0;                    // process-wide piece buffers
+  size_t pool_in_use = 0, pool_idle = 0, pool_idle_bytes = 0;   // process-wide piece buffers
   uint64_t pool_allocs = 0, pool_frees = 0, pool_locks = 0; // since start: buffers made /
                                                             // unmade, page-locked for a hasher
   size_t active_pieces = 0;

@@ -75,9 +75,12 @@ void put32(std::string& s, uint32_t v) {
 struct PiecePool {
   std::mutex mu;
   std::unordered_map<size_t, std::vector<std::pair<uint8_t*, const void*>>> idle;
-  size_t in_use = 0, idle_count = 0;
+  size_t in_use = 0, idle_count = 0, idle_bytes = 0;
   uint64_t allocs = 0, frees = 0, locks = 0;
-  static constexpr size_t kMaxIdle = 128;   // ~512 MiB of 4 MiB pieces kept
+  // Idle buffers kept (download.swarm_pool_mb): enough for the pieces in flight of a fast
+  // swarm - ~250 x 4 MiB at 7 GB/s behind the GPU's ~150 ms - or every new one costs ~1,000
+  // page faults in the reader that fills it and, in GPU mode, a page-locking.
+  size_t max_idle_bytes = (size_t)1 << 30;
 
   uint8_t* take(size_t n, const void** reg) {
     {
@@ -88,6 +91,7 @@ struct PiecePool {
         auto b = it->second.back();
         it->second.pop_back();
         idle_count--;
+        idle_bytes -= n;
         *reg = b.second;
         return b.first;
       }
@@ -110,9 +114,10 @@ struct PiecePool {
       in_use--;
       // a buffer locked for a hasher no longer installed goes (the API stays valid: retired
       // hashers are kept alive, ops/hashing.py)
-      if (idle_count < kMaxIdle && (!reg || reg == gpu_part_hasher_current())) {
+      if (idle_bytes + n <= max_idle_bytes && (!reg || reg == gpu_part_hasher_current())) {
         idle[n].push_back({b, reg});
         idle_count++;
+        idle_bytes += n;
         return;
       }
       frees++;
@@ -120,19 +125,22 @@ struct PiecePool {
     if (reg) ((const GpuPartHashApi*)reg)->unreg(((const GpuPartHashApi*)reg)->ctx, b);
     free(b);
   }
-  // Idle buffers page-locked for `api` are unlocked and freed (the hasher is going away).
-  void forget(const void* api) {
+  // Idle buffers page-locked for `api` (the hasher is going away; all == nullptr: every idle
+  // buffer), or beyond a new limit, are unlocked and freed.
+  void drop_idle(bool all, const void* api, size_t limit) {
     std::vector<std::pair<uint8_t*, const void*>> drop;
     {
       std::lock_guard<std::mutex> g(mu);
+      max_idle_bytes = limit;
       for (auto& kv : idle) {
         auto& v = kv.second;
         for (size_t i = 0; i < v.size();) {
-          if (v[i].second == api) {
+          if ((all && v[i].second == api) || idle_bytes > max_idle_bytes) {
             drop.push_back(v[i]);
             v[i] = v.back();
             v.pop_back();
             idle_count--;
+            idle_bytes -= kv.first;
             frees++;
           } else {
             ++i;
@@ -141,7 +149,8 @@ struct PiecePool {
       }
     }
     for (auto& b : drop) {
-      ((const GpuPartHashApi*)api)->unreg(((const GpuPartHashApi*)api)->ctx, b.first);
+      if (b.second)
+        ((const GpuPartHashApi*)b.second)->unreg(((const GpuPartHashApi*)b.second)->ctx, b.first);
       free(b.first);
     }
   }
@@ -155,8 +164,16 @@ PiecePool& piece_pool() {
 }  // namespace
 
 void swarm_piece_pool_forget(const void* api) {
-  if (api) piece_pool().forget(api);
+  PiecePool& p = piece_pool();
+  size_t limit;
+  {
+    std::lock_guard<std::mutex> g(p.mu);
+    limit = p.max_idle_bytes;
+  }
+  if (api) p.drop_idle(true, api, limit);
 }
+
+void swarm_piece_pool_limit(size_t bytes) { piece_pool().drop_idle(false, nullptr, bytes); }
 
 struct SwarmWire::Piece {
   uint32_t idx = 0;
@@ -1003,6 +1020,7 @@ SwarmWireStats SwarmWire::stats() {
     std::lock_guard<std::mutex> g2(pp.mu);
     s.pool_in_use = pp.in_use;
     s.pool_idle = pp.idle_count;
+    s.pool_idle_bytes = pp.idle_bytes;
     s.pool_allocs = pp.allocs;
     s.pool_frees = pp.frees;
     s.pool_locks = pp.locks;

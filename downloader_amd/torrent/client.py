@@ -32,8 +32,9 @@ class TorrentClient:
                  webseed_max_failures: int = 5,
                  idle_timeout: float = 120.0, connect_timeout: float = 10.0,
                  seed_after_done: bool = False, listen: bool = True,
-                 native_wire: bool = True, wire_verify_threads: int = 2,
-                 swarm_verify: str = "auto", wire_requests: bool = True):
+                 native_wire: bool = True, wire_verify_threads: int = 4,
+                 swarm_verify: str = "auto", wire_requests: bool = True,
+                 wire_pool_mb: int = 1024):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -65,6 +66,12 @@ class TorrentClient:
         self.swarm_verify = swarm_verify          # auto / gpu / cpu (native wire only)
         # whole pieces requested by the native wire itself (SwarmWire.assign), not per block
         self.wire_requests = wire_requests
+        if native_wire:
+            try:
+                from ..ops import native
+                native().swarm_piece_pool_limit(max(0, wire_pool_mb) << 20)
+            except Exception:
+                pass
         self.pex_interval = 60.0
         self.piece_cache_bytes = 64 << 20   # per-session LRU of pieces being served to peers
         self.dht_interval = 30.0
@@ -89,6 +96,7 @@ class TorrentClient:
                    native_wire=d.torrent_native_wire,
                    swarm_verify=d.swarm_verify_backend,
                    wire_requests=d.torrent_wire_requests,
+                   wire_verify_threads=d.swarm_verify_threads, wire_pool_mb=d.swarm_pool_mb,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

@@ -254,6 +254,12 @@ class DownloadConfig(BaseModel):
     # when it has the AVX-512 multi-buffer SHA-1, else the device. Config 6 (2 GB, 4 seeders):
     # 6.2 - 6.3 GB/s on the host vs 2.5 - 2.8 on the device (profiles/r5/swarm/)
     swarm_verify_backend: str = "auto"
+    # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
+    # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
+    swarm_verify_threads: int = 4
+    # idle swarm piece buffers kept per worker process (reused: no page faults per piece, and
+    # page-locked once in GPU mode)
+    swarm_pool_mb: int = 1024
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

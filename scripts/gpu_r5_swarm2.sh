@@ -7,14 +7,14 @@
 # process (the first is its cold one). The GPU test of the wire's device mode first.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm6}
+F=${OUT:-gpurun_out/r5_swarm7}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
 step gpu; timeout -k 10 300 python -u -m pytest tests/test_gpu_hash.py -m gpu -x -v --timeout 120 --timeout-method thread -k swarm > $F/pytest_gpu.txt 2>&1 || { tail -30 $F/pytest_gpu.txt; exit 1; }
 tail -1 $F/pytest_gpu.txt
 for i in 1 2 3; do
-  for v in python blocks owned owned_gpu; do
+  for v in ${VARIANTS:-python blocks owned owned_gpu}; do
     case $v in
       python) a="--wire python" ;;
       blocks) a="--wire native --swarm-verify cpu --wire-requests python" ;;

@@ -1360,3 +1360,30 @@ def test_worker_stages_a_base32_infohash_via_the_dht(run, tmp_path, make_cfg):
         assert s3.get("triton-staging", keys.object_key("b32", "film.mkv")) == data["film.mkv"]
         await w.stop(); await seeder.close(); await boot.close(); await s3.stop()
     run(go(), timeout=60)
+
+
+def test_swarm_piece_pool_is_bounded_in_bytes():
+    """The native wire's process-wide piece pool keeps released buffers for reuse up to
+    download.swarm_pool_mb; lowering the limit frees the idle ones beyond it at once."""
+    from downloader_amd.ops import native
+    n = native()
+    w = n.SwarmWire(1)
+    w.set_storage(65536, 4 * 65536, b"\0" * 80, [])
+    n.swarm_piece_pool_limit(1 << 30)
+    try:
+        for i in range(4):
+            w.begin_piece(i)
+        for i in range(4):
+            w.drop_piece(i)
+        st = w.stats()
+        assert st["pool_in_use"] == 0 and st["pool_idle_bytes"] >= 4 * 65536
+        n.swarm_piece_pool_limit(65536)
+        assert w.stats()["pool_idle_bytes"] <= 65536
+        w.begin_piece(0)
+        w.begin_piece(1)
+        w.drop_piece(0)
+        w.drop_piece(1)
+        assert w.stats()["pool_idle_bytes"] <= 65536
+    finally:
+        n.swarm_piece_pool_limit(1 << 30)
+        w.close()
