@@ -289,7 +289,9 @@ class SwarmWire {
   bool servable(uint32_t idx, uint32_t begin, uint32_t len);
   bool serve_block(Conn& c, const std::string& req);
   bool send_all(Conn& c, const char* p, size_t n, int flags);
-  void finish_piece(const Piece& p, const uint8_t* dig);   // compare, write, report
+  void finish_piece(std::shared_ptr<Piece> p, const uint8_t* dig);   // compare, then store
+  void store_loop();                                                  // the writer
+  void report(uint32_t idx, int status, const std::string& err);
   void gpu_loop();
   int take_from(Conn* c, uint32_t idx, uint32_t begin, const uint8_t* p, uint32_t len,
                 bool* owned, std::string* reqs, bool* need);
@@ -311,6 +313,11 @@ class SwarmWire {
   std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order
   bool gstop_ = false;
   std::vector<std::thread> gthreads_;
+  std::mutex smu_;
+  std::condition_variable scv_;
+  std::deque<std::shared_ptr<Piece>> sq_;       // verified pieces waiting for the writer
+  bool sstop_ = false;
+  std::thread sthread_;
   std::atomic<uint64_t> served_bytes_{0};
   uint64_t epoch_ = 0;
   SwarmWireStats stats_;

@@ -19,7 +19,8 @@
 //     receive batch (coalesced while Python has not polled: the busier the loop, the bigger
 //     the batches);
 //   * complete pieces are verified 16 at a time on the AVX-512 multi-buffer SHA-1 (sha1_mb),
-//     written to the storage files with pwrite, and reported as PIECE events;
+//     written to the storage files with pwrite by one writer thread, and reported as PIECE
+//     events;
 //   * one writer thread per connection sends what Python queues (requests, handshake-time
 //     messages) and serves the REQUESTs of peers Python has unchoked for pieces we have: the
 //     PIECE header, then the block straight from the storage files with sendfile (no copy
@@ -232,12 +233,15 @@ SwarmWire::SwarmWire(int verify_threads) {
     verifiers_.emplace_back([this] { verify_loop(); });
     pthread_setname_np(verifiers_.back().native_handle(), "wire-verify");
   }
-  // digest collectors: each takes the oldest submitted piece, waits for it, compares and writes
-  // it (the page-cache write, ~0.1 CPU-s/GB, is spread like the host verifiers')
+  // digest collectors: each takes the oldest submitted piece, waits for it and compares
   for (int i = 0; i < std::max(1, verify_threads); ++i) {
     gthreads_.emplace_back([this] { gpu_loop(); });
     pthread_setname_np(gthreads_.back().native_handle(), "wire-gpu");
   }
+  // one writer: page-cache writes into a file serialise on its inode anyway, and verifiers
+  // that wrote themselves spun on that lock (4 of them: 2x the write CPU of one)
+  sthread_ = std::thread([this] { store_loop(); });
+  pthread_setname_np(sthread_.native_handle(), "wire-store");
 }
 
 SwarmWire::~SwarmWire() { close(); }
@@ -265,6 +269,12 @@ void SwarmWire::close() {
   for (auto& t : gthreads_)                 // after the verifiers: nothing submits any more
     if (t.joinable()) t.join();
   gthreads_.clear();
+  {
+    std::lock_guard<std::mutex> g(smu_);
+    sstop_ = true;                          // (the writer drains its queue first)
+  }
+  scv_.notify_all();
+  if (sthread_.joinable()) sthread_.join();
   {
     std::lock_guard<std::mutex> g(mu_);
     pieces_.clear();                        // their pooled buffers go back before the pool
@@ -598,7 +608,8 @@ void SwarmWire::verify_loop() {
       stats_.verify_batches++;
       stats_.sha_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     }
-    for (size_t i = 0; i < host.size(); ++i) finish_piece(*host[i], (const uint8_t*)&dig[i * 20]);
+    for (size_t i = 0; i < host.size(); ++i)
+      finish_piece(std::move(host[i]), (const uint8_t*)&dig[i * 20]);
   }
 }
 
@@ -628,35 +639,62 @@ void SwarmWire::gpu_loop() {
       std::lock_guard<std::mutex> g(mu_);
       stats_.gpu_pieces++;
     }
-    finish_piece(p, dig);
+    finish_piece(std::move(job.first), dig);
   }
 }
 
-void SwarmWire::finish_piece(const Piece& p, const uint8_t* dig) {
+// A hashed piece: a mismatch is reported at once, a good one goes to the writer.
+void SwarmWire::finish_piece(std::shared_ptr<Piece> p, const uint8_t* dig) {
   bool ok;
   {
     std::lock_guard<std::mutex> g(mu_);
-    ok = memcmp(dig, hashes_.data() + (size_t)p.idx * 20, 20) == 0;
+    ok = memcmp(dig, hashes_.data() + (size_t)p->idx * 20, 20) == 0;
   }
-  std::string err;
-  if (ok) {
+  if (!ok) {
+    report(p->idx, 0, std::string());
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(smu_);
+    sq_.push_back(std::move(p));
+  }
+  scv_.notify_one();
+}
+
+void SwarmWire::store_loop() {
+  for (;;) {
+    std::shared_ptr<Piece> p;
+    {
+      std::unique_lock<std::mutex> lk(smu_);
+      scv_.wait(lk, [&] { return sstop_ || !sq_.empty(); });
+      if (sq_.empty()) return;
+      p = std::move(sq_.front());
+      sq_.pop_front();
+    }
     const auto w0 = std::chrono::steady_clock::now();
-    err = write_piece(p);
-    std::lock_guard<std::mutex> g(mu_);
-    stats_.write_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-        std::chrono::steady_clock::now() - w0).count();
+    std::string err = write_piece(*p);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stats_.write_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+          std::chrono::steady_clock::now() - w0).count();
+    }
+    report(p->idx, err.empty() ? 1 : 2, err);
   }
+}
+
+// PIECE event: 1 verified + written, 0 hash mismatch, 2 I/O error (+ message).
+void SwarmWire::report(uint32_t idx, int status, const std::string& err) {
   std::string ev;
-  put32(ev, p.idx);
-  ev.push_back(ok ? (err.empty() ? 1 : 2) : 0);   // 1 verified + written, 0 bad, 2 I/O
+  put32(ev, idx);
+  ev.push_back((char)status);
   ev += err;
   {
     std::lock_guard<std::mutex> g(mu_);
-    if (ok && err.empty()) {
+    if (status == 1) {
       stats_.verified++;
-      if (have_.size() <= p.idx / 8) have_.resize(p.idx / 8 + 1, 0);
-      have_[p.idx / 8] |= (uint8_t)(0x80 >> (p.idx % 8));   // servable from now on
-    } else if (!ok) {
+      if (have_.size() <= idx / 8) have_.resize(idx / 8 + 1, 0);
+      have_[idx / 8] |= (uint8_t)(0x80 >> (idx % 8));   // servable from now on
+    } else if (status == 0) {
       stats_.hash_fails++;
     }
   }
