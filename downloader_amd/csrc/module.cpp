@@ -265,8 +265,9 @@ PYBIND11_MODULE(_native, m) {
            py::arg("bits"))
       .def("set_have_piece", &SwarmWire::set_have_piece, py::arg("idx"))
       .def("set_serving", &SwarmWire::set_serving, py::arg("conn_id"), py::arg("on"))
-      .def("set_gpu", &SwarmWire::set_gpu, py::arg("on"),
-           "Verify complete pieces on the installed GPU part hasher (set_gpu_part_hasher)")
+      .def("set_gpu", &SwarmWire::set_gpu, py::arg("on"), py::arg("max_inflight") = 64,
+           "Verify complete pieces on the installed GPU part hasher (set_gpu_part_hasher), at "
+           "most max_inflight at once (the rest on the host)")
       .def("attach",
            [](SwarmWire& w, int fd, uint64_t id, const py::bytes& prefix) {
              w.attach(fd, id, std::string(prefix));
@@ -331,6 +332,7 @@ PYBIND11_MODULE(_native, m) {
              d["gpu_pieces"] = s.gpu_pieces;
              d["gpu_refused"] = s.gpu_refused;
              d["gpu_errors"] = s.gpu_errors;
+             d["gpu_overflow"] = s.gpu_overflow;    // hashed on the host: device full
              d["pool_in_use"] = s.pool_in_use;      // process-wide piece buffers
              d["pool_idle"] = s.pool_idle;
              d["pool_idle_bytes"] = s.pool_idle_bytes;

@@ -226,6 +226,7 @@ struct SwarmWireStats {
   uint64_t served_bytes = 0;                                // blocks served with sendfile
   uint64_t assigned = 0, requests = 0;                      // owned pieces, REQUESTs the wire sent
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
+  uint64_t gpu_overflow = 0;        // hashed on the host: max_inflight pieces on the device
   size_t pool_in_use = 0, pool_idle = 0, pool_idle_bytes = 0;   // process-wide piece buffers
   uint64_t pool_allocs = 0, pool_frees = 0, pool_locks = 0; // since start: buffers made /
                                                             // unmade, page-locked for a hasher
@@ -263,9 +264,10 @@ class SwarmWire {
   // Verify complete pieces on the installed GPU part hasher (gpu_part_api.h, the gfx950
   // PartHasher) instead of sha1_mb: piece buffers come from a pool page-locked for it, each
   // complete piece is submitted at once (the device batches them into sha1_lanes launches),
-  // collector threads (one per verifier) take the digests in order, compare, write. No hasher installed, or
-  // a part refused: sha1_mb as before.
-  void set_gpu(bool on);
+  // collector threads (one per verifier) take the digests in order and compare, the writer
+  // stores. At most max_inflight pieces are on the device at once: the rest, a piece the
+  // hasher refuses, or no hasher installed: sha1_mb as before.
+  void set_gpu(bool on, int max_inflight = 64);
   void attach(int fd, uint64_t id, const std::string& prefix);
   size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
   size_t pending_out(uint64_t id);
@@ -308,6 +310,7 @@ class SwarmWire {
   std::unordered_map<uint32_t, std::shared_ptr<Piece>> pieces_;
   std::vector<uint8_t> have_;                   // bitfield (BEP-3 bit order)
   std::atomic<bool> gpu_{false};
+  std::atomic<int> gpu_cap_{64}, gpu_inflight_{0};
   std::mutex gmu_;
   std::condition_variable gcv_;
   std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order

@@ -562,7 +562,10 @@ void SwarmWire::verify_loop() {
     std::vector<std::shared_ptr<Piece>> host;
     for (auto& p : batch) {
       uint64_t t = 0;
-      if (api) {
+      // the device takes pieces while fewer than gpu_cap_ are in flight on it (a 4 MiB piece
+      // spends ~75 ms there): past that the download outruns it, and the host hashes the
+      // rest instead of the pieces queueing (and their buffers piling up) behind the device
+      if (api && gpu_inflight_.load() < gpu_cap_.load()) {
         if (p->reg != api) {
           if (p->reg) ((const GpuPartHashApi*)p->reg)->unreg(((const GpuPartHashApi*)p->reg)->ctx, p->data);
           p->reg = api->reg(api->ctx, p->data, p->cap) == 0 ? api : nullptr;
@@ -574,13 +577,15 @@ void SwarmWire::verify_loop() {
         if (p->reg == api) t = api->submit(api->ctx, p->data, p->size, p->size);
       }
       if (t) {
+        gpu_inflight_.fetch_add(1);
         std::lock_guard<std::mutex> g(gmu_);
         gq_.push_back({std::move(p), t});
         gcv_.notify_one();
       } else {
         if (api) {
           std::lock_guard<std::mutex> g(mu_);
-          stats_.gpu_refused++;
+          if (gpu_inflight_.load() < gpu_cap_.load()) stats_.gpu_refused++;
+          else stats_.gpu_overflow++;
         }
         host.push_back(std::move(p));
       }
@@ -639,6 +644,7 @@ void SwarmWire::gpu_loop() {
       std::lock_guard<std::mutex> g(mu_);
       stats_.gpu_pieces++;
     }
+    gpu_inflight_.fetch_sub(1);
     finish_piece(std::move(job.first), dig);
   }
 }
@@ -701,7 +707,10 @@ void SwarmWire::report(uint32_t idx, int status, const std::string& err) {
   push(0, kEvPiece, std::move(ev));
 }
 
-void SwarmWire::set_gpu(bool on) { gpu_.store(on); }
+void SwarmWire::set_gpu(bool on, int max_inflight) {
+  gpu_cap_.store(std::max(1, max_inflight));
+  gpu_.store(on);
+}
 
 
 // The piece's bytes into the files it spans (pwrite; the storage owns the fds).

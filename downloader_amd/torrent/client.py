@@ -34,7 +34,7 @@ class TorrentClient:
                  seed_after_done: bool = False, listen: bool = True,
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
-                 wire_pool_mb: int = 1024):
+                 wire_pool_mb: int = 1024, wire_gpu_inflight: int = 64):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -66,6 +66,7 @@ class TorrentClient:
         self.swarm_verify = swarm_verify          # auto / gpu / cpu (native wire only)
         # whole pieces requested by the native wire itself (SwarmWire.assign), not per block
         self.wire_requests = wire_requests
+        self.wire_gpu_inflight = wire_gpu_inflight   # device-verified pieces at once (GPU mode)
         if native_wire:
             try:
                 from ..ops import native
@@ -97,6 +98,7 @@ class TorrentClient:
                    swarm_verify=d.swarm_verify_backend,
                    wire_requests=d.torrent_wire_requests,
                    wire_verify_threads=d.swarm_verify_threads, wire_pool_mb=d.swarm_pool_mb,
+                   wire_gpu_inflight=d.swarm_gpu_inflight,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

@@ -530,7 +530,7 @@ class TorrentSession:
                 on = False
             if not on and self.client.swarm_verify == "gpu":
                 raise TorrentError("swarm_verify_backend=gpu but no GPU part hasher")
-            self.wire.set_gpu(bool(on))
+            self.wire.set_gpu(bool(on), self.client.wire_gpu_inflight)
             self.stats["swarm_verify"] = "gpu" if on else "cpu"
         if self.wire is not None:
             self.wire.set_storage(meta.piece_length, meta.total_length, meta.pieces,

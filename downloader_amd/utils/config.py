@@ -260,6 +260,9 @@ class DownloadConfig(BaseModel):
     # idle swarm piece buffers kept per worker process (reused: no page faults per piece, and
     # page-locked once in GPU mode)
     swarm_pool_mb: int = 1024
+    # GPU mode: pieces on the device at once; past it the host hashes (a 4 MiB piece spends
+    # ~75 ms on the device, so 64 keep ~3.5 GB/s there)
+    swarm_gpu_inflight: int = 64
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -7,7 +7,7 @@
 # process (the first is its cold one). The GPU test of the wire's device mode first.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm8}
+F=${OUT:-gpurun_out/r5_swarm9}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }

@@ -326,6 +326,33 @@ def test_native_wire_pieces_verified_on_the_part_hasher(run, tmp_path):
         hashing.use_part_hasher(None)
 
 
+def test_native_wire_gpu_overflow_is_hashed_on_the_host(run, tmp_path):
+    """GPU mode with at most one piece on the (slow) device: the pieces that complete while it
+    is busy are SHA-1'd on the host instead of queueing behind it; every piece verifies."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 1_500_000}, piece=65536)
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=64,
+                                    wire_gpu_inflight=1).start()
+        meta = parse_torrent(raw)
+        s = await leech.add_torrent(meta, str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        st = s.wire.stats()
+        assert st["gpu_pieces"] >= 1 and st["gpu_overflow"] >= 1
+        assert st["gpu_pieces"] + st["gpu_overflow"] >= meta.num_pieces
+        assert st["verified"] == meta.num_pieces and st["hash_fails"] == 0
+        await leech.close(); await seeder.close()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.05), 4)
+    try:
+        run(go(), timeout=90)
+    finally:
+        hashing.use_part_hasher(None)
+
+
 def test_native_wire_bad_piece_is_refetched_and_peer_blamed(run, tmp_path):
     """A seeder serving a corrupt piece over the native wire: the native verifier rejects
     it (hash_fails), the session requeues it and gets it from the good seeder."""
