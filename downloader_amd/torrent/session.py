@@ -521,9 +521,9 @@ class TorrentSession:
         if self.wire is not None and want_gpu and meta.num_pieces > 1:
             # swarm pieces SHA-1'd by the gfx950 PartHasher (set up once per worker, off the
             # loop). `auto` only where the host lacks the AVX-512 multi-buffer SHA-1: config 6
-            # (2 GB, 4 seeders) on the MI355X box ran 6.2 - 6.3 GB/s verified on the host vs
-            # 2.5 - 2.8 GB/s on the device, whose ~75 ms per-piece latency lands on a job that
-            # short (profiles/r5/swarm/)
+            # (2 GB, 4 seeders) on the MI355X box ran 8.6 - 9.0 GB/s verified on the host vs
+            # 6.8 - 8.8 GB/s with up to 64 pieces on the device (~75 ms each) and the rest on
+            # the host (profiles/r5/swarm2/)
             try:
                 on = await loop.run_in_executor(None, hashing.gpu_relay_hashing)
             except Exception:

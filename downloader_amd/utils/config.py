@@ -252,7 +252,8 @@ class DownloadConfig(BaseModel):
     # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
     # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the host
     # when it has the AVX-512 multi-buffer SHA-1, else the device. Config 6 (2 GB, 4 seeders):
-    # 6.2 - 6.3 GB/s on the host vs 2.5 - 2.8 on the device (profiles/r5/swarm/)
+    # 8.6 - 9.0 GB/s on the host vs 6.8 - 8.8 with the device taking what it can
+    # (profiles/r5/swarm2/)
     swarm_verify_backend: str = "auto"
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
