@@ -2,6 +2,7 @@
 # Round 5 check of the tree: GPU tier (incl. swarm pieces on the gfx950 PartHasher), smoke,
 # the driver's bench line, then rocprofv3 kernel + memory-copy trace of the bench line's
 # same-call torrent A/B (the PartHasher's sha1_lanes launches inside the driver's command).
+# NOPROF=1: without the trace.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 F=$R/gpurun_out/${OUT_NAME:-r5_check}
@@ -19,6 +20,7 @@ j = json.load(open("$F/bench.json"))
 print("bench", j["value"], "p50", j["p50_job_latency_s"], "crc", j.get("crc_relay_MBps"), "util", j["cpu_utilisation"], j.get("crc_relay_cpu_utilisation"))
 print("torrent gpu", j.get("torrent_gpu_MBps"), j.get("torrent_gpu_MBps_runs"), "host", j.get("torrent_host_MBps"), j.get("torrent_host_MBps_runs"), "parts", j.get("gpu_parts"), "fallbacks", j.get("gpu_host_fallbacks"))
 PY
+[ -n "$NOPROF" ] && exit 0
 step prof
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $F/rocprof -o bench -- \
