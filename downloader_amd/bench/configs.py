@@ -498,8 +498,14 @@ async def config_swarm(a) -> Dict:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         verify = getattr(a, "swarm_verify", "auto")
         native_req = getattr(a, "wire_requests", "native") == "native"
+        extra = {}
+        if getattr(a, "swarm_gpu_inflight", 0):
+            extra["wire_gpu_inflight"] = a.swarm_gpu_inflight
+        if getattr(a, "swarm_pool_mb", 0):
+            extra["wire_pool_mb"] = a.swarm_pool_mb
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire,
-                                    swarm_verify=verify, wire_requests=native_req).start()
+                                    swarm_verify=verify, wire_requests=native_req,
+                                    **extra).start()
         if wire and verify == "gpu":
             # a worker sets its GPU up at start (download.gpu_prewarm), not inside a job
             from downloader_amd.ops import hashing
@@ -662,6 +668,10 @@ def main(argv=None) -> int:
                     help="config 6: peer connections on the native wire (csrc/peerwire.cpp) or "
                          "framed in Python (torrent/peer.py), leecher and seeders alike")
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
+    ap.add_argument("--swarm-gpu-inflight", type=int, default=0,
+                    help="config 6, GPU mode: pieces on the device at once (0: the default)")
+    ap.add_argument("--swarm-pool-mb", type=int, default=0,
+                    help="config 6: idle piece buffers kept (0: the default)")
     ap.add_argument("--wire-requests", choices=["native", "python"], default="native",
                     help="config 6, native wire: whole pieces requested by the wire itself, or "
                          "every block requested and booked in Python")
