@@ -299,6 +299,7 @@ class SwarmWire {
                 bool* owned, std::string* reqs, bool* need);
   bool pump(Conn& c, std::string* reqs);        // mu_ held
   void queue_out(Conn& c, std::string data);
+  void send_requests(Conn& c, std::string reqs);
   std::shared_ptr<Conn> conn(uint64_t id);
   std::string block_states(const Piece& p, const Conn* owner);   // mu_ held
 

@@ -197,6 +197,7 @@ struct SwarmWire::Conn {
   std::thread reader, writer;
   std::mutex wmu;
   std::condition_variable wcv;
+  std::mutex smu;                        // held while a whole message is being sent
   // FIFO of what to send: bytes from Python, or (serve != 0) a block to serve from storage:
   // piece, begin, length packed into `data`
   struct Item {
@@ -433,6 +434,27 @@ bool SwarmWire::pump(Conn& c, std::string* reqs) {
     return true;
   }
   return false;
+}
+
+// The reader's refill REQUESTs: sent right here when the writer is not mid-message (no
+// writer wake-up per receive batch, ~0.04 CPU-s/GB on config 6), else queued. A partial send
+// leaves the rest at the front of the queue, under smu, so it goes out next.
+void SwarmWire::send_requests(Conn& c, std::string reqs) {
+  if (!c.smu.try_lock()) {
+    queue_out(c, std::move(reqs));
+    return;
+  }
+  ssize_t w = ::send(c.fd, reqs.data(), reqs.size(), MSG_DONTWAIT | MSG_NOSIGNAL);
+  const size_t sent = w > 0 ? (size_t)w : 0;
+  if (sent < reqs.size()) {
+    std::lock_guard<std::mutex> g(c.wmu);
+    if (!c.stop) {
+      c.out_bytes += reqs.size() - sent;
+      c.out.push_front(Conn::Item{reqs.substr(sent), false});
+      c.wcv.notify_one();
+    }
+  }
+  c.smu.unlock();
 }
 
 void SwarmWire::queue_out(Conn& c, std::string data) {
@@ -858,7 +880,7 @@ void SwarmWire::read_loop(Conn& c) {
     }
     flush_blocks();
     if (!reqs.empty()) {
-      queue_out(c, std::move(reqs));      // one write for the whole batch's refill
+      send_requests(c, std::move(reqs));  // one write for the whole batch's refill
       reqs.clear();
     }
     if (need) {
@@ -972,11 +994,19 @@ bool SwarmWire::send_all(Conn& c, const char* p, size_t n, int flags) {
 
 void SwarmWire::write_loop(Conn& c) {
   for (;;) {
-    Conn::Item item;
     {
       std::unique_lock<std::mutex> lk(c.wmu);
       c.wcv.wait(lk, [&] { return c.stop || !c.out.empty(); });
       if (c.stop) return;
+    }
+    // the whole item goes out under smu, taken before the pop: a reader that sent part of its
+    // REQUESTs itself puts the rest at the front, and nothing may overtake it
+    std::lock_guard<std::mutex> sg(c.smu);
+    Conn::Item item;
+    {
+      std::lock_guard<std::mutex> lk(c.wmu);
+      if (c.stop) return;
+      if (c.out.empty()) continue;
       item = std::move(c.out.front());
       c.out.pop_front();
     }

@@ -991,7 +991,10 @@ class TorrentSession:
         for cb in self.piece_listeners:
             cb(idx)
         for p in list(self.peers.values()):
-            await p.send_have(idx)
+            # (not to a peer that has the piece: a seed gains nothing from it, and it costs a
+            # message per piece per seed)
+            if p.bitfield is None or idx not in p.bitfield:
+                await p.send_have(idx)
             if p.am_interested and p.bitfield is not None and \
                     not self.picker.peer_has_wanted(p.bitfield, id(p)):
                 await p.set_interested(False)
