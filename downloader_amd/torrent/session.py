@@ -92,6 +92,10 @@ class PiecePicker:
         self.n = meta.num_pieces
         self.avail = [0] * self.n
         self.active: Dict[int, _Active] = {}
+        # the active pieces requested block by block (not owned by a connection's native
+        # wire): the only ones the block loops below walk - with owned pieces, active also
+        # holds every piece awaiting its native verification
+        self.loose: Dict[int, _Active] = {}
         self.claimed: Set[int] = set()       # pieces owned by webseed workers
         self.verifying: Set[int] = set()     # all blocks in, SHA-1 / write in progress
         self.failed: Dict[int, int] = {}
@@ -202,8 +206,8 @@ class PiecePicker:
     def next_block(self, peer_id: int, bf: Bitfield, fresh: bool = True,
                    dups: bool = True) -> Optional[Tuple[int, int, int]]:
         # 1. a free block of an active piece this peer has
-        for ap in self.active.values():
-            if ap.idx in bf and ap.owner is None:
+        for ap in self.loose.values():
+            if ap.idx in bf:
                 for b in range(ap.nblocks):
                     if ap.state[b] == 0:
                         ap.state[b] = 1
@@ -216,14 +220,15 @@ class PiecePicker:
             if self.on_activate is not None:
                 self.on_activate(best)
             self.active[best] = ap
+            self.loose[best] = ap
             ap.state[0] = 1
             ap.req[0] = {peer_id}
             return best, 0, ap.block_len(0)
         # 3. endgame: duplicate an outstanding block this peer has not requested yet
         if not dups:
             return None
-        for ap in self.active.values():
-            if ap.idx in bf and ap.owner is None:
+        for ap in self.loose.values():
+            if ap.idx in bf:
                 for b in range(ap.nblocks):
                     if ap.state[b] == 1 and peer_id not in ap.req.get(b, ()):
                         ap.req.setdefault(b, set()).add(peer_id)
@@ -235,11 +240,12 @@ class PiecePicker:
         """Up to ``k`` blocks for one peer in one pass: free blocks of active pieces first,
         then whole new (rarest) pieces (``fresh``), then endgame duplicates (``dups``)."""
         out: List[Tuple[int, int, int]] = []
-        for ap in self.active.values():
+        if not fresh and not dups and not self.loose:
+            return out                  # (owned pieces only: nothing to request per block)
+        for ap in self.loose.values():
             if len(out) >= k:
                 return out
-            if ap.idx not in bf or ap.owner is not None or \
-                    ap.got + len(ap.req) >= ap.nblocks and 0 not in ap.state:
+            if ap.idx not in bf or ap.got + len(ap.req) >= ap.nblocks and 0 not in ap.state:
                 continue
             for b in range(ap.nblocks):
                 if ap.state[b] == 0:
@@ -289,6 +295,7 @@ class PiecePicker:
         (not a candidate again unless its hash check fails -> ``requeue``). False when it was
         not active any more: another follow-up (an endgame duplicate finishing the same
         piece) got there first and owns the verification."""
+        self.loose.pop(idx, None)
         if self.active.pop(idx, None) is None:
             return False
         self.verifying.add(idx)
@@ -657,6 +664,7 @@ class TorrentSession:
         owner still has requests out for stay its (``owner``: endgame) or are freed."""
         oid = ap.owner
         ap.owner = None
+        self.picker.loose[ap.idx] = ap
         ap.state = bytearray(states)
         ap.req = {}
         ap.got = 0
@@ -696,6 +704,7 @@ class TorrentSession:
                     ap = picker.active[idx]
                     ap.owner = None
                     ap.state = bytearray(ap.nblocks)
+                    picker.loose[idx] = ap
                     raise
         except Exception:
             return False

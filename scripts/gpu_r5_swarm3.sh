@@ -6,7 +6,7 @@
 # a smaller share of a longer job). 2 alternating rounds, 3 downloads per process.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm11}
+F=${OUT:-gpurun_out/r5_swarm12}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
