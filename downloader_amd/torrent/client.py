@@ -34,7 +34,8 @@ class TorrentClient:
                  seed_after_done: bool = False, listen: bool = True,
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
-                 wire_pool_mb: int = 1024, wire_gpu_inflight: int = 64):
+                 wire_pool_mb: int = 2048, wire_gpu_inflight: int = 512,
+                 swarm_gpu_min_bytes: int = 4 << 30):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -67,6 +68,7 @@ class TorrentClient:
         # whole pieces requested by the native wire itself (SwarmWire.assign), not per block
         self.wire_requests = wire_requests
         self.wire_gpu_inflight = wire_gpu_inflight   # device-verified pieces at once (GPU mode)
+        self.swarm_gpu_min_bytes = swarm_gpu_min_bytes   # `auto`: device from this size up
         if native_wire:
             try:
                 from ..ops import native
@@ -99,6 +101,7 @@ class TorrentClient:
                    wire_requests=d.torrent_wire_requests,
                    wire_verify_threads=d.swarm_verify_threads, wire_pool_mb=d.swarm_pool_mb,
                    wire_gpu_inflight=d.swarm_gpu_inflight,
+                   swarm_gpu_min_bytes=int(d.swarm_gpu_min_gb * (1 << 30)),
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

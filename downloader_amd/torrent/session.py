@@ -523,14 +523,16 @@ class TorrentSession:
         self.verified_bytes = sum(meta.piece_size(i) for i in range(meta.num_pieces)
                                   if i in self.have)
         self.picker = PiecePicker(meta, self.have)
-        want_gpu = self.client.swarm_verify == "gpu" or (
-            self.client.swarm_verify == "auto" and hashing.auto_may_use_gpu())
-        if self.wire is not None and want_gpu and meta.num_pieces > 1:
+        want_gpu = False
+        if self.wire is not None and meta.num_pieces > 1:
             # swarm pieces SHA-1'd by the gfx950 PartHasher (set up once per worker, off the
-            # loop). `auto` only where the host lacks the AVX-512 multi-buffer SHA-1: config 6
-            # (2 GB, 4 seeders) on the MI355X box ran 8.6 - 9.0 GB/s verified on the host vs
-            # 6.8 - 8.8 GB/s with up to 64 pieces on the device (~75 ms each) and the rest on
-            # the host (profiles/r5/swarm2/)
+            # loop): asked for, or `auto` on a torrent big enough to hide the device's
+            # per-piece latency (hashing.swarm_backend; the device check itself off the loop)
+            v = self.client.swarm_verify
+            want_gpu = v == "gpu" or (v == "auto" and await loop.run_in_executor(
+                None, hashing.swarm_backend, v, meta.total_length,
+                self.client.swarm_gpu_min_bytes) == "gpu")
+        if want_gpu:
             try:
                 on = await loop.run_in_executor(None, hashing.gpu_relay_hashing)
             except Exception:

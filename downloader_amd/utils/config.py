@@ -250,20 +250,21 @@ class DownloadConfig(BaseModel):
     # and pieces a choking / closing peer leaves go back to per-block requests
     torrent_wire_requests: bool = True
     # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
-    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the host
-    # when it has the AVX-512 multi-buffer SHA-1, else the device. Config 6 (2 GB, 4 seeders):
-    # 8.6 - 9.0 GB/s on the host vs 6.8 - 8.8 with the device taking what it can
-    # (profiles/r5/swarm2/)
+    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the device
+    # for torrents of swarm_gpu_min_gb and up (or on hosts without the AVX-512 multi-buffer
+    # SHA-1), else the host. Config 6 (4 seeders): at 8 GB the device is as fast at ~35 % less
+    # CPU per byte, at 2 GB the host is faster (profiles/r5/swarm3/)
     swarm_verify_backend: str = "auto"
+    swarm_gpu_min_gb: float = 4.0
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
     # idle swarm piece buffers kept per worker process (reused: no page faults per piece, and
-    # page-locked once in GPU mode)
-    swarm_pool_mb: int = 1024
-    # GPU mode: pieces on the device at once; past it the host hashes (a 4 MiB piece spends
-    # ~75 ms on the device, so 64 keep ~3.5 GB/s there)
-    swarm_gpu_inflight: int = 64
+    # page-locked once in GPU mode, where ~0.1 s of download is in flight on the device)
+    swarm_pool_mb: int = 2048
+    # GPU mode: pieces on the device at once (a 4 MiB piece spends ~75 ms there); past it the
+    # host hashes the overflow
+    swarm_gpu_inflight: int = 512
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -1414,3 +1414,18 @@ def test_swarm_piece_pool_is_bounded_in_bytes():
     finally:
         n.swarm_piece_pool_limit(1 << 30)
         w.close()
+
+
+def test_swarm_verify_backend_policy(monkeypatch):
+    """`auto` keeps small swarm torrents on the host's multi-buffer SHA-1 and sends big ones
+    (or any, on a host without it) to the device when there is one."""
+    from downloader_amd.ops import hashing
+    gb = 1 << 30
+    for mb, dev, size, want in [(True, True, 2 * gb, "cpu"), (True, True, 8 * gb, "gpu"),
+                                (True, False, 8 * gb, "cpu"), (False, True, 1 * gb, "gpu"),
+                                (False, False, 1 * gb, "cpu")]:
+        monkeypatch.setattr(hashing, "host_multibuffer", lambda mb=mb: mb)
+        monkeypatch.setattr(hashing, "gpu_available", lambda dev=dev: dev)
+        assert hashing.swarm_backend("auto", size, 4 * gb) == want, (mb, dev, size)
+    assert hashing.swarm_backend("cpu", 100 * gb, 4 * gb) == "cpu"
+    assert hashing.swarm_backend("gpu", 1, 4 * gb) == "gpu"
