@@ -34,8 +34,8 @@ class TorrentClient:
                  seed_after_done: bool = False, listen: bool = True,
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
-                 wire_pool_mb: int = 2048, wire_gpu_inflight: int = 512,
-                 swarm_gpu_min_bytes: int = 4 << 30):
+                 wire_pool_mb: int = 4096, wire_gpu_inflight: int = 1024,
+                 swarm_gpu_min_bytes: int = 8 << 30):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()

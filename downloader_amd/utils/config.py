@@ -255,16 +255,17 @@ class DownloadConfig(BaseModel):
     # SHA-1), else the host. Config 6 (4 seeders): at 8 GB the device is as fast at ~35 % less
     # CPU per byte, at 2 GB the host is faster (profiles/r5/swarm3/)
     swarm_verify_backend: str = "auto"
-    swarm_gpu_min_gb: float = 4.0
+    swarm_gpu_min_gb: float = 8.0
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
     # idle swarm piece buffers kept per worker process (reused: no page faults per piece, and
-    # page-locked once in GPU mode, where ~0.1 s of download is in flight on the device)
-    swarm_pool_mb: int = 2048
-    # GPU mode: pieces on the device at once (a 4 MiB piece spends ~75 ms there); past it the
-    # host hashes the overflow
-    swarm_gpu_inflight: int = 512
+    # page-locked once in GPU mode, where the download runs up to ~0.5 s ahead of the device)
+    swarm_pool_mb: int = 4096
+    # GPU mode: pieces on the device at once (a 4 MiB piece spends ~75 ms there plus its wait
+    # for a compute stream); past it the host hashes the overflow. 512 overflowed on config 6
+    # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/r5/swarm3/)
+    swarm_gpu_inflight: int = 1024
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -1,15 +1,17 @@
 #!/bin/bash
 # Round 5, fourth swarm call: config 6 at 2, 4 and 8 GB with pieces SHA-1'd on the host
-# (--swarm-verify cpu) vs on the gfx950 PartHasher (--swarm-verify gpu; defaults: up to 512
-# pieces on the device, 2 GB of idle piece buffers kept), to place download.swarm_gpu_min_gb
+# (--swarm-verify cpu) vs on the gfx950 PartHasher (--swarm-verify gpu; the download.swarm_gpu_inflight / swarm_pool_mb defaults)
+# to place download.swarm_gpu_min_gb
 # (where `auto` switches to the device). 2 alternating rounds, 3 downloads per process.
+# SCALES="4 8": other sizes (x GB of 2).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm13}
+F=${OUT:-gpurun_out/r5_swarm14}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
-for sc in 1 2 4; do
+df -h /tmp | tail -1
+for sc in ${SCALES:-1 2 4}; do
   for i in 1 2; do
     for v in cpu gpu; do
       step "$v x$sc $i"
