@@ -305,15 +305,13 @@ def auto_may_use_gpu() -> bool:
 def swarm_backend(requested: str, total_bytes: int, gpu_min_bytes: int) -> str:
     """Where the native peer wire SHA-1s a swarm torrent's pieces. ``auto``: the device when
     the host lacks the AVX-512 multi-buffer SHA-1, or for a torrent of at least
-    ``gpu_min_bytes`` - long enough that the ~75 ms a piece spends on the device is hidden,
-    so the download runs as fast as on the host at ~35 % less CPU per byte (config 6 at 8 GB:
-    7.2 - 8.4 vs 7.8 - 8.1 GB/s, 0.32 - 0.37 vs 0.49 - 0.51 CPU-s/GB; at 2 GB the host is
-    faster, profiles/r5/swarm3/)."""
+    ``gpu_min_bytes`` (0: never) - the device costs 20 - 40 % less CPU per byte and runs
+    20 - 35 % slower on config 6 (profiles/r5/swarm3/), a trade for CPU-bound nodes."""
     if requested == "cpu":
         return "cpu"
     if requested == "gpu":
         return "gpu"
-    if host_multibuffer() and total_bytes < gpu_min_bytes:
+    if host_multibuffer() and not (gpu_min_bytes and total_bytes >= gpu_min_bytes):
         return "cpu"
     return "gpu" if gpu_available() else "cpu"
 

@@ -250,12 +250,15 @@ class DownloadConfig(BaseModel):
     # and pieces a choking / closing peer leaves go back to per-block requests
     torrent_wire_requests: bool = True
     # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
-    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the device
-    # for torrents of swarm_gpu_min_gb and up (or on hosts without the AVX-512 multi-buffer
-    # SHA-1), else the host. Config 6 (4 seeders): at 8 GB the device is as fast at ~35 % less
-    # CPU per byte, at 2 GB the host is faster (profiles/r5/swarm3/)
+    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the host
+    # when it has the AVX-512 multi-buffer SHA-1 (else the device), and the device for torrents
+    # of swarm_gpu_min_gb and up when that is set (0: never). Config 6 (4 seeders) on the box:
+    # the device costs 20 - 40 % less leech CPU per byte and runs 20 - 35 % slower (2 GB:
+    # 5.7 - 5.9 vs 7.3 - 8.6 GB/s at 0.29 - 0.32 vs 0.46 - 0.51 CPU-s/GB; 16 GB: 6.7 - 7.0 vs
+    # 8.5 - 8.7 at 0.36 - 0.38 vs 0.47 - 0.48, profiles/r5/swarm3/) - worth it where the
+    # workers' CPUs, not one job's rate, are the limit
     swarm_verify_backend: str = "auto"
-    swarm_gpu_min_gb: float = 8.0
+    swarm_gpu_min_gb: float = 0.0
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4

@@ -1427,5 +1427,8 @@ def test_swarm_verify_backend_policy(monkeypatch):
         monkeypatch.setattr(hashing, "host_multibuffer", lambda mb=mb: mb)
         monkeypatch.setattr(hashing, "gpu_available", lambda dev=dev: dev)
         assert hashing.swarm_backend("auto", size, 4 * gb) == want, (mb, dev, size)
+    monkeypatch.setattr(hashing, "host_multibuffer", lambda: True)
+    monkeypatch.setattr(hashing, "gpu_available", lambda: True)
+    assert hashing.swarm_backend("auto", 100 * gb, 0) == "cpu"      # 0: never by size
     assert hashing.swarm_backend("cpu", 100 * gb, 4 * gb) == "cpu"
     assert hashing.swarm_backend("gpu", 1, 4 * gb) == "gpu"
