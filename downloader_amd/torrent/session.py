@@ -781,6 +781,9 @@ class TorrentSession:
         for idx, begin, ln, st in struct.iter_unpack(">IIII", data):
             inflight_pop((idx, begin), None)
             if not st:
+                # not taken (a duplicate, a bad length, a piece no longer assembling): if this
+                # peer was the one asked, the block is free again rather than stuck requested
+                picker.release(me, idx, begin)
                 continue
             got_bytes += ln
             if idx != last_idx:                    # blocks of one piece come in runs
