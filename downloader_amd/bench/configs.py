@@ -503,6 +503,8 @@ async def config_swarm(a) -> Dict:
             extra["wire_gpu_inflight"] = a.swarm_gpu_inflight
         if getattr(a, "swarm_pool_mb", 0):
             extra["wire_pool_mb"] = a.swarm_pool_mb
+        if getattr(a, "swarm_gpu_tail_mb", None) is not None:
+            extra["swarm_gpu_tail_bytes"] = a.swarm_gpu_tail_mb << 20
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire,
                                     swarm_verify=verify, wire_requests=native_req,
                                     **extra).start()
@@ -670,6 +672,8 @@ def main(argv=None) -> int:
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
     ap.add_argument("--swarm-gpu-inflight", type=int, default=0,
                     help="config 6, GPU mode: pieces on the device at once (0: the default)")
+    ap.add_argument("--swarm-gpu-tail-mb", type=int, default=None,
+                    help="config 6, GPU mode: the last MB hashed on the host (default: config)")
     ap.add_argument("--swarm-pool-mb", type=int, default=0,
                     help="config 6: idle piece buffers kept (0: the default)")
     ap.add_argument("--wire-requests", choices=["native", "python"], default="native",

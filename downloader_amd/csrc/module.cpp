@@ -265,6 +265,8 @@ PYBIND11_MODULE(_native, m) {
            py::arg("bits"))
       .def("set_have_piece", &SwarmWire::set_have_piece, py::arg("idx"))
       .def("set_serving", &SwarmWire::set_serving, py::arg("conn_id"), py::arg("on"))
+      .def("set_host_tail", &SwarmWire::set_host_tail, py::arg("on"),
+           "GPU mode: hash the pieces completing from now on on the host (the download's end)")
       .def("set_gpu", &SwarmWire::set_gpu, py::arg("on"), py::arg("max_inflight") = 64,
            "Verify complete pieces on the installed GPU part hasher (set_gpu_part_hasher), at "
            "most max_inflight at once (the rest on the host)")

@@ -268,6 +268,9 @@ class SwarmWire {
   // stores. At most max_inflight pieces are on the device at once: the rest, a piece the
   // hasher refuses, or no hasher installed: sha1_mb as before.
   void set_gpu(bool on, int max_inflight = 64);
+  // GPU mode, the end of the download: pieces completing from now on are hashed on the host
+  // (the last ~100 ms of download would otherwise wait out the device's per-piece latency).
+  void set_host_tail(bool on);
   void attach(int fd, uint64_t id, const std::string& prefix);
   size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
   size_t pending_out(uint64_t id);
@@ -312,6 +315,7 @@ class SwarmWire {
   std::vector<uint8_t> have_;                   // bitfield (BEP-3 bit order)
   std::atomic<bool> gpu_{false};
   std::atomic<int> gpu_cap_{64}, gpu_inflight_{0};
+  std::atomic<bool> host_tail_{false};
   std::mutex gmu_;
   std::condition_variable gcv_;
   std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order

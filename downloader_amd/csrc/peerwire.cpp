@@ -570,7 +570,7 @@ void SwarmWire::verify_loop() {
       // 4 MiB piece completes every ~1 ms) before hashing a short batch - a piece's HAVE is
       // late by at most this much (system_clock: steady-clock waits are invisible to GCC 11's
       // TSan, part_dispatch.h). The GPU batches by itself: no wait there.
-      if (vq_.size() < 16 && !vstop_ && !gpu_.load())
+      if (vq_.size() < 16 && !vstop_ && !(gpu_.load() && !host_tail_.load()))
         vcv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(20),
                         [&] { return vstop_ || vq_.size() >= 16; });
       while (!vq_.empty() && batch.size() < 16) {
@@ -580,7 +580,8 @@ void SwarmWire::verify_loop() {
     }
     // GPU mode: submit each piece to the installed hasher, the collector finishes it
     const GpuPartHashApi* api =
-        gpu_.load() ? (const GpuPartHashApi*)gpu_part_hasher_current() : nullptr;
+        gpu_.load() && !host_tail_.load() ? (const GpuPartHashApi*)gpu_part_hasher_current()
+                                          : nullptr;
     std::vector<std::shared_ptr<Piece>> host;
     for (auto& p : batch) {
       uint64_t t = 0;
@@ -728,6 +729,8 @@ void SwarmWire::report(uint32_t idx, int status, const std::string& err) {
   }
   push(0, kEvPiece, std::move(ev));
 }
+
+void SwarmWire::set_host_tail(bool on) { host_tail_.store(on); }
 
 void SwarmWire::set_gpu(bool on, int max_inflight) {
   gpu_cap_.store(std::max(1, max_inflight));

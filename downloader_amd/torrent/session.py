@@ -284,11 +284,15 @@ class PiecePicker:
         self.active[best] = ap
         return best
 
+    def unstarted(self) -> int:
+        """Missing pieces not active, not being verified and not claimed by a webseed."""
+        return self.n - self.have.count - len(self.active) - len(self.verifying) \
+            - len(self.claimed)
+
     def no_candidates(self) -> bool:
         """Every missing piece is active, being verified or claimed by a webseed: the
         endgame."""
-        return self.n - self.have.count - len(self.active) - len(self.verifying) \
-            - len(self.claimed) <= 0
+        return self.unstarted() <= 0
 
     def complete_blocks(self, idx: int) -> bool:
         """All blocks of active piece ``idx`` arrived: it leaves ``active`` for ``verifying``
@@ -445,6 +449,10 @@ class TorrentSession:
         # whole pieces requested by the wire itself (SwarmWire.assign) until the endgame
         self._owned_mode = bool(client.native_wire and client.wire_requests)
         self._endgame = False
+        # GPU mode: the wire's pieces go to the GPU part hasher, except once no more than
+        # _tail_bytes are left to start (_host_tail)
+        self._host_tail = False
+        self._tail_bytes = 0
         if client.native_wire:
             try:
                 from ..ops import native
@@ -540,6 +548,9 @@ class TorrentSession:
             if not on and self.client.swarm_verify == "gpu":
                 raise TorrentError("swarm_verify_backend=gpu but no GPU part hasher")
             self.wire.set_gpu(bool(on), self.client.wire_gpu_inflight)
+            # (at most a quarter of the torrent: a small one stays mostly on the device)
+            self._tail_bytes = min(self.client.swarm_gpu_tail_bytes,
+                                   meta.total_length // 4) if on else 0
             self.stats["swarm_verify"] = "gpu" if on else "cpu"
         if self.wire is not None:
             self.wire.set_storage(meta.piece_length, meta.total_length, meta.pieces,
@@ -699,6 +710,12 @@ class TorrentSession:
                     if t < self.client.pipeline and picker.no_candidates():
                         self._enter_endgame()
                     return False
+                if self._tail_bytes and not self._host_tail and picker.unstarted() * \
+                        self.meta.piece_length <= self._tail_bytes:
+                    # the last pieces are hashed on the host: on the device each would add its
+                    # ~75 ms (and its wait for a compute stream) to the end of the job
+                    self._host_tail = True
+                    wire.set_host_tail(True)
                 try:
                     t = wire.assign(me, idx)
                 except Exception:

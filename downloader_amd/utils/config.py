@@ -269,6 +269,9 @@ class DownloadConfig(BaseModel):
     # for a compute stream); past it the host hashes the overflow. 512 overflowed on config 6
     # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/r5/swarm3/)
     swarm_gpu_inflight: int = 1024
+    # GPU mode: once no more than this much of the torrent is left to start, the pieces are
+    # hashed on the host - on the device the last ones would each add ~0.1 s to the job
+    swarm_gpu_tail_mb: int = 1024
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -546,7 +546,8 @@ def test_swarm_pieces_verified_on_the_gfx950_part_hasher(run, tmp_path):
         (good_dir / "m.mkv").write_bytes(data)
         good = await TorrentClient().start()
         await good.add_torrent(meta, str(tmp_path / "good"))
-        leech = await TorrentClient(swarm_verify="gpu", pipeline=64).start()
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=64,
+                                    swarm_gpu_tail_bytes=0).start()
         s = await leech.add_torrent(meta, str(tmp_path / "dl"),
                                     peers=[("127.0.0.1", bad.listen_port)])
         await asyncio.sleep(0.5)

@@ -304,7 +304,8 @@ def test_native_wire_pieces_verified_on_the_part_hasher(run, tmp_path):
         for rel, d in data.items():
             (gdir / "Pack" / rel).write_bytes(d)
         await good.add_torrent(parse_torrent(raw), str(gdir))
-        leech = await TorrentClient(swarm_verify="gpu", pipeline=64).start()
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=64,
+                                    swarm_gpu_tail_bytes=0).start()
         meta = parse_torrent(raw)
         s = await leech.add_torrent(meta, str(tmp_path / "dl"),
                                     peers=[("127.0.0.1", seeder.listen_port)])
@@ -334,7 +335,7 @@ def test_native_wire_gpu_overflow_is_hashed_on_the_host(run, tmp_path):
     async def go():
         raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 1_500_000}, piece=65536)
         leech = await TorrentClient(swarm_verify="gpu", pipeline=64,
-                                    wire_gpu_inflight=1).start()
+                                    wire_gpu_inflight=1, swarm_gpu_tail_bytes=0).start()
         meta = parse_torrent(raw)
         s = await leech.add_torrent(meta, str(tmp_path / "dl"),
                                     peers=[("127.0.0.1", seeder.listen_port)])
@@ -1432,3 +1433,29 @@ def test_swarm_verify_backend_policy(monkeypatch):
     assert hashing.swarm_backend("auto", 100 * gb, 0) == "cpu"      # 0: never by size
     assert hashing.swarm_backend("cpu", 100 * gb, 4 * gb) == "cpu"
     assert hashing.swarm_backend("gpu", 1, 4 * gb) == "gpu"
+
+
+def test_native_wire_gpu_mode_hashes_the_tail_on_the_host(run, tmp_path):
+    """GPU mode hands the last pieces of a download (swarm_gpu_tail_bytes, at most a quarter
+    of the torrent) to the host SHA-1, so the job does not end waiting out the device."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 4_000_000}, piece=65536)
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=16,
+                                    swarm_gpu_tail_bytes=1 << 30).start()
+        meta = parse_torrent(raw)
+        s = await leech.add_torrent(meta, str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        st = s.wire.stats()
+        assert s._host_tail and st["verified"] == meta.num_pieces
+        assert 0 < st["gpu_pieces"] < meta.num_pieces and st["verify_batches"] > 0
+        await leech.close(); await seeder.close()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.002), 4)
+    try:
+        run(go(), timeout=90)
+    finally:
+        hashing.use_part_hasher(None)
