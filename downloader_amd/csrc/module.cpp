@@ -265,6 +265,9 @@ PYBIND11_MODULE(_native, m) {
            py::arg("bits"))
       .def("set_have_piece", &SwarmWire::set_have_piece, py::arg("idx"))
       .def("set_serving", &SwarmWire::set_serving, py::arg("conn_id"), py::arg("on"))
+      .def("set_backlog_cap", &SwarmWire::set_backlog_cap, py::arg("bytes"))
+      .def("backlogged", &SwarmWire::backlogged,
+           "True while complete, unreported pieces hold the cap or more (start no new piece)")
       .def("set_host_tail", &SwarmWire::set_host_tail, py::arg("on"),
            "GPU mode: hash the pieces completing from now on on the host (the download's end)")
       .def("set_gpu", &SwarmWire::set_gpu, py::arg("on"), py::arg("max_inflight") = 64,
@@ -335,6 +338,7 @@ PYBIND11_MODULE(_native, m) {
              d["gpu_refused"] = s.gpu_refused;
              d["gpu_errors"] = s.gpu_errors;
              d["gpu_overflow"] = s.gpu_overflow;    // hashed on the host: device full
+             d["backlog_bytes"] = s.backlog_bytes;
              d["pool_in_use"] = s.pool_in_use;      // process-wide piece buffers
              d["pool_idle"] = s.pool_idle;
              d["pool_idle_bytes"] = s.pool_idle_bytes;

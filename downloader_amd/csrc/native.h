@@ -227,6 +227,7 @@ struct SwarmWireStats {
   uint64_t assigned = 0, requests = 0;                      // owned pieces, REQUESTs the wire sent
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
   uint64_t gpu_overflow = 0;        // hashed on the host: max_inflight pieces on the device
+  int64_t backlog_bytes = 0;        // complete pieces not yet reported
   size_t pool_in_use = 0, pool_idle = 0, pool_idle_bytes = 0;   // process-wide piece buffers
   uint64_t pool_allocs = 0, pool_frees = 0, pool_locks = 0; // since start: buffers made /
                                                             // unmade, page-locked for a hasher
@@ -271,6 +272,11 @@ class SwarmWire {
   // GPU mode, the end of the download: pieces completing from now on are hashed on the host
   // (the last ~100 ms of download would otherwise wait out the device's per-piece latency).
   void set_host_tail(bool on);
+  // Back-pressure: complete pieces not yet reported (verifying, on the device, waiting for the
+  // writer) hold their buffers. backlogged() is true at `bytes` or more (Python then starts no
+  // new piece); when half has drained since, NEED arrives on conn 0 (refill every connection).
+  void set_backlog_cap(int64_t bytes);
+  bool backlogged();
   void attach(int fd, uint64_t id, const std::string& prefix);
   size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
   size_t pending_out(uint64_t id);
@@ -316,6 +322,8 @@ class SwarmWire {
   std::atomic<bool> gpu_{false};
   std::atomic<int> gpu_cap_{64}, gpu_inflight_{0};
   std::atomic<bool> host_tail_{false};
+  std::atomic<int64_t> backlog_bytes_{0}, backlog_cap_{0};
+  std::atomic<bool> backlog_full_{false};
   std::mutex gmu_;
   std::condition_variable gcv_;
   std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order

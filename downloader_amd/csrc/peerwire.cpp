@@ -400,6 +400,7 @@ int SwarmWire::take_from(Conn* c, uint32_t idx, uint32_t begin, const uint8_t* p
     auto it = pieces_.find(idx);
     if (it != pieces_.end() && it->second == pc) pieces_.erase(it);
   }
+  backlog_bytes_.fetch_add(pc->size);      // until its result is reported
   {
     std::lock_guard<std::mutex> g(vmu_);
     vq_.push_back(std::move(pc));
@@ -727,7 +728,21 @@ void SwarmWire::report(uint32_t idx, int status, const std::string& err) {
       stats_.hash_fails++;
     }
   }
+  // (off the backlog before the result is out: a session that ends on it sees it drained)
+  const int64_t left = backlog_bytes_.fetch_sub(piece_size(idx)) - piece_size(idx);
   push(0, kEvPiece, std::move(ev));
+  // back-pressure off: half the cap drained since backlogged() said full -> NEED on conn 0
+  if (backlog_full_.load() && left < backlog_cap_.load() / 2 && backlog_full_.exchange(false))
+    push(0, kEvNeed, std::string());
+}
+
+void SwarmWire::set_backlog_cap(int64_t bytes) { backlog_cap_.store(std::max<int64_t>(0, bytes)); }
+
+bool SwarmWire::backlogged() {
+  const int64_t cap = backlog_cap_.load();
+  if (cap <= 0 || backlog_bytes_.load() < cap) return false;
+  backlog_full_.store(true);
+  return true;
 }
 
 void SwarmWire::set_host_tail(bool on) { host_tail_.store(on); }
@@ -1095,6 +1110,7 @@ SwarmWireStats SwarmWire::stats() {
   s.rx_bytes = rx_bytes_.load();
   s.recvs = recvs_.load();
   s.served_bytes = served_bytes_.load();
+  s.backlog_bytes = backlog_bytes_.load();
   {
     PiecePool& pp = piece_pool();
     std::lock_guard<std::mutex> g2(pp.mu);

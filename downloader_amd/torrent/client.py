@@ -35,7 +35,8 @@ class TorrentClient:
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
                  wire_pool_mb: int = 4096, wire_gpu_inflight: int = 1024,
-                 swarm_gpu_min_bytes: int = 0, swarm_gpu_tail_bytes: int = 1 << 30):
+                 swarm_gpu_min_bytes: int = 0, swarm_gpu_tail_bytes: int = 1 << 30,
+                 swarm_backlog_bytes: int = 4 << 30):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -70,6 +71,7 @@ class TorrentClient:
         self.wire_gpu_inflight = wire_gpu_inflight   # device-verified pieces at once (GPU mode)
         self.swarm_gpu_min_bytes = swarm_gpu_min_bytes   # `auto`: device from this size up
         self.swarm_gpu_tail_bytes = swarm_gpu_tail_bytes # GPU mode: the last bytes on the host
+        self.swarm_backlog_bytes = swarm_backlog_bytes   # complete, unverified pieces at most
         if native_wire:
             try:
                 from ..ops import native
@@ -104,6 +106,7 @@ class TorrentClient:
                    wire_gpu_inflight=d.swarm_gpu_inflight,
                    swarm_gpu_min_bytes=int(d.swarm_gpu_min_gb * (1 << 30)),
                    swarm_gpu_tail_bytes=d.swarm_gpu_tail_mb << 20,
+                   swarm_backlog_bytes=d.swarm_backlog_mb << 20,
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

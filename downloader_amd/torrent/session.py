@@ -463,6 +463,8 @@ class TorrentSession:
                       # native wire: owned pieces handed back by a choking / closing peer, and
                       # made ordinary when the endgame began
                       "wire_released": 0, "wire_endgame_pieces": 0,
+                      # ... and fills that started no piece: the verify / write backlog was full
+                      "wire_backlogged": 0,
                       # summed over webseed streams: time in Range GETs / in piece verification
                       "webseed_fetch_s": 0.0, "webseed_verify_s": 0.0}
         self.add_peers(list(peers), "magnet")
@@ -558,6 +560,7 @@ class TorrentSession:
                                                                   self.storage.paths)])
             self.picker.on_activate = self.wire.begin_piece
             self.wire.set_pipeline(self.client.pipeline)
+            self.wire.set_backlog_cap(self.client.swarm_backlog_bytes)
             self.wire.set_have(self.have.to_bytes())     # what unchoked peers may be served
         self.meta_ready.set()
         for p in list(self.peers.values()):
@@ -703,6 +706,11 @@ class TorrentSession:
         try:
             t = wire.todo(me)
             while t < want:
+                if wire.backlogged():
+                    # complete pieces waiting for their hash / write hold their buffers: no new
+                    # piece until half of them are through (NEED on conn 0 refills everyone)
+                    self.stats["wire_backlogged"] += 1
+                    return True
                 idx = picker.take_piece(me, pc.bitfield)
                 if idx < 0:
                     # nothing left to start: once this connection is down to its last
@@ -769,6 +777,9 @@ class TorrentSession:
         for conn, kind, data in self.wire.poll():
             if kind == EV_PIECE:
                 self._wire_pieces.put_nowait(data)
+                continue
+            if conn == 0:                        # NEED on conn 0: the backlog drained
+                self._refill_all()
                 continue
             pc = self.peers.get(conn)
             if pc is None or pc._wq is None:
@@ -947,6 +958,8 @@ class TorrentSession:
                 or pc.bitfield is None:
             return
         fresh = dups = True
+        if self.wire is not None and self.wire.backlogged():
+            fresh = False                        # (per-block requests of started pieces only)
         if pc.wire is not None and self._owned_mode and not self._endgame:
             # whole pieces go to the wire; below, only free blocks of ordinary pieces (one a
             # choked or closed peer left) are requested per block, and duplicates once every

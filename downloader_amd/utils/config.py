@@ -272,6 +272,10 @@ class DownloadConfig(BaseModel):
     # GPU mode: once no more than this much of the torrent is left to start, the pieces are
     # hashed on the host - on the device the last ones would each add ~0.1 s to the job
     swarm_gpu_tail_mb: int = 1024
+    # complete swarm pieces waiting for their SHA-1 (host verifiers, the device) or the writer
+    # hold their buffers; at this much no new piece is started until half has drained. Without
+    # it a download faster than its verification ran GBs ahead (config 6 at 16 GB: 4 - 8 GB)
+    swarm_backlog_mb: int = 4096
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -2,10 +2,11 @@
 # Round 5, fifth swarm call: config 6 with the device SHA-1 handing the last GB to the host
 # (download.swarm_gpu_tail_mb, default 1024, at most a quarter of the torrent) vs all on the
 # device (--swarm-gpu-tail-mb 0) vs the host, at 2, 8 and 16 GB, with a piece pool big enough
-# (--swarm-pool-mb 8192) that no download after the first makes or page-locks buffers.
+# (POOL=8192: --swarm-pool-mb 8192) that no download after the first makes or page-locks
+# buffers; without POOL the defaults (4 GB pool, 4 GB verify backlog).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm15}
+F=${OUT:-gpurun_out/r5_swarm16}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
@@ -14,8 +15,8 @@ for sc in ${SCALES:-1 4 8}; do
     for v in cpu tail gpu; do
       case $v in
         cpu) a="--swarm-verify cpu" ;;
-        tail) a="--swarm-verify gpu --swarm-pool-mb 8192" ;;
-        gpu) a="--swarm-verify gpu --swarm-pool-mb 8192 --swarm-gpu-tail-mb 0" ;;
+        tail) a="--swarm-verify gpu ${POOL:+--swarm-pool-mb $POOL}" ;;
+        gpu) a="--swarm-verify gpu ${POOL:+--swarm-pool-mb $POOL} --swarm-gpu-tail-mb 0" ;;
       esac
       step "$v x$sc $i"
       timeout -k 10 400 python -m downloader_amd.bench.configs --config 6 --reps 3 --scale $sc $a > $F/swarm_${v}_x${sc}_$i.json 2>> $F/swarm.err || { tail -20 $F/swarm.err; exit 1; }

@@ -1459,3 +1459,30 @@ def test_native_wire_gpu_mode_hashes_the_tail_on_the_host(run, tmp_path):
         run(go(), timeout=90)
     finally:
         hashing.use_part_hasher(None)
+
+
+def test_native_wire_backlog_holds_back_new_pieces(run, tmp_path):
+    """Complete pieces waiting for a slow hasher hold their buffers: at swarm_backlog_bytes no
+    new piece is started until half of them are through (NEED on conn 0 refills everyone),
+    and the download still completes."""
+    from downloader_amd.ops import hashing, native
+
+    async def go():
+        raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 3_000_000}, piece=65536)
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=16, swarm_gpu_tail_bytes=0,
+                                    swarm_backlog_bytes=4 * 65536).start()
+        meta = parse_torrent(raw)
+        s = await leech.add_torrent(meta, str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        st = s.wire.stats()
+        assert s.stats["wire_backlogged"] > 0 and st["verified"] == meta.num_pieces
+        assert st["backlog_bytes"] == 0
+        await leech.close(); await seeder.close()
+
+    hashing.use_part_hasher(native().CpuPartHasher(0.02), 4)
+    try:
+        run(go(), timeout=90)
+    finally:
+        hashing.use_part_hasher(None)
