@@ -305,8 +305,9 @@ def auto_may_use_gpu() -> bool:
 def swarm_backend(requested: str, total_bytes: int, gpu_min_bytes: int) -> str:
     """Where the native peer wire SHA-1s a swarm torrent's pieces. ``auto``: the device when
     the host lacks the AVX-512 multi-buffer SHA-1, or for a torrent of at least
-    ``gpu_min_bytes`` (0: never) - the device costs 20 - 40 % less CPU per byte and runs
-    20 - 35 % slower on config 6 (profiles/r5/swarm3/), a trade for CPU-bound nodes."""
+    ``gpu_min_bytes`` (0: never): on config 6 at 16 GB the device runs within ~5 % of the
+    host's rate at 35 % less leech CPU per byte; at 2 GB its ~75 ms per piece costs 35 - 40 %
+    of the rate (profiles/r5/swarm4/)."""
     if requested == "cpu":
         return "cpu"
     if requested == "gpu":

@@ -250,15 +250,14 @@ class DownloadConfig(BaseModel):
     # and pieces a choking / closing peer leaves go back to per-block requests
     torrent_wire_requests: bool = True
     # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
-    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the host
-    # when it has the AVX-512 multi-buffer SHA-1 (else the device), and the device for torrents
-    # of swarm_gpu_min_gb and up when that is set (0: never). Config 6 (4 seeders) on the box:
-    # the device costs 20 - 40 % less leech CPU per byte and runs 20 - 35 % slower (2 GB:
-    # 5.7 - 5.9 vs 7.3 - 8.6 GB/s at 0.29 - 0.32 vs 0.46 - 0.51 CPU-s/GB; 16 GB: 6.7 - 7.0 vs
-    # 8.5 - 8.7 at 0.36 - 0.38 vs 0.47 - 0.48, profiles/r5/swarm3/) - worth it where the
-    # workers' CPUs, not one job's rate, are the limit
+    # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the device
+    # for torrents of swarm_gpu_min_gb and up (0: never) or on hosts without the AVX-512
+    # multi-buffer SHA-1, else the host. Config 6 (4 seeders) on the box: 16 GB on the device
+    # 8.7 - 9.0 GB/s at 0.28 - 0.29 leech CPU-s/GB vs 9.0 - 9.5 at 0.43 - 0.48 on the host;
+    # 2 GB 5.3 - 5.8 vs 8.9 - 9.2 (the device's ~75 ms per piece is a bigger share of a short
+    # job; profiles/r5/swarm4/)
     swarm_verify_backend: str = "auto"
-    swarm_gpu_min_gb: float = 0.0
+    swarm_gpu_min_gb: float = 8.0
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
@@ -269,9 +268,10 @@ class DownloadConfig(BaseModel):
     # for a compute stream); past it the host hashes the overflow. 512 overflowed on config 6
     # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/r5/swarm3/)
     swarm_gpu_inflight: int = 1024
-    # GPU mode: once no more than this much of the torrent is left to start, the pieces are
-    # hashed on the host - on the device the last ones would each add ~0.1 s to the job
-    swarm_gpu_tail_mb: int = 1024
+    # GPU mode: once no more than this much of the torrent (at most a quarter) is left to
+    # start, pieces are hashed on the host - on the device the last ones each add ~0.1 s to
+    # the job. 0: off. 1024 on config 6 at 2 GB: 5.9 - 6.8 vs 5.3 - 5.8 GB/s, at 16 GB no gain
+    swarm_gpu_tail_mb: int = 0
     # complete swarm pieces waiting for their SHA-1 (host verifiers, the device) or the writer
     # hold their buffers; at this much no new piece is started until half has drained. Without
     # it a download faster than its verification ran GBs ahead (config 6 at 16 GB: 4 - 8 GB)
