@@ -1486,3 +1486,82 @@ def test_native_wire_backlog_holds_back_new_pieces(run, tmp_path):
         run(go(), timeout=90)
     finally:
         hashing.use_part_hasher(None)
+
+
+def test_native_wire_fickle_peers_never_stall_the_download(run, tmp_path):
+    """Stress of the owned-piece bookkeeping: three peers that choke and unchoke at random
+    (dropping what was asked, as BEP-3 allows), answer out of order, send stray blocks, and
+    hang up; a good seeder joins late. Every piece must verify, with nothing left stuck as
+    requested."""
+    import random as _r
+    from downloader_amd.torrent.peer import handshake_bytes
+
+    async def go():
+        raw, data, seeder, _ = await _seed(tmp_path, {"x.mkv": 6_000_000}, piece=65536)
+        m = parse_torrent(raw)
+        blob = data["x.mkv"]
+
+        def fake(seed):
+            rnd = _r.Random(seed)
+
+            async def peer(r, w):
+                await r.readexactly(68)
+                w.write(handshake_bytes(m.info_hash, b"-XX0001-" + bytes([48 + seed]) * 12,
+                                        False))
+                bits = bytearray((m.num_pieces + 7) // 8)
+                for i in range(m.num_pieces):
+                    bits[i // 8] |= 0x80 >> (i % 8)
+                w.write(struct.pack(">IB", 1 + len(bits), 5) + bytes(bits))
+                w.write(struct.pack(">IB", 1, 1))
+                choked, pending = False, []
+                try:
+                    while True:
+                        n = int.from_bytes(await r.readexactly(4), "big")
+                        body = await r.readexactly(n) if n else b""
+                        if not body or body[0] != 6:
+                            continue
+                        if choked:
+                            if rnd.random() < 0.05:
+                                choked = False
+                                w.write(struct.pack(">IB", 1, 1))          # UNCHOKE
+                            continue                                       # dropped
+                        pending.append(struct.unpack(">III", body[1:13]))
+                        if len(pending) < 4 and rnd.random() < 0.7:
+                            continue
+                        rnd.shuffle(pending)                               # out of order
+                        for idx, begin, ln in pending:
+                            off = idx * m.piece_length + begin
+                            w.write(struct.pack(">IBII", 9 + ln, 7, idx, begin) +
+                                    blob[off:off + ln])
+                        pending = []
+                        x = rnd.random()
+                        if x < 0.03:
+                            w.close()
+                            return
+                        if x < 0.10:
+                            choked = True
+                            w.write(struct.pack(">IB", 1, 0))              # CHOKE
+                        elif x < 0.13:                                     # stray block
+                            i = rnd.randrange(m.num_pieces)
+                            w.write(struct.pack(">IBII", 9 + 16384, 7, i, 0) + b"z" * 16384)
+                        await w.drain()
+                except (asyncio.IncompleteReadError, ConnectionError):
+                    pass
+            return peer
+
+        servers = [await asyncio.start_server(fake(k), "127.0.0.1", 0) for k in range(3)]
+        leech = await TorrentClient(pipeline=8, idle_timeout=5.0).start()
+        s = await leech.add_torrent(m, str(tmp_path / "dl"),
+                                    peers=[("127.0.0.1", sv.sockets[0].getsockname()[1])
+                                           for sv in servers])
+        await asyncio.sleep(0.5)
+        s.add_peers([("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl", data)
+        assert s.wire.stats()["verified"] == m.num_pieces
+        assert not s.picker.active and not s.picker.loose
+        assert s.stats["wire_released"] >= 1 and s.wire.stats()["assigned"] >= 1
+        await leech.close(); await seeder.close()
+        for sv in servers:
+            sv.close()
+    run(go(), timeout=90)
