@@ -497,6 +497,8 @@ async def config_swarm(a) -> Dict:
             for _, conn in procs:
                 ports += await asyncio.get_running_loop().run_in_executor(None, conn.recv)
         verify = getattr(a, "swarm_verify", "auto")
+        if getattr(a, "swarm_job", False):
+            return await _swarm_jobs(a, meta, ports, total, dst, verify, wire, seeders, procs)
         native_req = getattr(a, "wire_requests", "native") == "native"
         extra = {}
         if getattr(a, "swarm_gpu_inflight", 0):
@@ -562,6 +564,50 @@ async def config_swarm(a) -> Dict:
                 proc.kill()
         shutil.rmtree(src, ignore_errors=True)
         shutil.rmtree(dst, ignore_errors=True)
+
+
+async def _swarm_jobs(a, meta, ports, total: int, dst: str, verify: str, wire: bool,
+                      seeders, procs) -> Dict:
+    """config 6 --swarm-job: the whole job the reference runs for a magnet (download.js:64 ->
+    upload.js): a worker takes a `v1.download` whose source is a magnet naming the seeders
+    (x.pe), fetches the metadata from them (BEP-9), downloads the swarm, stages the file to the
+    S3 sink (uploads start per completed file region while the swarm runs, eager staging),
+    writes the done marker and publishes `v1.convert`. MB/s = bytes / job seconds."""
+    from downloader_amd.torrent.magnet import Magnet
+    dl = {"swarm_verify_backend": verify, "torrent_native_wire": wire,
+          "torrent_request_pipeline": a.pipeline}
+    if getattr(a, "swarm_pool_mb", 0):
+        dl["swarm_pool_mb"] = a.swarm_pool_mb
+    runs = []
+    with Blobd(sink="discard") as b:
+        w = Worker(_cfg(a.mode, b.endpoint, dst, None, download=dl), broker=MemoryBroker())
+        await w.start(health=False)
+        try:
+            uri = Magnet(meta.info_hash, meta.name, [],
+                         peers=[("127.0.0.1", p) for p in ports]).to_uri()
+            for k in range(max(1, getattr(a, "reps", 1) or 1)):
+                m = api.make_download(f"swarm-job-{k}", "torrent", uri, "MOVIE")
+                cpu0, peer0, rx0 = _self_cpu(), b.cpu_seconds(), b.stats()["bytes_received"]
+                dt, r = await _run_jobs(w, [m])
+                cpu_s, peer_s = _self_cpu() - cpu0, b.cpu_seconds() - peer0
+                rx = b.stats()["bytes_received"] - rx0
+                await asyncio.get_running_loop().run_in_executor(
+                    None, get_reaper(w.services).drain, 600.0)
+                assert r[0].outcome == "staged", r[0]
+                runs.append((dt, cpu_s, peer_s, rx, r[0]))
+        finally:
+            await w.stop()
+    dt, cpu_s, peer_s, rx, r = runs[-1]
+    return {"config": "swarm-job", "bytes": total, "seeders": a.seeders, "pipeline": a.pipeline,
+            "wire": "native" if wire else "python", "swarm_verify": verify,
+            "seeder_procs": len(procs), "seeders_in_process": bool(seeders),
+            "piece_len": a.piece_mb << 20, "job_s": round(dt, 3),
+            "MBps": round(total / dt / MB, 1), "s3_bytes_received": rx,
+            "worker_cpu_s": round(cpu_s, 2), "worker_cpu_s_per_GB": round(cpu_s / (total / 1e9), 3),
+            "sink_cpu_s": round(peer_s, 2), "stage_s": r.stats.get("stage_s", {}),
+            "eager_upload_s": r.stats.get("eager_upload_s"),
+            "reps": len(runs), "MBps_reps": [round(total / x[0] / MB, 1) for x in runs],
+            "worker_cpu_s_per_GB_reps": [round(x[1] / (total / 1e9), 3) for x in runs]}
 
 
 # ---------------------------------------------------------------------------- config 9
@@ -672,6 +718,9 @@ def main(argv=None) -> int:
     ap.add_argument("--pipeline", type=int, default=64, help="config 6: requests in flight/peer")
     ap.add_argument("--swarm-gpu-inflight", type=int, default=0,
                     help="config 6, GPU mode: pieces on the device at once (0: the default)")
+    ap.add_argument("--swarm-job", action="store_true",
+                    help="config 6: the whole magnet job through a worker (metadata from the "
+                         "seeders, swarm download, staging to the S3 sink), not the bare leech")
     ap.add_argument("--swarm-gpu-tail-mb", type=int, default=None,
                     help="config 6, GPU mode: the last MB hashed on the host (default: config)")
     ap.add_argument("--swarm-pool-mb", type=int, default=0,
