@@ -37,3 +37,19 @@ def test_config9_control_plane_ceiling(run):
     assert r["staged"] == r["jobs"] == 150
     assert r["jobs_per_s"] > 0 and r["worker_cpu_ms_per_job"] > 0
     assert r["p99_latency_s"] >= r["p50_latency_s"]
+
+
+def test_config6_swarm_leech_and_whole_magnet_job(run):
+    """Config 6 at a tiny scale, seeders in-process: the bare leech on the native wire (every
+    piece assigned to and requested by the wire), then the whole magnet job through a worker
+    (--swarm-job), whose S3 sink receives every byte of every rep."""
+    base = dict(scale=0.01, piece_mb=1, seeders=2, seed_inproc=True, seeder_procs=0,
+                pipeline=16, reps=2, wire="native", swarm_verify="cpu", wire_requests="native",
+                swarm_gpu_inflight=0, swarm_pool_mb=0)
+    r = run(configs.config_swarm(_ns(**base)), timeout=120)
+    assert r["reps"] == 2 and r["hash_fails"] == 0 and r["wire"] == "native"
+    assert r["wire_stats"]["verified"] == r["bytes"] // (1 << 20) + 1
+    assert r["wire_stats"]["assigned"] > 0
+    j = run(configs.config_swarm(_ns(swarm_job=True, **base)), timeout=120)
+    assert j["config"] == "swarm-job" and j["reps"] == 2
+    assert j["s3_bytes_received"] >= j["bytes"]
