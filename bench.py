@@ -103,6 +103,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--torrent-gb", type=float, default=20.0,
                    help="same-call GPU vs host A/B of the streamed torrent path on a config-4 "
                         "shaped torrent of this many GB (50 files, 4 MiB pieces; 0 = skip)")
+    p.add_argument("--torrent-timeout", type=float, default=300.0,
+                   help="seconds the torrent A/B may take before it is reported as failed")
     p.add_argument("--torrent-pairs", type=int, default=3,
                    help="timed jobs per backend in the torrent A/B (alternating)")
     p.add_argument("--compare-reference", action="store_true",
@@ -536,9 +538,18 @@ def torrent_measure(args, dist: Dist) -> dict:
     over ranks (they run at once), device counters too."""
     from downloader_amd.bench.torrent_ab import torrent_ab
     dist.barrier()
-    r = asyncio.run(torrent_ab(total_bytes=int(args.torrent_gb * 1e9), pairs=args.torrent_pairs,
-                               tag=f"ab-r{dist.rank}"))
+    # An extra of the line: a failure (or a run past --torrent-timeout) is reported in it,
+    # never allowed to cost the headline above; every rank still reaches the gather.
+    try:
+        r = asyncio.run(asyncio.wait_for(
+            torrent_ab(total_bytes=int(args.torrent_gb * 1e9), pairs=args.torrent_pairs,
+                       tag=f"ab-r{dist.rank}"), args.torrent_timeout))
+    except Exception as e:   # (asyncio.TimeoutError included)
+        r = {"torrent_error": f"{type(e).__name__}: {e}"[:300]}
     allr = dist.gather(r)
+    failed = [x for x in allr if "torrent_error" in x]
+    if failed:
+        return {"torrent_error": failed[0]["torrent_error"], "torrent_ranks_failed": len(failed)}
     out = dict(allr[0])
     for k in ("torrent_gpu_MBps", "torrent_host_MBps", "gpu_parts", "gpu_host_fallbacks",
               "gpu_refused", "gpu_launches"):

@@ -148,6 +148,20 @@ def test_supervisor_auto_pinning_quota_share():
 
 
 @pytest.mark.slow
+def test_bench_torrent_ab_failure_never_costs_the_headline(tmp_path):
+    """The torrent A/B is an extra of the line: when it fails or overruns --torrent-timeout
+    the line still prints, with the headline and the error."""
+    env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1",
+                        "--warmup", "0", "--size-mb", "2", "--no-compare-single-put",
+                        "--no-compare-crc", "--torrent-gb", "0.2", "--torrent-timeout",
+                        "0.001"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads(r.stdout.strip().splitlines()[-1])
+    assert j["value"] > 0 and "TimeoutError" in j["torrent_error"]
+    assert j["torrent_ranks_failed"] == 1 and "torrent_gpu_MBps" not in j
+
+
 def test_bench_four_ranks_disjoint_cpus_and_own_peers(tmp_path):
     """The driver's N=4 launch rehearsed on CPU: 4 ranks over gloo, each pinned to its own
     GPU-slot CPU slice (disjoint, same size) with its own blobd peer, one JSON line whose
