@@ -12,6 +12,7 @@ from .metainfo import Metainfo
 from .peer import PeerConn, handshake_bytes, read_handshake
 from .session import TorrentError, TorrentSession
 from .tracker import random_peer_id
+from ..utils import membudget
 
 Peer = Tuple[str, int]
 
@@ -102,11 +103,12 @@ class TorrentClient:
                    native_wire=d.torrent_native_wire,
                    swarm_verify=d.swarm_verify_backend,
                    wire_requests=d.torrent_wire_requests,
-                   wire_verify_threads=d.swarm_verify_threads, wire_pool_mb=d.swarm_pool_mb,
+                   wire_verify_threads=d.swarm_verify_threads,
+                   wire_pool_mb=membudget.swarm_bytes(d.swarm_pool_mb) >> 20,
                    wire_gpu_inflight=d.swarm_gpu_inflight,
                    swarm_gpu_min_bytes=int(d.swarm_gpu_min_gb * (1 << 30)),
                    swarm_gpu_tail_bytes=d.swarm_gpu_tail_mb << 20,
-                   swarm_backlog_bytes=d.swarm_backlog_mb << 20,
+                   swarm_backlog_bytes=membudget.swarm_bytes(d.swarm_backlog_mb),
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 
     async def start(self) -> "TorrentClient":

@@ -262,8 +262,9 @@ class DownloadConfig(BaseModel):
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
     # idle swarm piece buffers kept per worker process (reused: no page faults per piece, and
-    # page-locked once in GPU mode, where the download runs up to ~0.5 s ahead of the device)
-    swarm_pool_mb: int = 4096
+    # page-locked once in GPU mode, where the download runs up to ~0.5 s ahead of the device).
+    # 0: 1/8 of this worker's share of the memory limit, at most 4096 (utils/membudget.py)
+    swarm_pool_mb: int = 0
     # GPU mode: pieces on the device at once (a 4 MiB piece spends ~75 ms there plus its wait
     # for a compute stream); past it the host hashes the overflow. 512 overflowed on config 6
     # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/r5/swarm3/)
@@ -274,8 +275,9 @@ class DownloadConfig(BaseModel):
     swarm_gpu_tail_mb: int = 0
     # complete swarm pieces waiting for their SHA-1 (host verifiers, the device) or the writer
     # hold their buffers; at this much no new piece is started until half has drained. Without
-    # it a download faster than its verification ran GBs ahead (config 6 at 16 GB: 4 - 8 GB)
-    swarm_backlog_mb: int = 4096
+    # it a download faster than its verification ran GBs ahead (config 6 at 16 GB: 4 - 8 GB).
+    # 0: like swarm_pool_mb
+    swarm_backlog_mb: int = 0
     webseed_streams: int = 4                    # concurrent Range GETs per webseed (0: http_streams)
     webseed_chunk: int = 64 * MiB               # bytes of whole pieces per webseed request run
     webseed_verify_depth: int = 2               # fetched runs hashing while a stream fetches on

@@ -107,6 +107,18 @@ def relay_budget_bytes(download_cfg) -> int:
     return max(MIN_BUDGET, int(lim // pool_workers() * frac))
 
 
+def swarm_bytes(mb: int, fraction: float = 0.125, cap_mb: int = 4096) -> int:
+    """Swarm piece memory (download.swarm_pool_mb / swarm_backlog_mb): ``mb`` MiB when set,
+    else ``fraction`` of this worker's share of the memory limit, at most ``cap_mb`` and at
+    least 256 MiB - 4 GiB each on a GPU box's 150 GiB share, 1 GiB in an 8 GiB container."""
+    if mb and mb > 0:
+        return int(mb) * MiB
+    lim = memory_limit()
+    if lim <= 0:
+        return cap_mb * MiB
+    return max(256 * MiB, min(cap_mb * MiB, int(lim // pool_workers() * fraction)))
+
+
 def buffer_bytes(n: int) -> int:
     """What a part of ``n`` bytes leases from the native pool."""
     return -(-max(1, n) // BUFFER_ALIGN) * BUFFER_ALIGN

@@ -674,3 +674,18 @@ def test_cgroup_memory_limit_v1_v2(tmp_path):
     assert cgroup_memory_limit(str(v1)) == 0
     (v1 / "memory" / "memory.limit_in_bytes").write_text("8589934592\n")
     assert cgroup_memory_limit(str(v1)) == 8 << 30
+
+
+def test_swarm_memory_defaults_follow_the_worker_share(monkeypatch):
+    """download.swarm_pool_mb / swarm_backlog_mb 0: 1/8 of the worker's share of the memory
+    limit, capped at 4 GiB, at least 256 MiB; an explicit value wins."""
+    from downloader_amd.utils import membudget
+    gib = 1 << 30
+    monkeypatch.setenv("STAGER_POOL_WORKERS", "2")
+    monkeypatch.setattr(membudget, "memory_limit", lambda: 300 * gib)
+    assert membudget.swarm_bytes(0) == 4 * gib
+    monkeypatch.setattr(membudget, "memory_limit", lambda: 8 * gib)
+    assert membudget.swarm_bytes(0) == gib // 2
+    monkeypatch.setattr(membudget, "memory_limit", lambda: 1 * gib)
+    assert membudget.swarm_bytes(0) == 256 << 20
+    assert membudget.swarm_bytes(100) == 100 << 20
