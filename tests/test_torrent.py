@@ -1488,12 +1488,15 @@ def test_native_wire_backlog_holds_back_new_pieces(run, tmp_path):
         hashing.use_part_hasher(None)
 
 
-def test_native_wire_fickle_peers_never_stall_the_download(run, tmp_path):
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_native_wire_fickle_peers_never_stall_the_download(run, tmp_path, mode):
     """Stress of the owned-piece bookkeeping: three peers that choke and unchoke at random
     (dropping what was asked, as BEP-3 allows), answer out of order, send stray blocks, and
     hang up; a good seeder joins late. Every piece must verify, with nothing left stuck as
-    requested."""
+    requested. ``device``: the same with the pieces on a slow GPU part hasher (its host
+    double), a 4-piece verify backlog and the last quarter hashed on the host."""
     import random as _r
+    from downloader_amd.ops import hashing, native
     from downloader_amd.torrent.peer import handshake_bytes
 
     async def go():
@@ -1550,7 +1553,9 @@ def test_native_wire_fickle_peers_never_stall_the_download(run, tmp_path):
             return peer
 
         servers = [await asyncio.start_server(fake(k), "127.0.0.1", 0) for k in range(3)]
-        leech = await TorrentClient(pipeline=8, idle_timeout=5.0).start()
+        extra = {} if mode == "host" else dict(swarm_verify="gpu", swarm_gpu_tail_bytes=1 << 30,
+                                                 swarm_backlog_bytes=4 * 65536)
+        leech = await TorrentClient(pipeline=8, idle_timeout=5.0, **extra).start()
         s = await leech.add_torrent(m, str(tmp_path / "dl"),
                                     peers=[("127.0.0.1", sv.sockets[0].getsockname()[1])
                                            for sv in servers])
@@ -1561,7 +1566,16 @@ def test_native_wire_fickle_peers_never_stall_the_download(run, tmp_path):
         assert s.wire.stats()["verified"] == m.num_pieces
         assert not s.picker.active and not s.picker.loose
         assert s.stats["wire_released"] >= 1 and s.wire.stats()["assigned"] >= 1
+        if mode == "device":
+            assert s.wire.stats()["gpu_pieces"] > 0 and s.wire.stats()["backlog_bytes"] == 0
         await leech.close(); await seeder.close()
         for sv in servers:
             sv.close()
-    run(go(), timeout=90)
+
+    if mode == "device":
+        hashing.use_part_hasher(native().CpuPartHasher(0.005), 4)
+    try:
+        run(go(), timeout=90)
+    finally:
+        if mode == "device":
+            hashing.use_part_hasher(None)
