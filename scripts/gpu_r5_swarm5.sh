@@ -6,13 +6,13 @@
 # buffers; without POOL the defaults (4 GB pool, 4 GB verify backlog).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm16}
+F=${OUT:-gpurun_out/r5_swarm17}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
 for sc in ${SCALES:-1 4 8}; do
   for i in 1 2; do
-    for v in cpu tail gpu; do
+    for v in ${VARIANTS:-cpu tail gpu}; do
       case $v in
         cpu) a="--swarm-verify cpu" ;;
         tail) a="--swarm-verify gpu ${POOL:+--swarm-pool-mb $POOL}" ;;
