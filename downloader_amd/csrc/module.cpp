@@ -334,8 +334,6 @@ PYBIND11_MODULE(_native, m) {
              d["served_bytes"] = s.served_bytes;
              d["assigned"] = s.assigned;            // owned pieces (SwarmWire.assign)
              d["requests"] = s.requests;            // REQUESTs the wire sent by itself
-             d["direct_blocks"] = s.direct_blocks;  // received straight into their piece
-             d["direct_bails"] = s.direct_bails;
              d["gpu_pieces"] = s.gpu_pieces;
              d["gpu_refused"] = s.gpu_refused;
              d["gpu_errors"] = s.gpu_errors;

@@ -225,8 +225,6 @@ struct SwarmWireStats {
                                                             // writing
   uint64_t served_bytes = 0;                                // blocks served with sendfile
   uint64_t assigned = 0, requests = 0;                      // owned pieces, REQUESTs the wire sent
-  uint64_t direct_blocks = 0, direct_bails = 0;             // received straight into the piece /
-                                                            // predictions the wire broke
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
   uint64_t gpu_overflow = 0;        // hashed on the host: max_inflight pieces on the device
   int64_t backlog_bytes = 0;        // complete pieces not yet reported
@@ -308,11 +306,6 @@ class SwarmWire {
   void gpu_loop();
   int take_from(Conn* c, uint32_t idx, uint32_t begin, const uint8_t* p, uint32_t len,
                 bool* owned, std::string* reqs, bool* need);
-  int block_in(std::shared_ptr<Piece> pc, uint32_t idx);   // one more block copied in
-  struct Direct;                                 // a block received straight into its piece
-  size_t reserve_direct(Conn& c, std::vector<Direct>& slots, size_t k);
-  void unreserve_direct(std::vector<Direct>& slots, size_t from);
-  int complete_direct(Conn& c, Direct& d, bool* owned, std::string* reqs, bool* need);
   bool pump(Conn& c, std::string* reqs);        // mu_ held
   void queue_out(Conn& c, std::string data);
   void send_requests(Conn& c, std::string reqs);

@@ -34,7 +34,6 @@
 #include <sys/eventfd.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
-#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -217,21 +216,7 @@ struct SwarmWire::Conn {
   // request (piece << 32 | begin) and blocks requested and not answered yet
   std::deque<uint64_t> todo;
   std::unordered_set<uint64_t> asked;
-  std::deque<uint64_t> order;            // the wire's REQUESTs in the order sent (stale kept)
   bool need_sent = false;
-};
-
-// Receiving straight into the piece: peers answer REQUESTs in the order they were sent, so the
-// reader predicts the next PIECE messages of its owned pieces (header, then the block into its
-// place in the piece buffer) and reads them with one readv. The blocks are reserved meanwhile
-// (claimed = 2: nobody else fills them); a header that is not the one predicted (another
-// message, an answer out of order) puts every byte from there back into the receive buffer
-// for the ordinary framing.
-struct SwarmWire::Direct {
-  std::shared_ptr<Piece> pc;
-  uint32_t idx = 0, begin = 0, len = 0;
-  uint8_t hdr[13], expect[13];           // as received / the PIECE header predicted
-  uint32_t hdr_have = 0, have = 0;
 };
 
 namespace {
@@ -408,12 +393,6 @@ int SwarmWire::take_from(Conn* c, uint32_t idx, uint32_t begin, const uint8_t* p
     stats_.block_bytes += len;
   }
   memcpy(pc->data + begin, p, len);        // outside the lock: readers copy in parallel
-  return block_in(std::move(pc), idx);
-}
-
-// A block of `pc` is in place: 1, or 2 when it was the last one (the piece goes to the
-// verifiers).
-int SwarmWire::block_in(std::shared_ptr<Piece> pc, uint32_t idx) {
   const uint32_t f = pc->filled.fetch_add(1, std::memory_order_acq_rel) + 1;
   if (f < pc->nblocks) return 1;
   {
@@ -430,82 +409,9 @@ int SwarmWire::block_in(std::shared_ptr<Piece> pc, uint32_t idx) {
   return 2;
 }
 
-// Reserve the next up to k blocks `c` expects, in request order, after those in `slots`
-// (mu_). Stops at the first that cannot be received in place (not owned by `c` any more,
-// already in, its piece gone): the peer answers that one next.
-size_t SwarmWire::reserve_direct(Conn& c, std::vector<Direct>& slots, size_t k) {
-  std::lock_guard<std::mutex> g(mu_);
-  while (!c.order.empty() && !c.asked.count(c.order.front())) c.order.pop_front();
-  size_t i = 0;
-  for (auto it = c.order.begin(); it != c.order.end() && slots.size() < k; ++it) {
-    if (!c.asked.count(*it)) continue;                     // answered (or dropped) already
-    if (i < slots.size()) {                                // (the partial one, first)
-      if (block_key(slots[i].idx, slots[i].begin) != *it) return slots.size();
-      ++i;
-      continue;
-    }
-    const uint32_t idx = (uint32_t)(*it >> 32), begin = (uint32_t)*it;
-    auto pit = pieces_.find(idx);
-    if (pit == pieces_.end() || pit->second->owner != c.id) break;
-    Piece& p = *pit->second;
-    const uint32_t b = begin / kBlock;
-    if (b >= p.nblocks || p.claimed[b]) break;
-    p.claimed[b] = 2;
-    Direct d;
-    d.pc = pit->second;
-    d.idx = idx;
-    d.begin = begin;
-    d.len = std::min(kBlock, p.size - begin);
-    std::string e;
-    put32(e, d.len + 9);
-    e.push_back((char)kPiece);
-    put32(e, idx);
-    put32(e, begin);
-    memcpy(d.expect, e.data(), 13);
-    slots.push_back(std::move(d));
-    ++i;
-  }
-  return slots.size();
-}
-
-void SwarmWire::unreserve_direct(std::vector<Direct>& slots, size_t from) {
-  std::lock_guard<std::mutex> g(mu_);
-  for (size_t i = from; i < slots.size(); ++i) {
-    Piece& p = *slots[i].pc;
-    const uint32_t b = slots[i].begin / kBlock;
-    if (p.claimed[b] == 2) p.claimed[b] = 0;
-  }
-  slots.resize(from);
-}
-
-// A reserved block fully received in place: taken like take_from would (0 if its piece moved
-// on meanwhile - re-begun after a failed check - and the bytes are dropped).
-int SwarmWire::complete_direct(Conn& c, Direct& d, bool* owned, std::string* reqs, bool* need) {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (c.asked.erase(block_key(d.idx, d.begin)) && pump(c, reqs)) *need = true;
-    Piece& p = *d.pc;
-    const uint32_t b = d.begin / kBlock;
-    auto it = pieces_.find(d.idx);
-    if (it == pieces_.end() || it->second != d.pc || p.claimed[b] != 2) {
-      if (p.claimed[b] == 2) p.claimed[b] = 0;
-      stats_.blocks_ignored++;
-      *owned = true;
-      return 0;
-    }
-    p.claimed[b] = 1;
-    *owned = p.owner != 0;     // (a piece released meanwhile: reported like any block)
-    stats_.blocks++;
-    stats_.block_bytes += d.len;
-    stats_.direct_blocks++;
-  }
-  return block_in(d.pc, d.idx);
-}
-
 // Next REQUESTs of `c`'s owned pieces, up to depth_ in flight (mu_ held). True the first time
 // the queue of blocks to request drops below a pipeline since Python last filled it.
 bool SwarmWire::pump(Conn& c, std::string* reqs) {
-  while (!c.order.empty() && !c.asked.count(c.order.front())) c.order.pop_front();
   while (c.asked.size() < depth_ && !c.todo.empty()) {
     const uint64_t k = c.todo.front();
     c.todo.pop_front();
@@ -515,7 +421,6 @@ bool SwarmWire::pump(Conn& c, std::string* reqs) {
     const Piece& p = *it->second;
     if (p.claimed[begin / kBlock]) continue;
     c.asked.insert(k);
-    c.order.push_back(k);
     stats_.requests++;
     if (reqs) {
       put32(*reqs, 13);
@@ -609,9 +514,7 @@ size_t SwarmWire::todo(uint64_t id) {
 std::string SwarmWire::block_states(const Piece& p, const Conn* owner) {
   std::string s(p.nblocks, '\0');
   for (uint32_t b = 0; b < p.nblocks; ++b)
-    s[b] = p.claimed[b] == 1 ? 2    // (2: reserved by the owner's reader, on its way in)
-           : (p.claimed[b] == 2 || (owner && owner->asked.count(block_key(p.idx, b * kBlock)))
-                  ? 1 : 0);
+    s[b] = p.claimed[b] ? 2 : (owner && owner->asked.count(block_key(p.idx, b * kBlock)) ? 1 : 0);
   return s;
 }
 
@@ -628,7 +531,6 @@ std::vector<std::pair<uint32_t, std::string>> SwarmWire::release(uint64_t id) {
   if (c) {
     c->todo.clear();
     c->asked.clear();      // a choking peer drops what we asked for (BEP-3)
-    c->order.clear();
     c->need_sent = false;
   }
   return out;
@@ -957,17 +859,6 @@ void SwarmWire::read_loop(Conn& c) {
       blocks.clear();
     }
   };
-  auto record = [&](uint32_t idx, uint32_t begin, uint32_t len, int st) {
-    put32(blocks, idx);
-    put32(blocks, begin);
-    put32(blocks, len);
-    put32(blocks, (uint32_t)st);
-  };
-  // Direct receive (struct Direct): while the buffer is drained, up to kDirect predicted
-  // PIECE messages are read in place; slots[0] may be one cut by the previous read.
-  constexpr size_t kDirect = 16;
-  std::vector<Direct> slots;
-  std::vector<iovec> iov;
   for (;;) {
     // frame every complete message in [start, end)
     bool bad = false;
@@ -985,7 +876,12 @@ void SwarmWire::read_loop(Conn& c) {
           const uint32_t idx = be32(m + 1), begin = be32(m + 5), len = n - 9;
           bool owned = false;
           const int st = take_from(&c, idx, begin, m + 9, len, &owned, &reqs, &need);
-          if (!owned) record(idx, begin, len, st);   // (an owned piece's are the wire's)
+          if (!owned) {                   // an owned piece's blocks are the wire's business
+            put32(blocks, idx);
+            put32(blocks, begin);
+            put32(blocks, len);
+            put32(blocks, (uint32_t)st);
+          }
         } else if (m[0] == kRequest && n == 13 && c.serving.load() &&
                    servable(be32(m + 1), be32(m + 5), be32(m + 9))) {
           std::string it(12, '\0');          // served by the writer, in order with the rest
@@ -1025,101 +921,18 @@ void SwarmWire::read_loop(Conn& c) {
       break;
     }
     if (pr <= 0) continue;
-    // reserved only with bytes waiting: a peer that went quiet (it choked us) must not hold
-    // blocks that other peers are asked for next
-    if (start == end && slots.size() < kDirect) reserve_direct(c, slots, kDirect);
-    ssize_t r;
-    if (slots.empty()) {
-      r = ::recv(c.fd, buf.data() + end, buf.size() - end, 0);
-    } else {
-      iov.clear();
-      for (auto& d : slots) {
-        if (d.hdr_have < 13) iov.push_back({d.hdr + d.hdr_have, 13 - d.hdr_have});
-        iov.push_back({d.pc->data + d.begin + d.have, d.len - d.have});
-      }
-      iov.push_back({buf.data(), buf.size() < (1u << 20) ? buf.size() : (size_t)(1u << 20)});
-      r = ::readv(c.fd, iov.data(), (int)iov.size());
-    }
+    ssize_t r = ::recv(c.fd, buf.data() + end, buf.size() - end, 0);
     if (r == 0) break;
     if (r < 0) {
       if (errno == EAGAIN || errno == EINTR) continue;
-      reason = std::string(slots.empty() ? "recv: " : "readv: ") + strerror(errno);
+      reason = std::string("recv: ") + strerror(errno);
       break;
     }
-    if (!slots.empty()) {
-      // hand the bytes out over the iovecs in wire order, checking each header as it completes
-      size_t left = (size_t)r, done = 0, j = 0;
-      bool bail = false, cut = false;
-      for (size_t si = 0; si < slots.size() && left > 0 && !cut && !bail; ++si) {
-        Direct& d = slots[si];
-        if (d.hdr_have < 13) {
-          const size_t k = std::min(left, iov[j].iov_len);
-          d.hdr_have += (uint32_t)k;
-          left -= k;
-          ++j;
-          // checked as far as it came: a message that is not the predicted PIECE (a CHOKE,
-          // a keep-alive) must reach the framing now, not wait for 13 bytes that never come
-          if (memcmp(d.hdr, d.expect, d.hdr_have) != 0) {
-            bail = true;                  // iovecs from j on hold what followed those bytes
-            done = si;
-            break;
-          }
-          if (d.hdr_have < 13) {
-            cut = true;
-            break;
-          }
-        }
-        const size_t k = std::min(left, iov[j].iov_len);
-        d.have += (uint32_t)k;
-        left -= k;
-        ++j;
-        if (d.have < d.len) {
-          cut = true;
-          break;
-        }
-        done = si + 1;
-      }
-      // the first `done` slots are whole and checked
-      for (size_t i = 0; i < done; ++i) {
-        bool owned = false;
-        const int st = complete_direct(c, slots[i], &owned, &reqs, &need);
-        if (!owned) record(slots[i].idx, slots[i].begin, slots[i].len, st);
-      }
-      if (bail) {
-        // every byte from the unexpected header on goes back into the buffer, in wire order:
-        // the header, then what the following iovecs took (block places, headers, the tail)
-        std::string back((const char*)slots[done].hdr, slots[done].hdr_have);
-        for (size_t jj = j; jj < iov.size() && left > 0; ++jj) {
-          const size_t k = std::min(left, iov[jj].iov_len);
-          back.append((const char*)iov[jj].iov_base, k);
-          left -= k;
-        }
-        unreserve_direct(slots, done);
-        slots.clear();
-        memcpy(buf.data(), back.data(), back.size());
-        start = 0;
-        end = back.size();
-        std::lock_guard<std::mutex> g(mu_);
-        stats_.direct_bails++;
-      } else if (cut) {
-        // the slot the read ended in stays reserved as the next read's first; later ones go
-        std::swap(slots[0], slots[done]);
-        unreserve_direct(slots, 1);
-        start = end = 0;
-      } else {
-        unreserve_direct(slots, done);    // (untouched ones: the read ended on a boundary)
-        slots.clear();
-        start = 0;
-        end = left;                       // bytes past every slot, in the tail: framed
-      }
-    } else {
-      end += (size_t)r;
-    }
+    end += (size_t)r;
     c.last_rx_ns.store(now_ns(), std::memory_order_relaxed);
     rx_bytes_.fetch_add((uint64_t)r, std::memory_order_relaxed);
     recvs_.fetch_add(1, std::memory_order_relaxed);
   }
-  unreserve_direct(slots, 0);             // (a block cut by the close is free again)
   c.dead.store(true);
   {
     std::lock_guard<std::mutex> g(c.wmu);

@@ -766,11 +766,8 @@ static void wire_owned_section() {
   for (int fd : theirs) close(fd);
   close(f1);
   unlink(p1);
-  CHECK(st.direct_blocks > 0);              // in-order answers were read in place
-  fprintf(stderr, "wire (owned): %d pieces, %d requests, %d NEED events, %llu blocks refused, "
-          "%llu read in place, %llu predictions broken\n",
-          done, requests.load(), needs, (unsigned long long)st.blocks_ignored,
-          (unsigned long long)st.direct_blocks, (unsigned long long)st.direct_bails);
+  fprintf(stderr, "wire (owned): %d pieces, %d requests, %d NEED events, %llu blocks refused\n",
+          done, requests.load(), needs, (unsigned long long)st.blocks_ignored);
 }
 
 static void stress_sections() {

@@ -6,7 +6,7 @@
 # buffers; without POOL the defaults (4 GB pool, 4 GB verify backlog).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-F=${OUT:-gpurun_out/r5_swarm17}
+F=${OUT:-gpurun_out/r5_swarm18}
 mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=${GRAFT_REPO_ROOT:-$PWD}
 step() { echo "== $1 $(date +%T)"; }
