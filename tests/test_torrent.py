@@ -1579,3 +1579,28 @@ def test_native_wire_fickle_peers_never_stall_the_download(run, tmp_path, mode):
     finally:
         if mode == "device":
             hashing.use_part_hasher(None)
+
+
+def test_swarm_wire_rx_idle_tracks_the_socket():
+    """The idle watchdog asks the native wire when a connection last received (blocks of
+    owned pieces are not reported one by one, so Python's own clock would go stale)."""
+    import socket as _s
+    import time as _t
+    from downloader_amd.ops import native
+    w = native().SwarmWire(1)
+    a, b = _s.socketpair()
+    try:
+        w.attach(os.dup(a.fileno()), 7, b"")
+        _t.sleep(0.3)
+        assert w.rx_idle(7) >= 0.25
+        b.sendall(struct.pack(">IB", 1, 2))              # INTERESTED
+        deadline = _t.monotonic() + 5
+        while w.rx_idle(7) > 0.2 and _t.monotonic() < deadline:
+            _t.sleep(0.01)
+        assert w.rx_idle(7) < 0.2
+        assert any(kind == 1 for _, kind, _ in w.poll())   # the message went up
+        assert w.rx_idle(12345) == 0.0                   # unknown connection
+    finally:
+        w.close()
+        a.close()
+        b.close()
