@@ -62,17 +62,22 @@ def report(pipe_sharers: int = 4) -> Dict[str, Any]:
     from . import membudget
     from .config import DownloadConfig
     lim = membudget.memory_limit()
-    part = membudget.relay_budget_bytes(DownloadConfig())
+    dc = DownloadConfig()
+    part = membudget.relay_budget_bytes(dc)
+    swarm = membudget.swarm_bytes(dc.swarm_pool_mb) + membudget.swarm_bytes(dc.swarm_backlog_mb)
+    # docs/OPERATIONS.md "Memory": fixed part + HIP runtime + part budget + swarm pieces
+    worst = part + swarm + int(2.3e9)
     out["memory"] = {"limit_bytes": lim or None,
                      "cgroup_limit_bytes": membudget.cgroup_memory_limit() or None,
                      "workers": membudget.pool_workers(),
                      "part_budget_bytes": part,
-                     # docs/OPERATIONS.md "Memory": fixed part + HIP runtime + part budget
-                     "worst_case_worker_bytes": part + int(2.3e9)}
-    if lim and membudget.pool_workers() * (part + int(2.3e9)) > lim:
+                     "swarm_pool_and_backlog_bytes": swarm,
+                     "worst_case_worker_bytes": worst}
+    if lim and membudget.pool_workers() * worst > lim:
         warn.append(f"{membudget.pool_workers()} workers x ({part >> 20} MiB part budget + "
-                    f"~2.3 GB) exceed the memory limit of {lim >> 20} MiB: lower "
-                    "download.relay_memory_mb or run fewer workers")
+                    f"{swarm >> 20} MiB swarm pieces + ~2.3 GB) exceed the memory limit of "
+                    f"{lim >> 20} MiB: lower download.relay_memory_mb / swarm_pool_mb / "
+                    "swarm_backlog_mb or run fewer workers")
 
     thp = _read("/sys/kernel/mm/transparent_hugepage/enabled")
     out["thp"] = thp
