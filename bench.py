@@ -19,14 +19,23 @@ at every N, so the 1/2/4/8 curve is weak scaling of one slot's host resources); 
 synchronise over gloo (the workload is host-side: there is no tensor compute).
 
 Objects above 64 MiB go as S3 multipart uploads of 64 MiB parts (minio-js' split), so a 100 MB
-job is 2 parts. The run fails unless the S3 peer's own counters, sampled at "go" and after the
-last timed job, show (a) at least as many bytes received as the workers claim to have staged,
-and (b) with ``--sink sample`` (default) / ``verify``, every timed object matched against the
-bytes the origin generated for it (sampled windows / every byte) with zero mismatches. A
-second, same-call run with the round-2 settings (single PUT up to 128 MiB) is reported as
-``single_put_MBps``, and a third with a CRC32C on every relayed PUT / part (``--checksum
-always``: aws-chunked trailer computed from a tee()d copy of the spliced pages, recomputed and
-checked by the sink) as ``crc_relay_MBps``.
+job is 2 parts. Every PUT and part carries a CRC32C of its payload (``s3.checksum: always``, the
+default since round 6: the relay peeks each byte once into user space for it), like minio-js
+hashes every byte it uploads (lib/upload.js:45). The run fails unless the S3 peer's own
+counters, sampled at "go" and after the last timed job, show (a) at least as many bytes
+received as the workers claim to have staged, (b) every timed media PUT / part carrying a
+CRC32C and none refused for a wrong one - the peer recomputes the CRC of a salted 1-in-8
+subset of the bodies (``--sink-crc-check``), so a wrong CRC is caught without the bench's S3
+re-reading every byte on the worker's CPUs - and (c) with ``--sink sample`` (default) /
+``verify``, every timed object matched against the bytes the origin generated for it (sampled
+windows / every byte) with zero mismatches. The origin's bytes repeat with a period of
+64 MiB + 4 KiB, so a part or piece fetched from the wrong offset never matches.
+
+Same-call extras of the line: ``unchecked_MBps`` (``s3.checksum: auto``: the plain relay
+spliced with no payload checksum), ``reference_mode_MBps`` (reference-equivalent mode,
+BASELINE.md: one serial prefetch-1 consumer per process, ``--ref-procs`` of them, on the same
+CPUs; ``vs_baseline`` = headline / it), ``workers_curve`` (MB/s and p50 at 1/2/4/8 worker
+processes of the rank) and the streamed-torrent GPU vs host A/B.
 """
 from __future__ import annotations
 
@@ -80,12 +89,17 @@ def parse() -> argparse.Namespace:
                         "bytes at the object offset; verify = compare every byte (checksum of the "
                         "body vs checksum of the generated range); discard = no check; checksum "
                         "= fold every byte, no comparison")
-    p.add_argument("--no-compare-single-put", dest="compare_single_put", action="store_false",
-                   help="skip the same-call comparison run with round-2 settings (objects up to "
-                        "128 MiB in one PUT)")
-    p.add_argument("--no-compare-crc", dest="compare_crc", action="store_false",
-                   help="skip the same-call comparison run with a CRC32C on every relayed PUT "
-                        "and part (--checksum always), checked by the S3 sink")
+    p.add_argument("--compare-single-put", dest="compare_single_put", action="store_true",
+                   help="add a same-call run with round-2 settings (objects up to 128 MiB in one "
+                        "PUT)")
+    p.add_argument("--no-compare-single-put", dest="compare_single_put", action="store_false")
+    p.add_argument("--no-compare-unchecked", "--no-compare-crc", dest="compare_unchecked",
+                   action="store_false",
+                   help="skip the same-call run of the unchecked spliced relay (--checksum auto)")
+    p.add_argument("--sink-crc-check", type=int, default=8,
+                   help="the S3 peer recomputes the CRC32C of 1 in N checksummed bodies (a "
+                        "salted hash of key + part picks them); the rest must carry a "
+                        "well-formed CRC and are dropped in the kernel")
     p.add_argument("--pipe-kb", type=int, default=0,
                    help="splice pipe KiB per transfer (0: the uid's pipe budget / workers)")
     p.add_argument("--checksum", choices=["auto", "always", "off"], default="",
@@ -107,8 +121,23 @@ def parse() -> argparse.Namespace:
                    help="seconds the torrent A/B may take before it is reported as failed")
     p.add_argument("--torrent-pairs", type=int, default=3,
                    help="timed jobs per backend in the torrent A/B (alternating)")
-    p.add_argument("--compare-reference", action="store_true",
-                   help="also time reference-equivalent mode and report the ratio")
+    p.add_argument("--no-compare-reference", dest="compare_reference", action="store_false",
+                   help="skip the same-call reference-equivalent run (vs_baseline then null)")
+    p.add_argument("--compare-reference", dest="compare_reference", action="store_true")
+    p.add_argument("--sink-crc-salt", type=int, default=0,
+                   help="salt of the sink's CRC subset (0: random per run)")
+    p.add_argument("--ref-procs", type=int, default=8,
+                   help="reference mode: serial prefetch-1 consumers (processes) on the rank's "
+                        "CPUs - BASELINE.json config 2 runs 8 workers")
+    p.add_argument("--ref-jobs", type=int, default=128, help="reference mode: timed jobs")
+    p.add_argument("--ref-warmup-jobs", type=int, default=2,
+                   help="reference mode: untimed jobs per process first")
+    p.add_argument("--workers-curve", default="1,2,4,8",
+                   help="worker-process counts of the same-call curve (MB/s + p50 at each; "
+                        "'' = skip)")
+    p.add_argument("--curve-steps", type=int, default=3, help="timed steps per curve point")
+    p.add_argument("--curve-warmup-jobs", type=int, default=8,
+                   help="untimed jobs per worker process before each curve point")
     return p.parse_args()
 
 
@@ -246,12 +275,17 @@ async def _start_worker(args, endpoint: str, mode: str, stage_root: str):
 
 def _tag(args, mode: str) -> str:
     """Job-id tag of a measurement: each one stages fresh ids (no done-marker skips)."""
-    return (mode + ("-1put" if getattr(args, "single_put", False) else "")
-            + ("-crc" if getattr(args, "crc_run", False) else ""))
+    return f"{mode}-m{getattr(args, 'measure_seq', 0)}"
+
+
+def _warmup_jobs(args) -> int:
+    """Untimed jobs each worker process stages before "go"."""
+    w = getattr(args, "warmup_jobs", None)
+    return args.warmup * args.jobs_per_step if w is None else w
 
 
 async def _warmup(args, worker, url, wid: int, mode: str) -> None:
-    _, wres = await run_phase(worker, url, wid, 0, args.warmup * args.jobs_per_step,
+    _, wres = await run_phase(worker, url, wid, 0, _warmup_jobs(args),
                               int(args.size_mb * 1e6), _tag(args, mode))
     bad = [r for r in wres if r.outcome != "staged"]
     if bad:
@@ -269,12 +303,11 @@ async def _timed(args, worker, url, wid: int, mode: str, count: int) -> dict:
     """The timed jobs of one worker process; ``elapsed`` is this process' own view and
     ``cpu_s`` / ``sys_s`` the CPU it spent inside that window only (no interpreter start,
     imports or warmup jobs)."""
-    B = args.jobs_per_step
     rc0 = _relay_counters()
     cpu0, sys0 = _cpu()
     t0 = time.perf_counter()
     loop_cpu0 = time.thread_time()
-    dt, res = await run_phase(worker, url, wid, args.warmup * B, count,
+    dt, res = await run_phase(worker, url, wid, _warmup_jobs(args), count,
                               int(args.size_mb * 1e6), _tag(args, mode))
     loop_cpu = time.thread_time() - loop_cpu0
     t1 = time.perf_counter()
@@ -449,11 +482,13 @@ def rank_procs(args, dist: Dist, endpoint: str, mode: str, stage_root: str, npro
 
 SINK_KEYS = ("bytes_received", "verify_objects", "verify_bytes", "verify_mismatches",
              "verify_unknown", "multipart_objects", "multipart_parts", "objects", "bad_digests",
-             "checksummed_puts")
+             "checksummed_puts", "crc_checked_puts", "crc_unchecked_puts", "media_puts",
+             "media_puts_crc")
 
 
 def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 1,
             cpus: Optional[list] = None):
+    args.measure_seq = getattr(args, "measure_seq", 0) + 1
     stage_root = args.stage_dir or tempfile.mkdtemp(prefix=f"stager-bench-r{dist.rank}-")
     at_go: dict = {}
     peer_cpu = [0.0, 0.0]
@@ -489,6 +524,7 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
     out["sink"] = {k: int(end.get(k, 0)) - int(at_go.get(k, 0)) for k in SINK_KEYS}
     out["sink"]["mismatches_total"] = int(end.get("verify_mismatches", 0))
     out["sink"]["unknown_total"] = int(end.get("verify_unknown", 0))
+    out["sink"]["bad_digests_total"] = int(end.get("bad_digests", 0))
     allr = dist.gather(out)
     elapsed = max(r["elapsed"] for r in allr)
     total_bytes = sum(r["bytes"] for r in allr)
@@ -498,6 +534,13 @@ def measure(args, dist: Dist, endpoint: str, mode: str, blob=None, nproc: int = 
     jobs = args.steps * args.jobs_per_step * dist.world
     if failed:
         raise RuntimeError(f"{failed} timed jobs failed: {[r['err'] for r in allr if r['err']][:1]}")
+    if sink["bad_digests_total"]:
+        raise RuntimeError(f"S3 peer refused {sink['bad_digests_total']} bodies whose payload "
+                           f"checksum did not match their bytes")
+    if integrity(args, args.checksum, mode) == "crc32c" and blob is not None \
+            and sink["media_puts_crc"] < sink["media_puts"]:
+        raise RuntimeError(f"{sink['media_puts'] - sink['media_puts_crc']} of "
+                           f"{sink['media_puts']} timed media PUTs / parts carried no CRC32C")
     if sink["bytes_received"] < total_bytes:
         raise RuntimeError(f"S3 peer received {sink['bytes_received']} bytes in the timed region "
                            f"< {total_bytes} claimed staged")
@@ -582,17 +625,20 @@ def pin_rank(dist: Dist, per_rank: int = 0) -> list:
     return cpus.pin_share(local, nlocal, per_rank)
 
 
-def integrity(args, checksum: str) -> str:
+def integrity(args, checksum: str, mode: str = "") -> str:
     """Payload integrity of the measured uploads: ``crc32c`` when every PUT / part carries an
-    x-amz-checksum-crc32c the sink recomputes, ``none`` when the relay is spliced unchecked
-    (``s3.checksum: auto`` on a plain-http relay: bytes never cross user space)."""
-    pol = checksum or "auto"
+    x-amz-checksum-crc32c (the sink checks each one's form and recomputes a salted subset),
+    ``sha256`` for reference mode over plain http (minio-js signs every payload), ``none``
+    when the relay is spliced unchecked (``s3.checksum: auto`` on a plain-http relay, or
+    ``off``)."""
+    if (mode or args.mode) == "reference":
+        return "sha256" if args.tls == "off" else "crc32c"
+    pol = checksum or "always"
     if pol == "off":
         return "none"
     if pol == "always":
         return "crc32c"
-    return "crc32c" if (args.tls != "off" or args.staging == "disk" or args.mode != "tuned") \
-        else "none"
+    return "crc32c" if (args.tls != "off" or args.staging == "disk") else "none"
 
 
 def slot_budget() -> tuple:
@@ -605,6 +651,37 @@ def slot_budget() -> tuple:
     q = cpus.cgroup_cpu_quota()
     budget = mask if q == math.inf else min(mask, max(1, math.ceil(q)))
     return slots, budget // max(1, slots)
+
+
+@contextlib.contextmanager
+def _override(args, **kw):
+    """Run one extra measurement with some arguments changed."""
+    saved = {k: getattr(args, k, None) for k in kw}
+    for k, v in kw.items():
+        setattr(args, k, v)
+    try:
+        yield
+    finally:
+        for k, v in saved.items():
+            setattr(args, k, v)
+
+
+def _plan_pipes(args, dist: Dist, nproc: int, base_conc: int) -> None:
+    """Splice pipes: every worker process on the node shares one uid's pipe page budget
+    (64 MiB for the unprivileged user of the GPU boxes); each relay in flight holds one."""
+    from downloader_amd.utils import limits
+    if args.pipe_kb:
+        args.pipe_kb_eff = args.pipe_kb
+        args.concurrency = base_conc
+    else:
+        args.concurrency, pipe = limits.relay_plan(base_conc, 2, dist.world * nproc)
+        args.pipe_kb_eff = pipe >> 10
+
+
+def _cpu_fields(m: dict, prefix: str = "") -> dict:
+    return {f"{prefix}worker_cpu_s_per_GB": round(m["worker_cpu_s_per_GB"], 4),
+            f"{prefix}peer_cpu_s_per_GB": round(m["peer_cpu_s_per_GB"], 4),
+            f"{prefix}cpu_utilisation": round(m["timed_cpu_s"] / max(1e-9, m["cpu_capacity_s"]), 3)}
 
 
 def main() -> int:
@@ -622,7 +699,8 @@ def main() -> int:
     if args.peers == "per-rank" or dist.rank == 0:
         # Native origin + S3 sink. per-rank: every worker gets its own peer (the external world
         # is not the bottleneck being measured); shared: one peer on rank 0 for all workers.
-        blob = Blobd(default_size=int(args.size_mb * 1e6), sink=args.sink, tls=cert).start()
+        blob = Blobd(default_size=int(args.size_mb * 1e6), sink=args.sink, tls=cert,
+                     crc_check=args.sink_crc_check, crc_salt=args.sink_crc_salt).start()
         endpoint = blob.endpoint
     if args.peers == "shared":
         endpoint, ca = dist.bcast((endpoint, cert[0] if cert else ""))
@@ -636,33 +714,45 @@ def main() -> int:
         nproc = max(1, min(8, len(pinned or os.sched_getaffinity(0)) // 8))
     if args.mode == "reference" and args.procs_per_rank <= 0:
         nproc = 1    # the reference is one serial consumer per container (explicit N: N of them)
-    # Splice pipes: every worker process on the node shares one uid's pipe page budget
-    # (64 MiB for the unprivileged user of the GPU boxes); each relay in flight holds one.
     from downloader_amd.utils import limits
-    if args.pipe_kb:
-        args.pipe_kb_eff = args.pipe_kb
-    else:
-        args.concurrency, pipe = limits.relay_plan(args.concurrency, 2, dist.world * nproc)
-        args.pipe_kb_eff = pipe >> 10
+    base_conc = args.concurrency
+    _plan_pipes(args, dist, nproc, base_conc)
+    head_conc, head_pipe_kb = args.concurrency, args.pipe_kb_eff
+    tuned_mode = args.mode == "tuned"
     try:
         tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
-        single = None
-        if args.compare_single_put and args.mode == "tuned":
-            args.single_put = True
-            single = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
-            args.single_put = False
-        crc = None
-        if args.compare_crc and args.mode == "tuned" and args.checksum != "always":
-            saved, args.checksum, args.crc_run = args.checksum, "always", True
-            crc = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
-            args.checksum, args.crc_run = saved, False
-        ref = measure(args, dist, endpoint, "reference", blob) if args.compare_reference else None
-        tor = torrent_measure(args, dist) if args.torrent_gb > 0 and args.mode == "tuned" else None
+        unchecked = single = ref = tor = None
+        curve = []
+        if args.compare_unchecked and tuned_mode and integrity(args, args.checksum) == "crc32c":
+            with _override(args, checksum="auto"):
+                if integrity(args, "auto") == "none":
+                    unchecked = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
+        if args.compare_single_put and tuned_mode:
+            with _override(args, single_put=True):
+                single = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
+        if args.compare_reference and tuned_mode and args.ref_procs > 0:
+            rp = args.ref_procs
+            jobs = max(rp, args.ref_jobs)
+            with _override(args, steps=1, jobs_per_step=jobs, warmup_jobs=args.ref_warmup_jobs):
+                _plan_pipes(args, dist, rp, 1)
+                ref = measure(args, dist, endpoint, "reference", blob, rp, pinned)
+        for k in [int(x) for x in args.workers_curve.split(",") if x.strip()] if tuned_mode else []:
+            with _override(args, steps=args.curve_steps, warmup_jobs=args.curve_warmup_jobs):
+                _plan_pipes(args, dist, k, base_conc)
+                m = measure(args, dist, endpoint, args.mode, blob, k, pinned)
+                curve.append({"procs": k, "MBps": round(m["mbps"], 1),
+                              "p50_s": round(m["p50"], 4), "p90_s": round(m["p90"], 4),
+                              "concurrency_per_worker": args.concurrency,
+                              "cpu_utilisation": round(m["timed_cpu_s"]
+                                                       / max(1e-9, m["cpu_capacity_s"]), 3)})
+        args.concurrency, args.pipe_kb_eff = head_conc, head_pipe_kb
+        tor = torrent_measure(args, dist) if args.torrent_gb > 0 and tuned_mode else None
     finally:
         if blob is not None:
             blob.stop()
     if dist.rank == 0:
         n = dist.world
+        ts = tuned["sink"]
         line = {
             "metric": METRIC,
             "value": round(tuned["mbps"], 2),
@@ -673,17 +763,28 @@ def main() -> int:
             "ms_per_step": round(tuned["elapsed"] / max(1, args.steps) * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            # headline / the same call's reference-equivalent mode (the reference
+            # publishes no number; this mode stands in for it on the same CPUs)
+            "vs_baseline": round(tuned["mbps"] / ref["mbps"], 3) if ref else None,
             "dtype": "bytes",
             "data": "synthetic random-byte media blobs served by the native blobd origin",
             "p50_job_latency_s": round(tuned["p50"], 4),
+            # what the headline's bytes were checked with on the way to S3: crc32c = every PUT /
+            # part carried an x-amz-checksum-crc32c of its payload (the sink checked that each
+            # is there and well-formed, and recomputed the crc_checked_parts subset)
+            "integrity": integrity(args, args.checksum),
+            "sink_crc_check": f"1/{args.sink_crc_check}",
+            "crc_parts": ts["media_puts_crc"],
+            "media_parts": ts["media_puts"],
+            "crc_checked_parts": ts["crc_checked_puts"],
+            "bad_digests": ts["bad_digests"],
             # S3 side, counted by the sink itself between "go" and the end of the timed jobs
-            "timed_sink_bytes": tuned["sink"]["bytes_received"],
+            "timed_sink_bytes": ts["bytes_received"],
             "parts_per_object": tuned["parts_per_object"],
             "sink": args.sink,
-            "sink_verified_objects": tuned["sink"]["verify_objects"],
-            "sink_verified_bytes": tuned["sink"]["verify_bytes"],
-            "sink_mismatches": tuned["sink"]["mismatches_total"],
+            "sink_verified_objects": ts["verify_objects"],
+            "sink_verified_bytes": ts["verify_bytes"],
+            "sink_mismatches": ts["mismatches_total"],
             "worker_cpu_s_per_GB": round(tuned["worker_cpu_s_per_GB"], 4),
             "worker_kernel_share": round(tuned["worker_sys_share"], 3),   # system / (user+system)
             "event_loop_busy": round(tuned["loop_busy"], 3),
@@ -694,11 +795,8 @@ def main() -> int:
             "worker_breakdown": tuned["breakdown"],
             # splice pipes created below their asked capacity (pipe page budget spent)
             "pipes_short": {"workers": tuned["pipes_short"], "of": tuned["pipes_created"]},
-            "pipe_kb": args.pipe_kb_eff,
+            "pipe_kb": head_pipe_kb,
             "pipe_budget_bytes": limits.pipe_budget_bytes(),
-            # what the headline's bytes were checked with on the way to S3 (the CRC'd relay
-            # of the same call is crc_relay_MBps)
-            "integrity": integrity(args, args.checksum),
             "gpu_slots": slots,
             "slot_budget_cpus": slot_cpus,
             "peers": args.peers,
@@ -707,10 +805,10 @@ def main() -> int:
             "rank_peers": [t["peer"] for t in topo],
             "p90_job_latency_s": round(tuned["p90"], 4),
             "mode": args.mode,
-            **({"checksum": args.checksum} if args.checksum else {}),
+            "checksum": args.checksum or "always",
             "staging": args.staging if args.mode == "tuned" else "disk",
             **({"tls": args.tls} if args.tls != "off" else {}),
-            "concurrency_per_worker": args.concurrency if args.mode == "tuned" else 1,
+            "concurrency_per_worker": head_conc if args.mode == "tuned" else 1,
             "procs_per_rank": nproc,
             "config": {
                 "model": "BASELINE.json config 2: HTTP media blob -> S3 multipart staging",
@@ -722,27 +820,27 @@ def main() -> int:
                 "jobs_timed": n * args.steps * args.jobs_per_step,
             },
         }
+        if ref is not None:      # same call: reference-equivalent mode
+            line["reference_mode_MBps"] = round(ref["mbps"], 2)
+            line["reference_mode_p50_s"] = round(ref["p50"], 4)
+            line["reference_mode_procs"] = args.ref_procs
+            line["reference_mode_jobs"] = n * max(args.ref_procs, args.ref_jobs)
+            line["reference_mode_integrity"] = integrity(args, args.checksum, "reference")
+            line.update(_cpu_fields(ref, "reference_mode_"))
+        if curve:                # same call: MB/s and p50 at 1/2/4/8 worker processes
+            line["workers_curve"] = curve
+        if unchecked is not None:   # same call: the spliced relay with no payload checksum
+            line["unchecked_MBps"] = round(unchecked["mbps"], 2)
+            line["unchecked_p50_s"] = round(unchecked["p50"], 4)
+            line["unchecked_integrity"] = "none"
+            line.update(_cpu_fields(unchecked, "unchecked_"))
+            line["unchecked_worker_breakdown"] = unchecked["breakdown"]
         if single is not None:   # same call, round-2 settings: 100 MB objects in one PUT
             line["single_put_MBps"] = round(single["mbps"], 2)
             line["single_put_p50_s"] = round(single["p50"], 4)
             line["single_put_parts_per_object"] = single["parts_per_object"]
-        if crc is not None:      # same call, a CRC32C on every relayed PUT / part
-            line["crc_relay_MBps"] = round(crc["mbps"], 2)
-            line["crc_relay_p50_s"] = round(crc["p50"], 4)
-            line["crc_relay_worker_cpu_s_per_GB"] = round(crc["worker_cpu_s_per_GB"], 4)
-            # the sink recomputes every CRC (recv + CRC instead of splice) on the same CPUs
-            line["crc_relay_peer_cpu_s_per_GB"] = round(crc["peer_cpu_s_per_GB"], 4)
-            line["crc_relay_cpu_utilisation"] = round(
-                crc["timed_cpu_s"] / max(1e-9, crc["cpu_capacity_s"]), 3)
-            line["crc_relay_worker_breakdown"] = crc["breakdown"]
-            line["crc_relay_sink_checked_puts"] = crc["sink"]["checksummed_puts"]
-            line["crc_relay_integrity"] = "crc32c"
         if tor is not None:      # same call: streamed torrent, GPU vs host piece hashing
             line.update(tor)
-        if ref is not None:
-            line["reference_mode_MBps"] = round(ref["mbps"], 2)
-            line["reference_mode_p50_s"] = round(ref["p50"], 4)
-            line["vs_reference_mode"] = round(tuned["mbps"] / ref["mbps"], 3)
         print(json.dumps(line), flush=True)
     dist.close()
     return 0

@@ -31,7 +31,8 @@ class Blobd:
                  tls: Optional[Tuple[str, str]] = None, s3_fail_rate: float = 0.0,
                  synth_bucket: str = "", synth_objects: Optional[Dict[str, int]] = None,
                  s3_corrupt_rate: float = 0.0,
-                 synth_files: Optional[Dict[str, Tuple[int, int]]] = None):
+                 synth_files: Optional[Dict[str, Tuple[int, int]]] = None,
+                 crc_check: int = 1, crc_salt: int = 0, synth_shift: int = 0):
         self.files_root = files_root
         # webseed files served from the origin pool: relpath -> (size, seed)
         self.synth_files = dict(synth_files or {})
@@ -42,6 +43,12 @@ class Blobd:
         self.synth_bucket = synth_bucket  # read-only source bucket of synthetic objects
         self.synth_objects = dict(synth_objects or {})
         self.sink = sink
+        # recompute the CRC32C of 1 in crc_check checksummed bodies (salted hash of key + part:
+        # fixed for a run, unknown to the sender; 0 salt = random); the rest are dropped in the
+        # kernel after their trailer is checked for form
+        self.crc_check = max(1, int(crc_check))
+        self.crc_salt = int(crc_salt)
+        self.synth_shift = int(synth_shift)   # serve the synth files this many bytes off (tests)
         self.keep_bytes = keep_bytes
         self.default_size = default_size
         self.host = host
@@ -49,7 +56,8 @@ class Blobd:
         self.port = 0
 
     def start(self, timeout: float = 30.0) -> "Blobd":
-        exe = build.build_blobd(verbose=False)
+        # STAGER_BLOBD_EXE: another build of the peer (A/B of a generator change)
+        exe = os.environ.get("STAGER_BLOBD_EXE") or build.build_blobd(verbose=False)
         d = tempfile.mkdtemp(prefix="blobd-")
         pf = os.path.join(d, "port")
         self.proc = subprocess.Popen(
@@ -57,6 +65,9 @@ class Blobd:
              "--keep-bytes", str(self.keep_bytes), "--default-size", str(self.default_size)]
             + (["--files-root", self.files_root] if self.files_root else [])
             + ["--sink", self.sink]
+            + (["--crc-check", str(self.crc_check)] if self.crc_check > 1 else [])
+            + (["--crc-salt", str(self.crc_salt)] if self.crc_salt else [])
+            + (["--synth-shift", str(self.synth_shift)] if self.synth_shift else [])
             + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else [])
             + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else [])
             + (["--s3-corrupt-rate", str(self.s3_corrupt_rate)] if self.s3_corrupt_rate else [])
@@ -94,7 +105,8 @@ class Blobd:
         return p
 
     def pool(self) -> bytes:
-        """The origin's 64 MiB byte pool: synthetic byte o of seed s = pool[(o + 7919 s) % 64 MiB]."""
+        """The origin's byte pool (64 MiB + 4 KiB): synthetic byte o of seed s =
+        pool[(o + 7919 s) % len(pool)]."""
         with urllib.request.urlopen(f"http://{self.endpoint}/_pool", timeout=60) as r:
             return r.read()
 
@@ -118,6 +130,13 @@ class Blobd:
             return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
         except (OSError, IndexError, ValueError):
             return 0.0
+
+    def crc_selected(self, key: str, part: int = 0) -> bool:
+        """Does the sink recompute the CRC32C of this body (``--crc-check`` subset)?"""
+        from urllib.parse import urlencode
+        with urllib.request.urlopen(f"http://{self.endpoint}/_crc_selected?"
+                                    + urlencode({"key": key, "part": part}), timeout=10) as r:
+            return r.read().strip() == b"1"
 
     def stats(self) -> Dict[str, int]:
         ctx = None

@@ -1,11 +1,13 @@
 """Torrents whose files are the bench origin's synthetic bytes (no data on disk).
 
-``blobd --synth-files`` serves BEP-19 webseed files made of its 64 MiB origin pool: byte ``o``
-of a file with seed ``s`` is ``pool[(o + 7919 s) % 64 MiB]`` (the same rule as its
-``/media/`` origin). This module writes the metainfo for such a file set: the piece SHA-1s are
-computed over the same rule, and because a file's bytes repeat every 64 MiB, a piece's content
-is fixed by where it starts in the pool - pieces that start at the same pool offset share
-their hash, so a 20 GB torrent of 4 MiB pieces costs a few GB of hashing, not 20, and no disk.
+``blobd --synth-files`` serves BEP-19 webseed files made of its origin pool: byte ``o`` of a
+file with seed ``s`` is ``pool[(o + 7919 s) % POOL]`` (the same rule as its ``/media/``
+origin). POOL is 64 MiB + 4 KiB, an odd number of pages: no power-of-two part or piece size
+divides it, so data fetched from the wrong part / piece offset never carries the right bytes
+(``csrc/blobd.cpp`` kPool). This module writes the metainfo for such a file set: the piece
+SHA-1s are computed over the same rule. Pieces that start at the same pool offset share their
+hash (computed once); with the odd period that happens only every 16385 pieces, so the
+hashing costs about the torrent's size, spread over threads, and no disk.
 
 Used by ``bench.py`` for the config-4-shaped GPU vs host A/B (20 GB, 50 files, 4 MiB pieces)
 that the driver's bench line carries, and by the tests in miniature.
@@ -18,7 +20,7 @@ from typing import Dict, List, Sequence, Tuple
 
 from ..torrent.bencode import bencode
 
-POOL = 64 << 20
+POOL = (64 << 20) + 4096     # blobd's kPool
 STRIDE = 7919
 
 
@@ -35,7 +37,7 @@ def served_paths(name: str, files: Sequence[Tuple[str, int, int]]) -> Dict[str, 
     return {f"{name}/{rel}": (size, seed) for rel, size, seed in files}
 
 
-def _segments(files: Sequence[Tuple[str, int, int]], piece_len: int):
+def _segments(files: Sequence[Tuple[str, int, int]], piece_len: int, period: int = POOL):
     """Per piece: the (pool offset, length) runs it is made of, in order."""
     out: List[Tuple[Tuple[int, int], ...]] = []
     cur: List[Tuple[int, int]] = []
@@ -44,7 +46,7 @@ def _segments(files: Sequence[Tuple[str, int, int]], piece_len: int):
         off = 0
         while off < size:
             k = min(room, size - off)
-            cur.append(((off + seed * STRIDE) % POOL, k))
+            cur.append(((off + seed * STRIDE) % period, k))
             off += k
             room -= k
             if room == 0:
@@ -57,12 +59,10 @@ def _segments(files: Sequence[Tuple[str, int, int]], piece_len: int):
 
 def piece_hashes(pool: bytes, files: Sequence[Tuple[str, int, int]], piece_len: int,
                  threads: int = 8) -> bytes:
-    if len(pool) != POOL:
-        raise ValueError(f"pool is {len(pool)} bytes, want {POOL}")
-    if piece_len > POOL:
+    if len(pool) < piece_len:
         raise ValueError("piece length above the pool size")
     ring = memoryview(pool + pool[:piece_len])     # any run of <= piece_len bytes is contiguous
-    segs = _segments(files, piece_len)
+    segs = _segments(files, piece_len, len(pool))   # the served pool's period (POOL normally)
     uniq = list(dict.fromkeys(segs))
 
     def h(key) -> bytes:

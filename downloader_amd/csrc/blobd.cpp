@@ -10,7 +10,8 @@
 //            PUT|GET|HEAD|DELETE /<bucket>/<key>, multipart (POST ?uploads, PUT ?partNumber,
 //            POST ?uploadId, DELETE ?uploadId)
 //   stats:   GET /_stats  (JSON: bytes received/served, objects, requests)
-//   pool:    GET /_pool   (the 64 MiB pool every synthetic byte is taken from)
+//   pool:    GET /_pool   (the pool every synthetic byte is taken from: 64 MiB + 4 KiB, see kPool)
+//   crc:     GET /_crc_selected?key=K&part=N  ("1" when --crc-check recomputes that body's CRC)
 //   --synth-files FILE ("<path> <size> <seed>" lines): BEP-19 webseed files under
 //            /files/<path> made of pool bytes (a 20 GB torrent without 20 GB on disk)
 //   --synth-bucket NAME --synth-manifest FILE ("<key> <size>" lines): a read-only source
@@ -42,6 +43,12 @@
 // an aws-chunked trailer (`x-amz-trailer`, `Content-Encoding: aws-chunked`), and `Content-MD5`;
 // a mismatch is answered 400 BadDigest and nothing is stored. --s3-corrupt-rate P flips one
 // byte of that share of checksummed bodies on arrival (transit corruption, fault injection).
+// --crc-check N recomputes the CRC32C of a deterministic 1-in-N subset of the checksummed
+// bodies (selected by a salted hash of key + part number the sender cannot predict,
+// --crc-salt); the others must still carry a well-formed CRC but are dropped in the kernel
+// like the sample sink's bytes. The bench's S3 then stops costing the worker's CPU slice a
+// full second read of every byte while any wrong CRC the worker sends is still caught with
+// probability 1/N per body (counters crc_checked_puts / crc_unchecked_puts / bad_digests).
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -128,10 +135,23 @@ std::string g_synth_bucket;                       // --synth-bucket
 // bytes are the origin pool's (no disk, sendfile from the pool's memfd)
 std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> g_synth_files;
 std::map<std::string, uint64_t> g_synth_objects;  // key -> size (--synth-manifest)
+uint64_t g_synth_shift = 0;  // --synth-shift B: webseed files served B bytes off (fault tests)
 double g_s3_fail_rate = 0;  // --s3-fail-rate: this share of object/part PUTs answer 503 SlowDown
 std::atomic<uint64_t> g_s3_faults{0};
+uint64_t g_crc_check = 1;        // --crc-check N: recompute 1 in N checksummed bodies
+uint64_t g_crc_salt = 0;         // --crc-salt S (default: random per run)
+std::atomic<uint64_t> g_crc_checked{0}, g_crc_unchecked{0}, g_media_puts{0}, g_media_puts_crc{0};
 
-constexpr size_t kPool = 64ull << 20;
+// Pool period: 64 MiB + one 4 KiB page. A period that divided the multipart part size (64 MiB)
+// or the torrent piece length (4 MiB) would make a part fetched with another part's Range, or
+// a webseed read shifted by whole parts, carry the very bytes it should: with 16385 pages
+// (odd, so coprime with every power of two) an offset error of k x 4 MiB aliases only when
+// k is a multiple of 16385 (64 GiB). Every rule below (origin, webseeds, sink compare,
+// bench/synth_torrent.py) uses this one constant.
+#ifndef BLOBD_POOL_BYTES      // (-D only to rebuild the round-5 generator for the A/B test)
+#define BLOBD_POOL_BYTES ((64ull << 20) + 4096)
+#endif
+constexpr size_t kPool = BLOBD_POOL_BYTES;
 
 uint64_t mix(uint64_t h, uint64_t v) {
   h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
@@ -165,6 +185,16 @@ struct Summer {
   }
   uint64_t final() const { return nc ? mix(h, carry ^ ((uint64_t)nc << 56)) : h; }
 };
+
+// Is the CRC32C of this body (`key`, multipart part number or 0) recomputed? A salted hash,
+// so the subset is fixed for a run but not known to the sender.
+bool crc_selected(const std::string& key, int part) {
+  if (g_crc_check <= 1) return true;
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (unsigned char ch : key) h = (h ^ ch) * 0x100000001b3ull;
+  h = mix(mix(g_crc_salt, h), (uint64_t)(uint32_t)part);
+  return (h >> 17) % g_crc_check == 0;
+}
 
 std::string hex64(uint64_t a, uint64_t b) {
   char buf[40];
@@ -613,16 +643,10 @@ class Conn {
           trailers[name] = vs == std::string::npos ? "" : line.substr(vs);
         }
       }
-      uint64_t left = k;
-      while (left > 0) {
-        if (pos_ == end_ && !fill()) return false;
-        size_t t = (size_t)std::min<uint64_t>(left, end_ - pos_);
-        c.feed(data_len, buf_.data() + pos_, t);
-        pos_ += t;
-        left -= t;
-        data_len += t;
-        g_rx += t;
-      }
+      // buffered bytes first, then the socket: dropped in the kernel (windows aside) when
+      // nothing needs every byte (a body outside the --crc-check subset on a discarding sink)
+      if (!read_plain((int64_t)k, c, data_len)) return false;
+      data_len += k;
       if (!get_line(line) || !line.empty()) return false;
     }
   }
@@ -720,7 +744,8 @@ class Conn {
   }
 
   // GET|HEAD (with Range) of a synthetic object: byte o = pool[(o + seed * 7919) % kPool].
-  bool serve_pool(const Request& r, uint64_t size, uint64_t seed, const char* ctype) {
+  bool serve_pool(const Request& r, uint64_t size, uint64_t seed, const char* ctype,
+                  uint64_t shift = 0) {
     uint64_t start = 0, end = size ? size - 1 : 0;
     bool ranged = false;
     auto it = r.h.find("range");
@@ -754,7 +779,7 @@ class Conn {
     if (r.method == "HEAD") return true;
     // Object byte at offset o = pool[(o + seed * 7919) % kPool]; the pool lives in a memfd so
     // the body goes out with sendfile (page references, no user-space copy).
-    uint64_t o = start, left = len;
+    uint64_t o = start + shift, left = len;
     while (left) {
       uint64_t po = (o + seed * 7919ull) % kPool;
       size_t k = (size_t)std::min<uint64_t>(left, std::min<uint64_t>(kPool - po, 4ull << 20));
@@ -781,7 +806,8 @@ class Conn {
   bool files(const Request& r) {
     std::string rel = r.path.substr(7);
     auto sy = g_synth_files.find(rel);      // a synthetic file (--synth-files): the origin pool
-    if (sy != g_synth_files.end()) return serve_pool(r, sy->second.first, sy->second.second, "");
+    if (sy != g_synth_files.end())
+      return serve_pool(r, sy->second.first, sy->second.second, "", g_synth_shift);
     if (g_files_root.empty() || rel.find("..") != std::string::npos)
       return respond(404, "Not Found", "no such file", "", "text/plain");
     std::string full = g_files_root + "/" + rel;
@@ -940,7 +966,10 @@ class Conn {
       const bool trailer_crc =
           tr != r.h.end() && strcasestr(tr->second.c_str(), "x-amz-checksum-crc32c") != nullptr;
       auto hm = r.h.find("content-md5");
-      c.crc_on = hc != r.h.end() || trailer_crc;
+      const bool has_crc = hc != r.h.end() || trailer_crc;
+      const int part_no = part ? atoi(r.q.count("partNumber") ? r.q.at("partNumber").c_str() : "0") : 0;
+      c.crc_on = has_crc && crc_selected(key, part_no);
+      if (has_crc) (c.crc_on ? g_crc_checked : g_crc_unchecked)++;
       if (hm != r.h.end()) {
         c.md5 = EVP_MD_CTX_new();
         EVP_DigestInit_ex(c.md5, EVP_md5(), nullptr);
@@ -952,6 +981,11 @@ class Conn {
         c.keep = g_keep_bytes;
       }
       const bool checking = g_sink == kSinkSample || g_sink == kSinkVerify;
+      if (key.find("/original/") != std::string::npos &&
+          !(key.size() >= 5 && key.compare(key.size() - 5, 5, "/done") == 0)) {
+        g_media_puts++;
+        if (has_crc) g_media_puts_crc++;
+      }
       bool media_like = false, known = false;
       uint64_t msize = 0, mseed = 0;
       if (checking) {
@@ -975,8 +1009,17 @@ class Conn {
         got = (uint64_t)std::max<int64_t>(0, r.content_length);
       }
       std::string extra;
-      if (c.crc_on || c.md5) g_checksummed++;
+      if (has_crc || c.md5) g_checksummed++;
       if (chunked && got != dlen) return s3_error(400, "Bad Request", "IncompleteBody", key);
+      if (has_crc && !c.crc_on) {     // not recomputed: it must still be there, well-formed
+        const std::string& v = hc != r.h.end() ? hc->second : trailers["x-amz-checksum-crc32c"];
+        std::string raw;
+        if (v.size() != 8 || !b64_decode(v, raw) || raw.size() != 4) {
+          g_bad_digest++;
+          return s3_error(400, "Bad Request", "InvalidDigest", key);
+        }
+        extra += "x-amz-checksum-crc32c: " + v + "\r\n";
+      }
       if (c.crc_on) {
         char b[9];
         crc32c_b64(c.crc, b);
@@ -1009,7 +1052,7 @@ class Conn {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_uploads.find(r.q.at("uploadId"));
         if (it == g_uploads.end()) return s3_error(404, "Not Found", "NoSuchUpload", key);
-        int num = atoi(r.q.count("partNumber") ? r.q.at("partNumber").c_str() : "0");
+        int num = part_no;
         it->second.parts[num] = std::move(o);
         if (checking && media_like) it->second.checks[num] = std::move(chk);
         g_parts++;
@@ -1113,7 +1156,7 @@ class Conn {
   }
 
   bool stats() {
-    char b[1536];
+    char b[2048];
     size_t nup;
     {
       std::lock_guard<std::mutex> lk(g_mu);
@@ -1127,16 +1170,24 @@ class Conn {
              ",\"sink\":\"%s\",\"verify_objects\":%" PRIu64 ",\"verify_bytes\":%" PRIu64
              ",\"verify_mismatches\":%" PRIu64 ",\"verify_unknown\":%" PRIu64
              ",\"checksummed_puts\":%" PRIu64 ",\"bad_digests\":%" PRIu64 ",\"corrupted\":%" PRIu64
-             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64 "}",
+             ",\"parts\":%" PRIu64 ",\"multipart_objects\":%" PRIu64 ",\"multipart_parts\":%" PRIu64
+             ",\"crc_check\":%" PRIu64 ",\"crc_checked_puts\":%" PRIu64 ",\"crc_unchecked_puts\":%" PRIu64
+             ",\"media_puts\":%" PRIu64 ",\"media_puts_crc\":%" PRIu64 "}",
              g_rx.load(), g_tx.load(), g_reqs.load(), g_objects.load(), nup, g_s3_faults.load(), sink,
              g_verify_objects.load(), g_verify_bytes.load(), g_verify_mismatch.load(),
              g_verify_unknown.load(), g_checksummed.load(), g_bad_digest.load(), g_corrupted.load(),
-             g_parts.load(), g_mp_objects.load(), g_mp_parts.load());
+             g_parts.load(), g_mp_objects.load(), g_mp_parts.load(), g_crc_check, g_crc_checked.load(),
+             g_crc_unchecked.load(), g_media_puts.load(), g_media_puts_crc.load());
     return respond(200, "OK", b, "", "application/json");
   }
 
   bool dispatch(const Request& r) {
     if (r.path == "/_stats") return stats();
+    if (r.path == "/_crc_selected") {
+      int part = atoi(r.q.count("part") ? r.q.at("part").c_str() : "0");
+      return respond(200, "OK", crc_selected(r.q.count("key") ? r.q.at("key") : "", part) ? "1" : "0",
+                     "", "text/plain");
+    }
     // the origin pool itself: lets a client build metainfo (piece hashes) for --synth-files
     if (r.path == "/_pool" && r.method == "GET") return serve_pool(r, kPool, 0, "");
     if (r.path.rfind("/media/", 0) == 0 && (r.method == "GET" || r.method == "HEAD")) return origin(r);
@@ -1175,6 +1226,9 @@ int main(int argc, char** argv) {
     else if (a == "--sample-stride") g_sample_stride = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
     else if (a == "--sample-len") g_sample_len = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
     else if (a == "--s3-corrupt-rate") g_s3_corrupt_rate = atof(next());
+    else if (a == "--crc-check") g_crc_check = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
+    else if (a == "--crc-salt") g_crc_salt = strtoull(next(), nullptr, 10);
+    else if (a == "--synth-shift") g_synth_shift = strtoull(next(), nullptr, 10);
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
     else if (a == "--s3-fail-rate") g_s3_fail_rate = atof(next());
@@ -1207,7 +1261,7 @@ int main(int argc, char** argv) {
     else {
       fprintf(stderr, "usage: blobd [--host H] [--port P] [--port-file F] [--keep-bytes N] "
                       "[--default-size N] [--files-root DIR] [--sink checksum|discard|sample|verify] "
-                      "[--sample-stride N] [--sample-len N] [--s3-corrupt-rate P] "
+                      "[--sample-stride N] [--sample-len N] [--s3-corrupt-rate P] [--crc-check N] [--crc-salt S] "
                       "[--tls-cert PEM --tls-key PEM] [--s3-fail-rate P]\n");
       return 2;
     }
@@ -1226,6 +1280,7 @@ int main(int argc, char** argv) {
     SSL_CTX_set_default_read_buffer_len(g_tls, 256 * 1024);
   }
   signal(SIGPIPE, SIG_IGN);
+  if (!g_crc_salt) g_crc_salt = std::random_device{}() | ((uint64_t)std::random_device{}() << 32);
   g_pool.resize(kPool);
   std::mt19937_64 rng(0xB10BDull);
   for (size_t i = 0; i < kPool; i += 8) {

@@ -4,6 +4,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <cstdlib>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
@@ -48,6 +50,47 @@ py::dict head_to_dict(const ResponseHead& h) {
 // Returns once the part's buffer is back in the pool (its DMA is over).
 void forget_ticket(uint64_t id) {
   if (id) gpu_part_forget(id);
+}
+
+// STAGER_FAULT_BAD_CRC=<pattern>[:count] (fault injection for the integrity tests): the
+// CRC32C trailer of the next `count` (default 1) relayed PUTs whose request head matches
+// `pattern` (substrings joined by '*', found in that order) goes out with one bit flipped, as a
+// corrupting hop between the worker's CRC and the socket would send it. The S3 side must
+// refuse it (400 BadDigest).
+static bool head_matches(const std::string& head, const std::string& pat) {
+  size_t at = 0, i = 0;
+  while (i <= pat.size()) {
+    size_t star = pat.find('*', i);
+    if (star == std::string::npos) star = pat.size();
+    std::string piece = pat.substr(i, star - i);
+    if (!piece.empty()) {
+      size_t f = head.find(piece, at);
+      if (f == std::string::npos) return false;
+      at = f + piece.size();
+    }
+    i = star + 1;
+  }
+  return true;
+}
+
+static bool fault_bad_crc(const std::string& put_head) {
+  static std::string pat;
+  static std::atomic<int64_t> left{[] {
+    const char* e = getenv("STAGER_FAULT_BAD_CRC");
+    if (!e || !*e) return (int64_t)0;
+    std::string v(e);
+    size_t c = v.rfind(':');
+    int64_t n = 1;
+    if (c != std::string::npos && c + 1 < v.size() &&
+        v.find_first_not_of("0123456789", c + 1) == std::string::npos) {
+      n = atoll(v.c_str() + c + 1);
+      v.resize(c);
+    }
+    pat = v;
+    return n;
+  }()};
+  if (left.load(std::memory_order_relaxed) <= 0 || !head_matches(put_head, pat)) return false;
+  return left.fetch_sub(1) > 0;
 }
 
 struct PieceSplit {
@@ -95,6 +138,7 @@ py::dict relay(HttpConn& src, const py::bytes& get_head, HttpConn& dst, const py
                                               crc ? &c : nullptr, gpu ? &ticket : nullptr)
                       : src.relay_body_to(dst, length, prog, crc ? &c : nullptr);
         if (crc) {
+          if (fault_bad_crc(ph)) c ^= 1u;
           crc_b64 = crc32c_base64(c);
           dst.send_raw(std::string(length > 0 ? "\r\n" : "") + "0\r\nx-amz-checksum-crc32c:" +
                        crc_b64 + "\r\n\r\n");

@@ -76,10 +76,12 @@ class S3Config(BaseModel):
     # threshold are relayed as up to max_inflight_parts parallel parts instead of one PUT
     split_tls_relays: bool = True
     # payload integrity per PUT / part: CRC32C (x-amz-checksum-crc32c) the server verifies.
-    # auto = wherever bytes cross user space anyway (memory, disk uploads, TLS relays,
-    # piece-hashed torrent relays); always = also the plain splice relay (copies through user
-    # space); off. minio-js sends Content-MD5 over https / a signed SHA-256 over http.
-    checksum: Literal["auto", "always", "off"] = "auto"
+    # always (default) = every PUT and part, the plain splice relay included (it peeks each
+    # byte once into user space for the CRC: +0.08 worker CPU-s/GB); auto = only where bytes
+    # cross user space anyway (memory, disk uploads, TLS relays, piece-hashed torrent relays:
+    # the plain relay then carries no payload checksum); off. minio-js hashes every byte it
+    # uploads: Content-MD5 over https / a signed SHA-256 over http (lib/upload.js:45).
+    checksum: Literal["auto", "always", "off"] = "always"
     connect_timeout_s: float = 10.0
     request_timeout_s: float = 300.0            # socket idle timeout of one request
     # retries of a retryable S3 error (5xx, SlowDown, resets) with jittered backoff

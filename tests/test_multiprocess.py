@@ -93,7 +93,7 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4", "--jobs-per-step", "2",
-           "--torrent-gb", "0.05", "--torrent-pairs", "1"]
+           "--torrent-gb", "0.05", "--torrent-pairs", "1", "--ref-jobs", "16", "--curve-steps", "1"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -104,6 +104,9 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
         assert k in j
     assert j["n_gpus"] == 2 and j["steps"] == 2 and j["value"] > 0
     assert j["config"]["jobs_timed"] == 2 * 2 * 2   # ranks x steps x jobs-per-step
+    # the default extras ran on both ranks (the driver launches N>1 with the defaults)
+    assert j["reference_mode_MBps"] > 0 and j["vs_baseline"] > 0 and len(j["workers_curve"]) == 4
+    assert j["integrity"] == "crc32c" and j["crc_parts"] == j["media_parts"] == 2 * 2 * 2
     # the torrent A/B ran on both ranks at once: rates and device counters are summed
     assert j["torrent_ranks"] == 2 and j["torrent_gpu_MBps"] > 0 and j["torrent_host_MBps"] > 0
 
@@ -112,23 +115,32 @@ def test_bench_single_rank_defaults_are_valid(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
                         "--warmup", "1", "--size-mb", "2", "--torrent-gb", "0.2",
-                        "--torrent-pairs", "1"], env=env, capture_output=True,
-                       text=True, timeout=300)
+                        "--torrent-pairs", "1", "--curve-steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["n_gpus"] == 1 and j["higher_is_better"] is True and j["scaling"] == "weak"
-    # same-call comparisons: one PUT per object, and a CRC32C on every relayed PUT / part that
-    # the sink recomputed (2 MB objects: 1 PUT + the done marker per job, 2 steps x 64 jobs)
-    assert j["single_put_MBps"] > 0 and j["crc_relay_MBps"] > 0
-    assert j["crc_relay_sink_checked_puts"] >= 2 * 64
-    # the line says what the headline's bytes were checked with (a spliced plain-http relay:
-    # nothing) and what the CRC'd run's were, with the CPU both sides spent on them
-    assert j["integrity"] == "none" and j["crc_relay_integrity"] == "crc32c"
-    assert j["crc_relay_worker_cpu_s_per_GB"] > 0 and j["crc_relay_peer_cpu_s_per_GB"] > 0
+    # the headline's bytes are checked: every timed media PUT carried a CRC32C (2 MB objects:
+    # one PUT per job, 2 steps x 64 jobs), the sink recomputed a salted 1-in-8 subset of them
+    # and refused none
+    assert j["integrity"] == "crc32c" and j["checksum"] == "always"
+    assert j["crc_parts"] == j["media_parts"] == 2 * 64 and j["bad_digests"] == 0
+    assert 0 < j["crc_checked_parts"] < j["crc_parts"] and j["sink_crc_check"] == "1/8"
+    # same call: the unchecked spliced relay, labelled as such
+    assert j["unchecked_MBps"] > 0 and j["unchecked_integrity"] == "none"
+    # same call: reference-equivalent mode (8 serial prefetch-1 consumers, SHA-256-signed
+    # payloads) on the same CPUs, and vs_baseline is the headline over it
+    assert j["reference_mode_MBps"] > 0 and j["reference_mode_procs"] == 8
+    assert j["reference_mode_integrity"] == "sha256"
+    assert j["vs_baseline"] == round(j["value"] / j["reference_mode_MBps"], 3)
+    # the BASELINE metric's curve: MB/s and p50 at 1/2/4/8 worker processes
+    assert [c["procs"] for c in j["workers_curve"]] == [1, 2, 4, 8]
+    assert all(c["MBps"] > 0 and c["p50_s"] > 0 for c in j["workers_curve"])
     assert j["gpu_slots"] >= 1 and j["slot_budget_cpus"] >= 1
     # CPU counted over the timed window only: worker + peer CPU fits in elapsed x the
     # rank's CPUs (BENCH_r04 claimed 19.9 CPU-s per second on a 16-CPU slice)
-    assert 0 < j["cpu_utilisation"] <= 1.05 and 0 < j["crc_relay_cpu_utilisation"] <= 1.05
+    assert 0 < j["cpu_utilisation"] <= 1.05 and 0 < j["unchecked_cpu_utilisation"] <= 1.05
+    assert j["worker_cpu_s_per_GB"] > 0 and j["peer_cpu_s_per_GB"] > 0
     # the same-call torrent A/B (config 4's shape in miniature; no GPU here: both backends
     # hash on the host, so the device counters stay 0 - on a GPU box gpu_parts > 0)
     assert j["torrent_files"] == 50 and j["torrent_gpu_MBps"] > 0 and j["torrent_host_MBps"] > 0
@@ -154,8 +166,8 @@ def test_bench_torrent_ab_failure_never_costs_the_headline(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1",
                         "--warmup", "0", "--size-mb", "2", "--no-compare-single-put",
-                        "--no-compare-crc", "--torrent-gb", "0.2", "--torrent-timeout",
-                        "0.001"], env=env, capture_output=True, text=True, timeout=300)
+                        "--no-compare-crc", "--no-compare-reference", "--workers-curve", "",
+                        "--torrent-gb", "0.2", "--torrent-timeout", "0.001"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["value"] > 0 and "TimeoutError" in j["torrent_error"]
@@ -170,7 +182,8 @@ def test_bench_four_ranks_disjoint_cpus_and_own_peers(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
            "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
            "--gpus", "4", "--steps", "2", "--warmup", "1", "--size-mb", "2", "--jobs-per-step", "2",
-           "--no-compare-single-put", "--torrent-gb", "0"]
+           "--no-compare-single-put", "--torrent-gb", "0", "--no-compare-reference",
+           "--workers-curve", ""]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
@@ -198,14 +211,16 @@ def test_bench_eight_ranks_as_the_driver_launches_them(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(REPO, "bench.py"),
            "--gpus", "8", "--steps", "2", "--warmup", "1", "--size-mb", "2", "--jobs-per-step", "2",
-           "--no-compare-single-put", "--no-compare-crc", "--torrent-gb", "0"]
+           "--no-compare-unchecked", "--no-compare-reference", "--workers-curve", "",
+           "--torrent-gb", "0"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 1, r.stdout                        # rank 0 prints the one line
     j = json.loads(lines[0])
     assert j["n_gpus"] == 8 and j["config"]["jobs_timed"] == 8 * 2 * 2
-    assert j["gpu_slots"] == 8 and j["integrity"] == "none"
+    assert j["gpu_slots"] == 8 and j["integrity"] == "crc32c" and j["bad_digests"] == 0
+    assert j["crc_parts"] == j["media_parts"] == 8 * 2 * 2
     cpus = [set(c) for c in j["rank_cpus"]]
     assert len(cpus) == 8
     if len(os.sched_getaffinity(0)) >= 8:
@@ -231,7 +246,8 @@ def test_bench_rank_with_two_worker_processes(tmp_path):
     env = dict(os.environ, PYTHONPATH=REPO, LOG_LEVEL="error")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
                         "--warmup", "1", "--jobs-per-step", "3", "--size-mb", "4",
-                        "--procs-per-rank", "2", "--torrent-gb", "0"],
+                        "--procs-per-rank", "2", "--torrent-gb", "0", "--compare-single-put",
+                        "--no-compare-reference", "--workers-curve", ""],
                        env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -255,7 +271,8 @@ def test_bench_multipart_objects_checked_against_the_origin(tmp_path, sink):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2",
                         "--warmup", "1", "--jobs-per-step", "2", "--size-mb", "12",
                         "--part-mb", "5", "--threshold-mb", "5", "--sink", sink,
-                        "--no-compare-single-put", "--torrent-gb", "0"],
+                        "--no-compare-single-put", "--torrent-gb", "0",
+                        "--no-compare-reference", "--workers-curve", ""],
                        env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
