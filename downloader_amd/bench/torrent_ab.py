@@ -17,7 +17,7 @@ import shutil
 import statistics
 import tempfile
 import time
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 from .infra import Blobd
 from .synth_torrent import config4_files, make_synth_torrent, served_paths
@@ -46,8 +46,9 @@ async def _stage(w, msg) -> tuple:
 
 async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len: int = 4 << 20,
                      pairs: int = 3, stage_root: str = "", tag: str = "ab",
-                     backends=("auto", "cpu")) -> Dict:
-    """Stage the torrent ``pairs`` times per backend, alternating; medians of the timed jobs."""
+                     backends=("auto", "cpu"), download: Optional[Dict] = None) -> Dict:
+    """Stage the torrent ``pairs`` times per backend, alternating; medians of the timed jobs.
+    ``download``: extra ``download.*`` settings of both workers (A/B knobs)."""
     from ..broker.memory import MemoryBroker
     from ..models import api
     from ..ops import hashing
@@ -74,7 +75,8 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
                     "s3": {"endpoint": b.endpoint}, "broker": {"backend": "memory"},
                     "health": {"enabled": False},
                     "download": {"torrent_enable_dht": False, "progress_interval_s": 5.0,
-                                 "stream_verify_backend": be, "gpu_prewarm": be != "cpu"}},
+                                 "stream_verify_backend": be, "gpu_prewarm": be != "cpu",
+                                 **(download or {})}},
                     env={})
                 w = Worker(cfg, broker=MemoryBroker())
                 await w.start(health=False)
@@ -97,7 +99,9 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
                     if k:
                         t = r.stats.get("torrent", {})
                         runs[be].append({"s": dt, "worker_cpu_s": c1 - c0, "peer_cpu_s": p1 - p0,
-                                         "hash_fails": t.get("hash_fails", 0)})
+                                         "hash_fails": t.get("hash_fails", 0),
+                                         "parts": t.get("parts", 0),
+                                         "gpu_parts": t.get("gpu_parts", 0)})
             dev1 = hashing.gpu_relay_stats() if any(be != "cpu" for be in backends) else {}
             st = b.stats()
     finally:
@@ -119,6 +123,10 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
         out[f"torrent_{key}_worker_cpu_s_per_GB"] = round(
             statistics.median(x["worker_cpu_s"] for x in xs) / (total / 1e9), 4)
         out[f"torrent_{key}_hash_fails"] = sum(x["hash_fails"] for x in xs)
+        if be != "cpu":      # parts whose pieces the device hashed / all parts, timed jobs
+            parts = sum(x["parts"] for x in xs)
+            out["gpu_part_share"] = round(sum(x["gpu_parts"] for x in xs) / parts, 3) \
+                if parts else 0.0
     if dev0 is not None:
         d = {k: dev1.get(k, 0) - dev0.get(k, 0) for k in
              ("submitted", "host_fallbacks", "refused", "device_launches", "device_lanes")}
@@ -128,4 +136,30 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
         out["gpu_launches"] = d["device_launches"]
         out["gpu_lanes_per_launch"] = round(d["device_lanes"] / d["device_launches"], 1) \
             if d["device_launches"] else 0.0
+        out["gpu_multi_slot_launches"] = dev1.get("device_multi_slot_launches", 0) - \
+            dev0.get("device_multi_slot_launches", 0)
+        out["gpu_max_launch_lanes"] = dev1.get("device_max_batch_lanes", 0)
     return out
+
+
+def main() -> None:
+    """``python -m downloader_amd.bench.torrent_ab --gb 20 --set stream_gpu_tail=32``: the A/B
+    alone, one JSON line (A/B of download.* knobs on the box)."""
+    import argparse
+    import json
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gb", type=float, default=20.0)
+    ap.add_argument("--pairs", type=int, default=3)
+    ap.add_argument("--set", action="append", default=[], help="download.KEY=VALUE (both arms)")
+    a = ap.parse_args()
+    over: Dict = {}
+    for kv in a.set:
+        k, _, v = kv.partition("=")
+        over[k] = json.loads(v) if v[:1] in "0123456789-[{tf\"" else v
+    out = asyncio.run(torrent_ab(total_bytes=int(a.gb * 1e9), pairs=a.pairs, download=over))
+    out["download"] = over
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -300,17 +300,18 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
   }
 }
 
-// Batch of relayed parts (PartHasher): lane i hashes lane_len[i] bytes at data + lane_off[i]
-// (pieces of many parts packed back to back in one device slot) into out + 20 * i.
+// Batch of relayed parts (PartHasher): lane i hashes lane_len[i] bytes at lane_ptr[i] - an
+// absolute device address, so one launch spans the pieces of several HBM slots (every slot
+// that closed while the compute streams were busy) - into out + 20 * i.
 template <int ALIGN>
-__global__ __launch_bounds__(256) void sha1_lanes(const uint8_t* __restrict__ data,
-                                                  const int64_t* __restrict__ lane_off,
+__global__ __launch_bounds__(256) void sha1_lanes(const uint64_t* __restrict__ lane_ptr,
                                                   const int64_t* __restrict__ lane_len, int n,
                                                   uint8_t* __restrict__ out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t hv[5];
-  sha1_piece<ALIGN, true, ALIGN == 16>(data + lane_off[i], lane_len[i], hv);
+  sha1_piece<ALIGN, true, ALIGN == 16>(reinterpret_cast<const uint8_t*>(lane_ptr[i]), lane_len[i],
+                                        hv);
   store_digest(out + (int64_t)i * 20, hv);
 }
 
@@ -906,25 +907,44 @@ class HipPartDevice {
     Slot& sl = slots_[(size_t)s];
     for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipEventRecord(sl.copied[k], copies_[k]));
   }
-  void launch(int s, int stream, int lanes, bool align16) {
-    Slot& sl = slots_[(size_t)s];
+  int64_t launch_lanes() const { return launch_lanes_; }
+  // One sha1_lanes kernel over the lanes of `nslots` slots, in order: the lane table of the
+  // launch (absolute device address + length per lane) is built in the stream's pinned table
+  // (free: the stream's previous launch, its H2D included, finished before this one is made),
+  // copied behind the slots' copy markers, and the digests come back with one D2H.
+  void launch(int stream, const int* slots, const int* lanes, int nslots, int total,
+              bool align16) {
+    if (total <= 0 || total > launch_lanes_) throw std::runtime_error("PartHasher: bad launch");
+    Run& r = runs_[(size_t)stream];
     hipStream_t st = streams_[(size_t)stream];
-    for (size_t k = 0; k < copies_.size(); ++k) HIP_CHECK(hipStreamWaitEvent(st, sl.copied[k], 0));
-    HIP_CHECK(hipMemcpyAsync(sl.d_lane, sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
+    uint64_t* hp = r.h_tab;
+    int64_t* hl = reinterpret_cast<int64_t*>(r.h_tab + total);
+    int i = 0;
+    for (int k = 0; k < nslots; ++k) {
+      Slot& sl = slots_[(size_t)slots[k]];
+      for (size_t c = 0; c < copies_.size(); ++c) HIP_CHECK(hipStreamWaitEvent(st, sl.copied[c], 0));
+      const uint64_t base = (uint64_t)(uintptr_t)sl.d_data;
+      for (int l = 0; l < lanes[k]; ++l, ++i) {
+        hp[i] = base + (uint64_t)sl.h_lane[l];
+        hl[i] = sl.h_lane[max_lanes_ + l];
+      }
+    }
+    if (i != total) throw std::runtime_error("PartHasher: lane count mismatch");
+    HIP_CHECK(hipMemcpyAsync(r.d_tab, r.h_tab, (size_t)total * 2 * sizeof(uint64_t),
                              hipMemcpyHostToDevice, st));
-    const int block = 64, grid = (lanes + block - 1) / block;
+    const uint64_t* dp = r.d_tab;
+    const int64_t* dl = reinterpret_cast<const int64_t*>(r.d_tab + total);
+    const int block = 64, grid = (total + block - 1) / block;
     if (align16)
-      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, sl.d_data, sl.d_lane,
-                         sl.d_lane + max_lanes_, lanes, sl.d_dig);
+      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, dp, dl, total, r.d_dig);
     else
-      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st, sl.d_data, sl.d_lane,
-                         sl.d_lane + max_lanes_, lanes, sl.d_dig);
+      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st, dp, dl, total, r.d_dig);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMemcpyAsync(sl.h_dig, sl.d_dig, (size_t)lanes * 20, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipEventRecord(sl.done, st));
+    HIP_CHECK(hipMemcpyAsync(r.h_dig, r.d_dig, (size_t)total * 20, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(r.done, st));
   }
-  bool finished(int s) { return query(slots_[(size_t)s].done); }
-  const uint8_t* digests(int s) { return slots_[(size_t)s].h_dig; }
+  bool finished(int stream) { return query(runs_[(size_t)stream].done); }
+  const uint8_t* digests(int stream) { return runs_[(size_t)stream].h_dig; }
   void drain_copies() noexcept {
     for (auto c : copies_) hipStreamSynchronize(c);
   }
@@ -940,11 +960,14 @@ class HipPartDevice {
  private:
   struct Slot {
     uint8_t* d_data = nullptr;
-    int64_t* d_lane = nullptr;
-    uint8_t* d_dig = nullptr;
-    int64_t* h_lane = nullptr;   // [off x max_lanes][len x max_lanes]
-    uint8_t* h_dig = nullptr;
+    int64_t* h_lane = nullptr;   // [off x max_lanes][len x max_lanes], offsets in the slot
     hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};   // one per copy stream
+  };
+  struct Run {                   // a compute stream's launch: lane table and digests
+    uint64_t* h_tab = nullptr;   // pinned [ptr x total][len x total]
+    uint64_t* d_tab = nullptr;
+    uint8_t* d_dig = nullptr;
+    uint8_t* h_dig = nullptr;
     hipEvent_t done = nullptr;
   };
 
@@ -972,13 +995,20 @@ class HipPartDevice {
     slots_.resize((size_t)slots);
     for (auto& sl : slots_) {
       HIP_CHECK(hipMalloc((void**)&sl.d_data, (size_t)slot_bytes_));
-      HIP_CHECK(hipMalloc((void**)&sl.d_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t)));
-      HIP_CHECK(hipMalloc((void**)&sl.d_dig, (size_t)max_lanes_ * 20));
       HIP_CHECK(hipHostMalloc((void**)&sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
                               hipHostMallocDefault));
-      HIP_CHECK(hipHostMalloc((void**)&sl.h_dig, (size_t)max_lanes_ * 20, hipHostMallocDefault));
       for (auto& e : sl.copied) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+    // a launch may carry every slot's lanes
+    launch_lanes_ = (int64_t)max_lanes_ * (int64_t)slots;
+    runs_.resize((size_t)compute);
+    for (auto& r : runs_) {
+      HIP_CHECK(hipHostMalloc((void**)&r.h_tab, (size_t)launch_lanes_ * 2 * sizeof(uint64_t),
+                              hipHostMallocDefault));
+      HIP_CHECK(hipMalloc((void**)&r.d_tab, (size_t)launch_lanes_ * 2 * sizeof(uint64_t)));
+      HIP_CHECK(hipMalloc((void**)&r.d_dig, (size_t)launch_lanes_ * 20));
+      HIP_CHECK(hipHostMalloc((void**)&r.h_dig, (size_t)launch_lanes_ * 20, hipHostMallocDefault));
+      HIP_CHECK(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
     }
   }
 
@@ -996,18 +1026,22 @@ class HipPartDevice {
       if (c) hipStreamDestroy(c);
     for (auto& sl : slots_) {
       if (sl.d_data) hipFree(sl.d_data);
-      if (sl.d_lane) hipFree(sl.d_lane);
-      if (sl.d_dig) hipFree(sl.d_dig);
       if (sl.h_lane) hipHostFree(sl.h_lane);
-      if (sl.h_dig) hipHostFree(sl.h_dig);
       for (auto e : sl.copied)
         if (e) hipEventDestroy(e);
-      if (sl.done) hipEventDestroy(sl.done);
+    }
+    for (auto& r : runs_) {
+      if (r.h_tab) hipHostFree(r.h_tab);
+      if (r.d_tab) hipFree(r.d_tab);
+      if (r.d_dig) hipFree(r.d_dig);
+      if (r.h_dig) hipHostFree(r.h_dig);
+      if (r.done) hipEventDestroy(r.done);
     }
     for (hipEvent_t e : free_events_) hipEventDestroy(e);
     copies_.clear();
     streams_.clear();
     slots_.clear();
+    runs_.clear();
     free_events_.clear();
   }
 
@@ -1025,9 +1059,11 @@ class HipPartDevice {
   int device_;
   int64_t slot_bytes_;
   int max_lanes_;
+  int64_t launch_lanes_ = 0;
   std::vector<hipStream_t> copies_;
   std::vector<hipStream_t> streams_;
   std::vector<Slot> slots_;
+  std::vector<Run> runs_;
   std::vector<hipEvent_t> free_events_;   // dispatcher thread only
 };
 
@@ -1040,6 +1076,8 @@ py::dict part_stats(PartHasher& h) {
   d["launches"] = s.launches;
   d["lanes"] = s.lanes;
   d["max_batch_lanes"] = s.max_batch_lanes;
+  d["multi_slot_launches"] = s.multi_slot_launches;   // launches spanning >= 2 HBM slots
+  d["max_launch_slots"] = s.max_launch_slots;
   d["broken"] = s.broken;
   d["pending"] = s.pending;
   d["registered"] = s.registered;       // part buffers page-locked (hipHostRegister)

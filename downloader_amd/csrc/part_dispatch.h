@@ -12,8 +12,11 @@
 // dispatcher thread DMAs it into the open device slot at once on a copy stream, and the relay's
 // lease on the buffer ends when that copy completes (COPIED) - not when the hash does; a slot
 // (up to slot_bytes / max_lanes pieces of any number of parts) is launched as ONE kernel as
-// soon as a compute stream is idle, while all are busy the open slot keeps filling, so batches
-// grow with the arrival rate; digests come back per slot (DONE). notify is called without mu_,
+// soon as a compute stream is idle - together with every other slot closed meanwhile, so one
+// launch spans all the slots that filled while the streams were busy and a launch is no longer
+// capped at one slot's lanes (1 GiB = 256 pieces of 4 MiB: ~15 GB/s per stream);
+// while all streams are busy the open slot keeps filling, so batches grow with the arrival
+// rate; digests come back per launch and are handed out per slot (DONE). notify is called without mu_,
 // on the dispatcher thread, for every phase a job reaches - including, when the device fails,
 // the phases the loop had already reached but not yet told (a waiter must never be left
 // without news: its buffer, budget and permit would leak).
@@ -26,9 +29,11 @@
 //   bool copied(Event e);                          // that DMA completed; throws on device error
 //   void recycle(Event e);
 //   void close_copies(int slot);                   // end of the slot's copies on every stream
-//   void launch(int slot, int stream, int lanes, bool align16);   // after the slot's copies
-//   bool finished(int slot);                       // its launch completed; throws on error
-//   const uint8_t* digests(int slot);              // 20 B per lane once finished
+//   int64_t launch_lanes() const;                  // lanes one launch may carry
+//   void launch(int stream, const int* slots, const int* lanes, int nslots, int total,
+//               bool align16);                     // after the slots' copies; lanes in order
+//   bool finished(int stream);                     // its launch completed; throws on error
+//   const uint8_t* digests(int stream);            // 20 B per lane of the launch, in order
 //   void drain_copies() noexcept;                  // failure path: queued DMAs still read
 //   int reg(void* p, size_t n); void unreg(void* p);
 #pragma once
@@ -54,6 +59,7 @@ namespace stager {
 
 struct PartDispatchStats {
   uint64_t submitted = 0, launches = 0, lanes = 0, max_batch_lanes = 0;
+  uint64_t multi_slot_launches = 0, max_launch_slots = 0;
   uint64_t registered = 0, unregistered = 0;
   double register_s = 0;
   bool broken = false;
@@ -68,7 +74,7 @@ class PartDispatcher {
   PartDispatcher(int64_t slot_bytes, int max_lanes, A&&... dev_args)
       : dev_(std::forward<A>(dev_args)...), slot_bytes_(slot_bytes), max_lanes_(max_lanes) {
     slots_.resize((size_t)dev_.slots());
-    streams_.assign((size_t)dev_.compute_streams(), -1);
+    running_.resize((size_t)dev_.compute_streams());
     api_.abi = GPU_PART_API_ABI;
     api_.ctx = this;
     api_.reg = [](void* c, void* p, size_t n) { return ((PartDispatcher*)c)->reg(p, n); };
@@ -315,59 +321,82 @@ class PartDispatcher {
           progressed = true;
         }
         tell(owed_copied, GPU_PART_COPIED);
-        // 3. finished kernels: publish digests, free slot and stream
-        for (size_t s = 0; s < streams_.size(); ++s) {
-          const int si = streams_[s];
-          if (si < 0) continue;
-          if (!dev_.finished(si)) continue;
-          Slot& sl = slots_[(size_t)si];
-          const uint8_t* dig = dev_.digests(si);
+        // 3. finished kernels: publish digests, free the launch's slots and its stream
+        for (size_t s = 0; s < running_.size(); ++s) {
+          std::vector<int>& group = running_[s];
+          if (group.empty()) continue;
+          if (!dev_.finished((int)s)) continue;
+          const uint8_t* dig = dev_.digests((int)s);
           std::vector<Event> late;
           {
             std::lock_guard<std::mutex> g(mu_);
-            for (uint64_t t : sl.jobs) {
-              Job& j = jobs_.at(t);
-              j.digests.assign((const char*)dig + (size_t)j.lane0 * 20, (size_t)j.np * 20);
-              j.done = true;
-              if (!j.copied) {
-                // its copy ended after step 2 looked (the kernel waited for it): a DONE
-                // implies COPIED, and a job the relay may now erase must leave `copying`
-                j.copied = true;
-                late.push_back(j.copy_ev);
-                j.copy_ev = Event{};
-                auto c = std::find(copying.begin(), copying.end(), t);
-                if (c != copying.end()) copying.erase(c);
-                owed_copied.push_back(t);
+            size_t base = 0;                  // first lane of each slot inside the launch
+            for (int si : group) {
+              Slot& sl = slots_[(size_t)si];
+              for (uint64_t t : sl.jobs) {
+                Job& j = jobs_.at(t);
+                j.digests.assign((const char*)dig + (base + (size_t)j.lane0) * 20, (size_t)j.np * 20);
+                j.done = true;
+                if (!j.copied) {
+                  // its copy ended after step 2 looked (the kernel waited for it): a DONE
+                  // implies COPIED, and a job the relay may now erase must leave `copying`
+                  j.copied = true;
+                  late.push_back(j.copy_ev);
+                  j.copy_ev = Event{};
+                  auto c = std::find(copying.begin(), copying.end(), t);
+                  if (c != copying.end()) copying.erase(c);
+                  owed_copied.push_back(t);
+                }
+                owed_done.push_back(t);
               }
-              owed_done.push_back(t);
+              base += (size_t)sl.lanes;
             }
           }
           for (Event e : late) dev_.recycle(e);
           wcv_.notify_all();
-          sl.state = 0;
-          sl.jobs.clear();
-          streams_[s] = -1;
+          for (int si : group) {
+            slots_[(size_t)si].state = 0;
+            slots_[(size_t)si].jobs.clear();
+          }
+          group.clear();
           progressed = true;
         }
         tell(owed_copied, GPU_PART_COPIED);
-        // 4. launch: closed slots first (oldest first), then the open one, on idle streams
-        for (size_t s = 0; s < streams_.size(); ++s) {
-          if (streams_[s] >= 0) continue;
-          int pick = oldest(2);
-          if (pick < 0 && filling >= 0 && slots_[(size_t)filling].lanes > 0) {
-            pick = filling;
-            dev_.close_copies(pick);
+        // 4. launch on each idle stream: every closed slot (oldest first), then the open one,
+        // as ONE kernel - up to the device's lanes per launch
+        for (size_t s = 0; s < running_.size(); ++s) {
+          if (!running_[s].empty()) continue;
+          std::vector<int> group, lanes;
+          int total = 0;
+          bool a16 = true;
+          for (int pick : closed_by_age()) {
+            const Slot& sl = slots_[(size_t)pick];
+            if (total + sl.lanes > dev_.launch_lanes()) break;
+            group.push_back(pick);
+            lanes.push_back(sl.lanes);
+            total += sl.lanes;
+            a16 = a16 && sl.align16;
+          }
+          if (filling >= 0 && slots_[(size_t)filling].lanes > 0 &&
+              total + slots_[(size_t)filling].lanes <= dev_.launch_lanes()) {
+            Slot& f = slots_[(size_t)filling];
+            dev_.close_copies(filling);
+            group.push_back(filling);
+            lanes.push_back(f.lanes);
+            total += f.lanes;
+            a16 = a16 && f.align16;
             filling = -1;
           }
-          if (pick < 0) break;
-          Slot& sl = slots_[(size_t)pick];
-          dev_.launch(pick, (int)s, sl.lanes, sl.align16);
-          sl.state = 3;
-          streams_[s] = pick;
+          if (group.empty()) break;
+          dev_.launch((int)s, group.data(), lanes.data(), (int)group.size(), total, a16);
+          for (int si : group) slots_[(size_t)si].state = 3;
+          running_[s] = group;
           std::lock_guard<std::mutex> g(mu_);
           stats_.launches++;
-          stats_.lanes += (uint64_t)sl.lanes;
-          stats_.max_batch_lanes = std::max<uint64_t>(stats_.max_batch_lanes, (uint64_t)sl.lanes);
+          stats_.lanes += (uint64_t)total;
+          stats_.max_batch_lanes = std::max<uint64_t>(stats_.max_batch_lanes, (uint64_t)total);
+          stats_.max_launch_slots = std::max<uint64_t>(stats_.max_launch_slots, group.size());
+          if (group.size() > 1) stats_.multi_slot_launches++;
           progressed = true;
         }
         tell(owed_done, GPU_PART_DONE);
@@ -411,8 +440,8 @@ class PartDispatcher {
   }
 
   bool any_running() const {
-    for (int s : streams_)
-      if (s >= 0) return true;
+    for (auto& g : running_)
+      if (!g.empty()) return true;
     return false;
   }
   bool any_closed() const {
@@ -425,20 +454,20 @@ class PartDispatcher {
       if (slots_[i].state == 0) return (int)i;
     return -1;
   }
-  int oldest(int state) const {
-    int best = -1;
+  std::vector<int> closed_by_age() const {
+    std::vector<int> out;
     for (size_t i = 0; i < slots_.size(); ++i)
-      if (slots_[i].state == state &&
-          (best < 0 || slots_[i].opened < slots_[(size_t)best].opened))
-        best = (int)i;
-    return best;
+      if (slots_[i].state == 2) out.push_back((int)i);
+    std::sort(out.begin(), out.end(),
+              [&](int a, int b) { return slots_[(size_t)a].opened < slots_[(size_t)b].opened; });
+    return out;
   }
 
   Dev dev_;                        // first member: destroyed last, after the thread joined
   int64_t slot_bytes_;
   int max_lanes_;
   size_t next_copy_ = 0;
-  std::vector<int> streams_;       // slot running on each compute stream (-1: idle)
+  std::vector<std::vector<int>> running_;   // slots of the launch on each compute stream
   std::vector<Slot> slots_;
   std::mutex mu_;
   std::condition_variable cv_, wcv_;

@@ -3,7 +3,8 @@
 //
 // Copy streams and compute streams are host threads with FIFO task queues, like HIP streams:
 // a "DMA" is a memcpy into the slot's host memory after a random delay, a "kernel" waits for
-// the slot's copy markers (close_copies), sleeps a random time and SHA-1s every lane. Events are
+// the copy markers (close_copies) of every slot of its launch, sleeps a random time and SHA-1s
+// every lane, slot after slot. Events are
 // shared atomic flags. On top of the device's own timing:
 //   * `lag`: probability that a completed copy still reads as not ready - the dispatcher then
 //     sees the slot's kernel finish before that copy, the order commit 363d26c had to handle;
@@ -49,10 +50,10 @@ class FakePartDevice {
     for (auto& s : slots_) {
       s.mem.assign((size_t)slot_bytes, 0);
       s.lanes.assign((size_t)max_lanes * 2, 0);
-      s.dig.assign((size_t)max_lanes * 20, 0);
       s.markers.resize((size_t)copy_streams);
-      s.done = std::make_shared<std::atomic<int>>(0);
     }
+    runs_.resize((size_t)compute_streams);
+    for (auto& r : runs_) r.done = std::make_shared<std::atomic<int>>(0);
     for (int i = 0; i < copy_streams; ++i) copies_.emplace_back(new Queue(k.seed * 7 + i));
     for (int i = 0; i < compute_streams; ++i) computes_.emplace_back(new Queue(k.seed * 13 + i));
   }
@@ -95,31 +96,45 @@ class FakePartDevice {
       copies_[k]->push([m] { m->store(1, std::memory_order_release); });
     }
   }
-  void launch(int s, int stream, int lanes, bool /*align16*/) {
+  int64_t launch_lanes() const { return (int64_t)max_lanes_ * (int64_t)slots_.size(); }
+  // One kernel over the lanes of several slots, in order (PartDispatcher's multi-slot launch).
+  void launch(int stream, const int* slots, const int* lanes, int nslots, int total,
+              bool /*align16*/) {
     if (k_.fail_launch_at && ++launches_ == k_.fail_launch_at)
       throw std::runtime_error("injected device fault (launch)");
-    Slot* sl = &slots_[(size_t)s];
-    sl->done->store(0, std::memory_order_relaxed);
-    std::vector<Event> markers = sl->markers;
+    Run* run = &runs_[(size_t)stream];
+    run->done->store(0, std::memory_order_relaxed);
+    std::vector<std::pair<Slot*, int>> group;
+    std::vector<Event> markers;
+    for (int k = 0; k < nslots; ++k) {
+      Slot* sl = &slots_[(size_t)slots[k]];
+      group.push_back({sl, lanes[k]});
+      markers.insert(markers.end(), sl->markers.begin(), sl->markers.end());
+    }
     const int us = k_.kernel_us_max, ml = max_lanes_;
     Queue* q = computes_[(size_t)stream].get();
-    q->push([sl, markers, lanes, us, ml, q] {
+    run->dig.assign((size_t)total * 20, 0);
+    q->push([run, group, markers, us, ml, q] {
       for (auto& m : markers)
         while (m && !m->load(std::memory_order_acquire)) std::this_thread::yield();
       q->nap(us);
-      for (int i = 0; i < lanes; ++i) {
-        const int64_t off = sl->lanes[(size_t)i], len = sl->lanes[(size_t)(ml + i)];
-        const std::string d = digest("sha1", sl->mem.data() + off, (size_t)len);
-        memcpy(sl->dig.data() + (size_t)i * 20, d.data(), 20);
+      size_t i = 0;
+      for (auto& g : group) {
+        Slot* sl = g.first;
+        for (int k = 0; k < g.second; ++k, ++i) {
+          const int64_t off = sl->lanes[(size_t)k], len = sl->lanes[(size_t)(ml + k)];
+          const std::string d = digest("sha1", sl->mem.data() + off, (size_t)len);
+          memcpy(run->dig.data() + i * 20, d.data(), 20);
+        }
       }
-      sl->done->store(1, std::memory_order_release);
+      run->done->store(1, std::memory_order_release);
     });
   }
-  bool finished(int s) {
+  bool finished(int stream) {
     tick();
-    return slots_[(size_t)s].done->load(std::memory_order_acquire) != 0;
+    return runs_[(size_t)stream].done->load(std::memory_order_acquire) != 0;
   }
-  const uint8_t* digests(int s) { return slots_[(size_t)s].dig.data(); }
+  const uint8_t* digests(int stream) { return runs_[(size_t)stream].dig.data(); }
   void drain_copies() noexcept {
     for (auto& q : copies_) q->drain();
   }
@@ -175,9 +190,12 @@ class FakePartDevice {
     }
   };
   struct Slot {
-    std::vector<uint8_t> mem, dig;
+    std::vector<uint8_t> mem;
     std::vector<int64_t> lanes;
     std::vector<Event> markers;
+  };
+  struct Run {                   // a compute stream's current launch
+    std::vector<uint8_t> dig;
     Event done;
   };
 
@@ -194,6 +212,7 @@ class FakePartDevice {
   std::mt19937 rng_;
   int launches_ = 0, queries_ = 0;
   std::vector<Slot> slots_;
+  std::vector<Run> runs_;
   std::vector<std::unique_ptr<Queue>> copies_, computes_;
 };
 

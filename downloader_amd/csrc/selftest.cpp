@@ -770,7 +770,55 @@ static void wire_owned_section() {
           done, requests.load(), needs, (unsigned long long)st.blocks_ignored);
 }
 
+// Multi-slot launches: with kernels slower than the parts arrive, slots
+// close while both compute streams are busy, and the next launch must take every closed slot
+// at once - lanes of several slots in one kernel, digests handed back to the right parts.
+static void multislot_section() {
+  Watchdog wd("multi-slot launches", 60);
+  FakeDeviceKnobs k;
+  k.kernel_us_max = 30000;                // 0 - 30 ms per launch: slots pile up behind them
+  k.copy_us_max = 100;
+  k.lag = 0.3;
+  k.seed = 7;
+  auto h = fake_hasher(k);                // 4 slots of 4 MiB / 256 lanes, 2 compute streams
+  const GpuPartHashApi* api = h->api();
+  const int64_t piece = 16 << 10;
+  const int parts = 160, pieces = 8;      // 8 pieces a part: 32 parts fill a slot
+  auto data = rnd((size_t)parts * pieces * piece, 91);
+  std::vector<uint64_t> tickets;
+  for (int i = 0; i < parts; ++i) {
+    const uint8_t* p = data.data() + (size_t)i * pieces * piece;
+    uint64_t t = 0;
+    while (!(t = api->submit(api->ctx, p, pieces * piece, piece)))
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    tickets.push_back(t);
+  }
+  bool ok = true;
+  for (int i = 0; i < parts; ++i) {
+    uint8_t dig[pieces * 20];
+    char err[256] = {0};
+    if (api->wait(api->ctx, tickets[(size_t)i], GPU_PART_DONE, dig, sizeof dig, err, sizeof err) != 0) {
+      fprintf(stderr, "multi-slot: part %d failed: %s\n", i, err);
+      ok = false;
+      continue;
+    }
+    for (int q = 0; q < pieces; ++q) {
+      const uint8_t* pc = data.data() + ((size_t)i * pieces + q) * piece;
+      if (digest("sha1", pc, (size_t)piece) != std::string((const char*)dig + q * 20, 20)) ok = false;
+    }
+  }
+  const PartDispatchStats st = h->stats();
+  fprintf(stderr, "multi-slot: %llu launches, %llu spanning >= 2 slots, up to %llu slots / %llu lanes\n",
+          (unsigned long long)st.launches, (unsigned long long)st.multi_slot_launches,
+          (unsigned long long)st.max_launch_slots, (unsigned long long)st.max_batch_lanes);
+  CHECK(ok);
+  CHECK(st.multi_slot_launches > 0 && st.max_launch_slots >= 2);
+  CHECK(st.max_batch_lanes > 256);        // more than one slot's lanes in one kernel
+  CHECK(st.lanes == (uint64_t)parts * pieces && st.pending == 0);
+}
+
 static void stress_sections() {
+  multislot_section();
   // ---- the completion machinery under load: 64 relays x 32 parts (2,048) through
   // PartDispatcher<FakePartDevice>, copies that complete before they are seen, hashers
   // replaced every few ms, the part budget oscillating, a third of the parts forgotten

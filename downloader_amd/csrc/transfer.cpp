@@ -831,8 +831,14 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
     return fin(2, relay_copy(dst, n, moved, prog, crc));
   if (crc) {
     // CRC staging, L2-sized: relaybench peekcrc at 8 threads, 64 / 128 / 256 / 512 / 1024
-    // KiB: 36.3 / 36.7 / 37.5 / 39.4 / 38.1 GB/s (profiles/archive/r4/peekbuf/)
-    thread_local std::vector<uint8_t> cbuf(512 * 1024);
+    // KiB: 36.3 / 36.7 / 37.5 / 39.4 / 38.1 GB/s (profiles/archive/r4/peekbuf/);
+    // STAGER_PEEK_KB: A/B knob
+    static const size_t peek_bytes = [] {
+      const char* e = getenv("STAGER_PEEK_KB");
+      long kb = e ? atol(e) : 0;
+      return (size_t)(kb >= 16 && kb <= 8192 ? kb : 512) * 1024;
+    }();
+    thread_local std::vector<uint8_t> cbuf(peek_bytes);
     int64_t m = relay_dup(
         dst, n, moved, prog,
         [&](size_t& len) {

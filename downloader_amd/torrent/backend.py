@@ -177,6 +177,7 @@ async def _stream_torrent(meta: Metainfo, seeds: List[str], selected: List[str],
                             "verify": st.stats.get("verify", "host"),
                             **({"verify_fallback": st.stats["verify_fallback"]}
                                if "verify_fallback" in st.stats else {}),
+                            "parts": st._n_parts,
                             "gpu_parts": st.stats.get("gpu_parts", 0),
                             "gpu_failures": st.stats.get("gpu_failures", 0),
                             "budget": st.stats.get("budget", {}),

@@ -93,7 +93,8 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--size-mb", "4", "--jobs-per-step", "2",
-           "--torrent-gb", "0.05", "--torrent-pairs", "1", "--ref-jobs", "16", "--curve-steps", "1"]
+           "--torrent-gb", "0.05", "--torrent-pairs", "1", "--ref-jobs", "16",
+           "--curve-steps", "1"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
@@ -167,7 +168,8 @@ def test_bench_torrent_ab_failure_never_costs_the_headline(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1",
                         "--warmup", "0", "--size-mb", "2", "--no-compare-single-put",
                         "--no-compare-crc", "--no-compare-reference", "--workers-curve", "",
-                        "--torrent-gb", "0.2", "--torrent-timeout", "0.001"], env=env, capture_output=True, text=True, timeout=300)
+                        "--torrent-gb", "0.2", "--torrent-timeout", "0.001"],
+                       env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     j = json.loads(r.stdout.strip().splitlines()[-1])
     assert j["value"] > 0 and "TimeoutError" in j["torrent_error"]
