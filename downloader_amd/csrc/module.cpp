@@ -263,7 +263,7 @@ PYBIND11_MODULE(_native, m) {
         "Keep at most n idle part buffers (the rest are unmapped on release)");
   py::class_<SwarmWire>(m, "SwarmWire",
                         "Native peer-wire receive path of one torrent session (peerwire.cpp)")
-      .def(py::init<int>(), py::arg("verify_threads") = 2)
+      .def(py::init<int, int>(), py::arg("verify_threads") = 2, py::arg("io_threads") = 4)
       .def("set_storage",
            [](SwarmWire& w, int64_t piece_length, int64_t total, const py::bytes& hashes,
               const std::vector<std::pair<int, int64_t>>& files) {
@@ -273,6 +273,8 @@ PYBIND11_MODULE(_native, m) {
       .def("begin_piece", &SwarmWire::begin_piece, py::arg("idx"))
       .def("drop_piece", &SwarmWire::drop_piece, py::arg("idx"))
       .def("set_pipeline", &SwarmWire::set_pipeline, py::arg("depth"))
+      .def("set_conn_pipeline", &SwarmWire::set_conn_pipeline, py::arg("conn_id"),
+           py::arg("depth"), "requests in flight on one connection (its bandwidth-delay product)")
       .def("assign", &SwarmWire::assign, py::arg("conn_id"), py::arg("idx"),
            "Own piece idx on the connection: the wire requests its blocks (returns the "
            "connection's blocks still to request)")
@@ -347,6 +349,8 @@ PYBIND11_MODULE(_native, m) {
            py::arg("conn_id"), py::arg("parts"),
            "Queue the concatenation of `parts` (buffers) for sending; the queued bytes after it")
       .def("pending_out", &SwarmWire::pending_out, py::arg("conn_id"))
+      .def("conn_rx", &SwarmWire::conn_rx, py::arg("conn_id"),
+           "bytes the connection received so far (per-peer rates)")
       .def("detach", &SwarmWire::detach, py::arg("conn_id"),
            py::call_guard<py::gil_scoped_release>())
       .def("eventfd", &SwarmWire::eventfd)
@@ -376,6 +380,9 @@ PYBIND11_MODULE(_native, m) {
              d["sha_s"] = s.sha_ns / 1e9;
              d["write_s"] = s.write_ns / 1e9;
              d["served_bytes"] = s.served_bytes;
+             d["io_threads"] = s.io_threads;
+             d["serve_floods"] = s.serve_floods;
+             d["serve_cancels"] = s.serve_cancels;
              d["assigned"] = s.assigned;            // owned pieces (SwarmWire.assign)
              d["requests"] = s.requests;            // REQUESTs the wire sent by itself
              d["gpu_pieces"] = s.gpu_pieces;

@@ -163,7 +163,7 @@ struct RelayPoolStats {
 void set_gpu_part_hasher(const void* api, int min_pieces);
 const void* gpu_part_hasher_current();        // the installed hasher's API (null: none)
 // The swarm wire's idle piece buffers page-locked for this hasher API are unlocked and freed
-// (before the hasher itself is destroyed; peerwire.cpp).
+// (peerwire.cpp); set_gpu_part_hasher calls it for the hasher it replaces.
 void swarm_piece_pool_forget(const void* api);
 // At most this many bytes of idle piece buffers are kept (beyond it they are freed now and on
 // release; download.swarm_pool_mb).
@@ -232,12 +232,16 @@ struct SwarmWireStats {
   uint64_t pool_allocs = 0, pool_frees = 0, pool_locks = 0; // since start: buffers made /
                                                             // unmade, page-locked for a hasher
   size_t active_pieces = 0;
+  size_t io_threads = 0;            // I/O threads (epoll) serving the connections
+  uint64_t serve_floods = 0;        // connections dropped for flooding REQUESTs
+  uint64_t serve_cancels = 0;       // queued blocks a CANCEL removed
 };
 class SwarmWire {
  public:
   // kEvNeed: the connection's native request queue fell below one pipeline (assign more)
   static constexpr int kEvMsg = 1, kEvBlocks = 2, kEvClosed = 3, kEvPiece = 4, kEvNeed = 5;
-  explicit SwarmWire(int verify_threads = 2);
+  // io_threads: epoll threads reading and writing the connections (spread, fewest first)
+  explicit SwarmWire(int verify_threads = 2, int io_threads = 4);
   ~SwarmWire();
   void set_storage(int64_t piece_length, int64_t total, const std::string& hashes,
                    const std::vector<std::pair<int, int64_t>>& files);
@@ -252,6 +256,7 @@ class SwarmWire {
   // pieces back into ordinary ones and return their per-block state: 2 received, 1 requested
   // from the owner and not answered yet, 0 neither.
   void set_pipeline(uint32_t depth);
+  void set_conn_pipeline(uint64_t conn, uint32_t depth);   // per connection (0: the default)
   size_t assign(uint64_t conn, uint32_t idx);
   size_t todo(uint64_t conn);
   std::vector<std::pair<uint32_t, std::string>> release(uint64_t conn);
@@ -280,7 +285,8 @@ class SwarmWire {
   void attach(int fd, uint64_t id, const std::string& prefix);
   size_t send(uint64_t id, std::string data);   // queued bytes after this one (0: closed)
   size_t pending_out(uint64_t id);
-  void detach(uint64_t id);                     // shut down, join, close the fd
+  uint64_t conn_rx(uint64_t id);                // bytes the connection received so far
+  void detach(uint64_t id);                     // shut down, off its I/O thread, close the fd
   int eventfd() const { return efd_; }
   std::vector<WireEvent> poll();
   SwarmWireStats stats();
@@ -290,16 +296,24 @@ class SwarmWire {
  private:
   struct Piece;
   struct Conn;
+  struct OutItem;
+  struct IoLoop;
   uint32_t piece_size(uint32_t idx) const;
   void verify_loop();
   std::string write_piece(const Piece& p);
   void push(uint64_t conn, int kind, std::string data);
-  void read_loop(Conn& c);
-  void write_loop(Conn& c);
+  IoLoop* pick_loop();                          // cmu_ held
+  void io_loop(IoLoop& l);
+  bool commands(IoLoop& l);
+  void kill(IoLoop& l, Conn& c, const std::string& reason);
+  void arm_out(IoLoop& l, Conn& c, bool on);
+  void on_readable(IoLoop& l, Conn& c);
+  void process(IoLoop& l, Conn& c);
+  void flush(IoLoop& l, Conn& c);
+  void kick(Conn& c);
+  int serve_step(Conn& c, OutItem& item);
   bool has(uint32_t idx);
   bool servable(uint32_t idx, uint32_t begin, uint32_t len);
-  bool serve_block(Conn& c, const std::string& req);
-  bool send_all(Conn& c, const char* p, size_t n, int flags);
   void finish_piece(std::shared_ptr<Piece> p, const uint8_t* dig);   // compare, then store
   void store_loop();                                                  // the writer
   void report(uint32_t idx, int status, const std::string& err);
@@ -308,7 +322,6 @@ class SwarmWire {
                 bool* owned, std::string* reqs, bool* need);
   bool pump(Conn& c, std::string* reqs);        // mu_ held
   void queue_out(Conn& c, std::string data);
-  void send_requests(Conn& c, std::string reqs);
   std::shared_ptr<Conn> conn(uint64_t id);
   std::string block_states(const Piece& p, const Conn* owner);   // mu_ held
 
@@ -338,8 +351,13 @@ class SwarmWire {
   uint64_t epoch_ = 0;
   SwarmWireStats stats_;
   std::atomic<uint64_t> rx_bytes_{0}, recvs_{0};
-  std::mutex cmu_;
+  std::mutex cmu_;                              // conns_, loops_
   std::unordered_map<uint64_t, std::shared_ptr<Conn>> conns_;
+  int io_threads_ = 4;
+  std::vector<std::unique_ptr<IoLoop>> loops_;
+  std::mutex lmu_;                              // Conn::removed (detach waits for it)
+  std::condition_variable lcv_;
+  std::atomic<uint64_t> serve_floods_{0}, serve_cancels_{0};
   std::mutex vmu_;
   std::condition_variable vcv_;
   std::deque<std::shared_ptr<Piece>> vq_;

@@ -1593,8 +1593,12 @@ void set_gpu_part_hasher(const void* api, int min_pieces) {
   if (a && a->abi != GPU_PART_API_ABI) throw std::invalid_argument("gpu_part_api ABI mismatch");
   if (a) a->set_notify(a->ctx, &gpu_notify, (void*)a);
   g_gpu_min_pieces.store(std::max(1, min_pieces));
-  g_gpu_api.store(a);
+  const GpuPartHashApi* old = g_gpu_api.exchange(a);
   part_pool().drop_foreign(a);
+  // idle swarm piece buffers page-locked for the hasher being replaced are unlocked and freed
+  // now, not whenever a verifier happens to touch them (retired hashers stay alive,
+  // ops/hashing.py, so `old` is still callable)
+  if (old && old != a) swarm_piece_pool_forget(old);
 }
 
 // ---- CpuPartHasher: the gpu_part_api.h contract served by a host thread ------------------

@@ -30,7 +30,9 @@ from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Union
 from urllib.parse import quote, urljoin, urlsplit
 
 from .proxy import Proxy, ProxyConfig
-from ..utils.log import redact_text, redact_url
+from ..utils.log import get_logger, redact_text, redact_url
+
+log = get_logger("http.py")
 
 Headers = Sequence[Tuple[str, str]]
 
@@ -537,10 +539,14 @@ class NativeTransport(Transport):
                                        gpu)
             try:
                 out = await asyncio.shield(fut)
-            except asyncio.CancelledError:
+            except asyncio.CancelledError as ce:
                 self._abort_slot(slot)
                 await _drain(fut)
-                await self._forget_ticket(fut)
+                held = await self._forget_ticket(fut)
+                if held is not None:
+                    # the device did not give the part's buffer back in time: the caller keeps
+                    # its budget bytes until it does (getattr(e, "held_until", None))
+                    ce.held_until = held
                 raise
             finally:
                 self._end_slot(slot)
@@ -558,19 +564,24 @@ class NativeTransport(Transport):
             src_url = nxt
         raise TransportError(f"relay source: more than {MAX_REDIRECTS} redirects", 310)
 
-    async def _forget_ticket(self, fut: "asyncio.Future") -> None:
+    FORGET_WAIT_S = 5.0
+
+    async def _forget_ticket(self, fut: "asyncio.Future") -> Optional["asyncio.Future"]:
         """A cancelled relay that had queued its part to the GPU hasher: nobody will ask for
         the digests; the native side returns the part's buffer to the pool when its DMA is
         over and drops the result. ``gpu_part_forget`` blocks until the DMA is (milliseconds),
         so it runs on a thread of its own - and this waits for it: the caller gives the part's
         bytes back to its PartBudget when the cancellation reaches it, which must not happen
-        while the buffer is still leased (the budget's bound was briefly exceeded)."""
+        while the buffer is still leased (the budget's bound was briefly exceeded).
+        The wait is bounded (FORGET_WAIT_S, ADVICE r5: a device that stopped answering must not
+        hang the cancellation, nor worker shutdown behind it): past it the future that ends
+        when the forget does is returned, and the caller holds the part's budget until then."""
         if not fut.done() or fut.cancelled() or fut.exception() is not None:
-            return
+            return None
         hashed = fut.result()[3]
         gid = hashed.get("gpu_ticket") if hashed else 0
         if not gid:
-            return
+            return None
         loop = asyncio.get_running_loop()
         over = loop.create_future()
 
@@ -588,9 +599,14 @@ class NativeTransport(Transport):
                     pass
         threading.Thread(target=forget, name="gpu-part-forget", daemon=True).start()
         try:
-            await asyncio.shield(over)
+            await asyncio.wait_for(asyncio.shield(over), self.FORGET_WAIT_S)
+        except asyncio.TimeoutError:
+            log.warn("gpu part forget still blocked: its budget stays held until it returns",
+                        ticket=gid, waited_s=self.FORGET_WAIT_S)
+            return over
         except asyncio.CancelledError:
             pass
+        return None
 
     async def close(self) -> None:
         with self._lock:

@@ -98,6 +98,18 @@ def build_blobd(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
+def build_swarmd(force: bool = False, verbose: bool = True) -> Path:
+    """Heterogeneous fake seeders for the swarm bench / tests (csrc/swarmd.cpp)."""
+    srcs = [CSRC / "swarmd.cpp"]
+    BIN.mkdir(exist_ok=True)
+    out = BIN / "swarmd"
+    if force or _stale(out, srcs):
+        cxx = os.environ.get("CXX", "g++")
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", str(srcs[0]), "-lpthread", "-o", str(out)]
+        _run(cmd, verbose)
+    return out
+
+
 def build_relaybench(force: bool = False, verbose: bool = True) -> Path:
     """Per-byte CPU of the relay modes (csrc/relaybench.cpp): the copy / CRC floor."""
     srcs = [CSRC / "relaybench.cpp"]
@@ -137,6 +149,8 @@ def build_all(force: bool = False, verbose: bool = True, gpu: bool = True) -> No
         build_blobd(force, verbose)
     if (CSRC / "relaybench.cpp").exists():
         build_relaybench(force, verbose)
+    if (CSRC / "swarmd.cpp").exists():
+        build_swarmd(force, verbose)
     if gpu and (CSRC / "gpu_sha1.hip").exists():
         if not (ROCM / "bin" / "hipcc").exists():
             raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")

@@ -16,6 +16,7 @@ assigns to the connection are requested by the wire itself (``SwarmWire.assign``
 from __future__ import annotations
 
 import asyncio
+import itertools
 import os
 import struct
 import time
@@ -61,10 +62,17 @@ async def read_handshake(reader: asyncio.StreamReader, timeout: float = 10.0) ->
     return data[20:28], data[28:48], data[48:68]
 
 
+# Connection ids (the native wire's connection key, session.peers and picker ownership):
+# process-wide and never reused. self.cid was reused by CPython as soon as a PeerConn was
+# freed, so a new connection could receive the events a detached one left behind.
+_CONN_IDS = itertools.count(1)
+
+
 class PeerConn:
     def __init__(self, session: "TorrentSession", reader: asyncio.StreamReader,
                  writer: asyncio.StreamWriter, addr: Tuple[str, int], remote_id: bytes,
                  reserved: bytes, outgoing: bool):
+        self.cid = next(_CONN_IDS)
         self.s = session
         self.reader = reader
         self.writer = writer
@@ -113,7 +121,7 @@ class PeerConn:
             buf.clear()
         fd = os.dup(sock.fileno())
         try:
-            wire.attach(fd, id(self), prefix)
+            wire.attach(fd, self.cid, prefix)
         except Exception:
             os.close(fd)
             transport.resume_reading()
@@ -142,7 +150,7 @@ class PeerConn:
         self._flush_due = False
         if self._out and not self.closed:
             if self.wire is not None:
-                self.wire.sendv(id(self), self._out)     # one copy, into the native queue
+                self.wire.sendv(self.cid, self._out)     # one copy, into the native queue
             else:
                 self.writer.write(b"".join(self._out))
         self._out.clear()
@@ -150,7 +158,7 @@ class PeerConn:
 
     async def _maybe_drain(self) -> None:
         if self.wire is not None:
-            while not self.closed and self.wire.pending_out(id(self)) > 1 << 20:
+            while not self.closed and self.wire.pending_out(self.cid) > 1 << 20:
                 await asyncio.sleep(0.001)
             return
         if self.writer.transport.get_write_buffer_size() > 1 << 20:
@@ -201,11 +209,11 @@ class PeerConn:
         if v != self.am_choking:
             self.am_choking = v
             if self.wire is not None and v:
-                self.wire.set_serving(id(self), False)    # before the CHOKE is queued
+                self.wire.set_serving(self.cid, False)    # before the CHOKE is queued
             await self.send(CHOKE if v else UNCHOKE)
             if self.wire is not None and not v:
                 self._flush()                             # the UNCHOKE goes out first, then
-                self.wire.set_serving(id(self), True)     # REQUESTs are served natively
+                self.wire.set_serving(self.cid, True)     # REQUESTs are served natively
 
     async def request(self, piece: int, begin: int, length: int) -> None:
         self.inflight[(piece, begin)] = time.monotonic()
@@ -237,7 +245,7 @@ class PeerConn:
         self.closed = True
         if self.wire is not None:
             try:
-                self.wire.detach(id(self))        # FIN, threads joined, its fd closed
+                self.wire.detach(self.cid)        # FIN, threads joined, its fd closed
             except Exception:
                 pass
         try:
@@ -256,7 +264,7 @@ class PeerConn:
                 # blocks of a piece the wire requests itself are not reported one by one: ask
                 # the wire when the socket last received
                 try:
-                    idle = min(idle, self.wire.rx_idle(id(self)))
+                    idle = min(idle, self.wire.rx_idle(self.cid))
                 except Exception:
                     pass
             if idle > self.s.idle_timeout:
@@ -358,7 +366,7 @@ class PeerConn:
                 self.bitfield.set(i)
         self._raw_bitfield = None
         self._early_haves.clear()
-        self.s.picker.add_peer(self.bitfield, id(self))
+        self.s.picker.add_peer(self.bitfield, self.cid)
 
     # ---------------------------------------------------------------- receiving
     async def _dispatch(self, mid: int, p: memoryview) -> None:
@@ -383,7 +391,7 @@ class PeerConn:
             if self.bitfield is None:
                 self._early_haves.add(idx)
             elif idx < self.bitfield.n and self.bitfield.set(idx):
-                s.picker.inc(idx, id(self))
+                s.picker.inc(idx, self.cid)
                 await s.update_interest(self)
                 await s.fill(self)
         elif mid == BITFIELD:
@@ -391,10 +399,10 @@ class PeerConn:
                 self._raw_bitfield = bytes(p)
             else:
                 if self.bitfield is not None:
-                    s.picker.remove_peer(self.bitfield, id(self))
+                    s.picker.remove_peer(self.bitfield, self.cid)
                 self.bitfield = Bitfield(s.meta.num_pieces)
                 self.bitfield.load(bytes(p))
-                s.picker.add_peer(self.bitfield, id(self))
+                s.picker.add_peer(self.bitfield, self.cid)
                 await s.update_interest(self)
                 await s.fill(self)
         elif mid == UNCHOKE:

@@ -633,7 +633,7 @@ class TorrentSession:
             return False
         if pc.addr in self.connected_addrs() or pc.remote_id == self.client.peer_id:
             return False
-        self.peers[id(pc)] = pc
+        self.peers[pc.cid] = pc
         self.stats["peers_connected"] += 1
         if self.wire is not None:
             try:
@@ -645,10 +645,10 @@ class TorrentSession:
         return True
 
     def peer_closed(self, pc: PeerConn) -> None:
-        if self.peers.pop(id(pc), None) is None:
+        if self.peers.pop(pc.cid, None) is None:
             return
         if pc.bitfield is not None and self.picker is not None:
-            self.picker.remove_peer(pc.bitfield, id(pc))
+            self.picker.remove_peer(pc.bitfield, pc.cid)
         self.release_inflight(pc)
         self._wake.set()
 
@@ -659,15 +659,15 @@ class TorrentSession:
         released = bool(pc.inflight)
         if self.picker is not None:
             for (piece, begin) in list(pc.inflight):
-                self.picker.release(id(pc), piece, begin)
+                self.picker.release(pc.cid, piece, begin)
             if pc.wire is not None and self._owned_mode:
                 try:
-                    back = self.wire.release(id(pc))
+                    back = self.wire.release(pc.cid)
                 except Exception:
                     back = []
                 for idx, states in back:
                     ap = self.picker.active.get(idx)
-                    if ap is not None and ap.owner == id(pc):
+                    if ap is not None and ap.owner == pc.cid:
                         self._to_block_mode(ap, states, None)
                         self.stats["wire_released"] += 1
                         released = True
@@ -701,7 +701,7 @@ class TorrentSession:
     def _assign(self, pc: PeerConn) -> bool:
         """Keep two pipelines of blocks queued on the connection's native wire, a whole piece
         at a time. False when no piece was left for it (the endgame may begin)."""
-        me, want = id(pc), 2 * self.client.pipeline
+        me, want = pc.cid, 2 * self.client.pipeline
         wire, picker = self.wire, self.picker
         try:
             t = wire.todo(me)
@@ -758,7 +758,7 @@ class TorrentSession:
     async def update_interest(self, pc: PeerConn) -> None:
         if self.picker is None or pc.bitfield is None:
             return
-        await pc.set_interested(self.picker.peer_has_wanted(pc.bitfield, id(pc)))
+        await pc.set_interested(self.picker.peer_has_wanted(pc.bitfield, pc.cid))
 
     async def maybe_unchoke(self, pc: PeerConn) -> None:
         unchoked = sum(1 for p in self.peers.values() if not p.am_choking)
@@ -803,7 +803,7 @@ class TorrentSession:
             return
         inflight_pop = pc.inflight.pop
         active_get = picker.active.get
-        me = id(pc)
+        me = pc.cid
         got_bytes = 0
         last_idx, ap = -1, None
         for idx, begin, ln, st in struct.iter_unpack(">IIII", data):
@@ -839,7 +839,7 @@ class TorrentSession:
     async def cancel_dups(self, pc: PeerConn, dup: Set[int], idx: int, begin: int,
                           ln: int) -> None:
         for other_id in dup:
-            if other_id != id(pc):
+            if other_id != pc.cid:
                 other = self.peers.get(other_id)
                 if other is not None:
                     await other.cancel(idx, begin, ln)
@@ -924,10 +924,10 @@ class TorrentSession:
         ap.buf[begin:begin + len(data)] = data
         ap.state[b] = 2
         ap.got += 1
-        ap.peers.add(id(pc))
+        ap.peers.add(pc.cid)
         self.downloaded += len(data)
         rs = ap.req.pop(b, None)
-        others = rs is not None and (len(rs) > 1 or id(pc) not in rs)   # endgame duplicates
+        others = rs is not None and (len(rs) > 1 or pc.cid not in rs)   # endgame duplicates
         if others or ap.got >= ap.nblocks:
             self._followup[(idx, b)] = (ap, rs if others else None)
             return True
@@ -940,10 +940,10 @@ class TorrentSession:
         b = begin // BLOCK
         ap.state[b] = 2
         ap.got += 1
-        ap.peers.add(id(pc))
+        ap.peers.add(pc.cid)
         self.downloaded += len(data)
         rs = ap.req.pop(b, None)
-        if rs is not None and (len(rs) > 1 or id(pc) not in rs):
+        if rs is not None and (len(rs) > 1 or pc.cid not in rs):
             self._spawn(self.cancel_dups(pc, rs, idx, begin, len(data)))
         if st == 2 and self.picker.complete_blocks(idx):
             self._verifying_ap[idx] = ap
@@ -971,7 +971,7 @@ class TorrentSession:
         # REQUEST messages instead of one syscall per 17-byte message.
         if room < max(1, self.client.pipeline // 4):
             return
-        blocks = self.picker.next_blocks(id(pc), pc.bitfield, room, fresh, dups)
+        blocks = self.picker.next_blocks(pc.cid, pc.bitfield, room, fresh, dups)
         if blocks:
             await pc.request_many(blocks)
 
@@ -986,7 +986,7 @@ class TorrentSession:
         # endgame: cancel the duplicates requested from other peers
         if dup:
             for other_id in dup:
-                if other_id != id(pc):
+                if other_id != pc.cid:
                     other = self.peers.get(other_id)
                     if other is not None:
                         await other.cancel(idx, begin, ln)
@@ -1040,7 +1040,7 @@ class TorrentSession:
             if p.bitfield is None or idx not in p.bitfield:
                 await p.send_have(idx)
             if p.am_interested and p.bitfield is not None and \
-                    not self.picker.peer_has_wanted(p.bitfield, id(p)):
+                    not self.picker.peer_has_wanted(p.bitfield, p.cid):
                 await p.set_interested(False)
         if self.have.complete:
             self._finish()

@@ -392,7 +392,7 @@ class StreamStager:
                 try:
                     res = await self._relay_part(u, gpu)
                 except BaseException as e:
-                    self._budget.release(nb)
+                    self._release_after(e, nb)
                     self._gpu_slots.release()
                     if not await self._unit_failed(u, e, queue):
                         return
@@ -437,6 +437,16 @@ class StreamStager:
             if self.error is not None:
                 return
             self._settle(u, requeue, queue)
+
+    def _release_after(self, e: BaseException, nb: int) -> None:
+        """A failed / cancelled relay's budget bytes: back now, or - when the cancellation
+        could not wait for the GPU hasher to hand the part's buffer back (``held_until``, set
+        by the transport) - once it has."""
+        held = getattr(e, "held_until", None)
+        if held is not None and not held.done():
+            held.add_done_callback(lambda _f, nb=nb: self._budget.release(nb))
+        else:
+            self._budget.release(nb)
 
     async def _forget_part(self, gid: int) -> None:
         """Drop a queued GPU part nobody will collect (blocks until its DMA is over, so on a

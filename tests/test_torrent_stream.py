@@ -864,3 +864,51 @@ def test_part_hasher_layout_comes_from_the_config(monkeypatch):
     assert stream._gpu_relay_on(cfg) is None
     (a, k), = seen
     assert a[1:] == (8, 2 << 30) and k == {"copy_streams": 1, "compute_streams": 3}
+
+
+def test_cancelled_relay_does_not_hang_on_a_stuck_gpu_forget(run):
+    """a cancelled relay waits for gpu_part_forget (its part's buffer must be back
+    before the budget is), but only FORGET_WAIT_S: a device that stopped answering returns the
+    future of the forget instead, and the caller keeps the part's budget bytes until it ends."""
+    import threading
+
+    from downloader_amd.net.http import NativeTransport
+
+    release = threading.Event()
+    calls = []
+
+    class SlowNative:
+        def gpu_part_forget(self, gid):
+            calls.append(gid)
+            release.wait(10)
+
+    t = NativeTransport.__new__(NativeTransport)
+    t._n = SlowNative()
+    t.FORGET_WAIT_S = 0.2
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        fut.set_result((None, None, None, {"gpu_ticket": 42}))
+        t0 = loop.time()
+        held = await t._forget_ticket(fut)
+        assert loop.time() - t0 < 2 and held is not None and not held.done()
+        released = []
+        from downloader_amd.torrent.stream import StreamStager
+
+        class Budget:
+            def release(self, nb):
+                released.append(nb)
+        st = StreamStager.__new__(StreamStager)
+        st._budget = Budget()
+        e = asyncio.CancelledError()
+        e.held_until = held
+        st._release_after(e, 7)
+        assert released == []                      # held while the forget is blocked
+        release.set()
+        await asyncio.wait_for(held, 5)
+        await asyncio.sleep(0)
+        assert released == [7] and calls == [42]
+        st._release_after(RuntimeError("x"), 3)     # no hold: back at once
+        assert released == [7, 3]
+    run(go(), timeout=30)
