@@ -300,18 +300,21 @@ __global__ __launch_bounds__(256) void sha1_pieces(const uint8_t* __restrict__ d
   }
 }
 
-// Batch of relayed parts (PartHasher): lane i hashes lane_len[i] bytes at lane_ptr[i] - an
-// absolute device address, so one launch spans the pieces of several HBM slots (every slot
-// that closed while the compute streams were busy) - into out + 20 * i.
+// Batch of relayed parts (PartHasher): lane i hashes lane_len[i] bytes at data + lane_off[i].
+// `data` is the base of the hasher's HBM arena (every slot is a window of one allocation), so
+// one launch spans the pieces of several slots - every slot that closed while the compute
+// streams were busy - and the loads stay global_load_dwordx4: an absolute address per lane
+// made them flat loads (a generic pointer), and the kernel 26 % slower (97.8 vs 77.7 ms per
+// 4 MiB piece, profiles/r6/parthasher/trace_summary.json).
 template <int ALIGN>
-__global__ __launch_bounds__(256) void sha1_lanes(const uint64_t* __restrict__ lane_ptr,
+__global__ __launch_bounds__(256) void sha1_lanes(const uint8_t* __restrict__ data,
+                                                  const int64_t* __restrict__ lane_off,
                                                   const int64_t* __restrict__ lane_len, int n,
                                                   uint8_t* __restrict__ out) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t hv[5];
-  sha1_piece<ALIGN, true, ALIGN == 16>(reinterpret_cast<const uint8_t*>(lane_ptr[i]), lane_len[i],
-                                        hv);
+  sha1_piece<ALIGN, true, ALIGN == 16>(data + lane_off[i], lane_len[i], hv);
   store_digest(out + (int64_t)i * 20, hv);
 }
 
@@ -909,7 +912,7 @@ class HipPartDevice {
   }
   int64_t launch_lanes() const { return launch_lanes_; }
   // One sha1_lanes kernel over the lanes of `nslots` slots, in order: the lane table of the
-  // launch (absolute device address + length per lane) is built in the stream's pinned table
+  // launch (offset in the arena + length per lane) is built in the stream's pinned table
   // (free: the stream's previous launch, its H2D included, finished before this one is made),
   // copied behind the slots' copy markers, and the digests come back with one D2H.
   void launch(int stream, const int* slots, const int* lanes, int nslots, int total,
@@ -917,28 +920,30 @@ class HipPartDevice {
     if (total <= 0 || total > launch_lanes_) throw std::runtime_error("PartHasher: bad launch");
     Run& r = runs_[(size_t)stream];
     hipStream_t st = streams_[(size_t)stream];
-    uint64_t* hp = r.h_tab;
-    int64_t* hl = reinterpret_cast<int64_t*>(r.h_tab + total);
+    int64_t* ho = r.h_tab;
+    int64_t* hl = r.h_tab + total;
     int i = 0;
     for (int k = 0; k < nslots; ++k) {
       Slot& sl = slots_[(size_t)slots[k]];
       for (size_t c = 0; c < copies_.size(); ++c) HIP_CHECK(hipStreamWaitEvent(st, sl.copied[c], 0));
-      const uint64_t base = (uint64_t)(uintptr_t)sl.d_data;
+      const int64_t base = (int64_t)(sl.d_data - arena_);
       for (int l = 0; l < lanes[k]; ++l, ++i) {
-        hp[i] = base + (uint64_t)sl.h_lane[l];
+        ho[i] = base + sl.h_lane[l];
         hl[i] = sl.h_lane[max_lanes_ + l];
       }
     }
     if (i != total) throw std::runtime_error("PartHasher: lane count mismatch");
-    HIP_CHECK(hipMemcpyAsync(r.d_tab, r.h_tab, (size_t)total * 2 * sizeof(uint64_t),
+    HIP_CHECK(hipMemcpyAsync(r.d_tab, r.h_tab, (size_t)total * 2 * sizeof(int64_t),
                              hipMemcpyHostToDevice, st));
-    const uint64_t* dp = r.d_tab;
-    const int64_t* dl = reinterpret_cast<const int64_t*>(r.d_tab + total);
+    const int64_t* dp = r.d_tab;
+    const int64_t* dl = r.d_tab + total;
     const int block = 64, grid = (total + block - 1) / block;
     if (align16)
-      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, dp, dl, total, r.d_dig);
+      hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, arena_, dp, dl, total,
+                         r.d_dig);
     else
-      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st, dp, dl, total, r.d_dig);
+      hipLaunchKernelGGL(sha1_lanes<1>, dim3(grid), dim3(block), 0, st, arena_, dp, dl, total,
+                         r.d_dig);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(r.h_dig, r.d_dig, (size_t)total * 20, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipEventRecord(r.done, st));
@@ -964,8 +969,8 @@ class HipPartDevice {
     hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};   // one per copy stream
   };
   struct Run {                   // a compute stream's launch: lane table and digests
-    uint64_t* h_tab = nullptr;   // pinned [ptr x total][len x total]
-    uint64_t* d_tab = nullptr;
+    int64_t* h_tab = nullptr;    // pinned [offset in the arena x total][len x total]
+    int64_t* d_tab = nullptr;
     uint8_t* d_dig = nullptr;
     uint8_t* h_dig = nullptr;
     hipEvent_t done = nullptr;
@@ -993,8 +998,11 @@ class HipPartDevice {
     streams_.resize((size_t)compute);
     for (auto& st : streams_) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     slots_.resize((size_t)slots);
-    for (auto& sl : slots_) {
-      HIP_CHECK(hipMalloc((void**)&sl.d_data, (size_t)slot_bytes_));
+    // one arena, a window per slot: lane offsets from its base keep the kernel's loads global
+    HIP_CHECK(hipMalloc((void**)&arena_, (size_t)slot_bytes_ * (size_t)slots));
+    for (size_t k = 0; k < slots_.size(); ++k) {
+      Slot& sl = slots_[k];
+      sl.d_data = arena_ + (size_t)slot_bytes_ * k;
       HIP_CHECK(hipHostMalloc((void**)&sl.h_lane, (size_t)max_lanes_ * 2 * sizeof(int64_t),
                               hipHostMallocDefault));
       for (auto& e : sl.copied) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1003,9 +1011,9 @@ class HipPartDevice {
     launch_lanes_ = (int64_t)max_lanes_ * (int64_t)slots;
     runs_.resize((size_t)compute);
     for (auto& r : runs_) {
-      HIP_CHECK(hipHostMalloc((void**)&r.h_tab, (size_t)launch_lanes_ * 2 * sizeof(uint64_t),
+      HIP_CHECK(hipHostMalloc((void**)&r.h_tab, (size_t)launch_lanes_ * 2 * sizeof(int64_t),
                               hipHostMallocDefault));
-      HIP_CHECK(hipMalloc((void**)&r.d_tab, (size_t)launch_lanes_ * 2 * sizeof(uint64_t)));
+      HIP_CHECK(hipMalloc((void**)&r.d_tab, (size_t)launch_lanes_ * 2 * sizeof(int64_t)));
       HIP_CHECK(hipMalloc((void**)&r.d_dig, (size_t)launch_lanes_ * 20));
       HIP_CHECK(hipHostMalloc((void**)&r.h_dig, (size_t)launch_lanes_ * 20, hipHostMallocDefault));
       HIP_CHECK(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
@@ -1024,8 +1032,9 @@ class HipPartDevice {
       }
     for (auto c : copies_)
       if (c) hipStreamDestroy(c);
+    if (arena_) hipFree(arena_);
+    arena_ = nullptr;
     for (auto& sl : slots_) {
-      if (sl.d_data) hipFree(sl.d_data);
       if (sl.h_lane) hipHostFree(sl.h_lane);
       for (auto e : sl.copied)
         if (e) hipEventDestroy(e);
@@ -1060,6 +1069,7 @@ class HipPartDevice {
   int64_t slot_bytes_;
   int max_lanes_;
   int64_t launch_lanes_ = 0;
+  uint8_t* arena_ = nullptr;     // slots x slot_bytes of HBM
   std::vector<hipStream_t> copies_;
   std::vector<hipStream_t> streams_;
   std::vector<Slot> slots_;

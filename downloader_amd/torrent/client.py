@@ -37,7 +37,7 @@ class TorrentClient:
                  swarm_verify: str = "auto", wire_requests: bool = True,
                  wire_pool_mb: int = 4096, wire_gpu_inflight: int = 1024,
                  swarm_gpu_min_bytes: int = 8 << 30, swarm_gpu_tail_bytes: int = 0,
-                 swarm_backlog_bytes: int = 4 << 30):
+                 swarm_backlog_bytes: int = 4 << 30, wire_io_threads: int = 4):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -66,6 +66,7 @@ class TorrentClient:
         # peer connections handed to the native wire after the handshake (csrc/peerwire.cpp)
         self.native_wire = native_wire
         self.wire_verify_threads = wire_verify_threads
+        self.wire_io_threads = wire_io_threads    # epoll threads of a session's native wire
         self.swarm_verify = swarm_verify          # auto / gpu / cpu (native wire only)
         # whole pieces requested by the native wire itself (SwarmWire.assign), not per block
         self.wire_requests = wire_requests
@@ -104,6 +105,7 @@ class TorrentClient:
                    swarm_verify=d.swarm_verify_backend,
                    wire_requests=d.torrent_wire_requests,
                    wire_verify_threads=d.swarm_verify_threads,
+                   wire_io_threads=d.swarm_wire_io_threads,
                    wire_pool_mb=membudget.swarm_bytes(d.swarm_pool_mb) >> 20,
                    wire_gpu_inflight=d.swarm_gpu_inflight,
                    swarm_gpu_min_bytes=int(d.swarm_gpu_min_gb * (1 << 30)),

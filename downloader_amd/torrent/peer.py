@@ -94,6 +94,18 @@ class PeerConn:
         self.inflight: Dict[Tuple[int, int], float] = {}
         self.closed = False
         self.down_bytes = 0
+        # receive rate (TorrentSession._rate_loop): the request pipeline is sized to the
+        # peer's bandwidth-delay product, and a peer far slower than its share of the swarm
+        # stops owning whole pieces (``slow``)
+        self.rx_mark = 0
+        self.rate: Optional[float] = None
+        self.last_rate = 0.0
+        # a new connection starts at 8 pipelines (slow start: the rate loop sizes it after its
+        # first samples; a slow peer gives its requests back within ~1 s)
+        self.depth = 8 * session.client.pipeline
+        self.slow = False
+        self.slow_ticks = 0
+        self.progress_t: Optional[float] = None   # last rate sample with bytes received
         self.up_bytes = 0
         self.hash_fails = 0
         self.connected_at = time.monotonic()
@@ -128,6 +140,10 @@ class PeerConn:
             raise
         self.wire = wire
         self._wq = asyncio.Queue()
+        try:
+            wire.set_conn_pipeline(self.cid, self.depth)
+        except Exception:
+            pass
 
     # ---------------------------------------------------------------- sending
     # Every message goes through one small output queue that is written out when the

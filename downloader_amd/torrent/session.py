@@ -254,20 +254,37 @@ class PiecePicker:
                     out.append((ap.idx, b * BLOCK, ap.block_len(b)))
                     if len(out) >= k:
                         return out
-        while len(out) < k:
-            nb = self.next_block(peer_id, bf, fresh, dups)
-            if nb is None:
+        # whole new pieces (rarest first), each taken block by block
+        while fresh and len(out) < k:
+            best = self._take_rarest(bf)
+            if best < 0:
                 break
-            out.append(nb)
-            ap = self.active.get(nb[0])
-            if ap is not None and nb[1] == 0:      # a fresh piece: take its remaining blocks
-                for b in range(1, ap.nblocks):
-                    if len(out) >= k:
-                        break
-                    if ap.state[b] == 0:
-                        ap.state[b] = 1
-                        ap.req.setdefault(b, set()).add(peer_id)
-                        out.append((ap.idx, b * BLOCK, ap.block_len(b)))
+            ap = _Active(best, self.meta.piece_size(best), self.on_activate is None)
+            if self.on_activate is not None:
+                self.on_activate(best)
+            self.active[best] = ap
+            self.loose[best] = ap
+            for b in range(ap.nblocks):
+                if len(out) >= k:
+                    break
+                ap.state[b] = 1
+                ap.req[b] = {peer_id}
+                out.append((best, b * BLOCK, ap.block_len(b)))
+        # endgame: duplicates of outstanding blocks this peer has not requested yet - one pass
+        # (next_block per duplicate rescanned every loose piece: quadratic in the pipeline
+        # depth, seconds of event loop per fill once depths reached ~1000 blocks)
+        if dups and len(out) < k:
+            for ap in self.loose.values():
+                if ap.idx not in bf:
+                    continue
+                for b in range(ap.nblocks):
+                    if ap.state[b] == 1:
+                        rs = ap.req.setdefault(b, set())
+                        if peer_id not in rs:
+                            rs.add(peer_id)
+                            out.append((ap.idx, b * BLOCK, ap.block_len(b)))
+                            if len(out) >= k:
+                                return out
         return out
 
     def take_piece(self, peer_id: int, bf: Bitfield) -> int:
@@ -398,6 +415,19 @@ class MetadataFetch:
         return data
 
 
+# Per-peer rates (TorrentSession._rate_loop): sampled every RATE_S; each connection keeps
+# QUEUE_S of its rate requested (at least the client's pipeline, at most MAX_DEPTH blocks =
+# 16 MiB), so a 50 MB/s peer 200 ms away is not capped at pipeline x 16 KiB / RTT; a peer below
+# SLOW_SHARE of the busy peers' mean rate for SLOW_TICKS samples in a row - or one that
+# received nothing for SLOW_TICKS samples while holding work (stalled) - gives back the whole
+# pieces it owns and only helps with loose blocks until it speeds up (above 2 x SLOW_SHARE).
+RATE_S = 0.25
+QUEUE_S = 0.5
+MAX_DEPTH = 1024
+SLOW_SHARE = 1 / 8
+SLOW_TICKS = 2
+
+
 class TorrentSession:
     def __init__(self, client: "TorrentClient", info_hash: bytes, root: str,
                  meta: Optional[Metainfo] = None, trackers=(), webseeds=(), peers=(), name: str = "",
@@ -456,7 +486,8 @@ class TorrentSession:
         if client.native_wire:
             try:
                 from ..ops import native
-                self.wire = native().SwarmWire(max(1, client.wire_verify_threads))
+                self.wire = native().SwarmWire(max(1, client.wire_verify_threads),
+                                               max(1, getattr(client, "wire_io_threads", 4)))
             except Exception:
                 self.wire = None
         self.stats = {"hash_fails": 0, "peers_connected": 0, "webseed_failures": 0,
@@ -465,6 +496,13 @@ class TorrentSession:
                       "wire_released": 0, "wire_endgame_pieces": 0,
                       # ... and fills that started no piece: the verify / write backlog was full
                       "wire_backlogged": 0,
+                      # peers marked slow (their owned pieces / requests given back) and the
+                      # owned pieces / requested blocks they gave back
+                      "slow_peers": 0, "slow_released_pieces": 0, "slow_released_blocks": 0,
+                      "max_depth": 0,
+                      # longest time a peer held owned pieces / requested blocks without
+                      # receiving anything (a stalled peer is shed after SLOW_TICKS samples)
+                      "max_owned_idle_s": 0.0,
                       # summed over webseed streams: time in Range GETs / in piece verification
                       "webseed_fetch_s": 0.0, "webseed_verify_s": 0.0}
         self.add_peers(list(peers), "magnet")
@@ -502,6 +540,108 @@ class TorrentSession:
         if self.client.dht is not None and not (self.meta and self.meta.private):
             self._spawn(self._dht_loop())
         self._spawn(self._pex_loop())
+        self._spawn(self._rate_loop())
+
+    def _peer_rx(self, p: PeerConn) -> int:
+        if p.wire is not None:
+            try:
+                return int(self.wire.conn_rx(p.cid))
+            except Exception:
+                return p.down_bytes
+        return p.down_bytes
+
+    async def _rate_loop(self) -> None:
+        """Per-peer receive rates every RATE_S: each connection's request pipeline follows its
+        bandwidth-delay product (BEP-3 leaves the depth to the client; libtorrent keeps ~3 s
+        of a peer's rate requested), and a peer far slower than its share of the swarm - or
+        stalled mid-piece - hands its owned pieces and requested blocks back so faster peers
+        finish them (a 100 KB/s peer sat on a whole 4 MiB piece until the
+        endgame)."""
+        last = self._t_start = time.monotonic()
+        while not self._closed and not self.done.is_set():
+            await asyncio.sleep(RATE_S)
+            now = time.monotonic()
+            dt, last = max(1e-3, now - last), now
+            if self.picker is None:
+                continue
+            tl = self.stats.setdefault("rate_timeline", [])
+            if len(tl) < 600:      # (t, MB verified, endgame) per sample: the bench's ramp / tail
+                tl.append((round(now - self._t_start, 2), round(self.verified_bytes / 1e6, 1),
+                           int(self._endgame)))
+            busy = []
+            total = 0.0
+            for p in list(self.peers.values()):
+                if p.closed:
+                    continue
+                rx = self._peer_rx(p)
+                r = max(0, rx - p.rx_mark) / dt
+                p.rx_mark = rx
+                p.rate = r if p.rate is None else 0.5 * p.rate + 0.5 * r
+                p.last_rate = r
+                if r > 0 or p.progress_t is None:
+                    p.progress_t = now
+                elif not p.slow and (p.inflight or self._owns(p)):
+                    self.stats["max_owned_idle_s"] = max(self.stats["max_owned_idle_s"],
+                                                         round(now - p.progress_t, 2))
+                if not p.peer_choking and p.am_interested and p.bitfield is not None:
+                    busy.append(p)
+                    total += p.rate
+            if len(busy) < 2 or total <= 0:
+                continue
+            share = total / len(busy)
+            base = self.client.pipeline
+            shed = False
+            for p in busy:
+                # grow at once (the last sample), shrink with the average
+                depth = int(min(MAX_DEPTH, max(base, max(p.rate, p.last_rate) * QUEUE_S / BLOCK)))
+                if depth != p.depth:
+                    p.depth = depth
+                    self.stats["max_depth"] = max(self.stats["max_depth"], depth)
+                    if p.wire is not None:
+                        try:
+                            self.wire.set_conn_pipeline(p.cid, depth)
+                        except Exception:
+                            pass
+                stalled = p.progress_t is not None and now - p.progress_t >= SLOW_TICKS * RATE_S
+                if (p.rate < share * SLOW_SHARE or stalled) and (p.inflight or self._owns(p)):
+                    p.slow_ticks = SLOW_TICKS if stalled else p.slow_ticks + 1
+                    if p.slow_ticks >= SLOW_TICKS and not p.slow:
+                        p.slow = True
+                        self.stats["slow_peers"] += 1
+                        self._shed(p)
+                        shed = True
+                else:
+                    p.slow_ticks = 0
+                    if p.slow and p.rate >= 2 * share * SLOW_SHARE:
+                        p.slow = False
+            if shed:
+                self._refill_all()
+
+    def _owns(self, p: PeerConn) -> bool:
+        return any(ap.owner == p.cid for ap in self.picker.active.values())
+
+    def _shed(self, p: PeerConn) -> None:
+        """A slow peer's work goes back: its owned pieces become ordinary (blocks received
+        kept, its outstanding requests still its own), and its outstanding block requests
+        may be asked of others too (its late answers are then duplicates)."""
+        if self.wire is not None and self._owned_mode:
+            for idx, ap in list(self.picker.active.items()):
+                if ap.owner != p.cid:
+                    continue
+                r = self.wire.release_piece(idx)
+                if r is None:
+                    continue            # complete, being verified
+                _, states = r
+                self._to_block_mode(ap, states, p)
+                self.stats["slow_released_pieces"] += 1
+        for (piece, begin) in list(p.inflight):
+            ap = self.picker.active.get(piece)
+            if ap is None:
+                continue
+            b = begin // BLOCK
+            if ap.state[b] == 1:
+                ap.state[b] = 0         # free for others; p's request stays in ap.req
+                self.stats["slow_released_blocks"] += 1
 
     def _spawn(self, coro) -> asyncio.Task:
         t = asyncio.get_running_loop().create_task(coro)
@@ -701,8 +841,12 @@ class TorrentSession:
     def _assign(self, pc: PeerConn) -> bool:
         """Keep two pipelines of blocks queued on the connection's native wire, a whole piece
         at a time. False when no piece was left for it (the endgame may begin)."""
-        me, want = pc.cid, 2 * self.client.pipeline
+        # blocks queued beyond those in flight: one pipeline (NEED asks for more when the
+        # queue runs below it) - a connection owns ~2 x its depth, ~2 x QUEUE_S of its rate
+        me, want = pc.cid, pc.depth
         wire, picker = self.wire, self.picker
+        if pc.slow:
+            return False                 # a slow peer helps with loose blocks only
         try:
             t = wire.todo(me)
             while t < want:
@@ -715,7 +859,7 @@ class TorrentSession:
                 if idx < 0:
                     # nothing left to start: once this connection is down to its last
                     # pipeline, the endgame begins (the others' queues become duplicable)
-                    if t < self.client.pipeline and picker.no_candidates():
+                    if t < pc.depth and picker.no_candidates():
                         self._enter_endgame()
                     return False
                 if self._tail_bytes and not self._host_tail and picker.unstarted() * \
@@ -744,8 +888,18 @@ class TorrentSession:
         if self._endgame or self.wire is None:
             return
         self._endgame = True
+        # pieces of connections at least half the swarm's mean rate stay theirs (they finish
+        # them sooner than duplicates would: a heterogeneous swarm spent 2/3 of its endgame on
+        # per-block duplicates of fast owners' pieces); slower owners' pieces go back to
+        # per-block requesting, where idle connections duplicate their missing blocks
+        rates = [p.rate for p in self.peers.values() if not p.closed and p.rate]
+        mean = sum(rates) / len(rates) if rates else 0.0
         for idx, ap in list(self.picker.active.items()):
             if ap.owner is None:
+                continue
+            owner = self.peers.get(ap.owner)
+            if owner is not None and not owner.closed and not owner.slow and mean > 0 and \
+                    (owner.rate or 0.0) >= mean / 2:
                 continue
             r = self.wire.release_piece(idx)
             if r is None:
@@ -903,7 +1057,7 @@ class TorrentSession:
 
     def refill_due(self, pc: PeerConn) -> bool:
         """Whether ``fill`` would send anything (checked without a coroutine per block)."""
-        return self.client.pipeline - len(pc.inflight) >= max(1, self.client.pipeline // 4)
+        return pc.depth - len(pc.inflight) >= max(1, pc.depth // 4)
 
     def take_block(self, pc: PeerConn, idx: int, begin: int, data) -> bool:
         """Synchronous part of ``on_block``: copy a block into its piece. True when
@@ -966,11 +1120,13 @@ class TorrentSession:
             # missing piece is being fetched
             fresh = False
             dups = not self._assign(pc) and self._endgame
-        room = self.client.pipeline - len(pc.inflight)
+        room = pc.depth - len(pc.inflight)
         # Refill in batches (at least a quarter of the pipeline) so one write carries many
         # REQUEST messages instead of one syscall per 17-byte message.
-        if room < max(1, self.client.pipeline // 4):
+        if room < max(1, pc.depth // 4):
             return
+        if pc.slow:
+            fresh = False                # no new pieces for a slow peer: loose blocks only
         blocks = self.picker.next_blocks(pc.cid, pc.bitfield, room, fresh, dups)
         if blocks:
             await pc.request_many(blocks)

@@ -263,6 +263,9 @@ class DownloadConfig(BaseModel):
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
+    # epoll threads reading and writing a session's peer connections on the native wire
+    # (connections spread over them): not two threads per connection
+    swarm_wire_io_threads: int = 4
     # idle swarm piece buffers kept per worker process (reused: no page faults per piece, and
     # page-locked once in GPU mode, where the download runs up to ~0.5 s ahead of the device).
     # 0: 1/8 of this worker's share of the memory limit, at most 4096 (utils/membudget.py)
