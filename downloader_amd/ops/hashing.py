@@ -307,7 +307,7 @@ def swarm_backend(requested: str, total_bytes: int, gpu_min_bytes: int) -> str:
     the host lacks the AVX-512 multi-buffer SHA-1, or for a torrent of at least
     ``gpu_min_bytes`` (0: never): on config 6 at 16 GB the device runs within ~5 % of the
     host's rate at 35 % less leech CPU per byte; at 2 GB its ~75 ms per piece costs 35 - 40 %
-    of the rate (profiles/r5/swarm4/)."""
+    of the rate (profiles/archive/r5/swarm/backpressure/)."""
     if requested == "cpu":
         return "cpu"
     if requested == "gpu":

@@ -951,7 +951,7 @@ class TorrentSession:
     def _wire_blocks(self, pc: PeerConn, data: bytes) -> None:
         """Book one batch of arrivals (16-byte records: piece, begin, length, status). The
         per-block work is what the Python wire did minus the copy and the framing: ~1.6 us a
-        block, 0.1 CPU-s per GB (profiles/r5/swarm/)."""
+        block, 0.1 CPU-s per GB (profiles/archive/r5/swarm/wire/)."""
         picker = self.picker
         if picker is None:
             return

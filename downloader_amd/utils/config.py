@@ -257,7 +257,7 @@ class DownloadConfig(BaseModel):
     # multi-buffer SHA-1, else the host. Config 6 (4 seeders) on the box: 16 GB on the device
     # 8.7 - 9.0 GB/s at 0.28 - 0.29 leech CPU-s/GB vs 9.0 - 9.5 at 0.43 - 0.48 on the host;
     # 2 GB 5.3 - 5.8 vs 8.9 - 9.2 (the device's ~75 ms per piece is a bigger share of a short
-    # job; profiles/r5/swarm4/)
+    # job; profiles/archive/r5/swarm/backpressure/)
     swarm_verify_backend: str = "auto"
     swarm_gpu_min_gb: float = 8.0
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
@@ -272,7 +272,7 @@ class DownloadConfig(BaseModel):
     swarm_pool_mb: int = 0
     # GPU mode: pieces on the device at once (a 4 MiB piece spends ~75 ms there plus its wait
     # for a compute stream); past it the host hashes the overflow. 512 overflowed on config 6
-    # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/r5/swarm3/)
+    # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/archive/r5/swarm/event_loop/)
     swarm_gpu_inflight: int = 1024
     # GPU mode: once no more than this much of the torrent (at most a quarter) is left to
     # start, pieces are hashed on the host - on the device the last ones each add ~0.1 s to

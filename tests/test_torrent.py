@@ -273,7 +273,7 @@ def test_swarm_native_and_python_wire(run, tmp_path, native_wire, wire_requests)
                 # whole pieces were handed to the wire, which asked for their blocks itself
                 # (on a torrent this small every piece is handed out at once, and the endgame
                 # soon turns most back to per-block requests; config 6 has the wire request
-                # 99.6 % of the blocks of 2 GB itself, profiles/r5/)
+                # 99.6 % of the blocks of 2 GB itself, profiles/archive/r5/)
                 assert st["assigned"] > 0 and st["requests"] > 0
             else:
                 assert st["assigned"] == 0 and st["requests"] == 0
