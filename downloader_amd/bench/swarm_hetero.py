@@ -192,7 +192,8 @@ async def run_hetero(total: int = 2 * 10 ** 9, piece_len: int = 4 << 20, peers: 
     mbps = total / dt / MB
     return {"config": "swarm-hetero", "wire": wire, "bytes": total, "piece_len": piece_len,
             "peers": peers, "seed": seed, "s": round(dt, 3), "MBps": round(mbps, 1),
-            "offered_MBps": round(offered / MB, 1), "of_offered": round(mbps / (offered / MB), 3),
+            "offered_MBps": round(offered / MB, 1),
+            "of_offered": round(mbps / (offered / MB), 3) if offered else None,
             "healthy": len(healthy), "stalling": sum(s["kind"] == "stall" for s in specs),
             "hanging_up": sum(s["kind"] == "hangup" for s in specs),
             "data_ok": same, "threads_before": threads0, "threads_peak": peak,

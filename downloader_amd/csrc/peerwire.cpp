@@ -70,9 +70,11 @@ constexpr uint8_t kPiece = 7;
 constexpr uint8_t kRequest = 6;
 constexpr uint8_t kCancel = 8;
 constexpr uint32_t kMaxServe = 131072;     // session.py serve_request's bound
-// blocks queued to serve on one connection: BEP-3 clients keep a few dozen requests out
-// (webtorrent: 5 - 250); more is a flood (the queue grew without bound)
-constexpr size_t kMaxServeQueue = 256;
+// blocks queued to serve on one connection (advertised as BEP-10 reqq, torrent/peer.py): a
+// leecher sizing its pipeline to a fast, distant link keeps up to ~1,000 out (ours: 1,024;
+// libtorrent allows 2,000); more is a flood (the queue grew without bound).
+// 12 bytes of request each: 2,048 is ~100 KiB a connection.
+constexpr size_t kMaxServeQueue = 2048;
 constexpr size_t kRecvBatch = 1u << 20;    // receive room kept per connection (plus kMaxMsg)
 
 uint32_t be32(const uint8_t* p) {
@@ -537,12 +539,16 @@ void SwarmWire::set_conn_pipeline(uint64_t id, uint32_t depth) {
   std::shared_ptr<Conn> c = conn(id);
   if (!c) return;
   std::string reqs;
+  bool need;
   {
     std::lock_guard<std::mutex> g(mu_);
     c->depth = std::max<uint32_t>(1, depth);
-    pump(*c, &reqs);
+    need = pump(*c, &reqs);
   }
   if (!reqs.empty()) queue_out(*c, std::move(reqs));
+  // a deeper pipeline drains the queue below it: Python must hear so (pump marked NEED sent;
+  // dropping it left the connection idle for good - config 6 stopped at 160 MiB)
+  if (need) push(c->id, kEvNeed, std::string());
 }
 
 size_t SwarmWire::assign(uint64_t id, uint32_t idx) {

@@ -103,6 +103,7 @@ class PeerConn:
         # a new connection starts at 8 pipelines (slow start: the rate loop sizes it after its
         # first samples; a slow peer gives its requests back within ~1 s)
         self.depth = 8 * session.client.pipeline
+        self.reqq = 0                  # the peer's advertised request queue (0: not said)
         self.slow = False
         self.slow_ticks = 0
         self.progress_t: Optional[float] = None   # last rate sample with bytes received
@@ -201,8 +202,10 @@ class PeerConn:
             await self.send(EXTENDED, bytes([mid]) + payload)
 
     async def send_ext_handshake(self) -> None:
+        # reqq: the requests the native wire queues per connection before it calls it a flood
+        # (csrc/peerwire.cpp kMaxServeQueue)
         d = {"m": {"ut_metadata": UT_METADATA_ID, "ut_pex": UT_PEX_ID}, "v": "downloader-amd 0.1",
-             "reqq": 256}
+             "reqq": 2048}
         if self.s.client.listen_port:
             d["p"] = self.s.client.listen_port
         if self.s.meta is not None:
@@ -454,6 +457,9 @@ class PeerConn:
                 self.ext = {k: int(v) for k, v in m.items() if isinstance(v, int) and v > 0}
             # untrusted: a negative size or an out-of-range port counts as absent
             ms, lp = d.get(b"metadata_size", 0), d.get(b"p", 0)
+            rq = d.get(b"reqq", 0)
+            # BEP-10 reqq: requests it keeps without dropping; our pipeline to it stays below
+            self.reqq = rq if isinstance(rq, int) and 0 < rq < 1 << 20 else 0
             self.metadata_size = ms if isinstance(ms, int) and ms > 0 else 0
             self.listen_port = lp if isinstance(lp, int) and 0 < lp < 65536 else 0
             if self.listen_port and not self.outgoing:

@@ -593,7 +593,8 @@ class TorrentSession:
             shed = False
             for p in busy:
                 # grow at once (the last sample), shrink with the average
-                depth = int(min(MAX_DEPTH, max(base, max(p.rate, p.last_rate) * QUEUE_S / BLOCK)))
+                cap = min(MAX_DEPTH, p.reqq) if p.reqq else MAX_DEPTH
+                depth = int(min(cap, max(min(base, cap), max(p.rate, p.last_rate) * QUEUE_S / BLOCK)))
                 if depth != p.depth:
                     p.depth = depth
                     self.stats["max_depth"] = max(self.stats["max_depth"], depth)
@@ -616,6 +617,14 @@ class TorrentSession:
                         p.slow = False
             if shed:
                 self._refill_all()
+            elif self.wire is not None and self._owned_mode and not self._endgame:
+                # safety net: a connection whose native queue ran below its pipeline without
+                # Python hearing of it (NEED is sent once per fill) gets a fill now
+                for p in busy:
+                    if p.wire is not None and not p.fill_queued and not p.slow and \
+                            p._wq is not None and self.wire.todo(p.cid) < p.depth:
+                        p.fill_queued = True
+                        p._wq.put_nowait((EV_FILL, None))
 
     def _owns(self, p: PeerConn) -> bool:
         return any(ap.owner == p.cid for ap in self.picker.active.values())

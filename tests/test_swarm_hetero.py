@@ -37,3 +37,16 @@ def test_hetero_swarm_completes_without_stuck_pieces(run, tmp_path, wire):
         assert r["wire_io_threads"] == 4
         assert r["threads_peak"] - r["threads_before"] <= 24, r
     assert r["MBps"] > 0
+
+
+@pytest.mark.slow
+def test_fast_seeders_pipeline_growth_never_idles_a_connection(run, tmp_path):
+    """Config 6's shape on swarmd: 4 unthrottled seeders, the rate loop growing every
+    connection's pipeline mid-download. A deeper pipeline drains the connection's queue of
+    blocks to request below it; that NEED must reach Python (it was dropped once, leaving all
+    four connections idle at 160 MiB of 256)."""
+    specs = [{"rate": 0, "delay_ms": 0, "stall": 0, "hangup": 0, "kind": "ok"} for _ in range(4)]
+    r = run(run_hetero(total=256 << 20, piece_len=4 << 20, peers=4, specs=specs, pipeline=64,
+                       src_dir=str(tmp_path), timeout=60), timeout=120)
+    assert r["data_ok"] and r["hash_fails"] == 0 and r["slow_peers"] == 0
+    assert r["max_depth"] > 8 * 64                     # the pipelines did grow

@@ -1550,7 +1550,9 @@ def test_native_wire_backlog_holds_back_new_pieces(run, tmp_path):
 
     async def go():
         raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 3_000_000}, piece=65536)
-        leech = await TorrentClient(swarm_verify="gpu", pipeline=16, swarm_gpu_tail_bytes=0,
+        # (pipeline 2: a connection starts at 8 pipelines = 16 blocks = 4 pieces queued, so
+        # pieces are started a few at a time and the backlog is met)
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=2, swarm_gpu_tail_bytes=0,
                                     swarm_backlog_bytes=4 * 65536).start()
         meta = parse_torrent(raw)
         s = await leech.add_torrent(meta, str(tmp_path / "dl"),
