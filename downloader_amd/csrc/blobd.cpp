@@ -139,6 +139,7 @@ uint64_t g_synth_shift = 0;  // --synth-shift B: webseed files served B bytes of
 double g_s3_fail_rate = 0;  // --s3-fail-rate: this share of object/part PUTs answer 503 SlowDown
 std::atomic<uint64_t> g_s3_faults{0};
 uint64_t g_crc_check = 1;        // --crc-check N: recompute 1 in N checksummed bodies
+int g_rcvlowat = 0;              // --rcvlowat KB: SO_RCVLOWAT of the sink's kernel drops
 uint64_t g_crc_salt = 0;         // --crc-salt S (default: random per run)
 std::atomic<uint64_t> g_crc_checked{0}, g_crc_unchecked{0}, g_media_puts{0}, g_media_puts_crc{0};
 
@@ -562,6 +563,17 @@ class Conn {
   // (fs.pipe-user-pages-soft, shared with the workers' relays on the same box).
   bool discard_plain(int64_t n, Consumer& c, uint64_t pos) {
     uint8_t win[16384];
+    bool lowat_set = false;
+    struct Reset {
+      int fd;
+      bool* on;
+      ~Reset() {
+        if (*on) {
+          int one = 1;
+          setsockopt(fd, SOL_SOCKET, SO_RCVLOWAT, &one, sizeof one);
+        }
+      }
+    } reset{fd_, &lowat_set};
     while (n > 0) {
       if (c.windows && c.in_window(pos)) {   // a sampled window: recv exactly its bytes
         size_t want = (size_t)std::min<uint64_t>((uint64_t)n, c.window_end(pos) - pos);
@@ -578,6 +590,12 @@ class Conn {
       uint64_t stop = c.windows ? std::min<uint64_t>(c.next_window(pos), pos + (uint64_t)n)
                                 : pos + (uint64_t)n;
       int64_t run = (int64_t)(stop - pos);
+      if (g_rcvlowat && run > g_rcvlowat && !lowat_set) {
+        // --rcvlowat: wake for at least this much (the run's tail still returns: TCP's
+        // target is min(lowat, asked))
+        setsockopt(fd_, SOL_SOCKET, SO_RCVLOWAT, &g_rcvlowat, sizeof g_rcvlowat);
+        lowat_set = true;
+      }
       while (run > 0) {
         // no buffer: TCP drops MSG_TRUNC bytes without copying (and a 16 KiB one with a
         // longer length trips _FORTIFY_SOURCE's recv check)
@@ -1229,6 +1247,7 @@ int main(int argc, char** argv) {
     else if (a == "--crc-check") g_crc_check = std::max<uint64_t>(1, strtoull(next(), nullptr, 10));
     else if (a == "--crc-salt") g_crc_salt = strtoull(next(), nullptr, 10);
     else if (a == "--synth-shift") g_synth_shift = strtoull(next(), nullptr, 10);
+    else if (a == "--rcvlowat") g_rcvlowat = atoi(next()) * 1024;
     else if (a == "--tls-cert") tls_cert = next();
     else if (a == "--tls-key") tls_key = next();
     else if (a == "--s3-fail-rate") g_s3_fail_rate = atof(next());

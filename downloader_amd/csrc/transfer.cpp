@@ -1069,6 +1069,25 @@ int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* 
     moved += (int64_t)len;
     if (prog) prog->bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
   }
+  // STAGER_RCVLOWAT_KB (A/B knob): the peek waits for this much (or the rest of the body)
+  // instead of waking on every segment that lands
+  static const int lowat = [] {
+    const char* e = getenv("STAGER_RCVLOWAT_KB");
+    long kb = e ? atol(e) : 0;
+    return (int)(kb > 0 && kb <= 4096 ? kb * 1024 : 0);
+  }();
+  struct LowatScope {
+    int fd, on;
+    LowatScope(int f, int v) : fd(f), on(v) {
+      if (on) setsockopt(fd, SOL_SOCKET, SO_RCVLOWAT, &on, sizeof on);
+    }
+    ~LowatScope() {
+      if (on) {
+        int one = 1;
+        setsockopt(fd, SOL_SOCKET, SO_RCVLOWAT, &one, sizeof one);
+      }
+    }
+  } lowat_scope(fd_, n - moved > (int64_t)lowat ? lowat : 0);
   while (moved < n) {
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;

@@ -27,6 +27,22 @@ print({k: j.get(k) for k in keys})
 print("curve", [(c["procs"], c["MBps"], c["p50_s"]) for c in j.get("workers_curve", [])])
 PY
 done
+if [[ -z "$SKIP_LOWAT" ]]; then
+X="--no-compare-unchecked --no-compare-reference --workers-curve= --torrent-gb 0"
+for rep in 1 2; do
+  for lw in 0 256; do
+    step "lowat $lw $rep"
+    if [ $lw = 0 ]; then
+      timeout -k 10 120 python bench.py $X > $F/lowat${lw}_$rep.json 2>> $F/bench.err || { tail -20 $F/bench.err; exit 1; }
+    else
+      STAGER_RCVLOWAT_KB=$lw STAGER_BLOBD_RCVLOWAT_KB=$lw timeout -k 10 120 python bench.py $X > $F/lowat${lw}_$rep.json 2>> $F/bench.err || { tail -20 $F/bench.err; exit 1; }
+    fi
+    python3 -c "
+import json; j=json.load(open('$F/lowat${lw}_$rep.json'))
+print('lowat $lw', j['value'], 'p50', j['p50_job_latency_s'], 'util', j['cpu_utilisation'], 'w', j['worker_cpu_s_per_GB'], 'peer', j['peer_cpu_s_per_GB'], j['worker_breakdown'])"
+  done
+done
+fi
 summ() {
 python3 - "$1" <<'PY'
 import json, sys
