@@ -574,10 +574,22 @@ class Conn {
         }
       }
     } reset{fd_, &lowat_set};
+    // --rcvlowat: wake for at least this much while more than twice that is still to come
+    // (TCP wakes a sleeping reader only once sk_rcvlowat bytes are queued, whatever it asked
+    // for: before fewer are left the mark goes back to 1). Checked before every recv.
+    auto adjust = [&] {
+      const bool want = g_rcvlowat && n > 2 * (int64_t)g_rcvlowat;
+      if (want != lowat_set) {
+        int v = want ? g_rcvlowat : 1;
+        setsockopt(fd_, SOL_SOCKET, SO_RCVLOWAT, &v, sizeof v);
+        lowat_set = want;
+      }
+    };
     while (n > 0) {
       if (c.windows && c.in_window(pos)) {   // a sampled window: recv exactly its bytes
         size_t want = (size_t)std::min<uint64_t>((uint64_t)n, c.window_end(pos) - pos);
         want = std::min(want, sizeof win);
+        adjust();
         ssize_t r = ::recv(fd_, win, want, 0);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) return false;
@@ -590,15 +602,11 @@ class Conn {
       uint64_t stop = c.windows ? std::min<uint64_t>(c.next_window(pos), pos + (uint64_t)n)
                                 : pos + (uint64_t)n;
       int64_t run = (int64_t)(stop - pos);
-      if (g_rcvlowat && run > g_rcvlowat && !lowat_set) {
-        // --rcvlowat: wake for at least this much (the run's tail still returns: TCP's
-        // target is min(lowat, asked))
-        setsockopt(fd_, SOL_SOCKET, SO_RCVLOWAT, &g_rcvlowat, sizeof g_rcvlowat);
-        lowat_set = true;
-      }
+
       while (run > 0) {
         // no buffer: TCP drops MSG_TRUNC bytes without copying (and a 16 KiB one with a
         // longer length trips _FORTIFY_SOURCE's recv check)
+        adjust();
         ssize_t in = ::recv(fd_, nullptr, (size_t)std::min<int64_t>(run, 1 << 20), MSG_TRUNC);
         if (in < 0 && errno == EINTR) continue;
         if (in <= 0) return false;

@@ -1076,19 +1076,24 @@ int64_t HttpConn::relay_peek(HttpConn& dst, int64_t n, int64_t moved, Progress* 
     long kb = e ? atol(e) : 0;
     return (int)(kb > 0 && kb <= 4096 ? kb * 1024 : 0);
   }();
+  // (TCP wakes a sleeping reader only once sk_rcvlowat bytes are queued, whatever it asked
+  // for: the mark must drop back to 1 before fewer than that are left to come)
   struct LowatScope {
     int fd, on;
     LowatScope(int f, int v) : fd(f), on(v) {
       if (on) setsockopt(fd, SOL_SOCKET, SO_RCVLOWAT, &on, sizeof on);
     }
-    ~LowatScope() {
+    void off() {
       if (on) {
         int one = 1;
         setsockopt(fd, SOL_SOCKET, SO_RCVLOWAT, &one, sizeof one);
+        on = 0;
       }
     }
-  } lowat_scope(fd_, n - moved > (int64_t)lowat ? lowat : 0);
+    ~LowatScope() { off(); }
+  } lowat_scope(fd_, n - moved > 2 * (int64_t)lowat ? lowat : 0);
   while (moved < n) {
+    if (lowat_scope.on && n - moved < 2 * (int64_t)lowat) lowat_scope.off();
     if (prog && prog->cancelled.load(std::memory_order_relaxed)) {
       reusable_ = false;
       dst.reusable_ = false;
