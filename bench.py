@@ -35,7 +35,8 @@ Same-call extras of the line: ``unchecked_MBps`` (``s3.checksum: auto``: the pla
 spliced with no payload checksum), ``reference_mode_MBps`` (reference-equivalent mode,
 BASELINE.md: one serial prefetch-1 consumer per process, ``--ref-procs`` of them, on the same
 CPUs; ``vs_baseline`` = headline / it), ``workers_curve`` (MB/s and p50 at 1/2/4/8 worker
-processes of the rank) and the streamed-torrent GPU vs host A/B.
+processes of the rank), config 1's p50 (a single 10 MB job, tuned and reference mode) and the
+streamed-torrent GPU vs host A/B.
 """
 from __future__ import annotations
 
@@ -135,7 +136,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--workers-curve", default="1,2,4,8",
                    help="worker-process counts of the same-call curve (MB/s + p50 at each; "
                         "'' = skip)")
-    p.add_argument("--curve-steps", type=int, default=3, help="timed steps per curve point")
+    p.add_argument("--curve-steps", type=int, default=6, help="timed steps per curve point")
+    p.add_argument("--no-config1", dest="config1", action="store_false",
+                   help="skip the same-call config 1 (single 10 MB job) p50, tuned and reference")
     p.add_argument("--curve-warmup-jobs", type=int, default=8,
                    help="untimed jobs per worker process before each curve point")
     return p.parse_args()
@@ -603,6 +606,53 @@ def torrent_measure(args, dist: Dist) -> dict:
     return out
 
 
+async def _config1(mode: str, jobs: int = 21, object_mb: int = 10) -> dict:
+    """BASELINE config 1 in miniature: a single 10 MB HTTP job at a time through one worker
+    (``bench/configs.config1``; the first job only warms the connections)."""
+    from downloader_amd.bench import configs
+    from downloader_amd.bench.infra import Blobd
+    from downloader_amd.broker.memory import MemoryBroker
+    from downloader_amd.models import api
+    from downloader_amd.service.worker import Worker
+    stage = tempfile.mkdtemp(prefix="bench-cfg1-")
+    try:
+        with Blobd(sink="discard") as b:
+            w = Worker(configs._cfg(mode, b.endpoint, stage, None, concurrency=1,
+                                    download={"gpu_prewarm": False}), broker=MemoryBroker())
+            await w.start(health=False)
+            lat = []
+            for i in range(jobs):
+                m = api.make_download(f"cfg1-{mode}-{i}", "http",
+                                      b.media_url(f"cfg1-{i}.mkv", object_mb * 10 ** 6, i))
+                _, r = await configs._run_jobs(w, [m])
+                if r[0].outcome != "staged":
+                    raise RuntimeError(f"config 1 job failed: {r[0].error}")
+                lat.append(r[0].seconds)
+            await w.stop()
+    finally:
+        shutil.rmtree(stage, ignore_errors=True)
+    lat = lat[1:] or lat
+    return {"p50_s": round(statistics.median(lat), 4),
+            "MBps_sequential": round(object_mb * 10 ** 6 / statistics.mean(lat) / 1e6, 1)}
+
+
+def config1_measure(args, dist: Dist) -> dict:
+    """Same call: config 1 (single 10 MB job, one worker) tuned and in reference mode, on
+    rank 0's CPUs - the p50 half of BASELINE's metric on its own config."""
+    out: dict = {}
+    if dist.rank == 0:
+        try:
+            t = asyncio.run(_config1("tuned"))
+            r = asyncio.run(_config1("reference"))
+            out = {"config1_p50_s": t["p50_s"], "config1_MBps_sequential": t["MBps_sequential"],
+                   "config1_reference_p50_s": r["p50_s"],
+                   "config1_reference_MBps_sequential": r["MBps_sequential"]}
+        except Exception as e:      # an extra of the line: never costs the headline
+            out = {"config1_error": f"{type(e).__name__}: {e}"[:300]}
+    dist.barrier()
+    return out
+
+
 def pin_rank(dist: Dist, per_rank: int = 0) -> list:
     """Give each rank (worker threads + its blobd, which inherits the mask) a disjoint slice
     of the allowed CPUs: no cross-rank cache thrash, and sockets/threads stay on a few CCDs
@@ -726,6 +776,7 @@ def main() -> int:
     try:
         tuned = measure(args, dist, endpoint, args.mode, blob, nproc, pinned)
         unchecked = single = ref = tor = None
+        cfg1: dict = {}
         curve = []
         if args.compare_unchecked and tuned_mode and integrity(args, args.checksum) == "crc32c":
             with _override(args, checksum="auto"):
@@ -750,6 +801,7 @@ def main() -> int:
                               "cpu_utilisation": round(m["timed_cpu_s"]
                                                        / max(1e-9, m["cpu_capacity_s"]), 3)})
         args.concurrency, args.pipe_kb_eff = head_conc, head_pipe_kb
+        cfg1 = config1_measure(args, dist) if args.config1 and tuned_mode else {}
         tor = torrent_measure(args, dist) if args.torrent_gb > 0 and tuned_mode else None
     finally:
         if blob is not None:
@@ -833,6 +885,7 @@ def main() -> int:
             line.update(_cpu_fields(ref, "reference_mode_"))
         if curve:                # same call: MB/s and p50 at 1/2/4/8 worker processes
             line["workers_curve"] = curve
+        line.update(cfg1)        # same call: config 1's p50, tuned and reference mode
         if unchecked is not None:   # same call: the spliced relay with no payload checksum
             line["unchecked_MBps"] = round(unchecked["mbps"], 2)
             line["unchecked_p50_s"] = round(unchecked["p50"], 4)

@@ -68,8 +68,10 @@ class Blobd:
             + (["--crc-check", str(self.crc_check)] if self.crc_check > 1 else [])
             + (["--crc-salt", str(self.crc_salt)] if self.crc_salt else [])
             + (["--synth-shift", str(self.synth_shift)] if self.synth_shift else [])
-            + (["--rcvlowat", os.environ["STAGER_BLOBD_RCVLOWAT_KB"]]
-               if os.environ.get("STAGER_BLOBD_RCVLOWAT_KB") else [])
+            # the sink's kernel drops wake per 256 KiB, not per segment (STAGER_BLOBD_RCVLOWAT_KB:
+            # another mark, 0 = off; profiles/r6/check2/lowat*)
+            + (["--rcvlowat", os.environ.get("STAGER_BLOBD_RCVLOWAT_KB", "256")]
+               if os.environ.get("STAGER_BLOBD_RCVLOWAT_KB", "256") != "0" else [])
             + (["--tls-cert", self.tls[0], "--tls-key", self.tls[1]] if self.tls else [])
             + (["--s3-fail-rate", str(self.s3_fail_rate)] if self.s3_fail_rate else [])
             + (["--s3-corrupt-rate", str(self.s3_corrupt_rate)] if self.s3_corrupt_rate else [])

@@ -190,10 +190,16 @@ async def run_hetero(total: int = 2 * 10 ** 9, piece_len: int = 4 << 20, peers: 
         shutil.rmtree(src, ignore_errors=True)
         shutil.rmtree(dst, ignore_errors=True)
     mbps = total / dt / MB
+    # what the stalling / hanging-up seeders did deliver before they stopped, added to the
+    # healthy ones' rates: the rate the swarm as a whole offered this download
+    partial = sum(b for sp, b in zip(specs, sent or []) if sp["kind"] != "ok") / dt
+    offered_all = offered + partial
     return {"config": "swarm-hetero", "wire": wire, "bytes": total, "piece_len": piece_len,
             "peers": peers, "seed": seed, "s": round(dt, 3), "MBps": round(mbps, 1),
             "offered_MBps": round(offered / MB, 1),
             "of_offered": round(mbps / (offered / MB), 3) if offered else None,
+            "offered_incl_partial_MBps": round(offered_all / MB, 1),
+            "of_offered_incl_partial": round(mbps / (offered_all / MB), 3) if offered_all else None,
             "healthy": len(healthy), "stalling": sum(s["kind"] == "stall" for s in specs),
             "hanging_up": sum(s["kind"] == "hangup" for s in specs),
             "data_ok": same, "threads_before": threads0, "threads_peak": peak,
