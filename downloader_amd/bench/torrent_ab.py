@@ -25,6 +25,14 @@ from .synth_torrent import config4_files, make_synth_torrent, served_paths
 MB = 1_000_000
 
 
+def _relay_counters() -> Dict:
+    try:
+        from ..ops import native
+        return dict(native().relay_counters())
+    except Exception:
+        return {}
+
+
 def _cpu() -> float:
     t = os.times()
     return t.user + t.system
@@ -90,8 +98,10 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
                         dev0 = hashing.gpu_relay_stats()
                     msg = api.make_download(f"{tag}-{be}-{k}", "http", url, "TV")
                     c0, p0 = _cpu(), b.cpu_seconds()
+                    rc0 = _relay_counters()
                     dt, r = await _stage(workers[be], msg)
                     c1, p1 = _cpu(), b.cpu_seconds()
+                    rc1 = _relay_counters()
                     if r.outcome != "staged":
                         raise RuntimeError(f"torrent A/B job ({be}) failed: {r.error}")
                     if r.bytes != total:
@@ -101,7 +111,8 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
                         runs[be].append({"s": dt, "worker_cpu_s": c1 - c0, "peer_cpu_s": p1 - p0,
                                          "hash_fails": t.get("hash_fails", 0),
                                          "parts": t.get("parts", 0),
-                                         "gpu_parts": t.get("gpu_parts", 0)})
+                                         "gpu_parts": t.get("gpu_parts", 0),
+                                         "relay": {k: rc1[k] - rc0.get(k, 0) for k in rc1}})
             dev1 = hashing.gpu_relay_stats() if any(be != "cpu" for be in backends) else {}
             st = b.stats()
     finally:
@@ -123,6 +134,23 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
         out[f"torrent_{key}_worker_cpu_s_per_GB"] = round(
             statistics.median(x["worker_cpu_s"] for x in xs) / (total / 1e9), 4)
         out[f"torrent_{key}_hash_fails"] = sum(x["hash_fails"] for x in xs)
+        # where the workers' CPU went (native relay counters, as the headline's
+        # worker_breakdown): relaying threads, CRC, host SHA-1, the rest
+        rc: Dict = {}
+        for x in xs:
+            for k, v in x["relay"].items():
+                rc[k] = rc.get(k, 0) + v
+        gb = max(1e-9, len(xs) * total / 1e9)
+        cpu = sum(x["worker_cpu_s"] for x in xs)
+        relay_s = sum(rc.get(f"{m}_cpu_ns", 0) for m in ("splice", "dup", "copy", "hashed")) / 1e9
+        out[f"torrent_{key}_breakdown"] = {
+            # relaying threads of the hashed relays (peek copy into the part buffer, CRC,
+            # splice; host SHA-1 of the parts not given to the device)
+            "relay_threads_cpu_s_per_GB": round(relay_s / gb, 4),
+            "host_sha1_s_per_GB": round(rc.get("sha1_ns", 0) / 1e9 / gb, 4),
+            "crc_cpu_s_per_GB": round(rc.get("crc_ns", 0) / 1e9 / gb, 4),
+            "other_worker_cpu_s_per_GB": round(max(0.0, cpu - relay_s) / gb, 4),
+            "relays": {m: rc.get(f"{m}_relays", 0) for m in ("splice", "dup", "copy", "hashed")}}
         if be != "cpu":      # parts whose pieces the device hashed / all parts, timed jobs
             parts = sum(x["parts"] for x in xs)
             out["gpu_part_share"] = round(sum(x["gpu_parts"] for x in xs) / parts, 3) \

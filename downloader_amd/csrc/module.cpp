@@ -404,8 +404,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("relay_counters", []() {
     RelayCounters c = relay_counters();
     py::dict d;
-    const char* modes[3] = {"splice", "dup", "copy"};
-    for (int i = 0; i < 3; ++i) {
+    const char* modes[4] = {"splice", "dup", "copy", "hashed"};
+    for (int i = 0; i < 4; ++i) {
       d[(std::string(modes[i]) + "_relays").c_str()] = c.relays[i];
       d[(std::string(modes[i]) + "_bytes").c_str()] = c.bytes[i];
       d[(std::string(modes[i]) + "_cpu_ns").c_str()] = c.cpu_ns[i];
@@ -416,6 +416,7 @@ PYBIND11_MODULE(_native, m) {
     d["dup_copied_bytes"] = c.dup_bytes;
     d["crc_ns"] = c.crc_ns;
     d["crc_bytes"] = c.crc_bytes;
+    d["sha1_ns"] = c.sha1_ns;
     return d;
   }, "Per-phase relay counters since start (relay_body_to): relays / bytes / relaying-thread "
      "CPU per mode (splice, dup = peek|tee copy + CRC, copy), syscalls, copy and CRC time");

@@ -132,10 +132,11 @@ PipeStats pipe_stats();
 // 1 dup (recv(MSG_PEEK) or tee() copy + CRC, splice), 2 copy (recv + send: TLS, no pipe).
 // `cpu_ns` is the relaying thread's own CPU (CLOCK_THREAD_CPUTIME_ID around the call).
 struct RelayCounters {
-  uint64_t relays[3], bytes[3], cpu_ns[3];
+  uint64_t relays[4], bytes[4], cpu_ns[4];      // splice, dup, copy, hashed (torrent parts)
   uint64_t splice_in_calls, splice_out_calls;   // socket -> pipe, pipe -> socket (all modes)
   uint64_t dup_calls, dup_bytes;                // recv(MSG_PEEK) / read(tee) copies
   uint64_t crc_ns, crc_bytes;                   // CRC32C over the copied bytes
+  uint64_t sha1_ns;                             // host piece SHA-1 inside hashed relays
 };
 RelayCounters relay_counters();
 // Capacity asked for new pipes: the splice pipe, and the tee() duplicate pipe (0 = keep).

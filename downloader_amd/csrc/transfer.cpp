@@ -63,12 +63,14 @@ std::atomic<size_t> g_pipe_main{size_t(1) << 20}, g_pipe_tee{size_t(1) << 20};
 // folds it into the process-wide atomics once per relay.
 struct RelayTally {
   uint64_t splice_in = 0, splice_out = 0, dup_calls = 0, dup_bytes = 0, crc_ns = 0, crc_bytes = 0;
+  uint64_t sha1_ns = 0;   // host piece SHA-1 inside hashed relays
 };
 thread_local RelayTally t_tally;
+// modes: 0 splice, 1 dup (peek / tee copy + CRC), 2 copy, 3 hashed (piece-hashed torrent part)
 struct {
-  std::atomic<uint64_t> relays[3], bytes[3], cpu_ns[3];
+  std::atomic<uint64_t> relays[4], bytes[4], cpu_ns[4];
   std::atomic<uint64_t> splice_in{0}, splice_out{0}, dup_calls{0}, dup_bytes{0}, crc_ns{0},
-      crc_bytes{0};
+      crc_bytes{0}, sha1_ns{0};
 } g_rc;
 
 uint64_t thread_cpu_ns() {
@@ -101,6 +103,7 @@ struct RelayScope {
     g_rc.dup_bytes.fetch_add(t.dup_bytes - t0.dup_bytes, std::memory_order_relaxed);
     g_rc.crc_ns.fetch_add(t.crc_ns - t0.crc_ns, std::memory_order_relaxed);
     g_rc.crc_bytes.fetch_add(t.crc_bytes - t0.crc_bytes, std::memory_order_relaxed);
+    g_rc.sha1_ns.fetch_add(t.sha1_ns - t0.sha1_ns, std::memory_order_relaxed);
   }
 };
 std::atomic<uint64_t> g_pipes_created{0}, g_pipes_short{0};
@@ -1198,6 +1201,9 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
                                     uint64_t* gpu_ticket) {
   if (skip < 0 || full_len < 0 || skip + full_len > n || piece_len <= 0)
     throw IoError("relay_body_hashed: bad piece split");
+  int64_t scoped = n;               // (counted as moved: a failed relay throws past it)
+  RelayScope scope(&scoped);
+  scope.mode = 3;
   const int64_t npieces = (full_len + piece_len - 1) / piece_len;
   if (npieces >= 8 && n <= kMaxBufferedPart && sha1_mb_supported())
     return relay_body_hashed_mb(dst, n, skip, full_len, piece_len, prog, digests, head, tail, crc,
@@ -1241,8 +1247,12 @@ int64_t HttpConn::relay_body_hashed(HttpConn& dst, int64_t n, int64_t skip, int6
             return buf.data();
           },
           [&](const uint8_t* p, size_t k) {
+            uint64_t t0 = mono_ns();
             if (crc) *crc = stager::crc32c(p, k, *crc);
+            uint64_t t1 = mono_ns();
             consume(p, (int64_t)k);
+            t_tally.crc_ns += t1 - t0;
+            t_tally.sha1_ns += mono_ns() - t1;
           }) >= 0)
     return pos;
   while (pos < n) {
@@ -1511,7 +1521,13 @@ void gpu_signal(uint64_t id) {   // g_gpu_mu held
   }
 }
 
+void host_digests_impl(const uint8_t* p, int64_t full_len, int64_t piece_len, std::string* out);
 void host_digests(const uint8_t* p, int64_t full_len, int64_t piece_len, std::string* out) {
+  const uint64_t t0 = mono_ns();
+  host_digests_impl(p, full_len, piece_len, out);
+  t_tally.sha1_ns += mono_ns() - t0;
+}
+void host_digests_impl(const uint8_t* p, int64_t full_len, int64_t piece_len, std::string* out) {
   const int64_t np = (full_len + piece_len - 1) / piece_len;
   std::vector<const uint8_t*> ptrs((size_t)np);
   std::vector<size_t> lens((size_t)np);
@@ -1865,7 +1881,7 @@ PipeStats pipe_stats() { return pipe_pool().stats(); }
 
 RelayCounters relay_counters() {
   RelayCounters c{};
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i) {
     c.relays[i] = g_rc.relays[i].load();
     c.bytes[i] = g_rc.bytes[i].load();
     c.cpu_ns[i] = g_rc.cpu_ns[i].load();
@@ -1876,6 +1892,7 @@ RelayCounters relay_counters() {
   c.dup_bytes = g_rc.dup_bytes.load();
   c.crc_ns = g_rc.crc_ns.load();
   c.crc_bytes = g_rc.crc_bytes.load();
+  c.sha1_ns = g_rc.sha1_ns.load();
   return c;
 }
 void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
@@ -1910,7 +1927,11 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
           return b + pos;
         },
         [&](const uint8_t* p, size_t k) {
-          if (crc) *crc = stager::crc32c(p, k, *crc);
+          if (crc) {
+            uint64_t t0 = mono_ns();
+            *crc = stager::crc32c(p, k, *crc);
+            t_tally.crc_ns += mono_ns() - t0;
+          }
           pos += (int64_t)k;
         });
   }
