@@ -668,13 +668,15 @@ class StreamStager:
                     sum(len(b) for b in got.values()) != hi - lo:
                 return False
             ver = self.frag_ver.get(p, 0)
-            data = b"".join(got[a] for a in sorted(got))
+            # the fragments in order, hashed where they lie (joining them first copied every
+            # boundary piece once more on the event loop: ~0.05 CPU-s/GB of a 50-file torrent)
+            frags = [got[a] for a in sorted(got)]
             self._checking.add(p)
             try:
-                if len(data) >= 1 << 20:
-                    digest = await asyncio.get_running_loop().run_in_executor(None, _sha1, data)
+                if hi - lo >= 1 << 20:
+                    digest = await asyncio.get_running_loop().run_in_executor(None, _sha1v, frags)
                 else:
-                    digest = _sha1(data)
+                    digest = _sha1v(frags)
             finally:
                 self._checking.discard(p)
             if self.frag_ver.get(p, 0) != ver:
@@ -702,6 +704,15 @@ class StreamStager:
 
 def _sha1(b: bytes) -> bytes:
     return hashlib.sha1(b).digest()
+
+
+def _sha1v(parts) -> bytes:
+    """SHA-1 of the concatenation of ``parts`` without building it (hashlib drops the GIL on
+    large updates)."""
+    h = hashlib.sha1()
+    for b in parts:
+        h.update(b)
+    return h.digest()
 
 
 def _gpu_relay_on(cfg) -> Optional[str]:

@@ -258,12 +258,12 @@ def test_check_piece_discards_stale_verdict(run, tmp_path, monkeypatch):
     a, b = st.units
     assert st.suppliers[1] == {a.uid, b.uid}
     gate, entered = threading.Event(), threading.Event()
-    real = stream_mod._sha1
+    real = stream_mod._sha1v
 
-    def slow_sha1(buf):
+    def slow_sha1(parts):
         entered.set()
         gate.wait(10)
-        return real(buf)
+        return real(parts)
 
     async def go():
         q = asyncio.Queue()
@@ -272,14 +272,14 @@ def test_check_piece_discards_stale_verdict(run, tmp_path, monkeypatch):
         st.frags[1][plen] = data[plen:half]                 # a's tail
         st.frags[1][half] = data[half:2 * plen]             # b's head
         st.frag_ver[1] = 2
-        monkeypatch.setattr(stream_mod, "_sha1", slow_sha1)
+        monkeypatch.setattr(stream_mod, "_sha1v", slow_sha1)
         chk = asyncio.ensure_future(st._check_piece(1))
         while not entered.is_set():
             await asyncio.sleep(0.005)
         st._settle(b, [b], q)                               # b's fragment dropped mid-hash
         gate.set()
         assert await chk is False and 1 not in st.verified
-        monkeypatch.setattr(stream_mod, "_sha1", real)
+        monkeypatch.setattr(stream_mod, "_sha1v", real)
         bad = bytearray(data[half:2 * plen])
         bad[7] ^= 0xFF
         st.frags[1][half] = bytes(bad)                      # the re-fetch brings bad bytes
