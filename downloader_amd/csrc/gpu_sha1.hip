@@ -318,6 +318,220 @@ __global__ __launch_bounds__(256) void sha1_lanes(const uint8_t* __restrict__ da
   store_digest(out + (int64_t)i * 20, hv);
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-wave variant of sha1_lanes: the same batch, but every piece is hashed by TWO waves.
+//
+// One lane of one wave is a serial chain of ~618 VALU ops per 64-byte block, and a wave alone
+// on its SIMD issues one wave64 VALU op per 4 cycles (MI355X_MICROARCH.md, 'vector-instruction
+// ISSUE cost'), so a 4 MiB piece takes ~65k blocks x ~2,500 cycles = 68 ms at 2.4 GHz however
+// idle the rest of the device is. In the PartHasher and the swarm that per-piece LATENCY - not
+// the device's throughput - is what lands on the end of a job. ~200
+// of those ops per block are the message schedule (W[16..79] = rotl1 of four older words) and
+// 16 the byte swaps; neither depends on the hash state. So a workgroup here is two waves on
+// different SIMDs (a workgroup's waves are dealt to SIMDs 0 -> 2 -> 1 -> 3) for the same 64
+// pieces:
+//   * wave 0, the producer, loads block k (dwordx4, one block ahead in registers), swaps it,
+//     expands the 80-word schedule and writes it to an LDS ring slot (20 ds_write_b128 per
+//     lane: lane l's 16-byte group g at ((slot * 20 + g) * 64 + l) - conflict-free);
+//   * wave 1, the consumer, reads block k - 1's 80 words back (20 ds_read_b128) and runs only
+//     the 80 rounds: Ch / parity / majority (v_bfi / v_bitop3), rotl5, rotl30 and the adds
+//     (K folds into an add3) - ~5 ops per round instead of ~8;
+//   * one s_barrier per block: the producer writes slot k % 2 while the consumer reads slot
+//     (k - 1) % 2. The producer's ~230 ops per block are well under the consumer's ~420, so the
+//     consumer never waits for the schedule.
+// Lanes of one workgroup may have different lengths: both waves step through the workgroup's
+// longest lane (every wave reaches every barrier), lanes past their own end idle.
+constexpr size_t kArenaPad = 256;             // bytes readable past a split launch's data
+constexpr int kSplitGroups = 20;              // 80 schedule words = 20 x uint4 per lane per block
+constexpr uint32_t kSplitSlots = 3;           // LDS ring: blocks k (written), k - 1 (read), k - 2
+
+__device__ __forceinline__ void split_produce(uint32_t w[16], uint4* __restrict__ slot) {
+  // slot already points at this lane's column: group g is slot[g * 64]
+#pragma unroll
+  for (int g = 0; g < 4; ++g) slot[g * 64] = make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]);
+#pragma unroll
+  for (int t = 16; t < 80; ++t) {
+    w[t & 15] = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+    if ((t & 3) == 3)
+      slot[(t >> 2) * 64] = make_uint4(w[(t - 3) & 15], w[(t - 2) & 15], w[(t - 1) & 15], w[t & 15]);
+  }
+}
+
+__device__ __forceinline__ uint32_t split_word(const uint4 g[kSplitGroups], int t) {
+  const uint4 v = g[t >> 2];
+  return (t & 3) == 0 ? v.x : (t & 3) == 1 ? v.y : (t & 3) == 2 ? v.z : v.w;
+}
+
+#define SHA1_SPLIT_ROUND(F, K)                                            \
+  {                                                                       \
+    uint32_t tmp = rotl(a, 5) + (F) + (e + (K) + split_word(g, t));       \
+    e = d;                                                                \
+    d = c;                                                                \
+    c = rotl(b, 30);                                                      \
+    b = a;                                                                \
+    a = tmp;                                                              \
+  }
+
+__device__ __forceinline__ void split_read(const uint4* __restrict__ slot, uint4 g[kSplitGroups]) {
+#pragma unroll
+  for (int k = 0; k < kSplitGroups; ++k) g[k] = slot[k * 64];
+}
+
+__device__ __forceinline__ void split_rounds(Sha1State& s, const uint4 g[kSplitGroups]) {
+  uint32_t a = s.h0, b = s.h1, c = s.h2, d = s.h3, e = s.h4;
+#pragma unroll
+  for (int t = 0; t < 80; ++t) {
+    if (t < 20) {
+      SHA1_SPLIT_ROUND((b & c) | (~b & d), 0x5A827999u);
+    } else if (t < 40) {
+      SHA1_SPLIT_ROUND(xor3(b, c, d), 0x6ED9EBA1u);
+    } else if (t < 60) {
+      SHA1_SPLIT_ROUND(maj(b, c, d), 0x8F1BBCDCu);
+    } else {
+      SHA1_SPLIT_ROUND(xor3(b, c, d), 0xCA62C1D6u);
+    }
+  }
+  s.h0 += a;
+  s.h1 += b;
+  s.h2 += c;
+  s.h3 += d;
+  s.h4 += e;
+}
+
+// The last one or two blocks of a lane from the 64 raw bytes at its tail (rem < 64 of them
+// belong to the piece): those bytes, 0x80, zero fill, and the bit length in the last block;
+// `second` = the all-zero block that follows when rem >= 56.
+__device__ __forceinline__ void tail_words(const uint4 v[4], int rem, bool last, bool second,
+                                           uint64_t bits, uint32_t w[16]) {
+  to_words(v, w);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = rem - 4 * i;                     // piece bytes left at word i
+    const uint32_t keep = r >= 4 ? 0xFFFFFFFFu : r <= 0 ? 0u : 0xFFFFFFFFu << (32 - 8 * r);
+    const uint32_t pad = (r >= 0 && r < 4) ? 0x80u << (24 - 8 * r) : 0u;
+    w[i] = second ? 0u : ((w[i] & keep) | pad);
+  }
+  if (last) {
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+  }
+}
+
+// Workgroup barrier that waits for this wave's LDS traffic only: __syncthreads() also drains
+// vmcnt, i.e. the producer's prefetch loads, which then had just its own ~240 ops per step to
+// land instead of the consumer's ~420 (measured: no gain over sha1_lanes with it).
+// The wait is the builtin (lgkmcnt(0), vmcnt / expcnt left at their maxima: 0xC07F on gfx9)
+// so the compiler's own wait insertion knows every LDS access before it is done - inside an
+// asm string it did not, and waited again for the consumer's NEXT block's reads before its
+// first round. The asm keeps the compiler from moving LDS accesses across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("s_barrier" ::: "memory");
+}
+
+// Lane i of the batch = (lane_off[i], lane_len[i]) in the arena, 16-byte aligned; 128-thread
+// workgroups (grid = ceil(n / 64)). VAR (kernel bench attribution only, digests meaningless
+// unless 0): 1 = the producer skips its LDS writes (times the rounds wave with the barriers),
+// 2 = the consumer skips its rounds (times the schedule wave with the barriers), 3 = the
+// consumer hashes each block right after reading it (no register prefetch).
+template <int VAR>
+__global__ __launch_bounds__(128) void sha1_lanes_split_v(const uint8_t* __restrict__ data,
+                                                        const int64_t* __restrict__ lane_off,
+                                                        const int64_t* __restrict__ lane_len,
+                                                        int n, uint8_t* __restrict__ out) {
+  __shared__ uint4 ring[kSplitSlots * kSplitGroups * 64];    // 60 KiB: three blocks' schedules
+  __shared__ uint32_t longest;
+  const int lane = threadIdx.x & 63;
+  const bool producer = threadIdx.x < 64;          // wave-uniform
+  const int i = blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  const int64_t len = live ? lane_len[i] : 0;
+  const uint32_t nfull = (uint32_t)(len >> 6);
+  const int rem = (int)(len & 63);
+  const int ntail = rem >= 56 ? 2 : 1;
+  const uint32_t nblk = live ? nfull + (uint32_t)ntail : 0u;
+  if (threadIdx.x == 0) longest = 0;
+  __syncthreads();
+  if (producer) atomicMax(&longest, nblk);
+  __syncthreads();
+  const uint32_t M = longest;                      // blocks of the workgroup's longest lane
+  // slot j of the ring, this lane's column (plain arithmetic on `ring`: an array of slot
+  // pointers made them generic pointers - flat_load / flat_store, waited for with vmcnt too)
+  auto col = [&](uint32_t j) { return ring + j * (kSplitGroups * 64) + lane; };
+  // Steps 0 .. M + 1 on both waves, one barrier each. Step k: the producer writes block k into
+  // slot k % 3; the consumer reads block k - 1 (slot (k - 1) % 3, published by the previous
+  // barrier) into registers and runs the rounds of block k - 2 from the registers it filled
+  // the step before - so its LDS reads overlap its rounds instead of stalling them.
+  if (producer) {
+    // Global loads run three blocks ahead in three register buffers with fixed roles
+    // (unrolled by 3, so the slot of each position is fixed too); the barrier waits for LDS
+    // only, so a load in flight stays in flight across it.
+    const uint8_t* p = data + (live ? lane_off[i] : 0);
+    const uint64_t bits = (uint64_t)len * 8ull;
+    const uint32_t last = nblk - 1;
+    uint4 b0[4], b1[4], b2[4];
+    uint32_t w[16];
+    // every load is unconditional (block index clamped to the tail block, which is read as 64
+    // raw bytes - the arena has a pad past its end), so the compiler counts them: the use of
+    // block k waits with vmcnt(8) for its own loads only, issued three steps earlier
+    auto at = [&](uint32_t k) { return p + ((int64_t)(k < nfull ? k : nfull) << 6); };
+    load_raw16(at(0), b0);
+    load_raw16(at(1), b1);
+    load_raw16(at(2), b2);
+    auto step = [&](uint32_t k, uint4 (&buf)[4], uint32_t slot) {
+      if (k < nblk) {
+        if (k < nfull) to_words(buf, w);
+        else tail_words(buf, rem, k == last, k > nfull, bits, w);
+        if constexpr (VAR != 1) split_produce(w, col(slot));
+      }
+      asm volatile("" ::: "memory");     // the refill below stays behind this block's use
+      load_raw16(at(k + 3), buf);
+      lds_barrier();
+    };
+    // whole triples in the loop (no conditional step inside it: every path round the back
+    // edge has issued the same loads, so the compiler's wait for block k stays counted), the
+    // 0 - 2 steps left after it
+    const uint32_t steps = M + 2;
+    uint32_t k = 0;
+    for (; k + 3 <= steps; k += 3) {
+      step(k, b0, 0);
+      step(k + 1, b1, 1);
+      step(k + 2, b2, 2);
+    }
+    if (k < steps) step(k, b0, 0);
+    if (k + 1 < steps) step(k + 1, b1, 1);
+  } else {
+    Sha1State s{0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    uint4 ga[kSplitGroups], gb[kSplitGroups];
+    auto step = [&](uint32_t k, uint4 (&fill)[kSplitGroups], const uint4 (&use)[kSplitGroups]) {
+      if constexpr (VAR == 3) {           // no register prefetch: read block k - 1, hash it
+        if (k >= 1 && k - 1 < nblk) {
+          split_read(col((k - 1) % kSplitSlots), fill);
+          split_rounds(s, fill);
+        }
+      } else {
+        if (k >= 1 && k - 1 < nblk) split_read(col((k - 1) % kSplitSlots), fill);
+        if (VAR != 2 && k >= 2 && k - 2 < nblk) split_rounds(s, use);
+        if (VAR == 2 && k >= 2 && k - 2 < nblk) s.h0 ^= use[0].x ^ use[19].w;
+      }
+      lds_barrier();
+    };
+    const uint32_t steps = M + 2;
+    uint32_t k = 0;
+    for (; k + 2 <= steps; k += 2) {
+      step(k, ga, gb);
+      step(k + 1, gb, ga);
+    }
+    if (k < steps) step(k, ga, gb);
+    if (live) {
+      const uint32_t hv[5] = {s.h0, s.h1, s.h2, s.h3, s.h4};
+      store_digest(out + (int64_t)i * 20, hv);
+    }
+  }
+}
+
+#define sha1_lanes_split sha1_lanes_split_v<0>
+
 // Chunk-streamed variant: lane k owns piece (first + k) of a window - or, with a piece list,
 // piece lane_piece[first + k] - and advances it by one CH-byte chunk per launch; the SHA-1
 // state lives in `state` between launches. The chunk of lane k sits at data + k * CH. On the
@@ -387,6 +601,20 @@ __global__ __launch_bounds__(256) void sha1_chunk(uint32_t* __restrict__ state,
     good = good && (e == hv[q]);
   }
   ok[gi] = good ? 1 : 0;
+}
+
+// Pseudo-random device fill (kernel benches: distinct pieces without a host copy).
+__global__ __launch_bounds__(256) void fill_mix(uint4* __restrict__ p, int64_t n16, uint32_t seed) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n16;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)j * 0x9E3779B1u ^ (uint32_t)(j >> 32) ^ seed;
+    uint4 v;
+    x ^= x >> 15; x *= 0x2C1B3C6Du; x ^= x >> 12; v.x = x;
+    x *= 0x297A2D39u; x ^= x >> 15; v.y = x;
+    x *= 0x2C1B3C6Du; x ^= x >> 12; v.z = x;
+    x *= 0x297A2D39u; x ^= x >> 15; v.w = x;
+    p[j] = v;
+  }
 }
 
 void launch(hipStream_t st, const uint8_t* d_data, int64_t piece_len, int64_t last_len, int n,
@@ -713,6 +941,65 @@ class GpuVerifier {
     return {t[0] / iters, t[1] / iters};
   }
 
+  // Kernel-only A/B of the PartHasher kernels on one lane table (device-resident, distinct
+  // pseudo-random pieces): ms per launch of sha1_lanes_split and sha1_lanes<16>, interleaved,
+  // and whether their digests agree. Lane i hashes piece_len - (i * 37) % 131 bytes at
+  // i * piece_len, so the lanes of a workgroup end at different blocks and every tail shape
+  // (rem < 56: one padding block, >= 56: two) comes up.
+  std::vector<double> kernel_bench_split(int64_t piece_len, int n_pieces, int iters,
+                                         int variant) {
+    HIP_CHECK(hipSetDevice(device_));
+    const size_t bytes = (size_t)piece_len * (size_t)n_pieces;
+    DevMem<uint8_t> data_buf(bytes + kArenaPad), out_a((size_t)n_pieces * 20),
+        out_b((size_t)n_pieces * 20);
+    DevMem<int64_t> tab((size_t)n_pieces * 2);
+    std::vector<int64_t> h((size_t)n_pieces * 2);
+    for (int i = 0; i < n_pieces; ++i) {
+      h[(size_t)i] = (int64_t)i * piece_len;
+      h[(size_t)n_pieces + i] = std::max<int64_t>(0, piece_len - (int64_t)((i * 37) % 131));
+    }
+    HIP_CHECK(hipMemcpy(tab.p, h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_mix, dim3(2048), dim3(256), 0, stream_[0],
+                       reinterpret_cast<uint4*>(data_buf.p), (int64_t)(bytes / 16), 0x51u);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemsetAsync(out_a.p, 0, (size_t)n_pieces * 20, stream_[0]));
+    HIP_CHECK(hipMemsetAsync(out_b.p, 0xff, (size_t)n_pieces * 20, stream_[0]));
+    DevEvent ev0(hipEventDefault), ev1(hipEventDefault);
+    hipEvent_t e0 = ev0.e, e1 = ev1.e;
+    const int grid = (n_pieces + 63) / 64;
+    double t[2] = {0, 0};
+    for (int it = 0; it < iters + 1; ++it) {
+      for (int v = 0; v < 2; ++v) {
+        HIP_CHECK(hipEventRecord(e0, stream_[0]));
+        if (v == 0 && variant == 1)
+          hipLaunchKernelGGL(sha1_lanes_split_v<1>, dim3(grid), dim3(128), 0, stream_[0],
+                             data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
+        else if (v == 0 && variant == 2)
+          hipLaunchKernelGGL(sha1_lanes_split_v<2>, dim3(grid), dim3(128), 0, stream_[0],
+                             data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
+        else if (v == 0 && variant == 3)
+          hipLaunchKernelGGL(sha1_lanes_split_v<3>, dim3(grid), dim3(128), 0, stream_[0],
+                             data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
+        else if (v == 0)
+          hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(128), 0, stream_[0], data_buf.p,
+                             tab.p, tab.p + n_pieces, n_pieces, out_a.p);
+        else
+          hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(64), 0, stream_[0], data_buf.p,
+                             tab.p, tab.p + n_pieces, n_pieces, out_b.p);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(e1, stream_[0]));
+        HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (it > 0) t[v] += ms;
+      }
+    }
+    std::vector<uint8_t> a((size_t)n_pieces * 20), b((size_t)n_pieces * 20);
+    HIP_CHECK(hipMemcpy(a.data(), out_a.p, a.size(), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(b.data(), out_b.p, b.size(), hipMemcpyDeviceToHost));
+    return {t[0] / iters, t[1] / iters, a == b ? 1.0 : 0.0};
+  }
+
   // Kernel-only timing (device-resident data, hipEvents): ms per launch hashing `n_pieces`
   // pieces of `piece_len` bytes; `bitop3` selects the v_bitop3 or the plain-C round forms
   // so both variants are A/B-timed interleaved in one process.
@@ -881,12 +1168,19 @@ class HipPartDevice {
   HipPartDevice(const HipPartDevice&) = delete;
   HipPartDevice& operator=(const HipPartDevice&) = delete;
 
+  static bool split_default() {
+    const char* e = getenv("STAGER_SHA1_KERNEL");
+    return !(e && std::string(e) == "lanes");
+  }
+
   static int hw_queues() {
     const char* e = getenv("GPU_MAX_HW_QUEUES");
     const int n = e ? atoi(e) : 0;
     return n > 0 ? n : 4;            // HIP's default
   }
 
+  // sha1_lanes_split (two waves per 64 pieces) unless STAGER_SHA1_KERNEL=lanes (A/B)
+  bool split() const { return split_; }
   int copy_streams() const { return (int)copies_.size(); }
   int compute_streams() const { return (int)streams_.size(); }
   int slots() const { return (int)slots_.size(); }
@@ -938,7 +1232,10 @@ class HipPartDevice {
     const int64_t* dp = r.d_tab;
     const int64_t* dl = r.d_tab + total;
     const int block = 64, grid = (total + block - 1) / block;
-    if (align16)
+    if (align16 && split_)
+      hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(2 * block), 0, st, arena_, dp, dl,
+                         total, r.d_dig);
+    else if (align16)
       hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, arena_, dp, dl, total,
                          r.d_dig);
     else
@@ -999,7 +1296,9 @@ class HipPartDevice {
     for (auto& st : streams_) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     slots_.resize((size_t)slots);
     // one arena, a window per slot: lane offsets from its base keep the kernel's loads global
-    HIP_CHECK(hipMalloc((void**)&arena_, (size_t)slot_bytes_ * (size_t)slots));
+    // + a pad: sha1_lanes_split reads a lane's tail block as 64 raw bytes, which may run past
+    // the last slot's end
+    HIP_CHECK(hipMalloc((void**)&arena_, (size_t)slot_bytes_ * (size_t)slots + kArenaPad));
     for (size_t k = 0; k < slots_.size(); ++k) {
       Slot& sl = slots_[k];
       sl.d_data = arena_ + (size_t)slot_bytes_ * k;
@@ -1068,6 +1367,7 @@ class HipPartDevice {
   int device_;
   int64_t slot_bytes_;
   int max_lanes_;
+  bool split_ = split_default();
   int64_t launch_lanes_ = 0;
   uint8_t* arena_ = nullptr;     // slots x slot_bytes of HBM
   std::vector<hipStream_t> copies_;
@@ -1095,6 +1395,7 @@ py::dict part_stats(PartHasher& h) {
   d["register_s"] = s.register_s;
   d["copy_streams"] = s.copy_streams;
   d["compute_streams"] = s.compute_streams;
+  d["kernel"] = h.device().split() ? "sha1_lanes_split" : "sha1_lanes";
   return d;
 }
 
@@ -1206,6 +1507,24 @@ PYBIND11_MODULE(_gpuhash, m) {
           },
           py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 5,
           "(ms_prefetch, ms_no_prefetch): kernel time per launch, device-resident data")
+      .def(
+          "kernel_bench_split",
+          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters, int variant) {
+            if (piece_len < 256 || piece_len % 16 || n_pieces <= 0 || iters <= 0 ||
+                variant < 0 || variant > 3)
+              throw std::invalid_argument("piece_len must be a multiple of 16, >= 256");
+            std::vector<double> r;
+            {
+              py::gil_scoped_release rel;
+              r = g.kernel_bench_split(piece_len, n_pieces, iters, variant);
+            }
+            return py::make_tuple(r[0], r[1], r[2] != 0.0);
+          },
+          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 3,
+          py::arg("variant") = 0,
+          "(ms_split, ms_lanes, digests_equal): the PartHasher's two kernels on one lane table "
+          "(variant 1 / 2: the split kernel without its LDS writes / rounds, for attribution; "
+          "3: without the consumer's register prefetch)")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
   py::class_<PartHasher>(m, "PartHasher")
       .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes,
