@@ -319,42 +319,55 @@ __global__ __launch_bounds__(256) void sha1_lanes(const uint8_t* __restrict__ da
 }
 
 // ---------------------------------------------------------------------------------------
-// Split-wave variant of sha1_lanes: the same batch, but every piece is hashed by TWO waves.
+// Split-wave variant of sha1_lanes: the same batch, every 64 pieces hashed by THREE waves.
 //
 // One lane of one wave is a serial chain of ~618 VALU ops per 64-byte block, and a wave alone
-// on its SIMD issues one wave64 VALU op per 4 cycles (MI355X_MICROARCH.md, 'vector-instruction
-// ISSUE cost'), so a 4 MiB piece takes ~65k blocks x ~2,500 cycles = 68 ms at 2.4 GHz however
-// idle the rest of the device is. In the PartHasher and the swarm that per-piece LATENCY - not
-// the device's throughput - is what lands on the end of a job. ~200
-// of those ops per block are the message schedule (W[16..79] = rotl1 of four older words) and
-// 16 the byte swaps; neither depends on the hash state. So a workgroup here is two waves on
-// different SIMDs (a workgroup's waves are dealt to SIMDs 0 -> 2 -> 1 -> 3) for the same 64
-// pieces:
-//   * wave 0, the producer, loads block k (dwordx4, one block ahead in registers), swaps it,
-//     expands the 80-word schedule and writes it to an LDS ring slot (20 ds_write_b128 per
-//     lane: lane l's 16-byte group g at ((slot * 20 + g) * 64 + l) - conflict-free);
-//   * wave 1, the consumer, reads block k - 1's 80 words back (20 ds_read_b128) and runs only
-//     the 80 rounds: Ch / parity / majority (v_bfi / v_bitop3), rotl5, rotl30 and the adds
-//     (K folds into an add3) - ~5 ops per round instead of ~8;
-//   * one s_barrier per block: the producer writes slot k % 2 while the consumer reads slot
-//     (k - 1) % 2. The producer's ~230 ops per block are well under the consumer's ~420, so the
-//     consumer never waits for the schedule.
-// Lanes of one workgroup may have different lengths: both waves step through the workgroup's
+// on its SIMD issues one wave64 VALU op per ~4 cycles (MI355X_MICROARCH.md, 'vector-instruction
+// ISSUE cost'), so a 4 MiB piece takes 65,536 blocks x ~2,650 cycles = 73 ms however idle the
+// rest of the device is. In the PartHasher and the swarm that per-piece LATENCY - not the
+// device's throughput - is what lands on the end of a job. ~210 of
+// those ops per block are the message schedule (W[16..79] = rotl1 of four older words) and the
+// byte swaps, which do not depend on the hash state. So a workgroup here is three waves on
+// three SIMDs (a workgroup's waves are dealt to SIMDs 0 -> 2 -> 1 -> 3) for the same 64 pieces:
+//   * waves 0 and 1, the producers, take the even / odd blocks: in its step a producer swaps
+//     its block (dwordx4 loads issued two steps ahead), expands the 80-word schedule and, at
+//     the end of the step, writes it to an LDS slot (20 ds_write_b128 per lane: lane l's
+//     16-byte group g at ((slot * 20 + g) * 64 + l) - conflict-free); then it idles a step.
+//     One producer doing that in every step took ~1,560 cycles per block alone (timed with
+//     the rounds taken out: the 20 wide LDS stores of one wave cost ~26 cycles each on top of
+//     its ~300 VALU ops) - as long as the rounds, so that pair was no faster than either;
+//   * wave 2, the consumer, reads block k + 1's 80 words (20 ds_read_b128) while it runs only
+//     the 80 rounds of block k: Ch / parity / majority (v_bitop3), rotl5, rotl30 and two add3
+//     (K folds in) - 5 ops per round instead of ~7.7;
+//   * one s_barrier per block.
+// Lanes of one workgroup may have different lengths: every wave steps through the workgroup's
 // longest lane (every wave reaches every barrier), lanes past their own end idle.
 constexpr size_t kArenaPad = 256;             // bytes readable past a split launch's data
 constexpr int kSplitGroups = 20;              // 80 schedule words = 20 x uint4 per lane per block
-constexpr uint32_t kSplitSlots = 3;           // LDS ring: blocks k (written), k - 1 (read), k - 2
+constexpr uint32_t kSplitSlots = 3;           // LDS ring: blocks k + 1 (read), k + 2 (written)
+constexpr int kSplitThreads = 192;            // two producer waves + one consumer wave
 
-__device__ __forceinline__ void split_produce(uint32_t w[16], uint4* __restrict__ slot) {
-  // slot already points at this lane's column: group g is slot[g * 64]
+// The 80-word schedule of one block from its 16 big-endian words.
+__device__ __forceinline__ void split_schedule(uint32_t w[16], uint4 g[kSplitGroups]) {
 #pragma unroll
-  for (int g = 0; g < 4; ++g) slot[g * 64] = make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]);
+  for (int q = 0; q < 4; ++q) g[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 #pragma unroll
   for (int t = 16; t < 80; ++t) {
     w[t & 15] = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
     if ((t & 3) == 3)
-      slot[(t >> 2) * 64] = make_uint4(w[(t - 3) & 15], w[(t - 2) & 15], w[(t - 1) & 15], w[t & 15]);
+      g[t >> 2] = make_uint4(w[(t - 3) & 15], w[(t - 2) & 15], w[(t - 1) & 15], w[t & 15]);
   }
+}
+
+// slot points at this lane's column of a ring slot: group q is slot[q * 64]
+__device__ __forceinline__ void split_write(const uint4 g[kSplitGroups], uint4* __restrict__ slot) {
+#pragma unroll
+  for (int q = 0; q < kSplitGroups; ++q) slot[q * 64] = g[q];
+}
+
+__device__ __forceinline__ void split_read(const uint4* __restrict__ slot, uint4 g[kSplitGroups]) {
+#pragma unroll
+  for (int q = 0; q < kSplitGroups; ++q) g[q] = slot[q * 64];
 }
 
 __device__ __forceinline__ uint32_t split_word(const uint4 g[kSplitGroups], int t) {
@@ -371,11 +384,6 @@ __device__ __forceinline__ uint32_t split_word(const uint4 g[kSplitGroups], int 
     b = a;                                                                \
     a = tmp;                                                              \
   }
-
-__device__ __forceinline__ void split_read(const uint4* __restrict__ slot, uint4 g[kSplitGroups]) {
-#pragma unroll
-  for (int k = 0; k < kSplitGroups; ++k) g[k] = slot[k * 64];
-}
 
 __device__ __forceinline__ void split_rounds(Sha1State& s, const uint4 g[kSplitGroups]) {
   uint32_t a = s.h0, b = s.h1, c = s.h2, d = s.h3, e = s.h4;
@@ -418,31 +426,30 @@ __device__ __forceinline__ void tail_words(const uint4 v[4], int rem, bool last,
 }
 
 // Workgroup barrier that waits for this wave's LDS traffic only: __syncthreads() also drains
-// vmcnt, i.e. the producer's prefetch loads, which then had just its own ~240 ops per step to
-// land instead of the consumer's ~420 (measured: no gain over sha1_lanes with it).
-// The wait is the builtin (lgkmcnt(0), vmcnt / expcnt left at their maxima: 0xC07F on gfx9)
-// so the compiler's own wait insertion knows every LDS access before it is done - inside an
-// asm string it did not, and waited again for the consumer's NEXT block's reads before its
-// first round. The asm keeps the compiler from moving LDS accesses across the barrier.
+// vmcnt, i.e. a producer's prefetch loads. The wait is the builtin (lgkmcnt(0), vmcnt / expcnt
+// left at their maxima: 0xC07F on gfx9) so the compiler's own wait insertion knows every LDS
+// access before it is done - inside an asm string it did not, and waited again at the next
+// uses. The asm keeps the compiler from moving LDS accesses across the barrier.
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);
   asm volatile("s_barrier" ::: "memory");
 }
 
-// Lane i of the batch = (lane_off[i], lane_len[i]) in the arena, 16-byte aligned; 128-thread
-// workgroups (grid = ceil(n / 64)). VAR (kernel bench attribution only, digests meaningless
-// unless 0): 1 = the producer skips its LDS writes (times the rounds wave with the barriers),
-// 2 = the consumer skips its rounds (times the schedule wave with the barriers), 3 = the
-// consumer hashes each block right after reading it (no register prefetch).
-template <int VAR>
-__global__ __launch_bounds__(128) void sha1_lanes_split_v(const uint8_t* __restrict__ data,
+// Lane i of the batch = (lane_off[i], lane_len[i]) in the arena, 16-byte aligned; 192-thread
+// workgroups (grid = ceil(n / 64)). Alternatives timed against this one in one process
+// (kernel bench, 4 MiB pieces, 64 / 1,024 lanes; profiles/r6/split/kernel_knobs.jsonl): a
+// producer that schedules in one step and writes in the next 60.9 - 61.2 ms, the consumer's
+// next-block reads spread through its rounds (one per 4 rounds, pinned by sched_barrier)
+// 60.7 - 60.9, both 60.8 - 61.5, the consumer at s_setprio 3 64.7 - 65.1, against 52.8 - 53.4
+// here and 73.2 - 73.5 for sha1_lanes<16>.
+__global__ __launch_bounds__(192) void sha1_lanes_split(const uint8_t* __restrict__ data,
                                                         const int64_t* __restrict__ lane_off,
                                                         const int64_t* __restrict__ lane_len,
                                                         int n, uint8_t* __restrict__ out) {
   __shared__ uint4 ring[kSplitSlots * kSplitGroups * 64];    // 60 KiB: three blocks' schedules
   __shared__ uint32_t longest;
   const int lane = threadIdx.x & 63;
-  const bool producer = threadIdx.x < 64;          // wave-uniform
+  const int wave = threadIdx.x >> 6;               // 0, 1: producers (even / odd blocks); 2
   const int i = blockIdx.x * 64 + lane;
   const bool live = i < n;
   const int64_t len = live ? lane_len[i] : 0;
@@ -452,85 +459,97 @@ __global__ __launch_bounds__(128) void sha1_lanes_split_v(const uint8_t* __restr
   const uint32_t nblk = live ? nfull + (uint32_t)ntail : 0u;
   if (threadIdx.x == 0) longest = 0;
   __syncthreads();
-  if (producer) atomicMax(&longest, nblk);
+  if (wave == 0) atomicMax(&longest, nblk);
   __syncthreads();
   const uint32_t M = longest;                      // blocks of the workgroup's longest lane
-  // slot j of the ring, this lane's column (plain arithmetic on `ring`: an array of slot
-  // pointers made them generic pointers - flat_load / flat_store, waited for with vmcnt too)
+  // this lane's column of slot j (plain arithmetic on `ring`: an array of slot pointers made
+  // them generic pointers - flat_load / flat_store, waited for with vmcnt too)
   auto col = [&](uint32_t j) { return ring + j * (kSplitGroups * 64) + lane; };
-  // Steps 0 .. M + 1 on both waves, one barrier each. Step k: the producer writes block k into
-  // slot k % 3; the consumer reads block k - 1 (slot (k - 1) % 3, published by the previous
-  // barrier) into registers and runs the rounds of block k - 2 from the registers it filled
-  // the step before - so its LDS reads overlap its rounds instead of stalling them.
-  if (producer) {
-    // Global loads run three blocks ahead in three register buffers with fixed roles
-    // (unrolled by 3, so the slot of each position is fixed too); the barrier waits for LDS
-    // only, so a load in flight stays in flight across it.
-    const uint8_t* p = data + (live ? lane_off[i] : 0);
+  // Two prologue steps, then steps k = 0 .. M - 1, one barrier each. Step k: the consumer hashes block k from registers (read in the step before) while its
+  // reads of block k + 1 (slot (k + 1) % 3) are in flight - their latency, and their queueing
+  // behind the stores, off its critical path. Producer k % 2 swaps, schedules and writes block
+  // k + 2 into slot (k + 2) % 3 (free: block k is in the consumer's registers) - the stores at
+  // the end of its step, after the consumer's reads - and idles in the next step.
+  if (wave < 2) {
+    const uint32_t p = (uint32_t)wave;
+    const uint8_t* src = data + (live ? lane_off[i] : 0);
     const uint64_t bits = (uint64_t)len * 8ull;
     const uint32_t last = nblk - 1;
-    uint4 b0[4], b1[4], b2[4];
+    // every load is unconditional (block index clamped to the tail block, read as 64 raw
+    // bytes - the arena has a pad past its end), so the compiler's wait counts stay exact
+    auto at = [&](uint32_t b) { return src + ((int64_t)(b < nfull ? b : nfull) << 6); };
+    uint4 raw[4], g[kSplitGroups];
     uint32_t w[16];
-    // every load is unconditional (block index clamped to the tail block, which is read as 64
-    // raw bytes - the arena has a pad past its end), so the compiler counts them: the use of
-    // block k waits with vmcnt(8) for its own loads only, issued three steps earlier
-    auto at = [&](uint32_t k) { return p + ((int64_t)(k < nfull ? k : nfull) << 6); };
-    load_raw16(at(0), b0);
-    load_raw16(at(1), b1);
-    load_raw16(at(2), b2);
-    auto step = [&](uint32_t k, uint4 (&buf)[4], uint32_t slot) {
-      if (k < nblk) {
-        if (k < nfull) to_words(buf, w);
-        else tail_words(buf, rem, k == last, k > nfull, bits, w);
-        if constexpr (VAR != 1) split_produce(w, col(slot));
+    auto compute = [&](uint32_t b) {             // raw holds block b: schedule it into g
+      if (b < nblk) {
+        if (b < nfull) to_words(raw, w);
+        else tail_words(raw, rem, b == last, b > nfull, bits, w);
       }
-      asm volatile("" ::: "memory");     // the refill below stays behind this block's use
-      load_raw16(at(k + 3), buf);
-      lds_barrier();
+      asm volatile("" ::: "memory");             // the refill below stays behind this use
+      load_raw16(at(b + 2), raw);                // this producer's next block, 2 steps ahead
+      if (b < nblk) split_schedule(w, g);
     };
-    // whole triples in the loop (no conditional step inside it: every path round the back
-    // edge has issued the same loads, so the compiler's wait for block k stays counted), the
-    // 0 - 2 steps left after it
-    const uint32_t steps = M + 2;
+    auto write = [&](uint32_t b) {
+      if (b < nblk) split_write(g, col(b % kSplitSlots));
+    };
+    // Roles fixed per wave and whole step pairs inside the loops: `raw` and `g` then stay in
+    // the same registers round the back edge - a phi between two register sets made the
+    // compiler copy `raw` right after issuing its loads, i.e. wait for them.
+    load_raw16(at(p), raw);
     uint32_t k = 0;
-    for (; k + 3 <= steps; k += 3) {
-      step(k, b0, 0);
-      step(k + 1, b1, 1);
-      step(k + 2, b2, 2);
+    if (p == 0) {
+      compute(0);
+      write(0);
+      lds_barrier();                           // prologue step -2
+      lds_barrier();                           // prologue step -1: idle
+      for (; k + 2 <= M; k += 2) {
+        compute(k + 2);
+        write(k + 2);
+        lds_barrier();                         // step k
+        lds_barrier();                         // step k + 1: idle
+      }
+      if (k < M) {
+        compute(k + 2);
+        write(k + 2);
+        lds_barrier();
+      }
+    } else {
+      lds_barrier();                           // prologue step -2: idle
+      compute(1);
+      write(1);
+      lds_barrier();                           // prologue step -1
+      for (; k + 2 <= M; k += 2) {
+        lds_barrier();                         // step k: idle
+        compute(k + 3);
+        write(k + 3);
+        lds_barrier();                         // step k + 1
+      }
+      if (k < M) lds_barrier();
     }
-    if (k < steps) step(k, b0, 0);
-    if (k + 1 < steps) step(k + 1, b1, 1);
   } else {
     Sha1State s{0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
     uint4 ga[kSplitGroups], gb[kSplitGroups];
+    // fixed roles per step of a pair (no register copies): fill one, hash the other
     auto step = [&](uint32_t k, uint4 (&fill)[kSplitGroups], const uint4 (&use)[kSplitGroups]) {
-      if constexpr (VAR == 3) {           // no register prefetch: read block k - 1, hash it
-        if (k >= 1 && k - 1 < nblk) {
-          split_read(col((k - 1) % kSplitSlots), fill);
-          split_rounds(s, fill);
-        }
-      } else {
-        if (k >= 1 && k - 1 < nblk) split_read(col((k - 1) % kSplitSlots), fill);
-        if (VAR != 2 && k >= 2 && k - 2 < nblk) split_rounds(s, use);
-        if (VAR == 2 && k >= 2 && k - 2 < nblk) s.h0 ^= use[0].x ^ use[19].w;
-      }
+      if (k + 1 < nblk) split_read(col((k + 1) % kSplitSlots), fill);
+      if (k < nblk) split_rounds(s, use);
       lds_barrier();
     };
-    const uint32_t steps = M + 2;
+    lds_barrier();                               // prologue step -2
+    if (0 < nblk) split_read(col(0), gb);
+    lds_barrier();                               // prologue step -1
     uint32_t k = 0;
-    for (; k + 2 <= steps; k += 2) {
+    for (; k + 2 <= M; k += 2) {
       step(k, ga, gb);
       step(k + 1, gb, ga);
     }
-    if (k < steps) step(k, ga, gb);
+    if (k < M) step(k, ga, gb);
     if (live) {
       const uint32_t hv[5] = {s.h0, s.h1, s.h2, s.h3, s.h4};
       store_digest(out + (int64_t)i * 20, hv);
     }
   }
 }
-
-#define sha1_lanes_split sha1_lanes_split_v<0>
 
 // Chunk-streamed variant: lane k owns piece (first + k) of a window - or, with a piece list,
 // piece lane_piece[first + k] - and advances it by one CH-byte chunk per launch; the SHA-1
@@ -946,8 +965,7 @@ class GpuVerifier {
   // and whether their digests agree. Lane i hashes piece_len - (i * 37) % 131 bytes at
   // i * piece_len, so the lanes of a workgroup end at different blocks and every tail shape
   // (rem < 56: one padding block, >= 56: two) comes up.
-  std::vector<double> kernel_bench_split(int64_t piece_len, int n_pieces, int iters,
-                                         int variant) {
+  std::vector<double> kernel_bench_split(int64_t piece_len, int n_pieces, int iters) {
     HIP_CHECK(hipSetDevice(device_));
     const size_t bytes = (size_t)piece_len * (size_t)n_pieces;
     DevMem<uint8_t> data_buf(bytes + kArenaPad), out_a((size_t)n_pieces * 20),
@@ -971,18 +989,9 @@ class GpuVerifier {
     for (int it = 0; it < iters + 1; ++it) {
       for (int v = 0; v < 2; ++v) {
         HIP_CHECK(hipEventRecord(e0, stream_[0]));
-        if (v == 0 && variant == 1)
-          hipLaunchKernelGGL(sha1_lanes_split_v<1>, dim3(grid), dim3(128), 0, stream_[0],
+        if (v == 0)
+          hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(kSplitThreads), 0, stream_[0],
                              data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
-        else if (v == 0 && variant == 2)
-          hipLaunchKernelGGL(sha1_lanes_split_v<2>, dim3(grid), dim3(128), 0, stream_[0],
-                             data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
-        else if (v == 0 && variant == 3)
-          hipLaunchKernelGGL(sha1_lanes_split_v<3>, dim3(grid), dim3(128), 0, stream_[0],
-                             data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
-        else if (v == 0)
-          hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(128), 0, stream_[0], data_buf.p,
-                             tab.p, tab.p + n_pieces, n_pieces, out_a.p);
         else
           hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(64), 0, stream_[0], data_buf.p,
                              tab.p, tab.p + n_pieces, n_pieces, out_b.p);
@@ -1233,8 +1242,8 @@ class HipPartDevice {
     const int64_t* dl = r.d_tab + total;
     const int block = 64, grid = (total + block - 1) / block;
     if (align16 && split_)
-      hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(2 * block), 0, st, arena_, dp, dl,
-                         total, r.d_dig);
+      hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(kSplitThreads), 0, st, arena_, dp,
+                         dl, total, r.d_dig);
     else if (align16)
       hipLaunchKernelGGL(sha1_lanes<16>, dim3(grid), dim3(block), 0, st, arena_, dp, dl, total,
                          r.d_dig);
@@ -1509,22 +1518,18 @@ PYBIND11_MODULE(_gpuhash, m) {
           "(ms_prefetch, ms_no_prefetch): kernel time per launch, device-resident data")
       .def(
           "kernel_bench_split",
-          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters, int variant) {
-            if (piece_len < 256 || piece_len % 16 || n_pieces <= 0 || iters <= 0 ||
-                variant < 0 || variant > 3)
+          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters) {
+            if (piece_len < 256 || piece_len % 16 || n_pieces <= 0 || iters <= 0)
               throw std::invalid_argument("piece_len must be a multiple of 16, >= 256");
             std::vector<double> r;
             {
               py::gil_scoped_release rel;
-              r = g.kernel_bench_split(piece_len, n_pieces, iters, variant);
+              r = g.kernel_bench_split(piece_len, n_pieces, iters);
             }
             return py::make_tuple(r[0], r[1], r[2] != 0.0);
           },
           py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 3,
-          py::arg("variant") = 0,
-          "(ms_split, ms_lanes, digests_equal): the PartHasher's two kernels on one lane table "
-          "(variant 1 / 2: the split kernel without its LDS writes / rounds, for attribution; "
-          "3: without the consumer's register prefetch)")
+          "(ms_split, ms_lanes, digests_equal): the PartHasher's two kernels on one lane table")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
   py::class_<PartHasher>(m, "PartHasher")
       .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes,

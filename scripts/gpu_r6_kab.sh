@@ -13,9 +13,9 @@ import json
 from downloader_amd.ops import gpuhash
 gv = gpuhash().GpuVerifier(0, 64 << 20, 8)
 for plen, lanes in ((65536 + 48, 200), (4 << 20, 64), (4 << 20, 1024)):
-    for var in (0, 1, 2, 3):
-        s, l, same = gv.kernel_bench_split(plen, lanes, 2, var)
-        print(json.dumps({"piece_len": plen, "lanes": lanes, "variant": var, "ms_split": round(s, 2),
+    for rep in (0, 1):
+        s, l, same = gv.kernel_bench_split(plen, lanes, 2)
+        print(json.dumps({"piece_len": plen, "lanes": lanes, "rep": rep, "ms_split": round(s, 2),
                           "ms_lanes": round(l, 2), "speedup": round(l / s, 3), "same": same}), flush=True)
 PY
 cat $F/kernel_ab.jsonl

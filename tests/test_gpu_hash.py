@@ -228,13 +228,14 @@ def test_part_hasher_matches_hashlib(part_hasher, piece, n):
 
 
 def test_split_kernel_matches_lanes_kernel_and_is_faster(gv):
-    """sha1_lanes_split (schedule wave + rounds wave per 64 pieces) against sha1_lanes<16> on
+    """sha1_lanes_split (two schedule waves + a rounds wave per 64 pieces) vs sha1_lanes<16> on
     one lane table whose lanes end at different blocks and with every tail shape: identical
-    digests, and a 4 MiB piece's latency cut (~618 -> ~410 VALU ops per block on the chain)."""
+    digests, and a 4 MiB piece's latency cut (~618 -> ~410 VALU ops per block on its chain:
+    73 -> 53 ms measured, profiles/r6/split/)."""
     ms_s, ms_l, same = gv.kernel_bench_split(65536 + 48, 200, 1)
     assert same, (ms_s, ms_l)
     ms_s, ms_l, same = gv.kernel_bench_split(4 << 20, 128, 2)
-    assert same and ms_l / ms_s > 1.15, (ms_s, ms_l)
+    assert same and ms_l / ms_s > 1.25, (ms_s, ms_l)
     with pytest.raises(ValueError):
         gv.kernel_bench_split(1000, 16, 1)
 
