@@ -42,7 +42,17 @@ def summarise(path: str) -> Dict[str, dict]:
                 busy += e - s
                 last = e
         wall = (spans[-1][1] - spans[0][0]) if spans else 0
-        out[k] = {"launches": len(rs), "ms_mean": round(statistics.mean(dur), 3),
+        # launches that ran alone vs beside another one of the same kernel (any overlap)
+        iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rs]
+        alone = [not any(s1 < e0 and s0 < e1 for m, (s1, e1) in enumerate(iv) if m != j)
+                 for j, (s0, e0) in enumerate(iv)]
+        solo = [d for d, a in zip(dur, alone) if a]
+        both = [d for d, a in zip(dur, alone) if not a]
+        extra = {"ms_median": round(statistics.median(dur), 3),
+                 "solo_launches": len(solo),
+                 "ms_solo_mean": round(statistics.mean(solo), 3) if solo else None,
+                 "ms_overlapped_mean": round(statistics.mean(both), 3) if both else None}
+        out[k] = {"launches": len(rs), "ms_mean": round(statistics.mean(dur), 3), **extra,
                   "ms_min": round(min(dur), 3), "ms_max": round(max(dur), 3),
                   "ms_total": round(sum(dur), 1),
                   "grid_threads_mean": round(statistics.mean(grid), 1),

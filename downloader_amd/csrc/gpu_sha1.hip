@@ -344,8 +344,15 @@ __global__ __launch_bounds__(256) void sha1_lanes(const uint8_t* __restrict__ da
 // longest lane (every wave reaches every barrier), lanes past their own end idle.
 constexpr size_t kArenaPad = 256;             // bytes readable past a split launch's data
 constexpr int kSplitGroups = 20;              // 80 schedule words = 20 x uint4 per lane per block
-constexpr uint32_t kSplitSlots = 3;           // LDS ring: blocks k + 1 (read), k + 2 (written)
+// LDS ring: blocks k + 1 (read) and k + 2 (written) of step k, and spare slots. 4 slots = 80 KiB
+// (+ 4 bytes) of LDS per workgroup, so at most ONE workgroup fits a CU (160 KiB): the
+// PartHasher's two compute streams run launches side by side, and with 60 KiB two of their
+// workgroups could land on one CU, their 6 waves on its 4 SIMDs (rocprofv3: 52.7 - 106 ms per
+// launch, 68.7 mean, vs 52.8 - 53.4 alone). 256 workgroups = 16,384 lanes still fit at once.
+constexpr uint32_t kSplitSlots = 4;
 constexpr int kSplitThreads = 192;            // two producer waves + one consumer wave
+static_assert(2 * (kSplitSlots * kSplitGroups * 64 * 16 + 4) > 160 * 1024,
+              "sha1_lanes_split must not fit twice on one CU");
 
 // The 80-word schedule of one block from its 16 big-endian words.
 __device__ __forceinline__ void split_schedule(uint32_t w[16], uint4 g[kSplitGroups]) {
@@ -442,21 +449,25 @@ __device__ __forceinline__ void lds_barrier() {
 // next-block reads spread through its rounds (one per 4 rounds, pinned by sched_barrier)
 // 60.7 - 60.9, both 60.8 - 61.5, the consumer at s_setprio 3 64.7 - 65.1, against 52.8 - 53.4
 // here and 73.2 - 73.5 for sha1_lanes<16>.
-__global__ __launch_bounds__(192) void sha1_lanes_split(const uint8_t* __restrict__ data,
-                                                        const int64_t* __restrict__ lane_off,
-                                                        const int64_t* __restrict__ lane_len,
-                                                        int n, uint8_t* __restrict__ out) {
-  __shared__ uint4 ring[kSplitSlots * kSplitGroups * 64];    // 60 KiB: three blocks' schedules
+template <bool DUP>
+__global__ __launch_bounds__(192) void sha1_lanes_split_t(const uint8_t* __restrict__ data,
+                                                          const int64_t* __restrict__ lane_off,
+                                                          const int64_t* __restrict__ lane_len,
+                                                          int n, uint8_t* __restrict__ out) {
+  __shared__ uint4 ring[kSplitSlots * kSplitGroups * 64];    // 80 KiB: four blocks' schedules
   __shared__ uint32_t longest;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;               // 0, 1: producers (even / odd blocks); 2
-  const int i = blockIdx.x * 64 + lane;
-  const bool live = i < n;
-  const int64_t len = live ? lane_len[i] : 0;
+  const int i0 = blockIdx.x * 64 + lane;
+  const bool live = i0 < n;
+  // DUP: a lane past n hashes a live lane's piece again (its digest is not stored)
+  const int i = DUP && !live ? blockIdx.x * 64 + lane % (n - (int)blockIdx.x * 64) : i0;
+  const bool work = DUP || live;
+  const int64_t len = work ? lane_len[i] : 0;
   const uint32_t nfull = (uint32_t)(len >> 6);
   const int rem = (int)(len & 63);
   const int ntail = rem >= 56 ? 2 : 1;
-  const uint32_t nblk = live ? nfull + (uint32_t)ntail : 0u;
+  const uint32_t nblk = work ? nfull + (uint32_t)ntail : 0u;
   if (threadIdx.x == 0) longest = 0;
   __syncthreads();
   if (wave == 0) atomicMax(&longest, nblk);
@@ -466,13 +477,13 @@ __global__ __launch_bounds__(192) void sha1_lanes_split(const uint8_t* __restric
   // them generic pointers - flat_load / flat_store, waited for with vmcnt too)
   auto col = [&](uint32_t j) { return ring + j * (kSplitGroups * 64) + lane; };
   // Two prologue steps, then steps k = 0 .. M - 1, one barrier each. Step k: the consumer hashes block k from registers (read in the step before) while its
-  // reads of block k + 1 (slot (k + 1) % 3) are in flight - their latency, and their queueing
+  // reads of block k + 1 (slot (k + 1) % 4) are in flight - their latency, and their queueing
   // behind the stores, off its critical path. Producer k % 2 swaps, schedules and writes block
-  // k + 2 into slot (k + 2) % 3 (free: block k is in the consumer's registers) - the stores at
+  // k + 2 into slot (k + 2) % 4 (free: block k is in the consumer's registers) - the stores at
   // the end of its step, after the consumer's reads - and idles in the next step.
   if (wave < 2) {
     const uint32_t p = (uint32_t)wave;
-    const uint8_t* src = data + (live ? lane_off[i] : 0);
+    const uint8_t* src = data + (work ? lane_off[i] : 0);
     const uint64_t bits = (uint64_t)len * 8ull;
     const uint32_t last = nblk - 1;
     // every load is unconditional (block index clamped to the tail block, read as 64 raw
@@ -550,6 +561,8 @@ __global__ __launch_bounds__(192) void sha1_lanes_split(const uint8_t* __restric
     }
   }
 }
+
+#define sha1_lanes_split sha1_lanes_split_t<false>
 
 // Chunk-streamed variant: lane k owns piece (first + k) of a window - or, with a piece list,
 // piece lane_piece[first + k] - and advances it by one CH-byte chunk per launch; the SHA-1
@@ -965,7 +978,8 @@ class GpuVerifier {
   // and whether their digests agree. Lane i hashes piece_len - (i * 37) % 131 bytes at
   // i * piece_len, so the lanes of a workgroup end at different blocks and every tail shape
   // (rem < 56: one padding block, >= 56: two) comes up.
-  std::vector<double> kernel_bench_split(int64_t piece_len, int n_pieces, int iters) {
+  std::vector<double> kernel_bench_split(int64_t piece_len, int n_pieces, int iters,
+                                         bool dup) {
     HIP_CHECK(hipSetDevice(device_));
     const size_t bytes = (size_t)piece_len * (size_t)n_pieces;
     DevMem<uint8_t> data_buf(bytes + kArenaPad), out_a((size_t)n_pieces * 20),
@@ -989,7 +1003,10 @@ class GpuVerifier {
     for (int it = 0; it < iters + 1; ++it) {
       for (int v = 0; v < 2; ++v) {
         HIP_CHECK(hipEventRecord(e0, stream_[0]));
-        if (v == 0)
+        if (v == 0 && dup)
+          hipLaunchKernelGGL(sha1_lanes_split_t<true>, dim3(grid), dim3(kSplitThreads), 0,
+                             stream_[0], data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
+        else if (v == 0)
           hipLaunchKernelGGL(sha1_lanes_split, dim3(grid), dim3(kSplitThreads), 0, stream_[0],
                              data_buf.p, tab.p, tab.p + n_pieces, n_pieces, out_a.p);
         else
@@ -1007,6 +1024,78 @@ class GpuVerifier {
     HIP_CHECK(hipMemcpy(a.data(), out_a.p, a.size(), hipMemcpyDeviceToHost));
     HIP_CHECK(hipMemcpy(b.data(), out_b.p, b.size(), hipMemcpyDeviceToHost));
     return {t[0] / iters, t[1] / iters, a == b ? 1.0 : 0.0};
+  }
+
+  // Two sha1_lanes_split launches at once on the two streams (as the PartHasher's compute
+  // streams run them), n0 and n1 lanes, against the first alone: (ms alone, ms stream 0, ms
+  // stream 1), means over `iters` rounds. mode 1: stream 1 copies 48 x 64 MiB host -> device
+  // (pinned) instead of its launch, as the PartHasher's copy streams do; mode 2: 40 ms of
+  // device idleness before each launch.
+  std::vector<double> kernel_bench_concurrent(int64_t piece_len, int n0, int n1, int iters,
+                                              int mode) {
+    HIP_CHECK(hipSetDevice(device_));
+    const int n = n0 + n1;
+    const size_t bytes = (size_t)piece_len * (size_t)n;
+    DevMem<uint8_t> data_buf(bytes + kArenaPad), out((size_t)n * 20);
+    DevMem<int64_t> tab((size_t)n * 2);
+    std::vector<int64_t> h((size_t)n * 2);
+    // launch s's table: offsets then lengths, at tab + (s ? 2 * n0 : 0)
+    for (int s = 0, base = 0; s < 2; base += s ? 0 : n0, ++s) {
+      const int m = s ? n1 : n0;
+      int64_t* t = h.data() + (s ? 2 * n0 : 0);
+      for (int i = 0; i < m; ++i) {
+        t[i] = ((int64_t)(s ? n0 : 0) + i) * piece_len;
+        t[m + i] = piece_len;
+      }
+    }
+    HIP_CHECK(hipMemcpy(tab.p, h.data(), h.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_mix, dim3(2048), dim3(256), 0, stream_[0],
+                       reinterpret_cast<uint4*>(data_buf.p), (int64_t)(bytes / 16), 0x77u);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(stream_[0]));
+    DevEvent a0(hipEventDefault), a1(hipEventDefault), b0(hipEventDefault), b1(hipEventDefault);
+    auto go = [&](int s, hipEvent_t e0, hipEvent_t e1) {
+      const int m = s ? n1 : n0;
+      const int64_t* t = tab.p + (s ? 2 * n0 : 0);
+      HIP_CHECK(hipEventRecord(e0, stream_[s]));
+      if (m > 0)
+        hipLaunchKernelGGL(sha1_lanes_split, dim3((m + 63) / 64), dim3(kSplitThreads), 0,
+                           stream_[s], data_buf.p, t, t + m, m,
+                           out.p + (size_t)(s ? n0 : 0) * 20);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipEventRecord(e1, stream_[s]));
+    };
+    const size_t cp = (size_t)64 << 20;
+    uint8_t* hpin = nullptr;
+    DevMem<uint8_t> dcp(mode == 1 ? cp : 0);
+    if (mode == 1) HIP_CHECK(hipHostMalloc((void**)&hpin, cp, hipHostMallocDefault));
+    double t[3] = {0, 0, 0};
+    for (int it = 0; it < iters + 1; ++it) {
+      if (mode == 2) std::this_thread::sleep_for(std::chrono::milliseconds(40));
+      go(0, a0.e, a1.e);
+      HIP_CHECK(hipEventSynchronize(a1.e));
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, a0.e, a1.e));
+      if (it > 0) t[0] += ms;
+      if (mode == 2) std::this_thread::sleep_for(std::chrono::milliseconds(40));
+      go(0, a0.e, a1.e);
+      if (mode == 1) {
+        HIP_CHECK(hipEventRecord(b0.e, stream_[1]));
+        for (int c = 0; c < 48; ++c)
+          HIP_CHECK(hipMemcpyAsync(dcp.p, hpin, cp, hipMemcpyHostToDevice, stream_[1]));
+        HIP_CHECK(hipEventRecord(b1.e, stream_[1]));
+      } else {
+        go(1, b0.e, b1.e);
+      }
+      HIP_CHECK(hipEventSynchronize(a1.e));
+      HIP_CHECK(hipEventSynchronize(b1.e));
+      HIP_CHECK(hipEventElapsedTime(&ms, a0.e, a1.e));
+      if (it > 0) t[1] += ms;
+      HIP_CHECK(hipEventElapsedTime(&ms, b0.e, b1.e));
+      if (it > 0) t[2] += ms;
+    }
+    if (hpin) hipHostFree(hpin);
+    return {t[0] / iters, t[1] / iters, t[2] / iters};
   }
 
   // Kernel-only timing (device-resident data, hipEvents): ms per launch hashing `n_pieces`
@@ -1517,18 +1606,36 @@ PYBIND11_MODULE(_gpuhash, m) {
           py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 5,
           "(ms_prefetch, ms_no_prefetch): kernel time per launch, device-resident data")
       .def(
+          "kernel_bench_concurrent",
+          [](GpuVerifier& g, int64_t piece_len, int n0, int n1, int iters, int mode) {
+            if (piece_len < 256 || piece_len % 16 || n0 <= 0 || n1 < 0 || iters <= 0 ||
+                mode < 0 || mode > 2)
+              throw std::invalid_argument("piece_len must be a multiple of 16, >= 256");
+            std::vector<double> r;
+            {
+              py::gil_scoped_release rel;
+              r = g.kernel_bench_concurrent(piece_len, n0, n1, iters, mode);
+            }
+            return py::make_tuple(r[0], r[1], r[2]);
+          },
+          py::arg("piece_len"), py::arg("n0"), py::arg("n1"), py::arg("iters") = 3,
+          py::arg("mode") = 0,
+          "(ms alone, ms on stream 0, ms on stream 1): sha1_lanes_split launches of n0 and n1 "
+          "lanes side by side (mode 0), n0 beside 48 x 64 MiB H2D copies (1), after 40 ms idle "
+          "(2)")
+      .def(
           "kernel_bench_split",
-          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters) {
+          [](GpuVerifier& g, int64_t piece_len, int n_pieces, int iters, bool dup) {
             if (piece_len < 256 || piece_len % 16 || n_pieces <= 0 || iters <= 0)
               throw std::invalid_argument("piece_len must be a multiple of 16, >= 256");
             std::vector<double> r;
             {
               py::gil_scoped_release rel;
-              r = g.kernel_bench_split(piece_len, n_pieces, iters);
+              r = g.kernel_bench_split(piece_len, n_pieces, iters, dup);
             }
             return py::make_tuple(r[0], r[1], r[2] != 0.0);
           },
-          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 3,
+          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 3, py::arg("dup") = false,
           "(ms_split, ms_lanes, digests_equal): the PartHasher's two kernels on one lane table")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
   py::class_<PartHasher>(m, "PartHasher")
