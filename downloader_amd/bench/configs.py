@@ -506,7 +506,8 @@ async def config_swarm(a) -> Dict:
         if getattr(a, "swarm_pool_mb", 0):
             extra["wire_pool_mb"] = a.swarm_pool_mb
         if getattr(a, "swarm_gpu_tail_mb", None) is not None:
-            extra["swarm_gpu_tail_bytes"] = a.swarm_gpu_tail_mb << 20
+            mb = a.swarm_gpu_tail_mb
+            extra["swarm_gpu_tail_bytes"] = mb << 20 if mb >= 0 else -1
         leech = await TorrentClient(max_peers=64, pipeline=a.pipeline, native_wire=wire,
                                     swarm_verify=verify, wire_requests=native_req,
                                     **extra).start()
@@ -547,7 +548,10 @@ async def config_swarm(a) -> Dict:
                "leech_cpu_s_per_GB": round(cpu_s / (total / 1e9), 3),
                "leech_thread_cpu": per_thread,
                "reps": len(runs), "MBps_reps": [round(total / r[0] / MB, 1) for r in runs],
-               "leech_cpu_s_per_GB_reps": [round(r[1] / (total / 1e9), 3) for r in runs]}
+               "leech_cpu_s_per_GB_reps": [round(r[1] / (total / 1e9), 3) for r in runs],
+               # GPU mode: bytes left to start when the rest went to the host (auto tail)
+               "gpu_host_tail_bytes_reps": [r[4].stats.get("gpu_host_tail_bytes", 0)
+                                            for r in runs]}
         await leech.close()
         return out
     finally:

@@ -460,7 +460,13 @@ __global__ __launch_bounds__(192) void sha1_lanes_split_t(const uint8_t* __restr
   const int wave = threadIdx.x >> 6;               // 0, 1: producers (even / odd blocks); 2
   const int i0 = blockIdx.x * 64 + lane;
   const bool live = i0 < n;
-  // DUP: a lane past n hashes a live lane's piece again (its digest is not stored)
+  // DUP: a lane past n hashes a live lane's piece again (its digest is not stored), so every
+  // lane of every wave is busy. A launch whose waves were partly empty took far longer - 1 /
+  // 8 / 16 / 32 live lanes of 64: 86 / 81 / 77 / 59 ms per 4 MiB piece, 80 lanes 74 ms (its
+  // second workgroup holds 16), against 57 ms for 48 / 64 and for every one of those counts
+  // with DUP (sha1_lanes, whose idle lanes exit: 82 - 88 vs 73 ms; profiles/r6/split/
+  // small_launch_dup.jsonl). In the PartHasher a launch is often one part (16 lanes), so its
+  // launches took 57 - 104 ms, 71 mean, where the kernel bench said 57.
   const int i = DUP && !live ? blockIdx.x * 64 + lane % (n - (int)blockIdx.x * 64) : i0;
   const bool work = DUP || live;
   const int64_t len = work ? lane_len[i] : 0;
@@ -562,7 +568,7 @@ __global__ __launch_bounds__(192) void sha1_lanes_split_t(const uint8_t* __restr
   }
 }
 
-#define sha1_lanes_split sha1_lanes_split_t<false>
+#define sha1_lanes_split sha1_lanes_split_t<true>
 
 // Chunk-streamed variant: lane k owns piece (first + k) of a window - or, with a piece list,
 // piece lane_piece[first + k] - and advances it by one CH-byte chunk per launch; the SHA-1
@@ -1635,8 +1641,9 @@ PYBIND11_MODULE(_gpuhash, m) {
             }
             return py::make_tuple(r[0], r[1], r[2] != 0.0);
           },
-          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 3, py::arg("dup") = false,
-          "(ms_split, ms_lanes, digests_equal): the PartHasher's two kernels on one lane table")
+          py::arg("piece_len"), py::arg("n_pieces"), py::arg("iters") = 3, py::arg("dup") = true,
+          "(ms_split, ms_lanes, digests_equal): the PartHasher's two kernels on one lane table "
+          "(dup=False: the split kernel with its idle lanes left idle)")
       .def_property_readonly("batch_bytes", &GpuVerifier::batch_bytes);
   py::class_<PartHasher>(m, "PartHasher")
       .def(py::init([](int device, int64_t slot_bytes, int slots, int streams, int max_lanes,

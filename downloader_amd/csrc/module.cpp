@@ -316,6 +316,9 @@ PYBIND11_MODULE(_native, m) {
            "True while complete, unreported pieces hold the cap or more (start no new piece)")
       .def("set_host_tail", &SwarmWire::set_host_tail, py::arg("on"),
            "GPU mode: hash the pieces completing from now on on the host (the download's end)")
+      .def("rx_total", &SwarmWire::rx_total, "bytes received on every connection so far")
+      .def("gpu_latency", &SwarmWire::gpu_latency,
+           "GPU mode: submission -> digest time of the device's pieces (EWMA, s; 0 = none yet)")
       .def("set_gpu", &SwarmWire::set_gpu, py::arg("on"), py::arg("max_inflight") = 64,
            "Verify complete pieces on the installed GPU part hasher (set_gpu_part_hasher), at "
            "most max_inflight at once (the rest on the host)")
@@ -389,6 +392,9 @@ PYBIND11_MODULE(_native, m) {
              d["gpu_refused"] = s.gpu_refused;
              d["gpu_errors"] = s.gpu_errors;
              d["gpu_overflow"] = s.gpu_overflow;    // hashed on the host: device full
+             d["gpu_latency_ms_mean"] =
+                 s.gpu_pieces ? s.gpu_latency_ns_sum / 1e6 / (double)s.gpu_pieces : 0.0;
+             d["gpu_latency_ms_max"] = s.gpu_latency_ns_max / 1e6;
              d["backlog_bytes"] = s.backlog_bytes;
              d["pool_in_use"] = s.pool_in_use;      // process-wide piece buffers
              d["pool_idle"] = s.pool_idle;

@@ -228,6 +228,7 @@ struct SwarmWireStats {
   uint64_t assigned = 0, requests = 0;                      // owned pieces, REQUESTs the wire sent
   uint64_t gpu_pieces = 0, gpu_refused = 0, gpu_errors = 0; // pieces SHA-1'd on the GPU hasher
   uint64_t gpu_overflow = 0;        // hashed on the host: max_inflight pieces on the device
+  int64_t gpu_latency_ns_sum = 0, gpu_latency_ns_max = 0;   // submission -> digest, device pieces
   int64_t backlog_bytes = 0;        // complete pieces not yet reported
   size_t pool_in_use = 0, pool_idle = 0, pool_idle_bytes = 0;   // process-wide piece buffers
   uint64_t pool_allocs = 0, pool_frees = 0, pool_locks = 0; // since start: buffers made /
@@ -278,6 +279,10 @@ class SwarmWire {
   // GPU mode, the end of the download: pieces completing from now on are hashed on the host
   // (the last ~100 ms of download would otherwise wait out the device's per-piece latency).
   void set_host_tail(bool on);
+  // GPU mode: a piece's time from its submission to its digest on the device (EWMA, seconds;
+  // 0 before the first one) - the session sizes the host-hashed tail of the download by it
+  double gpu_latency() const { return gpu_lat_ewma_ns_.load() / 1e9; }
+  uint64_t rx_total() const { return rx_bytes_.load(std::memory_order_relaxed); }
   // Back-pressure: complete pieces not yet reported (verifying, on the device, waiting for the
   // writer) hold their buffers. backlogged() is true at `bytes` or more (Python then starts no
   // new piece); when half has drained since, NEED arrives on conn 0 (refill every connection).
@@ -340,7 +345,13 @@ class SwarmWire {
   std::atomic<bool> backlog_full_{false};
   std::mutex gmu_;
   std::condition_variable gcv_;
-  std::deque<std::pair<std::shared_ptr<Piece>, uint64_t>> gq_;   // submitted, in order
+  struct GpuJob {
+    std::shared_ptr<Piece> piece;
+    uint64_t ticket;
+    int64_t submit_ns;
+  };
+  std::deque<GpuJob> gq_;                       // submitted, in order
+  std::atomic<int64_t> gpu_lat_ewma_ns_{0};
   bool gstop_ = false;
   std::vector<std::thread> gthreads_;
   std::mutex smu_;

@@ -677,7 +677,7 @@ void SwarmWire::verify_loop() {
       if (t) {
         gpu_inflight_.fetch_add(1);
         std::lock_guard<std::mutex> g(gmu_);
-        gq_.push_back({std::move(p), t});
+        gq_.push_back({std::move(p), t, now_ns()});
         gcv_.notify_one();
       } else {
         if (api) {
@@ -720,7 +720,7 @@ void SwarmWire::verify_loop() {
 // device hashes them in parallel anyway), so results come back in about submission order.
 void SwarmWire::gpu_loop() {
   for (;;) {
-    std::pair<std::shared_ptr<Piece>, uint64_t> job;
+    GpuJob job;
     {
       std::unique_lock<std::mutex> lk(gmu_);
       gcv_.wait(lk, [&] { return gstop_ || !gq_.empty(); });
@@ -728,22 +728,27 @@ void SwarmWire::gpu_loop() {
       job = std::move(gq_.front());
       gq_.pop_front();
     }
-    Piece& p = *job.first;
+    Piece& p = *job.piece;
     const GpuPartHashApi* api = (const GpuPartHashApi*)p.reg;
     uint8_t dig[20];
     char err[256] = {0};
-    if (api->wait(api->ctx, job.second, GPU_PART_DONE, dig, sizeof dig, err, sizeof err) != 0) {
+    if (api->wait(api->ctx, job.ticket, GPU_PART_DONE, dig, sizeof dig, err, sizeof err) != 0) {
       // the device failed: the bytes are still in the buffer - hash them here
       std::string d = digest("sha1", p.data, p.size);
       memcpy(dig, d.data(), 20);
       std::lock_guard<std::mutex> g(mu_);
       stats_.gpu_errors++;
     } else {
+      const int64_t lat = now_ns() - job.submit_ns;
+      const int64_t prev = gpu_lat_ewma_ns_.load();
+      gpu_lat_ewma_ns_.store(prev ? (prev * 7 + lat) / 8 : lat);
       std::lock_guard<std::mutex> g(mu_);
       stats_.gpu_pieces++;
+      stats_.gpu_latency_ns_sum += lat;
+      stats_.gpu_latency_ns_max = std::max(stats_.gpu_latency_ns_max, lat);
     }
     gpu_inflight_.fetch_sub(1);
-    finish_piece(std::move(job.first), dig);
+    finish_piece(std::move(job.piece), dig);
   }
 }
 

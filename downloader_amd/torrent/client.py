@@ -36,7 +36,7 @@ class TorrentClient:
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
                  wire_pool_mb: int = 4096, wire_gpu_inflight: int = 1024,
-                 swarm_gpu_min_bytes: int = 8 << 30, swarm_gpu_tail_bytes: int = 0,
+                 swarm_gpu_min_bytes: int = 8 << 30, swarm_gpu_tail_bytes: int = -1,
                  swarm_backlog_bytes: int = 4 << 30, wire_io_threads: int = 4):
         from ..net.http import make_transports
         self._own_transports = transports is None
@@ -72,7 +72,8 @@ class TorrentClient:
         self.wire_requests = wire_requests
         self.wire_gpu_inflight = wire_gpu_inflight   # device-verified pieces at once (GPU mode)
         self.swarm_gpu_min_bytes = swarm_gpu_min_bytes   # `auto`: device from this size up
-        self.swarm_gpu_tail_bytes = swarm_gpu_tail_bytes # GPU mode: the last bytes on the host
+        # GPU mode: the last bytes on the host (-1: sized by the measured device latency)
+        self.swarm_gpu_tail_bytes = swarm_gpu_tail_bytes
         self.swarm_backlog_bytes = swarm_backlog_bytes   # complete, unverified pieces at most
         if native_wire:
             try:
@@ -109,7 +110,8 @@ class TorrentClient:
                    wire_pool_mb=membudget.swarm_bytes(d.swarm_pool_mb) >> 20,
                    wire_gpu_inflight=d.swarm_gpu_inflight,
                    swarm_gpu_min_bytes=int(d.swarm_gpu_min_gb * (1 << 30)),
-                   swarm_gpu_tail_bytes=d.swarm_gpu_tail_mb << 20,
+                   swarm_gpu_tail_bytes=(d.swarm_gpu_tail_mb << 20) if d.swarm_gpu_tail_mb >= 0
+                   else -1,
                    swarm_backlog_bytes=membudget.swarm_bytes(d.swarm_backlog_mb),
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 

@@ -483,6 +483,9 @@ class TorrentSession:
         # _tail_bytes are left to start (_host_tail)
         self._host_tail = False
         self._tail_bytes = 0
+        self._tail_auto = False            # _tail_bytes follows rate x device latency
+        self._tail_t = 0.0                 # last auto check
+        self._tail_rx0: Optional[Tuple[float, int]] = None   # (time, bytes) at the first rx
         if client.native_wire:
             try:
                 from ..ops import native
@@ -549,6 +552,34 @@ class TorrentSession:
             except Exception:
                 return p.down_bytes
         return p.down_bytes
+
+    def _tail_due(self, unstarted: int) -> bool:
+        """GPU mode: hash the rest on the host now? Fixed tail: once no more than _tail_bytes
+        are left to start. Auto (VERDICT r5 item 6 - the device's per-piece latency landing
+        on the end of a small torrent): once what is left would download in less than the
+        device's submission -> digest time (measured by the wire, 0.12 s before the first
+        digest) x 1.3, at the rate the download has run since its first byte; at most half
+        of the torrent. Checked at most every 5 ms (it runs per piece assigned)."""
+        if not self._tail_auto:
+            return unstarted <= self._tail_bytes
+        if unstarted <= 0:
+            return True
+        now = time.monotonic()
+        if now - self._tail_t < 0.005:
+            return False
+        self._tail_t = now
+        rx = self.wire.rx_total()
+        if self._tail_rx0 is None:
+            if rx > 0:
+                self._tail_rx0 = (now, rx)
+            return False
+        t0, b0 = self._tail_rx0
+        if now - t0 < 0.02:
+            return False
+        rate = (rx - b0) / (now - t0)
+        lat = self.wire.gpu_latency() or 0.12
+        tail = min(self._tail_bytes, int(rate * lat * 1.3))
+        return unstarted <= tail
 
     async def _rate_loop(self) -> None:
         """Per-peer receive rates every RATE_S: each connection's request pipeline follows its
@@ -699,9 +730,12 @@ class TorrentSession:
             if not on and self.client.swarm_verify == "gpu":
                 raise TorrentError("swarm_verify_backend=gpu but no GPU part hasher")
             self.wire.set_gpu(bool(on), self.client.wire_gpu_inflight)
-            # (at most a quarter of the torrent: a small one stays mostly on the device)
-            self._tail_bytes = min(self.client.swarm_gpu_tail_bytes,
-                                   meta.total_length // 4) if on else 0
+            # fixed: at most a quarter of the torrent (a small one stays mostly on the device);
+            # auto: rate x device latency, at most half (_tail_due)
+            tb = self.client.swarm_gpu_tail_bytes
+            self._tail_auto = bool(on) and tb < 0
+            self._tail_bytes = (meta.total_length // 2 if tb < 0 else
+                                min(tb, meta.total_length // 4)) if on else 0
             self.stats["swarm_verify"] = "gpu" if on else "cpu"
         if self.wire is not None:
             self.wire.set_storage(meta.piece_length, meta.total_length, meta.pieces,
@@ -871,12 +905,13 @@ class TorrentSession:
                     if t < pc.depth and picker.no_candidates():
                         self._enter_endgame()
                     return False
-                if self._tail_bytes and not self._host_tail and picker.unstarted() * \
-                        self.meta.piece_length <= self._tail_bytes:
+                if self._tail_bytes and not self._host_tail and \
+                        self._tail_due(picker.unstarted() * self.meta.piece_length):
                     # the last pieces are hashed on the host: on the device each would add its
-                    # ~75 ms (and its wait for a compute stream) to the end of the job
+                    # submission -> digest time to the end of the job
                     self._host_tail = True
                     wire.set_host_tail(True)
+                    self.stats["gpu_host_tail_bytes"] = picker.unstarted() * self.meta.piece_length
                 try:
                     t = wire.assign(me, idx)
                 except Exception:

@@ -274,10 +274,12 @@ class DownloadConfig(BaseModel):
     # for a compute stream); past it the host hashes the overflow. 512 overflowed on config 6
     # at 8 GB (6.1 - 6.5 GB/s vs 7.2 - 8.4 with 4096, profiles/archive/r5/swarm/event_loop/)
     swarm_gpu_inflight: int = 1024
-    # GPU mode: once no more than this much of the torrent (at most a quarter) is left to
-    # start, pieces are hashed on the host - on the device the last ones each add ~0.1 s to
-    # the job. 0: off. 1024 on config 6 at 2 GB: 5.9 - 6.8 vs 5.3 - 5.8 GB/s, at 16 GB no gain
-    swarm_gpu_tail_mb: int = 0
+    # GPU mode: once no more than this much of the torrent is left to start, pieces are
+    # hashed on the host - on the device the last ones would each add their submission ->
+    # digest time (~60 - 120 ms) to the end of the job. -1 (auto): the download rate so far x
+    # that time as measured (1.3 x), at most half the torrent; 0: off; > 0: fixed (at most a
+    # quarter of the torrent)
+    swarm_gpu_tail_mb: int = -1
     # complete swarm pieces waiting for their SHA-1 (host verifiers, the device) or the writer
     # hold their buffers; at this much no new piece is started until half has drained. Without
     # it a download faster than its verification ran GBs ahead (config 6 at 16 GB: 4 - 8 GB).

@@ -240,6 +240,17 @@ def test_split_kernel_matches_lanes_kernel_and_is_faster(gv):
         gv.kernel_bench_split(1000, 16, 1)
 
 
+def test_split_kernel_small_launches(gv):
+    """A launch of one part (16 lanes of a 64-lane workgroup), with its idle lanes hashing live
+    lanes' pieces again (the default) or left idle: right digests either way, and the default
+    no slower (left idle it took 72 - 96 ms per 4 MiB piece on one box, 57 on another, against
+    57 with every lane busy; profiles/r6/split/small_launch_dup.jsonl)."""
+    dup, _, same = gv.kernel_bench_split(4 << 20, 16, 2, True)
+    idle, _, same2 = gv.kernel_bench_split(4 << 20, 16, 2, False)
+    assert same and same2
+    assert dup < idle * 1.1, (dup, idle)
+
+
 @pytest.mark.parametrize("kernel", ["sha1_lanes_split", "sha1_lanes"])
 def test_part_hasher_kernels_match_hashlib(monkeypatch, kernel):
     from downloader_amd.ops import gpuhash
