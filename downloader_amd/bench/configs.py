@@ -505,6 +505,10 @@ async def config_swarm(a) -> Dict:
             extra["wire_gpu_inflight"] = a.swarm_gpu_inflight
         if getattr(a, "swarm_pool_mb", 0):
             extra["wire_pool_mb"] = a.swarm_pool_mb
+        if getattr(a, "swarm_gpu_tail_x", None) is not None:
+            extra["swarm_gpu_tail_x"] = a.swarm_gpu_tail_x
+        if getattr(a, "swarm_gpu_tail_max", None) is not None:
+            extra["swarm_gpu_tail_max"] = a.swarm_gpu_tail_max
         if getattr(a, "swarm_gpu_tail_mb", None) is not None:
             mb = a.swarm_gpu_tail_mb
             extra["swarm_gpu_tail_bytes"] = mb << 20 if mb >= 0 else -1
@@ -551,7 +555,9 @@ async def config_swarm(a) -> Dict:
                "leech_cpu_s_per_GB_reps": [round(r[1] / (total / 1e9), 3) for r in runs],
                # GPU mode: bytes left to start when the rest went to the host (auto tail)
                "gpu_host_tail_bytes_reps": [r[4].stats.get("gpu_host_tail_bytes", 0)
-                                            for r in runs]}
+                                            for r in runs],
+               # piece buffers page-locked for the GPU hasher (process-wide, so far), per rep
+               "pool_locks_reps": [(r[3] or {}).get("pool_locks", 0) for r in runs]}
         await leech.close()
         return out
     finally:
@@ -727,6 +733,10 @@ def main(argv=None) -> int:
                          "seeders, swarm download, staging to the S3 sink), not the bare leech")
     ap.add_argument("--swarm-gpu-tail-mb", type=int, default=None,
                     help="config 6, GPU mode: the last MB hashed on the host (default: config)")
+    ap.add_argument("--swarm-gpu-tail-max", type=float, default=None,
+                    help="config 6, GPU mode: the auto tail's largest share of the torrent")
+    ap.add_argument("--swarm-gpu-tail-x", type=float, default=None,
+                    help="config 6, GPU mode: the auto tail's multiple of the device latency")
     ap.add_argument("--swarm-pool-mb", type=int, default=0,
                     help="config 6: idle piece buffers kept (0: the default)")
     ap.add_argument("--wire-requests", choices=["native", "python"], default="native",

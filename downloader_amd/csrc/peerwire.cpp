@@ -99,14 +99,27 @@ struct PiecePool {
   // page faults in the reader that fills it and, in GPU mode, a page-locking.
   size_t max_idle_bytes = (size_t)1 << 30;
 
-  uint8_t* take(size_t n, const void** reg) {
+  // locked_for: the hasher the piece will most likely go to (GPU mode), else nullptr - an
+  // idle buffer already page-locked for it is taken first (for a host piece, one that is not):
+  // a LIFO of mixed buffers handed device pieces unlocked ones while locked ones sat idle,
+  // ~30 page-lockings of a few ms each per 2 GB job after the first (config 6, r6/tail)
+  uint8_t* take(size_t n, const void** reg, const void* locked_for) {
     {
       std::lock_guard<std::mutex> g(mu);
       in_use++;
       auto it = idle.find(n);
       if (it != idle.end() && !it->second.empty()) {
-        auto b = it->second.back();
-        it->second.pop_back();
+        auto& v = it->second;
+        size_t k = v.size() - 1;
+        // newest first, among the last 64 (the search stays short)
+        for (size_t j = v.size(); j-- > 0 && j + 64 >= v.size();)
+          if (v[j].second == locked_for) {
+            k = j;
+            break;
+          }
+        auto b = v[k];
+        v[k] = v.back();
+        v.pop_back();
         idle_count--;
         idle_bytes -= n;
         *reg = b.second;
@@ -396,7 +409,9 @@ void SwarmWire::begin_piece(uint32_t idx) {
   // pooled and reused: a fresh 4 MiB buffer per piece cost ~1,000 page faults in the reader
   // that first writes it; in GPU mode the pool's buffers are also page-locked once
   p->cap = ((size_t)piece_length_ + 4095) & ~(size_t)4095;
-  p->data = piece_pool().take(p->cap, &p->reg);
+  p->data = piece_pool().take(p->cap, &p->reg,
+                              gpu_.load() && !host_tail_.load() ? gpu_part_hasher_current()
+                                                                : nullptr);
   p->claimed.assign(p->nblocks, 0);
   p->epoch = ++epoch_;
   pieces_[idx] = std::move(p);          // a re-begun piece (failed its check) starts over

@@ -36,8 +36,9 @@ class TorrentClient:
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
                  wire_pool_mb: int = 4096, wire_gpu_inflight: int = 1024,
-                 swarm_gpu_min_bytes: int = 8 << 30, swarm_gpu_tail_bytes: int = -1,
-                 swarm_backlog_bytes: int = 4 << 30, wire_io_threads: int = 4):
+                 swarm_gpu_min_bytes: int = 2 << 30, swarm_gpu_tail_bytes: int = -1,
+                 swarm_backlog_bytes: int = 4 << 30, wire_io_threads: int = 4,
+                 swarm_gpu_tail_x: float = 3.0, swarm_gpu_tail_max: float = 0.85):
         from ..net.http import make_transports
         self._own_transports = transports is None
         self.transports = transports or make_transports()
@@ -74,6 +75,8 @@ class TorrentClient:
         self.swarm_gpu_min_bytes = swarm_gpu_min_bytes   # `auto`: device from this size up
         # GPU mode: the last bytes on the host (-1: sized by the measured device latency)
         self.swarm_gpu_tail_bytes = swarm_gpu_tail_bytes
+        self.swarm_gpu_tail_x = swarm_gpu_tail_x         # auto tail: x the device's latency
+        self.swarm_gpu_tail_max = swarm_gpu_tail_max     # auto tail: share of the torrent, max
         self.swarm_backlog_bytes = swarm_backlog_bytes   # complete, unverified pieces at most
         if native_wire:
             try:
@@ -111,7 +114,8 @@ class TorrentClient:
                    wire_gpu_inflight=d.swarm_gpu_inflight,
                    swarm_gpu_min_bytes=int(d.swarm_gpu_min_gb * (1 << 30)),
                    swarm_gpu_tail_bytes=(d.swarm_gpu_tail_mb << 20) if d.swarm_gpu_tail_mb >= 0
-                   else -1,
+                   else -1, swarm_gpu_tail_x=d.swarm_gpu_tail_x,
+                   swarm_gpu_tail_max=d.swarm_gpu_tail_max,
                    swarm_backlog_bytes=membudget.swarm_bytes(d.swarm_backlog_mb),
                    dht_bootstrap=boot if boot is not None else DEFAULT_BOOTSTRAP, **kw)
 

@@ -558,8 +558,9 @@ class TorrentSession:
         are left to start. Auto (VERDICT r5 item 6 - the device's per-piece latency landing
         on the end of a small torrent): once what is left would download in less than the
         device's submission -> digest time (measured by the wire, 0.12 s before the first
-        digest) x 1.3, at the rate the download has run since its first byte; at most half
-        of the torrent. Checked at most every 5 ms (it runs per piece assigned)."""
+        digest) x swarm_gpu_tail_x (3), at the rate the download has run since its first
+        byte; at most swarm_gpu_tail_max (0.85) of the torrent. Checked at most every 5 ms
+        (it runs per piece assigned)."""
         if not self._tail_auto:
             return unstarted <= self._tail_bytes
         if unstarted <= 0:
@@ -578,7 +579,8 @@ class TorrentSession:
             return False
         rate = (rx - b0) / (now - t0)
         lat = self.wire.gpu_latency() or 0.12
-        tail = min(self._tail_bytes, int(rate * lat * 1.3))
+        x = getattr(self.client, "swarm_gpu_tail_x", 3.0)
+        tail = min(self._tail_bytes, int(rate * lat * x))
         return unstarted <= tail
 
     async def _rate_loop(self) -> None:
@@ -731,11 +733,12 @@ class TorrentSession:
                 raise TorrentError("swarm_verify_backend=gpu but no GPU part hasher")
             self.wire.set_gpu(bool(on), self.client.wire_gpu_inflight)
             # fixed: at most a quarter of the torrent (a small one stays mostly on the device);
-            # auto: rate x device latency, at most half (_tail_due)
+            # auto: rate x device latency, at most swarm_gpu_tail_max of it (_tail_due)
             tb = self.client.swarm_gpu_tail_bytes
             self._tail_auto = bool(on) and tb < 0
-            self._tail_bytes = (meta.total_length // 2 if tb < 0 else
-                                min(tb, meta.total_length // 4)) if on else 0
+            cap = int(meta.total_length * min(1.0, max(0.0, getattr(
+                self.client, "swarm_gpu_tail_max", 0.85))))
+            self._tail_bytes = (cap if tb < 0 else min(tb, meta.total_length // 4)) if on else 0
             self.stats["swarm_verify"] = "gpu" if on else "cpu"
         if self.wire is not None:
             self.wire.set_storage(meta.piece_length, meta.total_length, meta.pieces,

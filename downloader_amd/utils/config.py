@@ -254,12 +254,12 @@ class DownloadConfig(BaseModel):
     # SHA-1 of swarm pieces on the native wire: "cpu" = the host multi-buffer SHA-1 (16 pieces
     # at a time), "gpu" = the gfx950 PartHasher (set up once per worker), "auto" = the device
     # for torrents of swarm_gpu_min_gb and up (0: never) or on hosts without the AVX-512
-    # multi-buffer SHA-1, else the host. Config 6 (4 seeders) on the box: 16 GB on the device
-    # 8.7 - 9.0 GB/s at 0.28 - 0.29 leech CPU-s/GB vs 9.0 - 9.5 at 0.43 - 0.48 on the host;
-    # 2 GB 5.3 - 5.8 vs 8.9 - 9.2 (the device's ~75 ms per piece is a bigger share of a short
-    # job; profiles/archive/r5/swarm/backpressure/)
+    # multi-buffer SHA-1, else the host. Round 5 kept the device for 8 GB and up (2 GB: 5.3 -
+    # 5.8 vs 8.9 - 9.2 GB/s on the host - the last pieces' device latency on the job's end);
+    # with the split-wave kernel (57 vs 73 ms per 4 MiB piece) and the auto host tail below,
+    # config 6 runs within ~5 % of the host at 2 GB and 16 GB on less CPU (profiles/r6/tail/)
     swarm_verify_backend: str = "auto"
-    swarm_gpu_min_gb: float = 8.0
+    swarm_gpu_min_gb: float = 2.0
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
@@ -277,9 +277,15 @@ class DownloadConfig(BaseModel):
     # GPU mode: once no more than this much of the torrent is left to start, pieces are
     # hashed on the host - on the device the last ones would each add their submission ->
     # digest time (~60 - 120 ms) to the end of the job. -1 (auto): the download rate so far x
-    # that time as measured (1.3 x), at most half the torrent; 0: off; > 0: fixed (at most a
-    # quarter of the torrent)
+    # that time as measured (swarm_gpu_tail_x), at most swarm_gpu_tail_max of the torrent; 0:
+    # off; > 0: fixed (at most a quarter of the torrent)
     swarm_gpu_tail_mb: int = -1
+    # config 6 at 2 GB, steady reps, same calls (profiles/r6/tail/): x 1.3 / at most half
+    # 7.4 - 7.9 GB/s vs host 8.3 - 9.2; x 2 / 3/4 7.4 - 8.0 vs 8.1 - 9.2; x 3 / 0.85 7.9 - 8.4
+    # vs 8.1 - 9.2 (the device takes the first ~20 % of such a torrent: what it can hand back
+    # before the download ends)
+    swarm_gpu_tail_x: float = 3.0               # auto tail: x the measured device latency
+    swarm_gpu_tail_max: float = 0.85            # auto tail: at most this share of the torrent
     # complete swarm pieces waiting for their SHA-1 (host verifiers, the device) or the writer
     # hold their buffers; at this much no new piece is started until half has drained. Without
     # it a download faster than its verification ran GBs ahead (config 6 at 16 GB: 4 - 8 GB).

@@ -23,6 +23,7 @@ class _Wire:
 
 def _session(total: int, lat: float, auto: bool = True, fixed: int = 0):
     return SimpleNamespace(wire=_Wire(lat), _tail_auto=auto,
+                           client=SimpleNamespace(swarm_gpu_tail_x=1.3),
                            _tail_bytes=total // 2 if auto else fixed,
                            _tail_t=0.0, _tail_rx0=None)
 
