@@ -1523,7 +1523,10 @@ def test_native_wire_gpu_mode_hashes_the_tail_on_the_host(run, tmp_path):
 
     async def go():
         raw, data, seeder, src = await _seed(tmp_path, {"a.mkv": 4_000_000}, piece=65536)
-        leech = await TorrentClient(swarm_verify="gpu", pipeline=16,
+        # (pipeline 2: pieces are started a few at a time, so the first ones are verified
+        # before the last quarter is reached - with 16 half the torrent was requested at once
+        # and, on a loaded host, completed only after the switch: no piece on the device)
+        leech = await TorrentClient(swarm_verify="gpu", pipeline=2,
                                     swarm_gpu_tail_bytes=1 << 30).start()
         meta = parse_torrent(raw)
         s = await leech.add_torrent(meta, str(tmp_path / "dl"),
