@@ -36,7 +36,7 @@ class TorrentClient:
                  native_wire: bool = True, wire_verify_threads: int = 4,
                  swarm_verify: str = "auto", wire_requests: bool = True,
                  wire_pool_mb: int = 4096, wire_gpu_inflight: int = 1024,
-                 swarm_gpu_min_bytes: int = 2 << 30, swarm_gpu_tail_bytes: int = -1,
+                 swarm_gpu_min_bytes: int = 3 << 29, swarm_gpu_tail_bytes: int = -1,
                  swarm_backlog_bytes: int = 4 << 30, wire_io_threads: int = 4,
                  swarm_gpu_tail_x: float = 3.0, swarm_gpu_tail_max: float = 0.85):
         from ..net.http import make_transports

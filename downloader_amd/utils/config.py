@@ -259,7 +259,7 @@ class DownloadConfig(BaseModel):
     # with the split-wave kernel (57 vs 73 ms per 4 MiB piece) and the auto host tail below,
     # config 6 runs within ~5 % of the host at 2 GB and 16 GB on less CPU (profiles/r6/tail/)
     swarm_verify_backend: str = "auto"
-    swarm_gpu_min_gb: float = 2.0
+    swarm_gpu_min_gb: float = 1.5               # GiB: a "2 GB" (2e9-byte) torrent included
     # native wire threads verifying and writing complete pieces (and, in GPU mode, collecting
     # digests): 2 capped config 6 near 5 - 7 GB/s with pieces queueing behind them
     swarm_verify_threads: int = 4
