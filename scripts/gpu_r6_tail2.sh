@@ -8,7 +8,7 @@ mkdir -p $F
 export LOG_LEVEL=error TMPDIR=/tmp PYTHONPATH=$R
 cd $R
 step() { echo "== $1 $(date +%T)"; }
-for sc in 1 8; do
+for sc in ${SCALES:-1 8}; do
   for r in 1 2; do
     for v in ${VERIFY:-gpu cpu}; do
       step "config6 $v x$sc #$r"
