@@ -39,6 +39,11 @@ def summarise(path: str, piece_len: int = 0):
             if piece_len:
                 row["valu_insts_per_64B_block"] = round(row["valu_insts_per_wave"]
                                                         / (piece_len / 64), 1)
+                if "split" in key[0]:
+                    # three waves (two schedule producers, one rounds consumer) per 64 pieces:
+                    # the per-wave figure is their average; per 64 pieces it is their sum
+                    row["valu_insts_per_64B_block_per_64_pieces"] = round(
+                        3 * row["valu_insts_per_64B_block"], 1)
         if c.get("SQ_WAVE_CYCLES"):
             # SQ_ACTIVE_INST_VALU and SQ_WAVE_CYCLES are both per-wave cycle sums (quad-cycle
             # granularity on CDNA), so their ratio is the fraction of a wave's life spent issuing
