@@ -1536,6 +1536,19 @@ def test_native_wire_gpu_mode_hashes_the_tail_on_the_host(run, tmp_path):
         st = s.wire.stats()
         assert s._host_tail and st["verified"] == meta.num_pieces
         assert 0 < st["gpu_pieces"] < meta.num_pieces and st["verify_batches"] > 0
+        # the wire timed the device's pieces (submission -> digest; the auto tail's input)
+        assert s.wire.gpu_latency() > 0 and st["gpu_latency_ms_max"] >= st["gpu_latency_ms_mean"] > 0
+        await leech.remove(s)
+        # a second download reuses the pool's page-locked buffers for its device pieces
+        # instead of locking fresh ones (they are taken first, r6/tail)
+        locks = st["pool_locks"]
+        s = await leech.add_torrent(meta, str(tmp_path / "dl2"),
+                                    peers=[("127.0.0.1", seeder.listen_port)])
+        await asyncio.wait_for(s.wait(), 60)
+        _check(tmp_path / "dl2", data)
+        st2 = s.wire.stats()
+        assert st2["gpu_pieces"] > 0 and st2["pool_locks"] - locks <= st2["gpu_pieces"] // 2, \
+            (locks, st2["pool_locks"], st2["gpu_pieces"])
         await leech.close(); await seeder.close()
 
     hashing.use_part_hasher(native().CpuPartHasher(0.002), 4)
