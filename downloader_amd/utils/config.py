@@ -224,10 +224,14 @@ class DownloadConfig(BaseModel):
     stream_gpu_compute_streams: int = 0
     stream_gpu_min_pieces: int = 8              # parts with fewer whole pieces stay on the host
     # once fewer parts than this are queued, the job's remaining parts hash on the host (the
-    # GPU's per-piece latency would otherwise land on the end of the job): 16 / 48 / 96 / 128
-    # / 160 gave 21.2 - 21.8 / 22.7 - 23.6 / 25.0 - 29.1 / 25.7 - 28.5 / 24.4 - 27.5 GB/s
-    # for one 20 GB job vs 22.7 - 25.4 on the host (profiles/archive/r3_tail*/)
-    stream_gpu_tail: int = 96
+    # GPU's per-piece latency would otherwise land on the end of the job). With sha1_lanes
+    # (73 - 100 ms a launch) 16 / 48 / 96 / 128 / 160 gave 21.2 - 21.8 / 22.7 - 23.6 / 25.0 -
+    # 29.1 / 25.7 - 28.5 / 24.4 - 27.5 GB/s for one 20 GB job vs 22.7 - 25.4 on the host
+    # (profiles/archive/r3_tail*/); with sha1_lanes_split (57 ms) 96 / 64 / 48 / 32 run at the
+    # host arm's speed alike (ratios 0.96 - 1.05 over 9 same-call A/Bs) at 0.37 - 0.40 / 0.35 /
+    # 0.33 - 0.37 / 0.35 worker CPU-s/GB, 66 / 76 / 80 / 85 % of the parts on the device
+    # (profiles/r6/split/stream_tail/)
+    stream_gpu_tail: int = 32
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
     # without a HIP device) so "auto" sends rechecks >= 256 MiB and the webseed runs of
