@@ -179,13 +179,23 @@ def main() -> None:
     ap.add_argument("--gb", type=float, default=20.0)
     ap.add_argument("--pairs", type=int, default=3)
     ap.add_argument("--set", action="append", default=[], help="download.KEY=VALUE (both arms)")
+    ap.add_argument("--no-pin", action="store_true",
+                    help="run on the whole CPU mask (default: pinned like bench.py's rank)")
     a = ap.parse_args()
+    # as bench.py pins a rank (and its blobd, which inherits the mask) to one GPU slot's share
+    # of the CPUs: unpinned, a 16-CPU quota over a mask of hundreds throttles in bursts and
+    # both arms ran ~20 - 24 GB/s instead of 27 - 34, their ratio lost in it (r6/split/)
+    pinned = []
+    if not a.no_pin:
+        from ..utils import cpus
+        pinned = cpus.pin_slot(0, max(1, cpus.gpu_slots()))
     over: Dict = {}
     for kv in a.set:
         k, _, v = kv.partition("=")
         over[k] = json.loads(v) if v[:1] in "0123456789-[{tf\"" else v
     out = asyncio.run(torrent_ab(total_bytes=int(a.gb * 1e9), pairs=a.pairs, download=over))
     out["download"] = over
+    out["pinned_cpus"] = len(pinned)
     print(json.dumps(out), flush=True)
 
 

@@ -227,10 +227,10 @@ class DownloadConfig(BaseModel):
     # GPU's per-piece latency would otherwise land on the end of the job). With sha1_lanes
     # (73 - 100 ms a launch) 16 / 48 / 96 / 128 / 160 gave 21.2 - 21.8 / 22.7 - 23.6 / 25.0 -
     # 29.1 / 25.7 - 28.5 / 24.4 - 27.5 GB/s for one 20 GB job vs 22.7 - 25.4 on the host
-    # (profiles/archive/r3_tail*/); with sha1_lanes_split (57 ms) 96 / 64 / 48 / 32 run at the
-    # host arm's speed alike (ratios 0.96 - 1.05 over 9 same-call A/Bs) at 0.37 - 0.40 / 0.35 /
-    # 0.33 - 0.37 / 0.35 worker CPU-s/GB, 66 / 76 / 80 / 85 % of the parts on the device
-    # (profiles/r6/split/stream_tail/)
+    # (profiles/archive/r3_tail*/); with sha1_lanes_split (57 ms), pinned like bench.py's rank:
+    # 32 parts 34.0 vs 28.0 GB/s (1.22x, 85 % of the parts on the device), 16 parts 30.7 vs
+    # 26.2 (1.17x, 90 %); 1 copy + 3 compute streams 1.16 - 1.17x (profiles/r6/split/
+    # stream_tail/call3_pinned/; the unpinned calls beside it show both arms throttled alike)
     stream_gpu_tail: int = 32
     verify_threads: int = 0                     # host SHA-1 threads per check (0: usable CPUs)
     # Initialise the GPU verifier at worker start (device = worker index % GPUs; a no-op
