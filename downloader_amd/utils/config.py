@@ -164,7 +164,10 @@ class DownloadConfig(BaseModel):
     # disk hop (torrent/stream.py). auto: when the metainfo lists no trackers, first attempt
     # only (a retry takes the disk path with every source); always: whenever webseeds exist.
     torrent_stream: Literal["auto", "always", "off"] = "auto"
-    torrent_stream_parallel: int = 16           # parts (Range GETs) in flight per job
+    # parts (Range GETs) in flight per job: config 4, pinned A/B, 16 / 24 / 32: gfx950 arm
+    # 30.9 - 31.3 / 31.9 / 33.2 GB/s, host arm 26.1 - 26.6 / 27.9 / 27.8 (each relay leaves
+    # its thread ~half idle waiting on the webseed; profiles/r6/split/stream_parallel/)
+    torrent_stream_parallel: int = 32
     # Byte budget of the streamed relay's part buffers (one per part in flight, as large as
     # the part): relays in flight, parts awaiting their DMA to the GPU and idle pooled buffers
     # of ALL jobs of the worker draw from it, so their resident memory never exceeds it
