@@ -426,6 +426,10 @@ QUEUE_S = 0.5
 MAX_DEPTH = 1024
 SLOW_SHARE = 1 / 8
 SLOW_TICKS = 2
+# endgame: an owner keeps its piece if it would finish half a piece within this at its rate
+# (heterogeneous swarm on the CPU, 1 GB, 3 seeds: 3.15 - 3.68 s vs 3.44 - 4.07 s with the
+# mean/2 rule alone; 0.5 s: 3.33 - 3.38)
+ENDGAME_KEEP_S = 0.25
 
 
 class TorrentSession:
@@ -941,12 +945,16 @@ class TorrentSession:
         # per-block requesting, where idle connections duplicate their missing blocks
         rates = [p.rate for p in self.peers.values() if not p.closed and p.rate]
         mean = sum(rates) / len(rates) if rates else 0.0
+        # ... and only when they would finish it soon: half a piece within ENDGAME_KEEP_S at
+        # their rate (a 5 MB/s owner of a fresh 4 MiB piece kept the endgame waiting ~0.8 s)
+        keep_s = float(os.environ.get("STAGER_ENDGAME_KEEP_S", ENDGAME_KEEP_S))
+        keep = max(mean / 2, self.meta.piece_length / 2 / keep_s if keep_s > 0 else 0.0)
         for idx, ap in list(self.picker.active.items()):
             if ap.owner is None:
                 continue
             owner = self.peers.get(ap.owner)
             if owner is not None and not owner.closed and not owner.slow and mean > 0 and \
-                    (owner.rate or 0.0) >= mean / 2:
+                    (owner.rate or 0.0) >= keep:
                 continue
             r = self.wire.release_piece(idx)
             if r is None:
