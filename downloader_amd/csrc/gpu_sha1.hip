@@ -448,7 +448,9 @@ __device__ __forceinline__ void lds_barrier() {
 // producer that schedules in one step and writes in the next 60.9 - 61.2 ms, the consumer's
 // next-block reads spread through its rounds (one per 4 rounds, pinned by sched_barrier)
 // 60.7 - 60.9, both 60.8 - 61.5, the consumer at s_setprio 3 64.7 - 65.1, against 52.8 - 53.4
-// here and 73.2 - 73.5 for sha1_lanes<16>.
+// here and 73.2 - 73.5 for sha1_lanes<16>. Two blocks per barrier (a ring of three pairs, both
+// producers busy every step) came out 1.5 % slower, 58.0 - 58.5 vs 57.0 - 57.7 ms in one
+// process (pair_per_barrier.jsonl): the barriers are not where the consumer's time goes.
 template <bool DUP>
 __global__ __launch_bounds__(192) void sha1_lanes_split_t(const uint8_t* __restrict__ data,
                                                           const int64_t* __restrict__ lane_off,
@@ -482,8 +484,8 @@ __global__ __launch_bounds__(192) void sha1_lanes_split_t(const uint8_t* __restr
   // this lane's column of slot j (plain arithmetic on `ring`: an array of slot pointers made
   // them generic pointers - flat_load / flat_store, waited for with vmcnt too)
   auto col = [&](uint32_t j) { return ring + j * (kSplitGroups * 64) + lane; };
-  // Two prologue steps, then steps k = 0 .. M - 1, one barrier each. Step k: the consumer hashes block k from registers (read in the step before) while its
-  // reads of block k + 1 (slot (k + 1) % 4) are in flight - their latency, and their queueing
+  // Two prologue steps, then steps k = 0 .. M - 1, one barrier each. Step k: the consumer
+  // hashes block k from registers (read in the step before) while its reads of block k + 1 (slot (k + 1) % 4) are in flight - their latency, and their queueing
   // behind the stores, off its critical path. Producer k % 2 swaps, schedules and writes block
   // k + 2 into slot (k + 2) % 4 (free: block k is in the consumer's registers) - the stores at
   // the end of its step, after the consumer's reads - and idles in the next step.
