@@ -423,6 +423,7 @@ PYBIND11_MODULE(_native, m) {
     d["crc_ns"] = c.crc_ns;
     d["crc_bytes"] = c.crc_bytes;
     d["sha1_ns"] = c.sha1_ns;
+    d["nt_staged_bytes"] = c.nt_bytes;
     return d;
   }, "Per-phase relay counters since start (relay_body_to): relays / bytes / relaying-thread "
      "CPU per mode (splice, dup = peek|tee copy + CRC, copy), syscalls, copy and CRC time");

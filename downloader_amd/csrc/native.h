@@ -137,6 +137,7 @@ struct RelayCounters {
   uint64_t dup_calls, dup_bytes;                // recv(MSG_PEEK) / read(tee) copies
   uint64_t crc_ns, crc_bytes;                   // CRC32C over the copied bytes
   uint64_t sha1_ns;                             // host piece SHA-1 inside hashed relays
+  uint64_t nt_bytes;                            // hashed parts staged in L2 + streamed (NT)
 };
 RelayCounters relay_counters();
 // Capacity asked for new pipes: the splice pipe, and the tee() duplicate pipe (0 = keep).

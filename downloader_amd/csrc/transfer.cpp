@@ -33,6 +33,7 @@
 #include <sys/types.h>
 #include <unistd.h>
 #include <unordered_map>
+#include <immintrin.h>
 #include <map>
 #include <sys/eventfd.h>
 
@@ -70,7 +71,7 @@ thread_local RelayTally t_tally;
 struct {
   std::atomic<uint64_t> relays[4], bytes[4], cpu_ns[4];
   std::atomic<uint64_t> splice_in{0}, splice_out{0}, dup_calls{0}, dup_bytes{0}, crc_ns{0},
-      crc_bytes{0}, sha1_ns{0};
+      crc_bytes{0}, sha1_ns{0}, nt_bytes{0};
 } g_rc;
 
 uint64_t thread_cpu_ns() {
@@ -813,6 +814,17 @@ static bool relay_tee_on() {
   return on;
 }
 
+// CRC staging, L2-sized: relaybench peekcrc at 8 threads, 64 / 128 / 256 / 512 / 1024 KiB:
+// 36.3 / 36.7 / 37.5 / 39.4 / 38.1 GB/s (profiles/archive/r4/peekbuf/); STAGER_PEEK_KB: A/B knob
+static size_t peek_stage_bytes() {
+  static const size_t bytes = [] {
+    const char* e = getenv("STAGER_PEEK_KB");
+    long kb = e ? atol(e) : 0;
+    return (size_t)(kb >= 16 && kb <= 8192 ? kb : 512) * 1024;
+  }();
+  return bytes;
+}
+
 int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32_t* crc) {
   int64_t moved = 0, done = 0;
   RelayScope scope(&done);
@@ -833,15 +845,7 @@ int64_t HttpConn::relay_body_to(HttpConn& dst, int64_t n, Progress* prog, uint32
   if (ssl_ || dst.ssl_ || (crc && !relay_tee_on()))
     return fin(2, relay_copy(dst, n, moved, prog, crc));
   if (crc) {
-    // CRC staging, L2-sized: relaybench peekcrc at 8 threads, 64 / 128 / 256 / 512 / 1024
-    // KiB: 36.3 / 36.7 / 37.5 / 39.4 / 38.1 GB/s (profiles/archive/r4/peekbuf/);
-    // STAGER_PEEK_KB: A/B knob
-    static const size_t peek_bytes = [] {
-      const char* e = getenv("STAGER_PEEK_KB");
-      long kb = e ? atol(e) : 0;
-      return (size_t)(kb >= 16 && kb <= 8192 ? kb : 512) * 1024;
-    }();
-    thread_local std::vector<uint8_t> cbuf(peek_bytes);
+    thread_local std::vector<uint8_t> cbuf(peek_stage_bytes());
     int64_t m = relay_dup(
         dst, n, moved, prog,
         [&](size_t& len) {
@@ -1893,6 +1897,7 @@ RelayCounters relay_counters() {
   c.crc_ns = g_rc.crc_ns.load();
   c.crc_bytes = g_rc.crc_bytes.load();
   c.sha1_ns = g_rc.sha1_ns.load();
+  c.nt_bytes = g_rc.nt_bytes.load();
   return c;
 }
 void set_pipes_refused(bool on) { g_pipes_refused.store(on); }
@@ -1905,6 +1910,52 @@ void relay_pool_set_max_idle(size_t n) { part_pool().set_max_idle(n); }
 void relay_pool_set_budget(size_t bytes) { part_pool().set_budget(bytes); }
 void relay_pool_reset_peak() { part_pool().reset_peak(); }
 RelayPoolStats relay_pool_stats() { return part_pool().stats(); }
+
+// STAGER_PART_NT: how a hashed relay fills its part buffer. 0: the peek lands in the part
+// buffer itself (a cold 64 MiB buffer: the kernel's copy reads each line for ownership before
+// writing it back - three DRAM passes per byte once the DMA or the host's SHA-1 reads it
+// again); 1 (parts bound for the gfx950 PartHasher) / 2 (every hashed part): the peek lands in
+// an L2-sized buffer, is CRC'd there and streamed into the part buffer with non-temporal
+// stores - two passes, for one user-space copy out of L2. Pinned torrent A/B (config 4, 20 GB,
+// 5 alternating runs x 4 pairs each, profiles/r6/nt/): the device arm 33.7 - 34.0 GB/s with 1
+// vs 32.0 - 33.7 with 0 (ratio to the host arm 1.20 - 1.22 vs 1.13 - 1.20), worker 0.239 vs
+// 0.246 CPU-s/GB; 2 did not speed the host arm up (30.6 / 28.2 vs 31.9 / 29.9 GB/s with 0).
+static int part_nt_mode() {
+  static const int m = [] {
+    const char* e = getenv("STAGER_PART_NT");
+    return e ? std::max(0, std::min(2, atoi(e))) : 1;
+  }();
+  return m;
+}
+
+__attribute__((target("avx2"))) static void stream_copy_avx2(uint8_t* d, const uint8_t* s,
+                                                              size_t n) {
+  size_t head = std::min(n, (size_t)(-(uintptr_t)d & 31));
+  memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  for (; n >= 128; n -= 128, d += 128, s += 128) {
+    const __m256i a = _mm256_loadu_si256((const __m256i*)s);
+    const __m256i b = _mm256_loadu_si256((const __m256i*)(s + 32));
+    const __m256i c = _mm256_loadu_si256((const __m256i*)(s + 64));
+    const __m256i e = _mm256_loadu_si256((const __m256i*)(s + 96));
+    _mm256_stream_si256((__m256i*)d, a);
+    _mm256_stream_si256((__m256i*)(d + 32), b);
+    _mm256_stream_si256((__m256i*)(d + 64), c);
+    _mm256_stream_si256((__m256i*)(d + 96), e);
+  }
+  for (; n >= 32; n -= 32, d += 32, s += 32)
+    _mm256_stream_si256((__m256i*)d, _mm256_loadu_si256((const __m256i*)s));
+  memcpy(d, s, n);
+  _mm_sfence();                        // ordered before the part is handed to the DMA / hash
+}
+
+static void stream_copy(uint8_t* d, const uint8_t* s, size_t n) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2)
+    stream_copy_avx2(d, s, n);
+  else
+    memcpy(d, s, n);
+}
 
 int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
                                        int64_t full_len, int64_t piece_len, Progress* prog,
@@ -1919,7 +1970,29 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
   PartLease lease((size_t)n);
   uint8_t* b = lease.b->data;
   int64_t pos = 0;
-  if (!ssl_ && !dst.ssl_ && relay_tee_on()) {
+  const int64_t np = (full_len + piece_len - 1) / piece_len;
+  const GpuPartHashApi* api = gpu_ticket ? g_gpu_api.load() : nullptr;
+  const int nt = part_nt_mode();
+  if (!ssl_ && !dst.ssl_ && relay_tee_on() &&
+      (nt == 2 || (nt == 1 && api && np >= g_gpu_min_pieces.load()))) {
+    thread_local std::vector<uint8_t> sbuf(peek_stage_bytes());
+    relay_dup(
+        dst, n, 0, prog,
+        [&](size_t& len) {
+          len = std::min({len, sbuf.size(), (size_t)(n - pos)});
+          return sbuf.data();
+        },
+        [&](const uint8_t* p, size_t k) {
+          if (crc) {
+            uint64_t t0 = mono_ns();
+            *crc = stager::crc32c(p, k, *crc);
+            t_tally.crc_ns += mono_ns() - t0;
+          }
+          stream_copy(b + pos, p, k);
+          pos += (int64_t)k;
+        });
+    g_rc.nt_bytes.fetch_add((uint64_t)pos, std::memory_order_relaxed);
+  } else if (!ssl_ && !dst.ssl_ && relay_tee_on()) {
     relay_dup(
         dst, n, 0, prog,
         [&](size_t& len) {
@@ -1970,8 +2043,6 @@ int64_t HttpConn::relay_body_hashed_mb(HttpConn& dst, int64_t n, int64_t skip,
   }
   head->assign((const char*)b, (size_t)skip);
   tail->assign((const char*)b + skip + full_len, (size_t)(n - skip - full_len));
-  const int64_t np = (full_len + piece_len - 1) / piece_len;
-  const GpuPartHashApi* api = gpu_ticket ? g_gpu_api.load() : nullptr;
   if (api && np >= g_gpu_min_pieces.load()) {
     PartBuffer* pb = lease.b.get();
     if (!pb->reg_api && api->reg(api->ctx, pb->data, pb->cap) == 0)

@@ -912,3 +912,29 @@ def test_cancelled_relay_does_not_hang_on_a_stuck_gpu_forget(run):
         st._release_after(RuntimeError("x"), 3)     # no hold: back at once
         assert released == [7, 3]
     run(go(), timeout=30)
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_streamed_part_staging_keeps_bytes_and_digests(mode):
+    """STAGER_PART_NT (csrc/transfer.cpp ``part_nt_mode``): parts peeked into an L2-sized
+    buffer and streamed into the part buffer with non-temporal stores relay, hash and catch
+    corruption exactly like parts peeked straight into it (0; 1, the default: device-bound
+    parts, which the host double stands in for; 2: every hashed part). The mode is read once
+    per process, so the stream tests run again in a child with it set."""
+    import subprocess
+    import sys
+    env = dict(os.environ, STAGER_PART_NT=mode)
+    code = ("import sys, pytest\n"
+            f"rc = pytest.main(['-q', '-x', '-m', 'not gpu', '-p', 'no:cacheprovider', {__file__!r},"
+            " '-k', 'stream_matches_disk_path or async_part_hashing_with_host_double'])\n"
+            "from downloader_amd.ops import native\n"
+            "print('NT_STAGED', native().relay_counters()['nt_staged_bytes'])\n"
+            "sys.exit(int(rc))\n")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    staged = int(r.stdout.split("NT_STAGED")[1].split()[0])
+    if mode == "0":
+        assert staged == 0
+    else:
+        assert staged >= 23 << 20, r.stdout[-1000:]    # at least the host double's torrent
