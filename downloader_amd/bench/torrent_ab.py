@@ -112,6 +112,7 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
                                          "hash_fails": t.get("hash_fails", 0),
                                          "parts": t.get("parts", 0),
                                          "gpu_parts": t.get("gpu_parts", 0),
+                                         "timeline": dict(t.get("timeline", {}), job_s=dt),
                                          "relay": {k: rc1[k] - rc0.get(k, 0) for k in rc1}})
             dev1 = hashing.gpu_relay_stats() if any(be != "cpu" for be in backends) else {}
             st = b.stats()
@@ -134,6 +135,12 @@ async def torrent_ab(total_bytes: int = 20 * 10 ** 9, files: int = 50, piece_len
         out[f"torrent_{key}_worker_cpu_s_per_GB"] = round(
             statistics.median(x["worker_cpu_s"] for x in xs) / (total / 1e9), 4)
         out[f"torrent_{key}_hash_fails"] = sum(x["hash_fails"] for x in xs)
+        # where a job's time goes (torrent/stream.py timeline, seconds from the stager's
+        # start; job_s from the submit): medians over the timed jobs
+        keys_t = sorted({k for x in xs for k in x["timeline"]})
+        out[f"torrent_{key}_timeline_s"] = {
+            k: round(statistics.median(x["timeline"][k] for x in xs if k in x["timeline"]), 4)
+            for k in keys_t}
         # where the workers' CPU went (native relay counters, as the headline's
         # worker_breakdown): relaying threads, CRC, host SHA-1, the rest
         rc: Dict = {}

@@ -181,6 +181,7 @@ async def _stream_torrent(meta: Metainfo, seeds: List[str], selected: List[str],
                             "gpu_parts": st.stats.get("gpu_parts", 0),
                             "gpu_failures": st.stats.get("gpu_failures", 0),
                             "budget": st.stats.get("budget", {}),
+                            "timeline": dict(st.timeline),
                             "timeline_s": {"complete": round(time.perf_counter() - t0, 4)}}
     if sv.metrics is not None:
         sv.metrics.bytes_verified.labels("gpu" if st.stats.get("verify") == "gpu" else "host"

@@ -240,6 +240,10 @@ class StreamStager:
         self._outstanding = 0
         self._finished = asyncio.Event()
         self.stats = {"relay_s": 0.0, "gap_bytes": 0, "units": 0}
+        # seconds since run() began: uploads created, first / last relay over, last device
+        # digest in, every unit settled, uploads completed (where a job's time goes)
+        self.timeline: Dict[str, float] = {}
+        self._t0 = time.monotonic()
         # GPU piece hashing of relayed parts: at most this many parts awaiting digests,
         # across every stream stager of the process
         self._gpu_slots: Optional[asyncio.Semaphore] = None
@@ -317,6 +321,8 @@ class StreamStager:
         if _trim_handle is not None:           # a job started inside the warm window
             _trim_handle.cancel()
         self._budget = membudget.part_budget(self.budget_bytes)
+        self._t0 = time.monotonic()
+        self.stats["timeline"] = self.timeline
         try:
             from ..ops import native
             native().relay_pool_set_max_idle(POOL_IDLE_MAX)
@@ -336,6 +342,7 @@ class StreamStager:
             # all creations settle before a failure propagates: abort() then sees every
             # upload that was opened (none is left behind on the bucket)
             await gather_strict(*(create(t) for t in multi), cancel=False)
+            self._mark("created_s")
             queue: "asyncio.Queue[_Unit]" = asyncio.Queue()
             for u in self.units:
                 queue.put_nowait(u)
@@ -345,6 +352,7 @@ class StreamStager:
             workers = [asyncio.ensure_future(self._worker(queue)) for _ in range(self.parallel)]
             try:
                 await self._finished.wait()
+                self._mark("settled_s")
             finally:
                 for w in workers + list(self._continuations):
                     w.cancel()
@@ -359,6 +367,7 @@ class StreamStager:
                                                         sorted(t.etags.items()))
                 t.completed = True
             await gather_strict(*(complete(t) for t in multi), cancel=False)
+            self._mark("completed_s")
         except BaseException:
             await asyncio.shield(self.abort())
             raise
@@ -438,6 +447,11 @@ class StreamStager:
                 return
             self._settle(u, requeue, queue)
 
+    def _mark(self, key: str, first: bool = False) -> None:
+        t = round(time.monotonic() - self._t0, 4)
+        if not first or key not in self.timeline:
+            self.timeline[key] = t
+
     def _release_after(self, e: BaseException, nb: int) -> None:
         """A failed / cancelled relay's budget bytes: back now, or - when the cancellation
         could not wait for the GPU hasher to hand the part's buffer back (``held_until``, set
@@ -514,6 +528,7 @@ class StreamStager:
                 self.stats["gpu_failures"] = self.stats.get("gpu_failures", 0) + 1
                 raise TransportError(f"part {u.num}: {e}") from e
             self.stats["gpu_parts"] = self.stats.get("gpu_parts", 0) + 1
+            self._mark("last_gpu_digest_s")
             requeue = await self._after_fetch(u, self._accept(u, etag, h, digests))
         except BaseException as e:
             self._gpu_slots.release()
@@ -612,6 +627,10 @@ class StreamStager:
             part=None if t.single else (u.num, t.upload_id), content_type=self._ctype(t),
             gpu=gpu)
         self.stats["relay_s"] += time.perf_counter() - t0
+        self._mark("first_relay_s", first=True)
+        self._mark("last_relay_s")
+        if gpu and h.get("gpu_ticket"):
+            self._mark("last_gpu_relay_s")
         self.fetched_bytes += u.length
         return etag, h
 
